@@ -1,0 +1,115 @@
+"""Loader for the gfx950 C-ABI library ``libgr_hstu.so``.
+
+The ctypes signatures are derived from ``include/gr_hstu.h`` itself, so the Python
+side and the C-ABI cannot drift.  There is no fallback: if the library or a GPU is
+missing, every op raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import threading
+
+import torch  # noqa: F401  (import first: its HIP runtime is the one the .so binds to)
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO_DIR = os.path.dirname(PKG_DIR)
+LIB_PATH = os.path.join(PKG_DIR, "libgr_hstu.so")
+HEADER_PATH = os.path.join(REPO_DIR, "include", "gr_hstu.h")
+
+_CTYPES = {
+    "void": None,
+    "int": ctypes.c_int,
+    "int64_t": ctypes.c_int64,
+    "uint64_t": ctypes.c_uint64,
+    "size_t": ctypes.c_size_t,
+    "float": ctypes.c_float,
+    "const char*": ctypes.c_char_p,
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+def parse_header(path: str = HEADER_PATH):
+    """Returns {name: (restype_str, [argtype_str, ...])} for every GR_API function."""
+    text = open(path).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    out = {}
+    for m in re.finditer(r"GR_API\s+([\w\s\*]+?)\s*\b(\w+)\s*\(([^)]*)\)\s*;", text, flags=re.S):
+        ret, name, args = m.group(1).strip(), m.group(2), m.group(3).strip()
+        types = []
+        if args and args != "void":
+            for a in args.split(","):
+                a = " ".join(a.split())
+                a = re.sub(r"\s*\*\s*", "* ", a).strip()
+                # drop the parameter name
+                t = a.rsplit(" ", 1)[0] if " " in a else a
+                types.append(t.replace("* ", "*").strip())
+        out[name] = (ret.replace(" *", "*"), types)
+    return out
+
+
+def _ctype(t: str):
+    t = t.strip()
+    if t in _CTYPES:
+        return _CTYPES[t]
+    if t.endswith("*"):
+        return ctypes.c_void_p
+    raise TypeError(f"unmapped C type {t!r} in gr_hstu.h")
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; "
+                "g.build()'` (hipcc --offload-arch=gfx950). There is no CPU fallback.")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (ret, args) in parse_header().items():
+            fn = getattr(L, name)
+            fn.restype = _ctype(ret) if ret != "void" else None
+            fn.argtypes = [_ctype(a) for a in args]
+        _lib = L
+    return _lib
+
+
+class GrError(RuntimeError):
+    pass
+
+
+def call(name: str, *args):
+    """Calls a C-ABI entry point; raises GrError(gr_last_error()) on non-zero status."""
+    L = lib()
+    rc = getattr(L, name)(*args)
+    if rc != 0:
+        msg = L.gr_last_error().decode(errors="replace")
+        raise GrError(f"{name} failed (status {rc}): {msg}")
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a tensor (None for None)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_handle(device=None) -> int:
+    import torch as _t
+    return _t.cuda.current_stream(device).cuda_stream
+
+
+def require_gpu(*tensors):
+    import torch as _t
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise GrError("gr_hstu ops run on the MI355X only: got a CPU tensor "
+                          "(the CPU restatement lives in oracle/ and is test-only)")
+    if not _t.cuda.is_available():
+        raise GrError("no GPU visible: gr_hstu has no CPU path")

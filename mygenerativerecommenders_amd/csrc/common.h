@@ -1,0 +1,97 @@
+// Shared device/host helpers for the gfx950 HSTU + MIPS library.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <string>
+
+namespace gr {
+
+// ---------------------------------------------------------------- error plumbing
+void set_error(const char* fmt, ...);
+const char* last_error();
+
+#define GR_REQUIRE(cond, ...)                \
+  do {                                       \
+    if (!(cond)) {                           \
+      ::gr::set_error(__VA_ARGS__);          \
+      return 1;                              \
+    }                                        \
+  } while (0)
+
+#define GR_LAUNCH_CHECK(what)                                                   \
+  do {                                                                          \
+    hipError_t e_ = hipGetLastError();                                          \
+    if (e_ != hipSuccess) {                                                     \
+      ::gr::set_error("%s: launch failed: %s", what, hipGetErrorString(e_));     \
+      return 2;                                                                 \
+    }                                                                           \
+  } while (0)
+
+// ---------------------------------------------------------------- MFMA (f32 in / f32 acc)
+// v_mfma_f32_16x16x4_f32: A[i=l&15][k=l>>4], B[k=l>>4][j=l&15],
+// C/D: col = l&15, row = 4*(l>>4) + reg.  Bit-exact k-ordered fmaf chain.
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f4 mfma16x16x4(float a, float b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ f4 f4_zero() { return f4{0.f, 0.f, 0.f, 0.f}; }
+
+// ---------------------------------------------------------------- activations
+__device__ __forceinline__ float sigmoidf_(float x) {
+  return __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+}
+__device__ __forceinline__ float siluf_(float x) { return x * sigmoidf_(x); }
+// d silu / dx = s * (1 + x * (1 - s))
+__device__ __forceinline__ float silu_grad_(float x) {
+  float s = sigmoidf_(x);
+  return s * (1.0f + x * (1.0f - s));
+}
+
+// ---------------------------------------------------------------- counter-based RNG
+// Dropout masks are a pure function of (seed, element index): the backward pass
+// regenerates them instead of storing them.
+__device__ __forceinline__ uint32_t hash_u32(uint64_t seed, uint64_t idx) {
+  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (idx + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (uint32_t)(z >> 32);
+}
+
+// ---------------------------------------------------------------- wave reductions
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+// reduce across the 16 lanes that share (lane >> 4)
+__device__ __forceinline__ float sum16(float v) {
+#pragma unroll
+  for (int o = 8; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__host__ __device__ inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
+
+// relative-time bucket: max{b : thr[b] <= |dt|}, thr = integer threshold table of the
+// reference bucket fn (hstu.py:579-581, clamped at hstu.py:117-123).
+__device__ __forceinline__ int time_bucket(int64_t dt, const int64_t* thr_lds, int nb) {
+  uint64_t ad = dt < 0 ? (uint64_t)(-dt) : (uint64_t)dt;
+  int b = 0;
+  if (ad > 1) {
+    float f = (float)ad;
+    b = (int)(__log2f(f) * 2.30283176f);  // log2(x) * ln(2) / 0.301
+    b = b > nb ? nb : b;
+  }
+  while (b < nb && ad >= (uint64_t)thr_lds[b + 1]) ++b;
+  while (b > 0 && ad < (uint64_t)thr_lds[b]) --b;
+  return b;
+}
+
+}  // namespace gr

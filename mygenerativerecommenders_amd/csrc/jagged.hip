@@ -1,0 +1,101 @@
+// Jagged <-> padded layout kernels and the offsets scan.
+// Replace reference utils/ops.py:18-114 (fbgemm asynchronous_complete_cumsum /
+// dense_to_jagged / jagged_to_padded_dense, whose CPU fallback is a per-row Python
+// loop).  All are stream-ordered and sync-free: the total row count is read from
+// offsets[B] on the device.
+#include "common.h"
+
+#include "../../include/gr_hstu.h"
+
+namespace gr {
+
+// single workgroup exclusive scan: offsets[0] = 0, offsets[b+1] = sum_{<=b} lengths
+__global__ __launch_bounds__(1024) void cumsum_kernel(const int64_t* lengths, int B,
+                                                     int64_t* offsets) {
+  __shared__ int64_t part[1024];
+  const int t = threadIdx.x;
+  const int per = (B + 1023) / 1024;
+  const int lo = t * per, hi = min(B, lo + per);
+  int64_t s = 0;
+  for (int i = lo; i < hi; ++i) s += lengths[i];
+  part[t] = s;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan
+    int64_t v = t >= o ? part[t - o] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int64_t run = t ? part[t - 1] : 0;
+  if (t == 0) offsets[0] = 0;
+  for (int i = lo; i < hi; ++i) {
+    run += lengths[i];
+    offsets[i + 1] = run;
+  }
+}
+
+// one wave per padded row (b, p)
+__global__ __launch_bounds__(256) void dense_to_jagged_kernel(const float* dense,
+                                                              const int64_t* offsets, int B,
+                                                              int N, int D, float* jagged) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= (int64_t)B * N) return;
+  const int b = (int)(row / N), p = (int)(row - (int64_t)b * N);
+  const int64_t s0 = offsets[b];
+  if (p >= offsets[b + 1] - s0) return;
+  const float* src = dense + row * D;
+  float* dst = jagged + (s0 + p) * D;
+  for (int c = threadIdx.x & 63; c < D; c += 64) dst[c] = src[c];
+}
+
+__global__ __launch_bounds__(256) void jagged_to_padded_kernel(const float* jagged,
+                                                               const int64_t* offsets, int B,
+                                                               int N, int D, float* dense) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= (int64_t)B * N) return;
+  const int b = (int)(row / N), p = (int)(row - (int64_t)b * N);
+  const int64_t s0 = offsets[b];
+  const bool valid = p < offsets[b + 1] - s0;
+  const float* src = jagged + (s0 + p) * D;
+  float* dst = dense + row * D;
+  for (int c = threadIdx.x & 63; c < D; c += 64) dst[c] = valid ? src[c] : 0.f;
+}
+
+}  // namespace gr
+
+extern "C" {
+
+int gr_complete_cumsum(const int64_t* lengths, int B, int64_t* offsets, void* stream) {
+  GR_REQUIRE(offsets && (B == 0 || lengths) && B >= 0, "gr_complete_cumsum: bad args");
+  hipLaunchKernelGGL(gr::cumsum_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, lengths,
+                     B, offsets);
+  GR_LAUNCH_CHECK("gr_complete_cumsum");
+  return 0;
+}
+
+int gr_dense_to_jagged(const float* dense, const int64_t* offsets, int B, int N, int D,
+                       int64_t max_rows, float* jagged, void* stream) {
+  (void)max_rows;
+  GR_REQUIRE(dense && offsets && jagged && B >= 0 && N >= 0 && D > 0,
+             "gr_dense_to_jagged: bad args");
+  const int64_t rows = (int64_t)B * N;
+  if (rows == 0) return 0;
+  hipLaunchKernelGGL(gr::dense_to_jagged_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256),
+                     0, (hipStream_t)stream, dense, offsets, B, N, D, jagged);
+  GR_LAUNCH_CHECK("gr_dense_to_jagged");
+  return 0;
+}
+
+int gr_jagged_to_padded(const float* jagged, const int64_t* offsets, int B, int N, int D,
+                        float* dense, void* stream) {
+  GR_REQUIRE(dense && offsets && jagged && B >= 0 && N >= 0 && D > 0,
+             "gr_jagged_to_padded: bad args");
+  const int64_t rows = (int64_t)B * N;
+  if (rows == 0) return 0;
+  hipLaunchKernelGGL(gr::jagged_to_padded_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256),
+                     0, (hipStream_t)stream, jagged, offsets, B, N, D, dense);
+  GR_LAUNCH_CHECK("gr_jagged_to_padded");
+  return 0;
+}
+
+}  // extern "C"

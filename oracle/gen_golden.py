@@ -1,0 +1,236 @@
+"""Golden-fixture generator (TEST INFRASTRUCTURE — runs only in the survey/build
+container, never on the GPU box, never on the product path).
+
+It imports the REFERENCE implementation from ``/root/reference/src`` and records
+input -> output pairs as small ``.npz`` files under ``tests/golden/``.  Only these
+data files travel; the reference itself does not.
+
+Fixtures written:
+  * ``bucket_thresholds.npz``  -- for b in [0, 128], the smallest integer |dt| whose
+    reference bucket (``hstu.py:579-581`` lambda, clamped as at ``hstu.py:117-123``)
+    is >= b.  Found by binary search over the reference's own bucketization fn.
+  * ``hstu_*.npz``             -- ``HSTU.forward`` (``hstu.py:633-672``) output and
+    the gradients of the input embeddings and of every encoder parameter, eval mode
+    (dropout off), fp32, jagged lengths, seeded.
+  * ``topk_T1.npz`` / ``topk_T2.npz`` -- ``CandidateIndex.get_top_k_outputs``
+    (``candidate_index.py:107-164``) over ``MIPSBruteForceTopK`` (``top_k.py:44-70``)
+    with invalid ids. T1: random normal; T2: integer-valued, tie-free (exact in any
+    summation order).
+  * ``jagged_ops.npz``         -- the known-answer cases of the reference's
+    ``tests/test_ops.py:7-53`` (cumsum / dense_to_jagged / jagged_to_padded_dense).
+
+Usage:  python oracle/gen_golden.py   (writes tests/golden/*.npz)
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+import torch
+
+REF_SRC = "/root/reference/src"
+HERE = os.path.dirname(os.path.abspath(__file__))
+OUT = os.path.join(os.path.dirname(HERE), "tests", "golden")
+
+
+def _import_reference():
+    if REF_SRC not in sys.path:
+        sys.path.insert(0, REF_SRC)
+    from generative_recommenders_pl.models.indexing.candidate_index import (  # noqa
+        CandidateIndex,
+    )
+    from generative_recommenders_pl.models.indexing.top_k import (  # noqa
+        MIPSBruteForceTopK,
+    )
+    from generative_recommenders_pl.models.sequential_encoders.hstu import HSTU  # noqa
+    from generative_recommenders_pl.models.utils import ops  # noqa
+
+    return HSTU, CandidateIndex, MIPSBruteForceTopK, ops
+
+
+def synth_timestamps(gen: torch.Generator, B: int, N: int, lengths: torch.Tensor):
+    """SURVEY.md §8d timestamps: start U[9.5e8, 1.05e9], Exp(1e5 s) increments,
+    sorted, padded positions 0, the target timestamp sits at index L_b
+    (``features.py:53-57``)."""
+    ts = torch.zeros(B, N, dtype=torch.int64)
+    for b in range(B):
+        L = int(lengths[b])
+        start = 9.5e8 + float(torch.rand(1, generator=gen)) * 1e8
+        inc = -torch.log(torch.rand(L + 1, generator=gen).clamp_min(1e-12)) * 1e5
+        seq = (start + torch.cumsum(inc, 0)).to(torch.int64)
+        n_fill = min(L + 1, N)
+        ts[b, :n_fill] = seq[:n_fill]
+    return ts
+
+
+def gen_bucket_thresholds(HSTU):
+    enc = HSTU(
+        max_sequence_len=4, max_output_len=1, embedding_dim=8, item_embedding_dim=8,
+        num_blocks=1, num_heads=1, linear_dim=8, attention_dim=8,
+        normalization="rel_bias", linear_config="uvqk", linear_activation="silu",
+        linear_dropout_rate=0.0, attn_dropout_rate=0.0,
+    )
+    rab = enc._hstu._attention_layers[0]._rel_attn_bias
+    fn = rab._bucketization_fn
+    nb = rab._num_buckets
+
+    def bucket(x: int) -> int:
+        t = torch.tensor([x], dtype=torch.int64)
+        return int(torch.clamp(fn(t), min=0, max=nb)[0])
+
+    thr = np.zeros(nb + 1, dtype=np.int64)
+    hi_limit = (1 << 62)
+    for b in range(1, nb + 1):
+        lo, hi = 1, hi_limit
+        assert bucket(hi) >= b, b
+        while lo < hi:
+            mid = (lo + hi) // 2
+            if bucket(mid) >= b:
+                hi = mid
+            else:
+                lo = mid + 1
+        thr[b] = lo
+    # monotonicity spot check on a dense + log-spaced sweep
+    xs = np.unique(np.concatenate([
+        np.arange(0, 5000, dtype=np.int64),
+        np.logspace(0, 18, 20000).astype(np.int64),
+        thr, np.maximum(thr - 1, 0), thr + 1,
+    ]))
+    t = torch.from_numpy(xs)
+    ref = torch.clamp(fn(t), min=0, max=nb).numpy()
+    via_table = np.searchsorted(thr, xs, side="right") - 1
+    assert np.array_equal(ref, via_table), "bucket fn is not monotone / table wrong"
+    # negative deltas: reference takes abs()
+    ref_neg = torch.clamp(fn(-t), min=0, max=nb).numpy()
+    assert np.array_equal(ref_neg, via_table)
+    np.savez_compressed(os.path.join(OUT, "bucket_thresholds.npz"), thresholds=thr,
+             probe_x=xs, probe_bucket=ref.astype(np.int64))
+    print("bucket thresholds:", thr[:16].tolist(), "... max", thr[-1])
+    return thr
+
+
+def gen_hstu_case(HSTU, name, B, N0, out_len, D, H, dqk, dv, blocks, seed,
+                  lengths=None, with_ts=True, concat_ua=False):
+    torch.manual_seed(seed)
+    gen = torch.Generator().manual_seed(seed)
+    N = N0 + out_len
+    enc = HSTU(
+        max_sequence_len=N0, max_output_len=out_len, embedding_dim=D,
+        item_embedding_dim=D, num_blocks=blocks, num_heads=H, linear_dim=dv,
+        attention_dim=dqk, normalization="rel_bias", linear_config="uvqk",
+        linear_activation="silu", linear_dropout_rate=0.2, attn_dropout_rate=0.0,
+        concat_ua=concat_ua,
+    )
+    # the reference zero-inits nothing; pos/ts weights are N(0, 0.02).  Scale them up
+    # so the bias path is exercised with O(1) magnitudes.
+    with torch.no_grad():
+        for layer in enc._hstu._attention_layers:
+            layer._rel_attn_bias._ts_w.normal_(0, 0.5, generator=gen)
+            layer._rel_attn_bias._pos_w.normal_(0, 0.5, generator=gen)
+            layer._o.bias.normal_(0, 0.1, generator=gen)
+    enc.eval()
+    if lengths is None:
+        lengths = torch.randint(1, N0 + 1, (B,), generator=gen)
+    lengths = torch.as_tensor(lengths, dtype=torch.int64)
+    x = torch.randn(B, N, D, generator=gen)
+    # padded rows are ignored by the reference (dense_to_jagged drops them)
+    ts = synth_timestamps(gen, B, N, lengths)
+    payload = {"timestamps": ts} if with_ts else {}
+    x.requires_grad_(True)
+    y, _ = enc(past_lengths=lengths, user_embeddings=x,
+               valid_mask=torch.ones(B, N, 1), past_payloads=payload)
+    dy = torch.randn(y.shape, generator=gen)
+    (y * dy).sum().backward()
+    rec = {
+        "B": B, "N0": N0, "out_len": out_len, "N": N, "D": D, "H": H, "dqk": dqk,
+        "dv": dv, "blocks": blocks, "with_ts": int(with_ts), "concat_ua": int(concat_ua),
+        "lengths": lengths.numpy(), "x": x.detach().numpy(), "ts": ts.numpy(),
+        "y": y.detach().numpy(), "dy": dy.numpy(), "dx": x.grad.numpy(),
+    }
+    for pname, p in enc.named_parameters():
+        rec["param:" + pname] = p.detach().numpy()
+        rec["grad:" + pname] = (p.grad if p.grad is not None
+                                else torch.zeros_like(p)).numpy()
+    np.savez_compressed(os.path.join(OUT, f"hstu_{name}.npz"), **rec)
+    print(f"hstu_{name}: y {tuple(y.shape)} |y|max {y.abs().max():.3f}")
+
+
+def gen_topk_case(CandidateIndex, MIPSBruteForceTopK, name, B, X, D, k, N0, seed,
+                  integer=False):
+    gen = torch.Generator().manual_seed(seed)
+    ids = torch.arange(1, X + 1, dtype=torch.int64)
+    if integer:
+        # T2: integer-valued so fp32 sums are exact in ANY order; tie-free via the
+        # last component e_last = j (item index), q_last = 1, other dims scaled 2^12.
+        assert X <= 4096
+        E = torch.randint(-8, 9, (X, D), generator=gen).float() * 4096.0
+        E[:, -1] = torch.arange(X).float()
+        Q = torch.randint(-8, 9, (B, D), generator=gen).float()
+        Q[:, -1] = 1.0
+    else:
+        E = torch.randn(X, D, generator=gen)
+        E = E / E.norm(dim=-1, keepdim=True).clamp_min(1e-6)
+        Q = torch.randn(B, D, generator=gen)
+        Q = Q / Q.norm(dim=-1, keepdim=True).clamp_min(1e-6)
+    # invalid ids: mostly drawn from the top of each row's ranking (so exclusion
+    # matters), tail zero-padded like past_ids padding.
+    logits = Q @ E.T
+    order = torch.argsort(logits, dim=1, descending=True)
+    invalid = torch.zeros(B, N0, dtype=torch.int64)
+    for b in range(B):
+        n_valid = int(torch.randint(N0 // 2, N0 + 1, (1,), generator=gen))
+        pick = order[b, : 2 * N0][torch.randperm(2 * N0, generator=gen)[:n_valid]]
+        invalid[b, :n_valid] = ids[pick]
+    index = CandidateIndex(k=k, ids=ids, top_k_module=MIPSBruteForceTopK(),
+                           embeddings=E.unsqueeze(0))
+    top_ids, top_scores = index.get_top_k_outputs(query_embeddings=Q, invalid_ids=invalid)
+    np.savez_compressed(
+        os.path.join(OUT, f"topk_{name}.npz"), Q=Q.numpy(), E=E.numpy(), ids=ids.numpy(),
+        invalid=invalid.numpy(), k=k, top_ids=top_ids.numpy(),
+        top_scores=top_scores.numpy(), integer=int(integer))
+    print(f"topk_{name}: B={B} X={X} D={D} k={k} N0={N0}")
+
+
+def gen_jagged_ops(ops):
+    lengths = torch.tensor([1, 2], dtype=torch.int32)
+    offs = ops.asynchronous_complete_cumsum(lengths)
+    dense = torch.tensor([[1.0, 2, 3], [4, 5, 6]]).unsqueeze(-1)
+    jag = ops.dense_to_jagged(dense, offs)
+    values = torch.tensor([1.0, 4, 5]).unsqueeze(-1)
+    offs2 = torch.tensor([0, 1, 3])
+    pad = ops.jagged_to_padded_dense(values, offs2, 3, 0)
+    np.savez(os.path.join(OUT, "jagged_ops.npz"), lengths=lengths.numpy(),
+             offsets=offs.numpy(), dense=dense.numpy(), jagged=jag.numpy(),
+             values=values.numpy(), offsets2=offs2.numpy(), padded=pad.numpy())
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    HSTU, CandidateIndex, MIPSBruteForceTopK, ops = _import_reference()
+    gen_bucket_thresholds(HSTU)
+    gen_jagged_ops(ops)
+    # HSTU goldens: B=4, N0 in {16, 32}, D in {16, 50},
+    # h in {1, 2}, 2 blocks, jagged lengths.
+    gen_hstu_case(HSTU, "b4_n16_d16_h1", 4, 16, 11, 16, 1, 16, 16, 2, seed=1)
+    gen_hstu_case(HSTU, "b4_n32_d50_h1", 4, 32, 11, 50, 1, 50, 50, 2, seed=2)
+    gen_hstu_case(HSTU, "b4_n32_d16_h2", 4, 32, 11, 16, 2, 8, 8, 2, seed=3)
+    gen_hstu_case(HSTU, "b3_n64_d50_h2", 3, 64, 11, 50, 2, 25, 25, 2, seed=4,
+                  lengths=[64, 1, 37])
+    # full-length row (L_b = N0 so query N-1 ... uses ts[N-1] wrap) and no-timestamp
+    gen_hstu_case(HSTU, "b2_n8_d16_full", 2, 8, 0, 16, 1, 16, 16, 2, seed=5,
+                  lengths=[8, 5])
+    gen_hstu_case(HSTU, "b3_n16_d16_nots", 3, 16, 11, 16, 1, 16, 16, 2, seed=6,
+                  with_ts=False)
+    gen_hstu_case(HSTU, "b2_n16_d16_cua", 2, 16, 11, 16, 1, 16, 16, 1, seed=7,
+                  concat_ua=True)
+    gen_topk_case(CandidateIndex, MIPSBruteForceTopK, "T1", 16, 3000, 50, 200, 211,
+                  seed=11)
+    gen_topk_case(CandidateIndex, MIPSBruteForceTopK, "T2", 16, 4000, 50, 200, 211,
+                  seed=12, integer=True)
+    gen_topk_case(CandidateIndex, MIPSBruteForceTopK, "T3_small", 5, 300, 16, 10, 7,
+                  seed=13)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,188 @@
+"""CPU oracle for the HSTU encoder hot path — TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg
+may import this module, and only as the checker (or the timed CPU baseline) — never
+as the thing measured or shipped.  The product path lives in
+``mygenerativerecommenders_amd`` and fails loudly without its HIP library.
+
+This is a from-scratch fp32 restatement (PyTorch CPU tensors, autograd for the
+backward) of the reference's algorithm, parity-pinned against the golden fixtures
+under ``tests/golden/hstu_*.npz`` that ``oracle/gen_golden.py`` recorded from the
+reference itself (``tests/test_oracle_golden.py``).
+
+Two variants:
+  * jagged (``hstu_forward``): per-sequence dense L_b x L_b blocks — the math the
+    HIP kernels implement;
+  * padded (``hstu_forward_padded``): the reference's batched (B, N, N) op order,
+    used as the CPU throughput baseline (SURVEY.md §8d "padded-order restatement").
+
+Reference map (paths relative to ``src/generative_recommenders_pl/models``):
+  * relative bias ........ ``sequential_encoders/hstu.py:96-128`` (+ bucket fn 579-581)
+  * attention ............ ``sequential_encoders/hstu.py:134-205`` (non-cache branch)
+  * STU layer ............ ``sequential_encoders/hstu.py:266-423``
+  * HSTUJagged ........... ``sequential_encoders/hstu.py:439-518``
+  * HSTU.forward ......... ``sequential_encoders/hstu.py:633-672``
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+NUM_BUCKETS = 128  # hstu.py:577
+
+
+def bucket_reference_semantics(delta: torch.Tensor) -> torch.Tensor:
+    """hstu.py:579-581 + the clamp at hstu.py:117-123: fp32 log of |dt| clamped to 1,
+    divided by 0.301, truncated, clamped to [0, 128]."""
+    return torch.clamp(
+        (torch.log(torch.abs(delta).clamp(min=1)) / 0.301).long(), 0, NUM_BUCKETS)
+
+
+def bucket_via_thresholds(delta: torch.Tensor, thresholds: np.ndarray) -> torch.Tensor:
+    """The integer-threshold form the HIP kernels use: bucket = max{b : T[b] <= |dt|}."""
+    thr = torch.as_tensor(thresholds, dtype=torch.int64)
+    return torch.searchsorted(thr, delta.abs().contiguous(), right=True) - 1
+
+
+@dataclass
+class HSTUConfig:
+    N: int  # padded max length = max_sequence_len + max_output_len (hstu.py:596-605)
+    D: int
+    H: int
+    dqk: int
+    dv: int
+    concat_ua: bool = False
+    eps: float = 1e-6  # hstu.py:224
+
+
+def layer_params_from_state(state: Dict[str, torch.Tensor], i: int,
+                            prefix: str = "_hstu._attention_layers") -> Dict[str, torch.Tensor]:
+    p = f"{prefix}.{i}."
+    return {
+        "uvqk": state[p + "_uvqk"],
+        "o_w": state[p + "_o.weight"],
+        "o_b": state[p + "_o.bias"],
+        "ts_w": state[p + "_rel_attn_bias._ts_w"],
+        "pos_w": state[p + "_rel_attn_bias._pos_w"],
+    }
+
+
+def rel_bias_jagged(ts_b: torch.Tensor, L: int, N: int, pos_w: torch.Tensor,
+                    ts_w: torch.Tensor, thresholds: np.ndarray) -> torch.Tensor:
+    """(L, L) slice of the (N, N) bias of hstu.py:96-128 for one sequence.
+
+    pos[i, j] = pos_w[N - 1 + j - i] (the pad/repeat/reshape trick of :106-110,124);
+    query i uses the timestamp of item i + 1, with ext_ts[N] = ts[N - 1] (:113-119).
+    """
+    i = torch.arange(L)
+    j = torch.arange(L)
+    pos = pos_w[(N - 1) + j.view(1, L) - i.view(L, 1)]
+    ext = torch.cat([ts_b, ts_b[N - 1:N]])
+    delta = ext[1:L + 1].view(L, 1) - ts_b[:L].view(1, L)
+    bucket = bucket_via_thresholds(delta, thresholds)
+    return pos + ts_w[bucket]
+
+
+def hstu_attention_jagged(q, k, v, offsets, ts, cfg: HSTUConfig, pos_w, ts_w,
+                          thresholds) -> torch.Tensor:
+    """hstu.py:134-205 restated jagged: A = silu(QK^T + bias) / N, causal j <= i."""
+    H, dqk, dv, N = cfg.H, cfg.dqk, cfg.dv, cfg.N
+    outs = []
+    B = offsets.numel() - 1
+    for b in range(B):
+        s, e = int(offsets[b]), int(offsets[b + 1])
+        L = e - s
+        if L == 0:
+            continue
+        qb = q[s:e].view(L, H, dqk).transpose(0, 1)  # (H, L, dqk)
+        kb = k[s:e].view(L, H, dqk).transpose(0, 1)
+        vb = v[s:e].view(L, H, dv).transpose(0, 1)
+        scores = qb @ kb.transpose(1, 2)  # (H, L, L)
+        if ts is not None:
+            scores = scores + rel_bias_jagged(ts[b], L, N, pos_w, ts_w, thresholds)
+        a = F.silu(scores) / N
+        a = a * torch.tril(torch.ones(L, L, dtype=a.dtype))
+        outs.append((a @ vb).transpose(0, 1).reshape(L, H * dv))
+    return torch.cat(outs, 0) if outs else q.new_zeros(0, H * dv)
+
+
+def stu_layer_jagged(x, offsets, ts, cfg: HSTUConfig, p, thresholds):
+    """hstu.py:266-413 (eval mode, normalization='rel_bias', linear_config='uvqk',
+    linear_activation='silu')."""
+    H, dv, dqk = cfg.H, cfg.dv, cfg.dqk
+    normed = F.layer_norm(x, [cfg.D], eps=cfg.eps)
+    h = F.silu(normed @ p["uvqk"])
+    u, v, q, k = torch.split(h, [dv * H, dv * H, dqk * H, dqk * H], dim=1)
+    attn = hstu_attention_jagged(q, k, v, offsets, ts, cfg, p["pos_w"], p["ts_w"],
+                                 thresholds)
+    a = F.layer_norm(attn, [dv * H], eps=cfg.eps)
+    o_in = torch.cat([u, a, u * a], -1) if cfg.concat_ua else u * a
+    return o_in @ p["o_w"].t() + p["o_b"] + x
+
+
+def hstu_forward(lengths: torch.Tensor, user_embeddings: torch.Tensor,
+                 ts: Optional[torch.Tensor], cfg: HSTUConfig,
+                 layers: List[Dict[str, torch.Tensor]], thresholds) -> torch.Tensor:
+    """hstu.py:633-672 -> 482-518: dense->jagged, layer loop, jagged->padded (rows
+    >= L_b are zero)."""
+    B, N, D = user_embeddings.shape
+    offsets = torch.cat([torch.zeros(1, dtype=torch.int64),
+                         torch.cumsum(lengths.to(torch.int64), 0)])
+    rows = [user_embeddings[b, :int(lengths[b])] for b in range(B)]
+    x = torch.cat(rows, 0)
+    for p in layers:
+        x = stu_layer_jagged(x, offsets, ts, cfg, p, thresholds)
+    out = user_embeddings.new_zeros(B, N, D)
+    parts = []
+    for b in range(B):
+        s, e = int(offsets[b]), int(offsets[b + 1])
+        pad = user_embeddings.new_zeros(N - (e - s), D)
+        parts.append(torch.cat([x[s:e], pad], 0))
+    out = torch.stack(parts, 0)
+    return out
+
+
+# ----------------------------------------------------------------------------------
+# Padded (reference op-order) variant: the CPU throughput baseline.
+# ----------------------------------------------------------------------------------
+
+def rel_bias_padded(ts: torch.Tensor, N: int, pos_w, ts_w, thresholds) -> torch.Tensor:
+    """hstu.py:96-128 batched: (B, N, N)."""
+    i = torch.arange(N)
+    pos = pos_w[(N - 1) + i.view(1, N) - i.view(N, 1)]
+    ext = torch.cat([ts, ts[:, N - 1:N]], 1)
+    delta = ext[:, 1:].unsqueeze(2) - ext[:, :-1].unsqueeze(1)
+    bucket = bucket_reference_semantics(delta)
+    return pos.unsqueeze(0) + ts_w[bucket.view(-1)].view(ts.shape[0], N, N)
+
+
+def hstu_forward_padded(lengths, user_embeddings, ts, cfg: HSTUConfig, layers,
+                        thresholds=None) -> torch.Tensor:
+    """Same result as ``hstu_forward``; computes on the padded (B, N, ·) layout with
+    the reference's batched op order (bmm over (B, H, N, N)), masking padded rows."""
+    B, N, D = user_embeddings.shape
+    H, dqk, dv = cfg.H, cfg.dqk, cfg.dv
+    valid = (torch.arange(N).view(1, N) < lengths.view(B, 1)).to(user_embeddings.dtype)
+    valid = valid.unsqueeze(-1)
+    causal = torch.tril(torch.ones(N, N, dtype=user_embeddings.dtype))
+    x = user_embeddings * valid
+    for p in layers:
+        normed = F.layer_norm(x, [D], eps=cfg.eps)
+        h = F.silu(normed @ p["uvqk"])
+        u, v, q, k = torch.split(h, [dv * H, dv * H, dqk * H, dqk * H], dim=-1)
+        q = q * valid
+        k = k * valid
+        v = v * valid
+        s = torch.einsum("bnhd,bmhd->bhnm", q.view(B, N, H, dqk), k.view(B, N, H, dqk))
+        if ts is not None:
+            s = s + rel_bias_padded(ts, N, p["pos_w"], p["ts_w"], thresholds).unsqueeze(1)
+        a = F.silu(s) / N * causal
+        attn = torch.einsum("bhnm,bmhd->bnhd", a, v.view(B, N, H, dv)).reshape(B, N, H * dv)
+        an = F.layer_norm(attn, [dv * H], eps=cfg.eps)
+        o_in = torch.cat([u, an, u * an], -1) if cfg.concat_ua else u * an
+        x = (o_in @ p["o_w"].t() + p["o_b"] + x) * valid
+    return x

@@ -1,0 +1,93 @@
+"""GPU parity: HIP jagged HSTU attention vs the CPU oracle (oracle/hstu_oracle.py,
+itself pinned to the reference's golden fixtures).  Tolerance: fp32 — max abs error
+<= 2e-5 * (1 + max|ref|) on outputs; the kernel is f32 MFMA (exact fp32 products,
+different summation order from MKL)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import hstu_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+THR = None
+
+
+def _thr():
+    from mygenerativerecommenders_amd.bucket_table import BUCKET_THRESHOLDS
+    return np.asarray(BUCKET_THRESHOLDS, dtype=np.int64)
+
+
+def _case(seed, B, N, H, dqk, dv, lengths=None, with_ts=True, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    if lengths is None:
+        lengths = torch.randint(1, N + 1, (B,), generator=g)
+    lengths = torch.as_tensor(lengths, dtype=torch.int64)
+    offsets = torch.cat([torch.zeros(1, dtype=torch.int64), torch.cumsum(lengths, 0)])
+    T = int(offsets[-1])
+    uvqk = torch.randn(T, 2 * H * dv + 2 * H * dqk, generator=g) * scale
+    ts = None
+    if with_ts:
+        start = torch.randint(950_000_000, 1_050_000_000, (B, 1), generator=g)
+        inc = (torch.rand(B, N, generator=g) * 3e5).to(torch.int64)
+        ts = start + torch.cumsum(inc, 1)
+    pos_w = torch.randn(2 * N - 1, generator=g) * 0.5
+    ts_w = torch.randn(129, generator=g) * 0.5
+    return lengths, offsets, uvqk, ts, pos_w, ts_w
+
+
+def _run_gpu_fwd(offsets, uvqk, ts, pos_w, ts_w, B, N, H, dqk, dv):
+    from mygenerativerecommenders_amd import _lib
+    dev = torch.device("cuda")
+    u = uvqk.to(dev)
+    hv, hq = H * dv, H * dqk
+    q = u[:, 2 * hv:2 * hv + hq]
+    k = u[:, 2 * hv + hq:]
+    v = u[:, hv:2 * hv]
+    out = torch.full((u.shape[0], hv), float("nan"), device=dev)
+    offs = offsets.to(dev)
+    thr = torch.tensor(_thr(), device=dev)
+    tsd = ts.to(dev) if ts is not None else None
+    pw = pos_w.to(dev)
+    tw = ts_w.to(dev)
+    max_len = int((offsets[1:] - offsets[:-1]).max()) if B else 0
+    _lib.call("hstu_attn_fwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), u.stride(0), u.stride(0),
+              offs.data_ptr(), B, N, max_len, H, dqk, dv, _lib.ptr(tsd), pw.data_ptr(),
+              tw.data_ptr(), thr.data_ptr(), 128, out.data_ptr(), out.stride(0),
+              _lib.stream_handle())
+    torch.cuda.synchronize()
+    return out.cpu()
+
+
+@pytest.mark.parametrize("B,N,H,dqk,dv,with_ts", [
+    (4, 43, 1, 16, 16, True),
+    (4, 43, 1, 50, 50, True),
+    (3, 75, 2, 25, 25, True),
+    (2, 211, 1, 50, 50, True),
+    (3, 130, 2, 8, 8, False),
+    (2, 150, 1, 64, 64, True),
+    (2, 100, 1, 128, 96, True),
+])
+def test_attn_fwd_vs_oracle(B, N, H, dqk, dv, with_ts):
+    lengths, offsets, uvqk, ts, pos_w, ts_w = _case(B * 7 + N, B, N, H, dqk, dv,
+                                                      with_ts=with_ts)
+    hv, hq = H * dv, H * dqk
+    q = uvqk[:, 2 * hv:2 * hv + hq]
+    k = uvqk[:, 2 * hv + hq:]
+    v = uvqk[:, hv:2 * hv]
+    cfg = O.HSTUConfig(N=N, D=1, H=H, dqk=dqk, dv=dv)
+    ref = O.hstu_attention_jagged(q, k, v, offsets, ts, cfg, pos_w, ts_w, _thr())
+    got = _run_gpu_fwd(offsets, uvqk, ts, pos_w, ts_w, B, N, H, dqk, dv)
+    tol = 2e-5 * (1 + ref.abs().max().item())
+    assert torch.isfinite(got).all()
+    assert (got - ref).abs().max().item() <= tol
+
+
+def test_attn_fwd_full_length_and_len1():
+    B, N, H, d = 3, 64, 1, 16
+    lengths, offsets, uvqk, ts, pos_w, ts_w = _case(5, B, N, H, d, d, lengths=[64, 1, 63])
+    q, k, v = uvqk[:, 2 * d:3 * d], uvqk[:, 3 * d:], uvqk[:, d:2 * d]
+    cfg = O.HSTUConfig(N=N, D=1, H=H, dqk=d, dv=d)
+    ref = O.hstu_attention_jagged(q, k, v, offsets, ts, cfg, pos_w, ts_w, _thr())
+    got = _run_gpu_fwd(offsets, uvqk, ts, pos_w, ts_w, B, N, H, d, d)
+    assert (got - ref).abs().max().item() <= 2e-5 * (1 + ref.abs().max().item())
