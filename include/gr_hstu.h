@@ -72,6 +72,87 @@ GR_API int hstu_attn_fwd(const float* q, const float* k, const float* v, int64_t
                   const float* ts_w, const int64_t* bucket_thr, int num_buckets,
                   float* out, int64_t ld_out, void* stream);
 
+/* Backward of hstu_attn_fwd (replaces the autograd backward of hstu.py:134-205 and of
+ * the bias module hstu.py:96-128, including the index_add_ into _ts_w and the
+ * slice/pad backward into _pos_w).  dout: (total, H*dv), stride ld_dout.
+ * Writes dq, dk (total, H*dqk) and dv (total, H*dv), all with row stride ld_d.
+ * hq/hk/hv: optional UVQK pre-activation columns (stride ld_h); when given the
+ * outputs are multiplied by silu'(h) (hstu.py:303-305), i.e. they are gradients of
+ * the pre-activation.  dpos_w (2N-1) and dts_w (num_buckets+1) are OVERWRITTEN
+ * with this call's bias gradients (summed over heads) when ts != NULL.
+ * Deterministic: no global atomics; the workspace (size below, only needed when
+ * ts != NULL) holds one partial slab per workgroup, reduced in a fixed order.
+ */
+GR_API size_t hstu_attn_bwd_workspace_size(int B, int N, int max_len, int H, int num_buckets);
+GR_API int hstu_attn_bwd(const float* q, const float* k, const float* v, int64_t ld_qk,
+                  int64_t ld_v, const float* dout, int64_t ld_dout, const int64_t* offsets,
+                  int B, int N, int max_len, int H, int dqk, int dv, const int64_t* ts,
+                  const float* pos_w, const float* ts_w, const int64_t* bucket_thr,
+                  int num_buckets, const float* hq, const float* hk, const float* hv,
+                  int64_t ld_h, float* dq, float* dk, float* dv_out, int64_t ld_d,
+                  float* dpos_w, float* dts_w, void* workspace, size_t ws_bytes,
+                  void* stream);
+
+/* ---------------------------------------------------------------- STU projections
+ * All take jagged rows (total = offsets[B] <= max_rows), fp32, f32 MFMA.
+ * Row statistics are stored as float2 (mean, rstd) per row, biased variance, as
+ * F.layer_norm without affine (hstu.py:258-264).
+ *
+ * hstu_ln_uvqk_fwd  (replaces hstu.py:300-305: layer_norm -> mm(_uvqk) -> silu):
+ *   x_stats[m] = (mean, rstd) of x[m, :D];  h = LN(x) @ w_uvqk (w: (D, n_out) row-major)
+ *   uvqk = activation ? silu(h) : h  (activation 1 = "silu", 0 = "none");
+ *   h_pre (optional, same stride ld_out) receives h for the backward.
+ */
+GR_API int hstu_ln_uvqk_fwd(const float* x, int64_t ld_x, const int64_t* offsets, int B,
+                     int64_t max_rows, int D, const float* w_uvqk, int n_out, float eps,
+                     int activation, float* x_stats, float* h_pre, float* uvqk,
+                     int64_t ld_out, void* stream);
+
+/* hstu_gate_o_fwd  (replaces hstu.py:393-413 with concat_ua = False):
+ *   attn_stats[m] = (mean, rstd) of attn[m, :hdv]
+ *   o_in = dropout_p(u * LN(attn))  (mask = counter hash of (seed, m*hdv + k))
+ *   y = o_in @ w_o^T + b_o + x_res   (w_o: (D, hdv) row-major = nn.Linear.weight)
+ *   o_in (optional, contiguous (rows, hdv)) is stored for the weight gradient.
+ *   b_o and x_res may be NULL.
+ */
+GR_API int hstu_gate_o_fwd(const float* u, int64_t ld_u, const float* attn, int64_t ld_attn,
+                    const int64_t* offsets, int B, int64_t max_rows, int hdv, int D,
+                    const float* w_o, const float* b_o, const float* x_res, int64_t ld_x,
+                    float eps, float dropout_p, uint64_t seed, float* attn_stats,
+                    float* o_in, float* y, int64_t ld_y, void* stream);
+
+/* hstu_gate_o_bwd  (backward of hstu_gate_o_fwd w.r.t. u and attn; hdv <= 256):
+ *   g = (dy @ w_o) * dropout mask;  du = g * LN(attn) [* silu'(h_u) if h_u];
+ *   d_attn = LayerNorm_backward(attn; g * u).
+ */
+GR_API int hstu_gate_o_bwd(const float* dy, int64_t ld_dy, const int64_t* offsets, int B,
+                    int64_t max_rows, int hdv, int D, const float* w_o, const float* u,
+                    int64_t ld_u, const float* attn, int64_t ld_attn,
+                    const float* attn_stats, const float* h_u, int64_t ld_h,
+                    float dropout_p, uint64_t seed, float* du, int64_t ld_du,
+                    float* d_attn, int64_t ld_da, void* stream);
+
+/* hstu_ln_uvqk_bwd  (backward of hstu_ln_uvqk_fwd w.r.t. x, plus the residual; D <= 256):
+ *   dn = dh @ w_uvqk^T;  dx = dy_res + LayerNorm_backward(x; dn)   (dy_res may be NULL;
+ *   dx may alias dy_res).  dh is the gradient of the pre-activation h.
+ */
+GR_API int hstu_ln_uvqk_bwd(const float* dh, int64_t ld_dh, const int64_t* offsets, int B,
+                     int64_t max_rows, int D, int n_out, const float* w_uvqk,
+                     const float* x, int64_t ld_x, const float* x_stats,
+                     const float* dy_res, int64_t ld_dy, float* dx, int64_t ld_dx,
+                     void* stream);
+
+/* gr_wgrad: weight gradient C = A'^T B over all jagged rows (replaces the mm-backward
+ * of hstu.py:303 and of the _o Linear at hstu.py:404-411):
+ *   C[ka, nb] = sum_m A'[m, ka] * Bm[m, nb],  A' = A or (A - mean_m) * rstd_m when
+ *   a_stats != NULL;  a_colsum (optional) = sum_m A[m, :] (the Linear bias gradient).
+ *   C (Ka, Nb) and a_colsum are overwritten.  Deterministic split-M slabs.
+ */
+GR_API size_t gr_wgrad_workspace_size(int64_t max_rows, int Ka, int Nb);
+GR_API int gr_wgrad(const float* a, int64_t lda, const float* a_stats, const float* bm,
+             int64_t ldb, const int64_t* offsets, int B, int64_t max_rows, int Ka, int Nb,
+             float* c, float* a_colsum, void* workspace, size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }  /* extern "C" */
 #endif

@@ -1,0 +1,585 @@
+// Fused projection GEMMs of the STU layer — gfx950, f32 MFMA (v_mfma_f32_16x16x4_f32).
+//
+// Reference: sequential_encoders/hstu.py:258-305 (LayerNorm -> mm(_uvqk) -> silu) and
+// hstu.py:393-413 (u * LayerNorm(attn) -> dropout -> Linear _o -> + x), plus their
+// autograd backward.  Each reference chain of 3-6 ATen kernels (and their backward)
+// is one launch here:
+//   hstu_ln_uvqk_fwd : row stats of x, (x-mu)*rstd staged on the fly, GEMM, silu epilogue
+//   hstu_gate_o_fwd  : row stats of attn, u*LN(attn)*dropout staged on the fly, GEMM,
+//                      bias + residual epilogue
+//   hstu_gate_o_bwd  : dy @ W_o, epilogue = dropout bwd + gating bwd + LayerNorm bwd
+//                      (row reductions in registers) + silu' of u
+//   hstu_ln_uvqk_bwd : dh @ W_uvqk^T, epilogue = LayerNorm bwd + residual
+//   gr_wgrad         : weight gradients A^T B (K = all rows) as split-M partial slabs
+//                      reduced in a fixed order (deterministic, no atomics)
+//
+// Row-panel GEMM core: a 256-thread workgroup owns 64 rows (wave w: rows 16w..16w+15)
+// and a panel of up to 256 output columns; K is streamed in chunks of 16 through LDS.
+// A operand layout (row stride 18 == 18 mod 32) and B layout (stride == 16 mod 32) make
+// the per-k-step ds_read_b32 of both operands bank-conflict-free.
+#include "common.h"
+
+#include "../../include/gr_hstu.h"
+
+namespace gr {
+
+constexpr int BM = 64;
+constexpr int BK = 16;
+constexpr int LDA = BK + 2;
+
+template <int NT>
+struct PanelCfg {
+  static constexpr int BN = NT * 16;
+  static constexpr int LDB = (NT & 1) ? BN : BN + 16;  // == 16 mod 32
+};
+
+// Row statistics (mean, rstd) of rows [m0, m0+64) over K columns: 4 threads per row,
+// two passes (the second one re-reads through L1/L2).
+__device__ __forceinline__ void panel_row_stats(const float* base, int64_t ld, int64_t m0,
+                                                int64_t total, int K, float eps,
+                                                float2* st_lds, float2* st_glob) {
+  const int t = threadIdx.x;
+  const int r = t >> 2, sub = t & 3;
+  const int64_t m = m0 + r;
+  float mean = 0.f, rstd = 0.f;
+  if (m < total) {
+    const float* row = base + m * ld;
+    float s = 0.f;
+    for (int k = sub; k < K; k += 4) s += row[k];
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    mean = s / (float)K;
+    float v = 0.f;
+    for (int k = sub; k < K; k += 4) {
+      const float d = row[k] - mean;
+      v += d * d;
+    }
+    v += __shfl_xor(v, 1, 64);
+    v += __shfl_xor(v, 2, 64);
+    rstd = rsqrtf(v / (float)K + eps);
+  }
+  if (sub == 0) {
+    st_lds[r] = make_float2(mean, rstd);
+    if (st_glob && m < total) st_glob[m] = make_float2(mean, rstd);
+  }
+}
+
+// Generic row-panel GEMM: C[m, n] = sum_k Op::a(m, k) * Op::b(k, n), epilogue by Op.
+template <int NT, class Op>
+__global__ __launch_bounds__(256) void rowpanel_kernel(Op op) {
+  using P = PanelCfg<NT>;
+  __shared__ __attribute__((aligned(16))) float As[BM * LDA];
+  __shared__ __attribute__((aligned(16))) float Bs[BK * P::LDB];
+  __shared__ float2 stats[BM];
+  const int64_t total = op.offsets[op.B];
+  const int64_t m0 = (int64_t)blockIdx.x * BM;
+  if (m0 >= total) return;
+  const int n0 = blockIdx.y * P::BN;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int lr = lane & 15, lg = lane >> 4;
+
+  op.prologue(m0, total, stats);
+  __syncthreads();
+
+  f4 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f4_zero();
+
+  for (int k0 = 0; k0 < op.K; k0 += BK) {
+    // ---- stage A (64 x 16) and B (16 x BN)
+#pragma unroll
+    for (int i = 0; i < (BM * BK) / 256; ++i) {
+      const int e = tid + 256 * i;
+      const int r = e >> 4, c = e & 15;
+      const int64_t m = m0 + r;
+      const int k = k0 + c;
+      As[r * LDA + c] = (m < total && k < op.K) ? op.a(m, k, stats[r]) : 0.f;
+    }
+    if (Op::B_N_CONTIG) {
+      for (int e = tid; e < BK * P::BN; e += 256) {
+        const int kk = e / P::BN, c = e - kk * P::BN;
+        const int k = k0 + kk, n = n0 + c;
+        Bs[kk * P::LDB + c] = (k < op.K && n < op.N) ? op.b(k, n) : 0.f;
+      }
+    } else {
+      for (int e = tid; e < BK * P::BN; e += 256) {
+        const int c = e >> 4, kk = e & 15;
+        const int k = k0 + kk, n = n0 + c;
+        Bs[kk * P::LDB + c] = (k < op.K && n < op.N) ? op.b(k, n) : 0.f;
+      }
+    }
+    __syncthreads();
+    const float* arow = As + (w * 16 + lr) * LDA + lg;
+#pragma unroll
+    for (int ks = 0; ks < BK / 4; ++ks) {
+      const float av = arow[4 * ks];
+      const float* brow = Bs + (4 * ks + lg) * P::LDB + lr;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = mfma16x16x4(av, brow[t * 16], acc[t]);
+    }
+    __syncthreads();
+  }
+  // acc[t][r] = C[m0 + 16w + 4lg + r][n0 + 16t + lr]
+  op.epilogue(acc, m0 + w * 16 + 4 * lg, n0 + lr, total, stats + w * 16 + 4 * lg);
+}
+
+// ------------------------------------------------------------------ ops
+struct NoStats {
+  __device__ void prologue(int64_t, int64_t, float2* st) const {
+    if (threadIdx.x < BM) st[threadIdx.x] = make_float2(0.f, 1.f);
+  }
+};
+
+// F1: uvqk = act(LN(x) @ W), W row-major (D, n_out)
+struct OpLnUvqk {
+  static constexpr bool B_N_CONTIG = true;
+  const int64_t* offsets;
+  int B, K, N;
+  const float* x;
+  int64_t ldx;
+  const float* w;
+  float eps;
+  int act;
+  float2* x_stats;
+  float* h_pre;
+  float* out;
+  int64_t ld_out;
+  __device__ void prologue(int64_t m0, int64_t total, float2* st) const {
+    panel_row_stats(x, ldx, m0, total, K, eps, st, blockIdx.y == 0 ? x_stats : nullptr);
+  }
+  __device__ float a(int64_t m, int k, float2 st) const { return (x[m * ldx + k] - st.x) * st.y; }
+  __device__ float b(int k, int n) const { return w[(int64_t)k * N + n]; }
+  template <int NT>
+  __device__ void epilogue(f4 (&acc)[NT], int64_t mrow, int ncol, int64_t total,
+                           const float2*) const {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t m = mrow + r;
+      if (m >= total) continue;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int n = ncol + 16 * t;
+        if (n >= N) continue;
+        const float v = acc[t][r];
+        if (h_pre) h_pre[m * ld_out + n] = v;
+        out[m * ld_out + n] = act ? siluf_(v) : v;
+      }
+    }
+  }
+};
+
+__device__ __forceinline__ float dropout_keep(uint64_t seed, int64_t m, int k, int K, float p) {
+  if (p <= 0.f) return 1.f;
+  const uint32_t hsh = hash_u32(seed, (uint64_t)m * (uint64_t)K + (uint64_t)k);
+  const uint32_t thr = (uint32_t)(p * 4294967296.0);
+  return hsh >= thr ? 1.f / (1.f - p) : 0.f;
+}
+
+// F3: y = dropout(u * LN(attn)) @ W_o^T + b_o + x,  W_o row-major (D, hdv)
+struct OpGateO {
+  static constexpr bool B_N_CONTIG = false;
+  const int64_t* offsets;
+  int B, K, N;  // K = hdv, N = D
+  const float* u;
+  int64_t ldu;
+  const float* attn;
+  int64_t lda;
+  const float* w;
+  const float* bias;
+  const float* xres;
+  int64_t ldx;
+  float eps, p;
+  uint64_t seed;
+  float2* a_stats;
+  float* o_in;
+  float* y;
+  int64_t ldy;
+  __device__ void prologue(int64_t m0, int64_t total, float2* st) const {
+    panel_row_stats(attn, lda, m0, total, K, eps, st, blockIdx.y == 0 ? a_stats : nullptr);
+  }
+  __device__ float a(int64_t m, int k, float2 st) const {
+    float v = u[m * ldu + k] * ((attn[m * lda + k] - st.x) * st.y);
+    v *= dropout_keep(seed, m, k, K, p);
+    if (o_in && blockIdx.y == 0) o_in[m * K + k] = v;
+    return v;
+  }
+  __device__ float b(int k, int n) const { return w[(int64_t)n * K + k]; }
+  template <int NT>
+  __device__ void epilogue(f4 (&acc)[NT], int64_t mrow, int ncol, int64_t total,
+                           const float2*) const {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t m = mrow + r;
+      if (m >= total) continue;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int n = ncol + 16 * t;
+        if (n >= N) continue;
+        float v = acc[t][r];
+        if (bias) v = v + bias[n];
+        if (xres) v = v + xres[m * ldx + n];
+        y[m * ldy + n] = v;
+      }
+    }
+  }
+};
+
+// B1: g = dy @ W_o (rows, hdv); epilogue: dropout bwd, du = g*LN(a) (*silu'(h_u)),
+//     d_attn = LayerNorm_bwd(g * u).  Needs the whole hdv row in one panel.
+struct OpGateOBwd : NoStats {
+  static constexpr bool B_N_CONTIG = true;
+  const int64_t* offsets;
+  int B, K, N;  // K = D, N = hdv
+  const float* dy;
+  int64_t lddy;
+  const float* w;
+  const float* u;
+  int64_t ldu;
+  const float* attn;
+  int64_t lda;
+  const float2* a_stats;
+  const float* h_u;
+  int64_t ldh;
+  float p;
+  uint64_t seed;
+  float* du;
+  int64_t lddu;
+  float* da;
+  int64_t ldda;
+  __device__ float a(int64_t m, int k, float2) const { return dy[m * lddy + k]; }
+  __device__ float b(int k, int n) const { return w[(int64_t)k * N + n]; }
+  template <int NT>
+  __device__ void epilogue(f4 (&acc)[NT], int64_t mrow, int ncol, int64_t total,
+                           const float2*) const {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t m = mrow + r;
+      const bool row_ok = m < total;
+      float2 st = row_ok ? a_stats[m] : make_float2(0.f, 0.f);
+      float s1 = 0.f, s2 = 0.f;
+      float lnv[NT], dln[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int n = ncol + 16 * t;
+        lnv[t] = 0.f;
+        dln[t] = 0.f;
+        if (row_ok && n < N) {
+          const float g = acc[t][r] * dropout_keep(seed, m, n, N, p);
+          const float ln = (attn[m * lda + n] - st.x) * st.y;
+          const float uu = u[m * ldu + n];
+          float dd = g * ln;
+          if (h_u) dd *= silu_grad_(h_u[m * ldh + n]);
+          du[m * lddu + n] = dd;
+          lnv[t] = ln;
+          dln[t] = g * uu;
+          s1 += dln[t];
+          s2 += dln[t] * ln;
+        }
+      }
+      s1 = sum16(s1);
+      s2 = sum16(s2);
+      const float inv = 1.f / (float)N;
+      const float mean1 = s1 * inv, mean2 = s2 * inv;
+      if (!row_ok) continue;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int n = ncol + 16 * t;
+        if (n < N) da[m * ldda + n] = st.y * (dln[t] - mean1 - lnv[t] * mean2);
+      }
+    }
+  }
+};
+
+// B3: dn = dh @ W_uvqk^T (rows, D); epilogue: dx = dy + LayerNorm_bwd(x; dn).
+struct OpLnUvqkBwd : NoStats {
+  static constexpr bool B_N_CONTIG = false;
+  const int64_t* offsets;
+  int B, K, N;  // K = n_out (4hd), N = D
+  const float* dh;
+  int64_t lddh;
+  const float* w;  // (D, n_out) row-major -> b(k, n) = w[n][k]
+  const float* x;
+  int64_t ldx;
+  const float2* x_stats;
+  const float* dy;
+  int64_t lddy;
+  float* dx;
+  int64_t lddx;
+  __device__ float a(int64_t m, int k, float2) const { return dh[m * lddh + k]; }
+  __device__ float b(int k, int n) const { return w[(int64_t)n * K + k]; }
+  template <int NT>
+  __device__ void epilogue(f4 (&acc)[NT], int64_t mrow, int ncol, int64_t total,
+                           const float2*) const {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t m = mrow + r;
+      const bool row_ok = m < total;
+      float2 st = row_ok ? x_stats[m] : make_float2(0.f, 0.f);
+      float s1 = 0.f, s2 = 0.f;
+      float xh[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int n = ncol + 16 * t;
+        xh[t] = 0.f;
+        if (row_ok && n < N) {
+          xh[t] = (x[m * ldx + n] - st.x) * st.y;
+          s1 += acc[t][r];
+          s2 += acc[t][r] * xh[t];
+        }
+      }
+      s1 = sum16(s1);
+      s2 = sum16(s2);
+      const float inv = 1.f / (float)N;
+      const float mean1 = s1 * inv, mean2 = s2 * inv;
+      if (!row_ok) continue;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int n = ncol + 16 * t;
+        if (n < N) {
+          float v = st.y * (acc[t][r] - mean1 - xh[t] * mean2);
+          if (dy) v = dy[m * lddy + n] + v;
+          dx[m * lddx + n] = v;
+        }
+      }
+    }
+  }
+};
+
+template <class Op>
+static int launch_rowpanel(const Op& op, int64_t max_rows, bool full_row, const char* name,
+                           hipStream_t st) {
+  const int nt_needed = ceil_div(op.N, 16);
+  GR_REQUIRE(!full_row || nt_needed <= 16,
+             "%s: %d output columns exceed one 256-column panel (row-reduction epilogue)", name,
+             op.N);
+  const int nt = nt_needed > 16 ? 16 : nt_needed;
+  const int panels = ceil_div(op.N, nt * 16);
+  dim3 grid((unsigned)((max_rows + BM - 1) / BM), (unsigned)panels);
+  if (grid.x == 0) return 0;
+#define GR_NT_CASE(NT_)                                                            \
+  case NT_:                                                                        \
+    hipLaunchKernelGGL((rowpanel_kernel<NT_, Op>), grid, dim3(256), 0, st, op);    \
+    break;
+  switch (nt) {
+    GR_NT_CASE(1) GR_NT_CASE(2) GR_NT_CASE(3) GR_NT_CASE(4) GR_NT_CASE(5) GR_NT_CASE(6)
+    GR_NT_CASE(7) GR_NT_CASE(8) GR_NT_CASE(9) GR_NT_CASE(10) GR_NT_CASE(11) GR_NT_CASE(12)
+    GR_NT_CASE(13) GR_NT_CASE(14) GR_NT_CASE(15) GR_NT_CASE(16)
+    default: GR_REQUIRE(false, "%s: bad panel width", name);
+  }
+#undef GR_NT_CASE
+  GR_LAUNCH_CHECK(name);
+  return 0;
+}
+
+// ------------------------------------------------------------------ weight gradients
+// C[Ka, Nb] = sum_m A'(m, ka) * Bm(m, nb), A' = A or (A - mu_m) * rstd_m.
+// Grid: x = row chunk, y = output panel (64 ka x 256 nb).  Each workgroup writes its
+// partial panel to a slab; wgrad_reduce sums the chunks in order.
+constexpr int WG_KA = 64, WG_NB = 256, WG_LDA = WG_KA + 16, WG_LDB = WG_NB + 16;
+
+struct WgradArgs {
+  const float* a;
+  int64_t lda;
+  const float2* a_stats;
+  const float* bm;
+  int64_t ldb;
+  const int64_t* offsets;
+  int B, Ka, Nb;
+  int64_t rows_per_chunk;
+  int n_chunks, panels_nb;
+  float* slabs;    // [n_chunks][Ka][Nb]
+  float* colsums;  // [n_chunks][Ka] or null
+};
+
+__global__ __launch_bounds__(256) void wgrad_partial_kernel(WgradArgs g) {
+  __shared__ __attribute__((aligned(16))) float As[BK * WG_LDA];
+  __shared__ __attribute__((aligned(16))) float Bs[BK * WG_LDB];
+  const int chunk = blockIdx.x;
+  const int pa = blockIdx.y / g.panels_nb, pb = blockIdx.y % g.panels_nb;
+  const int ka0 = pa * WG_KA, nb0 = pb * WG_NB;
+  const int64_t total = g.offsets[g.B];
+  const int64_t r0 = (int64_t)chunk * g.rows_per_chunk;
+  const int64_t r1 = min(total, r0 + g.rows_per_chunk);
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int lr = lane & 15, lg = lane >> 4;
+  f4 acc[16];
+#pragma unroll
+  for (int t = 0; t < 16; ++t) acc[t] = f4_zero();
+  float csum = 0.f;  // thread tid < 64 sums column ka0 + tid
+  for (int64_t m0 = r0; m0 < r1; m0 += BK) {
+    for (int e = tid; e < BK * WG_KA; e += 256) {
+      const int rr = e / WG_KA, c = e - rr * WG_KA;
+      const int64_t m = m0 + rr;
+      const int ka = ka0 + c;
+      float v = 0.f;
+      if (m < r1 && ka < g.Ka) {
+        v = g.a[m * g.lda + ka];
+        if (g.a_stats) {
+          const float2 st = g.a_stats[m];
+          v = (v - st.x) * st.y;
+        }
+      }
+      As[rr * WG_LDA + c] = v;
+    }
+    for (int e = tid; e < BK * WG_NB; e += 256) {
+      const int rr = e / WG_NB, c = e - rr * WG_NB;
+      const int64_t m = m0 + rr;
+      const int nb = nb0 + c;
+      Bs[rr * WG_LDB + c] = (m < r1 && nb < g.Nb) ? g.bm[m * g.ldb + nb] : 0.f;
+    }
+    __syncthreads();
+    if (g.colsums && pb == 0 && tid < WG_KA) {
+#pragma unroll
+      for (int rr = 0; rr < BK; ++rr) csum += As[rr * WG_LDA + tid];
+    }
+    // wave w: output rows ka0 + 16w .. +15, all 16 column tiles
+#pragma unroll
+    for (int ks = 0; ks < BK / 4; ++ks) {
+      const float av = As[(4 * ks + lg) * WG_LDA + w * 16 + lr];
+      const float* brow = Bs + (4 * ks + lg) * WG_LDB + lr;
+#pragma unroll
+      for (int t = 0; t < 16; ++t) acc[t] = mfma16x16x4(av, brow[t * 16], acc[t]);
+    }
+    __syncthreads();
+  }
+  float* slab = g.slabs + (int64_t)chunk * g.Ka * g.Nb;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int ka = ka0 + w * 16 + 4 * lg + r;
+    if (ka >= g.Ka) continue;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int nb = nb0 + 16 * t + lr;
+      if (nb < g.Nb) slab[(int64_t)ka * g.Nb + nb] = acc[t][r];
+    }
+  }
+  if (g.colsums && pb == 0 && tid < WG_KA && ka0 + tid < g.Ka)
+    g.colsums[(int64_t)chunk * g.Ka + ka0 + tid] = csum;
+}
+
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* slabs, int n_chunks,
+                                                           int64_t n_elem, float* out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n_elem) return;
+  float s = 0.f;
+  for (int c = 0; c < n_chunks; ++c) s += slabs[(int64_t)c * n_elem + i];
+  out[i] = s;
+}
+
+static void wgrad_plan(int64_t max_rows, int Ka, int Nb, int* n_chunks, int64_t* rows_per_chunk,
+                       int* panels) {
+  const int pa = ceil_div(Ka, WG_KA), pb = ceil_div(Nb, WG_NB);
+  *panels = pa * pb;
+  int target = ceil_div(512, *panels);  // ~2 workgroups per CU
+  int64_t rpc = (max_rows + target - 1) / target;
+  rpc = ((rpc + 255) / 256) * 256;  // >= 256 rows per chunk
+  if (rpc < 256) rpc = 256;
+  *rows_per_chunk = rpc;
+  *n_chunks = (int)((max_rows + rpc - 1) / rpc);
+  if (*n_chunks < 1) *n_chunks = 1;
+}
+
+}  // namespace gr
+
+// ====================================================================== C-ABI
+using namespace gr;
+
+extern "C" int hstu_ln_uvqk_fwd(const float* x, int64_t ld_x, const int64_t* offsets, int B,
+                                int64_t max_rows, int D, const float* w_uvqk, int n_out,
+                                float eps, int activation, float* x_stats, float* h_pre,
+                                float* uvqk, int64_t ld_out, void* stream) {
+  GR_REQUIRE(x && offsets && w_uvqk && uvqk && x_stats, "hstu_ln_uvqk_fwd: null pointer");
+  GR_REQUIRE(D > 0 && n_out > 0 && B >= 0 && max_rows >= 0, "hstu_ln_uvqk_fwd: bad sizes");
+  GR_REQUIRE(activation == 0 || activation == 1, "hstu_ln_uvqk_fwd: activation must be 0|1");
+  OpLnUvqk op{offsets, B, D, n_out, x, ld_x, w_uvqk, eps, activation, (float2*)x_stats,
+              h_pre, uvqk, ld_out};
+  return launch_rowpanel(op, max_rows, false, "hstu_ln_uvqk_fwd", (hipStream_t)stream);
+}
+
+extern "C" int hstu_gate_o_fwd(const float* u, int64_t ld_u, const float* attn, int64_t ld_attn,
+                               const int64_t* offsets, int B, int64_t max_rows, int hdv, int D,
+                               const float* w_o, const float* b_o, const float* x_res,
+                               int64_t ld_x, float eps, float dropout_p, uint64_t seed,
+                               float* attn_stats, float* o_in, float* y, int64_t ld_y,
+                               void* stream) {
+  GR_REQUIRE(u && attn && offsets && w_o && y && attn_stats, "hstu_gate_o_fwd: null pointer");
+  GR_REQUIRE(hdv > 0 && D > 0 && B >= 0, "hstu_gate_o_fwd: bad sizes");
+  GR_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f, "hstu_gate_o_fwd: dropout_p %f", dropout_p);
+  OpGateO op{offsets, B, hdv, D, u, ld_u, attn, ld_attn, w_o, b_o, x_res, ld_x, eps, dropout_p,
+             seed, (float2*)attn_stats, o_in, y, ld_y};
+  return launch_rowpanel(op, max_rows, false, "hstu_gate_o_fwd", (hipStream_t)stream);
+}
+
+extern "C" int hstu_gate_o_bwd(const float* dy, int64_t ld_dy, const int64_t* offsets, int B,
+                               int64_t max_rows, int hdv, int D, const float* w_o,
+                               const float* u, int64_t ld_u, const float* attn, int64_t ld_attn,
+                               const float* attn_stats, const float* h_u, int64_t ld_h,
+                               float dropout_p, uint64_t seed, float* du, int64_t ld_du,
+                               float* d_attn, int64_t ld_da, void* stream) {
+  GR_REQUIRE(dy && offsets && w_o && u && attn && attn_stats && du && d_attn,
+             "hstu_gate_o_bwd: null pointer");
+  GR_REQUIRE(hdv > 0 && D > 0 && B >= 0, "hstu_gate_o_bwd: bad sizes");
+  OpGateOBwd op;
+  op.offsets = offsets; op.B = B; op.K = D; op.N = hdv; op.dy = dy; op.lddy = ld_dy;
+  op.w = w_o; op.u = u; op.ldu = ld_u; op.attn = attn; op.lda = ld_attn;
+  op.a_stats = (const float2*)attn_stats; op.h_u = h_u; op.ldh = ld_h; op.p = dropout_p;
+  op.seed = seed; op.du = du; op.lddu = ld_du; op.da = d_attn; op.ldda = ld_da;
+  return launch_rowpanel(op, max_rows, true, "hstu_gate_o_bwd", (hipStream_t)stream);
+}
+
+extern "C" int hstu_ln_uvqk_bwd(const float* dh, int64_t ld_dh, const int64_t* offsets, int B,
+                                int64_t max_rows, int D, int n_out, const float* w_uvqk,
+                                const float* x, int64_t ld_x, const float* x_stats,
+                                const float* dy_res, int64_t ld_dy, float* dx, int64_t ld_dx,
+                                void* stream) {
+  GR_REQUIRE(dh && offsets && w_uvqk && x && x_stats && dx, "hstu_ln_uvqk_bwd: null pointer");
+  GR_REQUIRE(D > 0 && n_out > 0 && B >= 0, "hstu_ln_uvqk_bwd: bad sizes");
+  OpLnUvqkBwd op;
+  op.offsets = offsets; op.B = B; op.K = n_out; op.N = D; op.dh = dh; op.lddh = ld_dh;
+  op.w = w_uvqk; op.x = x; op.ldx = ld_x; op.x_stats = (const float2*)x_stats;
+  op.dy = dy_res; op.lddy = ld_dy; op.dx = dx; op.lddx = ld_dx;
+  return launch_rowpanel(op, max_rows, true, "hstu_ln_uvqk_bwd", (hipStream_t)stream);
+}
+
+extern "C" size_t gr_wgrad_workspace_size(int64_t max_rows, int Ka, int Nb) {
+  if (max_rows <= 0 || Ka <= 0 || Nb <= 0) return 0;
+  int n_chunks, panels;
+  int64_t rpc;
+  wgrad_plan(max_rows, Ka, Nb, &n_chunks, &rpc, &panels);
+  return sizeof(float) * (size_t)n_chunks * ((size_t)Ka * Nb + Ka);
+}
+
+extern "C" int gr_wgrad(const float* a, int64_t lda, const float* a_stats, const float* bm,
+                        int64_t ldb, const int64_t* offsets, int B, int64_t max_rows, int Ka,
+                        int Nb, float* c, float* a_colsum, void* workspace, size_t ws_bytes,
+                        void* stream) {
+  GR_REQUIRE(a && bm && offsets && c, "gr_wgrad: null pointer");
+  GR_REQUIRE(Ka > 0 && Nb > 0 && B >= 0 && max_rows >= 0, "gr_wgrad: bad sizes");
+  hipStream_t st = (hipStream_t)stream;
+  if (max_rows == 0) {
+    (void)hipMemsetAsync(c, 0, sizeof(float) * (size_t)Ka * Nb, st);
+    if (a_colsum) (void)hipMemsetAsync(a_colsum, 0, sizeof(float) * Ka, st);
+    return 0;
+  }
+  int n_chunks, panels;
+  int64_t rpc;
+  wgrad_plan(max_rows, Ka, Nb, &n_chunks, &rpc, &panels);
+  const size_t need = sizeof(float) * (size_t)n_chunks * ((size_t)Ka * Nb + Ka);
+  GR_REQUIRE(workspace && ws_bytes >= need, "gr_wgrad: workspace %zu B < %zu B", ws_bytes, need);
+  float* slabs = (float*)workspace;
+  float* cs = a_colsum ? slabs + (size_t)n_chunks * Ka * Nb : nullptr;
+  WgradArgs g{a, lda, (const float2*)a_stats, bm, ldb, offsets, B, Ka, Nb, rpc, n_chunks,
+              ceil_div(Nb, WG_NB), slabs, cs};
+  hipLaunchKernelGGL(wgrad_partial_kernel, dim3(n_chunks, panels), dim3(256), 0, st, g);
+  GR_LAUNCH_CHECK("gr_wgrad(partial)");
+  const int64_t ne = (int64_t)Ka * Nb;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st,
+                     slabs, n_chunks, ne, c);
+  GR_LAUNCH_CHECK("gr_wgrad(reduce)");
+  if (a_colsum) {
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((Ka + 255) / 256)), dim3(256), 0,
+                       st, cs, n_chunks, (int64_t)Ka, a_colsum);
+    GR_LAUNCH_CHECK("gr_wgrad(colsum)");
+  }
+  return 0;
+}

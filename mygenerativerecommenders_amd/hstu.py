@@ -1,0 +1,309 @@
+"""HSTU sequential encoder — drop-in for the reference's
+``generative_recommenders_pl.models.sequential_encoders.hstu`` (Hydra ``_target_``
+``...sequential_encoders.hstu.HSTU``), running the MI355X kernels of
+``libgr_hstu.so``.
+
+Same constructor arguments, parameter names / shapes / initialisation and
+state-dict keys as the reference (``hstu.py:71-128, 208-672``), so checkpoints
+round-trip.  The compute is the fused jagged path: per layer 3 launches forward
+(LN+UVQK+SiLU GEMM, attention with in-kernel relative bias, gate+LN+O GEMM+residual)
+and 6 backward; nothing of size (B, N, N) is materialised.
+
+Not supported (raise): the incremental-decoding cache path (``delta_x_offsets`` /
+``cache``, hstu.py:293-298, 415-418 — used by no config), ``normalization=
+"softmax_rel_bias"`` (hstu.py:341-389 — used by no config), ``concat_ua=True``
+(hstu.py:398-400) and attention dropout > 0 (the reference ignores it too).
+"""
+from __future__ import annotations
+
+import abc
+from typing import Callable, Dict, List, Optional, Tuple
+
+import torch
+import torch.nn.functional as F  # noqa: F401  (kept for API parity of the module)
+
+from . import ops
+from .bucket_table import NUM_BUCKETS
+
+TIMESTAMPS_KEY = "timestamps"
+
+HSTUCacheState = Tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]
+
+
+def _default_bucketization_fn(x: torch.Tensor) -> torch.Tensor:
+    """hstu.py:579-581.  The fused kernel evaluates this function exactly through the
+    integer threshold table in ``bucket_table.py``; it is kept for API parity."""
+    return (torch.log(torch.abs(x).clamp(min=1)) / 0.301).long()
+
+
+class RelativeAttentionBiasModule(torch.nn.Module):
+    @abc.abstractmethod
+    def forward(self, all_timestamps: torch.Tensor) -> torch.Tensor:
+        pass
+
+
+class RelativeBucketedTimeAndPositionBasedBias(RelativeAttentionBiasModule):
+    """Parameter holder for the relative position + time bias (hstu.py:71-128).
+
+    ``_ts_w`` (num_buckets + 1) and ``_pos_w`` (2 * max_seq_len - 1), N(0, 0.02).
+    The bias itself is never materialised: ``hstu_attn_fwd`` rebuilds it per tile.
+    """
+
+    def __init__(self, max_seq_len: int, num_buckets: int,
+                 bucketization_fn: Callable[[torch.Tensor], torch.Tensor]) -> None:
+        super().__init__()
+        if num_buckets != NUM_BUCKETS or bucketization_fn is not _default_bucketization_fn:
+            # the threshold table encodes the reference's default function only
+            if num_buckets != NUM_BUCKETS:
+                raise ValueError(f"num_buckets must be {NUM_BUCKETS} (got {num_buckets})")
+        self._max_seq_len: int = max_seq_len
+        self._ts_w = torch.nn.Parameter(torch.empty(num_buckets + 1).normal_(mean=0, std=0.02))
+        self._pos_w = torch.nn.Parameter(
+            torch.empty(2 * max_seq_len - 1).normal_(mean=0, std=0.02))
+        self._num_buckets: int = num_buckets
+        self._bucketization_fn = bucketization_fn
+
+    def forward(self, all_timestamps: torch.Tensor) -> torch.Tensor:
+        raise NotImplementedError(
+            "the (B, N, N) bias is fused into hstu_attn_fwd and never materialised")
+
+
+class SequentialTransductionUnitJagged(torch.nn.Module):
+    """hstu.py:208-423, same constructor and parameters."""
+
+    def __init__(
+        self,
+        embedding_dim: int,
+        linear_hidden_dim: int,
+        attention_dim: int,
+        dropout_ratio: float,
+        attn_dropout_ratio: float,
+        num_heads: int,
+        linear_activation: str,
+        relative_attention_bias_module: Optional[RelativeAttentionBiasModule] = None,
+        normalization: str = "rel_bias",
+        linear_config: str = "uvqk",
+        concat_ua: bool = False,
+        epsilon: float = 1e-6,
+        max_length: Optional[int] = None,
+    ) -> None:
+        super().__init__()
+        self._embedding_dim = embedding_dim
+        self._linear_dim = linear_hidden_dim
+        self._attention_dim = attention_dim
+        self._dropout_ratio = dropout_ratio
+        self._attn_dropout_ratio = attn_dropout_ratio
+        self._num_heads = num_heads
+        self._rel_attn_bias = relative_attention_bias_module
+        self._normalization = normalization
+        self._linear_config = linear_config
+        if self._linear_config == "uvqk":
+            self._uvqk = torch.nn.Parameter(
+                torch.empty((embedding_dim,
+                             linear_hidden_dim * 2 * num_heads + attention_dim * num_heads * 2)
+                            ).normal_(mean=0, std=0.02))
+        else:
+            raise ValueError(f"Unknown linear_config {self._linear_config}")
+        self._linear_activation = linear_activation
+        self._concat_ua = concat_ua
+        self._o = torch.nn.Linear(
+            in_features=linear_hidden_dim * num_heads * (3 if concat_ua else 1),
+            out_features=embedding_dim)
+        torch.nn.init.xavier_uniform_(self._o.weight)
+        self._eps = epsilon
+        self._seed_gen = torch.Generator(device="cpu")
+        self._seed_gen.manual_seed(0x5EED)
+
+    def _geometry(self, n: int, max_len: int) -> ops.STUGeometry:
+        if self._linear_activation == "silu":
+            act = 1
+        elif self._linear_activation == "none":
+            act = 0
+        else:
+            raise ValueError(f"Unknown linear_activation {self._linear_activation}")
+        if self._normalization not in ("rel_bias", "hstu_rel_bias"):
+            if self._normalization == "softmax_rel_bias":
+                raise NotImplementedError("normalization='softmax_rel_bias' is not supported")
+            raise ValueError(f"Unknown normalization method {self._normalization}")
+        if self._concat_ua:
+            raise NotImplementedError("concat_ua=True is not supported by the fused kernels")
+        return ops.STUGeometry(
+            N=n, D=self._embedding_dim, H=self._num_heads, dqk=self._attention_dim,
+            dv=self._linear_dim, eps=self._eps, activation=act,
+            dropout_p=float(self._dropout_ratio) if self.training else 0.0,
+            max_len=max_len)
+
+    def forward(
+        self,
+        x: torch.Tensor,
+        x_offsets: torch.Tensor,
+        all_timestamps: Optional[torch.Tensor],
+        invalid_attn_mask: torch.Tensor,
+        delta_x_offsets: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+        cache: Optional[HSTUCacheState] = None,
+        return_cache_states: bool = False,
+        max_len: Optional[int] = None,
+    ):
+        """x: (rows, D) jagged; x_offsets (B+1,).  Returns (x', cache-state tuple);
+        cache states are (v, None, None, x') — padded q/k are never built."""
+        if delta_x_offsets is not None or cache is not None:
+            raise NotImplementedError("incremental (cached) HSTU decoding is not supported")
+        n = invalid_attn_mask.size(-1)
+        geo = self._geometry(n, n if max_len is None else max_len)
+        rab = self._rel_attn_bias
+        ts = all_timestamps if rab is not None else None
+        pos_w = rab._pos_w if ts is not None else None
+        ts_w = rab._ts_w if ts is not None else None
+        if ts is not None and pos_w.numel() != 2 * n - 1:
+            raise ValueError(f"_pos_w has {pos_w.numel()} entries, expected {2 * n - 1}")
+        seed = int(torch.randint(0, 2**62, (1,), generator=self._seed_gen)) if geo.dropout_p > 0 else 0
+        y = ops.stu_layer(x, x_offsets, ts, self._uvqk, self._o.weight, self._o.bias, pos_w,
+                          ts_w, geo, seed)
+        return y, (None, None, None, y)
+
+
+class HSTUJagged(torch.nn.Module):
+    """hstu.py:426-518."""
+
+    def __init__(self, modules: List[SequentialTransductionUnitJagged],
+                 autocast_dtype: Optional[torch.dtype]) -> None:
+        super().__init__()
+        self._attention_layers = torch.nn.ModuleList(modules=modules)
+        self._autocast_dtype = autocast_dtype
+
+    def jagged_forward(self, x, x_offsets, all_timestamps, invalid_attn_mask,
+                       delta_x_offsets=None, cache=None, return_cache_states=False,
+                       max_len: Optional[int] = None):
+        cache_states: List[HSTUCacheState] = []
+        for layer in self._attention_layers:
+            x, cs = layer(x=x, x_offsets=x_offsets, all_timestamps=all_timestamps,
+                          invalid_attn_mask=invalid_attn_mask,
+                          delta_x_offsets=delta_x_offsets, cache=None,
+                          return_cache_states=return_cache_states, max_len=max_len)
+            if return_cache_states:
+                cache_states.append(cs)
+        return x, cache_states
+
+    def forward(self, x, x_offsets, all_timestamps, invalid_attn_mask, delta_x_offsets=None,
+                cache=None, return_cache_states=False, max_len: Optional[int] = None):
+        n = invalid_attn_mask.size(1)
+        if x.dim() == 3:
+            x = ops.dense_to_jagged(x, x_offsets)  # B*N capacity rows: no host sync
+        jagged_x, cache_states = self.jagged_forward(
+            x, x_offsets, all_timestamps, invalid_attn_mask, delta_x_offsets, cache,
+            return_cache_states, max_len=max_len)
+        y = ops.jagged_to_padded_dense(jagged_x, x_offsets, n, 0.0)
+        return y, cache_states
+
+
+class HSTU(torch.nn.Module):
+    """Drop-in for reference ``HSTU`` (hstu.py:521-672)."""
+
+    def __init__(
+        self,
+        max_sequence_len: int,
+        max_output_len: int,
+        embedding_dim: int,
+        item_embedding_dim: int,
+        num_blocks: int,
+        num_heads: int,
+        linear_dim: int,
+        attention_dim: int,
+        normalization: str,
+        linear_config: str,
+        linear_activation: str,
+        linear_dropout_rate: float,
+        attn_dropout_rate: float,
+        enable_relative_attention_bias: bool = True,
+        concat_ua: bool = False,
+    ) -> None:
+        super().__init__()
+        self._embedding_dim = embedding_dim
+        self._item_embedding_dim = item_embedding_dim
+        self._max_sequence_length = max_sequence_len
+        self._num_blocks = num_blocks
+        self._num_heads = num_heads
+        self._dqk = attention_dim
+        self._dv = linear_dim
+        self._linear_activation = linear_activation
+        self._linear_dropout_rate = linear_dropout_rate
+        self._attn_dropout_rate = attn_dropout_rate
+        self._enable_relative_attention_bias = enable_relative_attention_bias
+        self._hstu = HSTUJagged(
+            modules=[
+                SequentialTransductionUnitJagged(
+                    embedding_dim=self._embedding_dim,
+                    linear_hidden_dim=linear_dim,
+                    attention_dim=attention_dim,
+                    normalization=normalization,
+                    linear_config=linear_config,
+                    linear_activation=linear_activation,
+                    num_heads=num_heads,
+                    relative_attention_bias_module=(
+                        RelativeBucketedTimeAndPositionBasedBias(
+                            max_seq_len=max_sequence_len + max_output_len,
+                            num_buckets=NUM_BUCKETS,
+                            bucketization_fn=_default_bucketization_fn,
+                        ) if enable_relative_attention_bias else None),
+                    dropout_ratio=linear_dropout_rate,
+                    attn_dropout_ratio=attn_dropout_rate,
+                    concat_ua=concat_ua,
+                )
+                for _ in range(num_blocks)
+            ],
+            autocast_dtype=None,
+        )
+        self.register_buffer(
+            "_attn_mask",
+            torch.triu(torch.ones((self._max_sequence_length + max_output_len,
+                                   self._max_sequence_length + max_output_len),
+                                  dtype=torch.bool), diagonal=1))
+        self.reset_params()
+
+    def reset_params(self):
+        # hstu.py:609-621: every parameter of this module lives under _hstu -> skipped.
+        for name, params in self.named_parameters():
+            if ("_hstu" in name) or ("_embedding_module" in name):
+                continue
+            try:
+                torch.nn.init.xavier_normal_(params.data)
+            except Exception:
+                pass
+
+    def debug_str(self) -> str:
+        s = (f"HSTU-b{self._num_blocks}-h{self._num_heads}-dqk{self._dqk}-dv{self._dv}"
+             f"-l{self._linear_activation}d{self._linear_dropout_rate}"
+             f"-ad{self._attn_dropout_rate}")
+        if not self._enable_relative_attention_bias:
+            s += "-norab"
+        return s
+
+    def forward(
+        self,
+        past_lengths: torch.Tensor,
+        user_embeddings: torch.Tensor,
+        valid_mask: torch.Tensor,
+        past_payloads: Dict[str, torch.Tensor],
+        delta_x_offsets: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+        cache: Optional[List[HSTUCacheState]] = None,
+        return_cache_states: bool = False,
+        max_len: Optional[int] = None,
+    ) -> Tuple[torch.Tensor, List[HSTUCacheState]]:
+        """past_lengths (B,), user_embeddings (B, N, D) fp32, past_payloads may hold
+        "timestamps" (B, N) int64.  Returns ((B, N, D), cache_states); rows >= length
+        are zero.  ``max_len`` (optional, host int) bounds the lengths to trim grids."""
+        float_dtype = user_embeddings.dtype
+        if float_dtype != torch.float32:
+            user_embeddings = user_embeddings.float()
+        y, cached_states = self._hstu(
+            x=user_embeddings,
+            x_offsets=ops.asynchronous_complete_cumsum(past_lengths),
+            all_timestamps=(past_payloads[TIMESTAMPS_KEY]
+                            if TIMESTAMPS_KEY in past_payloads else None),
+            invalid_attn_mask=self._attn_mask,
+            delta_x_offsets=delta_x_offsets,
+            cache=cache,
+            return_cache_states=return_cache_states,
+            max_len=max_len,
+        )
+        return y.to(float_dtype), cached_states

@@ -1,0 +1,282 @@
+"""Host-side operators over the gfx950 C-ABI (``libgr_hstu.so``).
+
+Python mirror of the reference's ``models/utils/ops.py`` jagged helpers plus the
+autograd wrapper of one fused STU layer.  Every op runs on the MI355X through the
+C-ABI; there is no CPU path (the CPU restatement in ``oracle/`` is test-only).
+
+Reference map (``src/generative_recommenders_pl/models/``):
+  * asynchronous_complete_cumsum .. utils/ops.py:18-38
+  * dense_to_jagged .............. utils/ops.py:41-64
+  * jagged_to_padded_dense ....... utils/ops.py:67-114
+  * get_current_embeddings ....... utils/ops.py:171-187
+  * STU layer fwd/bwd ............ sequential_encoders/hstu.py:266-413 (+ autograd)
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from . import _lib
+from .bucket_table import BUCKET_THRESHOLDS, NUM_BUCKETS
+
+_THR_CACHE: dict = {}
+
+
+def bucket_thresholds(device) -> torch.Tensor:
+    key = str(device)
+    t = _THR_CACHE.get(key)
+    if t is None:
+        t = torch.tensor(BUCKET_THRESHOLDS, dtype=torch.int64, device=device)
+        _THR_CACHE[key] = t
+    return t
+
+
+def _stream():
+    return _lib.stream_handle()
+
+
+# ------------------------------------------------------------------ jagged helpers
+
+def asynchronous_complete_cumsum(lengths: torch.Tensor) -> torch.Tensor:
+    """(B,) -> (B + 1,) int64 offsets [0, cumsum(lengths)] (utils/ops.py:18-38)."""
+    _lib.require_gpu(lengths)
+    lengths = lengths.to(torch.int64).contiguous()
+    B = lengths.numel()
+    out = torch.empty(B + 1, dtype=torch.int64, device=lengths.device)
+    _lib.call("gr_complete_cumsum", lengths.data_ptr(), B, out.data_ptr(), _stream())
+    return out
+
+
+class _DenseToJagged(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, dense, offsets, total_rows):
+        B, N, D = dense.shape
+        dense = dense.contiguous()
+        out = torch.empty(total_rows, D, dtype=dense.dtype, device=dense.device)
+        _lib.call("gr_dense_to_jagged", dense.data_ptr(), offsets.data_ptr(), B, N, D,
+                  total_rows, out.data_ptr(), _stream())
+        ctx.save_for_backward(offsets)
+        ctx.shape = (B, N, D)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (offsets,) = ctx.saved_tensors
+        B, N, D = ctx.shape
+        g = g.contiguous()
+        out = torch.empty(B, N, D, dtype=g.dtype, device=g.device)
+        _lib.call("gr_jagged_to_padded", g.data_ptr(), offsets.data_ptr(), B, N, D,
+                  out.data_ptr(), _stream())
+        return out, None, None
+
+
+class _JaggedToPadded(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, values, offsets, N):
+        B = offsets.numel() - 1
+        D = values.shape[1]
+        values = values.contiguous()
+        out = torch.empty(B, N, D, dtype=values.dtype, device=values.device)
+        _lib.call("gr_jagged_to_padded", values.data_ptr(), offsets.data_ptr(), B, N, D,
+                  out.data_ptr(), _stream())
+        ctx.save_for_backward(offsets)
+        ctx.meta = (B, N, D, values.shape[0])
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (offsets,) = ctx.saved_tensors
+        B, N, D, rows = ctx.meta
+        g = g.contiguous()
+        out = torch.empty(rows, D, dtype=g.dtype, device=g.device)
+        _lib.call("gr_dense_to_jagged", g.data_ptr(), offsets.data_ptr(), B, N, D, rows,
+                  out.data_ptr(), _stream())
+        return out, None, None
+
+
+def dense_to_jagged(dense_tensor: torch.Tensor, offsets: torch.Tensor,
+                    total_rows: Optional[int] = None) -> torch.Tensor:
+    """(B, N, D) -> (total, D) (utils/ops.py:41-64).  ``total_rows`` defaults to B*N
+    capacity (sync-free; rows past offsets[B] are scratch) — pass the exact total to
+    get an exact-size result."""
+    _lib.require_gpu(dense_tensor, offsets)
+    if dense_tensor.dtype != torch.float32:
+        raise TypeError("dense_to_jagged: float32 only")
+    B, N, _ = dense_tensor.shape
+    if total_rows is None:
+        total_rows = B * N
+    return _DenseToJagged.apply(dense_tensor, offsets.to(torch.int64), int(total_rows))
+
+
+def jagged_to_padded_dense(values: torch.Tensor, offsets: torch.Tensor, max_lengths: int,
+                           padding_value: float = 0.0) -> torch.Tensor:
+    """(total, D) -> (B, max_lengths, D), zero padded (utils/ops.py:67-114)."""
+    if not isinstance(max_lengths, int):
+        raise ValueError(f"max_lengths must be an integer, but got {type(max_lengths)}")
+    if padding_value != 0.0:
+        raise NotImplementedError("jagged_to_padded_dense: padding_value must be 0.0")
+    _lib.require_gpu(values, offsets)
+    squeeze = values.dim() == 1
+    v = values.unsqueeze(-1) if squeeze else values
+    if v.dtype != torch.float32:
+        raise TypeError("jagged_to_padded_dense: float32 only")
+    out = _JaggedToPadded.apply(v, offsets.to(torch.int64), max_lengths)
+    return out.squeeze(-1) if squeeze else out
+
+
+def get_current_embeddings(lengths: torch.Tensor, encoded_embeddings: torch.Tensor) -> torch.Tensor:
+    """(B, N, D) -> (B, D) with row lengths[b]-1 (utils/ops.py:171-187).  Pure index
+    arithmetic on the device (one gather)."""
+    B, N, D = encoded_embeddings.shape
+    idx = (lengths.to(torch.int64) - 1) + torch.arange(B, device=lengths.device) * N
+    return encoded_embeddings.reshape(-1, D).index_select(0, idx)
+
+
+# ------------------------------------------------------------------ fused STU layer
+
+@dataclass
+class STUGeometry:
+    N: int              # padded max length (attention normaliser and bias extent)
+    D: int
+    H: int
+    dqk: int
+    dv: int
+    eps: float
+    activation: int     # 1 = silu, 0 = none
+    dropout_p: float
+    max_len: int        # host bound on sequence lengths (<= N)
+
+    @property
+    def n_out(self):
+        return 2 * self.H * self.dv + 2 * self.H * self.dqk
+
+
+class STULayerFunction(torch.autograd.Function):
+    """One SequentialTransductionUnitJagged (hstu.py:266-413) as 3 fused launches
+    forward and 6 backward.  Inputs: jagged x (rows, D), offsets (B+1), timestamps
+    (B, N) or None; parameters _uvqk (D, n_out), _o.weight (D, hdv), _o.bias (D,),
+    _pos_w (2N-1,), _ts_w (129,)."""
+
+    @staticmethod
+    def forward(ctx, x, offsets, ts, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGeometry, seed: int):
+        dev = x.device
+        rows, D = x.shape
+        B = offsets.numel() - 1
+        H, dv, dqk = geo.H, geo.dv, geo.dqk
+        hv, hq = H * dv, H * dqk
+        n_out = geo.n_out
+        st = _stream()
+        x = x.contiguous()
+        w_uvqk = w_uvqk.contiguous()
+        w_o = w_o.contiguous()
+        x_stats = torch.empty(rows, 2, dtype=torch.float32, device=dev)
+        uvqk = torch.empty(rows, n_out, dtype=torch.float32, device=dev)
+        h_pre = torch.empty_like(uvqk) if geo.activation else None
+        _lib.call("hstu_ln_uvqk_fwd", x.data_ptr(), x.stride(0), offsets.data_ptr(), B, rows, D,
+                  w_uvqk.data_ptr(), n_out, geo.eps, geo.activation, x_stats.data_ptr(),
+                  _lib.ptr(h_pre), uvqk.data_ptr(), n_out, st)
+        attn = torch.empty(rows, hv, dtype=torch.float32, device=dev)
+        thr = bucket_thresholds(dev)
+        q = uvqk[:, 2 * hv:2 * hv + hq]
+        k = uvqk[:, 2 * hv + hq:]
+        v = uvqk[:, hv:2 * hv]
+        pos_w_c = pos_w.contiguous() if ts is not None else None
+        ts_w_c = ts_w.contiguous() if ts is not None else None
+        _lib.call("hstu_attn_fwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out, n_out,
+                  offsets.data_ptr(), B, geo.N, geo.max_len, H, dqk, dv, _lib.ptr(ts),
+                  _lib.ptr(pos_w_c), _lib.ptr(ts_w_c), thr.data_ptr(), NUM_BUCKETS,
+                  attn.data_ptr(), hv, st)
+        attn_stats = torch.empty(rows, 2, dtype=torch.float32, device=dev)
+        needs_w_grad = w_o.requires_grad or b_o.requires_grad
+        o_in = torch.empty(rows, hv, dtype=torch.float32, device=dev) if needs_w_grad else None
+        y = torch.empty(rows, D, dtype=torch.float32, device=dev)
+        b_o_c = b_o.contiguous()
+        _lib.call("hstu_gate_o_fwd", uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
+                  offsets.data_ptr(), B, rows, hv, D, w_o.data_ptr(), b_o_c.data_ptr(),
+                  x.data_ptr(), x.stride(0), geo.eps, geo.dropout_p, seed,
+                  attn_stats.data_ptr(), _lib.ptr(o_in), y.data_ptr(), D, st)
+        ctx.save_for_backward(x, offsets, ts, w_uvqk, w_o, pos_w_c, ts_w_c, x_stats, uvqk,
+                              h_pre, attn, attn_stats, o_in)
+        ctx.geo = geo
+        ctx.seed = seed
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x, offsets, ts, w_uvqk, w_o, pos_w, ts_w, x_stats, uvqk, h_pre, attn, attn_stats,
+         o_in) = ctx.saved_tensors
+        geo = ctx.geo
+        dev = x.device
+        rows, D = x.shape
+        B = offsets.numel() - 1
+        H, dv, dqk = geo.H, geo.dv, geo.dqk
+        hv, hq = H * dv, H * dqk
+        n_out = geo.n_out
+        st = _stream()
+        dy = dy.contiguous()
+        d_uvqk = torch.empty(rows, n_out, dtype=torch.float32, device=dev)
+        d_attn = torch.empty(rows, hv, dtype=torch.float32, device=dev)
+        _lib.call("hstu_gate_o_bwd", dy.data_ptr(), D, offsets.data_ptr(), B, rows, hv, D,
+                  w_o.data_ptr(), uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
+                  attn_stats.data_ptr(), _lib.ptr(h_pre), n_out, geo.dropout_p, ctx.seed,
+                  d_uvqk.data_ptr(), n_out, d_attn.data_ptr(), hv, st)
+        L = _lib.lib()
+        d_w_o = d_b_o = None
+        if o_in is not None:
+            d_w_o = torch.empty(D, hv, dtype=torch.float32, device=dev)
+            d_b_o = torch.empty(D, dtype=torch.float32, device=dev)
+            ws_n = L.gr_wgrad_workspace_size(rows, D, hv)
+            ws = torch.empty(max(ws_n, 4), dtype=torch.uint8, device=dev)
+            _lib.call("gr_wgrad", dy.data_ptr(), D, None, o_in.data_ptr(), hv,
+                      offsets.data_ptr(), B, rows, D, hv, d_w_o.data_ptr(), d_b_o.data_ptr(),
+                      ws.data_ptr(), ws_n, st)
+        thr = bucket_thresholds(dev)
+        d_pos_w = d_ts_w = None
+        ws_a = None
+        ws_a_n = 0
+        if ts is not None:
+            d_pos_w = torch.empty(2 * geo.N - 1, dtype=torch.float32, device=dev)
+            d_ts_w = torch.empty(NUM_BUCKETS + 1, dtype=torch.float32, device=dev)
+            ws_a_n = L.hstu_attn_bwd_workspace_size(B, geo.N, geo.max_len, H, NUM_BUCKETS)
+            ws_a = torch.empty(max(ws_a_n, 4), dtype=torch.uint8, device=dev)
+        q = uvqk[:, 2 * hv:2 * hv + hq]
+        k = uvqk[:, 2 * hv + hq:]
+        v = uvqk[:, hv:2 * hv]
+        if h_pre is not None:
+            hq_p = h_pre[:, 2 * hv:2 * hv + hq].data_ptr()
+            hk_p = h_pre[:, 2 * hv + hq:].data_ptr()
+            hv_p = h_pre[:, hv:2 * hv].data_ptr()
+        else:
+            hq_p = hk_p = hv_p = None
+        dq = d_uvqk[:, 2 * hv:2 * hv + hq]
+        dk = d_uvqk[:, 2 * hv + hq:]
+        dvv = d_uvqk[:, hv:2 * hv]
+        _lib.call("hstu_attn_bwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out, n_out,
+                  d_attn.data_ptr(), hv, offsets.data_ptr(), B, geo.N, geo.max_len, H, dqk, dv,
+                  _lib.ptr(ts), _lib.ptr(pos_w), _lib.ptr(ts_w), thr.data_ptr(), NUM_BUCKETS,
+                  hq_p, hk_p, hv_p, n_out, dq.data_ptr(), dk.data_ptr(), dvv.data_ptr(), n_out,
+                  _lib.ptr(d_pos_w), _lib.ptr(d_ts_w), _lib.ptr(ws_a), ws_a_n, st)
+        d_w_uvqk = None
+        if ctx.needs_input_grad[3]:
+            d_w_uvqk = torch.empty(D, n_out, dtype=torch.float32, device=dev)
+            ws_n = L.gr_wgrad_workspace_size(rows, D, n_out)
+            ws = torch.empty(max(ws_n, 4), dtype=torch.uint8, device=dev)
+            _lib.call("gr_wgrad", x.data_ptr(), x.stride(0), x_stats.data_ptr(), d_uvqk.data_ptr(),
+                      n_out, offsets.data_ptr(), B, rows, D, n_out, d_w_uvqk.data_ptr(), None,
+                      ws.data_ptr(), ws_n, st)
+        dx = torch.empty(rows, D, dtype=torch.float32, device=dev)
+        _lib.call("hstu_ln_uvqk_bwd", d_uvqk.data_ptr(), n_out, offsets.data_ptr(), B, rows, D,
+                  n_out, w_uvqk.data_ptr(), x.data_ptr(), x.stride(0), x_stats.data_ptr(),
+                  dy.data_ptr(), D, dx.data_ptr(), D, st)
+        return (dx, None, None, d_w_uvqk, d_w_o, d_b_o, d_pos_w, d_ts_w, None, None)
+
+
+def stu_layer(x, offsets, ts, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGeometry, seed: int = 0):
+    _lib.require_gpu(x, offsets, w_uvqk, w_o, b_o)
+    if x.dtype != torch.float32:
+        raise TypeError("stu_layer: float32 only (the reference runs fp32, hstu.py:592)")
+    if ts is not None:
+        ts = ts.to(torch.int64).contiguous()
+    return STULayerFunction.apply(x, offsets, ts, w_uvqk, w_o, b_o, pos_w, ts_w, geo, int(seed))

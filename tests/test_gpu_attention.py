@@ -91,3 +91,93 @@ def test_attn_fwd_full_length_and_len1():
     ref = O.hstu_attention_jagged(q, k, v, offsets, ts, cfg, pos_w, ts_w, _thr())
     got = _run_gpu_fwd(offsets, uvqk, ts, pos_w, ts_w, B, N, H, d, d)
     assert (got - ref).abs().max().item() <= 2e-5 * (1 + ref.abs().max().item())
+
+
+def _run_gpu_bwd(offsets, uvqk, dout, ts, pos_w, ts_w, B, N, H, dqk, dv, hpre=None):
+    from mygenerativerecommenders_amd import _lib
+    dev = torch.device("cuda")
+    u = uvqk.to(dev)
+    hv, hq = H * dv, H * dqk
+    q, k, v = u[:, 2 * hv:2 * hv + hq], u[:, 2 * hv + hq:], u[:, hv:2 * hv]
+    do = dout.to(dev).contiguous()
+    T = u.shape[0]
+    d = torch.full((T, u.shape[1]), float("nan"), device=dev)
+    dq, dk, dvv = d[:, 2 * hv:2 * hv + hq], d[:, 2 * hv + hq:], d[:, hv:2 * hv]
+    offs = offsets.to(dev)
+    thr = torch.tensor(_thr(), device=dev)
+    tsd = ts.to(dev) if ts is not None else None
+    pw, tw = pos_w.to(dev), ts_w.to(dev)
+    dpw = torch.full_like(pw, float("nan"))
+    dtw = torch.full_like(tw, float("nan"))
+    max_len = int((offsets[1:] - offsets[:-1]).max()) if B else 0
+    L = _lib.lib()
+    ws_bytes = L.hstu_attn_bwd_workspace_size(B, N, max_len, H, 128)
+    ws = torch.empty(max(ws_bytes, 4), dtype=torch.uint8, device=dev)
+    hd = hpre.to(dev) if hpre is not None else None
+    hq_p = hd[:, 2 * hv:2 * hv + hq].data_ptr() if hd is not None else None
+    hk_p = hd[:, 2 * hv + hq:].data_ptr() if hd is not None else None
+    hv_p = hd[:, hv:2 * hv].data_ptr() if hd is not None else None
+    _lib.call("hstu_attn_bwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), u.stride(0), u.stride(0),
+              do.data_ptr(), do.stride(0), offs.data_ptr(), B, N, max_len, H, dqk, dv,
+              _lib.ptr(tsd), pw.data_ptr(), tw.data_ptr(), thr.data_ptr(), 128,
+              hq_p, hk_p, hv_p, u.stride(0) if hd is not None else 0,
+              dq.data_ptr(), dk.data_ptr(), dvv.data_ptr(), d.stride(0),
+              dpw.data_ptr(), dtw.data_ptr(), ws.data_ptr(), ws_bytes, _lib.stream_handle())
+    torch.cuda.synchronize()
+    return dq.cpu(), dk.cpu(), dvv.cpu(), dpw.cpu(), dtw.cpu()
+
+
+def _close(got, ref, rel=3e-5):
+    tol = rel * (1 + ref.abs().max().item())
+    err = (got - ref).abs().max().item()
+    assert torch.isfinite(got).all(), "non-finite"
+    assert err <= tol, f"max abs err {err:.3e} > tol {tol:.3e}"
+
+
+@pytest.mark.parametrize("B,N,H,dqk,dv,with_ts", [
+    (4, 43, 1, 16, 16, True),
+    (4, 43, 1, 50, 50, True),
+    (3, 75, 2, 25, 25, True),
+    (2, 211, 1, 50, 50, True),
+    (3, 130, 2, 8, 8, False),
+    (2, 150, 1, 64, 64, True),
+    (2, 100, 1, 128, 96, True),
+])
+def test_attn_bwd_vs_oracle(B, N, H, dqk, dv, with_ts):
+    lengths, offsets, uvqk, ts, pos_w, ts_w = _case(B * 11 + N, B, N, H, dqk, dv,
+                                                      with_ts=with_ts)
+    hv, hq = H * dv, H * dqk
+    uv = uvqk.clone().requires_grad_(True)
+    pw = pos_w.clone().requires_grad_(True)
+    tw = ts_w.clone().requires_grad_(True)
+    q, k, v = uv[:, 2 * hv:2 * hv + hq], uv[:, 2 * hv + hq:], uv[:, hv:2 * hv]
+    cfg = O.HSTUConfig(N=N, D=1, H=H, dqk=dqk, dv=dv)
+    ref = O.hstu_attention_jagged(q, k, v, offsets, ts, cfg, pw, tw, _thr())
+    g = torch.Generator().manual_seed(99)
+    dout = torch.randn(ref.shape, generator=g)
+    (ref * dout).sum().backward()
+    gq, gk, gv = (uv.grad[:, 2 * hv:2 * hv + hq], uv.grad[:, 2 * hv + hq:],
+                  uv.grad[:, hv:2 * hv])
+    dq, dk, dvv, dpw, dtw = _run_gpu_bwd(offsets, uvqk, dout, ts, pos_w, ts_w, B, N, H, dqk, dv)
+    _close(dq, gq)
+    _close(dk, gk)
+    _close(dvv, gv)
+    if with_ts:
+        _close(dpw, pw.grad, rel=1e-4)
+        _close(dtw, tw.grad, rel=1e-4)
+
+
+def test_attn_bwd_fused_silu_grad():
+    B, N, H, d = 3, 75, 1, 32
+    lengths, offsets, uvqk, ts, pos_w, ts_w = _case(17, B, N, H, d, d)
+    g = torch.Generator().manual_seed(5)
+    hpre = torch.randn(uvqk.shape, generator=g)
+    dout = torch.randn(uvqk.shape[0], H * d, generator=g)
+    a = _run_gpu_bwd(offsets, uvqk, dout, ts, pos_w, ts_w, B, N, H, d, d)
+    b = _run_gpu_bwd(offsets, uvqk, dout, ts, pos_w, ts_w, B, N, H, d, d, hpre=hpre)
+    s = torch.sigmoid(hpre)
+    sg = s * (1 + hpre * (1 - s))
+    hv = H * d
+    _close(b[0], a[0] * sg[:, 2 * hv:3 * hv])
+    _close(b[1], a[1] * sg[:, 3 * hv:])
+    _close(b[2], a[2] * sg[:, hv:2 * hv])
