@@ -153,6 +153,42 @@ GR_API int gr_wgrad(const float* a, int64_t lda, const float* a_stats, const flo
              int64_t ldb, const int64_t* offsets, int B, int64_t max_rows, int Ka, int Nb,
              float* c, float* a_colsum, void* workspace, size_t ws_bytes, void* stream);
 
+/* ---------------------------------------------------------------- MIPS retrieval
+ * Replaces indexing/top_k.py:44-70 (MIPSBruteForceTopK: mm + torch.topk) and
+ * indexing/candidate_index.py:107-164 (get_top_k_outputs: top-(k+N0), drop the row's
+ * invalid ids, keep the first k) with one fused pass: scores are never materialised
+ * and invalid ids are excluded during selection (equivalent).
+ *
+ * mips_pack_items: re-lays the (X, D) row-major fp32 item table into the
+ * MFMA-native blocked layout the scorer streams (done once per
+ * CandidateIndex.update_embeddings); `packed` needs mips_packed_items_bytes(X, D).
+ *
+ * mips_topk: queries (B, D) fp32; scores are the k-ordered fp32 fmaf chain over d.
+ * Output rows are sorted by score desc, then catalog index asc (torch.topk leaves
+ * ties unspecified).  Candidate item i (local row) has global index index_base + i
+ * and id item_ids[i] (or index_base + i when item_ids is NULL).  Items whose id is in
+ * the query's row of invalid_ids (B, N0) are excluded (padding zeros included, as in
+ * the reference).  Rows with fewer than k valid items are padded with
+ * (-inf, id -1, index -1).  out_index (B, k) is optional.  Limits: D <= 256,
+ * k <= 256, N0 <= 256, X < 2^31.
+ */
+GR_API size_t mips_packed_items_bytes(int64_t X, int D);
+GR_API int mips_pack_items(const float* items, int64_t X, int D, float* packed, void* stream);
+GR_API size_t mips_topk_workspace_size(int B, int64_t X, int D, int k);
+GR_API int mips_topk(const float* queries, const float* packed_items, int64_t X, int D,
+              const int64_t* item_ids, int64_t index_base, const int64_t* invalid_ids,
+              int N0, int B, int k, float* out_scores, int64_t* out_ids, int64_t* out_index,
+              void* workspace, size_t ws_bytes, void* stream);
+
+/* mips_merge_topk: merges n_lists candidate lists per query (e.g. the all-gathered
+ * per-shard results of a row-sharded catalog) into the global top-k with the same
+ * canonical order.  cand_* are (n_lists, B, k_in); cand_index -1 marks an empty slot.
+ * n_lists * k_in <= 8192, k <= 256.
+ */
+GR_API int mips_merge_topk(const float* cand_scores, const int64_t* cand_index,
+                    const int64_t* cand_ids, int n_lists, int B, int k_in, int k,
+                    float* out_scores, int64_t* out_ids, int64_t* out_index, void* stream);
+
 #ifdef __cplusplus
 }  /* extern "C" */
 #endif

@@ -1,0 +1,644 @@
+// Brute-force MIPS top-k with fused invalid-id exclusion — gfx950, f32 MFMA.
+//
+// Replaces reference indexing/top_k.py:44-70 (mm -> (B, X) logits in HBM -> torch.topk)
+// and indexing/candidate_index.py:107-164 (top-(k+N0), (B, k', N0) compare, cumsum,
+// nonzero host sync, gather).  Nothing (B, X) is ever materialised.
+//
+// Item table layout (mips_pack_items): MFMA-native blocks of 16 items.  For item i,
+// dim d: block ib = i/16, lane l = 16*(d%4) + i%16, k-step st = d/4, stored at
+//   packed[((ib * KS2 + st/2) * 64 + l) * 2 + st%2]        (KS2 = ceil(ceil(D/4)/2))
+// so the A operand of v_mfma_f32_16x16x4_f32 for a whole block is read with fully
+// coalesced 512-B float2 loads (no LDS staging): the table is re-laid out once per
+// CandidateIndex.update_embeddings, not per query batch.
+//
+// Scores are the k-ordered fp32 fmaf chain over d = 0..D-1 (an f32 MFMA IS that chain),
+// bit-identical to oracle/topk_oracle.c.  Order: score desc, then catalog index asc.
+//
+// Phase 1 (mips_select_kernel): a workgroup = 4 waves = 16 queries x a contiguous item
+// range; every lane keeps its query's running threshold tau (the k-th best VALID score
+// seen so far).  Scores > tau are appended (LDS atomics) to a per-query LDS buffer;
+// when a buffer may overflow, the 4 waves compact it (invalid ids dropped by binary
+// search in the query's sorted invalid list, exact k-th by 8-bit radix select, ties
+// by index) and raise tau.  Each workgroup emits its range's exact top-k per query.
+// Phase 2 (mips_merge_kernel): one workgroup per query merges the per-range lists
+// (also used for the cross-GPU merge of a row-sharded catalog), radix-selects the
+// global top-k and bitonic-sorts it.
+#include "common.h"
+
+#include "../../include/gr_hstu.h"
+
+namespace gr {
+
+constexpr int QG = 16;       // queries per workgroup (MFMA column block)
+constexpr int CAP = 512;     // per-query candidate buffer
+constexpr int INV_MAX = 256; // max invalid ids per query
+constexpr uint32_t VERIFIED = 0x80000000u;
+
+__device__ __forceinline__ uint32_t ord_key(float s) {
+  // monotone map float -> uint32 with -0 == +0; 0 is reserved for "dropped"
+  if (s == 0.f) s = 0.f;
+  uint32_t b = __float_as_uint(s);
+  uint32_t k = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+  return k == 0u ? 1u : k;
+}
+__device__ __forceinline__ float key_to_float(uint32_t k) {
+  uint32_t b = (k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k;
+  return __uint_as_float(b);
+}
+
+__device__ __forceinline__ bool sorted_contains(const int64_t* v, int n, int64_t key) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    int m = (lo + hi) >> 1;
+    if (v[m] < key) lo = m + 1; else hi = m;
+  }
+  return lo < n && v[lo] == key;
+}
+
+// ----------------------------------------------------------------- packing
+__global__ void pack_items_kernel(const float* items, int64_t X, int D, int KS2, float* packed) {
+  const int64_t nblk = (X + 15) / 16;
+  const int64_t total = nblk * KS2 * 128;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int h = (int)(e & 1);
+    const int l = (int)((e >> 1) & 63);
+    const int64_t t = e >> 7;  // ib * KS2 + j
+    const int j = (int)(t % KS2);
+    const int64_t ib = t / KS2;
+    const int st = 2 * j + h;
+    const int d = 4 * st + (l >> 4);
+    const int64_t i = ib * 16 + (l & 15);
+    packed[e] = (i < X && d < D) ? items[i * D + d] : 0.f;
+  }
+}
+
+// ----------------------------------------------------------------- wave radix select
+// Finds K* = the k-th largest of the nonzero keys held by the wave (EPL per lane) and
+// how many entries equal to K* are needed (k_rem).  hist: 256 ints of LDS per wave.
+template <int EPL>
+__device__ void wave_radix_select(const uint32_t (&key)[EPL], int k, int* hist, uint32_t& kstar,
+                                  int& k_rem) {
+  const int lane = threadIdx.x & 63;
+  uint32_t prefix = 0, mask = 0;
+  int need = k;
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    for (int i = lane; i < 256; i += 64) hist[i] = 0;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+    for (int t = 0; t < EPL; ++t)
+      if (key[t] != 0u && (key[t] & mask) == prefix) atomicAdd(&hist[(key[t] >> shift) & 255], 1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // lane l owns digits 255-4l .. 252-4l (descending)
+    int c[4], s = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      c[j] = hist[255 - 4 * lane - j];
+      s += c[j];
+    }
+    int incl = s;  // inclusive scan over lanes (descending digits)
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      int v = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += v;
+    }
+    const int excl = incl - s;
+    // the lane whose range crosses `need`
+    const bool mine = excl < need && incl >= need;
+    const unsigned long long bal = __ballot(mine);
+    const int owner = __ffsll((long long)bal) - 1;
+    int digit = 0, above = 0;
+    if (mine) {
+      int run = excl;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (run + c[j] >= need) {
+          digit = 255 - 4 * lane - j;
+          above = run;
+          break;
+        }
+        run += c[j];
+      }
+    }
+    digit = __shfl(digit, owner, 64);
+    above = __shfl(above, owner, 64);
+    prefix |= (uint32_t)digit << shift;
+    mask |= 0xFFu << shift;
+    need -= above;
+  }
+  kstar = prefix;
+  k_rem = need;
+}
+
+// ----------------------------------------------------------------- phase 1
+struct SelectArgs {
+  const float* q;
+  const float* packed;
+  int64_t X;
+  int D, B, k, N0, n_ranges;
+  int64_t range_items;  // multiple of 4*64
+  const int64_t* item_ids;
+  int64_t index_base;
+  const int64_t* invalid;
+  float* part_score;   // [n_ranges][B][k]
+  int64_t* part_index; // [n_ranges][B][k]  (global index, -1 = empty)
+};
+
+template <int KS, int BLOCKS>
+__global__ __launch_bounds__(256) void mips_select_kernel(SelectArgs a) {
+  constexpr int KS2 = (KS + 1) / 2;
+  constexpr int STEP = BLOCKS * 16;  // items per wave per step
+  __shared__ float cs[QG * CAP];
+  __shared__ uint32_t ci[QG * CAP];
+  __shared__ int64_t inv[QG * INV_MAX];
+  __shared__ int hist[4 * 256];
+  __shared__ int cnt[QG];
+  __shared__ float tau_s[QG];
+  __shared__ int need_compact;
+
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int lr = lane & 15, lg = lane >> 4;
+  // XCD-aware decode: the query groups of one item range share blockIdx % 8
+  const int n_qg = (a.B + QG - 1) / QG;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, rest = bid >> 3;
+  const int g = rest % n_qg;
+  const int range = (rest / n_qg) * 8 + xcd;
+  if (range >= a.n_ranges) return;
+  const int q0 = g * QG;
+  const int64_t x_begin = (int64_t)range * a.range_items;
+  const int64_t x_end = min(a.X, x_begin + a.range_items);
+
+  // ---- prologue: sorted invalid lists, counters
+  const int n0p = a.N0 > 0 ? (a.N0 <= 64 ? 64 : (a.N0 <= 128 ? 128 : 256)) : 0;
+  for (int e = tid; e < QG * n0p; e += 256) {
+    const int qq = e / n0p, j = e - qq * n0p;
+    int64_t v = INT64_MAX;
+    if (q0 + qq < a.B && j < a.N0) v = a.invalid[(int64_t)(q0 + qq) * a.N0 + j];
+    inv[qq * INV_MAX + j] = v;
+  }
+  if (tid < QG) {
+    cnt[tid] = 0;
+    tau_s[tid] = q0 + tid < a.B ? -INFINITY : INFINITY;  // padded queries collect nothing
+  }
+  __syncthreads();
+  for (int size = 2; size <= n0p; size <<= 1) {  // bitonic sort, QG independent rows
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int e = tid; e < QG * (n0p / 2); e += 256) {
+        const int qq = e / (n0p / 2), p = e - qq * (n0p / 2);
+        const int i = 2 * p - (p & (stride - 1));
+        const int j = i + stride;
+        const bool up = (i & size) == 0;
+        int64_t* row = inv + qq * INV_MAX;
+        const int64_t x = row[i], y = row[j];
+        if ((x > y) == up) {
+          row[i] = y;
+          row[j] = x;
+        }
+      }
+      __syncthreads();
+    }
+  }
+
+  // ---- query fragments (B operand): Q[q0 + lr][4 st + lg]
+  float qreg[KS];
+  {
+    const int qq = q0 + lr;
+#pragma unroll
+    for (int st = 0; st < KS; ++st) {
+      const int d = 4 * st + lg;
+      qreg[st] = (qq < a.B && d < a.D) ? a.q[(int64_t)qq * a.D + d] : 0.f;
+    }
+  }
+
+  const int64_t n_items = x_end > x_begin ? x_end - x_begin : 0;
+  const int n_steps = (int)((n_items + 4 * STEP - 1) / (4 * STEP));
+  const float2* pk = reinterpret_cast<const float2*>(a.packed);
+  int* whist = hist + w * 256;
+
+  auto compact = [&](int qq, int kk) {
+    // one wave compacts query qq's buffer to its exact top-kk valid entries
+    uint32_t key[CAP / 64];
+    float sc[CAP / 64];
+    uint32_t ix[CAP / 64];
+    const int n = cnt[qq];
+    const int64_t* qinv = inv + qq * INV_MAX;
+    int nvalid = 0;
+#pragma unroll
+    for (int t = 0; t < CAP / 64; ++t) {
+      const int j = lane + 64 * t;
+      key[t] = 0u;
+      sc[t] = 0.f;
+      ix[t] = 0u;
+      if (j < n) {
+        sc[t] = cs[qq * CAP + j];
+        ix[t] = ci[qq * CAP + j];
+        bool ok = true;
+        if (!(ix[t] & VERIFIED)) {
+          const int64_t li = (int64_t)(ix[t] & ~VERIFIED);
+          const int64_t id = a.item_ids ? a.item_ids[li] : a.index_base + li;
+          ok = !(a.N0 > 0 && sorted_contains(qinv, a.N0, id));
+          ix[t] |= VERIFIED;
+        }
+        if (ok) {
+          key[t] = ord_key(sc[t]);
+          ++nvalid;
+        }
+      }
+    }
+    // total valid count
+    int tot = nvalid;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) tot += __shfl_xor(tot, o, 64);
+    uint32_t kstar = 0u;
+    int k_rem = 0;
+    bool all = tot <= kk;
+    int eq_cnt = 0;
+    if (!all) {
+      wave_radix_select<CAP / 64>(key, kk, whist, kstar, k_rem);
+#pragma unroll
+      for (int t = 0; t < CAP / 64; ++t) eq_cnt += key[t] == kstar;
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) eq_cnt += __shfl_xor(eq_cnt, o, 64);
+    }
+    // keep flags; ties at kstar: keep the k_rem smallest indices (O(T^2), rare)
+    bool keep[CAP / 64];
+#pragma unroll
+    for (int t = 0; t < CAP / 64; ++t) {
+      keep[t] = key[t] != 0u && (all || key[t] > kstar);
+      if (!all && key[t] == kstar) {
+        if (eq_cnt == k_rem) {
+          keep[t] = true;
+        } else {
+          // rank among equal keys by index: count equal entries with smaller index
+          const uint32_t my = ix[t] & ~VERIFIED;
+          int smaller = 0;
+          for (int j = 0; j < n; ++j) {
+            const uint32_t oj = ci[qq * CAP + j];
+            // equal keys only; already-dropped invalid ones never equal a valid key
+            // because they may carry the same score: re-check via the key array is
+            // not possible across lanes, so compare scores + verified-valid status
+            if (ord_key(cs[qq * CAP + j]) == kstar && (oj & ~VERIFIED) < my) {
+              const int64_t li = (int64_t)(oj & ~VERIFIED);
+              const int64_t id = a.item_ids ? a.item_ids[li] : a.index_base + li;
+              if (!(a.N0 > 0 && sorted_contains(qinv, a.N0, id))) ++smaller;
+            }
+          }
+          keep[t] = smaller < k_rem;
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    // write back compacted (wave-ordered), all reads above are done
+    int base = 0;
+#pragma unroll
+    for (int t = 0; t < CAP / 64; ++t) {
+      const unsigned long long bal = __ballot(keep[t]);
+      const int pos = base + __popcll(bal & ((1ull << lane) - 1ull));
+      if (keep[t]) {
+        cs[qq * CAP + pos] = sc[t];
+        ci[qq * CAP + pos] = ix[t];
+      }
+      base += __popcll(bal);
+    }
+    if (lane == 0) {
+      cnt[qq] = base;
+      tau_s[qq] = all ? -INFINITY : key_to_float(kstar);
+    }
+  };
+
+  float2 frag[BLOCKS][KS2];
+  auto load_step = [&](int step) {
+    const int64_t xb = x_begin + ((int64_t)step * 4 + w) * STEP;
+#pragma unroll
+    for (int bb = 0; bb < BLOCKS; ++bb) {
+      const int64_t ib = (xb >> 4) + bb;
+      const bool ok = xb + bb * 16 < x_end;
+#pragma unroll
+      for (int j = 0; j < KS2; ++j)
+        frag[bb][j] = ok ? pk[(ib * KS2 + j) * 64 + lane] : make_float2(0.f, 0.f);
+    }
+  };
+
+  if (n_steps > 0) load_step(0);
+  for (int step = 0; step < n_steps; ++step) {
+    float2 cur[BLOCKS][KS2];
+#pragma unroll
+    for (int bb = 0; bb < BLOCKS; ++bb)
+#pragma unroll
+      for (int j = 0; j < KS2; ++j) cur[bb][j] = frag[bb][j];
+    if (step + 1 < n_steps) load_step(step + 1);
+    const float tau = tau_s[lr];
+    const int64_t xb = x_begin + ((int64_t)step * 4 + w) * STEP;
+#pragma unroll
+    for (int bb = 0; bb < BLOCKS; ++bb) {
+      f4 s = f4_zero();
+#pragma unroll
+      for (int st = 0; st < KS; ++st)
+        s = mfma16x16x4((st & 1) ? cur[bb][st >> 1].y : cur[bb][st >> 1].x, qreg[st], s);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t item = xb + bb * 16 + 4 * lg + r;
+        if (item < x_end && s[r] > tau) {
+          const int slot = atomicAdd(&cnt[lr], 1);
+          cs[lr * CAP + slot] = s[r];
+          ci[lr * CAP + slot] = (uint32_t)item;  // local index
+        }
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int f = 0;
+      for (int qq = 0; qq < QG; ++qq) f |= cnt[qq] > CAP - 4 * STEP;
+      need_compact = f;
+    }
+    __syncthreads();
+    if (need_compact) {
+      for (int qq = w; qq < QG; qq += 4)
+        if (cnt[qq] > a.k) compact(qq, a.k);
+      __syncthreads();
+    }
+  }
+  // ---- final: exact top-k per query of this range
+  __syncthreads();
+  for (int qq = w; qq < QG; qq += 4) {
+    if (q0 + qq >= a.B) continue;
+    compact(qq, a.k);
+  }
+  __syncthreads();
+  for (int e = tid; e < QG * a.k; e += 256) {
+    const int qq = e / a.k, j = e - qq * a.k;
+    if (q0 + qq >= a.B) continue;
+    const int64_t o = ((int64_t)range * a.B + q0 + qq) * a.k + j;
+    if (j < cnt[qq]) {
+      a.part_score[o] = cs[qq * CAP + j];
+      a.part_index[o] = a.index_base + (int64_t)(ci[qq * CAP + j] & ~VERIFIED);
+    } else {
+      a.part_score[o] = -INFINITY;
+      a.part_index[o] = -1;
+    }
+  }
+}
+
+// ----------------------------------------------------------------- phase 2: merge
+struct MergeArgs {
+  const float* cand_score;    // [n_lists][B][k_in]
+  const int64_t* cand_index;  // [n_lists][B][k_in], -1 = empty
+  const int64_t* cand_ids;    // same shape or null
+  int n_lists, B, k_in, k;
+  const int64_t* item_ids;    // resolve ids when cand_ids == null
+  int64_t index_base;
+  float* out_score;
+  int64_t* out_ids;
+  int64_t* out_index;
+};
+
+constexpr int MERGE_MAX = 8192;
+
+__global__ __launch_bounds__(256) void mips_merge_kernel(MergeArgs a) {
+  __shared__ uint32_t key[MERGE_MAX];
+  __shared__ int hist[256];
+  __shared__ int sh_need, sh_digit;
+  __shared__ uint32_t s_key[256];
+  __shared__ int s_src[256];
+  __shared__ int s_cnt;
+  const int q = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int M = a.n_lists * a.k_in;
+  auto src_of = [&](int e) -> int64_t {
+    const int l = e / a.k_in, j = e - l * a.k_in;
+    return ((int64_t)l * a.B + q) * a.k_in + j;
+  };
+  int nvalid = 0;
+  for (int e = tid; e < M; e += 256) {
+    const int64_t s = src_of(e);
+    const bool ok = a.cand_index[s] >= 0;
+    key[e] = ok ? ord_key(a.cand_score[s]) : 0u;
+    nvalid += ok;
+  }
+  __syncthreads();
+  // block-wide count of valid
+  __shared__ int red[4];
+  int v = nvalid;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  if ((tid & 63) == 0) red[tid >> 6] = v;
+  __syncthreads();
+  const int tot = red[0] + red[1] + red[2] + red[3];
+  const int kk = a.k;
+  uint32_t kstar = 0u;
+  int k_rem = 0;
+  const bool all = tot <= kk;
+  if (!all) {
+    uint32_t prefix = 0, mask = 0;
+    int need = kk;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+      hist[tid] = 0;
+      __syncthreads();
+      for (int e = tid; e < M; e += 256) {
+        const uint32_t x = key[e];
+        if (x != 0u && (x & mask) == prefix) atomicAdd(&hist[(x >> shift) & 255], 1);
+      }
+      __syncthreads();
+      if (tid == 0) {
+        int run = 0, d = 255;
+        for (; d >= 0; --d) {
+          if (run + hist[d] >= need) break;
+          run += hist[d];
+        }
+        sh_digit = d;
+        sh_need = need - run;
+      }
+      __syncthreads();
+      prefix |= (uint32_t)sh_digit << shift;
+      mask |= 0xFFu << shift;
+      need = sh_need;
+      __syncthreads();
+    }
+    kstar = prefix;
+    k_rem = need;
+  }
+  // collect the selected entries: key > kstar, plus k_rem ties with smallest index
+  if (tid == 0) s_cnt = 0;
+  __syncthreads();
+  for (int e = tid; e < M; e += 256) {
+    const uint32_t x = key[e];
+    if (x == 0u) continue;
+    bool take = all || x > kstar;
+    if (!all && x == kstar) {
+      const int64_t my = a.cand_index[src_of(e)];
+      int smaller = 0;
+      for (int f = 0; f < M; ++f)
+        if (key[f] == kstar && a.cand_index[src_of(f)] < my) ++smaller;
+      take = smaller < k_rem;
+    }
+    if (take) {
+      const int p = atomicAdd(&s_cnt, 1);
+      s_key[p] = x;
+      s_src[p] = e;
+    }
+  }
+  __syncthreads();
+  const int n = s_cnt;
+  for (int p = n + tid; p < 256; p += 256) {
+    s_key[p] = 0u;
+    s_src[p] = -1;
+  }
+  __syncthreads();
+  // bitonic sort 256 entries: key desc, then candidate index asc
+  for (int size = 2; size <= 256; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      const int i = tid;
+      const int j = i ^ stride;
+      if (j > i) {
+        const uint32_t ki = s_key[i], kj = s_key[j];
+        const int64_t ii = s_src[i] >= 0 ? a.cand_index[src_of(s_src[i])] : INT64_MAX;
+        const int64_t ij = s_src[j] >= 0 ? a.cand_index[src_of(s_src[j])] : INT64_MAX;
+        const bool i_first = (ki > kj) || (ki == kj && ii < ij);
+        const bool desc = (i & size) == 0;
+        if (i_first != desc) {
+          s_key[i] = kj;
+          s_key[j] = ki;
+          const int t = s_src[i];
+          s_src[i] = s_src[j];
+          s_src[j] = t;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int r = tid; r < kk; r += 256) {
+    const int64_t o = (int64_t)q * kk + r;
+    if (r < n) {
+      const int64_t s = src_of(s_src[r]);
+      const int64_t gi = a.cand_index[s];
+      a.out_score[o] = a.cand_score[s];
+      if (a.out_index) a.out_index[o] = gi;
+      int64_t id;
+      if (a.cand_ids) id = a.cand_ids[s];
+      else id = a.item_ids ? a.item_ids[gi - a.index_base] : gi;
+      a.out_ids[o] = id;
+    } else {
+      a.out_score[o] = -INFINITY;
+      if (a.out_index) a.out_index[o] = -1;
+      a.out_ids[o] = -1;
+    }
+  }
+}
+
+struct TopkPlan {
+  int KS, n_ranges;
+  int64_t range_items;
+  size_t part_bytes;
+};
+
+static TopkPlan plan_topk(int B, int64_t X, int D, int k) {
+  TopkPlan p;
+  p.KS = ceil_div(D, 4);
+  const int n_qg = ceil_div(B, QG);
+  int target = ceil_div(256, n_qg);  // ~one workgroup per CU
+  int64_t step4 = 4 * 64;
+  int64_t ri = (X + target - 1) / target;
+  ri = ((ri + step4 - 1) / step4) * step4;
+  if (ri < step4) ri = step4;
+  p.range_items = ri;
+  p.n_ranges = (int)((X + ri - 1) / ri);
+  if (p.n_ranges < 1) p.n_ranges = 1;
+  while ((int64_t)p.n_ranges * k > MERGE_MAX) {  // merge capacity
+    p.range_items *= 2;
+    p.n_ranges = (int)((X + p.range_items - 1) / p.range_items);
+  }
+  p.part_bytes = (size_t)p.n_ranges * B * k * (sizeof(float) + sizeof(int64_t));
+  return p;
+}
+
+template <int KS>
+static int launch_select(const SelectArgs& a, hipStream_t st) {
+  constexpr int BLOCKS = KS <= 16 ? 4 : (KS <= 32 ? 2 : 1);
+  const int n_qg = ceil_div(a.B, QG);
+  const int n_r8 = ceil_div(a.n_ranges, 8) * 8;
+  const int grid = n_r8 * n_qg;
+  hipLaunchKernelGGL((mips_select_kernel<KS, BLOCKS>), dim3(grid), dim3(256), 0, st, a);
+  GR_LAUNCH_CHECK("mips_topk(select)");
+  return 0;
+}
+
+}  // namespace gr
+
+using namespace gr;
+
+extern "C" size_t mips_packed_items_bytes(int64_t X, int D) {
+  const int KS2 = (ceil_div(D, 4) + 1) / 2;
+  return sizeof(float) * (size_t)((X + 15) / 16) * KS2 * 128;
+}
+
+extern "C" int mips_pack_items(const float* items, int64_t X, int D, float* packed, void* stream) {
+  GR_REQUIRE(items && packed && X >= 0 && D > 0, "mips_pack_items: bad args");
+  if (X == 0) return 0;
+  const int KS2 = (ceil_div(D, 4) + 1) / 2;
+  hipLaunchKernelGGL(pack_items_kernel, dim3(2048), dim3(256), 0, (hipStream_t)stream, items, X,
+                     D, KS2, packed);
+  GR_LAUNCH_CHECK("mips_pack_items");
+  return 0;
+}
+
+extern "C" size_t mips_topk_workspace_size(int B, int64_t X, int D, int k) {
+  if (B <= 0 || X <= 0 || D <= 0 || k <= 0) return 0;
+  return plan_topk(B, X, D, k).part_bytes;
+}
+
+extern "C" int mips_topk(const float* queries, const float* packed_items, int64_t X, int D,
+                         const int64_t* item_ids, int64_t index_base, const int64_t* invalid_ids,
+                         int N0, int B, int k, float* out_scores, int64_t* out_ids,
+                         int64_t* out_index, void* workspace, size_t ws_bytes, void* stream) {
+  GR_REQUIRE(queries && packed_items && out_scores && out_ids, "mips_topk: null pointer");
+  GR_REQUIRE(B >= 0 && X >= 0 && D > 0 && D <= 256, "mips_topk: D=%d not in [1, 256]", D);
+  GR_REQUIRE(k > 0 && k <= 256, "mips_topk: k=%d not in [1, 256]", k);
+  GR_REQUIRE(N0 >= 0 && N0 <= INV_MAX && (N0 == 0 || invalid_ids),
+             "mips_topk: N0=%d not in [0, %d] (or invalid_ids null)", N0, INV_MAX);
+  GR_REQUIRE(X < 0x7FFFFFFF, "mips_topk: X must be < 2^31 per shard");
+  hipStream_t st = (hipStream_t)stream;
+  if (B == 0) return 0;
+  TopkPlan p = plan_topk(B, X > 0 ? X : 1, D, k);
+  GR_REQUIRE(workspace && ws_bytes >= p.part_bytes, "mips_topk: workspace %zu B < %zu B", ws_bytes,
+             p.part_bytes);
+  float* part_score = (float*)workspace;
+  int64_t* part_index = (int64_t*)(part_score + (size_t)p.n_ranges * B * k);
+  SelectArgs a{queries, packed_items, X, D, B, k, N0, p.n_ranges, p.range_items,
+               item_ids, index_base, invalid_ids, part_score, part_index};
+  int rc;
+  switch (p.KS) {
+    case 1: case 2: rc = launch_select<2>(a, st); break;
+    case 3: case 4: rc = launch_select<4>(a, st); break;
+    case 5: case 6: case 7: case 8: rc = launch_select<8>(a, st); break;
+    case 9: case 10: case 11: case 12: case 13: rc = launch_select<13>(a, st); break;
+    case 14: case 15: case 16: rc = launch_select<16>(a, st); break;
+    default:
+      if (p.KS <= 32) rc = launch_select<32>(a, st);
+      else rc = launch_select<64>(a, st);
+  }
+  if (rc) return rc;
+  MergeArgs m{part_score, part_index, nullptr, p.n_ranges, B, k, k, item_ids, index_base,
+              out_scores, out_ids, out_index};
+  hipLaunchKernelGGL(mips_merge_kernel, dim3(B), dim3(256), 0, st, m);
+  GR_LAUNCH_CHECK("mips_topk(merge)");
+  return 0;
+}
+
+extern "C" int mips_merge_topk(const float* cand_scores, const int64_t* cand_index,
+                               const int64_t* cand_ids, int n_lists, int B, int k_in, int k,
+                               float* out_scores, int64_t* out_ids, int64_t* out_index,
+                               void* stream) {
+  GR_REQUIRE(cand_scores && cand_index && cand_ids && out_scores && out_ids,
+             "mips_merge_topk: null pointer");
+  GR_REQUIRE(k > 0 && k <= 256 && k_in > 0 && n_lists > 0 && (int64_t)n_lists * k_in <= MERGE_MAX,
+             "mips_merge_topk: need 0 < k <= 256 and n_lists*k_in <= %d", MERGE_MAX);
+  if (B == 0) return 0;
+  MergeArgs m{cand_scores, cand_index, cand_ids, n_lists, B, k_in, k, nullptr, 0,
+              out_scores, out_ids, out_index};
+  hipLaunchKernelGGL(mips_merge_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, m);
+  GR_LAUNCH_CHECK("mips_merge_topk");
+  return 0;
+}

@@ -1,0 +1,137 @@
+"""Top-k modules — drop-in for reference ``models/indexing/top_k.py`` (Hydra
+``_target_: ...indexing.top_k.MIPSBruteForceTopK``), running the fused gfx950
+scorer + selector of ``libgr_hstu.so`` (``mips_topk``).
+
+Differences from the reference, all deliberate:
+  * results are always sorted, with a canonical tie order (score desc, catalog index
+    asc) — ``torch.topk`` leaves ties unspecified;
+  * the (B, X) logits are never materialised;
+  * invalid-id exclusion can be fused (``invalid_ids=``), which
+    ``CandidateIndex.get_top_k_outputs`` uses instead of top-(k+N0) + filtering;
+  * limits: D <= 256, k <= 256, N0 <= 256, X < 2^31 (per shard).
+"""
+from __future__ import annotations
+
+import abc
+from typing import Optional, Tuple
+
+import torch
+
+from . import _lib
+
+
+class TopKModule(torch.nn.Module):
+    """top_k.py:21-40."""
+
+    @abc.abstractmethod
+    def forward(self, query_embeddings: torch.Tensor, item_embeddings_t: torch.Tensor,
+                item_ids: torch.Tensor, k: int, sorted: bool = True
+                ) -> Tuple[torch.Tensor, torch.Tensor]:
+        pass
+
+
+class PackedItems:
+    """An item table in the MFMA-native blocked layout (``mips_pack_items``)."""
+
+    def __init__(self, items: torch.Tensor):
+        _lib.require_gpu(items)
+        if items.dim() != 2 or items.dtype != torch.float32:
+            raise TypeError("PackedItems: expected a (X, D) float32 tensor")
+        items = items.contiguous()
+        self.X, self.D = items.shape
+        if self.D > 256:
+            raise ValueError(f"mips_topk supports D <= 256 (got {self.D})")
+        nbytes = _lib.lib().mips_packed_items_bytes(self.X, self.D)
+        self.buf = torch.empty(max(nbytes // 4, 1), dtype=torch.float32, device=items.device)
+        _lib.call("mips_pack_items", items.data_ptr(), self.X, self.D, self.buf.data_ptr(),
+                  _lib.stream_handle())
+        self.device = items.device
+
+
+def mips_topk(queries: torch.Tensor, packed: PackedItems, k: int,
+              item_ids: Optional[torch.Tensor] = None, invalid_ids: Optional[torch.Tensor] = None,
+              index_base: int = 0, return_index: bool = False):
+    """Fused brute-force MIPS top-k over a packed table.  Returns (scores (B,k) f32,
+    ids (B,k) i64[, global index (B,k) i64])."""
+    _lib.require_gpu(queries)
+    B, D = queries.shape
+    if D != packed.D:
+        raise ValueError(f"query dim {D} != item dim {packed.D}")
+    if not 0 < k <= 256:
+        raise ValueError(f"mips_topk supports 0 < k <= 256 (got {k})")
+    q = queries.contiguous().float()
+    dev = q.device
+    ids = None
+    if item_ids is not None:
+        ids = item_ids.reshape(-1).to(device=dev, dtype=torch.int64).contiguous()
+        if ids.numel() != packed.X:
+            raise ValueError(f"item_ids has {ids.numel()} entries, table has {packed.X}")
+    inv = None
+    N0 = 0
+    if invalid_ids is not None:
+        inv = invalid_ids.to(device=dev, dtype=torch.int64).contiguous()
+        if inv.dim() != 2 or inv.shape[0] != B:
+            raise ValueError("invalid_ids must be (B, N0)")
+        N0 = inv.shape[1]
+        if N0 > 256:
+            raise ValueError(f"mips_topk supports N0 <= 256 invalid ids per row (got {N0})")
+    scores = torch.empty(B, k, dtype=torch.float32, device=dev)
+    out_ids = torch.empty(B, k, dtype=torch.int64, device=dev)
+    out_idx = torch.empty(B, k, dtype=torch.int64, device=dev) if return_index else None
+    ws_n = _lib.lib().mips_topk_workspace_size(B, packed.X, D, k)
+    ws = torch.empty(max(ws_n, 16), dtype=torch.uint8, device=dev)
+    _lib.call("mips_topk", q.data_ptr(), packed.buf.data_ptr(), packed.X, D, _lib.ptr(ids),
+              int(index_base), _lib.ptr(inv), N0, B, k, scores.data_ptr(), out_ids.data_ptr(),
+              _lib.ptr(out_idx), ws.data_ptr(), ws_n, _lib.stream_handle())
+    if return_index:
+        return scores, out_ids, out_idx
+    return scores, out_ids
+
+
+def merge_topk(cand_scores: torch.Tensor, cand_index: torch.Tensor, cand_ids: torch.Tensor,
+               k: int, return_index: bool = False):
+    """Merges (n_lists, B, k_in) candidate lists into the global (B, k) top-k
+    (``mips_merge_topk``): the reduction step of a row-sharded catalog."""
+    _lib.require_gpu(cand_scores, cand_index, cand_ids)
+    n_lists, B, k_in = cand_scores.shape
+    dev = cand_scores.device
+    s = cand_scores.contiguous()
+    i = cand_index.contiguous()
+    d = cand_ids.contiguous()
+    scores = torch.empty(B, k, dtype=torch.float32, device=dev)
+    out_ids = torch.empty(B, k, dtype=torch.int64, device=dev)
+    out_idx = torch.empty(B, k, dtype=torch.int64, device=dev) if return_index else None
+    _lib.call("mips_merge_topk", s.data_ptr(), i.data_ptr(), d.data_ptr(), n_lists, B, k_in, k,
+              scores.data_ptr(), out_ids.data_ptr(), _lib.ptr(out_idx), _lib.stream_handle())
+    if return_index:
+        return scores, out_ids, out_idx
+    return scores, out_ids
+
+
+class MIPSBruteForceTopK(TopKModule):
+    """top_k.py:43-70 — (scores, ids) of the k best inner products.
+
+    ``item_embeddings_t`` is the (D, X) transposed view the reference's CandidateIndex
+    keeps; the packed copy is cached per (storage, version) so a table is re-laid out
+    once per ``update_embeddings``, not once per query batch.
+    """
+
+    def __init__(self) -> None:
+        super().__init__()
+        self._cache_key = None
+        self._packed: Optional[PackedItems] = None
+
+    def packed_for(self, item_embeddings_t: torch.Tensor) -> PackedItems:
+        key = (item_embeddings_t.data_ptr(), item_embeddings_t._version,
+               tuple(item_embeddings_t.shape))
+        if self._packed is None or self._cache_key != key:
+            self._packed = PackedItems(item_embeddings_t.t())
+            self._cache_key = key
+        return self._packed
+
+    def forward(self, query_embeddings: torch.Tensor, item_embeddings_t: torch.Tensor,
+                item_ids: torch.Tensor, k: int, sorted: bool = True,
+                invalid_ids: Optional[torch.Tensor] = None
+                ) -> Tuple[torch.Tensor, torch.Tensor]:
+        packed = self.packed_for(item_embeddings_t)
+        return mips_topk(query_embeddings, packed, k, item_ids=item_ids, invalid_ids=invalid_ids)
