@@ -1,0 +1,333 @@
+"""Benchmark: HSTU encoder fwd+bwd seq/s (+ fused MIPS top-k items scored/s) at ml-1m
+shapes on MI355X — BASELINE.json configs[1] ("ml-1m-hstu bf16 on 1xMI355X, 4-layer d=50
+seq_len=200"); the path computes in fp32 (the reference's own precision, hstu.py:592).
+
+One step (per rank, weak scaling): synthetic batch B=128 sequences of length 200
+(N = 200 + 11 = 211 padded, D = 50, 1 head, 4 blocks, train mode with dropout 0.2):
+HSTU forward, backward (input + all parameter grads), flat-buffer RCCL all-reduce of
+the gradients (N > 1), AdamW step, then retrieval for the batch: the L2-normalised
+last-position encodings score the ml-1m catalog (3,953 items) with the batch's 211
+past ids excluded, top-200.  Inputs are resident in HBM before timing starts.
+
+A second timed leg measures retrieval at SURVEY.md C4 scale: a 10M-item catalog
+row-sharded over the N ranks (strong scaling), 128 queries, k = 200, 211 invalid ids,
+all-gather + device merge.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import time
+
+import torch
+
+
+def _sync_barrier(world):
+    torch.cuda.synchronize()
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+        torch.cuda.synchronize()
+
+
+def _max_over_ranks(x: float, world: int) -> float:
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def make_batch(B, N0, out_len, D, seed, device, fixed_len=True):
+    g = torch.Generator().manual_seed(seed)
+    N = N0 + out_len
+    if fixed_len:
+        lengths = torch.full((B,), N0, dtype=torch.int64)
+    else:
+        lengths = torch.randint(20, N0 + 1, (B,), generator=g)
+    x = torch.randn(B, N, D, generator=g)
+    ts = torch.zeros(B, N, dtype=torch.int64)
+    start = 950_000_000 + (torch.rand(B, generator=g) * 1e8).long()
+    inc = (-torch.log(torch.rand(B, N, generator=g).clamp_min(1e-12)) * 1e5).long()
+    full = start[:, None] + torch.cumsum(inc, 1)
+    pos = torch.arange(N)[None, :]
+    ts = torch.where(pos <= lengths[:, None], full, torch.zeros_like(full))
+    past_ids = torch.randint(1, 3953, (B, N), generator=g)
+    past_ids = torch.where(pos < lengths[:, None], past_ids, torch.zeros_like(past_ids))
+    dy = torch.randn(B, N, D, generator=g)
+    return (lengths.to(device), x.to(device), ts.to(device), past_ids.to(device), dy.to(device))
+
+
+def build_model(N0, out_len, D, blocks, device):
+    from mygenerativerecommenders_amd.hstu import HSTU
+    torch.manual_seed(0)
+    enc = HSTU(max_sequence_len=N0, max_output_len=out_len, embedding_dim=D,
+               item_embedding_dim=D, num_blocks=blocks, num_heads=1, linear_dim=D,
+               attention_dim=D, normalization="rel_bias", linear_config="uvqk",
+               linear_activation="silu", linear_dropout_rate=0.2, attn_dropout_rate=0.0)
+    return enc.to(device).train()
+
+
+def attn_flops(lengths, H, dqk, dv, blocks):
+    """Algorithmic attention FLOPs per launch kind, summed over the batch (causal
+    triangle incl. diagonal, no recompute counted)."""
+    T = float(sum(int(L) * (int(L) + 1) // 2 for L in lengths.tolist())) * H
+    fwd = 2 * T * (dqk + dv)
+    dkv = 2 * T * (2 * dv + dqk)   # dP, dV, dK
+    dq = 2 * T * dqk               # dQ
+    return fwd, dkv, dq
+
+
+def peak_table():
+    # MI355X_MICROARCH.md, chip-level parameters
+    return {"fp32_mfma_tflops": 157.3, "bf16_mfma_tflops": 2500.0, "hbm_gbs": 8000.0}
+
+
+def cpu_baseline_hstu(B_sample, N0, out_len, D, blocks, budget_s=12.0):
+    """Times the oracle's padded-order fp32 restatement (fwd+bwd) on the host cores."""
+    import numpy as np
+
+    from mygenerativerecommenders_amd.bucket_table import BUCKET_THRESHOLDS
+    from oracle import hstu_oracle as O
+    thr = np.asarray(BUCKET_THRESHOLDS)
+    enc = build_model(N0, out_len, D, blocks, "cpu")
+    lengths, x, ts, _, dy = make_batch(B_sample, N0, out_len, D, 123, "cpu")
+    st = {k: v.detach().clone().requires_grad_(True) for k, v in enc.state_dict().items()
+          if k != "_attn_mask"}
+    layers = [O.layer_params_from_state(st, i) for i in range(blocks)]
+    cfg = O.HSTUConfig(N=N0 + out_len, D=D, H=1, dqk=D, dv=D)
+
+    def one():
+        xr = x.clone().requires_grad_(True)
+        y = O.hstu_forward_padded(lengths, xr, ts, cfg, layers, thr)
+        (y * dy).sum().backward()
+
+    one()  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        one()
+        n += 1
+        if time.perf_counter() - t0 > budget_s / 2 or n >= 20:
+            break
+    dt = (time.perf_counter() - t0) / n
+    return B_sample / dt, n, dt
+
+
+def cpu_baseline_topk(B, X, D, k, N0, budget_s=8.0):
+    import numpy as np
+
+    from oracle import topk_oracle
+    g = np.random.default_rng(0)
+    E = g.standard_normal((X, D), dtype=np.float32)
+    Q = g.standard_normal((B, D), dtype=np.float32)
+    inv = g.integers(1, X + 1, (B, N0)).astype(np.int64)
+    ids = np.arange(1, X + 1, dtype=np.int64)
+    topk_oracle.mips_topk(Q[:4], E[:1000], ids[:1000], inv[:4], min(k, 100))  # warm/build
+    n, t0 = 0, time.perf_counter()
+    while True:
+        topk_oracle.mips_topk(Q, E, ids, inv, k)
+        n += 1
+        if time.perf_counter() - t0 > budget_s / 2 or n >= 10:
+            break
+    dt = (time.perf_counter() - t0) / n
+    return B * X / dt, n, dt
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--seq", type=int, default=200)
+    ap.add_argument("--out-len", type=int, default=11)
+    ap.add_argument("--dim", type=int, default=50)
+    ap.add_argument("--blocks", type=int, default=4)
+    ap.add_argument("--catalog", type=int, default=3953)
+    ap.add_argument("--k", type=int, default=200)
+    ap.add_argument("--retrieval-items", type=int, default=10_000_000)
+    ap.add_argument("--retrieval-steps", type=int, default=20)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-retrieval-leg", action="store_true")
+    args = ap.parse_args()
+
+    from mygenerativerecommenders_amd import _lib
+    from mygenerativerecommenders_amd.candidate_index import CandidateIndex
+    from mygenerativerecommenders_amd.distributed import (FlatGradAllReducer,
+                                                          ShardedCandidateIndex,
+                                                          init_from_env, shard_bounds)
+    from mygenerativerecommenders_amd.ops import get_current_embeddings
+    from mygenerativerecommenders_amd.top_k import MIPSBruteForceTopK
+
+    rank, world, local = init_from_env()
+    if world != args.gpus and rank == 0:
+        print(f"# note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", flush=True)
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    _lib.lib()
+
+    B, N0, out_len, D, blocks = args.batch, args.seq, args.out_len, args.dim, args.blocks
+    N = N0 + out_len
+    enc = build_model(N0, out_len, D, blocks, device)
+    reducer = FlatGradAllReducer(list(enc.parameters()))
+    opt = torch.optim.AdamW(enc.parameters(), lr=1e-3, betas=(0.9, 0.98), weight_decay=1e-3)
+    lengths, x, ts, past_ids, dy = make_batch(B, N0, out_len, D, 1000 + rank, device)
+    x.requires_grad_(True)
+    # ml-1m catalog (ids 1..3953, L2-normalised rows as Retrieval.on_validation_epoch_start)
+    gen = torch.Generator().manual_seed(7)
+    item_emb = torch.randn(args.catalog, D, generator=gen)
+    item_emb = (item_emb / item_emb.norm(dim=-1, keepdim=True).clamp_min(1e-6)).to(device)
+    index = CandidateIndex(k=args.k, ids=torch.arange(1, args.catalog + 1),
+                           top_k_module=MIPSBruteForceTopK(),
+                           embeddings=item_emb.unsqueeze(0)).to(device)
+
+    def step():
+        y, _ = enc(past_lengths=lengths, user_embeddings=x, valid_mask=None,
+                   past_payloads={"timestamps": ts}, max_len=N0)
+        y.backward(dy)
+        reducer.allreduce(world)
+        opt.step()
+        reducer.zero_grad()
+        x.grad = None
+        with torch.no_grad():
+            q = get_current_embeddings(lengths, y.detach())
+            q = q / q.norm(dim=-1, keepdim=True).clamp_min(1e-6)
+            ids, scores = index.get_top_k_outputs(q, invalid_ids=past_ids)
+        return ids
+
+    for _ in range(args.warmup):
+        step()
+    _sync_barrier(world)
+    timed = ("hstu_attn_fwd", "hstu_attn_bwd", "hstu_ln_uvqk_fwd", "hstu_gate_o_fwd",
+             "hstu_gate_o_bwd", "hstu_ln_uvqk_bwd", "gr_wgrad", "mips_topk")
+    for n in timed:
+        _lib.TIMED[n] = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    _sync_barrier(world)
+    dt = time.perf_counter() - t0
+    kern = {n: sum(a.elapsed_time(b) for a, b in _lib.TIMED[n]) / max(1, len(_lib.TIMED[n]))
+            for n in timed}
+    kern_total = {n: sum(a.elapsed_time(b) for a, b in _lib.TIMED[n]) / args.steps for n in timed}
+    _lib.TIMED.clear()
+    dt = _max_over_ranks(dt, world)
+    ms_per_step = dt / args.steps * 1e3
+    seq_per_s = B * world * args.steps / dt
+
+    # ---- roofline of the dominant kernel (largest per-step device time)
+    peaks = peak_table()
+    fwd_f, dkv_f, dq_f = attn_flops(lengths.cpu(), 1, D, D, blocks)
+    dominant = max(kern_total, key=kern_total.get)
+    flops_per_launch = {"hstu_attn_fwd": fwd_f, "hstu_attn_bwd": dkv_f + dq_f}
+    rows = B * N0
+    nout = 4 * D
+    gemm = {
+        "hstu_ln_uvqk_fwd": 2.0 * rows * D * nout,
+        "hstu_gate_o_fwd": 2.0 * rows * D * D,
+        "hstu_gate_o_bwd": 2.0 * rows * D * D,
+        "hstu_ln_uvqk_bwd": 2.0 * rows * nout * D,
+        "gr_wgrad": (2.0 * rows * D * D + 2.0 * rows * D * nout) / 2.0,  # avg of the two launches
+    }
+    flops_per_launch.update(gemm)
+    ach = flops_per_launch.get(dominant, 0.0) / (kern[dominant] * 1e-3) / 1e12 if kern[dominant] else 0.0
+    roofline = {"kernel": dominant, "bound": "mfma", "achieved": round(ach, 3),
+                "peak": peaks["fp32_mfma_tflops"], "unit": "TFLOP/s",
+                "frac": round(ach / peaks["fp32_mfma_tflops"], 4), "traffic": None,
+                "avg_launch_ms": round(kern[dominant], 5),
+                "flops_per_launch": flops_per_launch.get(dominant, 0.0),
+                "per_step_device_ms": {k: round(v, 4) for k, v in kern_total.items()}}
+
+    # ---- retrieval leg (C4): 10M items row-sharded over the ranks
+    retrieval = None
+    if not args.no_retrieval_leg:
+        X = args.retrieval_items
+        a, b = shard_bounds(X, world, rank)
+        g2 = torch.Generator(device=device)
+        g2.manual_seed(100 + rank)
+        shard = torch.randn(b - a, D, device=device, generator=g2)
+        shard = shard / shard.norm(dim=-1, keepdim=True).clamp_min(1e-6)
+        ids_shard = torch.arange(a + 1, b + 1, device=device)
+        g3 = torch.Generator(device=device)
+        g3.manual_seed(5)  # identical queries on every rank
+        Q = torch.randn(B, D, device=device, generator=g3)
+        Q = Q / Q.norm(dim=-1, keepdim=True)
+        inv = torch.randint(1, X + 1, (B, N), device=device, generator=g3)
+        sidx = ShardedCandidateIndex(args.k, ids_shard, shard, a)
+        del shard
+        for _ in range(3):
+            sidx.get_top_k_outputs(Q, invalid_ids=inv)
+        _sync_barrier(world)
+        _lib.TIMED["mips_topk"] = []
+        t1 = time.perf_counter()
+        for _ in range(args.retrieval_steps):
+            sidx.get_top_k_outputs(Q, invalid_ids=inv)
+        _sync_barrier(world)
+        dtr = time.perf_counter() - t1
+        ktop = sum(a_.elapsed_time(b_) for a_, b_ in _lib.TIMED["mips_topk"]) / max(1, len(_lib.TIMED["mips_topk"]))
+        _lib.TIMED.clear()
+        dtr = _max_over_ranks(dtr, world)
+        cand_per_s = B * X * args.retrieval_steps / dtr
+        fl = 2.0 * B * (b - a) * D
+        ach_r = fl / (ktop * 1e-3) / 1e12 if ktop else 0.0
+        retrieval = {
+            "metric": "top-k items scored/s", "value": cand_per_s, "unit": "items/s",
+            "scaling": "strong", "ms_per_query_batch": dtr / args.retrieval_steps * 1e3,
+            "config": {"workload": "C4: 10M-item catalog row-sharded, B=128 queries, k=200, "
+                                   "211 invalid ids, all-gather + device merge",
+                       "items": X, "queries": B, "k": args.k, "dim": D},
+            "roofline": {"kernel": "mips_topk (select + merge launches)", "bound": "mfma",
+                         "achieved": round(ach_r, 3), "peak": peaks["fp32_mfma_tflops"],
+                         "unit": "TFLOP/s", "frac": round(ach_r / peaks["fp32_mfma_tflops"], 4),
+                         "traffic": None, "avg_launch_ms": round(ktop, 4),
+                         "flops_per_launch": fl},
+        }
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = torch.get_num_threads()
+        sps, n_it, dt_it = cpu_baseline_hstu(16, N0, out_len, D, blocks)
+        cps, n_r, dt_r = cpu_baseline_topk(B, 200_000, D, args.k, N)
+        cpu = {"value": round(sps, 2), "unit": "seq/s", "cores": threads, "kind": "port",
+               "sample": f"oracle padded-order fp32 HSTU fwd+bwd, 16 seqs x {N0} tokens, "
+                         f"{blocks} blocks, {n_it} iters ({dt_it * 1e3:.0f} ms/iter)",
+               "retrieval": {"value": round(cps, 1), "unit": "items/s", "cores": threads,
+                             "kind": "port",
+                             "sample": f"C oracle (fmaf chain, OpenMP) B={B} X=200000 k={args.k}"
+                                       f" N0={N}, {n_r} iters"}}
+
+    if rank == 0:
+        out = {
+            "metric": "HSTU seq/s (fwd+bwd) + top-k items scored/s, ml-1m shapes, 1/2/4/8 MI355X",
+            "value": round(seq_per_s, 2),
+            "unit": "seq/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (random-init weights, synthetic ml-1m-shaped sequences)",
+            "config": {"workload": "ml-1m-hstu train step: HSTU 4 blocks d=50 h=1 fwd+bwd "
+                                   "(+grad all-reduce, AdamW) + top-200 retrieval over 3953 items",
+                       "global_batch": B * world, "seq_len": N0, "padded_len": N,
+                       "parallelism": f"dp{world}"},
+            "roofline": roofline,
+            "retrieval": retrieval,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

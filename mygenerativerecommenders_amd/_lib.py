@@ -84,10 +84,26 @@ class GrError(RuntimeError):
     pass
 
 
+# Optional live per-entry-point timing (bench.py): name -> list of (start, end) events
+# recorded on torch's current stream, which is the stream every entry point is
+# launched on.
+TIMED: dict = {}
+
+
 def call(name: str, *args):
     """Calls a C-ABI entry point; raises GrError(gr_last_error()) on non-zero status."""
     L = lib()
-    rc = getattr(L, name)(*args)
+    rec = TIMED.get(name)
+    if rec is not None:
+        import torch as _t
+        e0 = _t.cuda.Event(enable_timing=True)
+        e1 = _t.cuda.Event(enable_timing=True)
+        e0.record()
+        rc = getattr(L, name)(*args)
+        e1.record()
+        rec.append((e0, e1))
+    else:
+        rc = getattr(L, name)(*args)
     if rc != 0:
         msg = L.gr_last_error().decode(errors="replace")
         raise GrError(f"{name} failed (status {rc}): {msg}")
