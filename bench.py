@@ -153,6 +153,7 @@ def main():
     ap.add_argument("--retrieval-steps", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-retrieval-leg", action="store_true")
+    ap.add_argument("--eager", action="store_true", help="no HIP-graph capture of the step")
     args = ap.parse_args()
 
     from mygenerativerecommenders_amd import _lib
@@ -174,7 +175,8 @@ def main():
     N = N0 + out_len
     enc = build_model(N0, out_len, D, blocks, device)
     reducer = FlatGradAllReducer(list(enc.parameters()))
-    opt = torch.optim.AdamW(enc.parameters(), lr=1e-3, betas=(0.9, 0.98), weight_decay=1e-3)
+    opt = torch.optim.AdamW(enc.parameters(), lr=1e-3, betas=(0.9, 0.98), weight_decay=1e-3,
+                            capturable=True)
     lengths, x, ts, past_ids, dy = make_batch(B, N0, out_len, D, 1000 + rank, device)
     x.requires_grad_(True)
     # ml-1m catalog (ids 1..3953, L2-normalised rows as Retrieval.on_validation_epoch_start)
@@ -185,39 +187,81 @@ def main():
                            top_k_module=MIPSBruteForceTopK(),
                            embeddings=item_emb.unsqueeze(0)).to(device)
 
-    def step():
+    def fwd_bwd():
         y, _ = enc(past_lengths=lengths, user_embeddings=x, valid_mask=None,
                    past_payloads={"timestamps": ts}, max_len=N0)
         y.backward(dy)
-        reducer.allreduce(world)
+        return y
+
+    def opt_and_retrieve(y):
         opt.step()
-        reducer.zero_grad()
-        x.grad = None
         with torch.no_grad():
             q = get_current_embeddings(lengths, y.detach())
             q = q / q.norm(dim=-1, keepdim=True).clamp_min(1e-6)
             ids, scores = index.get_top_k_outputs(q, invalid_ids=past_ids)
         return ids
 
+    def eager_step():
+        reducer.zero_grad()
+        x.grad = None
+        y = fwd_bwd()
+        reducer.allreduce(world)
+        return opt_and_retrieve(y)
+
+    if hasattr(torch.autograd.graph, "set_warn_on_accumulate_grad_stream_mismatch"):
+        # x.grad's AccumulateGrad node was created on the warm-up stream; harmless
+        torch.autograd.graph.set_warn_on_accumulate_grad_stream_mismatch(False)
+    # warm-up (eager, on a side stream as graph capture requires), then capture the
+    # step as two HIP graphs around the RCCL all-reduce: [fwd + bwd] -> all-reduce ->
+    # [AdamW + retrieval].  Replays run the same kernels with no host launch gaps.
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(max(3, args.warmup)):
+            eager_step()
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    if args.eager:
+        step = eager_step
+    else:
+        reducer.zero_grad()
+        x.grad = None
+        g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g_fb):
+            y_static = fwd_bwd()
+        with torch.cuda.graph(g_opt):
+            opt_and_retrieve(y_static)
+
+        def step():
+            g_fb.replay()
+            reducer.allreduce(world, inplace=True)
+            g_opt.replay()
+
     for _ in range(args.warmup):
         step()
     _sync_barrier(world)
-    timed = ("hstu_attn_fwd", "hstu_attn_bwd", "hstu_ln_uvqk_fwd", "hstu_gate_o_fwd",
-             "hstu_gate_o_bwd", "hstu_ln_uvqk_bwd", "gr_wgrad", "mips_topk")
-    for n in timed:
-        _lib.TIMED[n] = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     _sync_barrier(world)
     dt = time.perf_counter() - t0
+    dt = _max_over_ranks(dt, world)
+    ms_per_step = dt / args.steps * 1e3
+    seq_per_s = B * world * args.steps / dt
+
+    # per-kernel device time: HIP events around every C-ABI launch over an eager re-run
+    # of the same K steps (kernel bodies are identical to the replayed graph's)
+    timed = ("hstu_bucket_map", "hstu_attn_fwd", "hstu_attn_bwd", "hstu_ln_uvqk_fwd",
+             "hstu_gate_o_fwd", "hstu_gate_o_bwd", "hstu_ln_uvqk_bwd", "gr_wgrad", "mips_topk")
+    for n in timed:
+        _lib.TIMED[n] = []
+    for _ in range(args.steps):
+        eager_step()
+    _sync_barrier(world)
     kern = {n: sum(a.elapsed_time(b) for a, b in _lib.TIMED[n]) / max(1, len(_lib.TIMED[n]))
             for n in timed}
     kern_total = {n: sum(a.elapsed_time(b) for a, b in _lib.TIMED[n]) / args.steps for n in timed}
     _lib.TIMED.clear()
-    dt = _max_over_ranks(dt, world)
-    ms_per_step = dt / args.steps * 1e3
-    seq_per_s = B * world * args.steps / dt
 
     # ---- roofline of the dominant kernel (largest per-step device time)
     peaks = peak_table()
@@ -316,6 +360,7 @@ def main():
             "data": "synthetic (random-init weights, synthetic ml-1m-shaped sequences)",
             "config": {"workload": "ml-1m-hstu train step: HSTU 4 blocks d=50 h=1 fwd+bwd "
                                    "(+grad all-reduce, AdamW) + top-200 retrieval over 3953 items",
+                       "execution": "eager" if args.eager else "hip-graph replay (2 graphs around the all-reduce)",
                        "global_batch": B * world, "seq_len": N0, "padded_len": N,
                        "parallelism": f"dp{world}"},
             "roofline": roofline,

@@ -54,23 +54,34 @@ GR_API int gr_jagged_to_padded(const float* jagged, const int64_t* offsets, int 
                         float* dense, void* stream);
 
 /* ---------------------------------------------------------------- HSTU attention
- * Replaces sequential_encoders/hstu.py:134-205 (_hstu_attention_maybe_from_cache,
- * non-cache branch) fused with the relative bias of hstu.py:96-128
- * (RelativeBucketedTimeAndPositionBasedBias.forward):
+ * hstu_bucket_map: the relative-time bucket of every causal (query i, key j) pair of
+ * every sequence, computed ONCE per batch and shared by all layers' attention forward
+ * and backward (reference hstu.py:111-123 rebuilds an int64 (B, N, N) tensor per
+ * layer).  bucket(i, j) = max{b : bucket_thr[b] <= |ts_next(i) - ts(j)|},
+ * ts_next(i) = ts[b, i + 1] (ts[b, N - 1] for i = N - 1), hstu.py:113-119;
+ * bucket_thr: (num_buckets + 1) int64 thresholds of the reference bucket function
+ * (hstu.py:579-581), num_buckets < 256.  ts: (B, N) int64.  `map` needs
+ * hstu_bucket_map_bytes(B, N) bytes (uint8, two tile orientations).
+ */
+GR_API size_t hstu_bucket_map_bytes(int B, int N);
+GR_API int hstu_bucket_map(const int64_t* ts, const int64_t* offsets, int B, int N,
+                    const int64_t* bucket_thr, int num_buckets, uint8_t* map, void* stream);
+
+/* hstu_attn_fwd — replaces sequential_encoders/hstu.py:134-205
+ * (_hstu_attention_maybe_from_cache, non-cache branch) fused with the relative bias of
+ * hstu.py:96-128 (RelativeBucketedTimeAndPositionBasedBias.forward):
  *   out[i, h, :] = sum_{j <= i < L_b} silu(q_i,h . k_j,h + pos_w[N-1+j-i]
- *                                          + ts_w[bucket(ts_next(i) - ts(j))]) / N * v_j,h
+ *                                          + ts_w[bucket(i, j)]) / N * v_j,h
  * q/k rows: (total, H*dqk) with row stride ld_qk; v rows: (total, H*dv), stride ld_v;
- * out: (total, H*dv), stride ld_out.  ts: (B, N) int64 timestamps or NULL (then NO
- * bias at all, hstu.py:191).  bucket_thr: (num_buckets + 1) int64 thresholds,
- * bucket(dt) = max{b : bucket_thr[b] <= |dt|}.  max_len: host upper bound on the
- * sequence lengths (<= N), sizes the grid.  fp32 in / fp32 out, f32 MFMA.
- * Supports dqk, dv <= 128.
+ * out: (total, H*dv), stride ld_out.  bucket_map: from hstu_bucket_map, or NULL for
+ * NO bias at all (no timestamps, hstu.py:191).  max_len: host upper bound on the
+ * sequence lengths (<= N), sizes the grid.  fp32 in / out, f32 MFMA.  dqk, dv <= 128.
  */
 GR_API int hstu_attn_fwd(const float* q, const float* k, const float* v, int64_t ld_qk,
                   int64_t ld_v, const int64_t* offsets, int B, int N, int max_len, int H,
-                  int dqk, int dv, const int64_t* ts, const float* pos_w,
-                  const float* ts_w, const int64_t* bucket_thr, int num_buckets,
-                  float* out, int64_t ld_out, void* stream);
+                  int dqk, int dv, const uint8_t* bucket_map, const float* pos_w,
+                  const float* ts_w, int num_buckets, float* out, int64_t ld_out,
+                  void* stream);
 
 /* Backward of hstu_attn_fwd (replaces the autograd backward of hstu.py:134-205 and of
  * the bias module hstu.py:96-128, including the index_add_ into _ts_w and the
@@ -79,15 +90,15 @@ GR_API int hstu_attn_fwd(const float* q, const float* k, const float* v, int64_t
  * hq/hk/hv: optional UVQK pre-activation columns (stride ld_h); when given the
  * outputs are multiplied by silu'(h) (hstu.py:303-305), i.e. they are gradients of
  * the pre-activation.  dpos_w (2N-1) and dts_w (num_buckets+1) are OVERWRITTEN
- * with this call's bias gradients (summed over heads) when ts != NULL.
- * Deterministic: no global atomics; the workspace (size below, only needed when
- * ts != NULL) holds one partial slab per workgroup, reduced in a fixed order.
+ * with this call's bias gradients (summed over heads) when bucket_map != NULL.
+ * Deterministic: no global atomics; the workspace (size below, only needed with a
+ * bucket map) holds one partial slab per workgroup, reduced in a fixed order.
  */
 GR_API size_t hstu_attn_bwd_workspace_size(int B, int N, int max_len, int H, int num_buckets);
 GR_API int hstu_attn_bwd(const float* q, const float* k, const float* v, int64_t ld_qk,
                   int64_t ld_v, const float* dout, int64_t ld_dout, const int64_t* offsets,
-                  int B, int N, int max_len, int H, int dqk, int dv, const int64_t* ts,
-                  const float* pos_w, const float* ts_w, const int64_t* bucket_thr,
+                  int B, int N, int max_len, int H, int dqk, int dv,
+                  const uint8_t* bucket_map, const float* pos_w, const float* ts_w,
                   int num_buckets, const float* hq, const float* hk, const float* hv,
                   int64_t ld_h, float* dq, float* dk, float* dv_out, int64_t ld_d,
                   float* dpos_w, float* dts_w, void* workspace, size_t ws_bytes,
@@ -110,7 +121,9 @@ GR_API int hstu_ln_uvqk_fwd(const float* x, int64_t ld_x, const int64_t* offsets
 
 /* hstu_gate_o_fwd  (replaces hstu.py:393-413 with concat_ua = False):
  *   attn_stats[m] = (mean, rstd) of attn[m, :hdv]
- *   o_in = dropout_p(u * LN(attn))  (mask = counter hash of (seed, m*hdv + k))
+ *   o_in = dropout_p(u * LN(attn))  (mask = counter hash of (seed', m*hdv + k), with
+ *   seed' = seed + *seed_offset when seed_offset (a device int64) is given: a graph
+ *   replay then draws a fresh mask by bumping the device counter)
  *   y = o_in @ w_o^T + b_o + x_res   (w_o: (D, hdv) row-major = nn.Linear.weight)
  *   o_in (optional, contiguous (rows, hdv)) is stored for the weight gradient.
  *   b_o and x_res may be NULL.
@@ -118,8 +131,8 @@ GR_API int hstu_ln_uvqk_fwd(const float* x, int64_t ld_x, const int64_t* offsets
 GR_API int hstu_gate_o_fwd(const float* u, int64_t ld_u, const float* attn, int64_t ld_attn,
                     const int64_t* offsets, int B, int64_t max_rows, int hdv, int D,
                     const float* w_o, const float* b_o, const float* x_res, int64_t ld_x,
-                    float eps, float dropout_p, uint64_t seed, float* attn_stats,
-                    float* o_in, float* y, int64_t ld_y, void* stream);
+                    float eps, float dropout_p, uint64_t seed, const int64_t* seed_offset,
+                    float* attn_stats, float* o_in, float* y, int64_t ld_y, void* stream);
 
 /* hstu_gate_o_bwd  (backward of hstu_gate_o_fwd w.r.t. u and attn; hdv <= 256):
  *   g = (dy @ w_o) * dropout mask;  du = g * LN(attn) [* silu'(h_u) if h_u];
@@ -129,8 +142,8 @@ GR_API int hstu_gate_o_bwd(const float* dy, int64_t ld_dy, const int64_t* offset
                     int64_t max_rows, int hdv, int D, const float* w_o, const float* u,
                     int64_t ld_u, const float* attn, int64_t ld_attn,
                     const float* attn_stats, const float* h_u, int64_t ld_h,
-                    float dropout_p, uint64_t seed, float* du, int64_t ld_du,
-                    float* d_attn, int64_t ld_da, void* stream);
+                    float dropout_p, uint64_t seed, const int64_t* seed_offset, float* du,
+                    int64_t ld_du, float* d_attn, int64_t ld_da, void* stream);
 
 /* hstu_ln_uvqk_bwd  (backward of hstu_ln_uvqk_fwd w.r.t. x, plus the residual; D <= 256):
  *   dn = dh @ w_uvqk^T;  dx = dy_res + LayerNorm_backward(x; dn)   (dy_res may be NULL;

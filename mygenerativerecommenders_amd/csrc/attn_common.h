@@ -1,0 +1,50 @@
+// Shared pieces of the jagged HSTU attention kernels (forward and backward).
+#pragma once
+
+#include "common.h"
+
+namespace gr {
+
+__host__ __device__ inline int attn_tiles_per_seq(int N) {
+  const int T = (N + 63) / 64;
+  return T * (T + 1) / 2;
+}
+__host__ __device__ inline int attn_tile_id(int qt, int kt) { return qt * (qt + 1) / 2 + kt; }
+
+// Register-staged 64-row tile of a jagged column block: rows [r0, r0 + 64) of a
+// (rows, ld) matrix, columns [c0, c0 + ncols) zero-padded to CP, rows >= L zero.
+// Loads are unconditional (clamped) and issued together; store() writes LDS.
+template <int CP>
+struct TileStage {
+  static constexpr int PER = (64 * CP + 255) / 256;
+  float v[PER];
+  __device__ __forceinline__ void load(const float* base, int64_t ld, int64_t s0, int r0, int L,
+                                       int c0, int ncols) {
+    gptr<float> g = as_global(base);
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int e = tid + 256 * i;
+      const int r = e / CP, c = e - (e / CP) * CP;
+      const int row = r0 + r;
+      const bool ok = e < 64 * CP && row < L && c < ncols;
+      const int rc = row < L ? row : L - 1;
+      const int cc = c < ncols ? c : ncols - 1;
+      const float x = g[(s0 + rc) * ld + c0 + cc];
+      v[i] = ok ? x : 0.f;
+    }
+  }
+  __device__ __forceinline__ void store(float* lds, int ldl) const {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int e = tid + 256 * i;
+      if (e < 64 * CP) {
+        const int r = e / CP, c = e - (e / CP) * CP;
+        lds[r * ldl + c] = v[i];
+      }
+    }
+  }
+};
+
+}  // namespace gr

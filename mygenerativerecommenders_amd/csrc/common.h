@@ -77,6 +77,29 @@ __device__ __forceinline__ float sum16(float v) {
   return v;
 }
 
+// Global-address-space view of a pointer: keeps hipcc on global_load (counted by
+// vmcnt alone) where address-space inference fails (pointers through structs /
+// lambdas), instead of flat_load (which forces vmcnt(0) + lgkmcnt(0) waits).
+template <class T>
+using gptr = const T __attribute__((address_space(1)))*;
+template <class T>
+__device__ __forceinline__ gptr<T> as_global(const T* p) {
+  return (gptr<T>)p;
+}
+
+__device__ __forceinline__ float2 ld_f2(const float2* p, int64_t i) {
+  typedef float fv2_ __attribute__((ext_vector_type(2)));
+  const fv2_ v = as_global(reinterpret_cast<const fv2_*>(p))[i];
+  return make_float2(v.x, v.y);
+}
+
+// Workgroup barrier that orders LDS only: waits for this wave's LDS operations and
+// meets the other waves, but leaves global loads in flight (a __syncthreads() lowers to
+// s_waitcnt vmcnt(0) as well, which drains register prefetches).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 __host__ __device__ inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
 
 // relative-time bucket: max{b : thr[b] <= |dt|}, thr = integer threshold table of the

@@ -2,18 +2,20 @@
 //
 // Replaces reference sequential_encoders/hstu.py:134-205 (pad q/k/v, bmm QK^T, + bias,
 // silu / N, causal mask, bmm AV, unpad) and the (B, N, N) bias materialisation of
-// hstu.py:96-128.  Nothing N x N is ever written: the bias is rebuilt per tile from
-// timestamps (int64 deltas -> integer threshold table) and pos_w held in LDS.
+// hstu.py:96-128.  Nothing N x N is written per layer: the bias is rebuilt per tile
+// from pos_w / ts_w (LDS) and the per-batch uint8 bucket map (hstu_bucket_map).
 //
 // Work decomposition: one workgroup = 4 waves = 64 queries of one (sequence, head);
 // wave w owns queries q0+16w .. q0+16w+15.  The workgroup walks key tiles of 64
-// (causal: tiles 0..qt) staged in LDS.  Per 16-key block a wave computes
+// (causal: tiles 0..qt) through LDS; tile kt+1 is loaded into registers while tile kt
+// is computed (LDS-only barriers keep the prefetch in flight).  Per 16-key block a
+// wave computes
 //   S^T (16 keys x 16 queries) = K_blk . Q^T  (A = K rows from LDS, B = Q^T in VGPRs)
 // so each lane holds 4 keys of ONE query; those 4 values are directly the A operand
 // of the next product  O += P . V  with the key order permuted per k-step
 // (k-step r uses keys 4g + r, g = lane>>4) — no LDS round trip for P.
 // Blocks are issued heaviest-first (largest query tile first) for causal balance.
-#include "common.h"
+#include "attn_common.h"
 
 #include "../../include/gr_hstu.h"
 
@@ -26,10 +28,9 @@ struct AttnFwdArgs {
   int64_t ld_qk, ld_v;
   const int64_t* offsets;
   int B, N, H, dqk, dv, n_qtiles;
-  const int64_t* ts;
+  const uint8_t* map_qk;  // null: no bias
   const float* pos_w;
   const float* ts_w;
-  const int64_t* thr;
   int nb;
   float* out;
   int64_t ld_out;
@@ -51,10 +52,8 @@ __global__ __launch_bounds__(256) void hstu_attn_fwd_kernel(AttnFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* Ks = reinterpret_cast<float*>(smem);
   float* Vs = Ks + 64 * C::LDK;
-  int64_t* tsk = reinterpret_cast<int64_t*>(Vs + 64 * C::LDV);  // 64 key timestamps
-  int64_t* thr = tsk + 64;                                       // nb + 1
-  float* tsw = reinterpret_cast<float*>(thr + (a.nb + 1));        // nb + 1
-  float* posw = tsw + (a.nb + 1);                                // 2N - 1
+  float* tsw = Vs + 64 * C::LDV;   // nb + 1
+  float* posw = tsw + (a.nb + 1);  // 2N - 1
 
   const int BH = a.B * a.H;
   const int id = blockIdx.x;
@@ -68,13 +67,10 @@ __global__ __launch_bounds__(256) void hstu_attn_fwd_kernel(AttnFwdArgs a) {
 
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int lr = lane & 15, lg = lane >> 4;
-  const bool has_bias = a.ts != nullptr;
+  const bool has_bias = a.map_qk != nullptr;
 
   if (has_bias) {
-    for (int i = tid; i <= a.nb; i += 256) {
-      thr[i] = a.thr[i];
-      tsw[i] = a.ts_w[i];
-    }
+    for (int i = tid; i <= a.nb; i += 256) tsw[i] = a.ts_w[i];
     for (int i = tid; i < 2 * a.N - 1; i += 256) posw[i] = a.pos_w[i];
   }
 
@@ -83,48 +79,44 @@ __global__ __launch_bounds__(256) void hstu_attn_fwd_kernel(AttnFwdArgs a) {
   const bool q_ok = qi < L;
   float qreg[KSTEPS];
   {
-    const float* qrow = a.q + (s0 + (q_ok ? qi : 0)) * a.ld_qk + h * a.dqk;
+    gptr<float> qrow = as_global(a.q) + (s0 + (q_ok ? qi : L - 1)) * a.ld_qk + h * a.dqk;
 #pragma unroll
     for (int st = 0; st < KSTEPS; ++st) {
       const int d = 4 * st + lg;
-      qreg[st] = (q_ok && d < a.dqk) ? qrow[d] : 0.f;
+      const float x = qrow[d < a.dqk ? d : a.dqk - 1];
+      qreg[st] = d < a.dqk ? x : 0.f;
     }
   }
-  int64_t ts_next = 0;
-  if (has_bias && q_ok) {
-    const int nx = qi + 1 < a.N ? qi + 1 : a.N - 1;  // ext_ts[N] = ts[N-1] (hstu.py:113-115)
-    ts_next = a.ts[(int64_t)b * a.N + nx];
-  }
+  const int tpb = attn_tiles_per_seq(a.N);
+  gptr<uint32_t> mapw = as_global(reinterpret_cast<const uint32_t*>(a.map_qk ? a.map_qk : (const uint8_t*)a.q));
+  const int64_t map_seq = (int64_t)b * tpb * 1024;                 // dwords
+  const int map_lane = (w * 16 + lr) * 16 + lg;                     // + kb * 4
 
   f4 acc[VTILES];
 #pragma unroll
   for (int ct = 0; ct < VTILES; ++ct) acc[ct] = f4_zero();
 
+  TileStage<C::KP> kst;
+  TileStage<C::VP> vst;
+  uint32_t mw[4], mwn[4];
+  auto load_tile = [&](int kt, uint32_t (&m)[4]) {
+    kst.load(a.k, a.ld_qk, s0, kt * 64, L, h * a.dqk, a.dqk);
+    vst.load(a.v, a.ld_v, s0, kt * 64, L, h * a.dv, a.dv);
+    const int64_t tb = map_seq + (int64_t)attn_tile_id(qt, kt) * 1024 + map_lane;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) m[kb] = has_bias ? mapw[tb + kb * 4] : 0u;
+  };
+
+  load_tile(0, mw);
+  kst.store(Ks, C::LDK);
+  vst.store(Vs, C::LDV);
+  __syncthreads();  // also publishes tsw / posw
+
   const int wq_lo = q0 + w * 16;  // first query of this wave
   for (int kt = 0; kt <= qt; ++kt) {
     const int k0 = kt * 64;
-    __syncthreads();
-    // ---- stage K, V tiles (zero-filled past L / past d) and key timestamps
-    for (int e = tid; e < 64 * C::KP; e += 256) {
-      const int r = e / C::KP, c = e - r * C::KP;
-      const int key = k0 + r;
-      float val = 0.f;
-      if (key < L && c < a.dqk) val = a.k[(s0 + key) * a.ld_qk + h * a.dqk + c];
-      Ks[r * C::LDK + c] = val;
-    }
-    for (int e = tid; e < 64 * C::VP; e += 256) {
-      const int r = e / C::VP, c = e - r * C::VP;
-      const int key = k0 + r;
-      float val = 0.f;
-      if (key < L && c < a.dv) val = a.v[(s0 + key) * a.ld_v + h * a.dv + c];
-      Vs[r * C::LDV + c] = val;
-    }
-    if (has_bias && tid < 64) {
-      const int key = k0 + tid;
-      tsk[tid] = key < L ? a.ts[(int64_t)b * a.N + key] : 0;
-    }
-    __syncthreads();
-
+    const bool more = kt < qt;
+    if (more) load_tile(kt + 1, mwn);
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
       const int kb0 = k0 + kb * 16;
@@ -140,10 +132,10 @@ __global__ __launch_bounds__(256) void hstu_attn_fwd_kernel(AttnFwdArgs a) {
         const int kj = kb0 + 4 * lg + r;
         float val = s[r];
         if (has_bias) {
-          const int bucket = time_bucket(ts_next - tsk[kb * 16 + 4 * lg + r], thr, a.nb);
-          const int pi = a.N - 1 + kj - qi;
-          const float bias = posw[pi < 0 ? 0 : (pi > 2 * a.N - 2 ? 2 * a.N - 2 : pi)] + tsw[bucket];
-          val = val + bias;
+          const int bucket = (mw[kb] >> (8 * r)) & 0xFF;
+          int pi = a.N - 1 + kj - qi;
+          pi = pi < 0 ? 0 : (pi > 2 * a.N - 2 ? 2 * a.N - 2 : pi);
+          val = val + (posw[pi] + tsw[bucket]);
         }
         p[r] = (q_ok && kj <= qi) ? siluf_(val) * a.inv_n : 0.f;
       }
@@ -154,6 +146,14 @@ __global__ __launch_bounds__(256) void hstu_attn_fwd_kernel(AttnFwdArgs a) {
         for (int ct = 0; ct < VTILES; ++ct)
           acc[ct] = mfma16x16x4(p[r], vrow[r * C::LDV + ct * 16], acc[ct]);
       }
+    }
+    if (more) {
+      lds_barrier();
+      kst.store(Ks, C::LDK);
+      vst.store(Vs, C::LDV);
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) mw[kb] = mwn[kb];
+      lds_barrier();
     }
   }
 
@@ -171,12 +171,10 @@ __global__ __launch_bounds__(256) void hstu_attn_fwd_kernel(AttnFwdArgs a) {
   }
 }
 
-// (KSTEPS, VTILES) instantiation ladder, chosen by max(dqk, dv) bracket
 template <int KS, int VT>
 static int launch_fwd(const AttnFwdArgs& a, int grid, hipStream_t st) {
   using C = AttnFwdCfg<KS, VT>;
-  size_t lds = sizeof(float) * C::LDS_FLOATS + sizeof(int64_t) * (64 + a.nb + 1) +
-               sizeof(float) * (a.nb + 1 + 2 * a.N - 1);
+  size_t lds = sizeof(float) * (C::LDS_FLOATS + a.nb + 1 + 2 * a.N - 1);
   GR_REQUIRE(lds <= 160 * 1024, "hstu_attn_fwd: LDS %zu B exceeds 160 KiB (N=%d)", lds, a.N);
   hipLaunchKernelGGL((hstu_attn_fwd_kernel<KS, VT>), dim3(grid), dim3(256), lds, st, a);
   GR_LAUNCH_CHECK("hstu_attn_fwd");
@@ -187,19 +185,20 @@ static int launch_fwd(const AttnFwdArgs& a, int grid, hipStream_t st) {
 
 extern "C" int hstu_attn_fwd(const float* q, const float* k, const float* v, int64_t ld_qk,
                              int64_t ld_v, const int64_t* offsets, int B, int N, int max_len,
-                             int H, int dqk, int dv, const int64_t* ts, const float* pos_w,
-                             const float* ts_w, const int64_t* bucket_thr, int num_buckets,
-                             float* out, int64_t ld_out, void* stream) {
+                             int H, int dqk, int dv, const uint8_t* bucket_map,
+                             const float* pos_w, const float* ts_w, int num_buckets, float* out,
+                             int64_t ld_out, void* stream) {
   using namespace gr;
   GR_REQUIRE(q && k && v && offsets && out, "hstu_attn_fwd: null pointer");
   GR_REQUIRE(B >= 0 && N > 0 && H > 0 && dqk > 0 && dv > 0, "hstu_attn_fwd: bad sizes");
   GR_REQUIRE(max_len >= 0 && max_len <= N, "hstu_attn_fwd: max_len %d not in [0, N=%d]", max_len, N);
   GR_REQUIRE(dqk <= 128 && dv <= 128, "hstu_attn_fwd: dqk/dv > 128 unsupported (%d, %d)", dqk, dv);
-  GR_REQUIRE(!ts || (pos_w && ts_w && bucket_thr && num_buckets > 0 && num_buckets < 1024),
-             "hstu_attn_fwd: ts given without pos_w/ts_w/bucket_thr");
+  GR_REQUIRE(!bucket_map || (pos_w && ts_w && num_buckets > 0 && num_buckets < 256),
+             "hstu_attn_fwd: bucket_map given without pos_w/ts_w");
   if (B == 0 || max_len == 0) return 0;
   AttnFwdArgs a{q, k, v, ld_qk, ld_v, offsets, B, N, H, dqk, dv, ceil_div(max_len, 64),
-                ts, pos_w, ts_w, bucket_thr, ts ? num_buckets : 0, out, ld_out, 1.0f / (float)N};
+                bucket_map, pos_w, ts_w, bucket_map ? num_buckets : 0, out, ld_out,
+                1.0f / (float)N};
   const int grid = a.n_qtiles * B * H;
   hipStream_t st = (hipStream_t)stream;
   const int d = dqk > dv ? dqk : dv;

@@ -33,38 +33,62 @@ struct PanelCfg {
   static constexpr int LDB = (NT & 1) ? BN : BN + 16;  // == 16 mod 32
 };
 
-// Row statistics (mean, rstd) of rows [m0, m0+64) over K columns: 4 threads per row,
-// two passes (the second one re-reads through L1/L2).
+// Every global load below is UNCONDITIONAL (indices clamped into the valid range, the
+// value masked afterwards): a guarded load makes hipcc branch around it and wait
+// vmcnt(0) per element, serialising dozens of L2 round trips per tile.
+
+// Row statistics (mean, rstd) of rows [m0, m0+64) over K columns: wave w owns 16 rows,
+// 4 at a time with 16 lanes per row; loads issued 4-deep before the reductions.
 __device__ __forceinline__ void panel_row_stats(const float* base, int64_t ld, int64_t m0,
                                                 int64_t total, int K, float eps,
                                                 float2* st_lds, float2* st_glob) {
-  const int t = threadIdx.x;
-  const int r = t >> 2, sub = t & 3;
-  const int64_t m = m0 + r;
-  float mean = 0.f, rstd = 0.f;
-  if (m < total) {
-    const float* row = base + m * ld;
+  gptr<float> src = as_global(base);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int sub = lane & 15, rq = lane >> 4;
+  const int64_t mlast = total - 1;
+  const float invk = 1.f / (float)K;
+#pragma unroll
+  for (int pass = 0; pass < 4; ++pass) {
+    const int r = w * 16 + pass * 4 + rq;
+    const int64_t m = m0 + r;
+    const int64_t mc = m < mlast ? m : mlast;
+    gptr<float> row = src + mc * ld;
     float s = 0.f;
-    for (int k = sub; k < K; k += 4) s += row[k];
-    s += __shfl_xor(s, 1, 64);
-    s += __shfl_xor(s, 2, 64);
-    mean = s / (float)K;
-    float v = 0.f;
-    for (int k = sub; k < K; k += 4) {
-      const float d = row[k] - mean;
-      v += d * d;
+    for (int k0 = 0; k0 < K; k0 += 64) {
+      float v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = k0 + 16 * u + sub;
+        v[u] = row[k < K ? k : K - 1];
+        v[u] = k < K ? v[u] : 0.f;
+      }
+      s += (v[0] + v[1]) + (v[2] + v[3]);
     }
-    v += __shfl_xor(v, 1, 64);
-    v += __shfl_xor(v, 2, 64);
-    rstd = rsqrtf(v / (float)K + eps);
-  }
-  if (sub == 0) {
-    st_lds[r] = make_float2(mean, rstd);
-    if (st_glob && m < total) st_glob[m] = make_float2(mean, rstd);
+    s = sum16(s);
+    const float mean = s * invk;
+    float q = 0.f;
+    for (int k0 = 0; k0 < K; k0 += 64) {
+      float v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = k0 + 16 * u + sub;
+        v[u] = row[k < K ? k : K - 1] - mean;
+        v[u] = k < K ? v[u] : 0.f;
+      }
+      q += (v[0] * v[0] + v[1] * v[1]) + (v[2] * v[2] + v[3] * v[3]);
+    }
+    q = sum16(q);
+    const float rstd = rsqrtf(q * invk + eps);
+    if (sub == 0) {
+      st_lds[r] = make_float2(mean, rstd);
+      if (st_glob && m < total) st_glob[m] = make_float2(mean, rstd);
+    }
   }
 }
 
 // Generic row-panel GEMM: C[m, n] = sum_k Op::a(m, k) * Op::b(k, n), epilogue by Op.
+// K streams through LDS in chunks of 16 with the next chunk prefetched into registers
+// (LDS-only barriers keep the prefetch in flight across the MFMA phase).
 template <int NT, class Op>
 __global__ __launch_bounds__(256) void rowpanel_kernel(Op op) {
   using P = PanelCfg<NT>;
@@ -77,38 +101,70 @@ __global__ __launch_bounds__(256) void rowpanel_kernel(Op op) {
   const int n0 = blockIdx.y * P::BN;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int lr = lane & 15, lg = lane >> 4;
+  const int64_t mlast = total - 1;
 
   op.prologue(m0, total, stats);
   __syncthreads();
+
+  float ra[4], rb[NT];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = tid + 256 * i;
+      const int r = e >> 4, c = e & 15;
+      const int64_t m = m0 + r;
+      const int k = k0 + c;
+      const bool ok = m < total && k < op.K;
+      const float v = op.a(m < mlast ? m : mlast, k < op.K ? k : op.K - 1, stats[r], ok);
+      ra[i] = ok ? v : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+      const int e = tid + 256 * i;
+      int kk, c;
+      if (Op::B_N_CONTIG) {
+        kk = e / P::BN;
+        c = e - kk * P::BN;
+      } else {
+        c = e >> 4;
+        kk = e & 15;
+      }
+      const int k = k0 + kk, n = n0 + c;
+      const float v = op.b(k < op.K ? k : op.K - 1, n < op.N ? n : op.N - 1);
+      rb[i] = (k < op.K && n < op.N) ? v : 0.f;
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = tid + 256 * i;
+      As[(e >> 4) * LDA + (e & 15)] = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+      const int e = tid + 256 * i;
+      int kk, c;
+      if (Op::B_N_CONTIG) {
+        kk = e / P::BN;
+        c = e - kk * P::BN;
+      } else {
+        c = e >> 4;
+        kk = e & 15;
+      }
+      Bs[kk * P::LDB + c] = rb[i];
+    }
+  };
 
   f4 acc[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = f4_zero();
 
+  load(0);
+  store();
+  lds_barrier();
   for (int k0 = 0; k0 < op.K; k0 += BK) {
-    // ---- stage A (64 x 16) and B (16 x BN)
-#pragma unroll
-    for (int i = 0; i < (BM * BK) / 256; ++i) {
-      const int e = tid + 256 * i;
-      const int r = e >> 4, c = e & 15;
-      const int64_t m = m0 + r;
-      const int k = k0 + c;
-      As[r * LDA + c] = (m < total && k < op.K) ? op.a(m, k, stats[r]) : 0.f;
-    }
-    if (Op::B_N_CONTIG) {
-      for (int e = tid; e < BK * P::BN; e += 256) {
-        const int kk = e / P::BN, c = e - kk * P::BN;
-        const int k = k0 + kk, n = n0 + c;
-        Bs[kk * P::LDB + c] = (k < op.K && n < op.N) ? op.b(k, n) : 0.f;
-      }
-    } else {
-      for (int e = tid; e < BK * P::BN; e += 256) {
-        const int c = e >> 4, kk = e & 15;
-        const int k = k0 + kk, n = n0 + c;
-        Bs[kk * P::LDB + c] = (k < op.K && n < op.N) ? op.b(k, n) : 0.f;
-      }
-    }
-    __syncthreads();
+    const bool more = k0 + BK < op.K;
+    if (more) load(k0 + BK);
     const float* arow = As + (w * 16 + lr) * LDA + lg;
 #pragma unroll
     for (int ks = 0; ks < BK / 4; ++ks) {
@@ -117,10 +173,14 @@ __global__ __launch_bounds__(256) void rowpanel_kernel(Op op) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) acc[t] = mfma16x16x4(av, brow[t * 16], acc[t]);
     }
-    __syncthreads();
+    lds_barrier();
+    if (more) {
+      store();
+      lds_barrier();
+    }
   }
   // acc[t][r] = C[m0 + 16w + 4lg + r][n0 + 16t + lr]
-  op.epilogue(acc, m0 + w * 16 + 4 * lg, n0 + lr, total, stats + w * 16 + 4 * lg);
+  op.epilogue(acc, m0 + w * 16 + 4 * lg, n0 + lr, total);
 }
 
 // ------------------------------------------------------------------ ops
@@ -129,6 +189,10 @@ struct NoStats {
     if (threadIdx.x < BM) st[threadIdx.x] = make_float2(0.f, 1.f);
   }
 };
+
+__device__ __forceinline__ int64_t clamp_row(int64_t m, int64_t total) {
+  return m < total ? m : total - 1;
+}
 
 // F1: uvqk = act(LN(x) @ W), W row-major (D, n_out)
 struct OpLnUvqk {
@@ -147,11 +211,12 @@ struct OpLnUvqk {
   __device__ void prologue(int64_t m0, int64_t total, float2* st) const {
     panel_row_stats(x, ldx, m0, total, K, eps, st, blockIdx.y == 0 ? x_stats : nullptr);
   }
-  __device__ float a(int64_t m, int k, float2 st) const { return (x[m * ldx + k] - st.x) * st.y; }
-  __device__ float b(int k, int n) const { return w[(int64_t)k * N + n]; }
+  __device__ float a(int64_t m, int k, float2 st, bool) const {
+    return (as_global(x)[m * ldx + k] - st.x) * st.y;
+  }
+  __device__ float b(int k, int n) const { return as_global(w)[(int64_t)k * N + n]; }
   template <int NT>
-  __device__ void epilogue(f4 (&acc)[NT], int64_t mrow, int ncol, int64_t total,
-                           const float2*) const {
+  __device__ void epilogue(f4 (&acc)[NT], int64_t mrow, int ncol, int64_t total) const {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int64_t m = mrow + r;
@@ -190,6 +255,7 @@ struct OpGateO {
   int64_t ldx;
   float eps, p;
   uint64_t seed;
+  const int64_t* seed_off;
   float2* a_stats;
   float* o_in;
   float* y;
@@ -197,28 +263,36 @@ struct OpGateO {
   __device__ void prologue(int64_t m0, int64_t total, float2* st) const {
     panel_row_stats(attn, lda, m0, total, K, eps, st, blockIdx.y == 0 ? a_stats : nullptr);
   }
-  __device__ float a(int64_t m, int k, float2 st) const {
-    float v = u[m * ldu + k] * ((attn[m * lda + k] - st.x) * st.y);
-    v *= dropout_keep(seed, m, k, K, p);
-    if (o_in && blockIdx.y == 0) o_in[m * K + k] = v;
+  __device__ float a(int64_t m, int k, float2 st, bool valid) const {
+    float v = as_global(u)[m * ldu + k] * ((as_global(attn)[m * lda + k] - st.x) * st.y);
+    if (p > 0.f) v *= dropout_keep(seed + (seed_off ? (uint64_t)*seed_off : 0ull), m, k, K, p);
+    if (valid && o_in && blockIdx.y == 0) o_in[m * K + k] = v;
     return v;
   }
-  __device__ float b(int k, int n) const { return w[(int64_t)n * K + k]; }
+  __device__ float b(int k, int n) const { return as_global(w)[(int64_t)n * K + k]; }
   template <int NT>
-  __device__ void epilogue(f4 (&acc)[NT], int64_t mrow, int ncol, int64_t total,
-                           const float2*) const {
+  __device__ void epilogue(f4 (&acc)[NT], int64_t mrow, int ncol, int64_t total) const {
+    float bv[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int n = ncol + 16 * t;
+      bv[t] = bias ? as_global(bias)[n < N ? n : N - 1] : 0.f;
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int64_t m = mrow + r;
+      const int64_t mc = clamp_row(m, total);
+      float xv[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int n = ncol + 16 * t;
+        xv[t] = xres ? as_global(xres)[mc * ldx + (n < N ? n : N - 1)] : 0.f;
+      }
       if (m >= total) continue;
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         const int n = ncol + 16 * t;
-        if (n >= N) continue;
-        float v = acc[t][r];
-        if (bias) v = v + bias[n];
-        if (xres) v = v + xres[m * ldx + n];
-        y[m * ldy + n] = v;
+        if (n < N) y[m * ldy + n] = (acc[t][r] + bv[t]) + xv[t];
       }
     }
   }
@@ -242,39 +316,45 @@ struct OpGateOBwd : NoStats {
   int64_t ldh;
   float p;
   uint64_t seed;
+  const int64_t* seed_off;
   float* du;
   int64_t lddu;
   float* da;
   int64_t ldda;
-  __device__ float a(int64_t m, int k, float2) const { return dy[m * lddy + k]; }
-  __device__ float b(int k, int n) const { return w[(int64_t)k * N + n]; }
+  __device__ float a(int64_t m, int k, float2, bool) const { return as_global(dy)[m * lddy + k]; }
+  __device__ float b(int k, int n) const { return as_global(w)[(int64_t)k * N + n]; }
   template <int NT>
-  __device__ void epilogue(f4 (&acc)[NT], int64_t mrow, int ncol, int64_t total,
-                           const float2*) const {
+  __device__ void epilogue(f4 (&acc)[NT], int64_t mrow, int ncol, int64_t total) const {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int64_t m = mrow + r;
       const bool row_ok = m < total;
-      float2 st = row_ok ? a_stats[m] : make_float2(0.f, 0.f);
+      const int64_t mc = clamp_row(m, total);
+      const float2 st = ld_f2(a_stats, mc);
+      float av[NT], uv[NT], hv[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int n = ncol + 16 * t;
+        const int nc = n < N ? n : N - 1;
+        av[t] = as_global(attn)[mc * lda + nc];
+        uv[t] = as_global(u)[mc * ldu + nc];
+        hv[t] = h_u ? as_global(h_u)[mc * ldh + nc] : 0.f;
+      }
       float s1 = 0.f, s2 = 0.f;
       float lnv[NT], dln[NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         const int n = ncol + 16 * t;
-        lnv[t] = 0.f;
-        dln[t] = 0.f;
-        if (row_ok && n < N) {
-          const float g = acc[t][r] * dropout_keep(seed, m, n, N, p);
-          const float ln = (attn[m * lda + n] - st.x) * st.y;
-          const float uu = u[m * ldu + n];
-          float dd = g * ln;
-          if (h_u) dd *= silu_grad_(h_u[m * ldh + n]);
-          du[m * lddu + n] = dd;
-          lnv[t] = ln;
-          dln[t] = g * uu;
-          s1 += dln[t];
-          s2 += dln[t] * ln;
-        }
+        const bool ok = row_ok && n < N;
+        const float g = p > 0.f ? acc[t][r] * dropout_keep(seed + (seed_off ? (uint64_t)*seed_off : 0ull), m, n, N, p) : acc[t][r];
+        const float ln = (av[t] - st.x) * st.y;
+        float dd = g * ln;
+        if (h_u) dd *= silu_grad_(hv[t]);
+        if (ok) du[m * lddu + n] = dd;
+        lnv[t] = ok ? ln : 0.f;
+        dln[t] = ok ? g * uv[t] : 0.f;
+        s1 += dln[t];
+        s2 += dln[t] * lnv[t];
       }
       s1 = sum16(s1);
       s2 = sum16(s2);
@@ -305,27 +385,34 @@ struct OpLnUvqkBwd : NoStats {
   int64_t lddy;
   float* dx;
   int64_t lddx;
-  __device__ float a(int64_t m, int k, float2) const { return dh[m * lddh + k]; }
-  __device__ float b(int k, int n) const { return w[(int64_t)n * K + k]; }
+  __device__ float a(int64_t m, int k, float2, bool) const { return as_global(dh)[m * lddh + k]; }
+  __device__ float b(int k, int n) const { return as_global(w)[(int64_t)n * K + k]; }
   template <int NT>
-  __device__ void epilogue(f4 (&acc)[NT], int64_t mrow, int ncol, int64_t total,
-                           const float2*) const {
+  __device__ void epilogue(f4 (&acc)[NT], int64_t mrow, int ncol, int64_t total) const {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int64_t m = mrow + r;
       const bool row_ok = m < total;
-      float2 st = row_ok ? x_stats[m] : make_float2(0.f, 0.f);
+      const int64_t mc = clamp_row(m, total);
+      const float2 st = ld_f2(x_stats, mc);
+      float xv[NT], dyv[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int n = ncol + 16 * t;
+        const int nc = n < N ? n : N - 1;
+        xv[t] = as_global(x)[mc * ldx + nc];
+        dyv[t] = dy ? as_global(dy)[mc * lddy + nc] : 0.f;
+      }
       float s1 = 0.f, s2 = 0.f;
       float xh[NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         const int n = ncol + 16 * t;
-        xh[t] = 0.f;
-        if (row_ok && n < N) {
-          xh[t] = (x[m * ldx + n] - st.x) * st.y;
-          s1 += acc[t][r];
-          s2 += acc[t][r] * xh[t];
-        }
+        const bool ok = row_ok && n < N;
+        xh[t] = ok ? (xv[t] - st.x) * st.y : 0.f;
+        const float dn = ok ? acc[t][r] : 0.f;
+        s1 += dn;
+        s2 += dn * xh[t];
       }
       s1 = sum16(s1);
       s2 = sum16(s2);
@@ -335,11 +422,7 @@ struct OpLnUvqkBwd : NoStats {
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         const int n = ncol + 16 * t;
-        if (n < N) {
-          float v = st.y * (acc[t][r] - mean1 - xh[t] * mean2);
-          if (dy) v = dy[m * lddy + n] + v;
-          dx[m * lddx + n] = v;
-        }
+        if (n < N) dx[m * lddx + n] = dyv[t] + st.y * (acc[t][r] - mean1 - xh[t] * mean2);
       }
     }
   }
@@ -373,9 +456,11 @@ static int launch_rowpanel(const Op& op, int64_t max_rows, bool full_row, const 
 
 // ------------------------------------------------------------------ weight gradients
 // C[Ka, Nb] = sum_m A'(m, ka) * Bm(m, nb), A' = A or (A - mu_m) * rstd_m.
-// Grid: x = row chunk, y = output panel (64 ka x 256 nb).  Each workgroup writes its
-// partial panel to a slab; wgrad_reduce sums the chunks in order.
-constexpr int WG_KA = 64, WG_NB = 256, WG_LDA = WG_KA + 16, WG_LDB = WG_NB + 16;
+// Grid: x = row chunk, y = output panel (64 ka x NT*16 nb).  Rows stream through LDS in
+// steps of 16 with a register prefetch of the next step (LDS-only barriers keep it in
+// flight).  Each workgroup writes its partial panel to a slab; wgrad_reduce sums the
+// chunks in a fixed order (deterministic, no atomics).
+constexpr int WG_KA = 64, WG_LDA = WG_KA + 16;
 
 struct WgradArgs {
   const float* a;
@@ -391,56 +476,95 @@ struct WgradArgs {
   float* colsums;  // [n_chunks][Ka] or null
 };
 
+template <int NT>
 __global__ __launch_bounds__(256) void wgrad_partial_kernel(WgradArgs g) {
+  constexpr int NBW = NT * 16;
+  constexpr int LDB = (NT & 1) ? NBW : NBW + 16;  // == 16 mod 32
+  constexpr int BPT = (16 * NBW) / 256;            // B elements per thread per step
   __shared__ __attribute__((aligned(16))) float As[BK * WG_LDA];
-  __shared__ __attribute__((aligned(16))) float Bs[BK * WG_LDB];
+  __shared__ __attribute__((aligned(16))) float Bs[BK * LDB];
   const int chunk = blockIdx.x;
   const int pa = blockIdx.y / g.panels_nb, pb = blockIdx.y % g.panels_nb;
-  const int ka0 = pa * WG_KA, nb0 = pb * WG_NB;
+  const int ka0 = pa * WG_KA, nb0 = pb * NBW;
   const int64_t total = g.offsets[g.B];
   const int64_t r0 = (int64_t)chunk * g.rows_per_chunk;
   const int64_t r1 = min(total, r0 + g.rows_per_chunk);
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int lr = lane & 15, lg = lane >> 4;
-  f4 acc[16];
+  gptr<float> A = as_global(g.a);
+  gptr<float> Bg = as_global(g.bm);
+  const int n_it = r1 > r0 ? (int)((r1 - r0 + BK - 1) / BK) : 0;
+  // staging coordinates: A element e = tid + 256 i -> (row e / 64, col e % 64)
+  float ra[4], rb[BPT];
+  auto load = [&](int it) {
+    const int64_t m0 = r0 + (int64_t)it * BK;
 #pragma unroll
-  for (int t = 0; t < 16; ++t) acc[t] = f4_zero();
-  float csum = 0.f;  // thread tid < 64 sums column ka0 + tid
-  for (int64_t m0 = r0; m0 < r1; m0 += BK) {
-    for (int e = tid; e < BK * WG_KA; e += 256) {
-      const int rr = e / WG_KA, c = e - rr * WG_KA;
+    for (int i = 0; i < 4; ++i) {
+      const int e = tid + 256 * i;
+      const int rr = e >> 6, c = e & 63;
       const int64_t m = m0 + rr;
       const int ka = ka0 + c;
-      float v = 0.f;
-      if (m < r1 && ka < g.Ka) {
-        v = g.a[m * g.lda + ka];
-        if (g.a_stats) {
-          const float2 st = g.a_stats[m];
-          v = (v - st.x) * st.y;
-        }
+      const int64_t mc = m < r1 ? m : r0;
+      const int kc = ka < g.Ka ? ka : 0;
+      float v = A[mc * g.lda + kc];
+      if (g.a_stats) {
+        const float2 st = g.a_stats[mc];
+        v = (v - st.x) * st.y;
       }
-      As[rr * WG_LDA + c] = v;
+      ra[i] = (m < r1 && ka < g.Ka) ? v : 0.f;
     }
-    for (int e = tid; e < BK * WG_NB; e += 256) {
-      const int rr = e / WG_NB, c = e - rr * WG_NB;
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) {
+      const int e = tid + 256 * i;
+      const int rr = e / NBW, c = e - rr * NBW;
       const int64_t m = m0 + rr;
       const int nb = nb0 + c;
-      Bs[rr * WG_LDB + c] = (m < r1 && nb < g.Nb) ? g.bm[m * g.ldb + nb] : 0.f;
+      const int64_t mc = m < r1 ? m : r0;
+      const int nc = nb < g.Nb ? nb : 0;
+      const float v = Bg[mc * g.ldb + nc];
+      rb[i] = (m < r1 && nb < g.Nb) ? v : 0.f;
     }
-    __syncthreads();
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = tid + 256 * i;
+      As[(e >> 6) * WG_LDA + (e & 63)] = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) {
+      const int e = tid + 256 * i;
+      const int rr = e / NBW, c = e - rr * NBW;
+      Bs[rr * LDB + c] = rb[i];
+    }
+  };
+  f4 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f4_zero();
+  float csum = 0.f;  // thread tid < 64 sums column ka0 + tid
+  if (n_it > 0) {
+    load(0);
+    store();
+    lds_barrier();
+  }
+  for (int it = 0; it < n_it; ++it) {
+    if (it + 1 < n_it) load(it + 1);
     if (g.colsums && pb == 0 && tid < WG_KA) {
 #pragma unroll
       for (int rr = 0; rr < BK; ++rr) csum += As[rr * WG_LDA + tid];
     }
-    // wave w: output rows ka0 + 16w .. +15, all 16 column tiles
 #pragma unroll
     for (int ks = 0; ks < BK / 4; ++ks) {
       const float av = As[(4 * ks + lg) * WG_LDA + w * 16 + lr];
-      const float* brow = Bs + (4 * ks + lg) * WG_LDB + lr;
+      const float* brow = Bs + (4 * ks + lg) * LDB + lr;
 #pragma unroll
-      for (int t = 0; t < 16; ++t) acc[t] = mfma16x16x4(av, brow[t * 16], acc[t]);
+      for (int t = 0; t < NT; ++t) acc[t] = mfma16x16x4(av, brow[t * 16], acc[t]);
     }
-    __syncthreads();
+    lds_barrier();
+    if (it + 1 < n_it) {
+      store();
+      lds_barrier();
+    }
   }
   float* slab = g.slabs + (int64_t)chunk * g.Ka * g.Nb;
 #pragma unroll
@@ -448,7 +572,7 @@ __global__ __launch_bounds__(256) void wgrad_partial_kernel(WgradArgs g) {
     const int ka = ka0 + w * 16 + 4 * lg + r;
     if (ka >= g.Ka) continue;
 #pragma unroll
-    for (int t = 0; t < 16; ++t) {
+    for (int t = 0; t < NT; ++t) {
       const int nb = nb0 + 16 * t + lr;
       if (nb < g.Nb) slab[(int64_t)ka * g.Nb + nb] = acc[t][r];
     }
@@ -457,23 +581,48 @@ __global__ __launch_bounds__(256) void wgrad_partial_kernel(WgradArgs g) {
     g.colsums[(int64_t)chunk * g.Ka + ka0 + tid] = csum;
 }
 
+// out[i] = sum_c slabs[c][i] in chunk order (4 waves x strided chunks, then wave order)
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* slabs, int n_chunks,
                                                            int64_t n_elem, float* out) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n_elem) return;
-  float s = 0.f;
-  for (int c = 0; c < n_chunks; ++c) s += slabs[(int64_t)c * n_elem + i];
-  out[i] = s;
+  __shared__ float part[4][64];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 64 + lane;
+  gptr<float> src = as_global(slabs);
+  float acc = 0.f;
+  if (i < n_elem) {
+    int c = w;
+    for (; c + 28 < n_chunks; c += 32) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = src[(int64_t)(c + 4 * u) * n_elem + i];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; c < n_chunks; c += 4) acc += src[(int64_t)c * n_elem + i];
+  }
+  part[w][lane] = acc;
+  __syncthreads();
+  if (w == 0 && i < n_elem) out[i] = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+}
+
+static int wgrad_nt(int Nb) {
+  const int nt = ceil_div(Nb, 16);
+  if (nt <= 4) return 4;
+  if (nt <= 8) return 8;
+  if (nt <= 13) return 13;
+  return 16;
 }
 
 static void wgrad_plan(int64_t max_rows, int Ka, int Nb, int* n_chunks, int64_t* rows_per_chunk,
-                       int* panels) {
-  const int pa = ceil_div(Ka, WG_KA), pb = ceil_div(Nb, WG_NB);
+                       int* panels, int* panels_nb) {
+  const int nt = wgrad_nt(Nb);
+  const int pa = ceil_div(Ka, WG_KA), pb = ceil_div(Nb, nt * 16);
   *panels = pa * pb;
+  *panels_nb = pb;
   int target = ceil_div(512, *panels);  // ~2 workgroups per CU
   int64_t rpc = (max_rows + target - 1) / target;
-  rpc = ((rpc + 255) / 256) * 256;  // >= 256 rows per chunk
-  if (rpc < 256) rpc = 256;
+  rpc = ((rpc + 15) / 16) * 16;
+  if (rpc < 64) rpc = 64;
   *rows_per_chunk = rpc;
   *n_chunks = (int)((max_rows + rpc - 1) / rpc);
   if (*n_chunks < 1) *n_chunks = 1;
@@ -500,13 +649,13 @@ extern "C" int hstu_gate_o_fwd(const float* u, int64_t ld_u, const float* attn, 
                                const int64_t* offsets, int B, int64_t max_rows, int hdv, int D,
                                const float* w_o, const float* b_o, const float* x_res,
                                int64_t ld_x, float eps, float dropout_p, uint64_t seed,
-                               float* attn_stats, float* o_in, float* y, int64_t ld_y,
-                               void* stream) {
+                               const int64_t* seed_offset, float* attn_stats, float* o_in,
+                               float* y, int64_t ld_y, void* stream) {
   GR_REQUIRE(u && attn && offsets && w_o && y && attn_stats, "hstu_gate_o_fwd: null pointer");
   GR_REQUIRE(hdv > 0 && D > 0 && B >= 0, "hstu_gate_o_fwd: bad sizes");
   GR_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f, "hstu_gate_o_fwd: dropout_p %f", dropout_p);
   OpGateO op{offsets, B, hdv, D, u, ld_u, attn, ld_attn, w_o, b_o, x_res, ld_x, eps, dropout_p,
-             seed, (float2*)attn_stats, o_in, y, ld_y};
+             seed, seed_offset, (float2*)attn_stats, o_in, y, ld_y};
   return launch_rowpanel(op, max_rows, false, "hstu_gate_o_fwd", (hipStream_t)stream);
 }
 
@@ -514,8 +663,9 @@ extern "C" int hstu_gate_o_bwd(const float* dy, int64_t ld_dy, const int64_t* of
                                int64_t max_rows, int hdv, int D, const float* w_o,
                                const float* u, int64_t ld_u, const float* attn, int64_t ld_attn,
                                const float* attn_stats, const float* h_u, int64_t ld_h,
-                               float dropout_p, uint64_t seed, float* du, int64_t ld_du,
-                               float* d_attn, int64_t ld_da, void* stream) {
+                               float dropout_p, uint64_t seed, const int64_t* seed_offset,
+                               float* du, int64_t ld_du, float* d_attn, int64_t ld_da,
+                               void* stream) {
   GR_REQUIRE(dy && offsets && w_o && u && attn && attn_stats && du && d_attn,
              "hstu_gate_o_bwd: null pointer");
   GR_REQUIRE(hdv > 0 && D > 0 && B >= 0, "hstu_gate_o_bwd: bad sizes");
@@ -523,7 +673,7 @@ extern "C" int hstu_gate_o_bwd(const float* dy, int64_t ld_dy, const int64_t* of
   op.offsets = offsets; op.B = B; op.K = D; op.N = hdv; op.dy = dy; op.lddy = ld_dy;
   op.w = w_o; op.u = u; op.ldu = ld_u; op.attn = attn; op.lda = ld_attn;
   op.a_stats = (const float2*)attn_stats; op.h_u = h_u; op.ldh = ld_h; op.p = dropout_p;
-  op.seed = seed; op.du = du; op.lddu = ld_du; op.da = d_attn; op.ldda = ld_da;
+  op.seed = seed; op.seed_off = seed_offset; op.du = du; op.lddu = ld_du; op.da = d_attn; op.ldda = ld_da;
   return launch_rowpanel(op, max_rows, true, "hstu_gate_o_bwd", (hipStream_t)stream);
 }
 
@@ -543,9 +693,9 @@ extern "C" int hstu_ln_uvqk_bwd(const float* dh, int64_t ld_dh, const int64_t* o
 
 extern "C" size_t gr_wgrad_workspace_size(int64_t max_rows, int Ka, int Nb) {
   if (max_rows <= 0 || Ka <= 0 || Nb <= 0) return 0;
-  int n_chunks, panels;
+  int n_chunks, panels, pnb;
   int64_t rpc;
-  wgrad_plan(max_rows, Ka, Nb, &n_chunks, &rpc, &panels);
+  wgrad_plan(max_rows, Ka, Nb, &n_chunks, &rpc, &panels, &pnb);
   return sizeof(float) * (size_t)n_chunks * ((size_t)Ka * Nb + Ka);
 }
 
@@ -561,23 +711,29 @@ extern "C" int gr_wgrad(const float* a, int64_t lda, const float* a_stats, const
     if (a_colsum) (void)hipMemsetAsync(a_colsum, 0, sizeof(float) * Ka, st);
     return 0;
   }
-  int n_chunks, panels;
+  int n_chunks, panels, pnb;
   int64_t rpc;
-  wgrad_plan(max_rows, Ka, Nb, &n_chunks, &rpc, &panels);
+  wgrad_plan(max_rows, Ka, Nb, &n_chunks, &rpc, &panels, &pnb);
   const size_t need = sizeof(float) * (size_t)n_chunks * ((size_t)Ka * Nb + Ka);
   GR_REQUIRE(workspace && ws_bytes >= need, "gr_wgrad: workspace %zu B < %zu B", ws_bytes, need);
   float* slabs = (float*)workspace;
   float* cs = a_colsum ? slabs + (size_t)n_chunks * Ka * Nb : nullptr;
   WgradArgs g{a, lda, (const float2*)a_stats, bm, ldb, offsets, B, Ka, Nb, rpc, n_chunks,
-              ceil_div(Nb, WG_NB), slabs, cs};
-  hipLaunchKernelGGL(wgrad_partial_kernel, dim3(n_chunks, panels), dim3(256), 0, st, g);
+              pnb, slabs, cs};
+  const dim3 grid(n_chunks, panels);
+  switch (wgrad_nt(Nb)) {
+    case 4: hipLaunchKernelGGL(wgrad_partial_kernel<4>, grid, dim3(256), 0, st, g); break;
+    case 8: hipLaunchKernelGGL(wgrad_partial_kernel<8>, grid, dim3(256), 0, st, g); break;
+    case 13: hipLaunchKernelGGL(wgrad_partial_kernel<13>, grid, dim3(256), 0, st, g); break;
+    default: hipLaunchKernelGGL(wgrad_partial_kernel<16>, grid, dim3(256), 0, st, g); break;
+  }
   GR_LAUNCH_CHECK("gr_wgrad(partial)");
   const int64_t ne = (int64_t)Ka * Nb;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st,
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((ne + 63) / 64)), dim3(256), 0, st,
                      slabs, n_chunks, ne, c);
   GR_LAUNCH_CHECK("gr_wgrad(reduce)");
   if (a_colsum) {
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((Ka + 255) / 256)), dim3(256), 0,
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((Ka + 63) / 64)), dim3(256), 0,
                        st, cs, n_chunks, (int64_t)Ka, a_colsum);
     GR_LAUNCH_CHECK("gr_wgrad(colsum)");
   }

@@ -138,12 +138,13 @@ struct SelectArgs {
   const float* packed;
   int64_t X;
   int D, B, k, N0, n_ranges;
+  int k_part;           // entries per (range, query) partial list (>= k)
   int64_t range_items;  // multiple of 4*64
   const int64_t* item_ids;
   int64_t index_base;
   const int64_t* invalid;
-  float* part_score;   // [n_ranges][B][k]
-  int64_t* part_index; // [n_ranges][B][k]  (global index, -1 = empty)
+  float* part_score;   // [n_ranges][B][k_part]
+  int64_t* part_index; // [n_ranges][B][k_part]  (global index, -1 = empty)
 };
 
 template <int KS, int BLOCKS>
@@ -215,7 +216,8 @@ __global__ __launch_bounds__(256) void mips_select_kernel(SelectArgs a) {
 
   const int64_t n_items = x_end > x_begin ? x_end - x_begin : 0;
   const int n_steps = (int)((n_items + 4 * STEP - 1) / (4 * STEP));
-  const float2* pk = reinterpret_cast<const float2*>(a.packed);
+  typedef float fv2 __attribute__((ext_vector_type(2)));
+  gptr<fv2> pk = as_global(reinterpret_cast<const fv2*>(a.packed));
   int* whist = hist + w * 256;
 
   auto compact = [&](int qq, int kk) {
@@ -226,27 +228,34 @@ __global__ __launch_bounds__(256) void mips_select_kernel(SelectArgs a) {
     const int n = cnt[qq];
     const int64_t* qinv = inv + qq * INV_MAX;
     int nvalid = 0;
+    // all LDS/global loads unconditional (clamped) so they are in flight together
+    int64_t id[CAP / 64];
+    bool need[CAP / 64];
 #pragma unroll
     for (int t = 0; t < CAP / 64; ++t) {
       const int j = lane + 64 * t;
-      key[t] = 0u;
-      sc[t] = 0.f;
-      ix[t] = 0u;
-      if (j < n) {
-        sc[t] = cs[qq * CAP + j];
-        ix[t] = ci[qq * CAP + j];
-        bool ok = true;
-        if (!(ix[t] & VERIFIED)) {
-          const int64_t li = (int64_t)(ix[t] & ~VERIFIED);
-          const int64_t id = a.item_ids ? a.item_ids[li] : a.index_base + li;
-          ok = !(a.N0 > 0 && sorted_contains(qinv, a.N0, id));
-          ix[t] |= VERIFIED;
-        }
-        if (ok) {
-          key[t] = ord_key(sc[t]);
-          ++nvalid;
-        }
+      const int jc = j < n ? j : 0;
+      sc[t] = cs[qq * CAP + jc];
+      ix[t] = ci[qq * CAP + jc];
+      need[t] = j < n && !(ix[t] & VERIFIED);
+      const int64_t li = (int64_t)(ix[t] & ~VERIFIED);
+      id[t] = a.item_ids ? as_global(a.item_ids)[li < a.X ? li : 0] : a.index_base + li;
+    }
+    const int nbits = a.N0 > 0 ? 32 - __clz(n0p - 1) : 0;  // log2(n0p)
+#pragma unroll
+    for (int t = 0; t < CAP / 64; ++t) {
+      // branchless lower_bound over the sorted (INT64_MAX padded) n0p-entry list
+      int pos = 0;
+      for (int bit = nbits - 1; bit >= 0; --bit) {
+        const int probe = pos + (1 << bit) - 1;
+        pos += (qinv[probe] < id[t]) ? (1 << bit) : 0;
       }
+      const bool hit = a.N0 > 0 && qinv[pos < n0p ? pos : n0p - 1] == id[t];
+      const int j = lane + 64 * t;
+      const bool ok = j < n && !(need[t] && hit);
+      ix[t] |= VERIFIED;
+      key[t] = ok ? ord_key(sc[t]) : 0u;
+      nvalid += ok;
     }
     // total valid count
     int tot = nvalid;
@@ -309,69 +318,82 @@ __global__ __launch_bounds__(256) void mips_select_kernel(SelectArgs a) {
     }
   };
 
-  float2 frag[BLOCKS][KS2];
-  auto load_step = [&](int step) {
+  // Double-buffered register prefetch (two named buffers: static indexing only).
+  // Loads are unconditional (block index clamped into the table): a guarded load
+  // would make hipcc branch around it and wait vmcnt(0) per element.
+  const int64_t last_blk = (a.X + 15) / 16 - 1;
+  fv2 fa[BLOCKS][KS2], fb[BLOCKS][KS2];
+  auto load_step = [&](fv2 (&f)[BLOCKS][KS2], int step) {
     const int64_t xb = x_begin + ((int64_t)step * 4 + w) * STEP;
 #pragma unroll
     for (int bb = 0; bb < BLOCKS; ++bb) {
-      const int64_t ib = (xb >> 4) + bb;
-      const bool ok = xb + bb * 16 < x_end;
+      int64_t ib = (xb >> 4) + bb;
+      ib = ib > last_blk ? last_blk : ib;
+      gptr<fv2> src = pk + ib * KS2 * 64 + lane;
 #pragma unroll
-      for (int j = 0; j < KS2; ++j)
-        frag[bb][j] = ok ? pk[(ib * KS2 + j) * 64 + lane] : make_float2(0.f, 0.f);
+      for (int j = 0; j < KS2; ++j) f[bb][j] = src[j * 64];
     }
   };
-
-  if (n_steps > 0) load_step(0);
-  for (int step = 0; step < n_steps; ++step) {
-    float2 cur[BLOCKS][KS2];
-#pragma unroll
-    for (int bb = 0; bb < BLOCKS; ++bb)
-#pragma unroll
-      for (int j = 0; j < KS2; ++j) cur[bb][j] = frag[bb][j];
-    if (step + 1 < n_steps) load_step(step + 1);
+  auto process = [&](const fv2 (&f)[BLOCKS][KS2], int step) {
     const float tau = tau_s[lr];
     const int64_t xb = x_begin + ((int64_t)step * 4 + w) * STEP;
+    f4 s[BLOCKS];
+#pragma unroll
+    for (int bb = 0; bb < BLOCKS; ++bb) s[bb] = f4_zero();
+#pragma unroll
+    for (int st = 0; st < KS; ++st)
+#pragma unroll
+      for (int bb = 0; bb < BLOCKS; ++bb)
+        s[bb] = mfma16x16x4((st & 1) ? f[bb][st >> 1].y : f[bb][st >> 1].x, qreg[st], s[bb]);
 #pragma unroll
     for (int bb = 0; bb < BLOCKS; ++bb) {
-      f4 s = f4_zero();
-#pragma unroll
-      for (int st = 0; st < KS; ++st)
-        s = mfma16x16x4((st & 1) ? cur[bb][st >> 1].y : cur[bb][st >> 1].x, qreg[st], s);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int64_t item = xb + bb * 16 + 4 * lg + r;
-        if (item < x_end && s[r] > tau) {
+        if (item < x_end && s[bb][r] > tau) {
           const int slot = atomicAdd(&cnt[lr], 1);
-          cs[lr * CAP + slot] = s[r];
+          cs[lr * CAP + slot] = s[bb][r];
           ci[lr * CAP + slot] = (uint32_t)item;  // local index
         }
       }
     }
-    __syncthreads();
-    if (tid == 0) {
-      int f = 0;
-      for (int qq = 0; qq < QG; ++qq) f |= cnt[qq] > CAP - 4 * STEP;
-      need_compact = f;
+    lds_barrier();
+    if (w == 0) {
+      const bool fl = lane < QG && cnt[lane] > CAP - 4 * STEP;
+      const unsigned long long bal = __ballot(fl);
+      if (lane == 0) need_compact = bal != 0ull;
     }
-    __syncthreads();
+    lds_barrier();
     if (need_compact) {
       for (int qq = w; qq < QG; qq += 4)
         if (cnt[qq] > a.k) compact(qq, a.k);
-      __syncthreads();
+      lds_barrier();
     }
+  };
+
+  // prefetches past the last step re-load the last step (harmless; keeps the loads
+  // unconditional so the waitcnt pass can count them)
+  const int last_step = n_steps > 0 ? n_steps - 1 : 0;
+  load_step(fa, 0);
+  for (int step = 0; step < n_steps; step += 2) {
+    load_step(fb, min(step + 1, last_step));
+    process(fa, step);
+    if (step + 1 >= n_steps) break;
+    load_step(fa, min(step + 2, last_step));
+    process(fb, step + 1);
   }
-  // ---- final: exact top-k per query of this range
+  // ---- final: this range's candidates per query (exact top-k_part, invalid removed;
+  // when at most k_part remain this is only the invalid-id filter: the merge selects)
   __syncthreads();
   for (int qq = w; qq < QG; qq += 4) {
     if (q0 + qq >= a.B) continue;
-    compact(qq, a.k);
+    compact(qq, a.k_part);
   }
   __syncthreads();
-  for (int e = tid; e < QG * a.k; e += 256) {
-    const int qq = e / a.k, j = e - qq * a.k;
+  for (int e = tid; e < QG * a.k_part; e += 256) {
+    const int qq = e / a.k_part, j = e - qq * a.k_part;
     if (q0 + qq >= a.B) continue;
-    const int64_t o = ((int64_t)range * a.B + q0 + qq) * a.k + j;
+    const int64_t o = ((int64_t)range * a.B + q0 + qq) * a.k_part + j;
     if (j < cnt[qq]) {
       a.part_score[o] = cs[qq * CAP + j];
       a.part_index[o] = a.index_base + (int64_t)(ci[qq * CAP + j] & ~VERIFIED);
@@ -397,13 +419,48 @@ struct MergeArgs {
 
 constexpr int MERGE_MAX = 8192;
 
+// Block-level digit search over a 256-bin histogram (wave 0): the digit d such that
+// count(digit > d) < need <= count(digit >= d); returns (d, count above d).
+__device__ __forceinline__ void hist_find_digit(const int* hist, int need, int* out_digit,
+                                                int* out_above) {
+  const int lane = threadIdx.x & 63;
+  int c[4], s = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    c[j] = hist[255 - 4 * lane - j];
+    s += c[j];
+  }
+  int incl = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int v = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += v;
+  }
+  const int excl = incl - s;
+  if (excl < need && incl >= need) {
+    int run = excl;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (run + c[j] >= need) {
+        *out_digit = 255 - 4 * lane - j;
+        *out_above = run;
+        break;
+      }
+      run += c[j];
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void mips_merge_kernel(MergeArgs a) {
   __shared__ uint32_t key[MERGE_MAX];
+  __shared__ int64_t idx[MERGE_MAX];
   __shared__ int hist[256];
-  __shared__ int sh_need, sh_digit;
+  __shared__ int sh_digit, sh_above;
   __shared__ uint32_t s_key[256];
+  __shared__ int64_t s_idx[256];
   __shared__ int s_src[256];
   __shared__ int s_cnt;
+  __shared__ int red[4];
   const int q = blockIdx.x;
   const int tid = threadIdx.x;
   const int M = a.n_lists * a.k_in;
@@ -414,13 +471,12 @@ __global__ __launch_bounds__(256) void mips_merge_kernel(MergeArgs a) {
   int nvalid = 0;
   for (int e = tid; e < M; e += 256) {
     const int64_t s = src_of(e);
-    const bool ok = a.cand_index[s] >= 0;
+    const int64_t gi = a.cand_index[s];
+    const bool ok = gi >= 0;
     key[e] = ok ? ord_key(a.cand_score[s]) : 0u;
+    idx[e] = ok ? gi : INT64_MAX;
     nvalid += ok;
   }
-  __syncthreads();
-  // block-wide count of valid
-  __shared__ int red[4];
   int v = nvalid;
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -442,41 +498,44 @@ __global__ __launch_bounds__(256) void mips_merge_kernel(MergeArgs a) {
         if (x != 0u && (x & mask) == prefix) atomicAdd(&hist[(x >> shift) & 255], 1);
       }
       __syncthreads();
-      if (tid == 0) {
-        int run = 0, d = 255;
-        for (; d >= 0; --d) {
-          if (run + hist[d] >= need) break;
-          run += hist[d];
-        }
-        sh_digit = d;
-        sh_need = need - run;
-      }
+      if (tid < 64) hist_find_digit(hist, need, &sh_digit, &sh_above);
       __syncthreads();
       prefix |= (uint32_t)sh_digit << shift;
       mask |= 0xFFu << shift;
-      need = sh_need;
-      __syncthreads();
+      need -= sh_above;
     }
     kstar = prefix;
     k_rem = need;
   }
-  // collect the selected entries: key > kstar, plus k_rem ties with smallest index
+  // ties at kstar: count them; if more than k_rem, keep the smallest indices
+  int eq = 0;
+  if (!all)
+    for (int e = tid; e < M; e += 256) eq += key[e] == kstar;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) eq += __shfl_xor(eq, o, 64);
+  __syncthreads();
+  if ((tid & 63) == 0) red[tid >> 6] = eq;
   if (tid == 0) s_cnt = 0;
   __syncthreads();
+  const int eq_tot = red[0] + red[1] + red[2] + red[3];
   for (int e = tid; e < M; e += 256) {
     const uint32_t x = key[e];
     if (x == 0u) continue;
     bool take = all || x > kstar;
     if (!all && x == kstar) {
-      const int64_t my = a.cand_index[src_of(e)];
-      int smaller = 0;
-      for (int f = 0; f < M; ++f)
-        if (key[f] == kstar && a.cand_index[src_of(f)] < my) ++smaller;
-      take = smaller < k_rem;
+      if (eq_tot == k_rem) {
+        take = true;
+      } else {
+        const int64_t my = idx[e];
+        int smaller = 0;
+        for (int f = 0; f < M; ++f) smaller += (key[f] == kstar && idx[f] < my);
+        take = smaller < k_rem;
+      }
     }
     if (take) {
       const int p = atomicAdd(&s_cnt, 1);
       s_key[p] = x;
+      s_idx[p] = idx[e];
       s_src[p] = e;
     }
   }
@@ -484,23 +543,25 @@ __global__ __launch_bounds__(256) void mips_merge_kernel(MergeArgs a) {
   const int n = s_cnt;
   for (int p = n + tid; p < 256; p += 256) {
     s_key[p] = 0u;
+    s_idx[p] = INT64_MAX;
     s_src[p] = -1;
   }
   __syncthreads();
-  // bitonic sort 256 entries: key desc, then candidate index asc
+  // bitonic sort 256 entries: key desc, then catalog index asc
   for (int size = 2; size <= 256; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
       const int i = tid;
       const int j = i ^ stride;
       if (j > i) {
         const uint32_t ki = s_key[i], kj = s_key[j];
-        const int64_t ii = s_src[i] >= 0 ? a.cand_index[src_of(s_src[i])] : INT64_MAX;
-        const int64_t ij = s_src[j] >= 0 ? a.cand_index[src_of(s_src[j])] : INT64_MAX;
+        const int64_t ii = s_idx[i], ij = s_idx[j];
         const bool i_first = (ki > kj) || (ki == kj && ii < ij);
-        const bool desc = (i & size) == 0;
-        if (i_first != desc) {
+        const bool asc = (i & size) == 0;
+        if (i_first != asc) {
           s_key[i] = kj;
           s_key[j] = ki;
+          s_idx[i] = ij;
+          s_idx[j] = ii;
           const int t = s_src[i];
           s_src[i] = s_src[j];
           s_src[j] = t;
@@ -513,7 +574,7 @@ __global__ __launch_bounds__(256) void mips_merge_kernel(MergeArgs a) {
     const int64_t o = (int64_t)q * kk + r;
     if (r < n) {
       const int64_t s = src_of(s_src[r]);
-      const int64_t gi = a.cand_index[s];
+      const int64_t gi = s_idx[r];
       a.out_score[o] = a.cand_score[s];
       if (a.out_index) a.out_index[o] = gi;
       int64_t id;
@@ -529,7 +590,7 @@ __global__ __launch_bounds__(256) void mips_merge_kernel(MergeArgs a) {
 }
 
 struct TopkPlan {
-  int KS, n_ranges;
+  int KS, n_ranges, k_part;
   int64_t range_items;
   size_t part_bytes;
 };
@@ -550,7 +611,12 @@ static TopkPlan plan_topk(int B, int64_t X, int D, int k) {
     p.range_items *= 2;
     p.n_ranges = (int)((X + p.range_items - 1) / p.range_items);
   }
-  p.part_bytes = (size_t)p.n_ranges * B * k * (sizeof(float) + sizeof(int64_t));
+  // hand the merge up to CAP/2 candidates per range when it has room: a range that
+  // saw <= k_part valid items then needs no selection in phase 1
+  int kp = MERGE_MAX / p.n_ranges;
+  kp = kp > CAP / 2 ? CAP / 2 : kp;
+  p.k_part = kp > k ? kp : k;
+  p.part_bytes = (size_t)p.n_ranges * B * p.k_part * (sizeof(float) + sizeof(int64_t));
   return p;
 }
 
@@ -605,8 +671,8 @@ extern "C" int mips_topk(const float* queries, const float* packed_items, int64_
   GR_REQUIRE(workspace && ws_bytes >= p.part_bytes, "mips_topk: workspace %zu B < %zu B", ws_bytes,
              p.part_bytes);
   float* part_score = (float*)workspace;
-  int64_t* part_index = (int64_t*)(part_score + (size_t)p.n_ranges * B * k);
-  SelectArgs a{queries, packed_items, X, D, B, k, N0, p.n_ranges, p.range_items,
+  int64_t* part_index = (int64_t*)(part_score + (size_t)p.n_ranges * B * p.k_part);
+  SelectArgs a{queries, packed_items, X, D, B, k, N0, p.n_ranges, p.k_part, p.range_items,
                item_ids, index_base, invalid_ids, part_score, part_index};
   int rc;
   switch (p.KS) {
@@ -620,7 +686,7 @@ extern "C" int mips_topk(const float* queries, const float* packed_items, int64_
       else rc = launch_select<64>(a, st);
   }
   if (rc) return rc;
-  MergeArgs m{part_score, part_index, nullptr, p.n_ranges, B, k, k, item_ids, index_base,
+  MergeArgs m{part_score, part_index, nullptr, p.n_ranges, B, p.k_part, k, item_ids, index_base,
               out_scores, out_ids, out_index};
   hipLaunchKernelGGL(mips_merge_kernel, dim3(B), dim3(256), 0, st, m);
   GR_LAUNCH_CHECK("mips_topk(merge)");

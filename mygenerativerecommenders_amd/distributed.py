@@ -4,11 +4,10 @@
 Reference parallelism: Lightning DDP only (configs/trainer/ddp.yaml) —
 one fp32 gradient all-reduce per step — and torchmetrics' all-gather of top-k ids.
 Here:
-  * ``FlatGradAllReducer``: every parameter's .grad is a view into ONE contiguous
-    fp32 buffer, so a step's gradient exchange is a single all-reduce (ml-1m encoder
-    grads are ~250 KB: latency-bound, one collective beats buckets); buckets of
-    ``bucket_bytes`` are used when the flat buffer is large (ml-20m scale) and can be
-    launched as soon as backward has produced them (``launch_ready``).
+  * ``FlatGradAllReducer``: the step's gradients are flattened into ONE contiguous
+    fp32 buffer and exchanged with a single all-reduce (ml-1m encoder grads are
+    ~250 KB: latency-bound, one collective beats buckets); buckets of
+    ``bucket_bytes`` are used when the flat buffer is large (ml-20m scale).
   * ``ShardedCandidateIndex``: the item table is row-sharded (rank r holds rows
     [r*X/P, (r+1)*X/P)); each rank runs the fused local top-k, the (B, k) score /
     index / id lists are all-gathered (12 B x B x k per rank) and merged on device.
@@ -40,53 +39,47 @@ def init_from_env(backend: Optional[str] = None):
 
 
 class FlatGradAllReducer:
-    """Gradient averaging over the data-parallel group with .grad tensors living in
-    one flat buffer (the DDP ``gradient_as_bucket_view`` idea, minus the hooks)."""
+    """Gradient averaging over the data-parallel group: the step's gradients are
+    flattened into ONE contiguous fp32 buffer and exchanged with a single RCCL
+    all-reduce (ml-1m encoder grads are ~250 KB: latency-bound, so one collective beats
+    buckets; above ``bucket_bytes`` the buffer is split into buckets issued together).
+    Gradients stay ordinary tensors (autograd "steals" the backward's outputs, so no
+    accumulate kernels run), which keeps the step capturable in a HIP graph."""
 
     def __init__(self, params: List[torch.nn.Parameter], group=None,
                  bucket_bytes: int = 64 << 20):
         self.params = [p for p in params if p.requires_grad]
         self.group = group
-        n = sum(p.numel() for p in self.params)
-        dev = self.params[0].device if self.params else torch.device("cpu")
-        self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
-        off = 0
-        self.slices = []
-        for p in self.params:
-            k = p.numel()
-            p.grad = self.flat[off:off + k].view_as(p)
-            self.slices.append((off, k))
-            off += k
-        # contiguous buckets over the flat buffer, in reverse parameter order (the
-        # order backward produces gradients)
-        self.buckets = []
-        max_el = max(1, bucket_bytes // 4)
-        end = n
-        while end > 0:
-            start = max(0, end - max_el)
-            self.buckets.append((start, end))
-            end = start
+        self.bucket_bytes = bucket_bytes
 
     def zero_grad(self):
-        self.flat.zero_()
+        for p in self.params:
+            p.grad = None
 
-    def rebind(self):
-        """Re-point .grad at the flat buffer (if an optimizer/user replaced it)."""
-        for p, (off, k) in zip(self.params, self.slices):
-            if p.grad is None or p.grad.data_ptr() != self.flat[off:].data_ptr():
-                p.grad = self.flat[off:off + k].view_as(p)
-
-    def allreduce(self, world: Optional[int] = None):
+    def allreduce(self, world: Optional[int] = None, inplace: bool = False):
+        """inplace=True copies the averaged gradients back into the existing .grad
+        tensors (static buffers of a captured graph) instead of re-pointing .grad."""
         if not (dist.is_available() and dist.is_initialized()):
             return
         world = world or dist.get_world_size(self.group)
         if world == 1:
             return
-        handles = [dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.SUM, group=self.group,
-                                   async_op=True) for (s, e) in self.buckets]
+        grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in self.params]
+        flat = torch.cat([g.reshape(-1) for g in grads])
+        max_el = max(1, self.bucket_bytes // 4)
+        handles = [dist.all_reduce(flat[s:s + max_el], op=dist.ReduceOp.SUM, group=self.group,
+                                   async_op=True) for s in range(0, flat.numel(), max_el)]
         for h in handles:
             h.wait()
-        self.flat.div_(world)
+        flat.div_(world)
+        off = 0
+        for p, g in zip(self.params, grads):
+            k = g.numel()
+            if inplace and p.grad is not None:
+                p.grad.copy_(flat[off:off + k].view_as(p))
+            else:
+                p.grad = flat[off:off + k].view_as(p)
+            off += k
 
 
 class ShardedCandidateIndex:
@@ -100,6 +93,10 @@ class ShardedCandidateIndex:
         self.k = k
         self.ids = ids_shard.to(torch.int64).contiguous()
         self.row_offset = int(row_offset)
+        # contiguous ids (the common 1..X catalog): derive ids from the index on device
+        start = int(self.ids[0].item()) if self.ids.numel() else 0
+        ar = torch.arange(start, start + self.ids.numel(), device=self.ids.device)
+        self.arange_base = start if bool(torch.equal(self.ids, ar)) else None
         self.group = group
         self.packed = PackedItems(emb_shard.float().contiguous())
 
@@ -107,9 +104,14 @@ class ShardedCandidateIndex:
                           invalid_ids: Optional[torch.Tensor] = None, k: Optional[int] = None):
         from .top_k import merge_topk, mips_topk
         k = k or self.k
-        s, i, x = mips_topk(query_embeddings, self.packed, k, item_ids=self.ids,
-                            invalid_ids=invalid_ids, index_base=self.row_offset,
-                            return_index=True)
+        if self.arange_base is not None:  # global index = id (monotone in the row)
+            s, i, x = mips_topk(query_embeddings, self.packed, k, item_ids=None,
+                                invalid_ids=invalid_ids, index_base=self.arange_base,
+                                return_index=True)
+        else:
+            s, i, x = mips_topk(query_embeddings, self.packed, k, item_ids=self.ids,
+                                invalid_ids=invalid_ids, index_base=self.row_offset,
+                                return_index=True)
         if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(self.group) == 1:
             return i, s
         P = dist.get_world_size(self.group)

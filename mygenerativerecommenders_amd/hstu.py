@@ -111,8 +111,12 @@ class SequentialTransductionUnitJagged(torch.nn.Module):
             out_features=embedding_dim)
         torch.nn.init.xavier_uniform_(self._o.weight)
         self._eps = epsilon
-        self._seed_gen = torch.Generator(device="cpu")
-        self._seed_gen.manual_seed(0x5EED)
+        # dropout: mask = hash(base seed + device step counter, element).  The counter
+        # is bumped on the device each training forward, so CUDA/HIP-graph replays draw
+        # fresh masks; the backward re-derives the forward's mask from the same counter.
+        self._dropout_seed = int(torch.randint(0, 2**62, (1,)).item())
+        self.register_buffer("_dropout_step", torch.zeros(1, dtype=torch.int64),
+                             persistent=False)
 
     def _geometry(self, n: int, max_len: int) -> ops.STUGeometry:
         if self._linear_activation == "silu":
@@ -143,22 +147,31 @@ class SequentialTransductionUnitJagged(torch.nn.Module):
         cache: Optional[HSTUCacheState] = None,
         return_cache_states: bool = False,
         max_len: Optional[int] = None,
+        bucket_map: Optional[torch.Tensor] = None,
     ):
         """x: (rows, D) jagged; x_offsets (B+1,).  Returns (x', cache-state tuple);
-        cache states are (v, None, None, x') — padded q/k are never built."""
+        cache states are (v, None, None, x') — padded q/k are never built.
+        ``bucket_map`` (optional) is the batch's ``ops.bucket_map`` — pass it to share
+        it across layers; otherwise it is built from ``all_timestamps``."""
         if delta_x_offsets is not None or cache is not None:
             raise NotImplementedError("incremental (cached) HSTU decoding is not supported")
         n = invalid_attn_mask.size(-1)
         geo = self._geometry(n, n if max_len is None else max_len)
         rab = self._rel_attn_bias
-        ts = all_timestamps if rab is not None else None
-        pos_w = rab._pos_w if ts is not None else None
-        ts_w = rab._ts_w if ts is not None else None
-        if ts is not None and pos_w.numel() != 2 * n - 1:
+        bmap = None
+        if rab is not None and all_timestamps is not None:
+            bmap = bucket_map if bucket_map is not None else ops.bucket_map(
+                all_timestamps, x_offsets, n)
+        pos_w = rab._pos_w if bmap is not None else None
+        ts_w = rab._ts_w if bmap is not None else None
+        if bmap is not None and pos_w.numel() != 2 * n - 1:
             raise ValueError(f"_pos_w has {pos_w.numel()} entries, expected {2 * n - 1}")
-        seed = int(torch.randint(0, 2**62, (1,), generator=self._seed_gen)) if geo.dropout_p > 0 else 0
-        y = ops.stu_layer(x, x_offsets, ts, self._uvqk, self._o.weight, self._o.bias, pos_w,
-                          ts_w, geo, seed)
+        step = None
+        if geo.dropout_p > 0:
+            self._dropout_step.add_(1)
+            step = self._dropout_step
+        y = ops.stu_layer(x, x_offsets, bmap, self._uvqk, self._o.weight, self._o.bias, pos_w,
+                          ts_w, geo, self._dropout_seed, step)
         return y, (None, None, None, y)
 
 
@@ -175,11 +188,18 @@ class HSTUJagged(torch.nn.Module):
                        delta_x_offsets=None, cache=None, return_cache_states=False,
                        max_len: Optional[int] = None):
         cache_states: List[HSTUCacheState] = []
+        n = invalid_attn_mask.size(-1)
+        # one bucket map per batch, shared by every layer's forward and backward
+        bmap = None
+        if all_timestamps is not None and any(
+                layer._rel_attn_bias is not None for layer in self._attention_layers):
+            bmap = ops.bucket_map(all_timestamps, x_offsets, n)
         for layer in self._attention_layers:
             x, cs = layer(x=x, x_offsets=x_offsets, all_timestamps=all_timestamps,
                           invalid_attn_mask=invalid_attn_mask,
                           delta_x_offsets=delta_x_offsets, cache=None,
-                          return_cache_states=return_cache_states, max_len=max_len)
+                          return_cache_states=return_cache_states, max_len=max_len,
+                          bucket_map=bmap)
             if return_cache_states:
                 cache_states.append(cs)
         return x, cache_states

@@ -134,6 +134,24 @@ def get_current_embeddings(lengths: torch.Tensor, encoded_embeddings: torch.Tens
     return encoded_embeddings.reshape(-1, D).index_select(0, idx)
 
 
+# ------------------------------------------------------------------ relative-time buckets
+
+def bucket_map(timestamps: torch.Tensor, offsets: torch.Tensor, N: int) -> torch.Tensor:
+    """uint8 relative-time bucket of every causal (query, key) pair, computed once per
+    batch and shared by all layers (``hstu_bucket_map``; reference hstu.py:111-123)."""
+    _lib.require_gpu(timestamps, offsets)
+    ts = timestamps.to(torch.int64).contiguous()
+    B = offsets.numel() - 1
+    if ts.shape != (B, N):
+        raise ValueError(f"timestamps must be (B, N) = ({B}, {N}), got {tuple(ts.shape)}")
+    nbytes = _lib.lib().hstu_bucket_map_bytes(B, N)
+    out = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=ts.device)
+    thr = bucket_thresholds(ts.device)
+    _lib.call("hstu_bucket_map", ts.data_ptr(), offsets.data_ptr(), B, N, thr.data_ptr(),
+              NUM_BUCKETS, out.data_ptr(), _stream())
+    return out
+
+
 # ------------------------------------------------------------------ fused STU layer
 
 @dataclass
@@ -155,12 +173,13 @@ class STUGeometry:
 
 class STULayerFunction(torch.autograd.Function):
     """One SequentialTransductionUnitJagged (hstu.py:266-413) as 3 fused launches
-    forward and 6 backward.  Inputs: jagged x (rows, D), offsets (B+1), timestamps
-    (B, N) or None; parameters _uvqk (D, n_out), _o.weight (D, hdv), _o.bias (D,),
+    forward and 6 backward.  Inputs: jagged x (rows, D), offsets (B+1), the batch's
+    bucket map (``bucket_map``) or None (no relative bias); parameters _uvqk (D, n_out), _o.weight (D, hdv), _o.bias (D,),
     _pos_w (2N-1,), _ts_w (129,)."""
 
     @staticmethod
-    def forward(ctx, x, offsets, ts, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGeometry, seed: int):
+    def forward(ctx, x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGeometry, seed: int,
+                seed_offset):
         dev = x.device
         rows, D = x.shape
         B = offsets.numel() - 1
@@ -178,16 +197,14 @@ class STULayerFunction(torch.autograd.Function):
                   w_uvqk.data_ptr(), n_out, geo.eps, geo.activation, x_stats.data_ptr(),
                   _lib.ptr(h_pre), uvqk.data_ptr(), n_out, st)
         attn = torch.empty(rows, hv, dtype=torch.float32, device=dev)
-        thr = bucket_thresholds(dev)
         q = uvqk[:, 2 * hv:2 * hv + hq]
         k = uvqk[:, 2 * hv + hq:]
         v = uvqk[:, hv:2 * hv]
-        pos_w_c = pos_w.contiguous() if ts is not None else None
-        ts_w_c = ts_w.contiguous() if ts is not None else None
+        pos_w_c = pos_w.contiguous() if bmap is not None else None
+        ts_w_c = ts_w.contiguous() if bmap is not None else None
         _lib.call("hstu_attn_fwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out, n_out,
-                  offsets.data_ptr(), B, geo.N, geo.max_len, H, dqk, dv, _lib.ptr(ts),
-                  _lib.ptr(pos_w_c), _lib.ptr(ts_w_c), thr.data_ptr(), NUM_BUCKETS,
-                  attn.data_ptr(), hv, st)
+                  offsets.data_ptr(), B, geo.N, geo.max_len, H, dqk, dv, _lib.ptr(bmap),
+                  _lib.ptr(pos_w_c), _lib.ptr(ts_w_c), NUM_BUCKETS, attn.data_ptr(), hv, st)
         attn_stats = torch.empty(rows, 2, dtype=torch.float32, device=dev)
         needs_w_grad = w_o.requires_grad or b_o.requires_grad
         o_in = torch.empty(rows, hv, dtype=torch.float32, device=dev) if needs_w_grad else None
@@ -195,17 +212,18 @@ class STULayerFunction(torch.autograd.Function):
         b_o_c = b_o.contiguous()
         _lib.call("hstu_gate_o_fwd", uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
                   offsets.data_ptr(), B, rows, hv, D, w_o.data_ptr(), b_o_c.data_ptr(),
-                  x.data_ptr(), x.stride(0), geo.eps, geo.dropout_p, seed,
+                  x.data_ptr(), x.stride(0), geo.eps, geo.dropout_p, seed, _lib.ptr(seed_offset),
                   attn_stats.data_ptr(), _lib.ptr(o_in), y.data_ptr(), D, st)
-        ctx.save_for_backward(x, offsets, ts, w_uvqk, w_o, pos_w_c, ts_w_c, x_stats, uvqk,
+        ctx.save_for_backward(x, offsets, bmap, w_uvqk, w_o, pos_w_c, ts_w_c, x_stats, uvqk,
                               h_pre, attn, attn_stats, o_in)
         ctx.geo = geo
         ctx.seed = seed
+        ctx.seed_offset = seed_offset
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        (x, offsets, ts, w_uvqk, w_o, pos_w, ts_w, x_stats, uvqk, h_pre, attn, attn_stats,
+        (x, offsets, bmap, w_uvqk, w_o, pos_w, ts_w, x_stats, uvqk, h_pre, attn, attn_stats,
          o_in) = ctx.saved_tensors
         geo = ctx.geo
         dev = x.device
@@ -221,7 +239,7 @@ class STULayerFunction(torch.autograd.Function):
         _lib.call("hstu_gate_o_bwd", dy.data_ptr(), D, offsets.data_ptr(), B, rows, hv, D,
                   w_o.data_ptr(), uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
                   attn_stats.data_ptr(), _lib.ptr(h_pre), n_out, geo.dropout_p, ctx.seed,
-                  d_uvqk.data_ptr(), n_out, d_attn.data_ptr(), hv, st)
+                  _lib.ptr(ctx.seed_offset), d_uvqk.data_ptr(), n_out, d_attn.data_ptr(), hv, st)
         L = _lib.lib()
         d_w_o = d_b_o = None
         if o_in is not None:
@@ -232,11 +250,10 @@ class STULayerFunction(torch.autograd.Function):
             _lib.call("gr_wgrad", dy.data_ptr(), D, None, o_in.data_ptr(), hv,
                       offsets.data_ptr(), B, rows, D, hv, d_w_o.data_ptr(), d_b_o.data_ptr(),
                       ws.data_ptr(), ws_n, st)
-        thr = bucket_thresholds(dev)
         d_pos_w = d_ts_w = None
         ws_a = None
         ws_a_n = 0
-        if ts is not None:
+        if bmap is not None:
             d_pos_w = torch.empty(2 * geo.N - 1, dtype=torch.float32, device=dev)
             d_ts_w = torch.empty(NUM_BUCKETS + 1, dtype=torch.float32, device=dev)
             ws_a_n = L.hstu_attn_bwd_workspace_size(B, geo.N, geo.max_len, H, NUM_BUCKETS)
@@ -255,7 +272,7 @@ class STULayerFunction(torch.autograd.Function):
         dvv = d_uvqk[:, hv:2 * hv]
         _lib.call("hstu_attn_bwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out, n_out,
                   d_attn.data_ptr(), hv, offsets.data_ptr(), B, geo.N, geo.max_len, H, dqk, dv,
-                  _lib.ptr(ts), _lib.ptr(pos_w), _lib.ptr(ts_w), thr.data_ptr(), NUM_BUCKETS,
+                  _lib.ptr(bmap), _lib.ptr(pos_w), _lib.ptr(ts_w), NUM_BUCKETS,
                   hq_p, hk_p, hv_p, n_out, dq.data_ptr(), dk.data_ptr(), dvv.data_ptr(), n_out,
                   _lib.ptr(d_pos_w), _lib.ptr(d_ts_w), _lib.ptr(ws_a), ws_a_n, st)
         d_w_uvqk = None
@@ -270,13 +287,16 @@ class STULayerFunction(torch.autograd.Function):
         _lib.call("hstu_ln_uvqk_bwd", d_uvqk.data_ptr(), n_out, offsets.data_ptr(), B, rows, D,
                   n_out, w_uvqk.data_ptr(), x.data_ptr(), x.stride(0), x_stats.data_ptr(),
                   dy.data_ptr(), D, dx.data_ptr(), D, st)
-        return (dx, None, None, d_w_uvqk, d_w_o, d_b_o, d_pos_w, d_ts_w, None, None)
+        return (dx, None, None, d_w_uvqk, d_w_o, d_b_o, d_pos_w, d_ts_w, None, None, None)
 
 
-def stu_layer(x, offsets, ts, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGeometry, seed: int = 0):
+def stu_layer(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGeometry, seed: int = 0,
+              seed_offset: Optional[torch.Tensor] = None):
+    """bmap: ``bucket_map(...)`` of the batch, or None for no relative bias.
+    Dropout masks hash (seed + *seed_offset, element); seed_offset is an optional device
+    int64 counter (bumped per forward so that captured graphs draw fresh masks)."""
     _lib.require_gpu(x, offsets, w_uvqk, w_o, b_o)
     if x.dtype != torch.float32:
         raise TypeError("stu_layer: float32 only (the reference runs fp32, hstu.py:592)")
-    if ts is not None:
-        ts = ts.to(torch.int64).contiguous()
-    return STULayerFunction.apply(x, offsets, ts, w_uvqk, w_o, b_o, pos_w, ts_w, geo, int(seed))
+    return STULayerFunction.apply(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo, int(seed),
+                                  seed_offset)

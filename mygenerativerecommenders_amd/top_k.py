@@ -120,6 +120,8 @@ class MIPSBruteForceTopK(TopKModule):
         super().__init__()
         self._cache_key = None
         self._packed: Optional[PackedItems] = None
+        self._ids_key = None
+        self._ids_arange_start: Optional[int] = None
 
     def packed_for(self, item_embeddings_t: torch.Tensor) -> PackedItems:
         key = (item_embeddings_t.data_ptr(), item_embeddings_t._version,
@@ -129,9 +131,26 @@ class MIPSBruteForceTopK(TopKModule):
             self._cache_key = key
         return self._packed
 
+    def _arange_start(self, item_ids: torch.Tensor) -> Optional[int]:
+        """ids == arange(s, s + X)?  Checked once per ids buffer (one host sync, like
+        the reference's per-epoch index refresh); then the kernel derives ids from
+        the catalog index and skips the id gathers."""
+        key = (item_ids.data_ptr(), item_ids._version, item_ids.numel())
+        if self._ids_key != key:
+            flat = item_ids.reshape(-1)
+            start = int(flat[0].item()) if flat.numel() else 0
+            ar = torch.arange(start, start + flat.numel(), device=flat.device, dtype=flat.dtype)
+            self._ids_arange_start = start if bool(torch.equal(flat, ar)) else None
+            self._ids_key = key
+        return self._ids_arange_start
+
     def forward(self, query_embeddings: torch.Tensor, item_embeddings_t: torch.Tensor,
                 item_ids: torch.Tensor, k: int, sorted: bool = True,
                 invalid_ids: Optional[torch.Tensor] = None
                 ) -> Tuple[torch.Tensor, torch.Tensor]:
         packed = self.packed_for(item_embeddings_t)
+        start = self._arange_start(item_ids)
+        if start is not None:
+            return mips_topk(query_embeddings, packed, k, item_ids=None, index_base=start,
+                             invalid_ids=invalid_ids)
         return mips_topk(query_embeddings, packed, k, item_ids=item_ids, invalid_ids=invalid_ids)

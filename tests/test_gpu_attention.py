@@ -51,10 +51,11 @@ def _run_gpu_fwd(offsets, uvqk, ts, pos_w, ts_w, B, N, H, dqk, dv):
     pw = pos_w.to(dev)
     tw = ts_w.to(dev)
     max_len = int((offsets[1:] - offsets[:-1]).max()) if B else 0
+    from mygenerativerecommenders_amd import ops
+    bmap = ops.bucket_map(tsd, offs, N) if tsd is not None else None
     _lib.call("hstu_attn_fwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), u.stride(0), u.stride(0),
-              offs.data_ptr(), B, N, max_len, H, dqk, dv, _lib.ptr(tsd), pw.data_ptr(),
-              tw.data_ptr(), thr.data_ptr(), 128, out.data_ptr(), out.stride(0),
-              _lib.stream_handle())
+              offs.data_ptr(), B, N, max_len, H, dqk, dv, _lib.ptr(bmap), pw.data_ptr(),
+              tw.data_ptr(), 128, out.data_ptr(), out.stride(0), _lib.stream_handle())
     torch.cuda.synchronize()
     return out.cpu()
 
@@ -112,14 +113,17 @@ def _run_gpu_bwd(offsets, uvqk, dout, ts, pos_w, ts_w, B, N, H, dqk, dv, hpre=No
     max_len = int((offsets[1:] - offsets[:-1]).max()) if B else 0
     L = _lib.lib()
     ws_bytes = L.hstu_attn_bwd_workspace_size(B, N, max_len, H, 128)
+    del thr
     ws = torch.empty(max(ws_bytes, 4), dtype=torch.uint8, device=dev)
     hd = hpre.to(dev) if hpre is not None else None
     hq_p = hd[:, 2 * hv:2 * hv + hq].data_ptr() if hd is not None else None
     hk_p = hd[:, 2 * hv + hq:].data_ptr() if hd is not None else None
     hv_p = hd[:, hv:2 * hv].data_ptr() if hd is not None else None
+    from mygenerativerecommenders_amd import ops
+    bmap = ops.bucket_map(tsd, offs, N) if tsd is not None else None
     _lib.call("hstu_attn_bwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), u.stride(0), u.stride(0),
               do.data_ptr(), do.stride(0), offs.data_ptr(), B, N, max_len, H, dqk, dv,
-              _lib.ptr(tsd), pw.data_ptr(), tw.data_ptr(), thr.data_ptr(), 128,
+              _lib.ptr(bmap), pw.data_ptr(), tw.data_ptr(), 128,
               hq_p, hk_p, hv_p, u.stride(0) if hd is not None else 0,
               dq.data_ptr(), dk.data_ptr(), dvv.data_ptr(), d.stride(0),
               dpw.data_ptr(), dtw.data_ptr(), ws.data_ptr(), ws_bytes, _lib.stream_handle())
@@ -181,3 +185,36 @@ def test_attn_bwd_fused_silu_grad():
     _close(b[0], a[0] * sg[:, 2 * hv:3 * hv])
     _close(b[1], a[1] * sg[:, 3 * hv:])
     _close(b[2], a[2] * sg[:, hv:2 * hv])
+
+
+def test_bucket_map_vs_reference_semantics():
+    """Every causal (i, j) bucket of the device map equals the reference bucket fn
+    (hstu.py:579-581 on ts_next(i) - ts(j)), including full-length rows (ts[N-1] wrap)
+    and huge deltas near the clamp."""
+    from mygenerativerecommenders_amd import ops
+    B, N = 3, 130
+    g = torch.Generator().manual_seed(3)
+    lengths = torch.tensor([130, 1, 77])
+    offsets = torch.cat([torch.zeros(1, dtype=torch.int64), torch.cumsum(lengths, 0)])
+    ts = torch.randint(0, 2**40, (B, N), generator=g)
+    ts[0, :64] = torch.cumsum(torch.randint(0, 50, (64,), generator=g), 0)
+    ts[2, 5] = 2**62
+    dev = torch.device("cuda")
+    bmap = ops.bucket_map(ts.to(dev), offsets.to(dev), N).cpu().numpy()
+    T = (N + 63) // 64
+    tpb = T * (T + 1) // 2
+    qk = bmap[: B * tpb * 4096].reshape(B, tpb, 64, 64)
+    kq = bmap[B * tpb * 4096:].reshape(B, tpb, 64, 64)
+    for b in range(B):
+        L = int(lengths[b])
+        ext = torch.cat([ts[b], ts[b, N - 1:N]])
+        for i in range(L):
+            j = torch.arange(i + 1)
+            ref = O.bucket_reference_semantics(ext[i + 1] - ts[b, :i + 1])
+            qt = i // 64
+            for jj in range(i + 1):
+                kt = jj // 64
+                t = qt * (qt + 1) // 2 + kt
+                assert qk[b, t, i % 64, jj % 64] == int(ref[jj]), (b, i, jj)
+                assert kq[b, t, jj % 64, i % 64] == int(ref[jj]), (b, i, jj)
+            del j

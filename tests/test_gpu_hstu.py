@@ -132,7 +132,8 @@ def test_hstu_train_mode_dropout_statistics():
     y = torch.empty(rows, D, device=dev)
     _lib.call("hstu_gate_o_fwd", u.data_ptr(), u.stride(0), attn.data_ptr(), hv,
               offsets.data_ptr(), 1, rows, hv, D, w.data_ptr(), b.data_ptr(), None, 0, 1e-6,
-              0.2, 1234, stats.data_ptr(), o_in.data_ptr(), y.data_ptr(), D, _lib.stream_handle())
+              0.2, 1234, None, stats.data_ptr(), o_in.data_ptr(), y.data_ptr(), D,
+              _lib.stream_handle())
     torch.cuda.synchronize()
     ln = torch.nn.functional.layer_norm(attn, [hv], eps=1e-6)
     full = u[:, :hv] * ln
@@ -141,4 +142,24 @@ def test_hstu_train_mode_dropout_statistics():
     assert abs(frac_drop - 0.2) < 0.01
     assert torch.allclose(o_in[kept], full[kept] / 0.8, rtol=1e-4, atol=1e-5)
     assert torch.allclose(y, o_in @ w.t(), rtol=1e-4, atol=1e-4)
+    # the backward regenerates the same mask from (seed, element)
+    dy = torch.randn(rows, D, device=dev)
+    du = torch.empty(rows, hv, device=dev)
+    da = torch.empty(rows, hv, device=dev)
+    _lib.call("hstu_gate_o_bwd", dy.data_ptr(), D, offsets.data_ptr(), 1, rows, hv, D,
+              w.data_ptr(), u.data_ptr(), u.stride(0), attn.data_ptr(), hv, stats.data_ptr(),
+              None, 0, 0.2, 1234, None, du.data_ptr(), hv, da.data_ptr(), hv,
+              _lib.stream_handle())
+    torch.cuda.synchronize()
+    g = (dy @ w) * kept.float() / 0.8
+    assert torch.allclose(du, g * ln, rtol=1e-4, atol=1e-5)
+    # a device seed offset changes the mask
+    off = torch.tensor([7], dtype=torch.int64, device=dev)
+    o_in2 = torch.empty_like(o_in)
+    _lib.call("hstu_gate_o_fwd", u.data_ptr(), u.stride(0), attn.data_ptr(), hv,
+              offsets.data_ptr(), 1, rows, hv, D, w.data_ptr(), b.data_ptr(), None, 0, 1e-6,
+              0.2, 1234, off.data_ptr(), stats.data_ptr(), o_in2.data_ptr(), y.data_ptr(), D,
+              _lib.stream_handle())
+    torch.cuda.synchronize()
+    assert ((o_in2 != 0) != kept).float().mean().item() > 0.2
     del ops
