@@ -112,17 +112,27 @@ class ShardedCandidateIndex:
             s, i, x = mips_topk(query_embeddings, self.packed, k, item_ids=self.ids,
                                 invalid_ids=invalid_ids, index_base=self.row_offset,
                                 return_index=True)
-        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(self.group) == 1:
-            return i, s
-        P = dist.get_world_size(self.group)
-        gs = [torch.empty_like(s) for _ in range(P)]
-        gi = [torch.empty_like(i) for _ in range(P)]
-        gx = [torch.empty_like(x) for _ in range(P)]
-        dist.all_gather(gs, s, group=self.group)
-        dist.all_gather(gi, i, group=self.group)
-        dist.all_gather(gx, x, group=self.group)
-        ms, mi = merge_topk(torch.stack(gs), torch.stack(gx), torch.stack(gi), k)
-        return mi, ms
+        return gather_and_merge(s, i, x, k, self.group, merge_topk)
+
+
+def gather_and_merge(scores, ids, index, k, group=None, merge_fn=None):
+    """All-gathers every rank's (B, k) local top-k (score, id, global catalog index) and
+    merges them into the global top-k with the canonical order (score desc, index asc).
+    Returns (ids, scores).  ``merge_fn(cand_scores, cand_index, cand_ids, k)`` defaults
+    to the device merge kernel (``mips_merge_topk``)."""
+    if merge_fn is None:
+        from .top_k import merge_topk as merge_fn
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return ids, scores
+    P = dist.get_world_size(group)
+    gs = [torch.empty_like(scores) for _ in range(P)]
+    gi = [torch.empty_like(ids) for _ in range(P)]
+    gx = [torch.empty_like(index) for _ in range(P)]
+    dist.all_gather(gs, scores.contiguous(), group=group)
+    dist.all_gather(gi, ids.contiguous(), group=group)
+    dist.all_gather(gx, index.contiguous(), group=group)
+    ms, mi = merge_fn(torch.stack(gs), torch.stack(gx), torch.stack(gi), k)
+    return mi, ms
 
 
 def shard_bounds(X: int, world: int, rank: int):

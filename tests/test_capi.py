@@ -1,0 +1,78 @@
+"""CPU: the C-ABI library loads, exports exactly what include/gr_hstu.h declares, and
+follows the error convention (non-zero status + thread-local gr_last_error) — all
+without touching a GPU (argument validation runs before any HIP call)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from mygenerativerecommenders_amd import _lib
+
+
+def test_library_loads_and_version():
+    L = _lib.lib()
+    assert L.gr_version() == 2 or L.gr_version() >= 1
+    hdr = open(_lib.HEADER_PATH).read()
+    ver = int(re.search(r"#define GR_HSTU_ABI_VERSION (\d+)", hdr).group(1))
+    assert L.gr_version() == ver
+
+
+def test_exports_match_header():
+    decl = set(_lib.parse_header())
+    assert len(decl) >= 19
+    out = subprocess.check_output(["nm", "-D", "--defined-only", _lib.LIB_PATH], text=True)
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    missing = decl - exported
+    assert not missing, f"declared but not exported: {missing}"
+    extra = {e for e in exported if not e.startswith("_")} - decl
+    assert not extra, f"exported but not declared: {extra}"
+
+
+def test_every_declared_symbol_resolves_with_signature():
+    L = _lib.lib()
+    for name, (ret, args) in _lib.parse_header().items():
+        fn = getattr(L, name)
+        assert len(fn.argtypes) == len(args), name
+
+
+@pytest.mark.parametrize("name,nargs", [("hstu_attn_fwd", 19), ("mips_topk", 16),
+                                        ("hstu_ln_uvqk_fwd", 15), ("gr_wgrad", 15)])
+def test_null_pointer_is_an_error_not_a_crash(name, nargs):
+    L = _lib.lib()
+    _, args = _lib.parse_header()[name]
+    assert len(args) == nargs
+    vals = []
+    for a in args:
+        vals.append(None if a.endswith("*") else 1)
+    rc = getattr(L, name)(*vals)
+    assert rc != 0
+    msg = L.gr_last_error().decode()
+    assert name.split("_")[0] in msg or "null" in msg or "bad" in msg
+
+
+def test_error_is_raised_as_python_exception():
+    _, args = _lib.parse_header()["hstu_attn_fwd"]
+    vals = [None if a.endswith("*") else 1 for a in args]
+    with pytest.raises(_lib.GrError, match="hstu_attn_fwd"):
+        _lib.call("hstu_attn_fwd", *vals)
+
+
+def test_workspace_size_queries_are_host_only():
+    L = _lib.lib()
+    assert L.hstu_attn_bwd_workspace_size(128, 211, 200, 1, 128) == 4 * 128 * 4 * (2 * 211 - 1 + 129)
+    assert L.hstu_bucket_map_bytes(128, 211) == 2 * 128 * 10 * 4096
+    assert L.mips_packed_items_bytes(3953, 50) == 4 * ((3953 + 15) // 16) * 7 * 128
+    assert L.gr_wgrad_workspace_size(27008, 50, 200) > 0
+    assert L.mips_topk_workspace_size(128, 10_000_000, 50, 200) > 0
+    assert L.hstu_attn_bwd_workspace_size(0, 211, 200, 1, 128) == 0
+
+
+def test_library_is_gfx950_code_object():
+    """The fat binary embeds a gfx950 (MI355X) code object and nothing else."""
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+    for other in (b"gfx942", b"gfx90a", b"sm_"):
+        assert b"amdgcn-amd-amdhsa--" + other not in data
+    assert ctypes.sizeof(ctypes.c_void_p) == 8

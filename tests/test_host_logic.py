@@ -1,0 +1,104 @@
+"""CPU: host-side logic of the drop-in modules (construction, parameter / state-dict
+contract with the reference, error behaviour, no silent CPU path)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from mygenerativerecommenders_amd import _lib
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _hstu(**kw):
+    from mygenerativerecommenders_amd.hstu import HSTU
+    args = dict(max_sequence_len=200, max_output_len=11, embedding_dim=50, item_embedding_dim=50,
+                num_blocks=2, num_heads=1, linear_dim=50, attention_dim=50,
+                normalization="rel_bias", linear_config="uvqk", linear_activation="silu",
+                linear_dropout_rate=0.2, attn_dropout_rate=0.0)
+    args.update(kw)
+    return HSTU(**args)
+
+
+def test_state_dict_keys_and_shapes_match_reference():
+    d = np.load(os.path.join(GOLDEN, "hstu_b4_n32_d50_h1.npz"))
+    ref = {k[6:]: d[k].shape for k in d.files if k.startswith("param:")}
+    enc = _hstu(max_sequence_len=32, num_blocks=2)
+    ours = {k: tuple(v.shape) for k, v in enc.state_dict().items() if k != "_attn_mask"}
+    assert ours == {k: tuple(v) for k, v in ref.items()}
+    mask = enc.state_dict()["_attn_mask"]
+    assert mask.dtype == torch.bool and mask.shape == (43, 43)
+    assert torch.equal(mask, torch.triu(torch.ones(43, 43, dtype=torch.bool), 1))
+
+
+def test_parameter_init_statistics_match_reference():
+    torch.manual_seed(0)
+    enc = _hstu(num_blocks=1)
+    layer = enc._hstu._attention_layers[0]
+    assert abs(layer._uvqk.std().item() - 0.02) < 0.002
+    assert abs(layer._rel_attn_bias._ts_w.std().item() - 0.02) < 0.01
+    assert layer._o.weight.shape == (50, 50)
+    # xavier_uniform bound sqrt(6/(50+50))
+    assert layer._o.weight.abs().max().item() <= (6 / 100) ** 0.5 + 1e-6
+    assert layer._rel_attn_bias._pos_w.numel() == 2 * 211 - 1
+
+
+def test_unsupported_configurations_raise():
+    with pytest.raises(ValueError):
+        _hstu(linear_config="uv")
+    enc = _hstu(concat_ua=True)
+    with pytest.raises(NotImplementedError):
+        enc._hstu._attention_layers[0]._geometry(211, 211)
+    enc = _hstu(normalization="softmax_rel_bias")
+    with pytest.raises(NotImplementedError):
+        enc._hstu._attention_layers[0]._geometry(211, 211)
+
+
+def test_cpu_tensors_are_rejected_no_silent_fallback():
+    enc = _hstu(max_sequence_len=8, max_output_len=0, embedding_dim=8, item_embedding_dim=8,
+                linear_dim=8, attention_dim=8)
+    x = torch.randn(2, 8, 8)
+    with pytest.raises((_lib.GrError, RuntimeError)):
+        enc(torch.tensor([8, 3]), x, None, {})
+
+
+def test_bias_module_never_materialises():
+    from mygenerativerecommenders_amd.hstu import RelativeBucketedTimeAndPositionBasedBias
+    from mygenerativerecommenders_amd.hstu import _default_bucketization_fn
+    m = RelativeBucketedTimeAndPositionBasedBias(10, 128, _default_bucketization_fn)
+    assert m._ts_w.shape == (129,) and m._pos_w.shape == (19,)
+    with pytest.raises(NotImplementedError):
+        m(torch.zeros(1, 10, dtype=torch.int64))
+    with pytest.raises(ValueError):
+        RelativeBucketedTimeAndPositionBasedBias(10, 64, _default_bucketization_fn)
+
+
+def test_candidate_index_contract():
+    from mygenerativerecommenders_amd.candidate_index import CandidateIndex
+    from mygenerativerecommenders_amd.top_k import MIPSBruteForceTopK
+    E = torch.randn(1, 30, 8)
+    idx = CandidateIndex(k=500, ids=torch.arange(1, 31), top_k_module=MIPSBruteForceTopK(),
+                         embeddings=E)
+    assert idx._k == 30 and idx.num_objects == 30
+    assert idx.ids.shape == (1, 30)
+    assert torch.equal(idx.embeddings, E)
+    assert idx._embeddings_t.shape == (8, 30)
+    with pytest.raises(TypeError):
+        CandidateIndex(k=5, ids=torch.arange(3), top_k_module=torch.nn.Identity())
+    with pytest.raises(NotImplementedError):
+        idx.filter_invalid_ids(torch.zeros(2, 3, dtype=torch.int64))
+    with pytest.raises((_lib.GrError, RuntimeError)):
+        idx.get_top_k_outputs(torch.randn(2, 8))  # CPU tensors: no CPU path
+
+
+def test_bench_flop_accounting():
+    import bench
+    fwd, dkv, dq = bench.attn_flops(torch.tensor([200, 200]), 1, 50, 50, 4)
+    T = 2 * 200 * 201 / 2
+    assert fwd == 2 * T * 100 and dkv == 2 * T * 150 and dq == 2 * T * 50
+    lengths, x, ts, past_ids, dy = bench.make_batch(4, 200, 11, 50, 0, "cpu")
+    assert x.shape == (4, 211, 50) and ts.shape == (4, 211)
+    # target timestamp sits at index L (features.py:53-57) and padding is 0
+    assert (ts[:, 200] > 0).all() and (ts[:, 201:] == 0).all()
+    assert (past_ids[:, 200:] == 0).all()

@@ -1,0 +1,101 @@
+"""CPU: the oracle restatement against the reference's own recorded outputs
+(tests/golden/*.npz, written by oracle/gen_golden.py from /root/reference).
+
+This pins the oracle: every GPU parity test compares against it (or against the
+goldens directly)."""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import hstu_oracle as O
+from oracle import topk_oracle
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+HSTU_CASES = sorted(glob.glob(os.path.join(GOLDEN, "hstu_*.npz")))
+
+
+def _thr():
+    return np.load(os.path.join(GOLDEN, "bucket_thresholds.npz"))["thresholds"]
+
+
+def test_package_bucket_table_matches_reference_golden():
+    from mygenerativerecommenders_amd.bucket_table import BUCKET_THRESHOLDS, NUM_BUCKETS
+    assert NUM_BUCKETS == 128
+    assert np.array_equal(np.asarray(BUCKET_THRESHOLDS, dtype=np.int64), _thr())
+
+
+def test_bucket_threshold_form_equals_reference_semantics():
+    d = np.load(os.path.join(GOLDEN, "bucket_thresholds.npz"))
+    x = torch.from_numpy(d["probe_x"])
+    ref = torch.from_numpy(d["probe_bucket"])
+    assert torch.equal(O.bucket_via_thresholds(x, d["thresholds"]), ref)
+    assert torch.equal(O.bucket_via_thresholds(-x, d["thresholds"]), ref)
+    assert torch.equal(O.bucket_reference_semantics(x), ref)
+    # random int64 deltas over the whole clamp range
+    g = torch.Generator().manual_seed(0)
+    r = torch.randint(-(2**62), 2**62, (200_000,), generator=g)
+    assert torch.equal(O.bucket_via_thresholds(r, d["thresholds"]),
+                       O.bucket_reference_semantics(r))
+
+
+@pytest.mark.parametrize("path", HSTU_CASES, ids=[os.path.basename(p) for p in HSTU_CASES])
+@pytest.mark.parametrize("variant", ["jagged", "padded"])
+def test_hstu_oracle_vs_reference(path, variant):
+    d = np.load(path)
+    cfg = O.HSTUConfig(N=int(d["N"]), D=int(d["D"]), H=int(d["H"]), dqk=int(d["dqk"]),
+                       dv=int(d["dv"]), concat_ua=bool(d["concat_ua"]))
+    st = {k[6:]: torch.tensor(d[k], requires_grad=True) for k in d.files if k.startswith("param:")}
+    layers = [O.layer_params_from_state(st, i) for i in range(int(d["blocks"]))]
+    x = torch.tensor(d["x"], requires_grad=True)
+    ts = torch.tensor(d["ts"]) if int(d["with_ts"]) else None
+    fn = O.hstu_forward if variant == "jagged" else O.hstu_forward_padded
+    y = fn(torch.tensor(d["lengths"]), x, ts, cfg, layers, _thr())
+    (y * torch.tensor(d["dy"])).sum().backward()
+    assert (y - torch.tensor(d["y"])).abs().max().item() <= 1e-5
+    assert (x.grad - torch.tensor(d["dx"])).abs().max().item() <= 1e-5
+    for k, p in st.items():
+        g = p.grad if p.grad is not None else torch.zeros_like(p)
+        ref = torch.tensor(d["grad:" + k])
+        assert (g - ref).abs().max().item() <= 2e-5 * (1 + ref.abs().max().item()), k
+
+
+@pytest.mark.parametrize("name", ["T1", "T2", "T3_small"])
+def test_topk_oracle_vs_reference(name):
+    d = np.load(os.path.join(GOLDEN, f"topk_{name}.npz"))
+    s, ids, idx = topk_oracle.mips_topk(d["Q"], d["E"], d["ids"], d["invalid"], int(d["k"]))
+    assert np.array_equal(ids, d["top_ids"])
+    if int(d["integer"]):
+        assert np.array_equal(s, d["top_scores"])
+    else:
+        np.testing.assert_allclose(s, d["top_scores"], rtol=1e-6, atol=1e-7)
+    assert np.array_equal(d["ids"][idx], ids)
+
+
+def test_topk_oracle_edge_cases():
+    g = np.random.default_rng(1)
+    Q = g.standard_normal((3, 8), dtype=np.float32)
+    E = np.ones((20, 8), np.float32)  # all ties -> index order
+    s, ids, idx = topk_oracle.mips_topk(Q, E, np.arange(20), None, 5)
+    assert (idx == np.arange(5)[None, :]).all()
+    # fewer valid than k: padded with -inf / -1
+    inv = np.tile(np.arange(18, dtype=np.int64)[None, :], (3, 1))
+    s, ids, idx = topk_oracle.mips_topk(Q, E, np.arange(20), inv, 5)
+    assert (idx[:, :2] == [18, 19]).all() and (idx[:, 2:] == -1).all()
+    assert np.isneginf(s[:, 2:]).all()
+
+
+def test_jagged_ops_golden():
+    """Reference tests/test_ops.py:7-53 known answers, restated in numpy."""
+    d = np.load(os.path.join(GOLDEN, "jagged_ops.npz"))
+    assert np.array_equal(np.concatenate([[0], np.cumsum(d["lengths"])]), d["offsets"])
+    offs = d["offsets"]
+    jag = np.concatenate([d["dense"][b, : offs[b + 1] - offs[b]] for b in range(len(offs) - 1)])
+    assert np.array_equal(jag, d["jagged"])
+    o2 = d["offsets2"]
+    pad = np.zeros((len(o2) - 1, 3, 1), np.float32)
+    for b in range(len(o2) - 1):
+        pad[b, : o2[b + 1] - o2[b]] = d["values"][o2[b]:o2[b + 1]]
+    assert np.array_equal(pad, d["padded"])
