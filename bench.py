@@ -137,6 +137,21 @@ def cpu_baseline_topk(B, X, D, k, N0, budget_s=8.0):
     return B * X / dt, n, dt
 
 
+def _gpu_hold_fn():
+    """Returns hold(ms): enqueue a device spin of about `ms` milliseconds."""
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    cyc = 20_000_000
+    e0.record()
+    torch.cuda._sleep(cyc)
+    e1.record()
+    e1.synchronize()
+    per_ms = cyc / max(e0.elapsed_time(e1), 1e-3)
+
+    def hold(ms):
+        torch.cuda._sleep(int(ms * per_ms))
+    return hold
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -249,42 +264,53 @@ def main():
     ms_per_step = dt / args.steps * 1e3
     seq_per_s = B * world * args.steps / dt
 
-    # per-kernel device time: HIP events around every C-ABI launch over an eager re-run
-    # of the same K steps (kernel bodies are identical to the replayed graph's)
-    timed = ("hstu_bucket_map", "hstu_attn_fwd", "hstu_attn_bwd", "hstu_ln_uvqk_fwd",
-             "hstu_gate_o_fwd", "hstu_gate_o_bwd", "hstu_ln_uvqk_bwd", "gr_wgrad", "mips_topk")
-    for n in timed:
-        _lib.TIMED[n] = []
+    # per-kernel device time: the library records a HIP event pair around every kernel
+    # launch (gr_timing_enable) over an eager re-run of the same K steps — the kernel
+    # bodies are identical to the replayed graph's, only the host gaps differ
+    # A GPU-side spin before each instrumented step lets the host enqueue the whole
+    # step ahead of the device, so every event pair brackets back-to-back device work
+    # (no host launch gap inside a pair).
+    hold = _gpu_hold_fn()
+    _lib.timing_enable(True)
     for _ in range(args.steps):
+        hold(20.0)
         eager_step()
     _sync_barrier(world)
-    kern = {n: sum(a.elapsed_time(b) for a, b in _lib.TIMED[n]) / max(1, len(_lib.TIMED[n]))
-            for n in timed}
-    kern_total = {n: sum(a.elapsed_time(b) for a, b in _lib.TIMED[n]) / args.steps for n in timed}
-    _lib.TIMED.clear()
+    _lib.timing_enable(False)
+    ktimes = _lib.kernel_times()
+    kern = {n: (t / c if c else 0.0) for n, (t, c) in ktimes.items()}
+    kern_total = {n: t / args.steps for n, (t, c) in ktimes.items() if c}
 
-    # ---- roofline of the dominant kernel (largest per-step device time)
+    # ---- roofline of the dominant kernel (largest device time per step)
     peaks = peak_table()
     fwd_f, dkv_f, dq_f = attn_flops(lengths.cpu(), 1, D, D, blocks)
-    dominant = max(kern_total, key=kern_total.get)
-    flops_per_launch = {"hstu_attn_fwd": fwd_f, "hstu_attn_bwd": dkv_f + dq_f}
     rows = B * N0
     nout = 4 * D
-    gemm = {
-        "hstu_ln_uvqk_fwd": 2.0 * rows * D * nout,
-        "hstu_gate_o_fwd": 2.0 * rows * D * D,
-        "hstu_gate_o_bwd": 2.0 * rows * D * D,
-        "hstu_ln_uvqk_bwd": 2.0 * rows * nout * D,
-        "gr_wgrad": (2.0 * rows * D * D + 2.0 * rows * D * nout) / 2.0,  # avg of the two launches
+    flops_per_launch = {
+        "attn_fwd": fwd_f, "attn_bwd_dkv": dkv_f, "attn_bwd_dq": dq_f,
+        "ln_uvqk_fwd": 2.0 * rows * D * nout, "gate_o_fwd": 2.0 * rows * D * D,
+        "gate_o_bwd": 2.0 * rows * D * D, "ln_uvqk_bwd": 2.0 * rows * nout * D,
+        "wgrad_partial": (2.0 * rows * D * D + 2.0 * rows * D * nout) / 2.0,
     }
-    flops_per_launch.update(gemm)
+    dominant = max(kern_total, key=kern_total.get)
     ach = flops_per_launch.get(dominant, 0.0) / (kern[dominant] * 1e-3) / 1e12 if kern[dominant] else 0.0
+    traffic, traffic_src = None, None
+    pmc_path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_latest.json")
+    if os.path.exists(pmc_path):
+        pmc = json.load(open(pmc_path))
+        ent = pmc.get("kernels", {}).get(dominant)
+        if ent:
+            traffic = ent["hbm_bytes_per_launch"]
+            traffic_src = pmc.get("source")
     roofline = {"kernel": dominant, "bound": "mfma", "achieved": round(ach, 3),
                 "peak": peaks["fp32_mfma_tflops"], "unit": "TFLOP/s",
-                "frac": round(ach / peaks["fp32_mfma_tflops"], 4), "traffic": None,
+                "frac": round(ach / peaks["fp32_mfma_tflops"], 4), "traffic": traffic,
+                "traffic_source": traffic_src,
                 "avg_launch_ms": round(kern[dominant], 5),
                 "flops_per_launch": flops_per_launch.get(dominant, 0.0),
-                "per_step_device_ms": {k: round(v, 4) for k, v in kern_total.items()}}
+                "per_step_device_ms": {k: round(v, 4) for k, v in sorted(
+                    kern_total.items(), key=lambda kv: -kv[1])},
+                "per_step_device_ms_total": round(sum(kern_total.values()), 4)}
 
     # ---- retrieval leg (C4): 10M items row-sharded over the ranks
     retrieval = None
@@ -306,14 +332,22 @@ def main():
         for _ in range(3):
             sidx.get_top_k_outputs(Q, invalid_ids=inv)
         _sync_barrier(world)
-        _lib.TIMED["mips_topk"] = []
         t1 = time.perf_counter()
         for _ in range(args.retrieval_steps):
             sidx.get_top_k_outputs(Q, invalid_ids=inv)
         _sync_barrier(world)
         dtr = time.perf_counter() - t1
-        ktop = sum(a_.elapsed_time(b_) for a_, b_ in _lib.TIMED["mips_topk"]) / max(1, len(_lib.TIMED["mips_topk"]))
-        _lib.TIMED.clear()
+        # per-kernel durations from a separate instrumented pass (the timed loop above
+        # carries no event overhead)
+        _lib.timing_enable(True)
+        for _ in range(args.retrieval_steps):
+            hold(5.0)
+            sidx.get_top_k_outputs(Q, invalid_ids=inv)
+        _sync_barrier(world)
+        _lib.timing_enable(False)
+        rt = _lib.kernel_times(("mips_select", "mips_merge", "mips_pack"))
+        ktop = rt["mips_select"][0] / max(1, rt["mips_select"][1])
+        kmerge = rt["mips_merge"][0] / max(1, rt["mips_merge"][1])
         dtr = _max_over_ranks(dtr, world)
         cand_per_s = B * X * args.retrieval_steps / dtr
         fl = 2.0 * B * (b - a) * D
@@ -324,10 +358,11 @@ def main():
             "config": {"workload": "C4: 10M-item catalog row-sharded, B=128 queries, k=200, "
                                    "211 invalid ids, all-gather + device merge",
                        "items": X, "queries": B, "k": args.k, "dim": D},
-            "roofline": {"kernel": "mips_topk (select + merge launches)", "bound": "mfma",
+            "roofline": {"kernel": "mips_select", "bound": "mfma",
                          "achieved": round(ach_r, 3), "peak": peaks["fp32_mfma_tflops"],
                          "unit": "TFLOP/s", "frac": round(ach_r / peaks["fp32_mfma_tflops"], 4),
                          "traffic": None, "avg_launch_ms": round(ktop, 4),
+                         "merge_avg_launch_ms": round(kmerge, 4),
                          "flops_per_launch": fl},
         }
 

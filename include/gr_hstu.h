@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GR_HSTU_ABI_VERSION 1
+#define GR_HSTU_ABI_VERSION 2
 
 #ifndef GR_API
 #define GR_API __attribute__((visibility("default")))
@@ -36,6 +36,18 @@ extern "C" {
 GR_API const char* gr_last_error(void);
 /* Returns GR_HSTU_ABI_VERSION. */
 GR_API int gr_version(void);
+
+/* Live per-kernel timing (measurement only; off by default).  When enabled, every
+ * launch records a HIP event pair on its stream; gr_timing_query(kernel, ...) waits
+ * for and drains that kernel's pairs, returning the summed device time and launch
+ * count.  Kernel names: bucket_map, attn_fwd, attn_bwd_dkv, attn_bwd_dq,
+ * attn_bias_reduce, ln_uvqk_fwd, gate_o_fwd, gate_o_bwd, ln_uvqk_bwd, wgrad_partial,
+ * wgrad_reduce, mips_pack, mips_select, mips_merge, cumsum, dense_to_jagged,
+ * jagged_to_padded.  Not for use inside a captured graph.
+ */
+GR_API int gr_timing_enable(int on);
+GR_API int gr_timing_query(const char* kernel, double* total_ms, int* launches);
+GR_API int gr_timing_reset(void);
 
 /* ---------------------------------------------------------------- jagged layout
  * Replaces utils/ops.py:18-38 asynchronous_complete_cumsum:

@@ -84,29 +84,38 @@ class GrError(RuntimeError):
     pass
 
 
-# Optional live per-entry-point timing (bench.py): name -> list of (start, end) events
-# recorded on torch's current stream, which is the stream every entry point is
-# launched on.
-TIMED: dict = {}
-
-
 def call(name: str, *args):
     """Calls a C-ABI entry point; raises GrError(gr_last_error()) on non-zero status."""
     L = lib()
-    rec = TIMED.get(name)
-    if rec is not None:
-        import torch as _t
-        e0 = _t.cuda.Event(enable_timing=True)
-        e1 = _t.cuda.Event(enable_timing=True)
-        e0.record()
-        rc = getattr(L, name)(*args)
-        e1.record()
-        rec.append((e0, e1))
-    else:
-        rc = getattr(L, name)(*args)
+    rc = getattr(L, name)(*args)
     if rc != 0:
         msg = L.gr_last_error().decode(errors="replace")
         raise GrError(f"{name} failed (status {rc}): {msg}")
+
+
+KERNEL_NAMES = ("bucket_map", "attn_fwd", "attn_bwd_dkv", "attn_bwd_dq", "attn_bias_reduce",
+                "ln_uvqk_fwd", "gate_o_fwd", "gate_o_bwd", "ln_uvqk_bwd", "wgrad_partial",
+                "wgrad_reduce", "mips_pack", "mips_select", "mips_merge", "cumsum",
+                "dense_to_jagged", "jagged_to_padded")
+
+
+def timing_enable(on: bool = True):
+    """Library-level live kernel timing (HIP event pair around every launch)."""
+    lib().gr_timing_enable(1 if on else 0)
+
+
+def kernel_times(names=KERNEL_NAMES) -> dict:
+    """Drains the recorded event pairs: {kernel: (total_ms, launches)}."""
+    L = lib()
+    out = {}
+    for n in names:
+        ms = ctypes.c_double(0.0)
+        cnt = ctypes.c_int(0)
+        rc = L.gr_timing_query(n.encode(), ctypes.byref(ms), ctypes.byref(cnt))
+        if rc != 0:
+            raise GrError(L.gr_last_error().decode())
+        out[n] = (ms.value, cnt.value)
+    return out
 
 
 def ptr(t) -> int | None:

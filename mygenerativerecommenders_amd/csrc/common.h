@@ -22,6 +22,28 @@ const char* last_error();
     }                                        \
   } while (0)
 
+// ---------------------------------------------------------------- live kernel timing
+// When enabled (gr_timing_enable), every launch site records a HIP event pair on the
+// launch stream; gr_timing_query drains and sums them per kernel name.
+bool timing_enabled();
+void timing_push(const char* name, hipEvent_t start, hipEvent_t stop);
+
+#define GR_TIMED(name, stream, ...)                                          \
+  do {                                                                       \
+    hipEvent_t e0_ = nullptr, e1_ = nullptr;                                 \
+    const bool tm_ = ::gr::timing_enabled();                                 \
+    if (tm_) {                                                               \
+      (void)hipEventCreate(&e0_);                                            \
+      (void)hipEventCreate(&e1_);                                            \
+      (void)hipEventRecord(e0_, (stream));                                   \
+    }                                                                        \
+    __VA_ARGS__;                                                             \
+    if (tm_) {                                                               \
+      (void)hipEventRecord(e1_, (stream));                                   \
+      ::gr::timing_push((name), e0_, e1_);                                   \
+    }                                                                        \
+  } while (0)
+
 #define GR_LAUNCH_CHECK(what)                                                   \
   do {                                                                          \
     hipError_t e_ = hipGetLastError();                                          \

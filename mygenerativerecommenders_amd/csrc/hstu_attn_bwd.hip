@@ -470,13 +470,13 @@ static int launch_bwd(const AttnBwdArgs& a, float* dpos_w, float* dts_w, hipStre
   const size_t lds_q = sizeof(float) * (64 * C::LDQ + 64 * LDV_Q) + tail;
   GR_REQUIRE(lds_kv <= 160 * 1024 && lds_q <= 160 * 1024,
              "hstu_attn_bwd: LDS (%zu, %zu B) exceeds 160 KiB (N=%d)", lds_kv, lds_q, a.N);
-  hipLaunchKernelGGL((attn_bwd_dkv_kernel<KS, VT>), dim3(grid), dim3(256), lds_kv, st, a);
+  GR_TIMED("attn_bwd_dkv", st, hipLaunchKernelGGL((attn_bwd_dkv_kernel<KS, VT>), dim3(grid), dim3(256), lds_kv, st, a));
   GR_LAUNCH_CHECK("hstu_attn_bwd(dkv)");
-  hipLaunchKernelGGL((attn_bwd_dq_kernel<KS, VT>), dim3(grid), dim3(256), lds_q, st, a);
+  GR_TIMED("attn_bwd_dq", st, hipLaunchKernelGGL((attn_bwd_dq_kernel<KS, VT>), dim3(grid), dim3(256), lds_q, st, a));
   GR_LAUNCH_CHECK("hstu_attn_bwd(dq)");
   if (a.map_kq) {
-    hipLaunchKernelGGL(bias_grad_reduce_kernel, dim3(ceil_div(nbins, 64)), dim3(256), 0, st,
-                       a.slabs, grid, 2 * a.N - 1, a.nb + 1, dpos_w, dts_w);
+    GR_TIMED("attn_bias_reduce", st, hipLaunchKernelGGL(bias_grad_reduce_kernel, dim3(ceil_div(nbins, 64)), dim3(256), 0, st,
+                       a.slabs, grid, 2 * a.N - 1, a.nb + 1, dpos_w, dts_w));
     GR_LAUNCH_CHECK("hstu_attn_bwd(bias reduce)");
   }
   return 0;

@@ -176,7 +176,7 @@ static int launch_fwd(const AttnFwdArgs& a, int grid, hipStream_t st) {
   using C = AttnFwdCfg<KS, VT>;
   size_t lds = sizeof(float) * (C::LDS_FLOATS + a.nb + 1 + 2 * a.N - 1);
   GR_REQUIRE(lds <= 160 * 1024, "hstu_attn_fwd: LDS %zu B exceeds 160 KiB (N=%d)", lds, a.N);
-  hipLaunchKernelGGL((hstu_attn_fwd_kernel<KS, VT>), dim3(grid), dim3(256), lds, st, a);
+  GR_TIMED("attn_fwd", st, hipLaunchKernelGGL((hstu_attn_fwd_kernel<KS, VT>), dim3(grid), dim3(256), lds, st, a));
   GR_LAUNCH_CHECK("hstu_attn_fwd");
   return 0;
 }

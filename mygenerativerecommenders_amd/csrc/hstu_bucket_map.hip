@@ -100,8 +100,8 @@ extern "C" int hstu_bucket_map(const int64_t* ts, const int64_t* offsets, int B,
   if (B == 0) return 0;
   const int tpb = gr::tiles_per_seq(N);
   uint8_t* map_kq = map + (size_t)B * tpb * 4096;
-  hipLaunchKernelGGL(gr::bucket_map_kernel, dim3(B * tpb), dim3(256), 0, (hipStream_t)stream, ts,
-                     offsets, B, N, bucket_thr, num_buckets, map, map_kq);
+  GR_TIMED("bucket_map", (hipStream_t)stream, hipLaunchKernelGGL(gr::bucket_map_kernel, dim3(B * tpb), dim3(256), 0, (hipStream_t)stream, ts,
+                     offsets, B, N, bucket_thr, num_buckets, map, map_kq));
   GR_LAUNCH_CHECK("hstu_bucket_map");
   return 0;
 }

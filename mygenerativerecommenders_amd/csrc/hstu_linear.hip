@@ -439,9 +439,11 @@ static int launch_rowpanel(const Op& op, int64_t max_rows, bool full_row, const 
   const int panels = ceil_div(op.N, nt * 16);
   dim3 grid((unsigned)((max_rows + BM - 1) / BM), (unsigned)panels);
   if (grid.x == 0) return 0;
-#define GR_NT_CASE(NT_)                                                            \
-  case NT_:                                                                        \
-    hipLaunchKernelGGL((rowpanel_kernel<NT_, Op>), grid, dim3(256), 0, st, op);    \
+  const char* tname = name + 5;  // "hstu_ln_uvqk_fwd" -> "ln_uvqk_fwd"
+#define GR_NT_CASE(NT_)                                                                     \
+  case NT_:                                                                                 \
+    GR_TIMED(tname, st, hipLaunchKernelGGL((rowpanel_kernel<NT_, Op>), grid, dim3(256), 0,  \
+                                           st, op));                                        \
     break;
   switch (nt) {
     GR_NT_CASE(1) GR_NT_CASE(2) GR_NT_CASE(3) GR_NT_CASE(4) GR_NT_CASE(5) GR_NT_CASE(6)
@@ -722,19 +724,19 @@ extern "C" int gr_wgrad(const float* a, int64_t lda, const float* a_stats, const
               pnb, slabs, cs};
   const dim3 grid(n_chunks, panels);
   switch (wgrad_nt(Nb)) {
-    case 4: hipLaunchKernelGGL(wgrad_partial_kernel<4>, grid, dim3(256), 0, st, g); break;
-    case 8: hipLaunchKernelGGL(wgrad_partial_kernel<8>, grid, dim3(256), 0, st, g); break;
-    case 13: hipLaunchKernelGGL(wgrad_partial_kernel<13>, grid, dim3(256), 0, st, g); break;
-    default: hipLaunchKernelGGL(wgrad_partial_kernel<16>, grid, dim3(256), 0, st, g); break;
+    case 4: GR_TIMED("wgrad_partial", st, hipLaunchKernelGGL(wgrad_partial_kernel<4>, grid, dim3(256), 0, st, g)); break;
+    case 8: GR_TIMED("wgrad_partial", st, hipLaunchKernelGGL(wgrad_partial_kernel<8>, grid, dim3(256), 0, st, g)); break;
+    case 13: GR_TIMED("wgrad_partial", st, hipLaunchKernelGGL(wgrad_partial_kernel<13>, grid, dim3(256), 0, st, g)); break;
+    default: GR_TIMED("wgrad_partial", st, hipLaunchKernelGGL(wgrad_partial_kernel<16>, grid, dim3(256), 0, st, g)); break;
   }
   GR_LAUNCH_CHECK("gr_wgrad(partial)");
   const int64_t ne = (int64_t)Ka * Nb;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((ne + 63) / 64)), dim3(256), 0, st,
-                     slabs, n_chunks, ne, c);
+  GR_TIMED("wgrad_reduce", st, hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((ne + 63) / 64)), dim3(256), 0, st,
+                     slabs, n_chunks, ne, c));
   GR_LAUNCH_CHECK("gr_wgrad(reduce)");
   if (a_colsum) {
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((Ka + 63) / 64)), dim3(256), 0,
-                       st, cs, n_chunks, (int64_t)Ka, a_colsum);
+    GR_TIMED("wgrad_reduce", st, hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((Ka + 63) / 64)), dim3(256), 0,
+                       st, cs, n_chunks, (int64_t)Ka, a_colsum));
     GR_LAUNCH_CHECK("gr_wgrad(colsum)");
   }
   return 0;

@@ -67,8 +67,8 @@ extern "C" {
 
 int gr_complete_cumsum(const int64_t* lengths, int B, int64_t* offsets, void* stream) {
   GR_REQUIRE(offsets && (B == 0 || lengths) && B >= 0, "gr_complete_cumsum: bad args");
-  hipLaunchKernelGGL(gr::cumsum_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, lengths,
-                     B, offsets);
+  GR_TIMED("cumsum", (hipStream_t)stream, hipLaunchKernelGGL(gr::cumsum_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, lengths,
+                     B, offsets));
   GR_LAUNCH_CHECK("gr_complete_cumsum");
   return 0;
 }
@@ -80,8 +80,8 @@ int gr_dense_to_jagged(const float* dense, const int64_t* offsets, int B, int N,
              "gr_dense_to_jagged: bad args");
   const int64_t rows = (int64_t)B * N;
   if (rows == 0) return 0;
-  hipLaunchKernelGGL(gr::dense_to_jagged_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256),
-                     0, (hipStream_t)stream, dense, offsets, B, N, D, jagged);
+  GR_TIMED("dense_to_jagged", (hipStream_t)stream, hipLaunchKernelGGL(gr::dense_to_jagged_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256),
+                     0, (hipStream_t)stream, dense, offsets, B, N, D, jagged));
   GR_LAUNCH_CHECK("gr_dense_to_jagged");
   return 0;
 }
@@ -92,8 +92,8 @@ int gr_jagged_to_padded(const float* jagged, const int64_t* offsets, int B, int 
              "gr_jagged_to_padded: bad args");
   const int64_t rows = (int64_t)B * N;
   if (rows == 0) return 0;
-  hipLaunchKernelGGL(gr::jagged_to_padded_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256),
-                     0, (hipStream_t)stream, jagged, offsets, B, N, D, dense);
+  GR_TIMED("jagged_to_padded", (hipStream_t)stream, hipLaunchKernelGGL(gr::jagged_to_padded_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256),
+                     0, (hipStream_t)stream, jagged, offsets, B, N, D, dense));
   GR_LAUNCH_CHECK("gr_jagged_to_padded");
   return 0;
 }

@@ -626,7 +626,7 @@ static int launch_select(const SelectArgs& a, hipStream_t st) {
   const int n_qg = ceil_div(a.B, QG);
   const int n_r8 = ceil_div(a.n_ranges, 8) * 8;
   const int grid = n_r8 * n_qg;
-  hipLaunchKernelGGL((mips_select_kernel<KS, BLOCKS>), dim3(grid), dim3(256), 0, st, a);
+  GR_TIMED("mips_select", st, hipLaunchKernelGGL((mips_select_kernel<KS, BLOCKS>), dim3(grid), dim3(256), 0, st, a));
   GR_LAUNCH_CHECK("mips_topk(select)");
   return 0;
 }
@@ -644,8 +644,8 @@ extern "C" int mips_pack_items(const float* items, int64_t X, int D, float* pack
   GR_REQUIRE(items && packed && X >= 0 && D > 0, "mips_pack_items: bad args");
   if (X == 0) return 0;
   const int KS2 = (ceil_div(D, 4) + 1) / 2;
-  hipLaunchKernelGGL(pack_items_kernel, dim3(2048), dim3(256), 0, (hipStream_t)stream, items, X,
-                     D, KS2, packed);
+  GR_TIMED("mips_pack", (hipStream_t)stream, hipLaunchKernelGGL(pack_items_kernel, dim3(2048), dim3(256), 0, (hipStream_t)stream, items, X,
+                     D, KS2, packed));
   GR_LAUNCH_CHECK("mips_pack_items");
   return 0;
 }
@@ -688,7 +688,7 @@ extern "C" int mips_topk(const float* queries, const float* packed_items, int64_
   if (rc) return rc;
   MergeArgs m{part_score, part_index, nullptr, p.n_ranges, B, p.k_part, k, item_ids, index_base,
               out_scores, out_ids, out_index};
-  hipLaunchKernelGGL(mips_merge_kernel, dim3(B), dim3(256), 0, st, m);
+  GR_TIMED("mips_merge", st, hipLaunchKernelGGL(mips_merge_kernel, dim3(B), dim3(256), 0, st, m));
   GR_LAUNCH_CHECK("mips_topk(merge)");
   return 0;
 }
@@ -704,7 +704,7 @@ extern "C" int mips_merge_topk(const float* cand_scores, const int64_t* cand_ind
   if (B == 0) return 0;
   MergeArgs m{cand_scores, cand_index, cand_ids, n_lists, B, k_in, k, nullptr, 0,
               out_scores, out_ids, out_index};
-  hipLaunchKernelGGL(mips_merge_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, m);
+  GR_TIMED("mips_merge", (hipStream_t)stream, hipLaunchKernelGGL(mips_merge_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, m));
   GR_LAUNCH_CHECK("mips_merge_topk");
   return 0;
 }
