@@ -48,7 +48,11 @@ class CandidateIndex(torch.nn.Module):
         return self._ids.size(1)
 
     @property
-    def embeddings(self) -> torch.Tensor:
+    def embeddings(self) -> Optional[torch.Tensor]:
+        """(1, X, D) view (candidate_index.py:45-51); None before update_embeddings(),
+        which is what Retrieval.retrieve tests for (retrieval.py:34)."""
+        if self._embeddings_t is None:
+            return None
         return self._embeddings_t.unsqueeze(2).permute(2, 1, 0).squeeze(2)
 
     def filter_invalid_ids(self, invalid_ids: torch.Tensor) -> "CandidateIndex":
