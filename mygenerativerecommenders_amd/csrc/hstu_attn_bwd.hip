@@ -49,8 +49,11 @@ struct AttnBwdArgs {
   float inv_n;
 };
 
-template <int KSTEPS, int VTILES>
+// TT = rows per streamed LDS tile (queries in dK/dV, keys in dQ): 64, or 16 for the
+// wide head dims (d > 128) where a 64-row register stage would not fit.
+template <int KSTEPS, int VTILES, int TT>
 struct AttnBwdCfg {
+  static constexpr int TB = TT / 16;             // 16-row blocks per tile
   static constexpr int KP = KSTEPS * 4;          // padded dqk (k-steps of the QK product)
   static constexpr int KT = (KP + 15) / 16;      // 16-col tiles of dK / dQ
   static constexpr int KPT = KT * 16;            // dqk padded to the output tile width
@@ -68,13 +71,13 @@ __device__ __forceinline__ float silu_grad_masked(const float* h, int64_t idx, b
 }
 
 // ------------------------------------------------------------------ key-major: dK, dV
-template <int KSTEPS, int VTILES>
+template <int KSTEPS, int VTILES, int TT>
 __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
-  using C = AttnBwdCfg<KSTEPS, VTILES>;
+  using C = AttnBwdCfg<KSTEPS, VTILES, TT>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* Qs = reinterpret_cast<float*>(smem);  // [64][LDQ]
-  float* Ds = Qs + 64 * C::LDQ;                // dO tile [64][LDV]
-  float* tsw = Ds + 64 * C::LDV;               // nb + 1
+  float* Qs = reinterpret_cast<float*>(smem);  // [TT][LDQ]
+  float* Ds = Qs + TT * C::LDQ;                // dO tile [TT][LDV]
+  float* tsw = Ds + TT * C::LDV;               // nb + 1
   float* posw = tsw + (a.nb + 1);              // 2N - 1
   const int nbins = 2 * a.N - 1 + a.nb + 1;
   float* hist = posw + (2 * a.N - 1);          // [4 waves][nbins]
@@ -139,31 +142,31 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
 #pragma unroll
   for (int t = 0; t < C::KT; ++t) dK[t] = f4_zero();
 
-  TileStage<C::KPT> qst;
-  TileStage<C::VP> dst;
-  uint32_t mw[4], mwn[4];
-  auto load_tile = [&](int qt, uint32_t (&m)[4]) {
-    qst.load(a.q, a.ld_qk, s0, qt * 64, L, h * a.dqk, a.dqk);
-    dst.load(a.dout, a.ld_dout, s0, qt * 64, L, h * a.dv, a.dv);
-    const int64_t tb = map_seq + (int64_t)attn_tile_id(qt, kt) * 1024 + map_lane;
+  TileStage<C::KPT, TT> qst;
+  TileStage<C::VP, TT> dst;
+  uint32_t mw[C::TB], mwn[C::TB];
+  auto load_tile = [&](int qt, uint32_t (&m)[C::TB]) {
+    qst.load(a.q, a.ld_qk, s0, qt * TT, L, h * a.dqk, a.dqk);
+    dst.load(a.dout, a.ld_dout, s0, qt * TT, L, h * a.dv, a.dv);
 #pragma unroll
-    for (int qb = 0; qb < 4; ++qb) m[qb] = has_bias ? mapw[tb + qb * 4] : 0u;
+    for (int qb = 0; qb < C::TB; ++qb)
+      m[qb] = has_bias ? mapw[map_block_word(map_seq, qt * TT + qb * 16, k0, map_lane, false)] : 0u;
   };
 
   const int wk_lo = k0 + w * 16;
-  const int last_qt = (L - 1) / 64;
+  const int last_qt = (L - 1) / TT;
   int run_b = 0;
   float run_s = 0.f;
-  load_tile(kt, mw);
+  load_tile(k0 / TT, mw);
   qst.store(Qs, C::LDQ);
   dst.store(Ds, C::LDV);
   __syncthreads();
-  for (int qt = kt; qt <= last_qt; ++qt) {
-    const int q0 = qt * 64;
+  for (int qt = k0 / TT; qt <= last_qt; ++qt) {
+    const int q0 = qt * TT;
     const bool more = qt < last_qt;
     if (more) load_tile(qt + 1, mwn);
 #pragma unroll
-    for (int qb = 0; qb < 4; ++qb) {
+    for (int qb = 0; qb < C::TB; ++qb) {
       const int qb0 = q0 + qb * 16;
       if (qb0 >= L) break;                // past the sequence
       if (qb0 + 15 < wk_lo) continue;     // all queries before this wave's keys
@@ -246,7 +249,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
       qst.store(Qs, C::LDQ);
       dst.store(Ds, C::LDV);
 #pragma unroll
-      for (int qb = 0; qb < 4; ++qb) mw[qb] = mwn[qb];
+      for (int qb = 0; qb < C::TB; ++qb) mw[qb] = mwn[qb];
       lds_barrier();
     }
   }
@@ -283,15 +286,15 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
 }
 
 // ------------------------------------------------------------------ query-major: dQ
-template <int KSTEPS, int VTILES>
+template <int KSTEPS, int VTILES, int TT>
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
-  using C = AttnBwdCfg<KSTEPS, VTILES>;
+  using C = AttnBwdCfg<KSTEPS, VTILES, TT>;
   constexpr int LDK = C::LDQ;
   constexpr int LDV = 32 * ((C::VP - 2 + 31) / 32) + 2;  // A-operand reads only
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* Ks = reinterpret_cast<float*>(smem);  // [64][LDK]
-  float* Vs = Ks + 64 * LDK;                   // [64][LDV]
-  float* tsw = Vs + 64 * LDV;
+  float* Ks = reinterpret_cast<float*>(smem);  // [TT][LDK]
+  float* Vs = Ks + TT * LDK;                   // [TT][LDV]
+  float* tsw = Vs + TT * LDV;
   float* posw = tsw + (a.nb + 1);
 
   const int BH = a.B * a.H;
@@ -342,27 +345,28 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   for (int t = 0; t < C::KT; ++t) dQ[t] = f4_zero();
   const int wq_lo = q0 + w * 16;
 
-  TileStage<C::KPT> kst;
-  TileStage<C::VP> vst;
-  uint32_t mw[4], mwn[4];
-  auto load_tile = [&](int kt, uint32_t (&m)[4]) {
-    kst.load(a.k, a.ld_qk, s0, kt * 64, L, h * a.dqk, a.dqk);
-    vst.load(a.v, a.ld_v, s0, kt * 64, L, h * a.dv, a.dv);
-    const int64_t tb = map_seq + (int64_t)attn_tile_id(qt, kt) * 1024 + map_lane;
+  TileStage<C::KPT, TT> kst;
+  TileStage<C::VP, TT> vst;
+  uint32_t mw[C::TB], mwn[C::TB];
+  auto load_tile = [&](int kt, uint32_t (&m)[C::TB]) {
+    kst.load(a.k, a.ld_qk, s0, kt * TT, L, h * a.dqk, a.dqk);
+    vst.load(a.v, a.ld_v, s0, kt * TT, L, h * a.dv, a.dv);
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb) m[kb] = has_bias ? mapw[tb + kb * 4] : 0u;
+    for (int kb = 0; kb < C::TB; ++kb)
+      m[kb] = has_bias ? mapw[map_block_word(map_seq, q0, kt * TT + kb * 16, map_lane, true)] : 0u;
   };
   load_tile(0, mw);
   kst.store(Ks, LDK);
   vst.store(Vs, LDV);
   __syncthreads();
 
-  for (int kt = 0; kt <= qt; ++kt) {
-    const int k0 = kt * 64;
-    const bool more = kt < qt;
+  const int last_kt = min(q0 + 63, L - 1) / TT;
+  for (int kt = 0; kt <= last_kt; ++kt) {
+    const int k0 = kt * TT;
+    const bool more = kt < last_kt;
     if (more) load_tile(kt + 1, mwn);
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
+    for (int kb = 0; kb < C::TB; ++kb) {
       const int kb0 = k0 + kb * 16;
       if (kb0 > wq_lo + 15 || kb0 >= L) break;
       f4 s = f4_zero(), dpt = f4_zero();
@@ -401,7 +405,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
       kst.store(Ks, LDK);
       vst.store(Vs, LDV);
 #pragma unroll
-      for (int kb = 0; kb < 4; ++kb) mw[kb] = mwn[kb];
+      for (int kb = 0; kb < C::TB; ++kb) mw[kb] = mwn[kb];
       lds_barrier();
     }
   }
@@ -458,21 +462,21 @@ static size_t bwd_slab_bytes(int B, int N, int max_len, int H, int nb) {
   return sizeof(float) * (size_t)n_tiles * B * H * (size_t)(2 * N - 1 + nb + 1);
 }
 
-template <int KS, int VT>
+template <int KS, int VT, int TT = 64>
 static int launch_bwd(const AttnBwdArgs& a, float* dpos_w, float* dts_w, hipStream_t st) {
-  using C = AttnBwdCfg<KS, VT>;
+  using C = AttnBwdCfg<KS, VT, TT>;
   const int grid = a.n_tiles * a.B * a.H;
   const int nbins = 2 * a.N - 1 + a.nb + 1;
   const size_t tail = sizeof(float) * (a.nb + 1 + 2 * a.N - 1);
-  const size_t lds_kv = sizeof(float) * (64 * C::LDQ + 64 * C::LDV) + tail +
+  const size_t lds_kv = sizeof(float) * (TT * C::LDQ + TT * C::LDV) + tail +
                         (a.map_kq ? sizeof(float) * (4 * nbins + 4 * 16 * 17) : 0);
   constexpr int LDV_Q = 32 * ((C::VP - 2 + 31) / 32) + 2;
-  const size_t lds_q = sizeof(float) * (64 * C::LDQ + 64 * LDV_Q) + tail;
+  const size_t lds_q = sizeof(float) * (TT * C::LDQ + TT * LDV_Q) + tail;
   GR_REQUIRE(lds_kv <= 160 * 1024 && lds_q <= 160 * 1024,
              "hstu_attn_bwd: LDS (%zu, %zu B) exceeds 160 KiB (N=%d)", lds_kv, lds_q, a.N);
-  GR_TIMED("attn_bwd_dkv", st, hipLaunchKernelGGL((attn_bwd_dkv_kernel<KS, VT>), dim3(grid), dim3(256), lds_kv, st, a));
+  GR_TIMED("attn_bwd_dkv", st, hipLaunchKernelGGL((attn_bwd_dkv_kernel<KS, VT, TT>), dim3(grid), dim3(256), lds_kv, st, a));
   GR_LAUNCH_CHECK("hstu_attn_bwd(dkv)");
-  GR_TIMED("attn_bwd_dq", st, hipLaunchKernelGGL((attn_bwd_dq_kernel<KS, VT>), dim3(grid), dim3(256), lds_q, st, a));
+  GR_TIMED("attn_bwd_dq", st, hipLaunchKernelGGL((attn_bwd_dq_kernel<KS, VT, TT>), dim3(grid), dim3(256), lds_q, st, a));
   GR_LAUNCH_CHECK("hstu_attn_bwd(dq)");
   if (a.map_kq) {
     GR_TIMED("attn_bias_reduce", st, hipLaunchKernelGGL(bias_grad_reduce_kernel, dim3(ceil_div(nbins, 64)), dim3(256), 0, st,
@@ -502,7 +506,7 @@ extern "C" int hstu_attn_bwd(const float* q, const float* k, const float* v, int
   GR_REQUIRE(q && k && v && dout && offsets && dq && dk && dvv, "hstu_attn_bwd: null pointer");
   GR_REQUIRE(B >= 0 && N > 0 && H > 0 && dqk > 0 && dv > 0, "hstu_attn_bwd: bad sizes");
   GR_REQUIRE(max_len >= 0 && max_len <= N, "hstu_attn_bwd: max_len %d not in [0, N=%d]", max_len, N);
-  GR_REQUIRE(dqk <= 128 && dv <= 128, "hstu_attn_bwd: dqk/dv > 128 unsupported (%d, %d)", dqk, dv);
+  GR_REQUIRE(dqk <= 256 && dv <= 256, "hstu_attn_bwd: dqk/dv > 256 unsupported (%d, %d)", dqk, dv);
   GR_REQUIRE((hq == nullptr) == (hk == nullptr) && (hk == nullptr) == (hv == nullptr),
              "hstu_attn_bwd: hq/hk/hv must be all given or all NULL");
   if (bucket_map) {
@@ -531,5 +535,6 @@ extern "C" int hstu_attn_bwd(const float* q, const float* k, const float* v, int
   if (d <= 32) return launch_bwd<8, 2>(a, dpos_w, dts_w, st);
   if (d <= 52) return launch_bwd<13, 4>(a, dpos_w, dts_w, st);
   if (d <= 64) return launch_bwd<16, 4>(a, dpos_w, dts_w, st);
-  return launch_bwd<32, 8>(a, dpos_w, dts_w, st);
+  if (d <= 128) return launch_bwd<32, 8>(a, dpos_w, dts_w, st);
+  return launch_bwd<64, 16, 16>(a, dpos_w, dts_w, st);
 }

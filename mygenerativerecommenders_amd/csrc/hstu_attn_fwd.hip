@@ -37,22 +37,25 @@ struct AttnFwdArgs {
   float inv_n;
 };
 
-template <int KSTEPS, int VTILES>
+// TK = keys per LDS tile (64, or 16 for the wide head dims where a 64-key register
+// stage would not fit next to the Q fragments and accumulators).
+template <int KSTEPS, int VTILES, int TK>
 struct AttnFwdCfg {
   static constexpr int KP = KSTEPS * 4;                      // padded dqk
   static constexpr int VP = VTILES * 16;                     // padded dv
   static constexpr int LDK = 32 * ((KP - 2 + 31) / 32) + 2;  // == 2 mod 32: conflict-free A reads
   static constexpr int LDV = VP + 4;                         // == 4 mod 8: conflict-free B reads
-  static constexpr int LDS_FLOATS = 64 * LDK + 64 * LDV;
+  static constexpr int LDS_FLOATS = TK * LDK + TK * LDV;
+  static constexpr int KB = TK / 16;                         // 16-key blocks per tile
 };
 
-template <int KSTEPS, int VTILES>
+template <int KSTEPS, int VTILES, int TK>
 __global__ __launch_bounds__(256) void hstu_attn_fwd_kernel(AttnFwdArgs a) {
-  using C = AttnFwdCfg<KSTEPS, VTILES>;
+  using C = AttnFwdCfg<KSTEPS, VTILES, TK>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* Ks = reinterpret_cast<float*>(smem);
-  float* Vs = Ks + 64 * C::LDK;
-  float* tsw = Vs + 64 * C::LDV;   // nb + 1
+  float* Vs = Ks + TK * C::LDK;
+  float* tsw = Vs + TK * C::LDV;   // nb + 1
   float* posw = tsw + (a.nb + 1);  // 2N - 1
 
   const int BH = a.B * a.H;
@@ -96,15 +99,15 @@ __global__ __launch_bounds__(256) void hstu_attn_fwd_kernel(AttnFwdArgs a) {
 #pragma unroll
   for (int ct = 0; ct < VTILES; ++ct) acc[ct] = f4_zero();
 
-  TileStage<C::KP> kst;
-  TileStage<C::VP> vst;
-  uint32_t mw[4], mwn[4];
-  auto load_tile = [&](int kt, uint32_t (&m)[4]) {
-    kst.load(a.k, a.ld_qk, s0, kt * 64, L, h * a.dqk, a.dqk);
-    vst.load(a.v, a.ld_v, s0, kt * 64, L, h * a.dv, a.dv);
-    const int64_t tb = map_seq + (int64_t)attn_tile_id(qt, kt) * 1024 + map_lane;
+  TileStage<C::KP, TK> kst;
+  TileStage<C::VP, TK> vst;
+  uint32_t mw[C::KB], mwn[C::KB];
+  auto load_tile = [&](int kt, uint32_t (&m)[C::KB]) {
+    kst.load(a.k, a.ld_qk, s0, kt * TK, L, h * a.dqk, a.dqk);
+    vst.load(a.v, a.ld_v, s0, kt * TK, L, h * a.dv, a.dv);
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb) m[kb] = has_bias ? mapw[tb + kb * 4] : 0u;
+    for (int kb = 0; kb < C::KB; ++kb)
+      m[kb] = has_bias ? mapw[map_block_word(map_seq, q0, kt * TK + kb * 16, map_lane, true)] : 0u;
   };
 
   load_tile(0, mw);
@@ -113,12 +116,13 @@ __global__ __launch_bounds__(256) void hstu_attn_fwd_kernel(AttnFwdArgs a) {
   __syncthreads();  // also publishes tsw / posw
 
   const int wq_lo = q0 + w * 16;  // first query of this wave
-  for (int kt = 0; kt <= qt; ++kt) {
-    const int k0 = kt * 64;
-    const bool more = kt < qt;
+  const int last_kt = min(q0 + 63, L - 1) / TK;
+  for (int kt = 0; kt <= last_kt; ++kt) {
+    const int k0 = kt * TK;
+    const bool more = kt < last_kt;
     if (more) load_tile(kt + 1, mwn);
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
+    for (int kb = 0; kb < C::KB; ++kb) {
       const int kb0 = k0 + kb * 16;
       if (kb0 > wq_lo + 15 || kb0 >= L) break;  // wave-uniform causal / length skip
       f4 s = f4_zero();
@@ -152,7 +156,7 @@ __global__ __launch_bounds__(256) void hstu_attn_fwd_kernel(AttnFwdArgs a) {
       kst.store(Ks, C::LDK);
       vst.store(Vs, C::LDV);
 #pragma unroll
-      for (int kb = 0; kb < 4; ++kb) mw[kb] = mwn[kb];
+      for (int kb = 0; kb < C::KB; ++kb) mw[kb] = mwn[kb];
       lds_barrier();
     }
   }
@@ -171,12 +175,12 @@ __global__ __launch_bounds__(256) void hstu_attn_fwd_kernel(AttnFwdArgs a) {
   }
 }
 
-template <int KS, int VT>
+template <int KS, int VT, int TK = 64>
 static int launch_fwd(const AttnFwdArgs& a, int grid, hipStream_t st) {
-  using C = AttnFwdCfg<KS, VT>;
+  using C = AttnFwdCfg<KS, VT, TK>;
   size_t lds = sizeof(float) * (C::LDS_FLOATS + a.nb + 1 + 2 * a.N - 1);
   GR_REQUIRE(lds <= 160 * 1024, "hstu_attn_fwd: LDS %zu B exceeds 160 KiB (N=%d)", lds, a.N);
-  GR_TIMED("attn_fwd", st, hipLaunchKernelGGL((hstu_attn_fwd_kernel<KS, VT>), dim3(grid), dim3(256), lds, st, a));
+  GR_TIMED("attn_fwd", st, hipLaunchKernelGGL((hstu_attn_fwd_kernel<KS, VT, TK>), dim3(grid), dim3(256), lds, st, a));
   GR_LAUNCH_CHECK("hstu_attn_fwd");
   return 0;
 }
@@ -192,7 +196,7 @@ extern "C" int hstu_attn_fwd(const float* q, const float* k, const float* v, int
   GR_REQUIRE(q && k && v && offsets && out, "hstu_attn_fwd: null pointer");
   GR_REQUIRE(B >= 0 && N > 0 && H > 0 && dqk > 0 && dv > 0, "hstu_attn_fwd: bad sizes");
   GR_REQUIRE(max_len >= 0 && max_len <= N, "hstu_attn_fwd: max_len %d not in [0, N=%d]", max_len, N);
-  GR_REQUIRE(dqk <= 128 && dv <= 128, "hstu_attn_fwd: dqk/dv > 128 unsupported (%d, %d)", dqk, dv);
+  GR_REQUIRE(dqk <= 256 && dv <= 256, "hstu_attn_fwd: dqk/dv > 256 unsupported (%d, %d)", dqk, dv);
   GR_REQUIRE(!bucket_map || (pos_w && ts_w && num_buckets > 0 && num_buckets < 256),
              "hstu_attn_fwd: bucket_map given without pos_w/ts_w");
   if (B == 0 || max_len == 0) return 0;
@@ -207,5 +211,6 @@ extern "C" int hstu_attn_fwd(const float* q, const float* k, const float* v, int
   if (d <= 32) return launch_fwd<8, 2>(a, grid, st);
   if (d <= 52) return launch_fwd<13, 4>(a, grid, st);
   if (d <= 64) return launch_fwd<16, 4>(a, grid, st);
-  return launch_fwd<32, 8>(a, grid, st);
+  if (d <= 128) return launch_fwd<32, 8>(a, grid, st);
+  return launch_fwd<64, 16, 16>(a, grid, st);
 }

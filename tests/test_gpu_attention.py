@@ -68,6 +68,9 @@ def _run_gpu_fwd(offsets, uvqk, ts, pos_w, ts_w, B, N, H, dqk, dv):
     (3, 130, 2, 8, 8, False),
     (2, 150, 1, 64, 64, True),
     (2, 100, 1, 128, 96, True),
+    (2, 150, 1, 256, 256, True),   # wide (C3 head dim): 16-key LDS tiles
+    (2, 90, 1, 200, 136, True),
+    (2, 70, 2, 160, 160, False),
 ])
 def test_attn_fwd_vs_oracle(B, N, H, dqk, dv, with_ts):
     lengths, offsets, uvqk, ts, pos_w, ts_w = _case(B * 7 + N, B, N, H, dqk, dv,
@@ -146,6 +149,9 @@ def _close(got, ref, rel=3e-5):
     (3, 130, 2, 8, 8, False),
     (2, 150, 1, 64, 64, True),
     (2, 100, 1, 128, 96, True),
+    (2, 150, 1, 256, 256, True),
+    (2, 90, 1, 200, 136, True),
+    (2, 70, 2, 160, 160, False),
 ])
 def test_attn_bwd_vs_oracle(B, N, H, dqk, dv, with_ts):
     lengths, offsets, uvqk, ts, pos_w, ts_w = _case(B * 11 + N, B, N, H, dqk, dv,
@@ -169,6 +175,32 @@ def test_attn_bwd_vs_oracle(B, N, H, dqk, dv, with_ts):
     if with_ts:
         _close(dpw, pw.grad, rel=1e-4)
         _close(dtw, tw.grad, rel=1e-4)
+
+
+def test_attn_c3_full_length():
+    """C3 geometry: one full-length ml-20m sequence (N = 2059, d = 256) plus a short one,
+    forward and backward against the oracle."""
+    B, N, H, d = 2, 2059, 1, 256
+    lengths, offsets, uvqk, ts, pos_w, ts_w = _case(23, B, N, H, d, d, lengths=[2059, 777],
+                                                    scale=0.5)
+    hv = H * d
+    uv = uvqk.clone().requires_grad_(True)
+    pw = pos_w.clone().requires_grad_(True)
+    tw = ts_w.clone().requires_grad_(True)
+    q, k, v = uv[:, 2 * hv:3 * hv], uv[:, 3 * hv:], uv[:, hv:2 * hv]
+    cfg = O.HSTUConfig(N=N, D=1, H=H, dqk=d, dv=d)
+    ref = O.hstu_attention_jagged(q, k, v, offsets, ts, cfg, pw, tw, _thr())
+    got = _run_gpu_fwd(offsets, uvqk, ts, pos_w, ts_w, B, N, H, d, d)
+    _close(got, ref.detach())
+    g = torch.Generator().manual_seed(7)
+    dout = torch.randn(ref.shape, generator=g)
+    (ref * dout).sum().backward()
+    dq, dk, dvv, dpw, dtw = _run_gpu_bwd(offsets, uvqk, dout, ts, pos_w, ts_w, B, N, H, d, d)
+    _close(dq, uv.grad[:, 2 * hv:3 * hv])
+    _close(dk, uv.grad[:, 3 * hv:])
+    _close(dvv, uv.grad[:, hv:2 * hv])
+    _close(dpw, pw.grad, rel=1e-4)
+    _close(dtw, tw.grad, rel=1e-4)
 
 
 def test_attn_bwd_fused_silu_grad():

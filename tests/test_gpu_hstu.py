@@ -70,15 +70,18 @@ def test_hstu_vs_reference_golden(name):
         _close(g, ref, 2e-4, "grad " + pname)
 
 
-def test_hstu_ml1m_shape_vs_oracle():
-    """ml-1m geometry (N = 211, D = 50, 4 blocks), jagged lengths U[20, 200], eval."""
+@pytest.mark.parametrize("B,N0,out_len,D,blocks,H,dh,min_len", [
+    (8, 200, 11, 50, 4, 1, 50, 20),     # ml-1m geometry (C2), jagged lengths U[20, 200]
+    (2, 500, 11, 256, 2, 1, 256, 200),  # ml-20m-like width (C3: D = d = 256), 8 key tiles
+    (2, 300, 11, 256, 1, 2, 128, 100),  # C3 variant h = 2, d = 128
+])
+def test_hstu_shapes_vs_oracle(B, N0, out_len, D, blocks, H, dh, min_len):
     from mygenerativerecommenders_amd.hstu import HSTU
     torch.manual_seed(0)
-    B, N0, out_len, D, blocks = 8, 200, 11, 50, 4
     N = N0 + out_len
     enc = HSTU(max_sequence_len=N0, max_output_len=out_len, embedding_dim=D,
-               item_embedding_dim=D, num_blocks=blocks, num_heads=1, linear_dim=D,
-               attention_dim=D, normalization="rel_bias", linear_config="uvqk",
+               item_embedding_dim=D, num_blocks=blocks, num_heads=H, linear_dim=dh,
+               attention_dim=dh, normalization="rel_bias", linear_config="uvqk",
                linear_activation="silu", linear_dropout_rate=0.2, attn_dropout_rate=0.0)
     g = torch.Generator().manual_seed(1)
     with torch.no_grad():
@@ -86,7 +89,7 @@ def test_hstu_ml1m_shape_vs_oracle():
             layer._rel_attn_bias._ts_w.normal_(0, 0.3, generator=g)
             layer._rel_attn_bias._pos_w.normal_(0, 0.3, generator=g)
     enc.eval()
-    lengths = torch.randint(20, N0 + 1, (B,), generator=g)
+    lengths = torch.randint(min_len, N0 + 1, (B,), generator=g)
     x = torch.randn(B, N, D, generator=g)
     ts = torch.zeros(B, N, dtype=torch.int64)
     for b in range(B):
@@ -94,7 +97,7 @@ def test_hstu_ml1m_shape_vs_oracle():
         ts[b, :L + 1] = 1_000_000_000 + torch.cumsum((torch.rand(L + 1, generator=g) * 2e5).long(), 0)
     thr = np.asarray(__import__("mygenerativerecommenders_amd.bucket_table",
                                 fromlist=["x"]).BUCKET_THRESHOLDS)
-    cfg = O.HSTUConfig(N=N, D=D, H=1, dqk=D, dv=D)
+    cfg = O.HSTUConfig(N=N, D=D, H=H, dqk=dh, dv=dh)
     st = {k: v.detach().clone().requires_grad_(True) for k, v in enc.state_dict().items()
           if k != "_attn_mask"}
     layers = [O.layer_params_from_state(st, i) for i in range(blocks)]
