@@ -15,7 +15,8 @@ import torch  # noqa: F401  (import first: its HIP runtime is the one the .so bi
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
-LIB_PATH = os.path.join(PKG_DIR, "libgr_hstu.so")
+# GR_HSTU_LIB selects an alternative build of the same library (kernel experiments).
+LIB_PATH = os.environ.get("GR_HSTU_LIB") or os.path.join(PKG_DIR, "libgr_hstu.so")
 HEADER_PATH = os.path.join(REPO_DIR, "include", "gr_hstu.h")
 
 _CTYPES = {

@@ -22,40 +22,68 @@ __device__ __forceinline__ int64_t map_block_word(int64_t map_seq, int q, int k,
   return map_seq + (int64_t)t * 1024 + lane_off + sub * 4;
 }
 
-// Register-staged ROWS-row tile of a jagged column block: rows [r0, r0 + ROWS) of a
-// (rows, ld) matrix, columns [c0, c0 + ncols) zero-padded to CP, rows >= L zero.
-// Loads are unconditional (clamped) and issued together; store() writes LDS.
-template <int CP, int ROWS = 64>
-struct TileStage {
-  static constexpr int PER = (ROWS * CP + 255) / 256;
+// Wave-uniform buffer descriptor over one sequence's rows of a column block:
+// element (r, c) of the block sits at byte ((r * ld) + c) * 4 from `base + s0*ld + c0`.
+// The record count ends exactly after column ncols-1 of row L-1, so every load of a row
+// >= L (and of the padding columns of the last row) returns 0 in hardware — no clamping.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t seq_rsrc(const float* base, int64_t ld,
+                                                          int64_t s0, int c0, int L, int ncols) {
+  const float* p = base + s0 * ld + c0;
+  const int64_t bytes = L > 0 ? ((int64_t)(L - 1) * ld + ncols) * 4 : 0;
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, (int)(bytes < 0x7fffffff ? bytes : 0x7fffffff),
+                                           0x00020000);
+}
+__device__ __forceinline__ float buf_ld(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+__device__ __forceinline__ uint32_t buf_ld_u32(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0);
+}
+
+// Register-staged ROWS x CP tile of a jagged column block, loaded through a seq_rsrc
+// descriptor.  Thread t owns column c_t = t % CPR (CPR = CP rounded up to a power of
+// two) of rows r_t + RPP * i: one voffset VGPR per thread, the row step is an SGPR
+// soffset, rows past the sequence come back as 0 from the range check.
+template <int CP, int ROWS>
+struct BufTile {
+  static constexpr int CPR = CP <= 16 ? 16 : CP <= 32 ? 32 : CP <= 64 ? 64 : CP <= 128 ? 128 : 256;
+  static constexpr int RPP = 256 / CPR;  // rows per pass
+  static constexpr int PER = (ROWS + RPP - 1) / RPP;
   float v[PER];
-  __device__ __forceinline__ void load(const float* base, int64_t ld, int64_t s0, int r0, int L,
-                                       int c0, int ncols) {
-    gptr<float> g = as_global(base);
+  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t r, int64_t ld, int r0, int ncols) {
     const int tid = threadIdx.x;
+    const int c = tid % CPR, rr = tid / CPR;
+    const int voff = ((r0 + rr) * (int)ld + c) * 4;
+    const int step = RPP * (int)ld * 4;
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
-      const int e = tid + 256 * i;
-      const int r = e / CP, c = e - (e / CP) * CP;
-      const int row = r0 + r;
-      const bool ok = e < ROWS * CP && row < L && c < ncols;
-      const int rc = row < L ? row : L - 1;
-      const int cc = c < ncols ? c : ncols - 1;
-      const float x = g[(s0 + rc) * ld + c0 + cc];
-      v[i] = ok ? x : 0.f;
+      const float x = buf_ld(r, voff, i * step);
+      v[i] = c < ncols ? x : 0.f;
     }
   }
   __device__ __forceinline__ void store(float* lds, int ldl) const {
     const int tid = threadIdx.x;
+    const int c = tid % CPR, rr = tid / CPR;
+    if (c < CP) {
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int e = tid + 256 * i;
-      if (e < ROWS * CP) {
-        const int r = e / CP, c = e - (e / CP) * CP;
-        lds[r * ldl + c] = v[i];
-      }
+      for (int i = 0; i < PER; ++i)
+        if (RPP * PER == ROWS || rr + RPP * i < ROWS) lds[(rr + RPP * i) * ldl + c] = v[i];
     }
   }
 };
+
+// Bucket-map descriptor for sequence b (tiles of 4096 bytes; records = 0 when there is
+// no map, so every map load returns bucket 0).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t map_rsrc(const uint8_t* map, int b, int tpb) {
+  const uint8_t* p = map ? map + (int64_t)b * tpb * 4096 : nullptr;
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, map ? tpb * 4096 : 0, 0x00020000);
+}
+// soffset (bytes) of the map word for the 16 x 16 block (q, k) (multiples of 16) in the
+// query-major (or key-major) orientation; the lane part is lane_off * 4.
+__device__ __forceinline__ int map_soff(int q, int k, bool query_major) {
+  const int t = attn_tile_id(q >> 6, k >> 6);
+  const int sub = query_major ? ((k & 63) >> 4) : ((q & 63) >> 4);
+  return (t * 1024 + sub * 4) * 4;
+}
 
 }  // namespace gr

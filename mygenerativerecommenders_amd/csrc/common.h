@@ -5,6 +5,8 @@
 #include <stdint.h>
 
 #include <cstdarg>
+#include <cstdlib>
+#include <initializer_list>
 #include <cstdio>
 #include <string>
 
@@ -121,6 +123,10 @@ __device__ __forceinline__ float2 ld_f2(const float2* p, int64_t i) {
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
+
+// Wave index as a scalar (threadIdx-derived values are otherwise divergent to hipcc,
+// which turns wave-uniform loop exits into exec-mask branches).
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
 __host__ __device__ inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
 

@@ -58,7 +58,6 @@ struct AttnBwdCfg {
   static constexpr int KT = (KP + 15) / 16;      // 16-col tiles of dK / dQ
   static constexpr int KPT = KT * 16;            // dqk padded to the output tile width
   static constexpr int VP = VTILES * 16;         // padded dv
-  static constexpr int VSTEPS = VP / 4;          // k-steps of the dO V^T product
   // row strides: == 4 mod 8 keeps the 4-row-apart B reads conflict-free; the 16-row
   // A reads are then 2-way (LDS is not the limiter at 32-cycle MFMAs).
   static constexpr int LDQ = KPT + 4;
@@ -71,6 +70,22 @@ __device__ __forceinline__ float silu_grad_masked(const float* h, int64_t idx, b
 }
 
 // ------------------------------------------------------------------ key-major: dK, dV
+// Per 16 x 16 (query, key) block a wave computes S and dP (A = Q / dO rows from LDS,
+// B = its keys' K^T / V^T fragments in VGPRs), the elementwise P / dS in registers
+// (branch-free; wave-uniform block skips are scalar branches), the relative-bias
+// gradients as LDS float adds into the wave's private histograms (dpos: one add per
+// element, <= 4-way address conflicts; dts: equal consecutive buckets of a lane merged
+// first), then dV += P^T dO and dK += dS^T Q (k-step r = queries 4g + r).
+#ifndef GR_DPOS_ROT
+#define GR_DPOS_ROT 1
+#endif
+#ifndef GR_DTS_COPIES
+#define GR_DTS_COPIES 16
+#endif
+// dts_w histogram: GR_DTS_COPIES copies per wave (lane lr uses copy lr % copies) so
+// lanes hitting the same bucket mostly hit different addresses; stride == 1 mod 32.
+__host__ __device__ constexpr int dts_stride(int nb1) { return ((nb1 + 30) / 32) * 32 + 1; }
+
 template <int KSTEPS, int VTILES, int TT>
 __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
   using C = AttnBwdCfg<KSTEPS, VTILES, TT>;
@@ -79,9 +94,11 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
   float* Ds = Qs + TT * C::LDQ;                // dO tile [TT][LDV]
   float* tsw = Ds + TT * C::LDV;               // nb + 1
   float* posw = tsw + (a.nb + 1);              // 2N - 1
-  const int nbins = 2 * a.N - 1 + a.nb + 1;
-  float* hist = posw + (2 * a.N - 1);          // [4 waves][nbins]
-  float* dsblk = hist + 4 * nbins;             // [4 waves][16][17] dS block
+  const int npos = 2 * a.N - 1;
+  const int nbins = npos + a.nb + 1;
+  const int tss = dts_stride(a.nb + 1);
+  const int wbins = npos + GR_DTS_COPIES * tss;  // per wave: dpos bins, dts copies
+  float* hist = posw + npos;                   // [4 waves][wbins]
 
   const int BH = a.B * a.H;
   const int id = blockIdx.x;
@@ -93,7 +110,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
   const int k0 = kt * 64;
   const bool has_bias = a.map_kq != nullptr;
   float* slab = a.slabs ? a.slabs + (int64_t)id * nbins : nullptr;
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int tid = threadIdx.x, w = wave_id(), lane = tid & 63;
   const int lr = lane & 15, lg = lane >> 4;
 
   if (k0 >= L) {  // this workgroup still owns a (zero) slab
@@ -103,15 +120,18 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
   }
   if (has_bias) {
     for (int i = tid; i <= a.nb; i += 256) tsw[i] = a.ts_w[i];
-    for (int i = tid; i < 2 * a.N - 1; i += 256) posw[i] = a.pos_w[i];
-    for (int i = tid; i < 4 * nbins; i += 256) hist[i] = 0.f;
+    for (int i = tid; i < npos; i += 256) posw[i] = a.pos_w[i];
+    for (int i = tid; i < 4 * wbins; i += 256) hist[i] = 0.f;
   }
-  float* whist = hist + w * nbins;
+  float* whist = hist + w * wbins;
+  float* wts = whist + npos + (lr % GR_DTS_COPIES) * tss;
+  float carry = 0.f;   // dpos: diagonal partial sums handed to the next block
+  int last_db = 0;
 
   // this lane's key (as the column of S and dP) and its K^T / V^T fragments
   const int kj = k0 + w * 16 + lr;
   const bool k_ok = kj < L;
-  float kreg[KSTEPS], vreg[C::VSTEPS];
+  float kreg[KSTEPS], vreg[KSTEPS];
   {
     const int64_t row = s0 + (k_ok ? kj : L - 1);
     gptr<float> krow = as_global(a.k) + row * a.ld_qk + h * a.dqk;
@@ -121,20 +141,14 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
       const int d = 4 * st + lg;
       const float x = krow[d < a.dqk ? d : a.dqk - 1];
       kreg[st] = d < a.dqk ? x : 0.f;
-    }
-#pragma unroll
-    for (int st = 0; st < C::VSTEPS; ++st) {
-      const int d = 4 * st + lg;
-      const float x = vrow[d < a.dv ? d : a.dv - 1];
-      vreg[st] = d < a.dv ? x : 0.f;
+      const float y = vrow[d < a.dv ? d : a.dv - 1];
+      vreg[st] = d < a.dv ? y : 0.f;
     }
   }
-  const int vsteps = (a.dv + 3) / 4;
-  const int tpb = attn_tiles_per_seq(a.N);
-  gptr<uint32_t> mapw =
-      as_global(reinterpret_cast<const uint32_t*>(a.map_kq ? a.map_kq : (const uint8_t*)a.q));
-  const int64_t map_seq = (int64_t)b * tpb * 1024;
-  const int map_lane = (w * 16 + lr) * 16 + lg;  // + qb * 4
+  const __amdgpu_buffer_rsrc_t rmap = map_rsrc(a.map_kq, b, attn_tiles_per_seq(a.N));
+  const int map_voff = ((w * 16 + lr) * 16 + lg) * 4;
+  const __amdgpu_buffer_rsrc_t rq = seq_rsrc(a.q, a.ld_qk, s0, h * a.dqk, L, a.dqk);
+  const __amdgpu_buffer_rsrc_t rdo = seq_rsrc(a.dout, a.ld_dout, s0, h * a.dv, L, a.dv);
 
   f4 dV[VTILES], dK[C::KT];
 #pragma unroll
@@ -142,21 +156,19 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
 #pragma unroll
   for (int t = 0; t < C::KT; ++t) dK[t] = f4_zero();
 
-  TileStage<C::KPT, TT> qst;
-  TileStage<C::VP, TT> dst;
+  BufTile<C::KPT, TT> qst;
+  BufTile<C::VP, TT> dst;
   uint32_t mw[C::TB], mwn[C::TB];
   auto load_tile = [&](int qt, uint32_t (&m)[C::TB]) {
-    qst.load(a.q, a.ld_qk, s0, qt * TT, L, h * a.dqk, a.dqk);
-    dst.load(a.dout, a.ld_dout, s0, qt * TT, L, h * a.dv, a.dv);
+    qst.load(rq, a.ld_qk, qt * TT, a.dqk);
+    dst.load(rdo, a.ld_dout, qt * TT, a.dv);
 #pragma unroll
     for (int qb = 0; qb < C::TB; ++qb)
-      m[qb] = has_bias ? mapw[map_block_word(map_seq, qt * TT + qb * 16, k0, map_lane, false)] : 0u;
+      m[qb] = buf_ld_u32(rmap, map_voff, map_soff(qt * TT + qb * 16, k0, false));
   };
 
   const int wk_lo = k0 + w * 16;
   const int last_qt = (L - 1) / TT;
-  int run_b = 0;
-  float run_s = 0.f;
   load_tile(k0 / TT, mw);
   qst.store(Qs, C::LDQ);
   dst.store(Ds, C::LDV);
@@ -168,80 +180,84 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
 #pragma unroll
     for (int qb = 0; qb < C::TB; ++qb) {
       const int qb0 = q0 + qb * 16;
-      if (qb0 >= L) break;                // past the sequence
-      if (qb0 + 15 < wk_lo) continue;     // all queries before this wave's keys
-      // S[query 4lg + r][key lr] and dP alike
-      f4 s = f4_zero(), dp = f4_zero();
-      const float* qrow = Qs + (qb * 16 + lr) * C::LDQ + lg;
+      if (qb0 < L && qb0 + 15 >= wk_lo) {  // wave-uniform: inside the sequence, causal
+        // S[query 4lg + r][key lr] and dP alike
+        f4 s = f4_zero(), dp = f4_zero();
+        const float* qrow = Qs + (qb * 16 + lr) * C::LDQ + lg;
+        const float* drow = Ds + (qb * 16 + lr) * C::LDV + lg;
 #pragma unroll
-      for (int st = 0; st < KSTEPS; ++st) s = mfma16x16x4(qrow[4 * st], kreg[st], s);
-      const float* drow = Ds + (qb * 16 + lr) * C::LDV + lg;
+        for (int st = 0; st < KSTEPS; ++st) {
+          s = mfma16x16x4(qrow[4 * st], kreg[st], s);
+          dp = mfma16x16x4(drow[4 * st], vreg[st], dp);
+        }
+        float p[4], ds[4];
+        int bk[4];
 #pragma unroll
-      for (int st = 0; st < C::VSTEPS; ++st)
-        if (st < vsteps) dp = mfma16x16x4(drow[4 * st], vreg[st], dp);
-      float p[4], ds[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int qi = qb0 + 4 * lg + r;
-        const bool ok = k_ok && qi < L && kj <= qi;
-        float x = s[r];
-        int bucket = 0, pi = 0;
+        for (int r = 0; r < 4; ++r) {
+          const int qi = qb0 + 4 * lg + r;
+          const bool ok = k_ok && qi < L && kj <= qi;
+          float x = s[r];
+          int pi = a.N - 1 + kj - qi;
+          pi = pi < 0 ? 0 : (pi > npos - 1 ? npos - 1 : pi);
+          bk[r] = (mw[qb] >> (8 * r)) & 0xFF;
+          if (has_bias) x = x + (posw[pi] + tsw[bk[r]]);
+          const float sg = sigmoidf_(x);
+          p[r] = ok ? x * sg * a.inv_n : 0.f;
+          ds[r] = ok ? dp[r] * (sg * (1.0f + x * (1.0f - sg))) * a.inv_n : 0.f;
+#if !GR_DPOS_ROT
+          if (has_bias) atomicAdd(&whist[pi], ds[r]);  // dpos_w (masked: adds 0)
+#endif
+        }
+#if GR_DPOS_ROT
         if (has_bias) {
-          bucket = (mw[qb] >> (8 * r)) & 0xFF;
-          pi = a.N - 1 + kj - qi;
-          pi = pi < 0 ? 0 : (pi > 2 * a.N - 2 ? 2 * a.N - 2 : pi);
-          x = x + (posw[pi] + tsw[bucket]);
-        }
-        const float sg = sigmoidf_(x);
-        p[r] = ok ? x * sg * a.inv_n : 0.f;
-        ds[r] = ok ? dp[r] * (sg * (1.0f + x * (1.0f - sg))) * a.inv_n : 0.f;
-        if (has_bias) {
-          // dts_w: run-length accumulation in registers (for a fixed key the bucket is
-          // non-decreasing in the query index when timestamps are sorted) — one LDS
-          // atomic per bucket change instead of one per element
-          if (ok && bucket != run_b) {
-            if (run_s != 0.f) atomicAdd(&whist[2 * a.N - 1 + run_b], run_s);
-            run_b = bucket;
-            run_s = 0.f;
+          // dpos_w: element (query 4lg + r, key lr) has diagonal e = lr - (4lg + r).
+          // Rotating row 4lg + r left by its index inside the 16-lane group puts the
+          // diagonals e = lr (main) and e = lr - 16 (wrapped) in lane lr; sum over r
+          // and the 4 lane groups, add the main part plus the previous block's wrapped
+          // part (same bins: the next block sits 16 queries later) to the histogram.
+          float dA = 0.f, dB = 0.f;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int ql = 4 * lg + r;
+            const float v = __shfl(ds[r], (lg << 4) | ((lr + ql) & 15), 64);
+            const bool main = lr + ql < 16;
+            dA += main ? v : 0.f;
+            dB += main ? 0.f : v;
           }
-          run_s += ds[r];
+          dA += __shfl_xor(dA, 16, 64);
+          dA += __shfl_xor(dA, 32, 64);
+          dB += __shfl_xor(dB, 16, 64);
+          dB += __shfl_xor(dB, 32, 64);
+          const int db = wk_lo - qb0;
+          int bin = a.N - 1 + db + lr;
+          bin = bin > npos - 1 ? npos - 1 : bin;
+          if (lg == 0) whist[bin] += dA + carry;
+          carry = dB;
+          last_db = db;
         }
-      }
-      if (has_bias) {
-        // dpos_w: diagonal sums of the 16x16 dS block through LDS, one plain add per
-        // diagonal (lanes own distinct bins of this wave's private histogram)
-        float* blk = dsblk + w * (16 * 17);
+#endif
+        if (has_bias) {  // dts_w: merge equal consecutive buckets of this lane, then add
+          float run = ds[0];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) blk[(4 * lg + r) * 17 + lr] = ds[r];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (lane < 31) {
-          const int dd = lane - 15;  // key - query inside the block
-          float acc_d = 0.f;
-#pragma unroll
-          for (int qq = 0; qq < 16; ++qq) {
-            const int kk = qq + dd;
-            if (kk >= 0 && kk < 16) acc_d += blk[qq * 17 + kk];
+          for (int r = 1; r < 4; ++r) {
+            const bool same = bk[r] == bk[r - 1];
+            atomicAdd(&wts[bk[r - 1]], same ? 0.f : run);
+            run = same ? run + ds[r] : ds[r];
           }
-          const int bin = a.N - 1 + (wk_lo - qb0) + dd;
-          if (bin >= 0 && bin <= 2 * a.N - 2) whist[bin] += acc_d;
+          atomicAdd(&wts[bk[3]], run);
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      }
-      // dV[key][c] += P^T dO ; dK[key][d] += dS^T Q   (k-step r: queries 4g + r)
-      const float* dcol = Ds + (qb * 16 + 4 * lg) * C::LDV + lr;
-      const float* qcol = Qs + (qb * 16 + 4 * lg) * C::LDQ + lr;
+        // dV[key][c] += P^T dO ; dK[key][d] += dS^T Q   (k-step r: queries 4g + r)
+        const float* dcol = Ds + (qb * 16 + 4 * lg) * C::LDV + lr;
+        const float* qcol = Qs + (qb * 16 + 4 * lg) * C::LDQ + lr;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
+        for (int r = 0; r < 4; ++r) {
 #pragma unroll
-        for (int t = 0; t < VTILES; ++t)
-          dV[t] = mfma16x16x4(p[r], dcol[r * C::LDV + t * 16], dV[t]);
+          for (int t = 0; t < VTILES; ++t)
+            dV[t] = mfma16x16x4(p[r], dcol[r * C::LDV + t * 16], dV[t]);
 #pragma unroll
-        for (int t = 0; t < C::KT; ++t)
-          dK[t] = mfma16x16x4(ds[r], qcol[r * C::LDQ + t * 16], dK[t]);
+          for (int t = 0; t < C::KT; ++t)
+            dK[t] = mfma16x16x4(ds[r], qcol[r * C::LDQ + t * 16], dK[t]);
+        }
       }
     }
     if (more) {
@@ -277,11 +293,22 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
       if (ok) a.dk[row * a.ld_d + h * a.dqk + c] = g;
     }
   }
-  if (has_bias && run_s != 0.f) atomicAdd(&whist[2 * a.N - 1 + run_b], run_s);
+#if GR_DPOS_ROT
+  if (has_bias && lg == 0) {  // the last block's wrapped diagonals
+    const int bin = a.N - 1 + last_db - 16 + lr;
+    if (bin >= 0 && bin < npos) whist[bin] += carry;
+  }
+#endif
   if (has_bias && slab) {
     __syncthreads();
-    for (int i = tid; i < nbins; i += 256)
-      slab[i] = ((hist[i] + hist[nbins + i]) + hist[2 * nbins + i]) + hist[3 * nbins + i];
+    for (int i = tid; i < npos; i += 256)
+      slab[i] = ((hist[i] + hist[wbins + i]) + hist[2 * wbins + i]) + hist[3 * wbins + i];
+    for (int i = tid; i <= a.nb; i += 256) {
+      float acc = 0.f;
+      for (int ww = 0; ww < 4; ++ww)
+        for (int c = 0; c < GR_DTS_COPIES; ++c) acc += hist[ww * wbins + npos + c * tss + i];
+      slab[npos + i] = acc;
+    }
   }
 }
 
@@ -306,7 +333,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   const int L = (int)(a.offsets[b + 1] - s0);
   const int q0 = qt * 64;
   if (q0 >= L) return;
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int tid = threadIdx.x, w = wave_id(), lane = tid & 63;
   const int lr = lane & 15, lg = lane >> 4;
   const bool has_bias = a.map_qk != nullptr;
   if (has_bias) {
@@ -315,7 +342,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   }
   const int qi = q0 + w * 16 + lr;
   const bool q_ok = qi < L;
-  float qreg[KSTEPS], doreg[C::VSTEPS];
+  float qreg[KSTEPS], doreg[KSTEPS];
   {
     const int64_t row = s0 + (q_ok ? qi : L - 1);
     gptr<float> qrow = as_global(a.q) + row * a.ld_qk + h * a.dqk;
@@ -325,35 +352,29 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
       const int d = 4 * st + lg;
       const float x = qrow[d < a.dqk ? d : a.dqk - 1];
       qreg[st] = d < a.dqk ? x : 0.f;
-    }
-#pragma unroll
-    for (int st = 0; st < C::VSTEPS; ++st) {
-      const int d = 4 * st + lg;
-      const float x = drow[d < a.dv ? d : a.dv - 1];
-      doreg[st] = d < a.dv ? x : 0.f;
+      const float y = drow[d < a.dv ? d : a.dv - 1];
+      doreg[st] = d < a.dv ? y : 0.f;
     }
   }
-  const int vsteps = (a.dv + 3) / 4;
-  const int tpb = attn_tiles_per_seq(a.N);
-  gptr<uint32_t> mapw =
-      as_global(reinterpret_cast<const uint32_t*>(a.map_qk ? a.map_qk : (const uint8_t*)a.q));
-  const int64_t map_seq = (int64_t)b * tpb * 1024;
-  const int map_lane = (w * 16 + lr) * 16 + lg;  // + kb * 4
+  const __amdgpu_buffer_rsrc_t rmap = map_rsrc(a.map_qk, b, attn_tiles_per_seq(a.N));
+  const int map_voff = ((w * 16 + lr) * 16 + lg) * 4;
+  const __amdgpu_buffer_rsrc_t rk = seq_rsrc(a.k, a.ld_qk, s0, h * a.dqk, L, a.dqk);
+  const __amdgpu_buffer_rsrc_t rv = seq_rsrc(a.v, a.ld_v, s0, h * a.dv, L, a.dv);
 
   f4 dQ[C::KT];
 #pragma unroll
   for (int t = 0; t < C::KT; ++t) dQ[t] = f4_zero();
   const int wq_lo = q0 + w * 16;
 
-  TileStage<C::KPT, TT> kst;
-  TileStage<C::VP, TT> vst;
+  BufTile<C::KPT, TT> kst;
+  BufTile<C::VP, TT> vst;
   uint32_t mw[C::TB], mwn[C::TB];
   auto load_tile = [&](int kt, uint32_t (&m)[C::TB]) {
-    kst.load(a.k, a.ld_qk, s0, kt * TT, L, h * a.dqk, a.dqk);
-    vst.load(a.v, a.ld_v, s0, kt * TT, L, h * a.dv, a.dv);
+    kst.load(rk, a.ld_qk, kt * TT, a.dqk);
+    vst.load(rv, a.ld_v, kt * TT, a.dv);
 #pragma unroll
     for (int kb = 0; kb < C::TB; ++kb)
-      m[kb] = has_bias ? mapw[map_block_word(map_seq, q0, kt * TT + kb * 16, map_lane, true)] : 0u;
+      m[kb] = buf_ld_u32(rmap, map_voff, map_soff(q0, kt * TT + kb * 16, true));
   };
   load_tile(0, mw);
   kst.store(Ks, LDK);
@@ -368,36 +389,37 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
 #pragma unroll
     for (int kb = 0; kb < C::TB; ++kb) {
       const int kb0 = k0 + kb * 16;
-      if (kb0 > wq_lo + 15 || kb0 >= L) break;
-      f4 s = f4_zero(), dpt = f4_zero();
-      const float* krow = Ks + (kb * 16 + lr) * LDK + lg;
+      if (kb0 <= wq_lo + 15 && kb0 < L) {  // wave-uniform causal / length skip
+        f4 s = f4_zero(), dpt = f4_zero();
+        const float* krow = Ks + (kb * 16 + lr) * LDK + lg;
+        const float* vrow = Vs + (kb * 16 + lr) * LDV + lg;
 #pragma unroll
-      for (int st = 0; st < KSTEPS; ++st) s = mfma16x16x4(krow[4 * st], qreg[st], s);
-      const float* vrow = Vs + (kb * 16 + lr) * LDV + lg;
-#pragma unroll
-      for (int st = 0; st < C::VSTEPS; ++st)
-        if (st < vsteps) dpt = mfma16x16x4(vrow[4 * st], doreg[st], dpt);
-      // s[r] = S^T[key kb0 + 4lg + r][query qi]
-      float ds[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int kj = kb0 + 4 * lg + r;
-        const bool ok = q_ok && kj <= qi;
-        float x = s[r];
-        if (has_bias) {
-          const int bucket = (mw[kb] >> (8 * r)) & 0xFF;
-          int pi = a.N - 1 + kj - qi;
-          pi = pi < 0 ? 0 : (pi > 2 * a.N - 2 ? 2 * a.N - 2 : pi);
-          x = x + (posw[pi] + tsw[bucket]);
+        for (int st = 0; st < KSTEPS; ++st) {
+          s = mfma16x16x4(krow[4 * st], qreg[st], s);
+          dpt = mfma16x16x4(vrow[4 * st], doreg[st], dpt);
         }
-        ds[r] = ok ? dpt[r] * silu_grad_(x) * a.inv_n : 0.f;
-      }
-      const float* kcol = Ks + (kb * 16 + 4 * lg) * LDK + lr;
+        // s[r] = S^T[key kb0 + 4lg + r][query qi]
+        float ds[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
+        for (int r = 0; r < 4; ++r) {
+          const int kj = kb0 + 4 * lg + r;
+          const bool ok = q_ok && kj <= qi;
+          float x = s[r];
+          if (has_bias) {
+            const int bucket = (mw[kb] >> (8 * r)) & 0xFF;
+            int pi = a.N - 1 + kj - qi;
+            pi = pi < 0 ? 0 : (pi > 2 * a.N - 2 ? 2 * a.N - 2 : pi);
+            x = x + (posw[pi] + tsw[bucket]);
+          }
+          ds[r] = ok ? dpt[r] * silu_grad_(x) * a.inv_n : 0.f;
+        }
+        const float* kcol = Ks + (kb * 16 + 4 * lg) * LDK + lr;
 #pragma unroll
-        for (int t = 0; t < C::KT; ++t)
-          dQ[t] = mfma16x16x4(ds[r], kcol[r * LDK + t * 16], dQ[t]);
+        for (int r = 0; r < 4; ++r) {
+#pragma unroll
+          for (int t = 0; t < C::KT; ++t)
+            dQ[t] = mfma16x16x4(ds[r], kcol[r * LDK + t * 16], dQ[t]);
+        }
       }
     }
     if (more) {
@@ -426,32 +448,33 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
 }
 
 // ------------------------------------------------------------------ slab reduce
-// Deterministic: a workgroup owns 64 bins; wave w sums slabs w, w+4, ... in order
-// (loads unrolled 8-deep), then the 4 partials are added in wave order.
+// Deterministic: a workgroup owns 16 bins; thread (bin, g) sums slabs g, g+16, ... in
+// order (loads 8-deep), then the 16 partials are added in g order.
 __global__ __launch_bounds__(256) void bias_grad_reduce_kernel(const float* slabs, int n_slabs,
                                                                int n_pos, int n_ts,
                                                                float* dpos_w, float* dts_w) {
-  __shared__ float part[4][64];
+  __shared__ float part[16][17];
   const int nbins = n_pos + n_ts;
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int i = blockIdx.x * 64 + lane;
+  const int bl = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int i = blockIdx.x * 16 + bl;
+  const int ic = i < nbins ? i : nbins - 1;
   gptr<float> src = as_global(slabs);
   float acc = 0.f;
-  if (i < nbins) {
-    int j = w;
-    for (; j + 28 < n_slabs; j += 32) {
-      float v[8];
+  int j = g;
+  for (; j + 112 < n_slabs; j += 128) {
+    float v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = src[(int64_t)(j + 4 * u) * nbins + i];
+    for (int u = 0; u < 8; ++u) v[u] = src[(int64_t)(j + 16 * u) * nbins + ic];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) acc += v[u];
-    }
-    for (; j < n_slabs; j += 4) acc += src[(int64_t)j * nbins + i];
+    for (int u = 0; u < 8; ++u) acc += v[u];
   }
-  part[w][lane] = acc;
+  for (; j < n_slabs; j += 16) acc += src[(int64_t)j * nbins + ic];
+  part[g][bl] = acc;
   __syncthreads();
-  if (w == 0 && i < nbins) {
-    const float s = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+  if (g == 0 && i < nbins) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += part[k][bl];
     if (i < n_pos) dpos_w[i] = s;
     else dts_w[i - n_pos] = s;
   }
@@ -469,7 +492,7 @@ static int launch_bwd(const AttnBwdArgs& a, float* dpos_w, float* dts_w, hipStre
   const int nbins = 2 * a.N - 1 + a.nb + 1;
   const size_t tail = sizeof(float) * (a.nb + 1 + 2 * a.N - 1);
   const size_t lds_kv = sizeof(float) * (TT * C::LDQ + TT * C::LDV) + tail +
-                        (a.map_kq ? sizeof(float) * (4 * nbins + 4 * 16 * 17) : 0);
+                        (a.map_kq ? sizeof(float) * 4 * (2 * a.N - 1 + GR_DTS_COPIES * dts_stride(a.nb + 1)) : 0);
   constexpr int LDV_Q = 32 * ((C::VP - 2 + 31) / 32) + 2;
   const size_t lds_q = sizeof(float) * (TT * C::LDQ + TT * LDV_Q) + tail;
   GR_REQUIRE(lds_kv <= 160 * 1024 && lds_q <= 160 * 1024,
@@ -479,7 +502,7 @@ static int launch_bwd(const AttnBwdArgs& a, float* dpos_w, float* dts_w, hipStre
   GR_TIMED("attn_bwd_dq", st, hipLaunchKernelGGL((attn_bwd_dq_kernel<KS, VT, TT>), dim3(grid), dim3(256), lds_q, st, a));
   GR_LAUNCH_CHECK("hstu_attn_bwd(dq)");
   if (a.map_kq) {
-    GR_TIMED("attn_bias_reduce", st, hipLaunchKernelGGL(bias_grad_reduce_kernel, dim3(ceil_div(nbins, 64)), dim3(256), 0, st,
+    GR_TIMED("attn_bias_reduce", st, hipLaunchKernelGGL(bias_grad_reduce_kernel, dim3(ceil_div(nbins, 16)), dim3(256), 0, st,
                        a.slabs, grid, 2 * a.N - 1, a.nb + 1, dpos_w, dts_w));
     GR_LAUNCH_CHECK("hstu_attn_bwd(bias reduce)");
   }

@@ -68,7 +68,7 @@ __global__ __launch_bounds__(256) void hstu_attn_fwd_kernel(AttnFwdArgs a) {
   const int q0 = qt * 64;
   if (q0 >= L) return;
 
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int tid = threadIdx.x, w = wave_id(), lane = tid & 63;
   const int lr = lane & 15, lg = lane >> 4;
   const bool has_bias = a.map_qk != nullptr;
 
@@ -90,24 +90,24 @@ __global__ __launch_bounds__(256) void hstu_attn_fwd_kernel(AttnFwdArgs a) {
       qreg[st] = d < a.dqk ? x : 0.f;
     }
   }
-  const int tpb = attn_tiles_per_seq(a.N);
-  gptr<uint32_t> mapw = as_global(reinterpret_cast<const uint32_t*>(a.map_qk ? a.map_qk : (const uint8_t*)a.q));
-  const int64_t map_seq = (int64_t)b * tpb * 1024;                 // dwords
-  const int map_lane = (w * 16 + lr) * 16 + lg;                     // + kb * 4
+  const __amdgpu_buffer_rsrc_t rmap = map_rsrc(a.map_qk, b, attn_tiles_per_seq(a.N));
+  const int map_voff = ((w * 16 + lr) * 16 + lg) * 4;
+  const __amdgpu_buffer_rsrc_t rk = seq_rsrc(a.k, a.ld_qk, s0, h * a.dqk, L, a.dqk);
+  const __amdgpu_buffer_rsrc_t rv = seq_rsrc(a.v, a.ld_v, s0, h * a.dv, L, a.dv);
 
   f4 acc[VTILES];
 #pragma unroll
   for (int ct = 0; ct < VTILES; ++ct) acc[ct] = f4_zero();
 
-  TileStage<C::KP, TK> kst;
-  TileStage<C::VP, TK> vst;
+  BufTile<C::KP, TK> kst;
+  BufTile<C::VP, TK> vst;
   uint32_t mw[C::KB], mwn[C::KB];
   auto load_tile = [&](int kt, uint32_t (&m)[C::KB]) {
-    kst.load(a.k, a.ld_qk, s0, kt * TK, L, h * a.dqk, a.dqk);
-    vst.load(a.v, a.ld_v, s0, kt * TK, L, h * a.dv, a.dv);
+    kst.load(rk, a.ld_qk, kt * TK, a.dqk);
+    vst.load(rv, a.ld_v, kt * TK, a.dv);
 #pragma unroll
     for (int kb = 0; kb < C::KB; ++kb)
-      m[kb] = has_bias ? mapw[map_block_word(map_seq, q0, kt * TK + kb * 16, map_lane, true)] : 0u;
+      m[kb] = buf_ld_u32(rmap, map_voff, map_soff(q0, kt * TK + kb * 16, true));
   };
 
   load_tile(0, mw);

@@ -18,6 +18,7 @@
 // A operand layout (row stride 18 == 18 mod 32) and B layout (stride == 16 mod 32) make
 // the per-k-step ds_read_b32 of both operands bank-conflict-free.
 #include "common.h"
+#include "rowwave.h"
 
 #include "../../include/gr_hstu.h"
 
@@ -630,6 +631,152 @@ static void wgrad_plan(int64_t max_rows, int Ka, int Nb, int* n_chunks, int64_t*
   if (*n_chunks < 1) *n_chunks = 1;
 }
 
+// ------------------------------------------------------------------ row-wave dispatch
+// Narrow shapes (weight panel in LDS, <= 80 KiB) run the row-wave kernel (rowwave.h);
+// everything else the row-panel kernel above.  Returns -1 when the shape / alignment
+// is not covered (caller falls back), else the launch status.
+constexpr size_t RW_LDS_MAX = 80 * 1024;
+
+static int num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+      n = v;
+    else
+      n = 256;
+  }
+  return n;
+}
+
+static int rw_bucket(int x) {  // 16-column groups, rounded up to an instantiated size
+  const int g = ceil_div(x, 16);
+  if (g <= 1) return 1;
+  if (g <= 2) return 2;
+  if (g <= 4) return 4;
+  if (g <= 8) return 8;
+  if (g <= 13) return 13;
+  if (g <= 16) return 16;
+  return -1;
+}
+
+template <int KG, int NT, int VEC, template <int, int, int> class OpT, class Args>
+static int rw_launch(const Args& args, int64_t max_rows, const char* tname, hipStream_t st) {
+  using C = RowWaveCfg<KG, NT>;
+  if constexpr (C::LDS_BYTES > RW_LDS_MAX) {
+    return -1;
+  } else {
+    OpT<KG, NT, VEC> op;
+    args.fill(op);
+    // grid-stride over 16-row units (persistent once the rows exceed 4 workgroups per CU)
+    const int64_t units = (max_rows + 15) / 16;
+    int grid = (int)((units + 3) / 4);
+    const int cap = 4 * num_cus();
+    if (grid > cap) grid = cap;
+    if (grid < 1) return 0;
+    GR_TIMED(tname, st, hipLaunchKernelGGL((rowwave_kernel<KG, NT, OpT<KG, NT, VEC>>), dim3(grid),
+                                           dim3(256), C::LDS_BYTES, st, op));
+    GR_LAUNCH_CHECK(tname);
+    return 0;
+  }
+}
+
+template <int KG, int VEC, template <int, int, int> class OpT, class Args>
+static int rw_nt(const Args& a, int nt, int64_t max_rows, const char* tname, hipStream_t st) {
+  switch (nt) {
+    case 1: return rw_launch<KG, 1, VEC, OpT>(a, max_rows, tname, st);
+    case 2: return rw_launch<KG, 2, VEC, OpT>(a, max_rows, tname, st);
+    case 4: return rw_launch<KG, 4, VEC, OpT>(a, max_rows, tname, st);
+    case 8: return rw_launch<KG, 8, VEC, OpT>(a, max_rows, tname, st);
+    case 13: return rw_launch<KG, 13, VEC, OpT>(a, max_rows, tname, st);
+    case 16: return rw_launch<KG, 16, VEC, OpT>(a, max_rows, tname, st);
+  }
+  return -1;
+}
+
+template <int VEC, template <int, int, int> class OpT, class Args>
+static int rw_kg(const Args& a, int kg, int nt, int64_t max_rows, const char* tname, hipStream_t st) {
+  switch (kg) {
+    case 1: return rw_nt<1, VEC, OpT>(a, nt, max_rows, tname, st);
+    case 2: return rw_nt<2, VEC, OpT>(a, nt, max_rows, tname, st);
+    case 4: return rw_nt<4, VEC, OpT>(a, nt, max_rows, tname, st);
+    case 8: return rw_nt<8, VEC, OpT>(a, nt, max_rows, tname, st);
+    case 13: return rw_nt<13, VEC, OpT>(a, nt, max_rows, tname, st);
+    case 16: return rw_nt<16, VEC, OpT>(a, nt, max_rows, tname, st);
+  }
+  return -1;
+}
+
+// vector width usable for every (pointer + column offset, leading dim, K, N) involved
+static int rw_vec(std::initializer_list<const void*> ptrs, std::initializer_list<int64_t> lds) {
+  for (int vec : {4, 2}) {
+    bool ok = true;
+    for (const void* p : ptrs)
+      if (p && ((uintptr_t)p % (4 * vec)) != 0) ok = false;
+    for (int64_t l : lds)
+      if (l % vec != 0) ok = false;
+    if (ok) return vec;
+  }
+  return 0;
+}
+
+template <template <int, int, int> class OpT, class Args>
+static int rw_dispatch(const Args& a, int K, int N, int vec, int64_t max_rows, const char* tname,
+                       hipStream_t st) {
+  const int kg = rw_bucket(K), nt = rw_bucket(N);
+  if (kg < 0 || nt < 0 || vec == 0) return -1;
+  if (max_rows * 4 * 1024 > 0x7fffffffLL) return -1;  // 32-bit buffer offsets
+  (void)vec;  // 4-aligned shapes run the 8-byte path too (one instantiation set)
+  return rw_kg<2, OpT>(a, kg, nt, max_rows, tname, st);
+}
+
+struct RwArgsLnUvqk {
+  const int64_t* offsets; int B, K, N; const float* x; int64_t ldx; const float* w; float eps;
+  int act; float2* x_stats; float* h_pre; float* out; int64_t ld_out;
+  template <class Op> void fill(Op& o) const {
+    o.offsets = offsets; o.B = B; o.K = K; o.N = N; o.x = x; o.ldx = ldx; o.w = w; o.eps = eps;
+    o.act = act; o.x_stats = x_stats; o.h_pre = h_pre; o.out = out; o.ld_out = ld_out;
+  }
+};
+struct RwArgsGateO {
+  const int64_t* offsets; int B, K, N; const float* u; int64_t ldu; const float* attn; int64_t lda;
+  const float* w; const float* bias; const float* xres; int64_t ldx; float eps, p; uint64_t seed;
+  const int64_t* seed_off; float2* a_stats; float* o_in; float* y; int64_t ldy;
+  template <class Op> void fill(Op& o) const {
+    o.offsets = offsets; o.B = B; o.K = K; o.N = N; o.u = u; o.ldu = ldu; o.attn = attn; o.lda = lda;
+    o.w = w; o.bias = bias; o.xres = xres; o.ldx = ldx; o.eps = eps; o.p = p; o.seed = seed;
+    o.seed_off = seed_off; o.a_stats = a_stats; o.o_in = o_in; o.y = y; o.ldy = ldy;
+  }
+};
+struct RwArgsGateOBwd {
+  const int64_t* offsets; int B, K, N; const float* dy; int64_t lddy; const float* w; const float* u;
+  int64_t ldu; const float* attn; int64_t lda; const float2* a_stats; const float* h_u; int64_t ldh;
+  float p; uint64_t seed; const int64_t* seed_off; float* du; int64_t lddu; float* da; int64_t ldda;
+  template <class Op> void fill(Op& o) const {
+    o.offsets = offsets; o.B = B; o.K = K; o.N = N; o.dy = dy; o.lddy = lddy; o.w = w; o.u = u;
+    o.ldu = ldu; o.attn = attn; o.lda = lda; o.a_stats = a_stats; o.h_u = h_u; o.ldh = ldh; o.p = p;
+    o.seed = seed; o.seed_off = seed_off; o.du = du; o.lddu = lddu; o.da = da; o.ldda = ldda;
+  }
+};
+struct RwArgsLnUvqkBwd {
+  const int64_t* offsets; int B, K, N; const float* dh; int64_t lddh; const float* w; const float* x;
+  int64_t ldx; const float2* x_stats; const float* dy; int64_t lddy; float* dx; int64_t lddx;
+  template <class Op> void fill(Op& o) const {
+    o.offsets = offsets; o.B = B; o.K = K; o.N = N; o.dh = dh; o.lddh = lddh; o.w = w; o.x = x;
+    o.ldx = ldx; o.x_stats = x_stats; o.dy = dy; o.lddy = lddy; o.dx = dx; o.lddx = lddx;
+  }
+};
+
+static bool rw_enabled() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("GR_ROWWAVE");
+    on = (e && e[0] == '0') ? 0 : 1;
+  }
+  return on == 1;
+}
+
 }  // namespace gr
 
 // ====================================================================== C-ABI
@@ -642,6 +789,13 @@ extern "C" int hstu_ln_uvqk_fwd(const float* x, int64_t ld_x, const int64_t* off
   GR_REQUIRE(x && offsets && w_uvqk && uvqk && x_stats, "hstu_ln_uvqk_fwd: null pointer");
   GR_REQUIRE(D > 0 && n_out > 0 && B >= 0 && max_rows >= 0, "hstu_ln_uvqk_fwd: bad sizes");
   GR_REQUIRE(activation == 0 || activation == 1, "hstu_ln_uvqk_fwd: activation must be 0|1");
+  if (rw_enabled()) {
+    RwArgsLnUvqk ra{offsets, B, D, n_out, x, ld_x, w_uvqk, eps, activation, (float2*)x_stats,
+                    h_pre, uvqk, ld_out};
+    const int vec = rw_vec({x, h_pre, uvqk}, {ld_x, ld_out, D, n_out});
+    const int rc = rw_dispatch<RwLnUvqk>(ra, D, n_out, vec, max_rows, "ln_uvqk_fwd", (hipStream_t)stream);
+    if (rc >= 0) return rc;
+  }
   OpLnUvqk op{offsets, B, D, n_out, x, ld_x, w_uvqk, eps, activation, (float2*)x_stats,
               h_pre, uvqk, ld_out};
   return launch_rowpanel(op, max_rows, false, "hstu_ln_uvqk_fwd", (hipStream_t)stream);
@@ -656,6 +810,13 @@ extern "C" int hstu_gate_o_fwd(const float* u, int64_t ld_u, const float* attn, 
   GR_REQUIRE(u && attn && offsets && w_o && y && attn_stats, "hstu_gate_o_fwd: null pointer");
   GR_REQUIRE(hdv > 0 && D > 0 && B >= 0, "hstu_gate_o_fwd: bad sizes");
   GR_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f, "hstu_gate_o_fwd: dropout_p %f", dropout_p);
+  if (rw_enabled()) {
+    RwArgsGateO ra{offsets, B, hdv, D, u, ld_u, attn, ld_attn, w_o, b_o, x_res, ld_x, eps,
+                   dropout_p, seed, seed_offset, (float2*)attn_stats, o_in, y, ld_y};
+    const int vec = rw_vec({u, attn, x_res, o_in, y}, {ld_u, ld_attn, ld_x, ld_y, hdv, D});
+    const int rc = rw_dispatch<RwGateO>(ra, hdv, D, vec, max_rows, "gate_o_fwd", (hipStream_t)stream);
+    if (rc >= 0) return rc;
+  }
   OpGateO op{offsets, B, hdv, D, u, ld_u, attn, ld_attn, w_o, b_o, x_res, ld_x, eps, dropout_p,
              seed, seed_offset, (float2*)attn_stats, o_in, y, ld_y};
   return launch_rowpanel(op, max_rows, false, "hstu_gate_o_fwd", (hipStream_t)stream);
@@ -671,6 +832,14 @@ extern "C" int hstu_gate_o_bwd(const float* dy, int64_t ld_dy, const int64_t* of
   GR_REQUIRE(dy && offsets && w_o && u && attn && attn_stats && du && d_attn,
              "hstu_gate_o_bwd: null pointer");
   GR_REQUIRE(hdv > 0 && D > 0 && B >= 0, "hstu_gate_o_bwd: bad sizes");
+  if (rw_enabled()) {
+    RwArgsGateOBwd ra{offsets, B, D, hdv, dy, ld_dy, w_o, u, ld_u, attn, ld_attn,
+                      (const float2*)attn_stats, h_u, ld_h, dropout_p, seed, seed_offset, du, ld_du,
+                      d_attn, ld_da};
+    const int vec = rw_vec({dy, u, attn, h_u, du, d_attn}, {ld_dy, ld_u, ld_attn, ld_h, ld_du, ld_da, hdv, D});
+    const int rc = rw_dispatch<RwGateOBwd>(ra, D, hdv, vec, max_rows, "gate_o_bwd", (hipStream_t)stream);
+    if (rc >= 0) return rc;
+  }
   OpGateOBwd op;
   op.offsets = offsets; op.B = B; op.K = D; op.N = hdv; op.dy = dy; op.lddy = ld_dy;
   op.w = w_o; op.u = u; op.ldu = ld_u; op.attn = attn; op.lda = ld_attn;
@@ -686,6 +855,14 @@ extern "C" int hstu_ln_uvqk_bwd(const float* dh, int64_t ld_dh, const int64_t* o
                                 void* stream) {
   GR_REQUIRE(dh && offsets && w_uvqk && x && x_stats && dx, "hstu_ln_uvqk_bwd: null pointer");
   GR_REQUIRE(D > 0 && n_out > 0 && B >= 0, "hstu_ln_uvqk_bwd: bad sizes");
+  // the row-wave variant is not faster here for K = n_out >= 128 (many k-groups per row)
+  if (rw_enabled() && n_out <= 64) {
+    RwArgsLnUvqkBwd ra{offsets, B, n_out, D, dh, ld_dh, w_uvqk, x, ld_x, (const float2*)x_stats,
+                       dy_res, ld_dy, dx, ld_dx};
+    const int vec = rw_vec({dh, x, dy_res, dx}, {ld_dh, ld_x, ld_dy, ld_dx, n_out, D});
+    const int rc = rw_dispatch<RwLnUvqkBwd>(ra, n_out, D, vec, max_rows, "ln_uvqk_bwd", (hipStream_t)stream);
+    if (rc >= 0) return rc;
+  }
   OpLnUvqkBwd op;
   op.offsets = offsets; op.B = B; op.K = n_out; op.N = D; op.dh = dh; op.lddh = ld_dh;
   op.w = w_uvqk; op.x = x; op.ldx = ld_x; op.x_stats = (const float2*)x_stats;

@@ -1,0 +1,520 @@
+// Row-wave projection GEMM for the narrow STU shapes (K <= 256, K x N weight panel fits
+// in LDS; ml-1m: D = 50, n_out = 200) — gfx950, f32 MFMA.
+//
+// Work unit = ONE WAVE x 16 rows.  A workgroup stages the whole weight panel W (K x N)
+// in LDS once and its 4 waves then loop over 16-row units (grid-stride, persistent),
+// with the next unit's rows prefetched into registers while the current one runs.
+// Per unit a lane holds the 16 rows' A values in the MFMA B-operand layout with a
+// permuted K order: lane (row lr, group lg) loads A[row][16g + 4lg .. 16g + 4lg + 3]
+// (one 8/16-byte load per g), and k-step j of group g uses k = 16g + 4lg + j — the
+// weight side reads W[16g + 4lg + j][n] from LDS accordingly.  The product is taken
+// transposed, C^T = W^T A^T, so a lane ends with 4 CONSECUTIVE output columns of its
+// row (acc[t][r] = C[row lr][16t + 4lg + r]) — vector stores and in-register row
+// reductions (lanes lr, lr+16, lr+32, lr+48 hold one row).
+#pragma once
+
+#include "common.h"
+
+namespace gr {
+
+typedef unsigned int u2v __attribute__((ext_vector_type(2)));
+typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+
+// Buffer descriptor over rows [0, rows) of a (rows, ld) f32 matrix starting at column c0
+// of `base`; loads past the last row return 0, stores there are dropped.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t mat_rsrc(const float* base, int64_t ld,
+                                                          int64_t rows, int c0) {
+  int64_t bytes = rows > 0 ? (rows * ld - c0) * 4 : 0;
+  if (bytes > 0x7fffffff) bytes = 0x7fffffff;
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(base + c0), 0, (int)bytes, 0x00020000);
+}
+
+// Byte offset that fails the buffer range check: loads through it return 0 and stores
+// are dropped — column / row masking without branches.
+constexpr int OOB = 0x40000000;
+
+// A lane's "quad": 4 columns of a 16-column tile (base tb) owned by lane group lg.
+//   VEC = 4 (16-byte aligned rows):  tb + 4lg + e                     (one 16-byte access)
+//   VEC = 2 ( 8-byte aligned rows):  tb + 2lg + (e & 1) + 8 (e >> 1)  (two 8-byte accesses;
+//                                     the 4 lane groups cover 32 contiguous bytes each)
+// With N % VEC == 0 each access is entirely inside or outside [0, N).
+template <int VEC>
+__device__ __forceinline__ int qcol(int tb, int lg, int e) {
+  return VEC == 4 ? tb + 4 * lg + e : tb + 2 * lg + (e & 1) + 8 * (e >> 1);
+}
+template <int VEC>
+__device__ __forceinline__ f4 ldq(__amdgpu_buffer_rsrc_t r, int64_t row_off, int tb, int lg,
+                                  int N = 1 << 30) {
+  if constexpr (VEC == 4) {
+    const int c = qcol<4>(tb, lg, 0);
+    const u4v v = __builtin_amdgcn_raw_buffer_load_b128(r, c < N ? (int)((row_off + c) * 4) : OOB, 0, 0);
+    return f4{__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w)};
+  } else {
+    const int c0 = qcol<2>(tb, lg, 0), c2 = qcol<2>(tb, lg, 2);
+    const u2v a = __builtin_amdgcn_raw_buffer_load_b64(r, c0 < N ? (int)((row_off + c0) * 4) : OOB, 0, 0);
+    const u2v b = __builtin_amdgcn_raw_buffer_load_b64(r, c2 < N ? (int)((row_off + c2) * 4) : OOB, 0, 0);
+    return f4{__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(b.x), __uint_as_float(b.y)};
+  }
+}
+template <int VEC>
+__device__ __forceinline__ void stq(__amdgpu_buffer_rsrc_t r, int64_t row_off, int tb, int lg,
+                                    int N, f4 v) {
+  if constexpr (VEC == 4) {
+    const int c = qcol<4>(tb, lg, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(
+        u4v{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])},
+        r, c < N ? (int)((row_off + c) * 4) : OOB, 0, 0);
+  } else {
+    const int c0 = qcol<2>(tb, lg, 0), c2 = qcol<2>(tb, lg, 2);
+    __builtin_amdgcn_raw_buffer_store_b64(u2v{__float_as_uint(v[0]), __float_as_uint(v[1])}, r,
+                                          c0 < N ? (int)((row_off + c0) * 4) : OOB, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(u2v{__float_as_uint(v[2]), __float_as_uint(v[3])}, r,
+                                          c2 < N ? (int)((row_off + c2) * 4) : OOB, 0, 0);
+  }
+}
+
+// sum over the 4 lanes holding one row (lanes lr, lr + 16, lr + 32, lr + 48)
+__device__ __forceinline__ float row4_sum(float v) {
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  return v;
+}
+
+template <int KG, int NT>
+struct RowWaveCfg {
+  static constexpr int KP = KG * 16;
+  static constexpr int NP = NT * 16;
+  // == 4 mod 16: the 4 lane groups' k-rows of one step (2 or 4 rows apart) cover every
+  // bank exactly twice (the minimum for 64 lanes)
+  static constexpr int LDW = NP + 4;
+  static constexpr size_t LDS_BYTES = sizeof(float) * KP * LDW;
+};
+
+// Op interface (VEC = quad access width, see qcol):
+//   K, N, offsets/B (total rows = offsets[B]); weight W'(k, n) = w[k * bks() + n * bns()],
+//   K_CONTIG: bks() == 1 (staging walks k fastest);
+//   setup(total); load(src, m, lg) issues a unit's input loads; prep(src, a, m, row_ok, lg)
+//   turns them into the A quads; epi(acc, m, row_ok, lg) consumes acc[t][e] =
+//   C[m][qcol(16t, lg, e)].
+template <int KG, int NT, class Op>
+__global__ __launch_bounds__(256) void rowwave_kernel(Op op) {
+  using C = RowWaveCfg<KG, NT>;
+  constexpr int VEC = Op::VEC;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* Wl = reinterpret_cast<float*>(smem);
+  const int tid = threadIdx.x, w = wave_id(), lane = tid & 63;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int64_t total = op.offsets[op.B];
+  op.setup(total);
+  const int64_t n_units = (total + 15) / 16;
+  int64_t u = (int64_t)blockIdx.x * 4 + w;
+  const int64_t ustep = (int64_t)gridDim.x * 4;
+  typename Op::Src cur, nxt;
+  if (u < n_units) op.load(cur, u * 16 + lr, lg);  // first unit's rows in flight during staging
+
+#ifndef GR_RW_NOSTAGE
+  // Stage W' once per workgroup.  LDS column 16t + i holds weight column 16t + pi(i),
+  // pi(4g + e) = qcol(0, g, e): MFMA output row i of tile t is then exactly the column
+  // the lane's quad stores.  Threads walk the memory-contiguous index fastest; batches
+  // of 16 loads in flight.
+  {
+    constexpr int FP = Op::K_CONTIG ? C::KP : C::NP;  // fast extent
+    constexpr int SP = Op::K_CONTIG ? C::NP : C::KP;  // slow extent
+    constexpr int FP2 = FP <= 16 ? 16 : FP <= 32 ? 32 : FP <= 64 ? 64 : FP <= 128 ? 128 : 256;
+    constexpr int SSTEP = 256 / FP2;
+    constexpr int ITER = SP / SSTEP;
+    constexpr int BATCH = ITER < 16 ? ITER : 16;
+    const int f = tid % FP2, s0 = tid / FP2;
+    if (f < FP) {
+#pragma unroll 1
+      for (int i0 = 0; i0 < ITER; i0 += BATCH) {
+        float v[BATCH];
+        int kk[BATCH], pp[BATCH];
+#pragma unroll
+        for (int i = 0; i < BATCH; ++i) {
+          const int sl = s0 + (i0 + i) * SSTEP;
+          const int k = Op::K_CONTIG ? f : sl;
+          const int p = Op::K_CONTIG ? sl : f;  // LDS column
+          const int n = (p & ~15) + qcol<VEC>(0, (p & 15) >> 2, p & 3);
+          const int kc = k < op.K ? k : op.K - 1, nc = n < op.N ? n : op.N - 1;
+          const float x = as_global(op.w)[(int64_t)kc * op.bks() + (int64_t)nc * op.bns()];
+          v[i] = (k < op.K && n < op.N) ? x : 0.f;
+          kk[i] = k;
+          pp[i] = p;
+        }
+#pragma unroll
+        for (int i = 0; i < BATCH; ++i)
+          if (i0 + i < ITER) Wl[kk[i] * C::LDW + pp[i]] = v[i];
+      }
+    }
+  }
+#endif
+  __syncthreads();
+  for (; u < n_units; u += ustep) {
+    const int64_t m = u * 16 + lr;
+    const bool more = u + ustep < n_units;
+    if (more) op.load(nxt, m + ustep * 16, lg);
+    float a[KG][4];
+    op.prep(cur, a, m, m < total, lg);
+    f4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = f4_zero();
+    // opaque zero: keeps hipcc from hoisting the (loop-invariant) LDS weight reads out
+    // of the unit loop into hundreds of registers
+    int wofs = 0;
+    asm volatile("" : "+v"(wofs));
+    const float* wbase = Wl + wofs + lr;
+    // k-step s = (g, e) uses k = qcol(16g, lg, e); software-pipelined: the NT weight
+    // values of step s+1 are read from LDS while the NT MFMAs of step s run
+    float wv[2][NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) wv[0][t] = wbase[qcol<VEC>(0, lg, 0) * C::LDW + 16 * t];
+#pragma unroll
+    for (int s = 0; s < 4 * KG; ++s) {
+      const int g = s >> 2, e = s & 3;
+      if (s + 1 < 4 * KG) {
+        const float* wrow = wbase + qcol<VEC>(16 * ((s + 1) >> 2), lg, (s + 1) & 3) * C::LDW;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) wv[(s + 1) & 1][t] = wrow[16 * t];
+      }
+      __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead of this step's MFMAs
+#ifndef GR_RW_NOMFMA
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = mfma16x16x4(wv[s & 1][t], a[g][e], acc[t]);
+#else
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t][0] += wv[s & 1][t] * a[g][e];
+#endif
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#ifndef GR_RW_NOSTORE
+    op.epi(acc, m, m < total, lg);
+#else
+    float sink = 0.f;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) sink += acc[t][0] + acc[t][1] + acc[t][2] + acc[t][3];
+    if (sink == 1.2345f) op.epi(acc, m, m < total, lg);
+#endif
+    if (more) cur = nxt;
+  }
+}
+
+// ------------------------------------------------------------------ ops
+// F1: uvqk = silu(LN(x) @ W), W (D, n_out) row-major; h_pre = pre-activation.
+template <int KG, int NT, int VEC_>
+struct RwLnUvqk {
+  static constexpr int VEC = VEC_;
+  static constexpr bool K_CONTIG = false;
+  const int64_t* offsets;
+  int B, K, N;
+  const float* x;
+  int64_t ldx;
+  const float* w;
+  float eps;
+  int act;
+  float2* x_stats;
+  float* h_pre;
+  float* out;
+  int64_t ld_out;
+  __amdgpu_buffer_rsrc_t rx, rh, ro;
+  struct Src { f4 v[KG]; };
+  __device__ int bks() const { return N; }
+  __device__ int bns() const { return 1; }
+  __device__ void setup(int64_t total) {
+    rx = mat_rsrc(x, ldx, total, 0);
+    rh = mat_rsrc(h_pre ? h_pre : out, ld_out, h_pre ? total : 0, 0);
+    ro = mat_rsrc(out, ld_out, total, 0);
+  }
+  __device__ void load(Src& s, int64_t m, int lg) const {
+#pragma unroll
+    for (int g = 0; g < KG; ++g) s.v[g] = ldq<VEC>(rx, m * ldx, 16 * g, lg, K);
+  }
+  __device__ void prep(const Src& s, float (&a)[KG][4], int64_t m, bool row_ok, int lg) const {
+    // columns >= K load as 0 (masked accesses), so plain sums are exact
+    float sum = 0.f;
+#pragma unroll
+    for (int g = 0; g < KG; ++g)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sum += s.v[g][e];
+    const float mean = row4_sum(sum) * (1.f / (float)K);
+    float sq = 0.f;
+#pragma unroll
+    for (int g = 0; g < KG; ++g)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float d = qcol<VEC>(16 * g, lg, e) < K ? s.v[g][e] - mean : 0.f;
+        sq += d * d;
+      }
+    const float rstd = rsqrtf(row4_sum(sq) * (1.f / (float)K) + eps);
+#pragma unroll
+    for (int g = 0; g < KG; ++g)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        a[g][e] = qcol<VEC>(16 * g, lg, e) < K ? (s.v[g][e] - mean) * rstd : 0.f;
+    if (lg == 0 && row_ok) x_stats[m] = make_float2(mean, rstd);
+  }
+  __device__ void epi(f4 (&acc)[NT], int64_t m, bool, int lg) const {
+    // rows past the end fall outside the descriptors (stores dropped)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      stq<VEC>(rh, m * ld_out, 16 * t, lg, N, acc[t]);  // records = 0 when h_pre is NULL
+      f4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = act ? siluf_(acc[t][e]) : acc[t][e];
+      stq<VEC>(ro, m * ld_out, 16 * t, lg, N, o);
+    }
+  }
+};
+
+__device__ __forceinline__ float rw_dropout_keep(uint64_t seed, int64_t m, int k, int K, float p) {
+  if (p <= 0.f) return 1.f;
+  const uint32_t hsh = hash_u32(seed, (uint64_t)m * (uint64_t)K + (uint64_t)k);
+  const uint32_t thr = (uint32_t)(p * 4294967296.0);
+  return hsh >= thr ? 1.f / (1.f - p) : 0.f;
+}
+
+// F3: y = dropout(u * LN(attn)) @ W_o^T + b_o + x;  W_o (D, hdv) row-major -> W'(k, n) = W_o[n][k]
+template <int KG, int NT, int VEC_>
+struct RwGateO {
+  static constexpr int VEC = VEC_;
+  static constexpr bool K_CONTIG = true;
+  const int64_t* offsets;
+  int B, K, N;  // K = hdv, N = D
+  const float* u;
+  int64_t ldu;
+  const float* attn;
+  int64_t lda;
+  const float* w;
+  const float* bias;
+  const float* xres;
+  int64_t ldx;
+  float eps, p;
+  uint64_t seed;
+  const int64_t* seed_off;
+  float2* a_stats;
+  float* o_in;
+  float* y;
+  int64_t ldy;
+  __amdgpu_buffer_rsrc_t ru, ra, rx, ro, ry, rb;
+  uint64_t seed_eff;
+  struct Src { f4 v[KG]; f4 uu[KG]; };
+  __device__ int bks() const { return 1; }
+  __device__ int bns() const { return K; }
+  __device__ void setup(int64_t total) {
+    ru = mat_rsrc(u, ldu, total, 0);
+    ra = mat_rsrc(attn, lda, total, 0);
+    rx = mat_rsrc(xres ? xres : y, ldx, xres ? total : 0, 0);
+    ro = mat_rsrc(o_in ? o_in : y, K, o_in ? total : 0, 0);
+    ry = mat_rsrc(y, ldy, total, 0);
+    rb = mat_rsrc(bias ? bias : y, N, bias ? 1 : 0, 0);
+    seed_eff = seed + (seed_off ? (uint64_t)*seed_off : 0ull);
+  }
+  __device__ void load(Src& s, int64_t m, int lg) const {
+#pragma unroll
+    for (int g = 0; g < KG; ++g) {
+      s.v[g] = ldq<VEC>(ra, m * lda, 16 * g, lg, K);
+      s.uu[g] = ldq<VEC>(ru, m * ldu, 16 * g, lg, K);
+    }
+  }
+  __device__ void prep(const Src& s, float (&a)[KG][4], int64_t m, bool row_ok, int lg) const {
+    float sum = 0.f;
+#pragma unroll
+    for (int g = 0; g < KG; ++g)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sum += s.v[g][e];
+    const float mean = row4_sum(sum) * (1.f / (float)K);
+    float sq = 0.f;
+#pragma unroll
+    for (int g = 0; g < KG; ++g)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float d = qcol<VEC>(16 * g, lg, e) < K ? s.v[g][e] - mean : 0.f;
+        sq += d * d;
+      }
+    const float rstd = rsqrtf(row4_sum(sq) * (1.f / (float)K) + eps);
+#pragma unroll
+    for (int g = 0; g < KG; ++g) {
+      f4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = qcol<VEC>(16 * g, lg, e);
+        float v = s.uu[g][e] * ((s.v[g][e] - mean) * rstd);
+        if (p > 0.f) v *= rw_dropout_keep(seed_eff, m, k, K, p);
+        a[g][e] = k < K ? v : 0.f;
+        o[e] = a[g][e];
+      }
+      stq<VEC>(ro, m * K, 16 * g, lg, K, o);  // records = 0 when o_in is NULL
+    }
+    if (lg == 0 && row_ok) a_stats[m] = make_float2(mean, rstd);
+  }
+  __device__ void epi(f4 (&acc)[NT], int64_t m, bool, int lg) const {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const f4 xv = ldq<VEC>(rx, m * ldx, 16 * t, lg, N);  // 0 when xres is NULL
+      const f4 bv = ldq<VEC>(rb, 0, 16 * t, lg, N);        // 0 when bias is NULL
+      f4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (acc[t][e] + bv[e]) + xv[e];
+      stq<VEC>(ry, m * ldy, 16 * t, lg, N, o);
+    }
+  }
+};
+
+// B1: g = dy @ W_o (rows, hdv), W'(k, n) = W_o[k][n]; epilogue: dropout bwd,
+//     du = g * LN(attn) (* silu'(h_u)), d_attn = LayerNorm_bwd(g * u).
+template <int KG, int NT, int VEC_>
+struct RwGateOBwd {
+  static constexpr int VEC = VEC_;
+  static constexpr bool K_CONTIG = false;
+  const int64_t* offsets;
+  int B, K, N;  // K = D, N = hdv
+  const float* dy;
+  int64_t lddy;
+  const float* w;
+  const float* u;
+  int64_t ldu;
+  const float* attn;
+  int64_t lda;
+  const float2* a_stats;
+  const float* h_u;
+  int64_t ldh;
+  float p;
+  uint64_t seed;
+  const int64_t* seed_off;
+  float* du;
+  int64_t lddu;
+  float* da;
+  int64_t ldda;
+  __amdgpu_buffer_rsrc_t rdy, ru, ra, rh, rdu, rda;
+  uint64_t seed_eff;
+  struct Src { f4 v[KG]; };
+  __device__ int bks() const { return N; }
+  __device__ int bns() const { return 1; }
+  __device__ void setup(int64_t total) {
+    rdy = mat_rsrc(dy, lddy, total, 0);
+    ru = mat_rsrc(u, ldu, total, 0);
+    ra = mat_rsrc(attn, lda, total, 0);
+    rh = mat_rsrc(h_u ? h_u : u, ldh, h_u ? total : 0, 0);
+    rdu = mat_rsrc(du, lddu, total, 0);
+    rda = mat_rsrc(da, ldda, total, 0);
+    seed_eff = seed + (seed_off ? (uint64_t)*seed_off : 0ull);
+  }
+  __device__ void load(Src& s, int64_t m, int lg) const {
+#pragma unroll
+    for (int g = 0; g < KG; ++g) s.v[g] = ldq<VEC>(rdy, m * lddy, 16 * g, lg, K);
+  }
+  __device__ void prep(const Src& s, float (&a)[KG][4], int64_t, bool, int) const {
+#pragma unroll
+    for (int g = 0; g < KG; ++g)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a[g][e] = s.v[g][e];  // columns >= K loaded as 0
+  }
+  __device__ void epi(f4 (&acc)[NT], int64_t m, bool row_ok, int lg) const {
+    const float2 st = ld_f2(a_stats, row_ok ? m : 0);
+    float s1 = 0.f, s2 = 0.f;
+    f4 lnv[NT], dln[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const f4 av = ldq<VEC>(ra, m * lda, 16 * t, lg, N);
+      const f4 uv = ldq<VEC>(ru, m * ldu, 16 * t, lg, N);
+      const f4 hv = ldq<VEC>(rh, m * ldh, 16 * t, lg, N);  // 0 when h_u is NULL
+      f4 duv;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int n = qcol<VEC>(16 * t, lg, e);
+        const bool ok = row_ok && n < N;
+        const float gg = p > 0.f ? acc[t][e] * rw_dropout_keep(seed_eff, m, n, N, p) : acc[t][e];
+        const float ln = (av[e] - st.x) * st.y;
+        float dd = gg * ln;
+        if (h_u) dd *= silu_grad_(hv[e]);
+        duv[e] = dd;
+        lnv[t][e] = ok ? ln : 0.f;
+        dln[t][e] = ok ? gg * uv[e] : 0.f;
+        s1 += dln[t][e];
+        s2 += dln[t][e] * lnv[t][e];
+      }
+      stq<VEC>(rdu, m * lddu, 16 * t, lg, N, duv);
+    }
+    s1 = row4_sum(s1);
+    s2 = row4_sum(s2);
+    const float inv = 1.f / (float)N;
+    const float mean1 = s1 * inv, mean2 = s2 * inv;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      f4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = st.y * (dln[t][e] - mean1 - lnv[t][e] * mean2);
+      stq<VEC>(rda, m * ldda, 16 * t, lg, N, o);
+    }
+  }
+};
+
+// B3: dn = dh @ W_uvqk^T (rows, D), W'(k, n) = W_uvqk[n][k]; epilogue: dx = dy + LN_bwd(x; dn).
+template <int KG, int NT, int VEC_>
+struct RwLnUvqkBwd {
+  static constexpr int VEC = VEC_;
+  static constexpr bool K_CONTIG = true;
+  const int64_t* offsets;
+  int B, K, N;  // K = n_out, N = D
+  const float* dh;
+  int64_t lddh;
+  const float* w;
+  const float* x;
+  int64_t ldx;
+  const float2* x_stats;
+  const float* dy;
+  int64_t lddy;
+  float* dx;
+  int64_t lddx;
+  __amdgpu_buffer_rsrc_t rdh, rx, rdy, rdx;
+  struct Src { f4 v[KG]; };
+  __device__ int bks() const { return 1; }
+  __device__ int bns() const { return K; }
+  __device__ void setup(int64_t total) {
+    rdh = mat_rsrc(dh, lddh, total, 0);
+    rx = mat_rsrc(x, ldx, total, 0);
+    rdy = mat_rsrc(dy ? dy : x, lddy, dy ? total : 0, 0);
+    rdx = mat_rsrc(dx, lddx, total, 0);
+  }
+  __device__ void load(Src& s, int64_t m, int lg) const {
+#pragma unroll
+    for (int g = 0; g < KG; ++g) s.v[g] = ldq<VEC>(rdh, m * lddh, 16 * g, lg, K);
+  }
+  __device__ void prep(const Src& s, float (&a)[KG][4], int64_t, bool, int) const {
+#pragma unroll
+    for (int g = 0; g < KG; ++g)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a[g][e] = s.v[g][e];
+  }
+  __device__ void epi(f4 (&acc)[NT], int64_t m, bool row_ok, int lg) const {
+    const float2 st = ld_f2(x_stats, row_ok ? m : 0);
+    float s1 = 0.f, s2 = 0.f;
+    f4 xh[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const f4 xv = ldq<VEC>(rx, m * ldx, 16 * t, lg, N);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool ok = row_ok && qcol<VEC>(16 * t, lg, e) < N;
+        xh[t][e] = ok ? (xv[e] - st.x) * st.y : 0.f;
+        const float dn = ok ? acc[t][e] : 0.f;
+        s1 += dn;
+        s2 += dn * xh[t][e];
+      }
+    }
+    s1 = row4_sum(s1);
+    s2 = row4_sum(s2);
+    const float inv = 1.f / (float)N;
+    const float mean1 = s1 * inv, mean2 = s2 * inv;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const f4 dyv = ldq<VEC>(rdy, m * lddy, 16 * t, lg, N);  // 0 when dy is NULL
+      f4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = dyv[e] + st.y * (acc[t][e] - mean1 - xh[t][e] * mean2);
+      stq<VEC>(rdx, m * lddx, 16 * t, lg, N, o);
+    }
+  }
+};
+
+}  // namespace gr

@@ -1,0 +1,100 @@
+"""Micro-benchmark of the attention kernels alone (forward, dK/dV, dQ, bias reduce) at
+the C2 (ml-1m) and C3 (ml-20m-like) shapes, timed by the library's live event timing.
+
+    python scripts/attn_micro.py --shape c2 --iters 50
+Run under rocprofv3 (program directly after `--`) for counters.
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from mygenerativerecommenders_amd import _lib, ops  # noqa: E402
+
+SHAPES = {
+    # B, N (padded), L (all sequences), d, H
+    "c2": (128, 211, 200, 50, 1),
+    "c3": (32, 2059, 2048, 256, 1),
+}
+
+
+def flops(B, L, d, H):
+    T = B * L * (L + 1) / 2 * H
+    return {"attn_fwd": 2 * T * 2 * d, "attn_bwd_dkv": 2 * T * 3 * d, "attn_bwd_dq": 2 * T * d}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shape", default="c2", choices=sorted(SHAPES))
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--only", default="", help="fwd|bwd")
+    args = ap.parse_args()
+    B, N, L, d, H = SHAPES[args.shape]
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev)
+    g.manual_seed(0)
+    rows = B * L
+    n_out = 4 * H * d
+    hv = H * d
+    uvqk = torch.randn(rows, n_out, device=dev, generator=g) * 0.5
+    q, k, v = uvqk[:, 2 * hv:3 * hv], uvqk[:, 3 * hv:], uvqk[:, hv:2 * hv]
+    offsets = torch.arange(0, B + 1, device=dev, dtype=torch.int64) * L
+    ts = (1_000_000_000 + torch.cumsum(torch.randint(0, 200_000, (B, N), device=dev,
+                                                     generator=g), 1)).to(torch.int64)
+    bmap = ops.bucket_map(ts, offsets, N)
+    pos_w = torch.randn(2 * N - 1, device=dev, generator=g) * 0.1
+    ts_w = torch.randn(129, device=dev, generator=g) * 0.1
+    out = torch.empty(rows, hv, device=dev)
+    dout = torch.randn(rows, hv, device=dev, generator=g)
+    dd = torch.empty(rows, n_out, device=dev)
+    dq, dk, dvv = dd[:, 2 * hv:3 * hv], dd[:, 3 * hv:], dd[:, hv:2 * hv]
+    dpw = torch.empty_like(pos_w)
+    dtw = torch.empty_like(ts_w)
+    L_ = _lib.lib()
+    ws_n = L_.hstu_attn_bwd_workspace_size(B, N, L, H, 128)
+    ws = torch.empty(max(ws_n, 4), dtype=torch.uint8, device=dev)
+    st = _lib.stream_handle()
+
+    def fwd():
+        _lib.call("hstu_attn_fwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out, n_out,
+                  offsets.data_ptr(), B, N, L, H, d, d, bmap.data_ptr(), pos_w.data_ptr(),
+                  ts_w.data_ptr(), 128, out.data_ptr(), hv, st)
+
+    def bwd():
+        _lib.call("hstu_attn_bwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out, n_out,
+                  dout.data_ptr(), hv, offsets.data_ptr(), B, N, L, H, d, d, bmap.data_ptr(),
+                  pos_w.data_ptr(), ts_w.data_ptr(), 128, None, None, None, 0,
+                  dq.data_ptr(), dk.data_ptr(), dvv.data_ptr(), n_out, dpw.data_ptr(),
+                  dtw.data_ptr(), ws.data_ptr(), ws_n, st)
+
+    for _ in range(3):
+        fwd()
+        bwd()
+    torch.cuda.synchronize()
+    _lib.timing_enable(True)
+    for _ in range(args.iters):
+        torch.cuda._sleep(2_000_000)
+        if args.only != "bwd":
+            fwd()
+        if args.only != "fwd":
+            bwd()
+    torch.cuda.synchronize()
+    _lib.timing_enable(False)
+    kt = _lib.kernel_times(("attn_fwd", "attn_bwd_dkv", "attn_bwd_dq", "attn_bias_reduce"))
+    fl = flops(B, L, d, H)
+    res = {}
+    for name, (tot, n) in kt.items():
+        if not n:
+            continue
+        avg = tot / n
+        res[name] = {"avg_us": round(avg * 1e3, 2),
+                     "tflops": round(fl.get(name, 0) / (avg * 1e-3) / 1e12, 2) if name in fl else None}
+    print(json.dumps({"shape": args.shape, "B": B, "N": N, "L": L, "d": d, "H": H,
+                      "kernels": res}))
+
+
+if __name__ == "__main__":
+    main()
