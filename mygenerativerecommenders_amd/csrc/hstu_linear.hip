@@ -457,180 +457,6 @@ static int launch_rowpanel(const Op& op, int64_t max_rows, bool full_row, const 
   return 0;
 }
 
-// ------------------------------------------------------------------ weight gradients
-// C[Ka, Nb] = sum_m A'(m, ka) * Bm(m, nb), A' = A or (A - mu_m) * rstd_m.
-// Grid: x = row chunk, y = output panel (64 ka x NT*16 nb).  Rows stream through LDS in
-// steps of 16 with a register prefetch of the next step (LDS-only barriers keep it in
-// flight).  Each workgroup writes its partial panel to a slab; wgrad_reduce sums the
-// chunks in a fixed order (deterministic, no atomics).
-constexpr int WG_KA = 64, WG_LDA = WG_KA + 16;
-
-struct WgradArgs {
-  const float* a;
-  int64_t lda;
-  const float2* a_stats;
-  const float* bm;
-  int64_t ldb;
-  const int64_t* offsets;
-  int B, Ka, Nb;
-  int64_t rows_per_chunk;
-  int n_chunks, panels_nb;
-  float* slabs;    // [n_chunks][Ka][Nb]
-  float* colsums;  // [n_chunks][Ka] or null
-};
-
-template <int NT>
-__global__ __launch_bounds__(256) void wgrad_partial_kernel(WgradArgs g) {
-  constexpr int NBW = NT * 16;
-  constexpr int LDB = (NT & 1) ? NBW : NBW + 16;  // == 16 mod 32
-  constexpr int BPT = (16 * NBW) / 256;            // B elements per thread per step
-  __shared__ __attribute__((aligned(16))) float As[BK * WG_LDA];
-  __shared__ __attribute__((aligned(16))) float Bs[BK * LDB];
-  const int chunk = blockIdx.x;
-  const int pa = blockIdx.y / g.panels_nb, pb = blockIdx.y % g.panels_nb;
-  const int ka0 = pa * WG_KA, nb0 = pb * NBW;
-  const int64_t total = g.offsets[g.B];
-  const int64_t r0 = (int64_t)chunk * g.rows_per_chunk;
-  const int64_t r1 = min(total, r0 + g.rows_per_chunk);
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  const int lr = lane & 15, lg = lane >> 4;
-  gptr<float> A = as_global(g.a);
-  gptr<float> Bg = as_global(g.bm);
-  const int n_it = r1 > r0 ? (int)((r1 - r0 + BK - 1) / BK) : 0;
-  // staging coordinates: A element e = tid + 256 i -> (row e / 64, col e % 64)
-  float ra[4], rb[BPT];
-  auto load = [&](int it) {
-    const int64_t m0 = r0 + (int64_t)it * BK;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int e = tid + 256 * i;
-      const int rr = e >> 6, c = e & 63;
-      const int64_t m = m0 + rr;
-      const int ka = ka0 + c;
-      const int64_t mc = m < r1 ? m : r0;
-      const int kc = ka < g.Ka ? ka : 0;
-      float v = A[mc * g.lda + kc];
-      if (g.a_stats) {
-        const float2 st = g.a_stats[mc];
-        v = (v - st.x) * st.y;
-      }
-      ra[i] = (m < r1 && ka < g.Ka) ? v : 0.f;
-    }
-#pragma unroll
-    for (int i = 0; i < BPT; ++i) {
-      const int e = tid + 256 * i;
-      const int rr = e / NBW, c = e - rr * NBW;
-      const int64_t m = m0 + rr;
-      const int nb = nb0 + c;
-      const int64_t mc = m < r1 ? m : r0;
-      const int nc = nb < g.Nb ? nb : 0;
-      const float v = Bg[mc * g.ldb + nc];
-      rb[i] = (m < r1 && nb < g.Nb) ? v : 0.f;
-    }
-  };
-  auto store = [&]() {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int e = tid + 256 * i;
-      As[(e >> 6) * WG_LDA + (e & 63)] = ra[i];
-    }
-#pragma unroll
-    for (int i = 0; i < BPT; ++i) {
-      const int e = tid + 256 * i;
-      const int rr = e / NBW, c = e - rr * NBW;
-      Bs[rr * LDB + c] = rb[i];
-    }
-  };
-  f4 acc[NT];
-#pragma unroll
-  for (int t = 0; t < NT; ++t) acc[t] = f4_zero();
-  float csum = 0.f;  // thread tid < 64 sums column ka0 + tid
-  if (n_it > 0) {
-    load(0);
-    store();
-    lds_barrier();
-  }
-  for (int it = 0; it < n_it; ++it) {
-    if (it + 1 < n_it) load(it + 1);
-    if (g.colsums && pb == 0 && tid < WG_KA) {
-#pragma unroll
-      for (int rr = 0; rr < BK; ++rr) csum += As[rr * WG_LDA + tid];
-    }
-#pragma unroll
-    for (int ks = 0; ks < BK / 4; ++ks) {
-      const float av = As[(4 * ks + lg) * WG_LDA + w * 16 + lr];
-      const float* brow = Bs + (4 * ks + lg) * LDB + lr;
-#pragma unroll
-      for (int t = 0; t < NT; ++t) acc[t] = mfma16x16x4(av, brow[t * 16], acc[t]);
-    }
-    lds_barrier();
-    if (it + 1 < n_it) {
-      store();
-      lds_barrier();
-    }
-  }
-  float* slab = g.slabs + (int64_t)chunk * g.Ka * g.Nb;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int ka = ka0 + w * 16 + 4 * lg + r;
-    if (ka >= g.Ka) continue;
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const int nb = nb0 + 16 * t + lr;
-      if (nb < g.Nb) slab[(int64_t)ka * g.Nb + nb] = acc[t][r];
-    }
-  }
-  if (g.colsums && pb == 0 && tid < WG_KA && ka0 + tid < g.Ka)
-    g.colsums[(int64_t)chunk * g.Ka + ka0 + tid] = csum;
-}
-
-// out[i] = sum_c slabs[c][i] in chunk order (4 waves x strided chunks, then wave order)
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* slabs, int n_chunks,
-                                                           int64_t n_elem, float* out) {
-  __shared__ float part[4][64];
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int64_t i = (int64_t)blockIdx.x * 64 + lane;
-  gptr<float> src = as_global(slabs);
-  float acc = 0.f;
-  if (i < n_elem) {
-    int c = w;
-    for (; c + 28 < n_chunks; c += 32) {
-      float v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = src[(int64_t)(c + 4 * u) * n_elem + i];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) acc += v[u];
-    }
-    for (; c < n_chunks; c += 4) acc += src[(int64_t)c * n_elem + i];
-  }
-  part[w][lane] = acc;
-  __syncthreads();
-  if (w == 0 && i < n_elem) out[i] = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
-}
-
-static int wgrad_nt(int Nb) {
-  const int nt = ceil_div(Nb, 16);
-  if (nt <= 4) return 4;
-  if (nt <= 8) return 8;
-  if (nt <= 13) return 13;
-  return 16;
-}
-
-static void wgrad_plan(int64_t max_rows, int Ka, int Nb, int* n_chunks, int64_t* rows_per_chunk,
-                       int* panels, int* panels_nb) {
-  const int nt = wgrad_nt(Nb);
-  const int pa = ceil_div(Ka, WG_KA), pb = ceil_div(Nb, nt * 16);
-  *panels = pa * pb;
-  *panels_nb = pb;
-  int target = ceil_div(512, *panels);  // ~2 workgroups per CU
-  int64_t rpc = (max_rows + target - 1) / target;
-  rpc = ((rpc + 15) / 16) * 16;
-  if (rpc < 64) rpc = 64;
-  *rows_per_chunk = rpc;
-  *n_chunks = (int)((max_rows + rpc - 1) / rpc);
-  if (*n_chunks < 1) *n_chunks = 1;
-}
-
 // ------------------------------------------------------------------ row-wave dispatch
 // Narrow shapes (weight panel in LDS, <= 80 KiB) run the row-wave kernel (rowwave.h);
 // everything else the row-panel kernel above.  Returns -1 when the shape / alignment
@@ -726,6 +552,10 @@ static int rw_dispatch(const Args& a, int K, int N, int vec, int64_t max_rows, c
                        hipStream_t st) {
   const int kg = rw_bucket(K), nt = rw_bucket(N);
   if (kg < 0 || nt < 0 || vec == 0) return -1;
+  // measured (ml-1m, MI355X): the row-wave form wins for the square D x D projections
+  // (gate/_o fwd+bwd, 26 -> 17 us, 20 -> 16 us); the row panel keeps the 4x-wide
+  // UVQK projection (27 vs 33 us fwd) where one 16-row unit carries 13 column tiles
+  if (kg > 8 || nt > 8) return -1;
   if (max_rows * 4 * 1024 > 0x7fffffffLL) return -1;  // 32-bit buffer offsets
   (void)vec;  // 4-aligned shapes run the 8-byte path too (one instantiation set)
   return rw_kg<2, OpT>(a, kg, nt, max_rows, tname, st);
@@ -855,8 +685,7 @@ extern "C" int hstu_ln_uvqk_bwd(const float* dh, int64_t ld_dh, const int64_t* o
                                 void* stream) {
   GR_REQUIRE(dh && offsets && w_uvqk && x && x_stats && dx, "hstu_ln_uvqk_bwd: null pointer");
   GR_REQUIRE(D > 0 && n_out > 0 && B >= 0, "hstu_ln_uvqk_bwd: bad sizes");
-  // the row-wave variant is not faster here for K = n_out >= 128 (many k-groups per row)
-  if (rw_enabled() && n_out <= 64) {
+  if (rw_enabled()) {
     RwArgsLnUvqkBwd ra{offsets, B, n_out, D, dh, ld_dh, w_uvqk, x, ld_x, (const float2*)x_stats,
                        dy_res, ld_dy, dx, ld_dx};
     const int vec = rw_vec({dh, x, dy_res, dx}, {ld_dh, ld_x, ld_dy, ld_dx, n_out, D});
@@ -868,53 +697,4 @@ extern "C" int hstu_ln_uvqk_bwd(const float* dh, int64_t ld_dh, const int64_t* o
   op.w = w_uvqk; op.x = x; op.ldx = ld_x; op.x_stats = (const float2*)x_stats;
   op.dy = dy_res; op.lddy = ld_dy; op.dx = dx; op.lddx = ld_dx;
   return launch_rowpanel(op, max_rows, true, "hstu_ln_uvqk_bwd", (hipStream_t)stream);
-}
-
-extern "C" size_t gr_wgrad_workspace_size(int64_t max_rows, int Ka, int Nb) {
-  if (max_rows <= 0 || Ka <= 0 || Nb <= 0) return 0;
-  int n_chunks, panels, pnb;
-  int64_t rpc;
-  wgrad_plan(max_rows, Ka, Nb, &n_chunks, &rpc, &panels, &pnb);
-  return sizeof(float) * (size_t)n_chunks * ((size_t)Ka * Nb + Ka);
-}
-
-extern "C" int gr_wgrad(const float* a, int64_t lda, const float* a_stats, const float* bm,
-                        int64_t ldb, const int64_t* offsets, int B, int64_t max_rows, int Ka,
-                        int Nb, float* c, float* a_colsum, void* workspace, size_t ws_bytes,
-                        void* stream) {
-  GR_REQUIRE(a && bm && offsets && c, "gr_wgrad: null pointer");
-  GR_REQUIRE(Ka > 0 && Nb > 0 && B >= 0 && max_rows >= 0, "gr_wgrad: bad sizes");
-  hipStream_t st = (hipStream_t)stream;
-  if (max_rows == 0) {
-    (void)hipMemsetAsync(c, 0, sizeof(float) * (size_t)Ka * Nb, st);
-    if (a_colsum) (void)hipMemsetAsync(a_colsum, 0, sizeof(float) * Ka, st);
-    return 0;
-  }
-  int n_chunks, panels, pnb;
-  int64_t rpc;
-  wgrad_plan(max_rows, Ka, Nb, &n_chunks, &rpc, &panels, &pnb);
-  const size_t need = sizeof(float) * (size_t)n_chunks * ((size_t)Ka * Nb + Ka);
-  GR_REQUIRE(workspace && ws_bytes >= need, "gr_wgrad: workspace %zu B < %zu B", ws_bytes, need);
-  float* slabs = (float*)workspace;
-  float* cs = a_colsum ? slabs + (size_t)n_chunks * Ka * Nb : nullptr;
-  WgradArgs g{a, lda, (const float2*)a_stats, bm, ldb, offsets, B, Ka, Nb, rpc, n_chunks,
-              pnb, slabs, cs};
-  const dim3 grid(n_chunks, panels);
-  switch (wgrad_nt(Nb)) {
-    case 4: GR_TIMED("wgrad_partial", st, hipLaunchKernelGGL(wgrad_partial_kernel<4>, grid, dim3(256), 0, st, g)); break;
-    case 8: GR_TIMED("wgrad_partial", st, hipLaunchKernelGGL(wgrad_partial_kernel<8>, grid, dim3(256), 0, st, g)); break;
-    case 13: GR_TIMED("wgrad_partial", st, hipLaunchKernelGGL(wgrad_partial_kernel<13>, grid, dim3(256), 0, st, g)); break;
-    default: GR_TIMED("wgrad_partial", st, hipLaunchKernelGGL(wgrad_partial_kernel<16>, grid, dim3(256), 0, st, g)); break;
-  }
-  GR_LAUNCH_CHECK("gr_wgrad(partial)");
-  const int64_t ne = (int64_t)Ka * Nb;
-  GR_TIMED("wgrad_reduce", st, hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((ne + 63) / 64)), dim3(256), 0, st,
-                     slabs, n_chunks, ne, c));
-  GR_LAUNCH_CHECK("gr_wgrad(reduce)");
-  if (a_colsum) {
-    GR_TIMED("wgrad_reduce", st, hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((Ka + 63) / 64)), dim3(256), 0,
-                       st, cs, n_chunks, (int64_t)Ka, a_colsum));
-    GR_LAUNCH_CHECK("gr_wgrad(colsum)");
-  }
-  return 0;
 }

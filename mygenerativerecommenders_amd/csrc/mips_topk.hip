@@ -30,7 +30,9 @@
 namespace gr {
 
 constexpr int QG = 16;       // queries per workgroup (MFMA column block)
-constexpr int CAP = 512;     // per-query candidate buffer
+constexpr int SW = 8;        // waves per select workgroup (2 per SIMD, one LDS buffer set)
+constexpr int ST = SW * 64;  // select threads
+constexpr int CAP = 512;     // per-query candidate buffer: k (<= 256) + one step (SW * STEP <= 256)
 constexpr int INV_MAX = 256; // max invalid ids per query
 constexpr uint32_t VERIFIED = 0x80000000u;
 
@@ -148,18 +150,18 @@ struct SelectArgs {
 };
 
 template <int KS, int BLOCKS>
-__global__ __launch_bounds__(256) void mips_select_kernel(SelectArgs a) {
+__global__ __launch_bounds__(ST) void mips_select_kernel(SelectArgs a) {
   constexpr int KS2 = (KS + 1) / 2;
   constexpr int STEP = BLOCKS * 16;  // items per wave per step
   __shared__ float cs[QG * CAP];
   __shared__ uint32_t ci[QG * CAP];
   __shared__ int64_t inv[QG * INV_MAX];
-  __shared__ int hist[4 * 256];
+  __shared__ int hist[SW * 256];
   __shared__ int cnt[QG];
   __shared__ float tau_s[QG];
   __shared__ int need_compact;
 
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int tid = threadIdx.x, w = wave_id(), lane = tid & 63;
   const int lr = lane & 15, lg = lane >> 4;
   // XCD-aware decode: the query groups of one item range share blockIdx % 8
   const int n_qg = (a.B + QG - 1) / QG;
@@ -174,7 +176,7 @@ __global__ __launch_bounds__(256) void mips_select_kernel(SelectArgs a) {
 
   // ---- prologue: sorted invalid lists, counters
   const int n0p = a.N0 > 0 ? (a.N0 <= 64 ? 64 : (a.N0 <= 128 ? 128 : 256)) : 0;
-  for (int e = tid; e < QG * n0p; e += 256) {
+  for (int e = tid; e < QG * n0p; e += ST) {
     const int qq = e / n0p, j = e - qq * n0p;
     int64_t v = INT64_MAX;
     if (q0 + qq < a.B && j < a.N0) v = a.invalid[(int64_t)(q0 + qq) * a.N0 + j];
@@ -187,7 +189,7 @@ __global__ __launch_bounds__(256) void mips_select_kernel(SelectArgs a) {
   __syncthreads();
   for (int size = 2; size <= n0p; size <<= 1) {  // bitonic sort, QG independent rows
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int e = tid; e < QG * (n0p / 2); e += 256) {
+      for (int e = tid; e < QG * (n0p / 2); e += ST) {
         const int qq = e / (n0p / 2), p = e - qq * (n0p / 2);
         const int i = 2 * p - (p & (stride - 1));
         const int j = i + stride;
@@ -215,7 +217,7 @@ __global__ __launch_bounds__(256) void mips_select_kernel(SelectArgs a) {
   }
 
   const int64_t n_items = x_end > x_begin ? x_end - x_begin : 0;
-  const int n_steps = (int)((n_items + 4 * STEP - 1) / (4 * STEP));
+  const int n_steps = (int)((n_items + SW * STEP - 1) / (SW * STEP));
   typedef float fv2 __attribute__((ext_vector_type(2)));
   gptr<fv2> pk = as_global(reinterpret_cast<const fv2*>(a.packed));
   int* whist = hist + w * 256;
@@ -324,7 +326,7 @@ __global__ __launch_bounds__(256) void mips_select_kernel(SelectArgs a) {
   const int64_t last_blk = (a.X + 15) / 16 - 1;
   fv2 fa[BLOCKS][KS2], fb[BLOCKS][KS2];
   auto load_step = [&](fv2 (&f)[BLOCKS][KS2], int step) {
-    const int64_t xb = x_begin + ((int64_t)step * 4 + w) * STEP;
+    const int64_t xb = x_begin + ((int64_t)step * SW + w) * STEP;
 #pragma unroll
     for (int bb = 0; bb < BLOCKS; ++bb) {
       int64_t ib = (xb >> 4) + bb;
@@ -336,7 +338,7 @@ __global__ __launch_bounds__(256) void mips_select_kernel(SelectArgs a) {
   };
   auto process = [&](const fv2 (&f)[BLOCKS][KS2], int step) {
     const float tau = tau_s[lr];
-    const int64_t xb = x_begin + ((int64_t)step * 4 + w) * STEP;
+    const int64_t xb = x_begin + ((int64_t)step * SW + w) * STEP;
     f4 s[BLOCKS];
 #pragma unroll
     for (int bb = 0; bb < BLOCKS; ++bb) s[bb] = f4_zero();
@@ -359,13 +361,13 @@ __global__ __launch_bounds__(256) void mips_select_kernel(SelectArgs a) {
     }
     lds_barrier();
     if (w == 0) {
-      const bool fl = lane < QG && cnt[lane] > CAP - 4 * STEP;
+      const bool fl = lane < QG && cnt[lane] > CAP - SW * STEP;
       const unsigned long long bal = __ballot(fl);
       if (lane == 0) need_compact = bal != 0ull;
     }
     lds_barrier();
     if (need_compact) {
-      for (int qq = w; qq < QG; qq += 4)
+      for (int qq = w; qq < QG; qq += SW)
         if (cnt[qq] > a.k) compact(qq, a.k);
       lds_barrier();
     }
@@ -385,12 +387,12 @@ __global__ __launch_bounds__(256) void mips_select_kernel(SelectArgs a) {
   // ---- final: this range's candidates per query (exact top-k_part, invalid removed;
   // when at most k_part remain this is only the invalid-id filter: the merge selects)
   __syncthreads();
-  for (int qq = w; qq < QG; qq += 4) {
+  for (int qq = w; qq < QG; qq += SW) {
     if (q0 + qq >= a.B) continue;
     compact(qq, a.k_part);
   }
   __syncthreads();
-  for (int e = tid; e < QG * a.k_part; e += 256) {
+  for (int e = tid; e < QG * a.k_part; e += ST) {
     const int qq = e / a.k_part, j = e - qq * a.k_part;
     if (q0 + qq >= a.B) continue;
     const int64_t o = ((int64_t)range * a.B + q0 + qq) * a.k_part + j;
@@ -600,7 +602,7 @@ static TopkPlan plan_topk(int B, int64_t X, int D, int k) {
   p.KS = ceil_div(D, 4);
   const int n_qg = ceil_div(B, QG);
   int target = ceil_div(256, n_qg);  // ~one workgroup per CU
-  int64_t step4 = 4 * 64;
+  int64_t step4 = SW * 64;
   int64_t ri = (X + target - 1) / target;
   ri = ((ri + step4 - 1) / step4) * step4;
   if (ri < step4) ri = step4;
@@ -622,11 +624,11 @@ static TopkPlan plan_topk(int B, int64_t X, int D, int k) {
 
 template <int KS>
 static int launch_select(const SelectArgs& a, hipStream_t st) {
-  constexpr int BLOCKS = KS <= 16 ? 4 : (KS <= 32 ? 2 : 1);
+  constexpr int BLOCKS = KS <= 16 ? 2 : 1;  // SW * 16 * BLOCKS <= CAP - 256
   const int n_qg = ceil_div(a.B, QG);
   const int n_r8 = ceil_div(a.n_ranges, 8) * 8;
   const int grid = n_r8 * n_qg;
-  GR_TIMED("mips_select", st, hipLaunchKernelGGL((mips_select_kernel<KS, BLOCKS>), dim3(grid), dim3(256), 0, st, a));
+  GR_TIMED("mips_select", st, hipLaunchKernelGGL((mips_select_kernel<KS, BLOCKS>), dim3(grid), dim3(ST), 0, st, a));
   GR_LAUNCH_CHECK("mips_topk(select)");
   return 0;
 }
