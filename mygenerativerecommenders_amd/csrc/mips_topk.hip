@@ -591,7 +591,88 @@ __global__ __launch_bounds__(256) void mips_merge_kernel(MergeArgs a) {
   }
 }
 
+// ----------------------------------------------------------------- small catalogs
+// X <= MERGE_MAX: a workgroup per query scores every item (the same k-ordered fmaf chain,
+// read from the packed layout), excludes its invalid ids (arange ids: direct index
+// scatter after the scores are written; explicit ids: binary search in the sorted list)
+// and hands all X scores to the merge kernel as one candidate list.  Replaces the
+// range/threshold machinery, whose fixed per-workgroup costs dominate at ml-1m sizes.
+struct ScoreAllArgs {
+  const float* q;
+  const float* packed;
+  int64_t X;
+  int D, B, N0;
+  const int64_t* item_ids;
+  int64_t index_base;
+  const int64_t* invalid;
+  float* out_score;    // [B][X]
+  int64_t* out_index;  // [B][X], -1 = excluded
+};
+
+template <int KS2>
+__global__ __launch_bounds__(256) void mips_scoreall_kernel(ScoreAllArgs a) {
+  __shared__ float qv[8 * KS2];
+  __shared__ int64_t inv[INV_MAX];
+  const int q = blockIdx.x, tid = threadIdx.x;
+  for (int d = tid; d < 8 * KS2; d += 256) qv[d] = d < a.D ? a.q[(int64_t)q * a.D + d] : 0.f;
+  const bool search = a.item_ids && a.N0 > 0;
+  const int n0p = a.N0 <= 64 ? 64 : (a.N0 <= 128 ? 128 : 256);
+  if (search) {
+    for (int j = tid; j < n0p; j += 256) inv[j] = j < a.N0 ? a.invalid[(int64_t)q * a.N0 + j] : INT64_MAX;
+    __syncthreads();
+    for (int size = 2; size <= n0p; size <<= 1)
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        for (int p = tid; p < n0p / 2; p += 256) {
+          const int i = 2 * p - (p & (stride - 1)), j = i + stride;
+          const bool up = (i & size) == 0;
+          const int64_t x = inv[i], y = inv[j];
+          if ((x > y) == up) {
+            inv[i] = y;
+            inv[j] = x;
+          }
+        }
+        __syncthreads();
+      }
+  }
+  __syncthreads();
+  typedef float fv2 __attribute__((ext_vector_type(2)));
+  gptr<fv2> pk = as_global(reinterpret_cast<const fv2*>(a.packed));
+  float* os = a.out_score + (int64_t)q * a.X;
+  int64_t* oi = a.out_index + (int64_t)q * a.X;
+  for (int64_t i = tid; i < a.X; i += 256) {
+    const int64_t ib = i >> 4;
+    const int il = (int)(i & 15);
+    float e[8 * KS2];
+#pragma unroll
+    for (int j = 0; j < KS2; ++j)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const fv2 v = pk[(ib * KS2 + j) * 64 + 16 * c + il];
+        e[8 * j + c] = v.x;      // d = 8j + c      (k-step 2j)
+        e[8 * j + 4 + c] = v.y;  // d = 8j + 4 + c  (k-step 2j + 1)
+      }
+    float sc = 0.f;
+#pragma unroll
+    for (int d = 0; d < 8 * KS2; ++d) sc = fmaf(qv[d], e[d], sc);  // padding adds +0 exactly
+    bool ok = true;
+    if (search) ok = !sorted_contains(inv, a.N0 > 0 ? n0p : 0, a.item_ids[i]);
+    os[i] = ok ? sc : -INFINITY;
+    oi[i] = ok ? a.index_base + i : -1;
+  }
+  if (!a.item_ids && a.N0 > 0) {  // arange ids: exclude by direct index
+    __syncthreads();
+    for (int j = tid; j < a.N0; j += 256) {
+      const int64_t li = a.invalid[(int64_t)q * a.N0 + j] - a.index_base;
+      if (li >= 0 && li < a.X) {
+        os[li] = -INFINITY;
+        oi[li] = -1;
+      }
+    }
+  }
+}
+
 struct TopkPlan {
+  bool small;
   int KS, n_ranges, k_part;
   int64_t range_items;
   size_t part_bytes;
@@ -619,6 +700,11 @@ static TopkPlan plan_topk(int B, int64_t X, int D, int k) {
   kp = kp > CAP / 2 ? CAP / 2 : kp;
   p.k_part = kp > k ? kp : k;
   p.part_bytes = (size_t)p.n_ranges * B * p.k_part * (sizeof(float) + sizeof(int64_t));
+  p.small = X > 0 && X <= MERGE_MAX && (p.KS + 1) / 2 <= 8;  // D <= 64
+  if (p.small) {
+    const size_t sb = (size_t)B * X * (sizeof(float) + sizeof(int64_t));
+    if (sb > p.part_bytes) p.part_bytes = sb;
+  }
   return p;
 }
 
@@ -672,6 +758,27 @@ extern "C" int mips_topk(const float* queries, const float* packed_items, int64_
   TopkPlan p = plan_topk(B, X > 0 ? X : 1, D, k);
   GR_REQUIRE(workspace && ws_bytes >= p.part_bytes, "mips_topk: workspace %zu B < %zu B", ws_bytes,
              p.part_bytes);
+  if (p.small) {
+    float* sc = (float*)workspace;
+    int64_t* ix = (int64_t*)(sc + (size_t)B * X);
+    ScoreAllArgs s{queries, packed_items, X, D, B, N0, item_ids, index_base, invalid_ids, sc, ix};
+    const int KS2 = (p.KS + 1) / 2;
+#define GR_SA(K2)                                                                           \
+  case K2:                                                                                  \
+    GR_TIMED("mips_select", st, hipLaunchKernelGGL(mips_scoreall_kernel<K2>, dim3(B), dim3(256), 0, st, s)); \
+    break;
+    switch (KS2) {
+      GR_SA(1) GR_SA(2) GR_SA(3) GR_SA(4) GR_SA(5) GR_SA(6) GR_SA(7) GR_SA(8)
+      default: GR_REQUIRE(false, "mips_topk: score-all path needs D <= 64");
+    }
+#undef GR_SA
+    GR_LAUNCH_CHECK("mips_topk(score-all)");
+    MergeArgs m{sc, ix, nullptr, 1, B, (int)X, k, item_ids, index_base,
+                out_scores, out_ids, out_index};
+    GR_TIMED("mips_merge", st, hipLaunchKernelGGL(mips_merge_kernel, dim3(B), dim3(256), 0, st, m));
+    GR_LAUNCH_CHECK("mips_topk(merge)");
+    return 0;
+  }
   float* part_score = (float*)workspace;
   int64_t* part_index = (int64_t*)(part_score + (size_t)p.n_ranges * B * p.k_part);
   SelectArgs a{queries, packed_items, X, D, B, k, N0, p.n_ranges, p.k_part, p.range_items,

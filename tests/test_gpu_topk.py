@@ -82,6 +82,22 @@ def test_mips_topk_bitexact_vs_oracle(B, X, D, k, N0):
     _check_exact(Q, E, ids, inv, k)
 
 
+@pytest.mark.parametrize("X", [3953, 40_000])
+def test_mips_topk_explicit_ids_bitexact(X):
+    """Non-arange item ids (explicit id table): the small-catalog path searches each item
+    in the sorted invalid list, the large path filters during compaction."""
+    g = np.random.default_rng(X)
+    B, D, k, N0 = 96, 50, 200, 211
+    E = g.standard_normal((X, D), dtype=np.float32)
+    Q = g.standard_normal((B, D), dtype=np.float32)
+    ids = g.permutation(np.arange(10, 10 + 3 * X, 3, dtype=np.int64))
+    inv = np.zeros((B, N0), np.int64)
+    for b in range(B):
+        inv[b] = g.choice(ids, N0)
+    inv[:, -5:] = 0  # padding ids that match nothing
+    _check_exact(Q, E, ids, inv, k)
+
+
 def test_mips_topk_adversarial_orderings():
     """Sorted catalog (every item beats the running threshold: maximum compactions),
     all-equal scores (ties resolved by index), duplicated / zero invalid ids, and
