@@ -41,36 +41,79 @@ __device__ __forceinline__ uint32_t buf_ld_u32(__amdgpu_buffer_rsrc_t r, int vof
 }
 
 // Register-staged ROWS x CP tile of a jagged column block, loaded through a seq_rsrc
-// descriptor.  Thread t owns column c_t = t % CPR (CPR = CP rounded up to a power of
-// two) of rows r_t + RPP * i: one voffset VGPR per thread, the row step is an SGPR
-// soffset, rows past the sequence come back as 0 from the range check.
+// descriptor; rows past the sequence come back as 0 from the range check.
+//   dword path: thread t owns column t % CPR (CPR = CP rounded up to a power of two) of
+//               rows t / CPR + RPP i;
+//   pair path (vec2: 8-byte aligned rows, even ncols): thread t owns columns 2(t % CPH),
+//               +1 (CPH = CPR / 2) of rows t / CPH + RPP2 i — half the load / LDS-store
+//               instructions (vector-memory issue is the limiter when a CU's waves
+//               stage tiles together).
+// One voffset VGPR per thread, the row step is an SGPR soffset.
 template <int CP, int ROWS>
 struct BufTile {
   static constexpr int CPR = CP <= 16 ? 16 : CP <= 32 ? 32 : CP <= 64 ? 64 : CP <= 128 ? 128 : 256;
-  static constexpr int RPP = 256 / CPR;  // rows per pass
+  static constexpr int RPP = 256 / CPR;  // rows per pass (dwords)
   static constexpr int PER = (ROWS + RPP - 1) / RPP;
-  float v[PER];
-  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t r, int64_t ld, int r0, int ncols) {
+  static constexpr int CPH = CPR / 2;
+  static constexpr int RPP2 = 256 / CPH;  // rows per pass (pairs)
+  static constexpr int PER2 = (ROWS + RPP2 - 1) / RPP2;
+  static constexpr int NV = PER > 2 * PER2 ? PER : 2 * PER2;
+  float v[NV];
+  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t r, int64_t ld, int r0, int ncols,
+                                       bool vec2) {
     const int tid = threadIdx.x;
-    const int c = tid % CPR, rr = tid / CPR;
-    const int voff = ((r0 + rr) * (int)ld + c) * 4;
-    const int step = RPP * (int)ld * 4;
+    if (vec2) {
+      const int c = 2 * (tid % CPH), rr = tid / CPH;
+      const int voff = c < ncols ? ((r0 + rr) * (int)ld + c) * 4 : 0x40000000;
+      const int step = RPP2 * (int)ld * 4;
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const float x = buf_ld(r, voff, i * step);
-      v[i] = c < ncols ? x : 0.f;
+      for (int i = 0; i < PER2; ++i) {
+        typedef unsigned int u2_ __attribute__((ext_vector_type(2)));
+        const u2_ x = __builtin_amdgcn_raw_buffer_load_b64(r, voff, i * step, 0);
+        v[2 * i] = __uint_as_float(x.x);
+        v[2 * i + 1] = __uint_as_float(x.y);
+      }
+    } else {
+      const int c = tid % CPR, rr = tid / CPR;
+      const int voff = ((r0 + rr) * (int)ld + c) * 4;
+      const int step = RPP * (int)ld * 4;
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const float x = buf_ld(r, voff, i * step);
+        v[i] = c < ncols ? x : 0.f;
+      }
     }
   }
-  __device__ __forceinline__ void store(float* lds, int ldl) const {
+  __device__ __forceinline__ void store(float* lds, int ldl, bool vec2) const {
     const int tid = threadIdx.x;
-    const int c = tid % CPR, rr = tid / CPR;
-    if (c < CP) {
+    if (vec2) {
+      const int c = 2 * (tid % CPH), rr = tid / CPH;
+      if (c < CP) {
 #pragma unroll
-      for (int i = 0; i < PER; ++i)
-        if (RPP * PER == ROWS || rr + RPP * i < ROWS) lds[(rr + RPP * i) * ldl + c] = v[i];
+        for (int i = 0; i < PER2; ++i)
+          if (RPP2 * PER2 == ROWS || rr + RPP2 * i < ROWS)
+            *reinterpret_cast<float2*>(lds + (rr + RPP2 * i) * ldl + c) =
+                make_float2(v[2 * i], v[2 * i + 1]);
+      }
+    } else {
+      const int c = tid % CPR, rr = tid / CPR;
+      if (c < CP) {
+#pragma unroll
+        for (int i = 0; i < PER; ++i)
+          if (RPP * PER == ROWS || rr + RPP * i < ROWS) lds[(rr + RPP * i) * ldl + c] = v[i];
+      }
     }
   }
 };
+
+// Host: true when every pointer is 8-byte aligned and every stride / width is even.
+inline int pair_aligned(std::initializer_list<const void*> ptrs, std::initializer_list<int64_t> vals) {
+  for (const void* p : ptrs)
+    if ((uintptr_t)p % 8 != 0) return 0;
+  for (int64_t v : vals)
+    if (v % 2 != 0) return 0;
+  return 1;
+}
 
 // Bucket-map descriptor for sequence b (tiles of 4096 bytes; records = 0 when there is
 // no map, so every map load returns bucket 0).

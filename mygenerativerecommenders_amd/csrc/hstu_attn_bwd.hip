@@ -23,6 +23,26 @@
 
 namespace gr {
 
+#ifdef GR_STAMP
+// Diagnostic build only: per-wave phase cycle sums of the dK/dV kernel.
+__device__ unsigned long long gr_stamp_buf[1 << 16];
+__device__ __forceinline__ unsigned long long gr_stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define GR_ST(acc)                                \
+  do {                                            \
+    const unsigned long long t1_ = gr_stamp();    \
+    acc += t1_ - st_t0;                           \
+    st_t0 = t1_;                                  \
+  } while (0)
+#else
+#define GR_ST(acc) do { } while (0)
+#endif
+
 struct AttnBwdArgs {
   const float* q;
   const float* k;
@@ -47,6 +67,7 @@ struct AttnBwdArgs {
   int64_t ld_d;
   float* slabs;  // [grid][2N-1 + nb+1]
   float inv_n;
+  int vec2;  // 8-byte pair staging (aligned rows, even widths)
 };
 
 // TT = rows per streamed LDS tile (queries in dK/dV, keys in dQ): 64, or 16 for the
@@ -160,8 +181,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
   BufTile<C::VP, TT> dst;
   uint32_t mw[C::TB], mwn[C::TB];
   auto load_tile = [&](int qt, uint32_t (&m)[C::TB]) {
-    qst.load(rq, a.ld_qk, qt * TT, a.dqk);
-    dst.load(rdo, a.ld_dout, qt * TT, a.dv);
+    qst.load(rq, a.ld_qk, qt * TT, a.dqk, a.vec2);
+    dst.load(rdo, a.ld_dout, qt * TT, a.dv, a.vec2);
 #pragma unroll
     for (int qb = 0; qb < C::TB; ++qb)
       m[qb] = buf_ld_u32(rmap, map_voff, map_soff(qt * TT + qb * 16, k0, false));
@@ -170,13 +191,18 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
   const int wk_lo = k0 + w * 16;
   const int last_qt = (L - 1) / TT;
   load_tile(k0 / TT, mw);
-  qst.store(Qs, C::LDQ);
-  dst.store(Ds, C::LDV);
+  qst.store(Qs, C::LDQ, a.vec2);
+  dst.store(Ds, C::LDV, a.vec2);
   __syncthreads();
+#ifdef GR_STAMP
+  unsigned long long st_t0 = gr_stamp(), st_ld = 0, st_mm1 = 0, st_ew = 0, st_bias = 0,
+                     st_mm2 = 0, st_sync = 0;
+#endif
   for (int qt = k0 / TT; qt <= last_qt; ++qt) {
     const int q0 = qt * TT;
     const bool more = qt < last_qt;
     if (more) load_tile(qt + 1, mwn);
+    GR_ST(st_ld);
 #pragma unroll
     for (int qb = 0; qb < C::TB; ++qb) {
       const int qb0 = q0 + qb * 16;
@@ -190,6 +216,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
           s = mfma16x16x4(qrow[4 * st], kreg[st], s);
           dp = mfma16x16x4(drow[4 * st], vreg[st], dp);
         }
+        GR_ST(st_mm1);
         float p[4], ds[4];
         int bk[4];
 #pragma unroll
@@ -208,6 +235,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
           if (has_bias) atomicAdd(&whist[pi], ds[r]);  // dpos_w (masked: adds 0)
 #endif
         }
+        GR_ST(st_ew);
 #if GR_DPOS_ROT
         if (has_bias) {
           // dpos_w: element (query 4lg + r, key lr) has diagonal e = lr - (4lg + r).
@@ -246,29 +274,71 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
           }
           atomicAdd(&wts[bk[3]], run);
         }
+        GR_ST(st_bias);
         // dV[key][c] += P^T dO ; dK[key][d] += dS^T Q   (k-step r: queries 4g + r)
         const float* dcol = Ds + (qb * 16 + 4 * lg) * C::LDV + lr;
         const float* qcol = Qs + (qb * 16 + 4 * lg) * C::LDQ + lr;
+        if constexpr (VTILES + C::KT > 8) {  // wide heads: no registers to spare
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+#pragma unroll
+            for (int t = 0; t < VTILES; ++t)
+              dV[t] = mfma16x16x4(p[r], dcol[r * C::LDV + t * 16], dV[t]);
+#pragma unroll
+            for (int t = 0; t < C::KT; ++t)
+              dK[t] = mfma16x16x4(ds[r], qcol[r * C::LDQ + t * 16], dK[t]);
+          }
+        } else {
+        // B operands of k-step r+1 are read from LDS while the MFMAs of step r run
+        float bvv[2][VTILES], bvk[2][C::KT];
+#pragma unroll
+        for (int t = 0; t < VTILES; ++t) bvv[0][t] = dcol[t * 16];
+#pragma unroll
+        for (int t = 0; t < C::KT; ++t) bvk[0][t] = qcol[t * 16];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
+          if (r + 1 < 4) {
 #pragma unroll
-          for (int t = 0; t < VTILES; ++t)
-            dV[t] = mfma16x16x4(p[r], dcol[r * C::LDV + t * 16], dV[t]);
+            for (int t = 0; t < VTILES; ++t) bvv[(r + 1) & 1][t] = dcol[(r + 1) * C::LDV + t * 16];
 #pragma unroll
-          for (int t = 0; t < C::KT; ++t)
-            dK[t] = mfma16x16x4(ds[r], qcol[r * C::LDQ + t * 16], dK[t]);
+            for (int t = 0; t < C::KT; ++t) bvk[(r + 1) & 1][t] = qcol[(r + 1) * C::LDQ + t * 16];
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int t = 0; t < VTILES; ++t) dV[t] = mfma16x16x4(p[r], bvv[r & 1][t], dV[t]);
+#pragma unroll
+          for (int t = 0; t < C::KT; ++t) dK[t] = mfma16x16x4(ds[r], bvk[r & 1][t], dK[t]);
+          __builtin_amdgcn_sched_barrier(0);
         }
+        }
+        GR_ST(st_mm2);
       }
     }
     if (more) {
       lds_barrier();
-      qst.store(Qs, C::LDQ);
-      dst.store(Ds, C::LDV);
+      qst.store(Qs, C::LDQ, a.vec2);
+      dst.store(Ds, C::LDV, a.vec2);
 #pragma unroll
       for (int qb = 0; qb < C::TB; ++qb) mw[qb] = mwn[qb];
       lds_barrier();
     }
+    GR_ST(st_sync);
   }
+#ifdef GR_STAMP
+  if (lane == 0) {
+    const int slot = (blockIdx.x * 4 + w) * 8;
+    if (slot + 8 <= (1 << 16)) {
+      gr_stamp_buf[slot + 0] = st_ld;
+      gr_stamp_buf[slot + 1] = st_mm1;
+      gr_stamp_buf[slot + 2] = st_ew;
+      gr_stamp_buf[slot + 3] = st_bias;
+      gr_stamp_buf[slot + 4] = st_mm2;
+      gr_stamp_buf[slot + 5] = st_sync;
+      gr_stamp_buf[slot + 6] = (unsigned long long)kt;
+      gr_stamp_buf[slot + 7] = 1;
+    }
+  }
+#endif
 
   // ---- epilogue: rows = keys wk_lo + 4lg + r, cols = lr + 16 t
 #pragma unroll
@@ -370,15 +440,15 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   BufTile<C::VP, TT> vst;
   uint32_t mw[C::TB], mwn[C::TB];
   auto load_tile = [&](int kt, uint32_t (&m)[C::TB]) {
-    kst.load(rk, a.ld_qk, kt * TT, a.dqk);
-    vst.load(rv, a.ld_v, kt * TT, a.dv);
+    kst.load(rk, a.ld_qk, kt * TT, a.dqk, a.vec2);
+    vst.load(rv, a.ld_v, kt * TT, a.dv, a.vec2);
 #pragma unroll
     for (int kb = 0; kb < C::TB; ++kb)
       m[kb] = buf_ld_u32(rmap, map_voff, map_soff(q0, kt * TT + kb * 16, true));
   };
   load_tile(0, mw);
-  kst.store(Ks, LDK);
-  vst.store(Vs, LDV);
+  kst.store(Ks, LDK, a.vec2);
+  vst.store(Vs, LDV, a.vec2);
   __syncthreads();
 
   const int last_kt = min(q0 + 63, L - 1) / TT;
@@ -414,18 +484,34 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
           ds[r] = ok ? dpt[r] * silu_grad_(x) * a.inv_n : 0.f;
         }
         const float* kcol = Ks + (kb * 16 + 4 * lg) * LDK + lr;
+        if constexpr (C::KT > 8) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int t = 0; t < C::KT; ++t)
+              dQ[t] = mfma16x16x4(ds[r], kcol[r * LDK + t * 16], dQ[t]);
+        } else {
+        float bk[2][C::KT];
+#pragma unroll
+        for (int t = 0; t < C::KT; ++t) bk[0][t] = kcol[t * 16];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
+          if (r + 1 < 4) {
 #pragma unroll
-          for (int t = 0; t < C::KT; ++t)
-            dQ[t] = mfma16x16x4(ds[r], kcol[r * LDK + t * 16], dQ[t]);
+            for (int t = 0; t < C::KT; ++t) bk[(r + 1) & 1][t] = kcol[(r + 1) * LDK + t * 16];
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int t = 0; t < C::KT; ++t) dQ[t] = mfma16x16x4(ds[r], bk[r & 1][t], dQ[t]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
         }
       }
     }
     if (more) {
       lds_barrier();
-      kst.store(Ks, LDK);
-      vst.store(Vs, LDV);
+      kst.store(Ks, LDK, a.vec2);
+      vst.store(Vs, LDV, a.vec2);
 #pragma unroll
       for (int kb = 0; kb < C::TB; ++kb) mw[kb] = mwn[kb];
       lds_barrier();
@@ -511,6 +597,12 @@ static int launch_bwd(const AttnBwdArgs& a, float* dpos_w, float* dts_w, hipStre
 
 }  // namespace gr
 
+#ifdef GR_STAMP
+extern "C" __attribute__((visibility("default"))) int gr_stamp_read(unsigned long long* host, int n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(gr::gr_stamp_buf), sizeof(unsigned long long) * n) == hipSuccess ? 0 : 1;
+}
+#endif
+
 extern "C" size_t hstu_attn_bwd_workspace_size(int B, int N, int max_len, int H,
                                                int num_buckets) {
   if (B <= 0 || N <= 0 || H <= 0 || max_len <= 0) return 0;
@@ -551,7 +643,8 @@ extern "C" int hstu_attn_bwd(const float* q, const float* k, const float* v, int
   AttnBwdArgs a{q, k, v, ld_qk, ld_v, dout, ld_dout, offsets, B, N, H, dqk, dv,
                 ceil_div(max_len, 64), bucket_map, map_kq, pos_w, ts_w,
                 bucket_map ? num_buckets : 0, hq, hk, hv, ld_h, dq, dk, dvv, ld_d,
-                bucket_map ? (float*)workspace : nullptr, 1.0f / (float)N};
+                bucket_map ? (float*)workspace : nullptr, 1.0f / (float)N, 0};
+  a.vec2 = pair_aligned({q, k, v, dout}, {ld_qk, ld_v, ld_dout, dqk, dv});
   const int d = dqk > dv ? dqk : dv;
   if (d <= 8) return launch_bwd<2, 1>(a, dpos_w, dts_w, st);
   if (d <= 16) return launch_bwd<4, 1>(a, dpos_w, dts_w, st);

@@ -35,6 +35,7 @@ struct AttnFwdArgs {
   float* out;
   int64_t ld_out;
   float inv_n;
+  int vec2;  // 8-byte pair staging (aligned rows, even widths)
 };
 
 // TK = keys per LDS tile (64, or 16 for the wide head dims where a 64-key register
@@ -103,16 +104,16 @@ __global__ __launch_bounds__(256) void hstu_attn_fwd_kernel(AttnFwdArgs a) {
   BufTile<C::VP, TK> vst;
   uint32_t mw[C::KB], mwn[C::KB];
   auto load_tile = [&](int kt, uint32_t (&m)[C::KB]) {
-    kst.load(rk, a.ld_qk, kt * TK, a.dqk);
-    vst.load(rv, a.ld_v, kt * TK, a.dv);
+    kst.load(rk, a.ld_qk, kt * TK, a.dqk, a.vec2);
+    vst.load(rv, a.ld_v, kt * TK, a.dv, a.vec2);
 #pragma unroll
     for (int kb = 0; kb < C::KB; ++kb)
       m[kb] = buf_ld_u32(rmap, map_voff, map_soff(q0, kt * TK + kb * 16, true));
   };
 
   load_tile(0, mw);
-  kst.store(Ks, C::LDK);
-  vst.store(Vs, C::LDV);
+  kst.store(Ks, C::LDK, a.vec2);
+  vst.store(Vs, C::LDV, a.vec2);
   __syncthreads();  // also publishes tsw / posw
 
   const int wq_lo = q0 + w * 16;  // first query of this wave
@@ -153,8 +154,8 @@ __global__ __launch_bounds__(256) void hstu_attn_fwd_kernel(AttnFwdArgs a) {
     }
     if (more) {
       lds_barrier();
-      kst.store(Ks, C::LDK);
-      vst.store(Vs, C::LDV);
+      kst.store(Ks, C::LDK, a.vec2);
+      vst.store(Vs, C::LDV, a.vec2);
 #pragma unroll
       for (int kb = 0; kb < C::KB; ++kb) mw[kb] = mwn[kb];
       lds_barrier();
@@ -202,7 +203,8 @@ extern "C" int hstu_attn_fwd(const float* q, const float* k, const float* v, int
   if (B == 0 || max_len == 0) return 0;
   AttnFwdArgs a{q, k, v, ld_qk, ld_v, offsets, B, N, H, dqk, dv, ceil_div(max_len, 64),
                 bucket_map, pos_w, ts_w, bucket_map ? num_buckets : 0, out, ld_out,
-                1.0f / (float)N};
+                1.0f / (float)N, 0};
+  a.vec2 = pair_aligned({q, k, v}, {ld_qk, ld_v, dqk, dv});
   const int grid = a.n_qtiles * B * H;
   hipStream_t st = (hipStream_t)stream;
   const int d = dqk > dv ? dqk : dv;
