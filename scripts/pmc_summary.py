@@ -30,14 +30,14 @@ _MAP = [
     (r"attn_bwd_dkv_kernel", "attn_bwd_dkv"),
     (r"attn_bwd_dq_kernel", "attn_bwd_dq"),
     (r"bias_grad_reduce_kernel", "attn_bias_reduce"),
-    (r"OpLnUvqkBwd", "ln_uvqk_bwd"),
-    (r"OpLnUvqk", "ln_uvqk_fwd"),
-    (r"OpGateOBwd", "gate_o_bwd"),
-    (r"OpGateO", "gate_o_fwd"),
+    (r"(Op|Rw)LnUvqkBwd", "ln_uvqk_bwd"),
+    (r"(Op|Rw)LnUvqk", "ln_uvqk_fwd"),
+    (r"(Op|Rw)GateOBwd", "gate_o_bwd"),
+    (r"(Op|Rw)GateO", "gate_o_fwd"),
     (r"wgrad_partial_kernel", "wgrad_partial"),
     (r"wgrad_reduce_kernel", "wgrad_reduce"),
     (r"mips_pack_kernel", "mips_pack"),
-    (r"mips_select_kernel", "mips_select"),
+    (r"mips_select_kernel|mips_scoreall_kernel", "mips_select"),
     (r"mips_merge_kernel", "mips_merge"),
     (r"cumsum_kernel", "cumsum"),
     (r"dense_to_jagged_kernel", "dense_to_jagged"),
