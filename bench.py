@@ -190,8 +190,12 @@ def main():
     N = N0 + out_len
     enc = build_model(N0, out_len, D, blocks, device)
     reducer = FlatGradAllReducer(list(enc.parameters()))
-    opt = torch.optim.AdamW(enc.parameters(), lr=1e-3, betas=(0.9, 0.98), weight_decay=1e-3,
-                            capturable=True)
+    try:  # one fused multi-tensor kernel per step (same AdamW math), graph-capturable
+        opt = torch.optim.AdamW(enc.parameters(), lr=1e-3, betas=(0.9, 0.98), weight_decay=1e-3,
+                                fused=True, capturable=True)
+    except (RuntimeError, TypeError, ValueError):
+        opt = torch.optim.AdamW(enc.parameters(), lr=1e-3, betas=(0.9, 0.98), weight_decay=1e-3,
+                                capturable=True)
     lengths, x, ts, past_ids, dy = make_batch(B, N0, out_len, D, 1000 + rank, device)
     x.requires_grad_(True)
     # ml-1m catalog (ids 1..3953, L2-normalised rows as Retrieval.on_validation_epoch_start)
@@ -211,8 +215,8 @@ def main():
     def opt_and_retrieve(y):
         opt.step()
         with torch.no_grad():
-            q = get_current_embeddings(lengths, y.detach())
-            q = q / q.norm(dim=-1, keepdim=True).clamp_min(1e-6)
+            # L2NormEmbeddingPostprocessor + get_current_embeddings as one kernel
+            q = get_current_embeddings(lengths, y.detach(), normalize=True, eps=1e-6)
             ids, scores = index.get_top_k_outputs(q, invalid_ids=past_ids)
         return ids
 

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GR_HSTU_ABI_VERSION 2
+#define GR_HSTU_ABI_VERSION 3
 
 #ifndef GR_API
 #define GR_API __attribute__((visibility("default")))
@@ -64,6 +64,19 @@ GR_API int gr_dense_to_jagged(const float* dense, const int64_t* offsets, int B,
  * jagged (offsets[B], D) -> dense (B, N, D); rows >= length are zero. */
 GR_API int gr_jagged_to_padded(const float* jagged, const int64_t* offsets, int B, int N, int D,
                         float* dense, void* stream);
+
+/* Replaces postprocessors.py:47-56 (L2NormEmbeddingPostprocessor.forward) and
+ * negative_sampler.py:31-37: out[r] = x[r] / max(||x[r]||_2, eps), rows of width D. */
+GR_API int gr_l2_normalize(const float* x, int64_t ld_x, int64_t rows, int D, float eps, float* out,
+                           int64_t ld_out, void* stream);
+/* Autograd backward of gr_l2_normalize (recomputes ||x||). */
+GR_API int gr_l2_normalize_bwd(const float* x, int64_t ld_x, const float* dy, int64_t ld_dy,
+                               int64_t rows, int D, float eps, float* dx, int64_t ld_dx,
+                               void* stream);
+/* Replaces utils/ops.py:171-187 get_current_embeddings: out[b] = encoded[b, lengths[b]-1]
+ * of a (B, N, D) tensor, optionally L2-normalised (the retrieval query path). */
+GR_API int gr_current_embeddings(const float* encoded, const int64_t* lengths, int B, int N, int D,
+                                 int normalize, float eps, float* out, void* stream);
 
 /* ---------------------------------------------------------------- HSTU attention
  * hstu_bucket_map: the relative-time bucket of every causal (query i, key j) pair of

@@ -148,11 +148,15 @@ class SequentialTransductionUnitJagged(torch.nn.Module):
         return_cache_states: bool = False,
         max_len: Optional[int] = None,
         bucket_map: Optional[torch.Tensor] = None,
+        dropout_step: Optional[torch.Tensor] = None,
     ):
         """x: (rows, D) jagged; x_offsets (B+1,).  Returns (x', cache-state tuple);
         cache states are (v, None, None, x') — padded q/k are never built.
         ``bucket_map`` (optional) is the batch's ``ops.bucket_map`` — pass it to share
-        it across layers; otherwise it is built from ``all_timestamps``."""
+        it across layers; otherwise it is built from ``all_timestamps``.
+        ``dropout_step`` (optional) is an already-advanced device step counter shared by
+        the layers of one encoder forward (one increment per forward instead of one per
+        layer); by default the layer advances its own."""
         if delta_x_offsets is not None or cache is not None:
             raise NotImplementedError("incremental (cached) HSTU decoding is not supported")
         n = invalid_attn_mask.size(-1)
@@ -168,8 +172,11 @@ class SequentialTransductionUnitJagged(torch.nn.Module):
             raise ValueError(f"_pos_w has {pos_w.numel()} entries, expected {2 * n - 1}")
         step = None
         if geo.dropout_p > 0:
-            self._dropout_step.add_(1)
-            step = self._dropout_step
+            if dropout_step is not None:
+                step = dropout_step
+            else:
+                self._dropout_step.add_(1)
+                step = self._dropout_step
         y = ops.stu_layer(x, x_offsets, bmap, self._uvqk, self._o.weight, self._o.bias, pos_w,
                           ts_w, geo, self._dropout_seed, step)
         return y, (None, None, None, y)
@@ -183,6 +190,9 @@ class HSTUJagged(torch.nn.Module):
         super().__init__()
         self._attention_layers = torch.nn.ModuleList(modules=modules)
         self._autocast_dtype = autocast_dtype
+        # one device dropout counter per encoder forward (layers hash with their own seed)
+        self.register_buffer("_dropout_step", torch.zeros(1, dtype=torch.int64),
+                             persistent=False)
 
     def jagged_forward(self, x, x_offsets, all_timestamps, invalid_attn_mask,
                        delta_x_offsets=None, cache=None, return_cache_states=False,
@@ -194,12 +204,16 @@ class HSTUJagged(torch.nn.Module):
         if all_timestamps is not None and any(
                 layer._rel_attn_bias is not None for layer in self._attention_layers):
             bmap = ops.bucket_map(all_timestamps, x_offsets, n)
+        step = None
+        if self.training and any(layer._dropout_ratio > 0 for layer in self._attention_layers):
+            self._dropout_step.add_(1)
+            step = self._dropout_step
         for layer in self._attention_layers:
             x, cs = layer(x=x, x_offsets=x_offsets, all_timestamps=all_timestamps,
                           invalid_attn_mask=invalid_attn_mask,
                           delta_x_offsets=delta_x_offsets, cache=None,
                           return_cache_states=return_cache_states, max_len=max_len,
-                          bucket_map=bmap)
+                          bucket_map=bmap, dropout_step=step)
             if return_cache_states:
                 cache_states.append(cs)
         return x, cache_states

@@ -149,12 +149,56 @@ def jagged_to_padded_dense(values: torch.Tensor, offsets: torch.Tensor, max_leng
     return out.squeeze(-1) if squeeze else out
 
 
-def get_current_embeddings(lengths: torch.Tensor, encoded_embeddings: torch.Tensor) -> torch.Tensor:
-    """(B, N, D) -> (B, D) with row lengths[b]-1 (utils/ops.py:171-187).  Pure index
-    arithmetic on the device (one gather)."""
+def get_current_embeddings(lengths: torch.Tensor, encoded_embeddings: torch.Tensor,
+                           normalize: bool = False, eps: float = 1e-6) -> torch.Tensor:
+    """(B, N, D) -> (B, D) with row lengths[b]-1 (utils/ops.py:171-187), optionally
+    L2-normalised (the retrieval query, postprocessors.py:47-56).  One kernel
+    (``gr_current_embeddings``); under autograd it is an index_select (+ l2_normalize)."""
     B, N, D = encoded_embeddings.shape
-    idx = (lengths.to(torch.int64) - 1) + torch.arange(B, device=lengths.device) * N
-    return encoded_embeddings.reshape(-1, D).index_select(0, idx)
+    if encoded_embeddings.requires_grad and torch.is_grad_enabled():
+        idx = (lengths.to(torch.int64) - 1) + torch.arange(B, device=lengths.device) * N
+        out = encoded_embeddings.reshape(-1, D).index_select(0, idx)
+        return l2_normalize(out, eps) if normalize else out
+    _lib.require_gpu(lengths, encoded_embeddings)
+    enc = encoded_embeddings.contiguous()
+    lens = lengths.to(torch.int64).contiguous()
+    out = torch.empty(B, D, dtype=enc.dtype, device=enc.device)
+    _lib.call("gr_current_embeddings", enc.data_ptr(), lens.data_ptr(), B, N, D,
+              1 if normalize else 0, eps, out.data_ptr(), _stream())
+    return out
+
+
+class _L2Normalize(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, eps):
+        shape = x.shape
+        D = shape[-1]
+        x2 = x.reshape(-1, D).contiguous()
+        y = torch.empty_like(x2)
+        _lib.call("gr_l2_normalize", x2.data_ptr(), D, x2.shape[0], D, eps, y.data_ptr(), D,
+                  _stream())
+        ctx.save_for_backward(x2)
+        ctx.eps = eps
+        ctx.shape = shape
+        return y.reshape(shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x2,) = ctx.saved_tensors
+        D = x2.shape[1]
+        g = dy.reshape(-1, D).contiguous()
+        dx = torch.empty_like(x2)
+        _lib.call("gr_l2_normalize_bwd", x2.data_ptr(), D, g.data_ptr(), D, x2.shape[0], D,
+                  ctx.eps, dx.data_ptr(), D, _stream())
+        return dx.reshape(ctx.shape), None
+
+
+def l2_normalize(x: torch.Tensor, eps: float = 1e-6) -> torch.Tensor:
+    """x / clamp(||x||_2, eps) over the last dim (postprocessors.py:47-56), fwd + bwd."""
+    _lib.require_gpu(x)
+    if x.dtype != torch.float32:
+        raise TypeError("l2_normalize: float32 only")
+    return _L2Normalize.apply(x, float(eps))
 
 
 # ------------------------------------------------------------------ relative-time buckets
