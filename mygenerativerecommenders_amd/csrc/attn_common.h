@@ -106,6 +106,15 @@ struct BufTile {
   }
 };
 
+// Work rank of workgroup `id` (rank 0 = heaviest).  Workgroups id and id + C (C = number
+// of CUs) land on the same CU when the grid is resident in a few rounds, so odd rounds
+// are reversed ("snake"): each CU pairs a heavy tile with a light one instead of two
+// heavy or two light ones (C2: 6 vs 4 tile-units per CU becomes 5 and 5).
+__device__ __forceinline__ int snake_rank(int id, int C) {
+  const int r = id / C, p = id - r * C;
+  return r * C + ((r & 1) ? C - 1 - p : p);
+}
+
 // Host: true when every pointer is 8-byte aligned and every stride / width is even.
 inline int pair_aligned(std::initializer_list<const void*> ptrs, std::initializer_list<int64_t> vals) {
   for (const void* p : ptrs)

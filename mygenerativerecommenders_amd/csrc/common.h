@@ -130,6 +130,20 @@ __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane
 
 __host__ __device__ inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
 
+// CU count of the current device (cached; 256 on MI355X).
+inline int device_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+      n = v;
+    else
+      n = 256;
+  }
+  return n;
+}
+
 // relative-time bucket: max{b : thr[b] <= |dt|}, thr = integer threshold table of the
 // reference bucket fn (hstu.py:579-581, clamped at hstu.py:117-123).
 __device__ __forceinline__ int time_bucket(int64_t dt, const int64_t* thr_lds, int nb) {

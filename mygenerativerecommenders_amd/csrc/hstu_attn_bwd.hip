@@ -68,6 +68,7 @@ struct AttnBwdArgs {
   float* slabs;  // [grid][2N-1 + nb+1]
   float inv_n;
   int vec2;  // 8-byte pair staging (aligned rows, even widths)
+  int cus;   // CU count (snake_rank)
 };
 
 // TT = rows per streamed LDS tile (queries in dK/dV, keys in dQ): 64, or 16 for the
@@ -123,8 +124,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
 
   const int BH = a.B * a.H;
   const int id = blockIdx.x;
-  const int kt = id / BH;  // kt = 0 (the most query tiles) first
-  const int bh = id % BH;
+  const int rank = snake_rank(id, a.cus);
+  const int kt = rank / BH;  // kt = 0 (the most query tiles) first
+  const int bh = rank % BH;
   const int b = bh / a.H, h = bh % a.H;
   const int64_t s0 = a.offsets[b];
   const int L = (int)(a.offsets[b + 1] - s0);
@@ -396,8 +398,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
 
   const int BH = a.B * a.H;
   const int id = blockIdx.x;
-  const int qt = a.n_tiles - 1 - id / BH;
-  const int bh = id % BH;
+  const int rank = snake_rank(id, a.cus);
+  const int qt = a.n_tiles - 1 - rank / BH;
+  const int bh = rank % BH;
   const int b = bh / a.H, h = bh % a.H;
   const int64_t s0 = a.offsets[b];
   const int L = (int)(a.offsets[b + 1] - s0);
@@ -644,6 +647,9 @@ extern "C" int hstu_attn_bwd(const float* q, const float* k, const float* v, int
                 ceil_div(max_len, 64), bucket_map, map_kq, pos_w, ts_w,
                 bucket_map ? num_buckets : 0, hq, hk, hv, ld_h, dq, dk, dvv, ld_d,
                 bucket_map ? (float*)workspace : nullptr, 1.0f / (float)N, 0};
+  // snake pairing only when the grid is resident in <= 2 rounds; otherwise plain
+  // heaviest-first (dynamic dispatch = longest-processing-time order)
+  a.cus = (int64_t)a.n_tiles * B * H <= 2 * device_cus() ? device_cus() : (1 << 30);
   a.vec2 = pair_aligned({q, k, v, dout}, {ld_qk, ld_v, ld_dout, dqk, dv});
   const int d = dqk > dv ? dqk : dv;
   if (d <= 8) return launch_bwd<2, 1>(a, dpos_w, dts_w, st);

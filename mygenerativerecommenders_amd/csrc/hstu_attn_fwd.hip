@@ -36,6 +36,7 @@ struct AttnFwdArgs {
   int64_t ld_out;
   float inv_n;
   int vec2;  // 8-byte pair staging (aligned rows, even widths)
+  int cus;   // CU count (snake_rank)
 };
 
 // TK = keys per LDS tile (64, or 16 for the wide head dims where a 64-key register
@@ -61,8 +62,9 @@ __global__ __launch_bounds__(256) void hstu_attn_fwd_kernel(AttnFwdArgs a) {
 
   const int BH = a.B * a.H;
   const int id = blockIdx.x;
-  const int qt = a.n_qtiles - 1 - id / BH;  // heaviest tiles first
-  const int bh = id % BH;
+  const int rank = snake_rank(id, a.cus);
+  const int qt = a.n_qtiles - 1 - rank / BH;  // heaviest tiles first
+  const int bh = rank % BH;
   const int b = bh / a.H, h = bh % a.H;
   const int64_t s0 = a.offsets[b];
   const int L = (int)(a.offsets[b + 1] - s0);
@@ -204,6 +206,9 @@ extern "C" int hstu_attn_fwd(const float* q, const float* k, const float* v, int
   AttnFwdArgs a{q, k, v, ld_qk, ld_v, offsets, B, N, H, dqk, dv, ceil_div(max_len, 64),
                 bucket_map, pos_w, ts_w, bucket_map ? num_buckets : 0, out, ld_out,
                 1.0f / (float)N, 0};
+  // snake pairing only when the grid is resident in <= 2 rounds; otherwise plain
+  // heaviest-first (dynamic dispatch = longest-processing-time order)
+  a.cus = (int64_t)a.n_qtiles * B * H <= 2 * device_cus() ? device_cus() : (1 << 30);
   a.vec2 = pair_aligned({q, k, v}, {ld_qk, ld_v, dqk, dv});
   const int grid = a.n_qtiles * B * H;
   hipStream_t st = (hipStream_t)stream;
