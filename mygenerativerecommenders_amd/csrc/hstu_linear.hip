@@ -18,6 +18,7 @@
 // A operand layout (row stride 18 == 18 mod 32) and B layout (stride == 16 mod 32) make
 // the per-k-step ds_read_b32 of both operands bank-conflict-free.
 #include "common.h"
+#include "attn_common.h"
 #include "rowwave.h"
 
 #include "../../include/gr_hstu.h"
@@ -87,12 +88,22 @@ __device__ __forceinline__ void panel_row_stats(const float* base, int64_t ld, i
   }
 }
 
-// Generic row-panel GEMM: C[m, n] = sum_k Op::a(m, k) * Op::b(k, n), epilogue by Op.
+// Generic row-panel GEMM: C[m, n] = sum_k A'(m, k) * W'(k, n), epilogue by Op.
 // K streams through LDS in chunks of 16 with the next chunk prefetched into registers
-// (LDS-only barriers keep the prefetch in flight across the MFMA phase).
+// (LDS-only barriers keep the prefetch in flight across the MFMA phase).  All operand
+// loads go through buffer descriptors: A rows from m0 (rows past the end read 0), one
+// voffset VGPR per thread with the row / k steps in SGPR soffsets; the raw values are
+// transformed (LayerNorm, gating, dropout) when they are written to LDS.
+//   Op: a_rsrc0/1(m0, total), a_ld0/1(), NSRC, a_xform(v0, v1, m, k, stats, valid),
+//       w, bks(), bns()  (W'(k, n) = w[k * bks + n * bns]), prologue, epilogue.
 template <int NT, class Op>
 __global__ __launch_bounds__(256) void rowpanel_kernel(Op op) {
   using P = PanelCfg<NT>;
+  constexpr int NP2 = P::BN <= 16 ? 16 : P::BN <= 32 ? 32 : P::BN <= 64 ? 64 : P::BN <= 128 ? 128 : 256;
+  // B staging walks the memory-contiguous index fastest: n for row-major W' (RPB k-rows
+  // per pass), k for transposed W' (16 k per column, 16 columns per pass)
+  constexpr int RPB = 256 / NP2;
+  constexpr int NB = Op::B_N_CONTIG ? BK / RPB : NT;
   __shared__ __attribute__((aligned(16))) float As[BM * LDA];
   __shared__ __attribute__((aligned(16))) float Bs[BK * P::LDB];
   __shared__ float2 stats[BM];
@@ -100,59 +111,63 @@ __global__ __launch_bounds__(256) void rowpanel_kernel(Op op) {
   const int64_t m0 = (int64_t)blockIdx.x * BM;
   if (m0 >= total) return;
   const int n0 = blockIdx.y * P::BN;
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int tid = threadIdx.x, w = wave_id(), lane = tid & 63;
   const int lr = lane & 15, lg = lane >> 4;
-  const int64_t mlast = total - 1;
 
   op.prologue(m0, total, stats);
   __syncthreads();
 
-  float ra[4], rb[NT];
+  const __amdgpu_buffer_rsrc_t ra0 = op.a_rsrc0(m0, total);
+  const __amdgpu_buffer_rsrc_t ra1 = op.a_rsrc1(m0, total);
+  const int ld0 = (int)op.a_ld0(), ld1 = (int)op.a_ld1();
+  const int a_c = tid & 15, a_r = tid >> 4;  // A: column k0 + a_c of rows a_r + 16 i
+  const int va0 = (a_r * ld0 + a_c) * 4, va1 = (a_r * ld1 + a_c) * 4;
+  const __amdgpu_buffer_rsrc_t rw =
+      __builtin_amdgcn_make_buffer_rsrc((void*)op.w, 0, op.K * op.N * 4, 0x00020000);
+  const int bks = op.bks(), bns = op.bns();
+  const int b_c = Op::B_N_CONTIG ? tid % NP2 : tid >> 4;  // B: column n0 + b_c (+16 i)
+  const int b_r = Op::B_N_CONTIG ? tid / NP2 : tid & 15;   // of k-row b_r (+RPB i)
+  const bool b_col = Op::B_N_CONTIG ? (b_c < P::BN && n0 + b_c < op.N) : true;
+  const int vb = b_col ? (b_r * bks + (n0 + b_c) * bns) * 4 : 0x40000000;
+
+  float ra[4], ra2[Op::NSRC == 2 ? 4 : 1], rb[NB];
   auto load = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int e = tid + 256 * i;
-      const int r = e >> 4, c = e & 15;
-      const int64_t m = m0 + r;
-      const int k = k0 + c;
-      const bool ok = m < total && k < op.K;
-      const float v = op.a(m < mlast ? m : mlast, k < op.K ? k : op.K - 1, stats[r], ok);
-      ra[i] = ok ? v : 0.f;
+      ra[i] = buf_ld(ra0, va0 + k0 * 4, i * 16 * ld0 * 4);
+      if constexpr (Op::NSRC == 2) ra2[i] = buf_ld(ra1, va1 + k0 * 4, i * 16 * ld1 * 4);
     }
 #pragma unroll
-    for (int i = 0; i < NT; ++i) {
-      const int e = tid + 256 * i;
-      int kk, c;
-      if (Op::B_N_CONTIG) {
-        kk = e / P::BN;
-        c = e - kk * P::BN;
-      } else {
-        c = e >> 4;
-        kk = e & 15;
-      }
-      const int k = k0 + kk, n = n0 + c;
-      const float v = op.b(k < op.K ? k : op.K - 1, n < op.N ? n : op.N - 1);
-      rb[i] = (k < op.K && n < op.N) ? v : 0.f;
+    for (int i = 0; i < NB; ++i) {
+      if constexpr (Op::B_N_CONTIG)
+        rb[i] = buf_ld(rw, vb, (k0 + RPB * i) * bks * 4);
+      else
+        rb[i] = buf_ld(rw, vb, (k0 * bks + 16 * i * bns) * 4);
     }
   };
-  auto store = [&]() {
+  auto store = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int e = tid + 256 * i;
-      As[(e >> 4) * LDA + (e & 15)] = ra[i];
+      const int r = a_r + 16 * i, k = k0 + a_c;
+      const bool ok = m0 + r < total && k < op.K;
+      const float v = op.a_xform(ra[i], Op::NSRC == 2 ? ra2[Op::NSRC == 2 ? i : 0] : 0.f, m0 + r, k,
+                                 stats[r], ok);
+      As[r * LDA + a_c] = ok ? v : 0.f;
     }
+    if constexpr (Op::B_N_CONTIG) {
+      if (b_c < P::BN) {
 #pragma unroll
-    for (int i = 0; i < NT; ++i) {
-      const int e = tid + 256 * i;
-      int kk, c;
-      if (Op::B_N_CONTIG) {
-        kk = e / P::BN;
-        c = e - kk * P::BN;
-      } else {
-        c = e >> 4;
-        kk = e & 15;
+        for (int i = 0; i < NB; ++i) {
+          const int kk = b_r + RPB * i;
+          Bs[kk * P::LDB + b_c] = (b_col && k0 + kk < op.K) ? rb[i] : 0.f;
+        }
       }
-      Bs[kk * P::LDB + c] = rb[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const int c = b_c + 16 * i;
+        Bs[b_r * P::LDB + c] = (n0 + c < op.N && k0 + b_r < op.K) ? rb[i] : 0.f;
+      }
     }
   };
 
@@ -161,27 +176,46 @@ __global__ __launch_bounds__(256) void rowpanel_kernel(Op op) {
   for (int t = 0; t < NT; ++t) acc[t] = f4_zero();
 
   load(0);
-  store();
+  store(0);
   lds_barrier();
   for (int k0 = 0; k0 < op.K; k0 += BK) {
     const bool more = k0 + BK < op.K;
     if (more) load(k0 + BK);
     const float* arow = As + (w * 16 + lr) * LDA + lg;
+    // operands of k-step ks+1 read from LDS while the MFMAs of step ks run
+    float av[2], bv[2][NT];
+    av[0] = arow[0];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) bv[0][t] = Bs[lg * P::LDB + lr + t * 16];
 #pragma unroll
     for (int ks = 0; ks < BK / 4; ++ks) {
-      const float av = arow[4 * ks];
-      const float* brow = Bs + (4 * ks + lg) * P::LDB + lr;
+      if (ks + 1 < BK / 4) {
+        av[(ks + 1) & 1] = arow[4 * (ks + 1)];
+        const float* brow = Bs + (4 * (ks + 1) + lg) * P::LDB + lr;
 #pragma unroll
-      for (int t = 0; t < NT; ++t) acc[t] = mfma16x16x4(av, brow[t * 16], acc[t]);
+        for (int t = 0; t < NT; ++t) bv[(ks + 1) & 1][t] = brow[t * 16];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = mfma16x16x4(av[ks & 1], bv[ks & 1][t], acc[t]);
+      __builtin_amdgcn_sched_barrier(0);
     }
     lds_barrier();
     if (more) {
-      store();
+      store(k0 + BK);
       lds_barrier();
     }
   }
   // acc[t][r] = C[m0 + 16w + 4lg + r][n0 + 16t + lr]
   op.epilogue(acc, m0 + w * 16 + 4 * lg, n0 + lr, total);
+}
+
+// descriptor over rows [m0, total) of a (rows, ld) matrix (column offset folded in base)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const float* base, int64_t ld,
+                                                           int64_t m0, int64_t total) {
+  int64_t bytes = (total - m0) * ld * 4;
+  if (bytes > 0x7fffffff) bytes = 0x7fffffff;
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(base + m0 * ld), 0, (int)bytes, 0x00020000);
 }
 
 // ------------------------------------------------------------------ ops
@@ -212,10 +246,16 @@ struct OpLnUvqk {
   __device__ void prologue(int64_t m0, int64_t total, float2* st) const {
     panel_row_stats(x, ldx, m0, total, K, eps, st, blockIdx.y == 0 ? x_stats : nullptr);
   }
-  __device__ float a(int64_t m, int k, float2 st, bool) const {
-    return (as_global(x)[m * ldx + k] - st.x) * st.y;
+  static constexpr int NSRC = 1;
+  __device__ __amdgpu_buffer_rsrc_t a_rsrc0(int64_t m0, int64_t t) const { return rows_rsrc(x, ldx, m0, t); }
+  __device__ __amdgpu_buffer_rsrc_t a_rsrc1(int64_t m0, int64_t t) const { return rows_rsrc(x, ldx, m0, t); }
+  __device__ int64_t a_ld0() const { return ldx; }
+  __device__ int64_t a_ld1() const { return ldx; }
+  __device__ float a_xform(float v, float, int64_t, int, float2 st, bool) const {
+    return (v - st.x) * st.y;
   }
-  __device__ float b(int k, int n) const { return as_global(w)[(int64_t)k * N + n]; }
+  __device__ int bks() const { return N; }
+  __device__ int bns() const { return 1; }
   template <int NT>
   __device__ void epilogue(f4 (&acc)[NT], int64_t mrow, int ncol, int64_t total) const {
 #pragma unroll
@@ -264,13 +304,19 @@ struct OpGateO {
   __device__ void prologue(int64_t m0, int64_t total, float2* st) const {
     panel_row_stats(attn, lda, m0, total, K, eps, st, blockIdx.y == 0 ? a_stats : nullptr);
   }
-  __device__ float a(int64_t m, int k, float2 st, bool valid) const {
-    float v = as_global(u)[m * ldu + k] * ((as_global(attn)[m * lda + k] - st.x) * st.y);
+  static constexpr int NSRC = 2;
+  __device__ __amdgpu_buffer_rsrc_t a_rsrc0(int64_t m0, int64_t t) const { return rows_rsrc(u, ldu, m0, t); }
+  __device__ __amdgpu_buffer_rsrc_t a_rsrc1(int64_t m0, int64_t t) const { return rows_rsrc(attn, lda, m0, t); }
+  __device__ int64_t a_ld0() const { return ldu; }
+  __device__ int64_t a_ld1() const { return lda; }
+  __device__ float a_xform(float uv, float av, int64_t m, int k, float2 st, bool valid) const {
+    float v = uv * ((av - st.x) * st.y);
     if (p > 0.f) v *= dropout_keep(seed + (seed_off ? (uint64_t)*seed_off : 0ull), m, k, K, p);
     if (valid && o_in && blockIdx.y == 0) o_in[m * K + k] = v;
     return v;
   }
-  __device__ float b(int k, int n) const { return as_global(w)[(int64_t)n * K + k]; }
+  __device__ int bks() const { return 1; }
+  __device__ int bns() const { return K; }
   template <int NT>
   __device__ void epilogue(f4 (&acc)[NT], int64_t mrow, int ncol, int64_t total) const {
     float bv[NT];
@@ -322,8 +368,14 @@ struct OpGateOBwd : NoStats {
   int64_t lddu;
   float* da;
   int64_t ldda;
-  __device__ float a(int64_t m, int k, float2, bool) const { return as_global(dy)[m * lddy + k]; }
-  __device__ float b(int k, int n) const { return as_global(w)[(int64_t)k * N + n]; }
+  static constexpr int NSRC = 1;
+  __device__ __amdgpu_buffer_rsrc_t a_rsrc0(int64_t m0, int64_t t) const { return rows_rsrc(dy, lddy, m0, t); }
+  __device__ __amdgpu_buffer_rsrc_t a_rsrc1(int64_t m0, int64_t t) const { return rows_rsrc(dy, lddy, m0, t); }
+  __device__ int64_t a_ld0() const { return lddy; }
+  __device__ int64_t a_ld1() const { return lddy; }
+  __device__ float a_xform(float v, float, int64_t, int, float2, bool) const { return v; }
+  __device__ int bks() const { return N; }
+  __device__ int bns() const { return 1; }
   template <int NT>
   __device__ void epilogue(f4 (&acc)[NT], int64_t mrow, int ncol, int64_t total) const {
 #pragma unroll
@@ -386,8 +438,14 @@ struct OpLnUvqkBwd : NoStats {
   int64_t lddy;
   float* dx;
   int64_t lddx;
-  __device__ float a(int64_t m, int k, float2, bool) const { return as_global(dh)[m * lddh + k]; }
-  __device__ float b(int k, int n) const { return as_global(w)[(int64_t)n * K + k]; }
+  static constexpr int NSRC = 1;
+  __device__ __amdgpu_buffer_rsrc_t a_rsrc0(int64_t m0, int64_t t) const { return rows_rsrc(dh, lddh, m0, t); }
+  __device__ __amdgpu_buffer_rsrc_t a_rsrc1(int64_t m0, int64_t t) const { return rows_rsrc(dh, lddh, m0, t); }
+  __device__ int64_t a_ld0() const { return lddh; }
+  __device__ int64_t a_ld1() const { return lddh; }
+  __device__ float a_xform(float v, float, int64_t, int, float2, bool) const { return v; }
+  __device__ int bks() const { return 1; }
+  __device__ int bns() const { return K; }
   template <int NT>
   __device__ void epilogue(f4 (&acc)[NT], int64_t mrow, int ncol, int64_t total) const {
 #pragma unroll
