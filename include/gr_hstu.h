@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GR_HSTU_ABI_VERSION 3
+#define GR_HSTU_ABI_VERSION 4
 
 #ifndef GR_API
 #define GR_API __attribute__((visibility("default")))
@@ -43,7 +43,8 @@ GR_API int gr_version(void);
  * count.  Kernel names: bucket_map, attn_fwd, attn_bwd_dkv, attn_bwd_dq,
  * attn_bias_reduce, ln_uvqk_fwd, gate_o_fwd, gate_o_bwd, ln_uvqk_bwd, wgrad_partial,
  * wgrad_reduce, mips_pack, mips_select, mips_merge, cumsum, dense_to_jagged,
- * jagged_to_padded.  Not for use inside a captured graph.
+ * jagged_to_padded, l2_normalize, current_embeddings, sampled_softmax_fwd,
+ * sampled_softmax_bwd, sampled_softmax_csr, sampled_softmax_table_grad.  Not for use inside a captured graph.
  */
 GR_API int gr_timing_enable(int on);
 GR_API int gr_timing_query(const char* kernel, double* total_ms, int* launches);
@@ -77,6 +78,36 @@ GR_API int gr_l2_normalize_bwd(const float* x, int64_t ld_x, const float* dy, in
  * of a (B, N, D) tensor, optionally L2-normalised (the retrieval query path). */
 GR_API int gr_current_embeddings(const float* encoded, const int64_t* lengths, int B, int N, int D,
                                  int normalize, float eps, float* out, void* stream);
+
+/* ---------------------------------------------------------------- sampled-softmax loss
+ * Fused LocalNegativesSampler.forward (negative_sampler.py:105-131, after its randint) +
+ * DotProductSimilarity.forward (dot_product.py:31-64) + SampledSoftmaxLoss.jagged_forward
+ * (autoregressive_losses.py:259-306), per jagged token t of M, R sampled negatives:
+ *   pos_logit = <out[t], pos[t]> / T
+ *   neg_r     = id(off[t,r]) == sup_ids[t] ? -5e4 : <out[t], table[off[t,r]]> / T
+ *   loss[t]   = logsumexp(pos_logit, neg_0..neg_{R-1}) - pos_logit,  lse[t] saved.
+ * `pos` is the (normalised) positive embedding, `table` the (normalised) embedding of
+ * every catalog row, indexed by the sampled offset (0 <= off < V; clamped);
+ * id(off) = all_ids[off], or off when all_ids is NULL.  D <= 256.  The weighted mean
+ * (autoregressive_losses.py:306) is left to the caller. */
+GR_API int gr_sampled_softmax_fwd(const float* out, int64_t ld_out, const float* pos, int64_t ld_pos,
+                                  const int64_t* sup_ids, const float* table, int64_t ld_table,
+                                  int64_t V, const int64_t* all_ids, const int64_t* offsets,
+                                  int64_t M, int R, int D, float temperature, float* loss,
+                                  float* lse, void* stream);
+/* Backward of gr_sampled_softmax_fwd given dloss[t] (the per-token upstream gradient):
+ * writes d_out and d_pos (M x D) and d_table (V x D, every row; rows never sampled get 0).
+ * The table gradient is accumulated per catalog row after a counting sort of the
+ * offsets; its summation order within a row is not fixed (integer atomics).  M*R and V must fit int32; tables
+ * and row arrays must be < 2 GiB.  workspace: gr_sampled_softmax_workspace_size bytes. */
+GR_API size_t gr_sampled_softmax_workspace_size(int64_t M, int R, int64_t V, int D);
+GR_API int gr_sampled_softmax_bwd(const float* out, int64_t ld_out, const float* pos, int64_t ld_pos,
+                                  const int64_t* sup_ids, const float* table, int64_t ld_table,
+                                  int64_t V, const int64_t* all_ids, const int64_t* offsets,
+                                  int64_t M, int R, int D, float temperature, const float* lse,
+                                  const float* dloss, float* d_out, int64_t ld_dout, float* d_pos,
+                                  int64_t ld_dpos, float* d_table, int64_t ld_dtable,
+                                  void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------- HSTU attention
  * hstu_bucket_map: the relative-time bucket of every causal (query i, key j) pair of

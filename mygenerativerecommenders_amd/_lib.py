@@ -97,7 +97,9 @@ def call(name: str, *args):
 KERNEL_NAMES = ("bucket_map", "attn_fwd", "attn_bwd_dkv", "attn_bwd_dq", "attn_bias_reduce",
                 "ln_uvqk_fwd", "gate_o_fwd", "gate_o_bwd", "ln_uvqk_bwd", "wgrad_partial",
                 "wgrad_reduce", "mips_pack", "mips_select", "mips_merge", "cumsum",
-                "dense_to_jagged", "jagged_to_padded", "l2_normalize", "current_embeddings")
+                "dense_to_jagged", "jagged_to_padded", "l2_normalize", "current_embeddings",
+                "sampled_softmax_fwd", "sampled_softmax_bwd", "sampled_softmax_csr",
+                "sampled_softmax_table_grad")
 
 
 def timing_enable(on: bool = True):

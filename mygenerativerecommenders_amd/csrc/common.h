@@ -94,10 +94,19 @@ __device__ __forceinline__ float wave_sum(float v) {
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
-// reduce across the 16 lanes that share (lane >> 4)
+// DPP lane move within a 16-lane row (no LDS crossbar traffic, unlike __shfl*).
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+// reduce across the 16 lanes that share (lane >> 4): quad xor 1, quad xor 2, then the
+// half-row and row mirrors (every lane of a quad / half-row already holds the same
+// partial, so the mirrors equal xor 4 / xor 8 — the same sums as the xor butterfly).
 __device__ __forceinline__ float sum16(float v) {
-#pragma unroll
-  for (int o = 8; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_mov<0x141>(v);  // row_half_mirror
+  v += dpp_mov<0x140>(v);  // row_mirror
   return v;
 }
 

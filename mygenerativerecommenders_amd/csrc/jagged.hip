@@ -118,8 +118,9 @@ extern "C" {
 
 int gr_l2_normalize(const float* x, int64_t ld_x, int64_t rows, int D, float eps, float* out,
                     int64_t ld_out, void* stream) {
-  GR_REQUIRE(x && out && rows >= 0 && D > 0, "gr_l2_normalize: bad args");
+  GR_REQUIRE(rows >= 0 && D > 0, "gr_l2_normalize: bad args");
   if (rows == 0) return 0;
+  GR_REQUIRE(x && out, "gr_l2_normalize: null pointer");
   GR_TIMED("l2_normalize", (hipStream_t)stream,
            hipLaunchKernelGGL(gr::l2norm_kernel, dim3((unsigned)((rows + 15) / 16)), dim3(256), 0,
                               (hipStream_t)stream, x, ld_x, rows, D, eps, nullptr, 0, 1, out, ld_out));
@@ -129,8 +130,9 @@ int gr_l2_normalize(const float* x, int64_t ld_x, int64_t rows, int D, float eps
 
 int gr_l2_normalize_bwd(const float* x, int64_t ld_x, const float* dy, int64_t ld_dy, int64_t rows,
                         int D, float eps, float* dx, int64_t ld_dx, void* stream) {
-  GR_REQUIRE(x && dy && dx && rows >= 0 && D > 0, "gr_l2_normalize_bwd: bad args");
+  GR_REQUIRE(rows >= 0 && D > 0, "gr_l2_normalize_bwd: bad args");
   if (rows == 0) return 0;
+  GR_REQUIRE(x && dy && dx, "gr_l2_normalize_bwd: null pointer");
   GR_TIMED("l2_normalize", (hipStream_t)stream,
            hipLaunchKernelGGL(gr::l2norm_bwd_kernel, dim3((unsigned)((rows + 15) / 16)), dim3(256), 0,
                               (hipStream_t)stream, x, ld_x, dy, ld_dy, rows, D, eps, dx, ld_dx));

@@ -9,6 +9,8 @@ Reference map (``src/generative_recommenders_pl/models/``):
   * dense_to_jagged .............. utils/ops.py:41-64
   * jagged_to_padded_dense ....... utils/ops.py:67-114
   * get_current_embeddings ....... utils/ops.py:171-187
+  * sampled_softmax_loss ......... losses/autoregressive_losses.py:259-306 (+ the
+                                   negatives gather of negative_sampler.py:105-131)
   * STU layer fwd/bwd ............ sequential_encoders/hstu.py:266-413 (+ autograd)
 """
 from __future__ import annotations
@@ -388,3 +390,74 @@ def stu_layer(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGeometry,
         raise TypeError("stu_layer: float32 only (the reference runs fp32, hstu.py:592)")
     return STULayerFunction.apply(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo, int(seed),
                                   seed_offset)
+
+
+# ------------------------------------------------------------------ sampled-softmax loss
+
+class _SampledSoftmax(torch.autograd.Function):
+    """Per-token sampled-softmax loss (``gr_sampled_softmax_fwd`` / ``_bwd``).
+
+    Differentiable inputs: ``out`` (M, D) query rows, ``pos`` (M, D) normalised positive
+    rows, ``table`` (V, D) normalised catalog rows.  ``offsets`` (M, R) index ``table``;
+    ``all_ids`` (V,) maps an offset to its item id for the collision mask."""
+
+    @staticmethod
+    def forward(ctx, out, pos, table, sup_ids, offsets, all_ids, temperature):
+        M, D = out.shape
+        V = table.shape[0]
+        R = offsets.shape[1] if offsets.dim() == 2 else 0
+        out_c, pos_c, table_c = out.contiguous(), pos.contiguous(), table.contiguous()
+        sup = sup_ids.to(torch.int64).contiguous()
+        offs = offsets.to(torch.int64).contiguous()
+        ids = all_ids.to(torch.int64).contiguous() if all_ids is not None else None
+        loss = torch.empty(M, dtype=torch.float32, device=out.device)
+        lse = torch.empty(M, dtype=torch.float32, device=out.device)
+        _lib.call("gr_sampled_softmax_fwd", out_c.data_ptr(), D, pos_c.data_ptr(), D,
+                  sup.data_ptr(), table_c.data_ptr(), D, V,
+                  ids.data_ptr() if ids is not None else None, offs.data_ptr(), M, R, D,
+                  float(temperature), loss.data_ptr(), lse.data_ptr(), _stream())
+        ctx.save_for_backward(out_c, pos_c, table_c, sup, offs, lse)
+        ctx.ids = ids
+        ctx.meta = (M, R, D, V, float(temperature))
+        return loss
+
+    @staticmethod
+    def backward(ctx, dloss):
+        out_c, pos_c, table_c, sup, offs, lse = ctx.saved_tensors
+        M, R, D, V, temperature = ctx.meta
+        g = dloss.to(torch.float32).contiguous()
+        d_out = torch.empty_like(out_c)
+        d_pos = torch.empty_like(pos_c)
+        d_table = torch.empty_like(table_c)
+        ids = ctx.ids
+        ws_n = _lib.lib().gr_sampled_softmax_workspace_size(M, R, V, D)
+        ws = torch.empty(max(ws_n, 4), dtype=torch.uint8, device=out_c.device)
+        _lib.call("gr_sampled_softmax_bwd", out_c.data_ptr(), D, pos_c.data_ptr(), D,
+                  sup.data_ptr(), table_c.data_ptr(), D, V,
+                  ids.data_ptr() if ids is not None else None, offs.data_ptr(), M, R, D,
+                  temperature, lse.data_ptr(), g.data_ptr(), d_out.data_ptr(), D,
+                  d_pos.data_ptr(), D, d_table.data_ptr(), D, ws.data_ptr(), ws.numel(),
+                  _stream())
+        return d_out, d_pos, d_table, None, None, None, None
+
+
+def sampled_softmax_loss(out: torch.Tensor, pos: torch.Tensor, table: torch.Tensor,
+                         sup_ids: torch.Tensor, offsets: torch.Tensor,
+                         all_ids: Optional[torch.Tensor], temperature: float) -> torch.Tensor:
+    """(M,) per-token ``-log_softmax(cat[pos, neg])[:, 0]`` of
+    autoregressive_losses.py:259-305, the negatives being ``table[offsets]``."""
+    _lib.require_gpu(out, pos, table, sup_ids, offsets, all_ids)
+    for name, t in (("out", out), ("pos", pos), ("table", table)):
+        if t.dtype != torch.float32 or t.dim() != 2:
+            raise TypeError(f"sampled_softmax_loss: {name} must be a 2-D float32 tensor")
+    M, D = out.shape
+    if pos.shape != (M, D) or table.shape[1] != D:
+        raise ValueError(f"sampled_softmax_loss: shapes out {tuple(out.shape)}, pos "
+                         f"{tuple(pos.shape)}, table {tuple(table.shape)} disagree")
+    if D > 256:
+        raise ValueError("sampled_softmax_loss: D <= 256")
+    if sup_ids.shape != (M,) or offsets.dim() != 2 or offsets.shape[0] != M:
+        raise ValueError("sampled_softmax_loss: sup_ids (M,) and offsets (M, R) expected")
+    if all_ids is not None and all_ids.shape != (table.shape[0],):
+        raise ValueError("sampled_softmax_loss: all_ids must have one id per table row")
+    return _SampledSoftmax.apply(out, pos, table, sup_ids, offsets, all_ids, float(temperature))

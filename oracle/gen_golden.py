@@ -18,8 +18,13 @@ Fixtures written:
     summation order).
   * ``jagged_ops.npz``         -- the known-answer cases of the reference's
     ``tests/test_ops.py:7-53`` (cumsum / dense_to_jagged / jagged_to_padded_dense).
+  * ``ssm_*.npz``              -- ``SampledSoftmaxLoss.jagged_forward``
+    (``autoregressive_losses.py:259-306``) with ``LocalNegativesSampler``
+    (``negative_sampler.py:66-131``) and ``DotProductSimilarity``: inputs, the seed of
+    the sampling draw, the sampled ids / offsets it produced, the loss and the
+    gradients of the query rows, the supervision embeddings and the embedding table.
 
-Usage:  python oracle/gen_golden.py   (writes tests/golden/*.npz)
+Usage:  python oracle/gen_golden.py [--only loss]   (writes tests/golden/*.npz)
 """
 from __future__ import annotations
 
@@ -205,8 +210,102 @@ def gen_jagged_ops(ops):
              values=values.numpy(), offsets2=offs2.numpy(), padded=pad.numpy())
 
 
+def _import_reference_loss():
+    if REF_SRC not in sys.path:
+        sys.path.insert(0, REF_SRC)
+    from generative_recommenders_pl.models.losses.autoregressive_losses import (  # noqa
+        SampledSoftmaxLoss,
+    )
+    from generative_recommenders_pl.models.negatives_samples.negative_sampler import (  # noqa
+        LocalNegativesSampler,
+    )
+    from generative_recommenders_pl.models.similarity.dot_product import (  # noqa
+        DotProductSimilarity,
+    )
+
+    return SampledSoftmaxLoss, LocalNegativesSampler, DotProductSimilarity
+
+
+def gen_sampled_softmax_case(name, M, D, n_catalog, R, T, l2_norm, seed, use_all_ids=True,
+                             zero_rows=False, unit_out=False):
+    SampledSoftmaxLoss, LocalNegativesSampler, DotProductSimilarity = _import_reference_loss()
+
+    class _Capture(LocalNegativesSampler):
+        def forward(self, positive_ids, num_to_sample):
+            ids, emb = super().forward(positive_ids, num_to_sample)
+            self.captured = ids.detach().clone()
+            return ids, emb
+
+    class _Emb(torch.nn.Module):
+        def __init__(self, weight):
+            super().__init__()
+            self.emb = torch.nn.Embedding.from_pretrained(weight, freeze=False)
+
+        def get_item_embeddings(self, ids):
+            return self.emb(ids)
+
+    g = torch.Generator().manual_seed(seed)
+    if use_all_ids:
+        all_ids = (torch.randperm(n_catalog, generator=g) + 1).tolist()
+        sampler = _Capture(l2_norm=l2_norm, l2_norm_eps=1e-6, all_item_ids=all_ids)
+    else:
+        all_ids = list(range(n_catalog))
+        sampler = _Capture(l2_norm=l2_norm, l2_norm_eps=1e-6, num_items=n_catalog)
+    weight = torch.randn(max(all_ids) + 1, D, generator=g) * 0.5
+    out = torch.randn(M, D, generator=g)
+    if unit_out:  # as the training step's L2-normalised encoder output
+        out = out / out.norm(dim=-1, keepdim=True)
+    sup_emb = torch.randn(M, D, generator=g)
+    if zero_rows:
+        weight[all_ids[0]] = 0.0
+        weight[all_ids[1]] *= 1e-8
+        sup_emb[0] = 0.0
+    cat = torch.tensor(all_ids)
+    sup_ids = cat[torch.randint(0, n_catalog, (M,), generator=g)]
+    sup_ids[torch.rand(M, generator=g) < 0.15] = 0
+    weights = (sup_ids != 0).float()
+    emb = _Emb(weight.clone())
+    sampler._embeddings_module = emb
+    out.requires_grad_(True)
+    sup_emb.requires_grad_(True)
+    rng_seed = seed + 1000
+    torch.manual_seed(rng_seed)
+    loss = SampledSoftmaxLoss(num_to_sample=R, softmax_temperature=T).jagged_forward(
+        output_embeddings=out, supervision_ids=sup_ids, supervision_embeddings=sup_emb,
+        supervision_weights=weights, negatives_sampler=sampler,
+        similarity=DotProductSimilarity())
+    loss.backward()
+    sampled = sampler.captured
+    inv = {int(v): i for i, v in enumerate(all_ids)}
+    offsets = torch.tensor([[inv[int(v)] for v in row] for row in sampled.reshape(M, R)],
+                           dtype=torch.int64).reshape(M, R)
+    rec = dict(out=out.detach().numpy(), sup_ids=sup_ids.numpy(),
+               sup_emb=sup_emb.detach().numpy(), weights=weights.numpy(),
+               weight=weight.numpy(), all_ids=np.array(all_ids, dtype=np.int64),
+               use_all_ids=np.array(use_all_ids), sampled_ids=sampled.numpy(),
+               offsets=offsets.numpy(), rng_seed=np.array(rng_seed), R=np.array(R),
+               T=np.array(T, dtype=np.float64), l2_norm=np.array(l2_norm),
+               eps=np.array(1e-6), loss=np.array(loss.item(), dtype=np.float32),
+               d_out=out.grad.numpy(), d_sup_emb=sup_emb.grad.numpy(),
+               d_weight=emb.emb.weight.grad.numpy())
+    np.savez_compressed(os.path.join(OUT, f"ssm_{name}.npz"), **rec)
+    n_coll = int((sampled.reshape(M, R) == sup_ids[:, None]).sum())
+    print(f"ssm_{name}: loss {loss.item():.6f} collisions {n_coll}")
+
+
+def gen_sampled_softmax():
+    gen_sampled_softmax_case("small", 37, 16, 40, 24, 0.05, True, seed=21)
+    gen_sampled_softmax_case("d50", 64, 50, 300, 128, 0.05, True, seed=22, unit_out=True)
+    gen_sampled_softmax_case("nol2", 29, 24, 20, 70, 0.1, False, seed=23, use_all_ids=False)
+    gen_sampled_softmax_case("zero", 16, 8, 12, 5, 0.05, True, seed=24, zero_rows=True)
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
+    if "--only" in sys.argv and sys.argv[sys.argv.index("--only") + 1] == "loss":
+        gen_sampled_softmax()
+        return
+    gen_sampled_softmax()
     HSTU, CandidateIndex, MIPSBruteForceTopK, ops = _import_reference()
     gen_bucket_thresholds(HSTU)
     gen_jagged_ops(ops)

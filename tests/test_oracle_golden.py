@@ -99,3 +99,50 @@ def test_jagged_ops_golden():
     for b in range(len(o2) - 1):
         pad[b, : o2[b + 1] - o2[b]] = d["values"][o2[b]:o2[b + 1]]
     assert np.array_equal(pad, d["padded"])
+
+
+# ---------------------------------------------------------------- sampled-softmax loss (N1)
+
+SSM_CASES = sorted(glob.glob(os.path.join(GOLDEN, "ssm_*.npz")))
+
+
+@pytest.mark.parametrize("path", SSM_CASES, ids=lambda p: os.path.basename(p))
+def test_loss_oracle_matches_reference_golden(path):
+    from oracle import loss_oracle
+    z = np.load(path)
+    r = loss_oracle.from_golden(z)
+    assert abs(float(r["loss"]) - float(z["loss"])) <= 1e-6 * max(1.0, abs(float(z["loss"])))
+    for key in ("d_out", "d_sup_emb", "d_weight"):
+        ref = z[key].astype(np.float64)
+        err = np.abs(r[key] - ref).max() / max(np.abs(ref).max(), 1e-30)
+        assert err < 1e-5, (key, err)
+
+
+@pytest.mark.parametrize("path", SSM_CASES, ids=lambda p: os.path.basename(p))
+def test_sampler_draw_matches_reference(path):
+    """LocalNegativesSampler.sample_offsets consumes the generator exactly as the
+    reference's forward (negative_sampler.py:110-118): same seed, same sampled ids."""
+    from mygenerativerecommenders_amd.negatives_sampler import LocalNegativesSampler
+    z = np.load(path)
+    M, R = z["offsets"].shape
+    if bool(z["use_all_ids"]):
+        s = LocalNegativesSampler(True, 1e-6, all_item_ids=z["all_ids"].tolist())
+    else:
+        s = LocalNegativesSampler(True, 1e-6, num_items=len(z["all_ids"]))
+    torch.manual_seed(int(z["rng_seed"]))
+    offs = s.sample_offsets(torch.from_numpy(z["sup_ids"]), R)
+    assert np.array_equal(offs.numpy(), z["offsets"])
+    assert np.array_equal(s.all_item_ids[offs].numpy(), z["sampled_ids"].reshape(M, R))
+
+
+def test_sampler_argument_validation():
+    from mygenerativerecommenders_amd.negatives_sampler import LocalNegativesSampler
+    with pytest.raises(ValueError):
+        LocalNegativesSampler(True, 1e-6)
+    with pytest.raises(ValueError):
+        LocalNegativesSampler(True, 1e-6, num_items=3, all_item_ids=[1, 2])
+    s = LocalNegativesSampler(False, 1e-6, num_items=5)
+    assert s.all_item_ids.tolist() == [0, 1, 2, 3, 4]
+    assert s.debug_str() == "local"
+    with pytest.raises(RuntimeError):
+        s.item_table()
