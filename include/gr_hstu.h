@@ -44,7 +44,7 @@ GR_API int gr_version(void);
  * attn_bias_reduce, ln_uvqk_fwd, gate_o_fwd, gate_o_bwd, ln_uvqk_bwd, wgrad_partial,
  * wgrad_reduce, mips_pack, mips_select, mips_merge, cumsum, dense_to_jagged,
  * jagged_to_padded, l2_normalize, current_embeddings, sampled_softmax_fwd,
- * sampled_softmax_bwd, sampled_softmax_csr, sampled_softmax_table_grad.  Not for use inside a captured graph.
+ * sampled_softmax_bwd, sampled_softmax_csr, sampled_softmax_table_grad, preproc.  Not for use inside a captured graph.
  */
 GR_API int gr_timing_enable(int on);
 GR_API int gr_timing_query(const char* kernel, double* total_ms, int* launches);
@@ -78,6 +78,22 @@ GR_API int gr_l2_normalize_bwd(const float* x, int64_t ld_x, const float* dy, in
  * of a (B, N, D) tensor, optionally L2-normalised (the retrieval query path). */
 GR_API int gr_current_embeddings(const float* encoded, const int64_t* lengths, int B, int N, int D,
                                  int normalize, float eps, float* out, void* stream);
+
+/* ---------------------------------------------------------------- input preprocessor
+ * Replaces LearnablePositionalEmbeddingInputFeaturesPreprocessor.forward
+ * (preprocessors/learnable_positional_embedding.py:42-58) on (B, N, D) contiguous rows:
+ *   y = dropout(x * scale + pos_w[n]) * (past_ids != 0),   scale = sqrt(D) in the reference
+ * dropout keeps an element iff hash(seed + *seed_offset, element index) >= p * 2^32 (kept
+ * values scaled by 1/(1-p)); seed_offset is a device counter (NULL = 0) so a captured graph
+ * draws a new mask per replay.  The backward regenerates the mask:
+ *   dx = dy * mask * scale,  dpos_w[n] = sum_b dy[b, n] * mask (fixed order over b);
+ * either output may be NULL. */
+GR_API int gr_preproc_fwd(const float* x, const int64_t* past_ids, const float* pos_w, int B, int N,
+                          int D, float scale, float dropout_p, uint64_t seed,
+                          const int64_t* seed_offset, float* y, void* stream);
+GR_API int gr_preproc_bwd(const float* dy, const int64_t* past_ids, int B, int N, int D, float scale,
+                          float dropout_p, uint64_t seed, const int64_t* seed_offset, float* dx,
+                          float* dpos_w, void* stream);
 
 /* ---------------------------------------------------------------- sampled-softmax loss
  * Fused LocalNegativesSampler.forward (negative_sampler.py:105-131, after its randint) +

@@ -99,7 +99,7 @@ KERNEL_NAMES = ("bucket_map", "attn_fwd", "attn_bwd_dkv", "attn_bwd_dq", "attn_b
                 "wgrad_reduce", "mips_pack", "mips_select", "mips_merge", "cumsum",
                 "dense_to_jagged", "jagged_to_padded", "l2_normalize", "current_embeddings",
                 "sampled_softmax_fwd", "sampled_softmax_bwd", "sampled_softmax_csr",
-                "sampled_softmax_table_grad")
+                "sampled_softmax_table_grad", "preproc")
 
 
 def timing_enable(on: bool = True):

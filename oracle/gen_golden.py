@@ -18,13 +18,16 @@ Fixtures written:
     summation order).
   * ``jagged_ops.npz``         -- the known-answer cases of the reference's
     ``tests/test_ops.py:7-53`` (cumsum / dense_to_jagged / jagged_to_padded_dense).
+  * ``preproc.npz``            -- ``LearnablePositionalEmbeddingInputFeaturesPreprocessor``
+    (``learnable_positional_embedding.py:42-58``), eval mode, with input / table grads.
+  * ``muon.npz``               -- two ``Muon.step`` (``optimizers/muon.py:46-86``) on CPU.
   * ``ssm_*.npz``              -- ``SampledSoftmaxLoss.jagged_forward``
     (``autoregressive_losses.py:259-306``) with ``LocalNegativesSampler``
     (``negative_sampler.py:66-131``) and ``DotProductSimilarity``: inputs, the seed of
     the sampling draw, the sampled ids / offsets it produced, the loss and the
     gradients of the query rows, the supervision embeddings and the embedding table.
 
-Usage:  python oracle/gen_golden.py [--only loss]   (writes tests/golden/*.npz)
+Usage:  python oracle/gen_golden.py [--only loss|preproc|muon]   (writes tests/golden/*.npz)
 """
 from __future__ import annotations
 
@@ -293,6 +296,57 @@ def gen_sampled_softmax_case(name, M, D, n_catalog, R, T, l2_norm, seed, use_all
     print(f"ssm_{name}: loss {loss.item():.6f} collisions {n_coll}")
 
 
+def gen_preprocessor():
+    """LearnablePositionalEmbeddingInputFeaturesPreprocessor.forward (eval: dropout off)
+    and the gradients of its input and positional table."""
+    if REF_SRC not in sys.path:
+        sys.path.insert(0, REF_SRC)
+    from generative_recommenders_pl.models.preprocessors.learnable_positional_embedding import (  # noqa
+        LearnablePositionalEmbeddingInputFeaturesPreprocessor as Pre,
+    )
+    torch.manual_seed(31)
+    B, N, D = 3, 13, 24
+    m = Pre(max_sequence_len=20, embedding_dim=D, dropout_rate=0.2).eval()
+    g = torch.Generator().manual_seed(32)
+    x = torch.randn(B, N, D, generator=g, requires_grad=True)
+    ids = torch.randint(1, 50, (B, N), generator=g)
+    ids[0, 9:] = 0
+    ids[2, 4:] = 0
+    lengths = (ids != 0).sum(1)
+    _, y, valid, _ = m(lengths, ids, x, {})
+    dy = torch.randn(B, N, D, generator=g)
+    (y * dy).sum().backward()
+    np.savez_compressed(os.path.join(OUT, "preproc.npz"), x=x.detach().numpy(), ids=ids.numpy(),
+                        pos_w=m._pos_emb.weight.detach().numpy(), y=y.detach().numpy(),
+                        valid=valid.numpy(), dy=dy.numpy(), dx=x.grad.numpy(),
+                        dpos=m._pos_emb.weight.grad.numpy())
+    print(f"preproc: y {tuple(y.shape)}")
+
+
+def gen_muon():
+    """Two steps of the reference Muon (optimizers/muon.py:46-86) on CPU over parameters of
+    three shape classes (wide, tall, two square of one shape) with fixed gradients."""
+    if REF_SRC not in sys.path:
+        sys.path.insert(0, REF_SRC)
+    from generative_recommenders_pl.models.optimizers.muon import Muon  # noqa
+    g = torch.Generator().manual_seed(41)
+    shapes = [(8, 24), (24, 8), (12, 12), (12, 12)]
+    params = [torch.nn.Parameter(torch.randn(s, generator=g)) for s in shapes]
+    p0 = [p.detach().clone() for p in params]
+    opt = Muon(params, lr=0.02, weight_decay=0.01, momentum=0.95)
+    rec = {f"p0_{i}": p.numpy() for i, p in enumerate(p0)}
+    for step in range(2):
+        for i, p in enumerate(params):
+            gr = torch.randn(p.shape, generator=g)
+            rec[f"g{step}_{i}"] = gr.numpy()
+            p.grad = gr.clone()
+        opt.step()
+        for i, p in enumerate(params):
+            rec[f"p{step + 1}_{i}"] = p.detach().numpy().copy()
+    np.savez_compressed(os.path.join(OUT, "muon.npz"), **rec)
+    print("muon: 2 steps over", shapes)
+
+
 def gen_sampled_softmax():
     gen_sampled_softmax_case("small", 37, 16, 40, 24, 0.05, True, seed=21)
     gen_sampled_softmax_case("d50", 64, 50, 300, 128, 0.05, True, seed=22, unit_out=True)
@@ -302,10 +356,19 @@ def gen_sampled_softmax():
 
 def main():
     os.makedirs(OUT, exist_ok=True)
-    if "--only" in sys.argv and sys.argv[sys.argv.index("--only") + 1] == "loss":
+    only = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None
+    if only == "loss":
         gen_sampled_softmax()
         return
+    if only == "preproc":
+        gen_preprocessor()
+        return
+    if only == "muon":
+        gen_muon()
+        return
     gen_sampled_softmax()
+    gen_preprocessor()
+    gen_muon()
     HSTU, CandidateIndex, MIPSBruteForceTopK, ops = _import_reference()
     gen_bucket_thresholds(HSTU)
     gen_jagged_ops(ops)

@@ -1,0 +1,60 @@
+"""GPU: N3 RetrievalMetrics on device tensors (against the oracle restatement) and N4 Muon
+on the MI355X (bf16 Newton-Schulz on the matrix cores) against the reference's two
+recorded CPU steps.  Tolerance for Muon: 2e-2 of the step size (bf16 GEMMs accumulate
+in a different order on the GPU than on the CPU that recorded the golden)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import metrics_oracle
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def test_metrics_on_device():
+    from mygenerativerecommenders_amd.metrics import RetrievalMetrics
+    g = torch.Generator().manual_seed(9)
+    B, k = 128, 200
+    top = torch.stack([torch.randperm(3953, generator=g)[:k] + 1 for _ in range(B)])
+    tgt = torch.randint(1, 3954, (B,), generator=g)
+    top[::2, 5] = tgt[::2]
+    m = RetrievalMetrics(k=k, at_k_list=[10, 50, 100, 200])
+    m.update(top_k_ids=top.cuda(), target_ids=tgt.cuda().view(-1, 1))
+    got = m.compute()
+    ref = metrics_oracle.retrieval_metrics(top.numpy(), tgt.numpy(), [10, 50, 100, 200])
+    for key, v in ref.items():
+        assert got[key].is_cuda
+        assert abs(float(got[key]) - v) < 1e-6, key
+
+
+def test_muon_on_gpu_matches_reference_golden():
+    from mygenerativerecommenders_amd.muon import Muon
+    z = np.load(os.path.join(GOLDEN, "muon.npz"))
+    n = len([k for k in z.files if k.startswith("p0_")])
+    params = [torch.nn.Parameter(torch.from_numpy(z[f"p0_{i}"]).cuda()) for i in range(n)]
+    opt = Muon(params, lr=0.02, weight_decay=0.01, momentum=0.95)
+    for step in range(2):
+        for i, p in enumerate(params):
+            p.grad = torch.from_numpy(z[f"g{step}_{i}"]).cuda()
+        opt.step()
+        for i, p in enumerate(params):
+            ref = z[f"p{step + 1}_{i}"]
+            delta = np.abs(ref - z[f"p{step}_{i}"]).max()
+            err = np.abs(p.detach().cpu().numpy() - ref).max()
+            assert err <= 2e-2 * delta, (step, i, err, delta)
+
+
+def test_muon_orthogonalises_hstu_shapes():
+    """Singular values of the NS output sit in the quintic's band (~0.5 .. 1.5) for the
+    ml-20m HSTU weight shapes (C5)."""
+    from mygenerativerecommenders_amd.muon import zeropower_via_newtonschulz5
+    g = torch.Generator(device="cuda")
+    g.manual_seed(0)
+    for shape in [(3, 256, 1024), (3, 256, 256), (4, 50, 200)]:
+        G = torch.randn(shape, device="cuda", generator=g)
+        X = zeropower_via_newtonschulz5(G, 5).float()
+        s = torch.linalg.svdvals(X)
+        assert float(s.min()) > 0.3 and float(s.max()) < 1.6, (shape, s.min(), s.max())

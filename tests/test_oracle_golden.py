@@ -146,3 +146,17 @@ def test_sampler_argument_validation():
     assert s.debug_str() == "local"
     with pytest.raises(RuntimeError):
         s.item_table()
+
+
+# ---------------------------------------------------------------- input preprocessor (N2)
+
+def test_preproc_oracle_matches_reference_golden():
+    from oracle import preproc_oracle
+    z = np.load(os.path.join(GOLDEN, "preproc.npz"))
+    D = z["x"].shape[-1]
+    y, valid = preproc_oracle.preprocess(z["x"], z["ids"], z["pos_w"], D ** 0.5)
+    assert np.allclose(y, z["y"], rtol=1e-6, atol=1e-6)
+    assert np.array_equal(valid, z["valid"])
+    dx, dpos = preproc_oracle.preprocess_bwd(z["dy"], z["ids"], D ** 0.5, z["pos_w"].shape[0])
+    assert np.allclose(dx, z["dx"], rtol=1e-6, atol=1e-6)
+    assert np.allclose(dpos, z["dpos"], rtol=1e-5, atol=1e-6)
