@@ -49,7 +49,9 @@ def test_muon_on_gpu_matches_reference_golden():
 
 def test_muon_orthogonalises_hstu_shapes():
     """Singular values of the NS output sit in the quintic's band (~0.5 .. 1.5) for the
-    ml-20m HSTU weight shapes (C5)."""
+    ml-20m HSTU weight shapes (C5).  A square Gaussian matrix has a few singular values
+    near 0 (~1/n) that 5 NS steps cannot lift, so the band is checked on the bulk: at
+    most 2 % of the values may sit below 0.3, none above 1.6."""
     from mygenerativerecommenders_amd.muon import zeropower_via_newtonschulz5
     g = torch.Generator(device="cuda")
     g.manual_seed(0)
@@ -57,4 +59,6 @@ def test_muon_orthogonalises_hstu_shapes():
         G = torch.randn(shape, device="cuda", generator=g)
         X = zeropower_via_newtonschulz5(G, 5).float()
         s = torch.linalg.svdvals(X)
-        assert float(s.min()) > 0.3 and float(s.max()) < 1.6, (shape, s.min(), s.max())
+        low = float((s < 0.3).float().mean())
+        assert low <= 0.02 and float(s.max()) < 1.6, (shape, low, s.max())
+        assert 0.6 < float(s.median()) < 1.4, (shape, s.median())
