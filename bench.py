@@ -349,9 +349,14 @@ def main():
             sidx.get_top_k_outputs(Q, invalid_ids=inv)
         _sync_barrier(world)
         _lib.timing_enable(False)
-        rt = _lib.kernel_times(("mips_select", "mips_merge", "mips_pack"))
-        ktop = rt["mips_select"][0] / max(1, rt["mips_select"][1])
+        rnames = ("mips_sample", "mips_tau", "mips_filter", "mips_merge", "mips_select",
+                  "mips_select_fallback", "mips_merge_fallback", "mips_pack")
+        rt = _lib.kernel_times(rnames)
+        rkern = "mips_filter" if rt["mips_filter"][1] else "mips_select"
+        ktop = rt[rkern][0] / max(1, rt[rkern][1])
         kmerge = rt["mips_merge"][0] / max(1, rt["mips_merge"][1])
+        rsteps = max(1, args.retrieval_steps)
+        r_dev = {n: round(v[0] / rsteps, 4) for n, v in rt.items() if v[1] and n != "mips_pack"}
         dtr = _max_over_ranks(dtr, world)
         cand_per_s = B * X * args.retrieval_steps / dtr
         fl = 2.0 * B * (b - a) * D
@@ -362,7 +367,8 @@ def main():
             "config": {"workload": "C4: 10M-item catalog row-sharded, B=128 queries, k=200, "
                                    "211 invalid ids, all-gather + device merge",
                        "items": X, "queries": B, "k": args.k, "dim": D},
-            "roofline": {"kernel": "mips_select", "bound": "mfma",
+            "per_query_batch_device_ms": r_dev,
+            "roofline": {"kernel": rkern, "bound": "mfma",
                          "achieved": round(ach_r, 3), "peak": peaks["fp32_mfma_tflops"],
                          "unit": "TFLOP/s", "frac": round(ach_r / peaks["fp32_mfma_tflops"], 4),
                          "traffic": None, "avg_launch_ms": round(ktop, 4),

@@ -147,6 +147,7 @@ struct SelectArgs {
   const int64_t* invalid;
   float* part_score;   // [n_ranges][B][k_part]
   int64_t* part_index; // [n_ranges][B][k_part]  (global index, -1 = empty)
+  const int* gate;      // non-null: run only when *gate != 0 (fallback of the filter path)
 };
 
 template <int KS, int BLOCKS>
@@ -160,6 +161,7 @@ __global__ __launch_bounds__(ST) void mips_select_kernel(SelectArgs a) {
   __shared__ int cnt[QG];
   __shared__ float tau_s[QG];
   __shared__ int need_compact;
+  if (a.gate && *a.gate == 0) return;
 
   const int tid = threadIdx.x, w = wave_id(), lane = tid & 63;
   const int lr = lane & 15, lg = lane >> 4;
@@ -417,6 +419,7 @@ struct MergeArgs {
   float* out_score;
   int64_t* out_ids;
   int64_t* out_index;
+  const int* gate;            // non-null: run only when *gate != 0
 };
 
 constexpr int MERGE_MAX = 8192;
@@ -453,16 +456,127 @@ __device__ __forceinline__ void hist_find_digit(const int* hist, int need, int* 
   }
 }
 
+// Shared LDS state of the block-level exact selection (merge kernels).
+struct SelLDS {
+  int hist[256];
+  int digit, above, cnt;
+  int red[4];
+  uint32_t s_key[256];
+  int64_t s_idx[256];
+  int s_src[256];
+};
+
+// k-th largest nonzero key of key[0..M) by 8-bit radix passes (256 threads).
+__device__ void block_radix_kth(const uint32_t* key, int M, int kk, SelLDS& L, uint32_t& kstar,
+                                int& k_rem) {
+  const int tid = threadIdx.x;
+  uint32_t prefix = 0, mask = 0;
+  int need = kk;
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    L.hist[tid] = 0;
+    __syncthreads();
+    for (int e = tid; e < M; e += 256) {
+      const uint32_t x = key[e];
+      if (x != 0u && (x & mask) == prefix) atomicAdd(&L.hist[(x >> shift) & 255], 1);
+    }
+    __syncthreads();
+    if (tid < 64) hist_find_digit(L.hist, need, &L.digit, &L.above);
+    __syncthreads();
+    prefix |= (uint32_t)L.digit << shift;
+    mask |= 0xFFu << shift;
+    need -= L.above;
+    __syncthreads();
+  }
+  kstar = prefix;
+  k_rem = need;
+}
+
+__device__ __forceinline__ int block_sum(int v, SelLDS& L) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) L.red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return L.red[0] + L.red[1] + L.red[2] + L.red[3];
+}
+
+// The kk (<= 256) largest nonzero keys of key[0..M) (tot = their count), ties at the
+// k-th key broken by the smaller idx, sorted (key desc, idx asc) into L.s_key / s_idx /
+// s_src (source position); returns how many were taken.
+__device__ int block_topk_sorted(const uint32_t* key, const int64_t* idx, int M, int kk, int tot,
+                                 SelLDS& L) {
+  const int tid = threadIdx.x;
+  uint32_t kstar = 0u;
+  int k_rem = 0;
+  const bool all = tot <= kk;
+  if (!all) block_radix_kth(key, M, kk, L, kstar, k_rem);
+  // ties at kstar: count them; if more than k_rem, keep the smallest indices
+  int eq = 0;
+  if (!all)
+    for (int e = tid; e < M; e += 256) eq += key[e] == kstar;
+  const int eq_tot = block_sum(eq, L);
+  if (tid == 0) L.cnt = 0;
+  __syncthreads();
+  for (int e = tid; e < M; e += 256) {
+    const uint32_t x = key[e];
+    if (x == 0u) continue;
+    bool take = all || x > kstar;
+    if (!all && x == kstar) {
+      if (eq_tot == k_rem) {
+        take = true;
+      } else {
+        const int64_t my = idx[e];
+        int smaller = 0;
+        for (int f = 0; f < M; ++f) smaller += (key[f] == kstar && idx[f] < my);
+        take = smaller < k_rem;
+      }
+    }
+    if (take) {
+      const int p = atomicAdd(&L.cnt, 1);
+      L.s_key[p] = x;
+      L.s_idx[p] = idx[e];
+      L.s_src[p] = e;
+    }
+  }
+  __syncthreads();
+  const int n = L.cnt;
+  for (int p = n + tid; p < 256; p += 256) {
+    L.s_key[p] = 0u;
+    L.s_idx[p] = INT64_MAX;
+    L.s_src[p] = -1;
+  }
+  __syncthreads();
+  // bitonic sort 256 entries: key desc, then catalog index asc
+  for (int size = 2; size <= 256; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      const int i = tid;
+      const int j = i ^ stride;
+      if (j > i) {
+        const uint32_t ki = L.s_key[i], kj = L.s_key[j];
+        const int64_t ii = L.s_idx[i], ij = L.s_idx[j];
+        const bool i_first = (ki > kj) || (ki == kj && ii < ij);
+        const bool asc = (i & size) == 0;
+        if (i_first != asc) {
+          L.s_key[i] = kj;
+          L.s_key[j] = ki;
+          L.s_idx[i] = ij;
+          L.s_idx[j] = ii;
+          const int t = L.s_src[i];
+          L.s_src[i] = L.s_src[j];
+          L.s_src[j] = t;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  return n;
+}
+
 __global__ __launch_bounds__(256) void mips_merge_kernel(MergeArgs a) {
+  if (a.gate && *a.gate == 0) return;  // fallback merge: only when the filter path failed
   __shared__ uint32_t key[MERGE_MAX];
   __shared__ int64_t idx[MERGE_MAX];
-  __shared__ int hist[256];
-  __shared__ int sh_digit, sh_above;
-  __shared__ uint32_t s_key[256];
-  __shared__ int64_t s_idx[256];
-  __shared__ int s_src[256];
-  __shared__ int s_cnt;
-  __shared__ int red[4];
+  __shared__ SelLDS L;
   const int q = blockIdx.x;
   const int tid = threadIdx.x;
   const int M = a.n_lists * a.k_in;
@@ -479,104 +593,14 @@ __global__ __launch_bounds__(256) void mips_merge_kernel(MergeArgs a) {
     idx[e] = ok ? gi : INT64_MAX;
     nvalid += ok;
   }
-  int v = nvalid;
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-  if ((tid & 63) == 0) red[tid >> 6] = v;
-  __syncthreads();
-  const int tot = red[0] + red[1] + red[2] + red[3];
+  const int tot = block_sum(nvalid, L);
   const int kk = a.k;
-  uint32_t kstar = 0u;
-  int k_rem = 0;
-  const bool all = tot <= kk;
-  if (!all) {
-    uint32_t prefix = 0, mask = 0;
-    int need = kk;
-    for (int shift = 24; shift >= 0; shift -= 8) {
-      hist[tid] = 0;
-      __syncthreads();
-      for (int e = tid; e < M; e += 256) {
-        const uint32_t x = key[e];
-        if (x != 0u && (x & mask) == prefix) atomicAdd(&hist[(x >> shift) & 255], 1);
-      }
-      __syncthreads();
-      if (tid < 64) hist_find_digit(hist, need, &sh_digit, &sh_above);
-      __syncthreads();
-      prefix |= (uint32_t)sh_digit << shift;
-      mask |= 0xFFu << shift;
-      need -= sh_above;
-    }
-    kstar = prefix;
-    k_rem = need;
-  }
-  // ties at kstar: count them; if more than k_rem, keep the smallest indices
-  int eq = 0;
-  if (!all)
-    for (int e = tid; e < M; e += 256) eq += key[e] == kstar;
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) eq += __shfl_xor(eq, o, 64);
-  __syncthreads();
-  if ((tid & 63) == 0) red[tid >> 6] = eq;
-  if (tid == 0) s_cnt = 0;
-  __syncthreads();
-  const int eq_tot = red[0] + red[1] + red[2] + red[3];
-  for (int e = tid; e < M; e += 256) {
-    const uint32_t x = key[e];
-    if (x == 0u) continue;
-    bool take = all || x > kstar;
-    if (!all && x == kstar) {
-      if (eq_tot == k_rem) {
-        take = true;
-      } else {
-        const int64_t my = idx[e];
-        int smaller = 0;
-        for (int f = 0; f < M; ++f) smaller += (key[f] == kstar && idx[f] < my);
-        take = smaller < k_rem;
-      }
-    }
-    if (take) {
-      const int p = atomicAdd(&s_cnt, 1);
-      s_key[p] = x;
-      s_idx[p] = idx[e];
-      s_src[p] = e;
-    }
-  }
-  __syncthreads();
-  const int n = s_cnt;
-  for (int p = n + tid; p < 256; p += 256) {
-    s_key[p] = 0u;
-    s_idx[p] = INT64_MAX;
-    s_src[p] = -1;
-  }
-  __syncthreads();
-  // bitonic sort 256 entries: key desc, then catalog index asc
-  for (int size = 2; size <= 256; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      const int i = tid;
-      const int j = i ^ stride;
-      if (j > i) {
-        const uint32_t ki = s_key[i], kj = s_key[j];
-        const int64_t ii = s_idx[i], ij = s_idx[j];
-        const bool i_first = (ki > kj) || (ki == kj && ii < ij);
-        const bool asc = (i & size) == 0;
-        if (i_first != asc) {
-          s_key[i] = kj;
-          s_key[j] = ki;
-          s_idx[i] = ij;
-          s_idx[j] = ii;
-          const int t = s_src[i];
-          s_src[i] = s_src[j];
-          s_src[j] = t;
-        }
-      }
-      __syncthreads();
-    }
-  }
+  const int n = block_topk_sorted(key, idx, M, kk, tot, L);
   for (int r = tid; r < kk; r += 256) {
     const int64_t o = (int64_t)q * kk + r;
     if (r < n) {
-      const int64_t s = src_of(s_src[r]);
-      const int64_t gi = s_idx[r];
+      const int64_t s = src_of(L.s_src[r]);
+      const int64_t gi = L.s_idx[r];
       a.out_score[o] = a.cand_score[s];
       if (a.out_index) a.out_index[o] = gi;
       int64_t id;
@@ -671,12 +695,364 @@ __global__ __launch_bounds__(256) void mips_scoreall_kernel(ScoreAllArgs a) {
   }
 }
 
+// ----------------------------------------------------------------- large catalogs
+// Threshold-filter path (D <= 64, X >= FILTER_MIN_X).  The 16-query-per-workgroup
+// select above re-reads the table once per query group (8x at B = 128) and keeps
+// per-query candidate buffers in LDS; here every workgroup scores ALL queries of its
+// chunk (up to 128, fragments held in VGPRs) against each item block it loads, so the
+// table streams from HBM once and the MFMA pipe is the bound.  The per-query selection
+// state becomes one threshold tau_q, fixed before the pass:
+//   1. sample:  score every SR-th item block; each wave reduces its group of sample
+//      blocks to one max per query -> smax[q][g] (G groups).
+//   2. tau:     tau_q = the M_SAMPLE-th largest of the G group maxima.  Those maxima
+//      are real catalog items, so >= M_SAMPLE items score >= tau_q, and (1/SR
+//      sampled) about M_SAMPLE * SR do.
+//   3. filter:  full pass; scores >= tau_q are appended (global atomics; ~1e-4 of
+//      scores) to a per-query list of FILTER_CAP.
+//   4. merge:   per query, drop invalid ids, exact top-k (radix select + sort).  Every
+//      uncollected item scores < tau_q <= every collected one, so the result is exact
+//      whenever the list did not overflow and kept >= k valid items.  Otherwise the
+//      merge raises a device flag and the exact select + merge kernels above (gated on
+//      that flag, no host sync) recompute every query.
+constexpr int SAMPLE_STRIDE = 16;       // sample every 16th item block
+constexpr int SAMPLE_GROUPS = 4096;     // target number of group maxima per query
+constexpr int M_SAMPLE = 64;            // tau = 64th largest group max -> ~1024 candidates
+constexpr int FILTER_CAP = 4096;        // candidate list per query
+constexpr int NSUB = 16;                // ... split into sub-lists by workgroup (blockIdx % 16)
+constexpr int SUBCAP = FILTER_CAP / NSUB;  // so each counter sees 1/16 of the atomics
+constexpr int64_t FILTER_MIN_X = (int64_t)SAMPLE_STRIDE * 16 * 1024;  // >= 1024 sample blocks
+
+struct FilterArgs {
+  const float* q;
+  const float* packed;
+  int64_t X;
+  int D, B;
+  int64_t n_blocks;
+  // sample pass
+  int GB, G;          // sample blocks per group, groups
+  float* smax;        // [B][G]
+  // filter pass
+  int64_t RB;         // item blocks per wave
+  const float* tau;   // [B]
+  int* cnt;           // [B][NSUB]
+  float* cand_s;      // [B][NSUB][SUBCAP]
+  int* cand_i;        // [B][NSUB][SUBCAP]  local item index
+  int* flag;          // set when a workgroup's staging buffer overflows
+  int nohit;          // profiling knob (GR_MIPS_DEBUG_NOHIT): thresholds +inf
+};
+
+constexpr int WG_CAP = 4096;  // per-workgroup LDS staging of filter hits (~256 expected)
+constexpr int WV_CAP = WG_CAP / 4;  // per-wave segment
+
+template <int KS, int NQG, bool SAMPLE>
+__global__ __launch_bounds__(256) void mips_filter_kernel(FilterArgs a) {
+  constexpr int KS2 = (KS + 1) / 2;
+  typedef float fv2 __attribute__((ext_vector_type(2)));
+  const int lane = threadIdx.x & 63, lr = lane & 15, lg = lane >> 4;
+  const int64_t wv = (int64_t)blockIdx.x * 4 + wave_id();
+  const int qb = blockIdx.y * (NQG * 16);
+
+  int64_t b0 = 0, b1 = 0, bstride;
+  if (SAMPLE) {
+    const int64_t n_sb = (a.n_blocks + SAMPLE_STRIDE - 1) / SAMPLE_STRIDE;
+    const int64_t s0 = wv * a.GB, s1 = min(n_sb, s0 + a.GB);
+    if (wv < a.G) {
+      b0 = s0 * SAMPLE_STRIDE;
+      b1 = s1 * SAMPLE_STRIDE;
+    }
+    bstride = SAMPLE_STRIDE;
+  } else {
+    b0 = wv * a.RB;
+    b1 = min(a.n_blocks, b0 + a.RB);
+    bstride = 1;
+  }
+  __shared__ float l_s[SAMPLE ? 1 : WG_CAP];
+  __shared__ int l_i[SAMPLE ? 1 : WG_CAP];
+  __shared__ uint8_t l_q[SAMPLE ? 1 : WG_CAP];
+  __shared__ int l_wn[4];
+  const int w_base = wave_id() * WV_CAP;
+  int w_n = 0;  // wave-uniform hit count of this wave's segment
+  // The chunk's query fragments, staged once per workgroup with coalesced row reads
+  // (every wave of the grid loading its own fragments hammers the L2 lines of the
+  // same 25 KB query block: ~90 us of contention at launch), in MFMA B-operand order
+  // so each wave's reads are conflict-free: frag[(g KS + st) 64 + lr + 16 lg] =
+  // Q[qb + 16 g + lr][4 st + lg].
+  __shared__ float q_lds[NQG * KS * 64];
+  __shared__ float tau_lds[NQG * 16];
+  {
+    const int rows = NQG * 16, cols = 4 * KS;
+    for (int e = threadIdx.x; e < rows * cols; e += 256) {
+      const int r = e / cols, d = e - r * cols;
+      const int qq = qb + r;
+      const float v = (qq < a.B && d < a.D) ? a.q[(int64_t)qq * a.D + d] : 0.f;
+      q_lds[((r >> 4) * KS + (d >> 2)) * 64 + (r & 15) + 16 * (d & 3)] = v;
+    }
+    for (int r = threadIdx.x; r < rows; r += 256) {
+      const int qq = qb + r;
+      tau_lds[r] = SAMPLE ? -INFINITY : (qq < a.B && !a.nohit ? a.tau[qq] : INFINITY);
+    }
+    __syncthreads();
+  }
+  float qreg[NQG][KS];
+#pragma unroll
+  for (int g = 0; g < NQG; ++g)
+#pragma unroll
+    for (int st = 0; st < KS; ++st) qreg[g][st] = q_lds[(g * KS + st) * 64 + lane];
+  float thr[NQG];  // filter: tau of query 16 g + lr (+inf for padded queries); sample: running max
+#pragma unroll
+  for (int g = 0; g < NQG; ++g) thr[g] = tau_lds[16 * g + lr];
+
+  gptr<fv2> pk = as_global(reinterpret_cast<const fv2*>(a.packed));
+  gptr<float> pk1 = as_global(a.packed);
+  // An odd KS leaves the .y half of the last pair unused (zero padding): load only the
+  // .x half, so no in-flight load targets a register the compiler considers dead (it
+  // would reuse it as a temporary and wait vmcnt(0) on the prefetch).
+  constexpr int NP = KS / 2;  // full pairs
+  struct Frag {
+    fv2 p[NP > 0 ? NP : 1];
+    float t;
+  };
+  Frag fa, fb;
+  auto load = [&](Frag& f, int64_t ib) {
+    ib = ib < b1 ? ib : b1 - bstride;  // clamped: loads stay unconditional
+    gptr<fv2> src = pk + ib * KS2 * 64 + lane;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) f.p[j] = src[j * 64];
+    if (KS & 1) f.t = pk1[((ib * KS2 + NP) * 64 + lane) * 2];
+  };
+  auto process = [&](const Frag& f, int64_t ib) {
+    f4 s[NQG];
+#pragma unroll
+    for (int g = 0; g < NQG; ++g) s[g] = f4_zero();
+#pragma unroll
+    for (int st = 0; st < KS; ++st) {
+      const float av = (st >> 1) < NP ? ((st & 1) ? f.p[st >> 1].y : f.p[st >> 1].x) : f.t;
+#pragma unroll
+      for (int g = 0; g < NQG; ++g) s[g] = mfma16x16x4(av, qreg[g][st], s[g]);
+    }
+    const int64_t item0 = ib * 16 + 4 * lg;  // rows 4 lg + r of the block
+    const bool full = ib * 16 + 16 <= a.X;   // wave-uniform
+    if (SAMPLE) {
+#pragma unroll
+      for (int g = 0; g < NQG; ++g)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          thr[g] = fmaxf(thr[g], (full || item0 + r < a.X) ? s[g][r] : -INFINITY);
+    } else {
+      // hits are rare (~1e-4 of scores): one wave-wide OR per block; a block with any
+      // hit appends them to this wave's private LDS segment at positions from
+      // ballots and a wave-uniform (scalar) counter: no atomics, no waits
+      bool hit = false;
+#pragma unroll
+      for (int g = 0; g < NQG; ++g)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) hit |= s[g][r] >= thr[g];
+      if (__builtin_expect(__ballot(hit) != 0ull, 0)) {
+#pragma unroll
+        for (int g = 0; g < NQG; ++g) {
+          bool hg = false;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) hg |= s[g][r] >= thr[g];
+          if (__ballot(hg) == 0ull) continue;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const bool h = s[g][r] >= thr[g] && (full || item0 + r < a.X);
+            const uint64_t bl = __ballot(h);
+            if (bl) {
+              const int p = w_n + __builtin_amdgcn_mbcnt_hi((uint32_t)(bl >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)bl, 0));
+              if (h && p < WV_CAP) {
+                l_s[w_base + p] = s[g][r];
+                l_i[w_base + p] = (int)(item0 + r);
+                l_q[w_base + p] = (uint8_t)(16 * g + lr);
+              }
+              w_n += __popcll(bl);
+            }
+          }
+        }
+      }
+    }
+  };
+
+  if (SAMPLE && b0 < b1) {
+    // a few sample blocks per wave at a 16-block stride: issue a chunk's loads
+    // together, then score them (duplicated clamped blocks leave the max unchanged)
+    constexpr int CH = 4;
+    for (int64_t ib = b0; ib < b1; ib += CH * bstride) {
+      Frag f[CH];
+#pragma unroll
+      for (int c = 0; c < CH; ++c) load(f[c], ib + c * bstride);
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        const int64_t jb = ib + c * bstride;
+        process(f[c], jb < b1 ? jb : b1 - bstride);
+      }
+    }
+  } else if (!SAMPLE && b0 < b1) {
+    load(fa, b0);
+    for (int64_t ib = b0; ib < b1; ib += 2 * bstride) {
+      load(fb, ib + bstride);
+      process(fa, ib);
+      if (ib + bstride >= b1) break;
+      load(fa, ib + 2 * bstride);
+      process(fb, ib + bstride);
+    }
+  }
+  if (!SAMPLE) {  // flush the workgroup's hits to the per-query lists
+    if (lane == 0) l_wn[wave_id()] = w_n;
+    __syncthreads();
+    if (threadIdx.x == 0 && (l_wn[0] > WV_CAP || l_wn[1] > WV_CAP || l_wn[2] > WV_CAP ||
+                             l_wn[3] > WV_CAP))
+      atomicExch(a.flag, 1);  // a segment overflowed: the exact fallback recomputes
+    for (int w = 0; w < 4; ++w) {
+      const int n = l_wn[w] < WV_CAP ? l_wn[w] : WV_CAP;
+      for (int e = threadIdx.x; e < n; e += 256) {
+        const int src = w * WV_CAP + e;
+        const int qq = qb + l_q[src];
+        const int64_t sub = (int64_t)qq * NSUB + (blockIdx.x & (NSUB - 1));
+        const int pos = atomicAdd(&a.cnt[sub], 1);
+        if (pos < SUBCAP) {
+          a.cand_s[sub * SUBCAP + pos] = l_s[src];
+          a.cand_i[sub * SUBCAP + pos] = l_i[src];
+        }
+      }
+    }
+  }
+  if (SAMPLE && b0 < b1) {
+#pragma unroll
+    for (int g = 0; g < NQG; ++g) {
+      float m = thr[g];
+      m = fmaxf(m, __shfl_xor(m, 16, 64));
+      m = fmaxf(m, __shfl_xor(m, 32, 64));
+      const int qq = qb + 16 * g + lr;
+      if (lg == 0 && qq < a.B) a.smax[(int64_t)qq * a.G + wv] = m;
+    }
+  }
+}
+
+// tau_q = M_SAMPLE-th largest group max (one workgroup per query); also resets the
+// query's candidate counter and (query 0) the fallback flag.
+__global__ __launch_bounds__(256) void mips_tau_kernel(const float* smax, int G, float* tau, int* cnt,
+                                                       int* flag) {
+  __shared__ uint32_t key[SAMPLE_GROUPS];
+  __shared__ SelLDS L;
+  const int q = blockIdx.x, tid = threadIdx.x;
+  for (int e = tid; e < G; e += 256) key[e] = ord_key(smax[(int64_t)q * G + e]);
+  __syncthreads();
+  const int m = G < M_SAMPLE ? G : M_SAMPLE;
+  uint32_t kstar;
+  int k_rem;
+  block_radix_kth(key, G, m, L, kstar, k_rem);
+  if (tid < NSUB) cnt[q * NSUB + tid] = 0;
+  if (tid == 0) {
+    tau[q] = key_to_float(kstar);
+    if (q == 0) *flag = 0;
+  }
+}
+
+struct FilterMergeArgs {
+  const float* cand_s;
+  const int* cand_i;
+  const int* cnt;
+  int B, k, N0;
+  const int64_t* item_ids;
+  int64_t index_base;
+  const int64_t* invalid;
+  float* out_score;
+  int64_t* out_ids;
+  int64_t* out_index;
+  int* flag;
+};
+
+__global__ __launch_bounds__(256) void mips_filter_merge_kernel(FilterMergeArgs a) {
+  __shared__ uint32_t key[FILTER_CAP];
+  __shared__ int64_t idx[FILTER_CAP];
+  __shared__ int64_t inv[INV_MAX];
+  __shared__ SelLDS L;
+  __shared__ int sub_off[NSUB + 1];
+  __shared__ float cs[FILTER_CAP];
+  __shared__ int ci[FILTER_CAP];
+  const int q = blockIdx.x, tid = threadIdx.x;
+  if (tid == 0) {
+    int o = 0;
+    bool over = false;
+    for (int u = 0; u < NSUB; ++u) {
+      const int c = a.cnt[q * NSUB + u];
+      over |= c > SUBCAP;
+      sub_off[u] = o;
+      o += c < SUBCAP ? c : SUBCAP;
+    }
+    sub_off[NSUB] = over ? -1 : o;
+  }
+  __syncthreads();
+  const int n_raw = sub_off[NSUB];
+  if (n_raw < 0) {  // a sub-list overflowed: the exact fallback recomputes
+    if (tid == 0) atomicExch(a.flag, 1);
+    return;
+  }
+  for (int u = 0; u < NSUB; ++u) {  // compact the sub-lists into LDS
+    const int n = (u + 1 < NSUB ? sub_off[u + 1] : n_raw) - sub_off[u];
+    const int64_t src = ((int64_t)q * NSUB + u) * SUBCAP;
+    for (int e = tid; e < n; e += 256) {
+      cs[sub_off[u] + e] = a.cand_s[src + e];
+      ci[sub_off[u] + e] = a.cand_i[src + e];
+    }
+  }
+  const int n0p = a.N0 <= 0 ? 0 : (a.N0 <= 64 ? 64 : (a.N0 <= 128 ? 128 : 256));
+  for (int j = tid; j < n0p; j += 256)
+    inv[j] = j < a.N0 ? a.invalid[(int64_t)q * a.N0 + j] : INT64_MAX;
+  __syncthreads();
+  for (int size = 2; size <= n0p; size <<= 1)
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int p = tid; p < n0p / 2; p += 256) {
+        const int i = 2 * p - (p & (stride - 1)), j = i + stride;
+        const bool up = (i & size) == 0;
+        const int64_t x = inv[i], y = inv[j];
+        if ((x > y) == up) {
+          inv[i] = y;
+          inv[j] = x;
+        }
+      }
+      __syncthreads();
+    }
+  int nvalid = 0;
+  for (int e = tid; e < n_raw; e += 256) {
+    const int64_t li = ci[e];
+    const int64_t id = a.item_ids ? a.item_ids[li] : a.index_base + li;
+    const bool ok = !(n0p > 0 && sorted_contains(inv, n0p, id));
+    key[e] = ok ? ord_key(cs[e]) : 0u;
+    idx[e] = a.index_base + li;
+    nvalid += ok;
+  }
+  const int tot = block_sum(nvalid, L);
+  if (tot < a.k) {  // fewer than k valid items at or above tau: not provably exact
+    if (tid == 0) atomicExch(a.flag, 1);
+    return;
+  }
+  const int n = block_topk_sorted(key, idx, n_raw, a.k, tot, L);
+  for (int r = tid; r < a.k; r += 256) {
+    const int64_t o = (int64_t)q * a.k + r;
+    const int e = L.s_src[r];  // r < n == k
+    const int64_t gi = L.s_idx[r];
+    a.out_score[o] = cs[e];
+    if (a.out_index) a.out_index[o] = gi;
+    a.out_ids[o] = a.item_ids ? a.item_ids[gi - a.index_base] : gi;
+  }
+  (void)n;
+}
+
 struct TopkPlan {
-  bool small;
+  bool small, filter;
   int KS, n_ranges, k_part;
   int64_t range_items;
-  size_t part_bytes;
+  size_t part_bytes;   // legacy select partial lists (also the filter path's fallback)
+  // filter path
+  int64_t n_blocks, RB;
+  int GB, G, NQG, n_chunks, filter_waves;
+  size_t off_tau, off_cnt, off_smax, off_cs, off_ci, off_part, total_bytes;
 };
+
+static size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 
 static TopkPlan plan_topk(int B, int64_t X, int D, int k) {
   TopkPlan p;
@@ -705,7 +1081,63 @@ static TopkPlan plan_topk(int B, int64_t X, int D, int k) {
     const size_t sb = (size_t)B * X * (sizeof(float) + sizeof(int64_t));
     if (sb > p.part_bytes) p.part_bytes = sb;
   }
+  p.filter = !p.small && X >= FILTER_MIN_X && p.KS <= 16;
+  p.total_bytes = p.part_bytes;
+  p.off_part = 0;
+  if (p.filter) {
+    p.n_blocks = (X + 15) / 16;
+    const int64_t n_sb = (p.n_blocks + SAMPLE_STRIDE - 1) / SAMPLE_STRIDE;
+    p.GB = (int)((n_sb + SAMPLE_GROUPS - 1) / SAMPLE_GROUPS);
+    p.G = (int)((n_sb + p.GB - 1) / p.GB);
+    p.NQG = B <= 32 ? 2 : 8;
+    p.n_chunks = ceil_div(B, p.NQG * 16);
+    // whole rounds of 2 four-wave workgroups per CU, >= ~48 blocks per wave
+    const int64_t per_round = (int64_t)device_cus() * 8;
+    int64_t rounds = (p.n_blocks + per_round * 48 - 1) / (per_round * 48);
+    static const char* env_rounds = getenv("GR_MIPS_FILTER_ROUNDS");  // tuning knob
+    if (env_rounds) rounds = atoi(env_rounds);
+    if (rounds < 1) rounds = 1;
+    p.RB = (p.n_blocks + per_round * rounds - 1) / (per_round * rounds);
+    p.filter_waves = (int)((p.n_blocks + p.RB - 1) / p.RB);
+    size_t o = 256;  // [0, 4): fallback flag
+    p.off_tau = o;  o = align256(o + sizeof(float) * B);
+    p.off_cnt = o;  o = align256(o + sizeof(int) * B * NSUB);
+    p.off_smax = o; o = align256(o + sizeof(float) * (size_t)B * p.G);
+    p.off_cs = o;   o = align256(o + sizeof(float) * (size_t)B * FILTER_CAP);
+    p.off_ci = o;   o = align256(o + sizeof(int) * (size_t)B * FILTER_CAP);
+    p.off_part = o;
+    p.total_bytes = o + p.part_bytes;
+  }
   return p;
+}
+
+template <int KS, int NQG>
+static int launch_filter_pair(const FilterArgs& f, const TopkPlan& p, bool sample, hipStream_t st) {
+  if (sample) {
+    const dim3 g(ceil_div(p.G, 4), p.n_chunks);
+    GR_TIMED("mips_sample", st, hipLaunchKernelGGL((mips_filter_kernel<KS, NQG, true>), g, dim3(256), 0, st, f));
+    GR_LAUNCH_CHECK("mips_topk(sample)");
+  } else {
+    const dim3 g(ceil_div(p.filter_waves, 4), p.n_chunks);
+    GR_TIMED("mips_filter", st, hipLaunchKernelGGL((mips_filter_kernel<KS, NQG, false>), g, dim3(256), 0, st, f));
+    GR_LAUNCH_CHECK("mips_topk(filter)");
+  }
+  return 0;
+}
+
+template <int KS>
+static int launch_filter_ks(const FilterArgs& f, const TopkPlan& p, bool sample, hipStream_t st) {
+  return p.NQG == 2 ? launch_filter_pair<KS, 2>(f, p, sample, st) : launch_filter_pair<KS, 8>(f, p, sample, st);
+}
+
+static int launch_filter(const FilterArgs& f, const TopkPlan& p, bool sample, hipStream_t st) {
+  switch (p.KS) {
+    case 1: case 2: return launch_filter_ks<2>(f, p, sample, st);
+    case 3: case 4: return launch_filter_ks<4>(f, p, sample, st);
+    case 5: case 6: case 7: case 8: return launch_filter_ks<8>(f, p, sample, st);
+    case 9: case 10: case 11: case 12: case 13: return launch_filter_ks<13>(f, p, sample, st);
+    default: return launch_filter_ks<16>(f, p, sample, st);
+  }
 }
 
 template <int KS>
@@ -714,7 +1146,7 @@ static int launch_select(const SelectArgs& a, hipStream_t st) {
   const int n_qg = ceil_div(a.B, QG);
   const int n_r8 = ceil_div(a.n_ranges, 8) * 8;
   const int grid = n_r8 * n_qg;
-  GR_TIMED("mips_select", st, hipLaunchKernelGGL((mips_select_kernel<KS, BLOCKS>), dim3(grid), dim3(ST), 0, st, a));
+  GR_TIMED(a.gate ? "mips_select_fallback" : "mips_select", st, hipLaunchKernelGGL((mips_select_kernel<KS, BLOCKS>), dim3(grid), dim3(ST), 0, st, a));
   GR_LAUNCH_CHECK("mips_topk(select)");
   return 0;
 }
@@ -740,7 +1172,7 @@ extern "C" int mips_pack_items(const float* items, int64_t X, int D, float* pack
 
 extern "C" size_t mips_topk_workspace_size(int B, int64_t X, int D, int k) {
   if (B <= 0 || X <= 0 || D <= 0 || k <= 0) return 0;
-  return plan_topk(B, X, D, k).part_bytes;
+  return plan_topk(B, X, D, k).total_bytes;
 }
 
 extern "C" int mips_topk(const float* queries, const float* packed_items, int64_t X, int D,
@@ -756,8 +1188,8 @@ extern "C" int mips_topk(const float* queries, const float* packed_items, int64_
   hipStream_t st = (hipStream_t)stream;
   if (B == 0) return 0;
   TopkPlan p = plan_topk(B, X > 0 ? X : 1, D, k);
-  GR_REQUIRE(workspace && ws_bytes >= p.part_bytes, "mips_topk: workspace %zu B < %zu B", ws_bytes,
-             p.part_bytes);
+  GR_REQUIRE(workspace && ws_bytes >= p.total_bytes, "mips_topk: workspace %zu B < %zu B", ws_bytes,
+             p.total_bytes);
   if (p.small) {
     float* sc = (float*)workspace;
     int64_t* ix = (int64_t*)(sc + (size_t)B * X);
@@ -774,15 +1206,36 @@ extern "C" int mips_topk(const float* queries, const float* packed_items, int64_
 #undef GR_SA
     GR_LAUNCH_CHECK("mips_topk(score-all)");
     MergeArgs m{sc, ix, nullptr, 1, B, (int)X, k, item_ids, index_base,
-                out_scores, out_ids, out_index};
+                out_scores, out_ids, out_index, nullptr};
     GR_TIMED("mips_merge", st, hipLaunchKernelGGL(mips_merge_kernel, dim3(B), dim3(256), 0, st, m));
     GR_LAUNCH_CHECK("mips_topk(merge)");
     return 0;
   }
-  float* part_score = (float*)workspace;
+  char* ws = (char*)workspace;
+  int* flag = nullptr;
+  if (p.filter) {
+    flag = (int*)ws;
+    float* tau = (float*)(ws + p.off_tau);
+    int* cnt = (int*)(ws + p.off_cnt);
+    FilterArgs f{queries, packed_items, X, D, B, p.n_blocks, p.GB, p.G, (float*)(ws + p.off_smax),
+                 p.RB, tau, cnt, (float*)(ws + p.off_cs), (int*)(ws + p.off_ci), (int*)ws,
+                 getenv("GR_MIPS_DEBUG_NOHIT") != nullptr};
+    int rc = launch_filter(f, p, true, st);
+    if (rc) return rc;
+    GR_TIMED("mips_tau", st, hipLaunchKernelGGL(mips_tau_kernel, dim3(B), dim3(256), 0, st, f.smax, p.G, tau, cnt, flag));
+    GR_LAUNCH_CHECK("mips_topk(tau)");
+    rc = launch_filter(f, p, false, st);
+    if (rc) return rc;
+    FilterMergeArgs fm{f.cand_s, f.cand_i, cnt, B, k, N0, item_ids, index_base, invalid_ids,
+                       out_scores, out_ids, out_index, flag};
+    GR_TIMED("mips_merge", st, hipLaunchKernelGGL(mips_filter_merge_kernel, dim3(B), dim3(256), 0, st, fm));
+    GR_LAUNCH_CHECK("mips_topk(filter merge)");
+  }
+  // exact range-select path (the filter path's fallback, gated on its flag)
+  float* part_score = (float*)(ws + p.off_part);
   int64_t* part_index = (int64_t*)(part_score + (size_t)p.n_ranges * B * p.k_part);
   SelectArgs a{queries, packed_items, X, D, B, k, N0, p.n_ranges, p.k_part, p.range_items,
-               item_ids, index_base, invalid_ids, part_score, part_index};
+               item_ids, index_base, invalid_ids, part_score, part_index, flag};
   int rc;
   switch (p.KS) {
     case 1: case 2: rc = launch_select<2>(a, st); break;
@@ -796,8 +1249,8 @@ extern "C" int mips_topk(const float* queries, const float* packed_items, int64_
   }
   if (rc) return rc;
   MergeArgs m{part_score, part_index, nullptr, p.n_ranges, B, p.k_part, k, item_ids, index_base,
-              out_scores, out_ids, out_index};
-  GR_TIMED("mips_merge", st, hipLaunchKernelGGL(mips_merge_kernel, dim3(B), dim3(256), 0, st, m));
+              out_scores, out_ids, out_index, flag};
+  GR_TIMED(flag ? "mips_merge_fallback" : "mips_merge", st, hipLaunchKernelGGL(mips_merge_kernel, dim3(B), dim3(256), 0, st, m));
   GR_LAUNCH_CHECK("mips_topk(merge)");
   return 0;
 }
@@ -812,7 +1265,7 @@ extern "C" int mips_merge_topk(const float* cand_scores, const int64_t* cand_ind
              "mips_merge_topk: need 0 < k <= 256 and n_lists*k_in <= %d", MERGE_MAX);
   if (B == 0) return 0;
   MergeArgs m{cand_scores, cand_index, cand_ids, n_lists, B, k_in, k, nullptr, 0,
-              out_scores, out_ids, out_index};
+              out_scores, out_ids, out_index, nullptr};
   GR_TIMED("mips_merge", (hipStream_t)stream, hipLaunchKernelGGL(mips_merge_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, m));
   GR_LAUNCH_CHECK("mips_merge_topk");
   return 0;

@@ -48,11 +48,19 @@ class PackedItems:
         self.device = items.device
 
 
+def topk_workspace_bytes(B: int, X: int, D: int, k: int) -> int:
+    """Workspace ``mips_topk`` needs for a (B, D) query batch over X items."""
+    return max(int(_lib.lib().mips_topk_workspace_size(B, X, D, k)), 16)
+
+
 def mips_topk(queries: torch.Tensor, packed: PackedItems, k: int,
               item_ids: Optional[torch.Tensor] = None, invalid_ids: Optional[torch.Tensor] = None,
-              index_base: int = 0, return_index: bool = False):
+              index_base: int = 0, return_index: bool = False,
+              workspace: Optional[torch.Tensor] = None):
     """Fused brute-force MIPS top-k over a packed table.  Returns (scores (B,k) f32,
-    ids (B,k) i64[, global index (B,k) i64])."""
+    ids (B,k) i64[, global index (B,k) i64]).  ``workspace`` (uint8, at least
+    ``topk_workspace_bytes``) may be passed to reuse one buffer across calls; on the
+    large-catalog filter path its first int32 is 1 when the exact fallback ran."""
     _lib.require_gpu(queries)
     B, D = queries.shape
     if D != packed.D:
@@ -78,8 +86,13 @@ def mips_topk(queries: torch.Tensor, packed: PackedItems, k: int,
     scores = torch.empty(B, k, dtype=torch.float32, device=dev)
     out_ids = torch.empty(B, k, dtype=torch.int64, device=dev)
     out_idx = torch.empty(B, k, dtype=torch.int64, device=dev) if return_index else None
-    ws_n = _lib.lib().mips_topk_workspace_size(B, packed.X, D, k)
-    ws = torch.empty(max(ws_n, 16), dtype=torch.uint8, device=dev)
+    ws_n = topk_workspace_bytes(B, packed.X, D, k)
+    if workspace is None:
+        ws = torch.empty(ws_n, dtype=torch.uint8, device=dev)
+    else:
+        if workspace.dtype != torch.uint8 or workspace.numel() < ws_n or workspace.device != dev:
+            raise ValueError(f"workspace must be a uint8 tensor of >= {ws_n} bytes on {dev}")
+        ws = workspace
     _lib.call("mips_topk", q.data_ptr(), packed.buf.data_ptr(), packed.X, D, _lib.ptr(ids),
               int(index_base), _lib.ptr(inv), N0, B, k, scores.data_ptr(), out_ids.data_ptr(),
               _lib.ptr(out_idx), ws.data_ptr(), ws_n, _lib.stream_handle())

@@ -144,3 +144,114 @@ def test_sharded_merge_equals_full():
     assert np.array_equal(x.cpu().numpy(), rx)
     assert np.array_equal(i.cpu().numpy(), ri)
     assert np.array_equal(s.cpu().numpy(), rs)
+
+
+# ---------------------------------------------------------------- large-catalog filter path
+# X >= 262,144 and D <= 64 take the sample -> tau -> filter -> merge path; its result must
+# be bit-identical to the oracle whether the fast path held (flag 0) or the exact
+# fallback ran (flag 1).  The flag is the first int32 of the workspace.
+
+def _gpu_flag(Q, E, ids, invalid, k, index_base=0):
+    from mygenerativerecommenders_amd.top_k import PackedItems, mips_topk, topk_workspace_bytes
+    dev = torch.device("cuda")
+    packed = PackedItems(torch.as_tensor(E).to(dev))
+    ws = torch.full((topk_workspace_bytes(Q.shape[0], E.shape[0], E.shape[1], k),), 7,
+                    dtype=torch.uint8, device=dev)
+    s, i, x = mips_topk(torch.as_tensor(Q).to(dev), packed, k,
+                        item_ids=None if ids is None else torch.as_tensor(ids).to(dev),
+                        invalid_ids=None if invalid is None else torch.as_tensor(invalid).to(dev),
+                        index_base=index_base, return_index=True, workspace=ws)
+    torch.cuda.synchronize()
+    flag = int(ws[:4].view(torch.int32).item())
+    return s.cpu().numpy(), i.cpu().numpy(), x.cpu().numpy(), flag
+
+
+def _check_filter(Q, E, ids, invalid, k, expect_flag):
+    s, i, x, flag = _gpu_flag(Q, E, ids, invalid, k)
+    rs, ri, rx = topk_oracle.mips_topk(Q, E, ids, invalid, k)
+    assert flag == expect_flag, f"fallback flag {flag}, expected {expect_flag}"
+    assert np.array_equal(x, rx), f"index mismatch rows {np.where((x != rx).any(1))[0][:8]}"
+    assert np.array_equal(i, ri)
+    assert np.array_equal(s.view(np.uint32), rs.view(np.uint32))
+
+
+def _normal_catalog(g, B, X, D, N0):
+    E = g.standard_normal((X, D), dtype=np.float32)
+    E /= np.linalg.norm(E, axis=1, keepdims=True)
+    Q = g.standard_normal((B, D), dtype=np.float32)
+    Q /= np.linalg.norm(Q, axis=1, keepdims=True)
+    inv = None
+    if N0:
+        inv = np.zeros((B, N0), np.int64)
+        for b in range(B):
+            n = g.integers(N0 // 2, N0 + 1)
+            inv[b, :n] = g.integers(1, X + 1, n)
+    return Q, E, inv
+
+
+@pytest.mark.parametrize("B,X,D,k,N0", [
+    (128, 600_001, 50, 200, 211),   # C4 shape per 16 shards-ish, ragged last block
+    (200, 300_000, 50, 200, 211),   # two query chunks (128 + 72)
+    (8, 262_144, 16, 100, 0),       # narrow chunk (NQG 2), no invalid ids
+    (64, 400_000, 64, 256, 256),    # D = 64, k = N0 = 256
+])
+def test_mips_filter_path_bitexact(B, X, D, k, N0):
+    g = np.random.default_rng(B + X + D)
+    Q, E, inv = _normal_catalog(g, B, X, D, N0)
+    _check_filter(Q, E, np.arange(1, X + 1, dtype=np.int64), inv, k, expect_flag=0)
+
+
+def test_mips_filter_path_explicit_ids():
+    g = np.random.default_rng(5)
+    B, X, D, k, N0 = 96, 300_000, 50, 200, 211
+    Q, E, _ = _normal_catalog(g, B, X, D, 0)
+    ids = g.permutation(np.arange(10, 10 + 3 * X, 3, dtype=np.int64))
+    # invalid ids drawn from each query's own top-500, so the exclusion really bites
+    sc = Q @ E.T
+    inv = np.zeros((B, N0), np.int64)
+    for b in range(B):
+        top = np.argpartition(-sc[b], 500)[:500]
+        inv[b, :200] = ids[g.choice(top, 200, replace=False)]
+    _check_filter(Q, E, ids, inv, k, expect_flag=0)
+
+
+def test_mips_filter_path_fallbacks():
+    """Inputs that defeat the sampled threshold must still give the exact answer through
+    the gated fallback: the best items all inside sampled blocks (too few candidates),
+    scores increasing with the index (list overflow), all-equal scores (overflow, ties
+    by index)."""
+    g = np.random.default_rng(3)
+    B, X, D, k = 32, 300_000, 16, 200
+    Q = np.abs(g.standard_normal((B, D), dtype=np.float32)) + 0.1
+    ids = np.arange(X, dtype=np.int64)
+    E = (0.01 * g.standard_normal((X, D))).astype(np.float32)
+    blk = np.arange(X) // 16
+    E[blk % 16 == 0] += 1.0  # every sampled block beats every other item
+    _check_filter(Q, E, ids, None, k, expect_flag=1)
+    base = np.linspace(0.0, 1.0, X, dtype=np.float32)[:, None]
+    _check_filter(Q, (base * np.ones((1, D), np.float32)).astype(np.float32), ids, None, k,
+                  expect_flag=1)
+    inv = np.tile(np.arange(0, 40, dtype=np.int64)[None, :], (B, 1))
+    _check_filter(Q, np.ones((X, D), np.float32), ids, inv, k, expect_flag=1)
+
+
+def test_sharded_merge_equals_full_filter_path():
+    """Two 300K-row shards through the filter path, then the cross-shard merge."""
+    from mygenerativerecommenders_amd.top_k import PackedItems, merge_topk, mips_topk
+    g = np.random.default_rng(12)
+    B, X, D, k, N0 = 128, 600_000, 50, 200, 211
+    Q, E, inv = _normal_catalog(g, B, X, D, N0)
+    ids = np.arange(1, X + 1, dtype=np.int64)
+    dev = torch.device("cuda")
+    parts = []
+    for a, b in ((0, 300_000), (300_000, X)):
+        pk = PackedItems(torch.tensor(E[a:b]).to(dev))
+        parts.append(mips_topk(torch.tensor(Q).to(dev), pk, k, item_ids=None,
+                               invalid_ids=torch.tensor(inv).to(dev), index_base=int(a) + 1,
+                               return_index=True))
+    s, i, x = merge_topk(torch.stack([p[0] for p in parts]), torch.stack([p[2] for p in parts]),
+                         torch.stack([p[1] for p in parts]), k, return_index=True)
+    rs, ri, rx = topk_oracle.mips_topk(Q, E, ids, inv, k)
+    assert np.array_equal(i.cpu().numpy(), ri)
+    assert np.array_equal(x.cpu().numpy() - 1, rx)
+    assert np.array_equal(s.cpu().numpy().view(np.uint32), rs.view(np.uint32))
