@@ -24,23 +24,23 @@
 namespace gr {
 
 #ifdef GR_STAMP
-// Diagnostic build only: per-wave phase cycle sums of the dK/dV kernel.
+// Diagnostic build only (-DGR_STAMP): per-wave phase cycle sums of the dK/dV kernel.
 __device__ unsigned long long gr_stamp_buf[1 << 16];
 __device__ __forceinline__ unsigned long long gr_stamp() {
-  unsigned long long t;
   __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  const unsigned long long t = __builtin_amdgcn_s_memtime();
   __builtin_amdgcn_sched_barrier(0);
   return t;
 }
-#define GR_ST(acc)                                \
-  do {                                            \
-    const unsigned long long t1_ = gr_stamp();    \
-    acc += t1_ - st_t0;                           \
-    st_t0 = t1_;                                  \
+#define GR_ST(acc, dep)                                \
+  do {                                                 \
+    asm volatile("" ::"v"(dep));                       \
+    const unsigned long long t1_ = gr_stamp();         \
+    acc += t1_ - st_t0;                                \
+    st_t0 = t1_;                                       \
   } while (0)
 #else
-#define GR_ST(acc) do { } while (0)
+#define GR_ST(acc, dep) do { } while (0)
 #endif
 
 struct AttnBwdArgs {
@@ -98,17 +98,15 @@ __device__ __forceinline__ float silu_grad_masked(const float* h, int64_t idx, b
 // gradients as LDS float adds into the wave's private histograms (dpos: one add per
 // element, <= 4-way address conflicts; dts: equal consecutive buckets of a lane merged
 // first), then dV += P^T dO and dK += dS^T Q (k-step r = queries 4g + r).
-#ifndef GR_DPOS_ROT
-#define GR_DPOS_ROT 1
-#endif
 #ifndef GR_DTS_COPIES
-#define GR_DTS_COPIES 16
+#define GR_DTS_COPIES 4
 #endif
 // dts_w histogram: GR_DTS_COPIES copies per wave (lane lr uses copy lr % copies) so
-// lanes hitting the same bucket mostly hit different addresses; stride == 1 mod 32.
+// lanes flushing the same bucket together mostly hit different addresses; stride == 1
+// mod 32.
 __host__ __device__ constexpr int dts_stride(int nb1) { return ((nb1 + 30) / 32) * 32 + 1; }
 
-template <int KSTEPS, int VTILES, int TT>
+template <int KSTEPS, int VTILES, int TT, bool HB>
 __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
   using C = AttnBwdCfg<KSTEPS, VTILES, TT>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -131,7 +129,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
   const int64_t s0 = a.offsets[b];
   const int L = (int)(a.offsets[b + 1] - s0);
   const int k0 = kt * 64;
-  const bool has_bias = a.map_kq != nullptr;
+  constexpr bool has_bias = HB;  // compile-time: the 4 bias gathers of a lane issue together
   float* slab = a.slabs ? a.slabs + (int64_t)id * nbins : nullptr;
   const int tid = threadIdx.x, w = wave_id(), lane = tid & 63;
   const int lr = lane & 15, lg = lane >> 4;
@@ -150,6 +148,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
   float* wts = whist + npos + (lr % GR_DTS_COPIES) * tss;
   float carry = 0.f;   // dpos: diagonal partial sums handed to the next block
   int last_db = 0;
+  // dts: a lane walks its key's queries in order, and the relative-time bucket of
+  // (query, key) is non-decreasing along that walk for time-ordered sequences, so the
+  // lane keeps a running (bucket, sum) and adds to the histogram only when the bucket
+  // changes (any order stays correct: every change flushes)
+  int run_b = -1;
+  float run_s = 0.f;
 
   // this lane's key (as the column of S and dP) and its K^T / V^T fragments
   const int kj = k0 + w * 16 + lr;
@@ -199,12 +203,13 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
 #ifdef GR_STAMP
   unsigned long long st_t0 = gr_stamp(), st_ld = 0, st_mm1 = 0, st_ew = 0, st_bias = 0,
                      st_mm2 = 0, st_sync = 0;
+  const unsigned long long st_begin = st_t0;
 #endif
   for (int qt = k0 / TT; qt <= last_qt; ++qt) {
     const int q0 = qt * TT;
     const bool more = qt < last_qt;
     if (more) load_tile(qt + 1, mwn);
-    GR_ST(st_ld);
+    GR_ST(st_ld, 0);
 #pragma unroll
     for (int qb = 0; qb < C::TB; ++qb) {
       const int qb0 = q0 + qb * 16;
@@ -213,74 +218,105 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
         f4 s = f4_zero(), dp = f4_zero();
         const float* qrow = Qs + (qb * 16 + lr) * C::LDQ + lg;
         const float* drow = Ds + (qb * 16 + lr) * C::LDV + lg;
+        // every LDS operand of the block is requested before the first MFMA (the
+        // chain then waits on in-order completions instead of one round trip per
+        // k-step); the bias terms are gathered in the same burst
+        float qa[KSTEPS], da[KSTEPS], bias[4];
+        int bk[4];
 #pragma unroll
         for (int st = 0; st < KSTEPS; ++st) {
-          s = mfma16x16x4(qrow[4 * st], kreg[st], s);
-          dp = mfma16x16x4(drow[4 * st], vreg[st], dp);
+          qa[st] = qrow[4 * st];
+          da[st] = drow[4 * st];
         }
-        GR_ST(st_mm1);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int qi = qb0 + 4 * lg + r;
+          int pi = a.N - 1 + kj - qi;
+          pi = pi < 0 ? 0 : (pi > npos - 1 ? npos - 1 : pi);
+          bk[r] = (mw[qb] >> (8 * r)) & 0xFF;
+          bias[r] = has_bias ? posw[pi] + tsw[bk[r]] : 0.f;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int st = 0; st < KSTEPS; ++st) {
+          s = mfma16x16x4(qa[st], kreg[st], s);
+          dp = mfma16x16x4(da[st], vreg[st], dp);
+        }
+        GR_ST(st_mm1, s[0] + dp[0]);
         float p[4], ds[4];
-        int bk[4];
+        bool okr[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int qi = qb0 + 4 * lg + r;
           const bool ok = k_ok && qi < L && kj <= qi;
+          okr[r] = ok;
           float x = s[r];
           int pi = a.N - 1 + kj - qi;
           pi = pi < 0 ? 0 : (pi > npos - 1 ? npos - 1 : pi);
-          bk[r] = (mw[qb] >> (8 * r)) & 0xFF;
-          if (has_bias) x = x + (posw[pi] + tsw[bk[r]]);
+          if (has_bias) x = x + bias[r];
           const float sg = sigmoidf_(x);
           p[r] = ok ? x * sg * a.inv_n : 0.f;
           ds[r] = ok ? dp[r] * (sg * (1.0f + x * (1.0f - sg))) * a.inv_n : 0.f;
-#if !GR_DPOS_ROT
-          if (has_bias) atomicAdd(&whist[pi], ds[r]);  // dpos_w (masked: adds 0)
+#ifdef GR_STAMP
+          if (r == 3) GR_ST(st_ew, ds[0] + ds[1] + ds[2] + ds[3] + p[0] + p[1] + p[2] + p[3]);
 #endif
         }
-        GR_ST(st_ew);
-#if GR_DPOS_ROT
-        if (has_bias) {
-          // dpos_w: element (query 4lg + r, key lr) has diagonal e = lr - (4lg + r).
-          // Rotating row 4lg + r left by its index inside the 16-lane group puts the
-          // diagonals e = lr (main) and e = lr - 16 (wrapped) in lane lr; sum over r
-          // and the 4 lane groups, add the main part plus the previous block's wrapped
-          // part (same bins: the next block sits 16 queries later) to the histogram.
-          float dA = 0.f, dB = 0.f;
+        // Relative-bias gradients.  dpos_w: element (query 4lg + r, key lr) has diagonal
+        // e = lr - (4lg + r); rotating row 4lg + r left by its index inside the 16-lane
+        // group puts the diagonals e = lr (main) and e = lr - 16 (wrapped) in lane lr;
+        // they are summed over r and the 4 lane groups, and the main part plus the
+        // previous block's wrapped part (same bins: the next block sits 16 queries
+        // later) is added to the wave's histogram.  dts_w: equal consecutive buckets of
+        // a lane are merged, then added.  The histograms are private to the wave, so the
+        // LDS adds land in program order (deterministic).
+        const int db = wk_lo - qb0;
+        float rot[4], dA = 0.f, dB = 0.f;
+        auto bias_stage = [&](int stage) {
+          if (!has_bias) return;
+          if (stage == 0) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int ql = 4 * lg + r;
-            const float v = __shfl(ds[r], (lg << 4) | ((lr + ql) & 15), 64);
-            const bool main = lr + ql < 16;
-            dA += main ? v : 0.f;
-            dB += main ? 0.f : v;
-          }
-          dA += __shfl_xor(dA, 16, 64);
-          dA += __shfl_xor(dA, 32, 64);
-          dB += __shfl_xor(dB, 16, 64);
-          dB += __shfl_xor(dB, 32, 64);
-          const int db = wk_lo - qb0;
-          int bin = a.N - 1 + db + lr;
-          bin = bin > npos - 1 ? npos - 1 : bin;
-          if (lg == 0) whist[bin] += dA + carry;
-          carry = dB;
-          last_db = db;
-        }
-#endif
-        if (has_bias) {  // dts_w: merge equal consecutive buckets of this lane, then add
-          float run = ds[0];
+            for (int r = 0; r < 4; ++r)
+              rot[r] = __shfl(ds[r], (lg << 4) | ((lr + 4 * lg + r) & 15), 64);
+          } else if (stage == 1) {
 #pragma unroll
-          for (int r = 1; r < 4; ++r) {
-            const bool same = bk[r] == bk[r - 1];
-            atomicAdd(&wts[bk[r - 1]], same ? 0.f : run);
-            run = same ? run + ds[r] : ds[r];
+            for (int r = 0; r < 4; ++r) {
+              const bool main = lr + 4 * lg + r < 16;
+              dA += main ? rot[r] : 0.f;
+              dB += main ? 0.f : rot[r];
+            }
+            // sums over the lane groups: rows xor 1 (permlane16 swap), halves (permlane32)
+            auto ta = __builtin_amdgcn_permlane16_swap(__float_as_uint(dA), __float_as_uint(dA), false, false);
+            auto tb = __builtin_amdgcn_permlane16_swap(__float_as_uint(dB), __float_as_uint(dB), false, false);
+            dA = __uint_as_float(ta[0]) + __uint_as_float(ta[1]);
+            dB = __uint_as_float(tb[0]) + __uint_as_float(tb[1]);
+            auto ua = __builtin_amdgcn_permlane32_swap(__float_as_uint(dA), __float_as_uint(dA), false, false);
+            auto ub = __builtin_amdgcn_permlane32_swap(__float_as_uint(dB), __float_as_uint(dB), false, false);
+            dA = __uint_as_float(ua[0]) + __uint_as_float(ua[1]);
+            dB = __uint_as_float(ub[0]) + __uint_as_float(ub[1]);
+          } else if (stage == 2) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              if (okr[r] && bk[r] != run_b) {  // rare: the bucket changed
+                if (run_b >= 0) atomicAdd(&wts[run_b], run_s);
+                run_b = bk[r];
+                run_s = 0.f;
+              }
+              run_s += ds[r];
+            }
+          } else {
+            int bin = a.N - 1 + db + lr;
+            bin = bin > npos - 1 ? npos - 1 : bin;
+            if (lg == 0) atomicAdd(&whist[bin], dA + carry);
+            carry = dB;
+            last_db = db;
           }
-          atomicAdd(&wts[bk[3]], run);
-        }
-        GR_ST(st_bias);
+        };
         // dV[key][c] += P^T dO ; dK[key][d] += dS^T Q   (k-step r: queries 4g + r)
         const float* dcol = Ds + (qb * 16 + 4 * lg) * C::LDV + lr;
         const float* qcol = Qs + (qb * 16 + 4 * lg) * C::LDQ + lr;
         if constexpr (VTILES + C::KT > 8) {  // wide heads: no registers to spare
+#pragma unroll
+          for (int stage = 0; stage < 4; ++stage) bias_stage(stage);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
 #pragma unroll
@@ -291,7 +327,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
               dK[t] = mfma16x16x4(ds[r], qcol[r * C::LDQ + t * 16], dK[t]);
           }
         } else {
-        // B operands of k-step r+1 are read from LDS while the MFMAs of step r run
+        // B operands of k-step r+1 are read from LDS while the MFMAs of step r run, and
+        // bias stage r (shuffles / LDS adds: latency, little issue) is issued between
+        // the MFMA groups so it runs under them
         float bvv[2][VTILES], bvk[2][C::KT];
 #pragma unroll
         for (int t = 0; t < VTILES; ++t) bvv[0][t] = dcol[t * 16];
@@ -305,6 +343,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
 #pragma unroll
             for (int t = 0; t < C::KT; ++t) bvk[(r + 1) & 1][t] = qcol[(r + 1) * C::LDQ + t * 16];
           }
+          bias_stage(r);
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int t = 0; t < VTILES; ++t) dV[t] = mfma16x16x4(p[r], bvv[r & 1][t], dV[t]);
@@ -313,7 +352,11 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
           __builtin_amdgcn_sched_barrier(0);
         }
         }
-        GR_ST(st_mm2);
+        GR_ST(st_mm2, dV[0][0] + dK[0][0] + dV[VTILES - 1][3] + dK[C::KT - 1][3]);
+#ifdef GR_STAMP
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        GR_ST(st_bias, 0);
+#endif
       }
     }
     if (more) {
@@ -324,7 +367,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
       for (int qb = 0; qb < C::TB; ++qb) mw[qb] = mwn[qb];
       lds_barrier();
     }
-    GR_ST(st_sync);
+    GR_ST(st_sync, 0);
   }
 #ifdef GR_STAMP
   if (lane == 0) {
@@ -337,11 +380,10 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
       gr_stamp_buf[slot + 4] = st_mm2;
       gr_stamp_buf[slot + 5] = st_sync;
       gr_stamp_buf[slot + 6] = (unsigned long long)kt;
-      gr_stamp_buf[slot + 7] = 1;
+      gr_stamp_buf[slot + 7] = gr_stamp() - st_begin;
     }
   }
 #endif
-
   // ---- epilogue: rows = keys wk_lo + 4lg + r, cols = lr + 16 t
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -365,12 +407,11 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
       if (ok) a.dk[row * a.ld_d + h * a.dqk + c] = g;
     }
   }
-#if GR_DPOS_ROT
   if (has_bias && lg == 0) {  // the last block's wrapped diagonals
     const int bin = a.N - 1 + last_db - 16 + lr;
     if (bin >= 0 && bin < npos) whist[bin] += carry;
   }
-#endif
+  if (has_bias && run_b >= 0) atomicAdd(&wts[run_b], run_s);  // the open dts run
   if (has_bias && slab) {
     __syncthreads();
     for (int i = tid; i < npos; i += 256)
@@ -385,7 +426,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
 }
 
 // ------------------------------------------------------------------ query-major: dQ
-template <int KSTEPS, int VTILES, int TT>
+template <int KSTEPS, int VTILES, int TT, bool HB>
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   using C = AttnBwdCfg<KSTEPS, VTILES, TT>;
   constexpr int LDK = C::LDQ;
@@ -408,7 +449,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   if (q0 >= L) return;
   const int tid = threadIdx.x, w = wave_id(), lane = tid & 63;
   const int lr = lane & 15, lg = lane >> 4;
-  const bool has_bias = a.map_qk != nullptr;
+  constexpr bool has_bias = HB;
   if (has_bias) {
     for (int i = tid; i <= a.nb; i += 256) tsw[i] = a.ts_w[i];
     for (int i = tid; i < 2 * a.N - 1; i += 256) posw[i] = a.pos_w[i];
@@ -586,9 +627,17 @@ static int launch_bwd(const AttnBwdArgs& a, float* dpos_w, float* dts_w, hipStre
   const size_t lds_q = sizeof(float) * (TT * C::LDQ + TT * LDV_Q) + tail;
   GR_REQUIRE(lds_kv <= 160 * 1024 && lds_q <= 160 * 1024,
              "hstu_attn_bwd: LDS (%zu, %zu B) exceeds 160 KiB (N=%d)", lds_kv, lds_q, a.N);
-  GR_TIMED("attn_bwd_dkv", st, hipLaunchKernelGGL((attn_bwd_dkv_kernel<KS, VT, TT>), dim3(grid), dim3(256), lds_kv, st, a));
+  if (a.map_kq) {
+    GR_TIMED("attn_bwd_dkv", st, hipLaunchKernelGGL((attn_bwd_dkv_kernel<KS, VT, TT, true>), dim3(grid), dim3(256), lds_kv, st, a));
+  } else {
+    GR_TIMED("attn_bwd_dkv", st, hipLaunchKernelGGL((attn_bwd_dkv_kernel<KS, VT, TT, false>), dim3(grid), dim3(256), lds_kv, st, a));
+  }
   GR_LAUNCH_CHECK("hstu_attn_bwd(dkv)");
-  GR_TIMED("attn_bwd_dq", st, hipLaunchKernelGGL((attn_bwd_dq_kernel<KS, VT, TT>), dim3(grid), dim3(256), lds_q, st, a));
+  if (a.map_qk) {
+    GR_TIMED("attn_bwd_dq", st, hipLaunchKernelGGL((attn_bwd_dq_kernel<KS, VT, TT, true>), dim3(grid), dim3(256), lds_q, st, a));
+  } else {
+    GR_TIMED("attn_bwd_dq", st, hipLaunchKernelGGL((attn_bwd_dq_kernel<KS, VT, TT, false>), dim3(grid), dim3(256), lds_q, st, a));
+  }
   GR_LAUNCH_CHECK("hstu_attn_bwd(dq)");
   if (a.map_kq) {
     GR_TIMED("attn_bias_reduce", st, hipLaunchKernelGGL(bias_grad_reduce_kernel, dim3(ceil_div(nbins, 16)), dim3(256), 0, st,

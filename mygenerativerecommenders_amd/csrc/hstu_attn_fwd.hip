@@ -51,7 +51,7 @@ struct AttnFwdCfg {
   static constexpr int KB = TK / 16;                         // 16-key blocks per tile
 };
 
-template <int KSTEPS, int VTILES, int TK>
+template <int KSTEPS, int VTILES, int TK, bool HB>
 __global__ __launch_bounds__(256) void hstu_attn_fwd_kernel(AttnFwdArgs a) {
   using C = AttnFwdCfg<KSTEPS, VTILES, TK>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -73,7 +73,7 @@ __global__ __launch_bounds__(256) void hstu_attn_fwd_kernel(AttnFwdArgs a) {
 
   const int tid = threadIdx.x, w = wave_id(), lane = tid & 63;
   const int lr = lane & 15, lg = lane >> 4;
-  const bool has_bias = a.map_qk != nullptr;
+  constexpr bool has_bias = HB;  // compile-time: the bias gathers of a lane issue together
 
   if (has_bias) {
     for (int i = tid; i <= a.nb; i += 256) tsw[i] = a.ts_w[i];
@@ -183,7 +183,11 @@ static int launch_fwd(const AttnFwdArgs& a, int grid, hipStream_t st) {
   using C = AttnFwdCfg<KS, VT, TK>;
   size_t lds = sizeof(float) * (C::LDS_FLOATS + a.nb + 1 + 2 * a.N - 1);
   GR_REQUIRE(lds <= 160 * 1024, "hstu_attn_fwd: LDS %zu B exceeds 160 KiB (N=%d)", lds, a.N);
-  GR_TIMED("attn_fwd", st, hipLaunchKernelGGL((hstu_attn_fwd_kernel<KS, VT, TK>), dim3(grid), dim3(256), lds, st, a));
+  if (a.map_qk) {
+    GR_TIMED("attn_fwd", st, hipLaunchKernelGGL((hstu_attn_fwd_kernel<KS, VT, TK, true>), dim3(grid), dim3(256), lds, st, a));
+  } else {
+    GR_TIMED("attn_fwd", st, hipLaunchKernelGGL((hstu_attn_fwd_kernel<KS, VT, TK, false>), dim3(grid), dim3(256), lds, st, a));
+  }
   GR_LAUNCH_CHECK("hstu_attn_fwd");
   return 0;
 }

@@ -18,6 +18,9 @@ SHAPES = {
     # B, N (padded), L (all sequences), d, H
     "c2": (128, 211, 200, 50, 1),
     "c3": (32, 2059, 2048, 256, 1),
+    "c2b64": (64, 211, 200, 50, 1),
+    "c2b32": (32, 211, 200, 50, 1),
+    "c2b256": (256, 211, 200, 50, 1),
 }
 
 
@@ -31,8 +34,15 @@ def main():
     ap.add_argument("--shape", default="c2", choices=sorted(SHAPES))
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--only", default="", help="fwd|bwd")
+    ap.add_argument("--batch", type=int, default=0, help="override B")
+    ap.add_argument("--len", type=int, default=0, help="override L (N = L + 11)")
+    ap.add_argument("--nobias", action="store_true", help="no relative bias (timestamps absent)")
     args = ap.parse_args()
     B, N, L, d, H = SHAPES[args.shape]
+    if args.batch:
+        B = args.batch
+    if args.len:
+        L, N = args.len, args.len + 11
     dev = torch.device("cuda")
     g = torch.Generator(device=dev)
     g.manual_seed(0)
@@ -58,14 +68,17 @@ def main():
     ws = torch.empty(max(ws_n, 4), dtype=torch.uint8, device=dev)
     st = _lib.stream_handle()
 
+    if args.nobias:
+        bmap = None
+
     def fwd():
         _lib.call("hstu_attn_fwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out, n_out,
-                  offsets.data_ptr(), B, N, L, H, d, d, bmap.data_ptr(), pos_w.data_ptr(),
+                  offsets.data_ptr(), B, N, L, H, d, d, _lib.ptr(bmap), pos_w.data_ptr(),
                   ts_w.data_ptr(), 128, out.data_ptr(), hv, st)
 
     def bwd():
         _lib.call("hstu_attn_bwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out, n_out,
-                  dout.data_ptr(), hv, offsets.data_ptr(), B, N, L, H, d, d, bmap.data_ptr(),
+                  dout.data_ptr(), hv, offsets.data_ptr(), B, N, L, H, d, d, _lib.ptr(bmap),
                   pos_w.data_ptr(), ts_w.data_ptr(), 128, None, None, None, 0,
                   dq.data_ptr(), dk.data_ptr(), dvv.data_ptr(), n_out, dpw.data_ptr(),
                   dtw.data_ptr(), ws.data_ptr(), ws_n, st)
