@@ -357,6 +357,11 @@ def main():
         kmerge = rt["mips_merge"][0] / max(1, rt["mips_merge"][1])
         rsteps = max(1, args.retrieval_steps)
         r_dev = {n: round(v[0] / rsteps, 4) for n, v in rt.items() if v[1] and n != "mips_pack"}
+        r_traffic = None
+        if os.path.exists(pmc_path):
+            ent = json.load(open(pmc_path)).get("kernels", {}).get(rkern)
+            if ent:
+                r_traffic = ent["hbm_bytes_per_launch"]
         dtr = _max_over_ranks(dtr, world)
         cand_per_s = B * X * args.retrieval_steps / dtr
         fl = 2.0 * B * (b - a) * D
@@ -371,7 +376,9 @@ def main():
             "roofline": {"kernel": rkern, "bound": "mfma",
                          "achieved": round(ach_r, 3), "peak": peaks["fp32_mfma_tflops"],
                          "unit": "TFLOP/s", "frac": round(ach_r / peaks["fp32_mfma_tflops"], 4),
-                         "traffic": None, "avg_launch_ms": round(ktop, 4),
+                         "traffic": r_traffic, "traffic_source": traffic_src,
+                         "algorithmic_bytes": 4.0 * (b - a) * 8 * ((D + 7) // 8),
+                         "avg_launch_ms": round(ktop, 4),
                          "merge_avg_launch_ms": round(kmerge, 4),
                          "flops_per_launch": fl},
         }

@@ -38,6 +38,10 @@ _MAP = [
     (r"wgrad_reduce_kernel", "wgrad_reduce"),
     (r"mips_pack_kernel", "mips_pack"),
     (r"mips_select_kernel|mips_scoreall_kernel", "mips_select"),
+    (r"mips_filter_merge_kernel", "mips_merge"),
+    (r"mips_filter_kernel<[^>]*true>", "mips_sample"),
+    (r"mips_filter_kernel<[^>]*false>", "mips_filter"),
+    (r"mips_tau_kernel", "mips_tau"),
     (r"mips_merge_kernel", "mips_merge"),
     (r"cumsum_kernel", "cumsum"),
     (r"dense_to_jagged_kernel", "dense_to_jagged"),
