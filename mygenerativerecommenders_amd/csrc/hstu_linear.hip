@@ -96,16 +96,23 @@ __device__ __forceinline__ void panel_row_stats(const float* base, int64_t ld, i
 // transformed (LayerNorm, gating, dropout) when they are written to LDS.
 //   Op: a_rsrc0/1(m0, total), a_ld0/1(), NSRC, a_xform(v0, v1, m, k, stats, valid),
 //       w, bks(), bns()  (W'(k, n) = w[k * bks + n * bns]), prologue, epilogue.
-template <int NT, class Op>
+template <int NT, int BKT, class Op>
 __global__ __launch_bounds__(256) void rowpanel_kernel(Op op) {
+  // BKT = K chunk per LDS stage: 16, or 64 when K is small enough for one or a few
+  // chunks (ml-1m: K = 50 in one stage, K = 200 in 4) so the next chunk's global loads
+  // are not exposed once per 16 columns of K
   using P = PanelCfg<NT>;
+  constexpr int LDAT = BKT == 16 ? LDA : BKT + 4;  // 64-bank LDS: BKT + 4 == 4 mod 64
   constexpr int NP2 = P::BN <= 16 ? 16 : P::BN <= 32 ? 32 : P::BN <= 64 ? 64 : P::BN <= 128 ? 128 : 256;
   // B staging walks the memory-contiguous index fastest: n for row-major W' (RPB k-rows
-  // per pass), k for transposed W' (16 k per column, 16 columns per pass)
+  // per pass), k for transposed W' (BKT k per column, CPP columns per pass)
   constexpr int RPB = 256 / NP2;
-  constexpr int NB = Op::B_N_CONTIG ? BK / RPB : NT;
-  __shared__ __attribute__((aligned(16))) float As[BM * LDA];
-  __shared__ __attribute__((aligned(16))) float Bs[BK * P::LDB];
+  constexpr int CPP = 256 / BKT;
+  constexpr int NB = Op::B_N_CONTIG ? (BKT + RPB - 1) / RPB : (P::BN + CPP - 1) / CPP;
+  constexpr int RPA = 256 / BKT;  // A rows per pass
+  constexpr int NA = BM / RPA;
+  __shared__ __attribute__((aligned(16))) float As[BM * LDAT];
+  __shared__ __attribute__((aligned(16))) float Bs[BKT * P::LDB];
   __shared__ float2 stats[BM];
   const int64_t total = op.offsets[op.B];
   const int64_t m0 = (int64_t)blockIdx.x * BM;
@@ -120,53 +127,55 @@ __global__ __launch_bounds__(256) void rowpanel_kernel(Op op) {
   const __amdgpu_buffer_rsrc_t ra0 = op.a_rsrc0(m0, total);
   const __amdgpu_buffer_rsrc_t ra1 = op.a_rsrc1(m0, total);
   const int ld0 = (int)op.a_ld0(), ld1 = (int)op.a_ld1();
-  const int a_c = tid & 15, a_r = tid >> 4;  // A: column k0 + a_c of rows a_r + 16 i
+  const int a_c = tid % BKT, a_r = tid / BKT;  // A: column k0 + a_c of rows a_r + RPA i
   const int va0 = (a_r * ld0 + a_c) * 4, va1 = (a_r * ld1 + a_c) * 4;
   const __amdgpu_buffer_rsrc_t rw =
       __builtin_amdgcn_make_buffer_rsrc((void*)op.w, 0, op.K * op.N * 4, 0x00020000);
   const int bks = op.bks(), bns = op.bns();
-  const int b_c = Op::B_N_CONTIG ? tid % NP2 : tid >> 4;  // B: column n0 + b_c (+16 i)
-  const int b_r = Op::B_N_CONTIG ? tid / NP2 : tid & 15;   // of k-row b_r (+RPB i)
+  const int b_c = Op::B_N_CONTIG ? tid % NP2 : tid / BKT;  // B: column n0 + b_c (+CPP i)
+  const int b_r = Op::B_N_CONTIG ? tid / NP2 : tid % BKT;  // of k-row b_r (+RPB i)
   const bool b_col = Op::B_N_CONTIG ? (b_c < P::BN && n0 + b_c < op.N) : true;
   const int vb = b_col ? (b_r * bks + (n0 + b_c) * bns) * 4 : 0x40000000;
 
-  float ra[4], ra2[Op::NSRC == 2 ? 4 : 1], rb[NB];
+  float ra[NA], ra2[Op::NSRC == 2 ? NA : 1], rb[NB];
   auto load = [&](int k0) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      ra[i] = buf_ld(ra0, va0 + k0 * 4, i * 16 * ld0 * 4);
-      if constexpr (Op::NSRC == 2) ra2[i] = buf_ld(ra1, va1 + k0 * 4, i * 16 * ld1 * 4);
+    for (int i = 0; i < NA; ++i) {
+      ra[i] = buf_ld(ra0, va0 + k0 * 4, i * RPA * ld0 * 4);
+      if constexpr (Op::NSRC == 2) ra2[i] = buf_ld(ra1, va1 + k0 * 4, i * RPA * ld1 * 4);
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       if constexpr (Op::B_N_CONTIG)
         rb[i] = buf_ld(rw, vb, (k0 + RPB * i) * bks * 4);
       else
-        rb[i] = buf_ld(rw, vb, (k0 * bks + 16 * i * bns) * 4);
+        rb[i] = buf_ld(rw, vb, (k0 * bks + CPP * i * bns) * 4);
     }
   };
   auto store = [&](int k0) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = a_r + 16 * i, k = k0 + a_c;
+    for (int i = 0; i < NA; ++i) {
+      const int r = a_r + RPA * i, k = k0 + a_c;
       const bool ok = m0 + r < total && k < op.K;
       const float v = op.a_xform(ra[i], Op::NSRC == 2 ? ra2[Op::NSRC == 2 ? i : 0] : 0.f, m0 + r, k,
                                  stats[r], ok);
-      As[r * LDA + a_c] = ok ? v : 0.f;
+      As[r * LDAT + a_c] = ok ? v : 0.f;
     }
     if constexpr (Op::B_N_CONTIG) {
       if (b_c < P::BN) {
 #pragma unroll
         for (int i = 0; i < NB; ++i) {
           const int kk = b_r + RPB * i;
-          Bs[kk * P::LDB + b_c] = (b_col && k0 + kk < op.K) ? rb[i] : 0.f;
+          if (RPB * NB == BKT || kk < BKT)
+            Bs[kk * P::LDB + b_c] = (b_col && k0 + kk < op.K) ? rb[i] : 0.f;
         }
       }
     } else {
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
-        const int c = b_c + 16 * i;
-        Bs[b_r * P::LDB + c] = (n0 + c < op.N && k0 + b_r < op.K) ? rb[i] : 0.f;
+        const int c = b_c + CPP * i;
+        if (CPP * NB == P::BN || c < P::BN)
+          Bs[b_r * P::LDB + c] = (n0 + c < op.N && k0 + b_r < op.K) ? rb[i] : 0.f;
       }
     }
   };
@@ -178,31 +187,35 @@ __global__ __launch_bounds__(256) void rowpanel_kernel(Op op) {
   load(0);
   store(0);
   lds_barrier();
-  for (int k0 = 0; k0 < op.K; k0 += BK) {
-    const bool more = k0 + BK < op.K;
-    if (more) load(k0 + BK);
-    const float* arow = As + (w * 16 + lr) * LDA + lg;
-    // operands of k-step ks+1 read from LDS while the MFMAs of step ks run
+  for (int k0 = 0; k0 < op.K; k0 += BKT) {
+    const bool more = k0 + BKT < op.K;
+    if (more) load(k0 + BKT);
+    const float* arow = As + (w * 16 + lr) * LDAT + lg;
+    // operands of k-step ks+1 read from LDS while the MFMAs of step ks run; steps past
+    // K (zero padding) are skipped when the whole K fits one stage
+    const int ksn = more || BKT == 16 ? BKT / 4 : (op.K - k0 + 3) / 4;
     float av[2], bv[2][NT];
     av[0] = arow[0];
 #pragma unroll
     for (int t = 0; t < NT; ++t) bv[0][t] = Bs[lg * P::LDB + lr + t * 16];
 #pragma unroll
-    for (int ks = 0; ks < BK / 4; ++ks) {
-      if (ks + 1 < BK / 4) {
-        av[(ks + 1) & 1] = arow[4 * (ks + 1)];
-        const float* brow = Bs + (4 * (ks + 1) + lg) * P::LDB + lr;
+    for (int ks = 0; ks < BKT / 4; ++ks) {
+      if (ks < ksn) {
+        if (ks + 1 < BKT / 4) {
+          av[(ks + 1) & 1] = arow[4 * (ks + 1)];
+          const float* brow = Bs + (4 * (ks + 1) + lg) * P::LDB + lr;
 #pragma unroll
-        for (int t = 0; t < NT; ++t) bv[(ks + 1) & 1][t] = brow[t * 16];
+          for (int t = 0; t < NT; ++t) bv[(ks + 1) & 1][t] = brow[t * 16];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = mfma16x16x4(av[ks & 1], bv[ks & 1][t], acc[t]);
+        __builtin_amdgcn_sched_barrier(0);
       }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int t = 0; t < NT; ++t) acc[t] = mfma16x16x4(av[ks & 1], bv[ks & 1][t], acc[t]);
-      __builtin_amdgcn_sched_barrier(0);
     }
     lds_barrier();
     if (more) {
-      store(k0 + BK);
+      store(k0 + BKT);
       lds_barrier();
     }
   }
@@ -499,16 +512,30 @@ static int launch_rowpanel(const Op& op, int64_t max_rows, bool full_row, const 
   dim3 grid((unsigned)((max_rows + BM - 1) / BM), (unsigned)panels);
   if (grid.x == 0) return 0;
   const char* tname = name + 5;  // "hstu_ln_uvqk_fwd" -> "ln_uvqk_fwd"
-#define GR_NT_CASE(NT_)                                                                     \
-  case NT_:                                                                                 \
-    GR_TIMED(tname, st, hipLaunchKernelGGL((rowpanel_kernel<NT_, Op>), grid, dim3(256), 0,  \
-                                           st, op));                                        \
+  // one 64-wide K stage when all of K fits it (ml-1m forward, K = 50: no K streaming,
+  // padding k-steps skipped); measured slower for streamed K (the backward's K = 200:
+  // 18.6 -> 27 us), so longer K keeps the 16-wide stages
+  const bool wide_k = op.K > 16 && op.K <= 64 && nt <= 13;
+#define GR_NT_CASE(NT_, BKT_)                                                                \
+  case NT_:                                                                                  \
+    GR_TIMED(tname, st, hipLaunchKernelGGL((rowpanel_kernel<NT_, BKT_, Op>), grid, dim3(256), 0, \
+                                           st, op));                                         \
     break;
-  switch (nt) {
-    GR_NT_CASE(1) GR_NT_CASE(2) GR_NT_CASE(3) GR_NT_CASE(4) GR_NT_CASE(5) GR_NT_CASE(6)
-    GR_NT_CASE(7) GR_NT_CASE(8) GR_NT_CASE(9) GR_NT_CASE(10) GR_NT_CASE(11) GR_NT_CASE(12)
-    GR_NT_CASE(13) GR_NT_CASE(14) GR_NT_CASE(15) GR_NT_CASE(16)
-    default: GR_REQUIRE(false, "%s: bad panel width", name);
+  if (wide_k) {
+    switch (nt) {
+      GR_NT_CASE(1, 64) GR_NT_CASE(2, 64) GR_NT_CASE(3, 64) GR_NT_CASE(4, 64) GR_NT_CASE(5, 64)
+      GR_NT_CASE(6, 64) GR_NT_CASE(7, 64) GR_NT_CASE(8, 64) GR_NT_CASE(9, 64) GR_NT_CASE(10, 64)
+      GR_NT_CASE(11, 64) GR_NT_CASE(12, 64) GR_NT_CASE(13, 64)
+      default: GR_REQUIRE(false, "%s: bad panel width", name);
+    }
+  } else {
+    switch (nt) {
+      GR_NT_CASE(1, 16) GR_NT_CASE(2, 16) GR_NT_CASE(3, 16) GR_NT_CASE(4, 16) GR_NT_CASE(5, 16)
+      GR_NT_CASE(6, 16) GR_NT_CASE(7, 16) GR_NT_CASE(8, 16) GR_NT_CASE(9, 16) GR_NT_CASE(10, 16)
+      GR_NT_CASE(11, 16) GR_NT_CASE(12, 16) GR_NT_CASE(13, 16) GR_NT_CASE(14, 16)
+      GR_NT_CASE(15, 16) GR_NT_CASE(16, 16)
+      default: GR_REQUIRE(false, "%s: bad panel width", name);
+    }
   }
 #undef GR_NT_CASE
   GR_LAUNCH_CHECK(name);
