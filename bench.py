@@ -291,7 +291,7 @@ def main():
     rows = B * N0
     nout = 4 * D
     flops_per_launch = {
-        "attn_fwd": fwd_f, "attn_bwd_dkv": dkv_f, "attn_bwd_dq": dq_f,
+        "attn_fwd": fwd_f, "attn_bwd_dkv": dkv_f, "attn_bwd_dq": dq_f, "attn_bwd": dkv_f + dq_f,
         "ln_uvqk_fwd": 2.0 * rows * D * nout, "gate_o_fwd": 2.0 * rows * D * D,
         "gate_o_bwd": 2.0 * rows * D * D, "ln_uvqk_bwd": 2.0 * rows * nout * D,
         "wgrad_partial": (2.0 * rows * D * D + 2.0 * rows * D * nout) / 2.0,

@@ -107,7 +107,7 @@ __device__ __forceinline__ float silu_grad_masked(const float* h, int64_t idx, b
 __host__ __device__ constexpr int dts_stride(int nb1) { return ((nb1 + 30) / 32) * 32 + 1; }
 
 template <int KSTEPS, int VTILES, int TT, bool HB>
-__global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
+__device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const int id) {
   using C = AttnBwdCfg<KSTEPS, VTILES, TT>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* Qs = reinterpret_cast<float*>(smem);  // [TT][LDQ]
@@ -121,7 +121,6 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
   float* hist = posw + npos;                   // [4 waves][wbins]
 
   const int BH = a.B * a.H;
-  const int id = blockIdx.x;
   const int rank = snake_rank(id, a.cus);
   const int kt = rank / BH;  // kt = 0 (the most query tiles) first
   const int bh = rank % BH;
@@ -371,7 +370,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
   }
 #ifdef GR_STAMP
   if (lane == 0) {
-    const int slot = (blockIdx.x * 4 + w) * 8;
+    const int slot = (id * 4 + w) * 8;
     if (slot + 8 <= (1 << 16)) {
       gr_stamp_buf[slot + 0] = st_ld;
       gr_stamp_buf[slot + 1] = st_mm1;
@@ -427,7 +426,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
 
 // ------------------------------------------------------------------ query-major: dQ
 template <int KSTEPS, int VTILES, int TT, bool HB>
-__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
+__device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& a, const int id) {
   using C = AttnBwdCfg<KSTEPS, VTILES, TT>;
   constexpr int LDK = C::LDQ;
   constexpr int LDV = 32 * ((C::VP - 2 + 31) / 32) + 2;  // A-operand reads only
@@ -438,7 +437,6 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   float* posw = tsw + (a.nb + 1);
 
   const int BH = a.B * a.H;
-  const int id = blockIdx.x;
   const int rank = snake_rank(id, a.cus);
   const int qt = a.n_tiles - 1 - rank / BH;
   const int bh = rank % BH;
@@ -577,6 +575,30 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   }
 }
 
+// ------------------------------------------------------------------ entry points
+template <int KSTEPS, int VTILES, int TT, bool HB>
+__global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
+  attn_bwd_dkv_body<KSTEPS, VTILES, TT, HB>(a, blockIdx.x);
+}
+template <int KSTEPS, int VTILES, int TT, bool HB>
+__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
+  attn_bwd_dq_body<KSTEPS, VTILES, TT, HB>(a, blockIdx.x);
+}
+// dK/dV and dQ in ONE launch: workgroups [0, grid) run the key-major pass (heaviest key
+// tiles first), the next grid run the query-major pass.  At narrow heads both are bound
+// by their heavy workgroups' chains of blocks with the CUs half idle, so the dQ
+// workgroups fill the slots the light dK/dV workgroups free (a horizontal fusion: one
+// dispatch, no stream fork/join).
+// (Interleaving the two passes' workgroups measured slower: 72 vs 62 us at C2.)
+template <int KSTEPS, int VTILES, int TT, bool HB>
+__global__ __launch_bounds__(256) void attn_bwd_fused_kernel(AttnBwdArgs a, int grid_kv) {
+  const int id = blockIdx.x;
+  if (id < grid_kv)
+    attn_bwd_dkv_body<KSTEPS, VTILES, TT, HB>(a, id);
+  else
+    attn_bwd_dq_body<KSTEPS, VTILES, TT, HB>(a, id - grid_kv);
+}
+
 // ------------------------------------------------------------------ slab reduce
 // Deterministic: a workgroup owns 16 bins; thread (bin, g) sums slabs g, g+16, ... in
 // order (loads 8-deep), then the 16 partials are added in g order.
@@ -627,18 +649,29 @@ static int launch_bwd(const AttnBwdArgs& a, float* dpos_w, float* dts_w, hipStre
   const size_t lds_q = sizeof(float) * (TT * C::LDQ + TT * LDV_Q) + tail;
   GR_REQUIRE(lds_kv <= 160 * 1024 && lds_q <= 160 * 1024,
              "hstu_attn_bwd: LDS (%zu, %zu B) exceeds 160 KiB (N=%d)", lds_kv, lds_q, a.N);
-  if (a.map_kq) {
-    GR_TIMED("attn_bwd_dkv", st, hipLaunchKernelGGL((attn_bwd_dkv_kernel<KS, VT, TT, true>), dim3(grid), dim3(256), lds_kv, st, a));
+  static const bool split = getenv("GR_ATTN_BWD_SPLIT") != nullptr;  // A/B knob
+  if (!split && C::KT <= 8) {
+    const size_t lds = lds_kv > lds_q ? lds_kv : lds_q;
+    if (a.map_kq) {
+      GR_TIMED("attn_bwd", st, hipLaunchKernelGGL((attn_bwd_fused_kernel<KS, VT, TT, true>), dim3(2 * grid), dim3(256), lds, st, a, grid));
+    } else {
+      GR_TIMED("attn_bwd", st, hipLaunchKernelGGL((attn_bwd_fused_kernel<KS, VT, TT, false>), dim3(2 * grid), dim3(256), lds, st, a, grid));
+    }
+    GR_LAUNCH_CHECK("hstu_attn_bwd(fused)");
   } else {
-    GR_TIMED("attn_bwd_dkv", st, hipLaunchKernelGGL((attn_bwd_dkv_kernel<KS, VT, TT, false>), dim3(grid), dim3(256), lds_kv, st, a));
+    if (a.map_kq) {
+      GR_TIMED("attn_bwd_dkv", st, hipLaunchKernelGGL((attn_bwd_dkv_kernel<KS, VT, TT, true>), dim3(grid), dim3(256), lds_kv, st, a));
+    } else {
+      GR_TIMED("attn_bwd_dkv", st, hipLaunchKernelGGL((attn_bwd_dkv_kernel<KS, VT, TT, false>), dim3(grid), dim3(256), lds_kv, st, a));
+    }
+    GR_LAUNCH_CHECK("hstu_attn_bwd(dkv)");
+    if (a.map_qk) {
+      GR_TIMED("attn_bwd_dq", st, hipLaunchKernelGGL((attn_bwd_dq_kernel<KS, VT, TT, true>), dim3(grid), dim3(256), lds_q, st, a));
+    } else {
+      GR_TIMED("attn_bwd_dq", st, hipLaunchKernelGGL((attn_bwd_dq_kernel<KS, VT, TT, false>), dim3(grid), dim3(256), lds_q, st, a));
+    }
+    GR_LAUNCH_CHECK("hstu_attn_bwd(dq)");
   }
-  GR_LAUNCH_CHECK("hstu_attn_bwd(dkv)");
-  if (a.map_qk) {
-    GR_TIMED("attn_bwd_dq", st, hipLaunchKernelGGL((attn_bwd_dq_kernel<KS, VT, TT, true>), dim3(grid), dim3(256), lds_q, st, a));
-  } else {
-    GR_TIMED("attn_bwd_dq", st, hipLaunchKernelGGL((attn_bwd_dq_kernel<KS, VT, TT, false>), dim3(grid), dim3(256), lds_q, st, a));
-  }
-  GR_LAUNCH_CHECK("hstu_attn_bwd(dq)");
   if (a.map_kq) {
     GR_TIMED("attn_bias_reduce", st, hipLaunchKernelGGL(bias_grad_reduce_kernel, dim3(ceil_div(nbins, 16)), dim3(256), 0, st,
                        a.slabs, grid, 2 * a.N - 1, a.nb + 1, dpos_w, dts_w));

@@ -26,7 +26,8 @@ SHAPES = {
 
 def flops(B, L, d, H):
     T = B * L * (L + 1) / 2 * H
-    return {"attn_fwd": 2 * T * 2 * d, "attn_bwd_dkv": 2 * T * 3 * d, "attn_bwd_dq": 2 * T * d}
+    return {"attn_fwd": 2 * T * 2 * d, "attn_bwd_dkv": 2 * T * 3 * d, "attn_bwd_dq": 2 * T * d,
+            "attn_bwd": 2 * T * 4 * d}
 
 
 def main():
@@ -96,7 +97,7 @@ def main():
             bwd()
     torch.cuda.synchronize()
     _lib.timing_enable(False)
-    kt = _lib.kernel_times(("attn_fwd", "attn_bwd_dkv", "attn_bwd_dq", "attn_bias_reduce"))
+    kt = _lib.kernel_times(("attn_fwd", "attn_bwd", "attn_bwd_dkv", "attn_bwd_dq", "attn_bias_reduce"))
     fl = flops(B, L, d, H)
     res = {}
     for name, (tot, n) in kt.items():

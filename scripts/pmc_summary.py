@@ -27,6 +27,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 _MAP = [
     (r"bucket_map_kernel", "bucket_map"),
     (r"attn_fwd_kernel", "attn_fwd"),
+    (r"attn_bwd_fused_kernel", "attn_bwd"),
     (r"attn_bwd_dkv_kernel", "attn_bwd_dkv"),
     (r"attn_bwd_dq_kernel", "attn_bwd_dq"),
     (r"bias_grad_reduce_kernel", "attn_bias_reduce"),
