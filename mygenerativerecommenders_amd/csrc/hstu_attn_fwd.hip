@@ -124,34 +124,55 @@ __global__ __launch_bounds__(256) void hstu_attn_fwd_kernel(AttnFwdArgs a) {
     const int k0 = kt * TK;
     const bool more = kt < last_kt;
     if (more) load_tile(kt + 1, mwn);
+    // key blocks in pairs: the two S = K Q^T chains interleave (one 13-deep chain of
+    // dependent MFMAs alone is latency-bound); each block's arithmetic is unchanged
 #pragma unroll
-    for (int kb = 0; kb < C::KB; ++kb) {
+    for (int kb = 0; kb < C::KB; kb += 2) {
       const int kb0 = k0 + kb * 16;
       if (kb0 > wq_lo + 15 || kb0 >= L) break;  // wave-uniform causal / length skip
-      f4 s = f4_zero();
+      const bool two = kb + 1 < C::KB && kb0 + 16 <= wq_lo + 15 && kb0 + 16 < L;
+      f4 s0 = f4_zero(), s1 = f4_zero();
       const float* krow = Ks + (kb * 16 + lr) * C::LDK + lg;
+      if (two) {
 #pragma unroll
-      for (int st = 0; st < KSTEPS; ++st) s = mfma16x16x4(krow[4 * st], qreg[st], s);
-      // s[r] = S^T[key kb0 + 4lg + r][query qi]
-      float p[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int kj = kb0 + 4 * lg + r;
-        float val = s[r];
-        if (has_bias) {
-          const int bucket = (mw[kb] >> (8 * r)) & 0xFF;
-          int pi = a.N - 1 + kj - qi;
-          pi = pi < 0 ? 0 : (pi > 2 * a.N - 2 ? 2 * a.N - 2 : pi);
-          val = val + (posw[pi] + tsw[bucket]);
+        for (int st = 0; st < KSTEPS; ++st) {
+          s0 = mfma16x16x4(krow[4 * st], qreg[st], s0);
+          s1 = mfma16x16x4(krow[16 * C::LDK + 4 * st], qreg[st], s1);
         }
-        p[r] = (q_ok && kj <= qi) ? siluf_(val) * a.inv_n : 0.f;
+      } else {
+#pragma unroll
+        for (int st = 0; st < KSTEPS; ++st) s0 = mfma16x16x4(krow[4 * st], qreg[st], s0);
       }
+      // s[r] = S^T[key kb0 + 16 j + 4lg + r][query qi]
+      float p[2][4];
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int kj = kb0 + 16 * j + 4 * lg + r;
+          float val = j ? s1[r] : s0[r];
+          if (has_bias) {
+            const int bucket = (mw[kb + (j && kb + 1 < C::KB ? 1 : 0)] >> (8 * r)) & 0xFF;
+            int pi = a.N - 1 + kj - qi;
+            pi = pi < 0 ? 0 : (pi > 2 * a.N - 2 ? 2 * a.N - 2 : pi);
+            val = val + (posw[pi] + tsw[bucket]);
+          }
+          p[j][r] = (q_ok && kj <= qi) ? siluf_(val) * a.inv_n : 0.f;
+        }
       const float* vrow = Vs + (kb * 16 + 4 * lg) * C::LDV + lr;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
 #pragma unroll
         for (int ct = 0; ct < VTILES; ++ct)
-          acc[ct] = mfma16x16x4(p[r], vrow[r * C::LDV + ct * 16], acc[ct]);
+          acc[ct] = mfma16x16x4(p[0][r], vrow[r * C::LDV + ct * 16], acc[ct]);
+      }
+      if (two) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+#pragma unroll
+          for (int ct = 0; ct < VTILES; ++ct)
+            acc[ct] = mfma16x16x4(p[1][r], vrow[(16 + r) * C::LDV + ct * 16], acc[ct]);
+        }
       }
     }
     if (more) {
