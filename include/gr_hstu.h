@@ -256,6 +256,11 @@ GR_API int gr_wgrad(const float* a, int64_t lda, const float* a_stats, const flo
  * the reference).  Rows with fewer than k valid items are padded with
  * (-inf, id -1, index -1).  out_index (B, k) is optional.  Limits: D <= 256,
  * k <= 256, N0 <= 256, X < 2^31.
+ * Catalogs of X >= 262,144 items with D <= 64 take a threshold-filter path (sampled
+ * per-query threshold, one all-query scoring pass that reads the table once, exact
+ * merge); inputs that defeat the threshold raise a device flag and an exact path,
+ * gated on that flag, recomputes (no host sync).  The first int32 of the workspace
+ * is that flag after the call (1 = the exact fallback ran).
  */
 GR_API size_t mips_packed_items_bytes(int64_t X, int D);
 GR_API int mips_pack_items(const float* items, int64_t X, int D, float* packed, void* stream);
