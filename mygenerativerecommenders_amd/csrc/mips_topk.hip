@@ -730,6 +730,7 @@ struct FilterArgs {
   int64_t n_blocks;
   // sample pass
   int GB, G;          // sample blocks per group, groups
+  int sr;             // sample stride (item blocks)
   float* smax;        // [B][G]
   // filter pass
   int64_t RB;         // item blocks per wave
@@ -754,13 +755,13 @@ __global__ __launch_bounds__(256) void mips_filter_kernel(FilterArgs a) {
 
   int64_t b0 = 0, b1 = 0, bstride;
   if (SAMPLE) {
-    const int64_t n_sb = (a.n_blocks + SAMPLE_STRIDE - 1) / SAMPLE_STRIDE;
+    const int64_t n_sb = (a.n_blocks + a.sr - 1) / a.sr;
     const int64_t s0 = wv * a.GB, s1 = min(n_sb, s0 + a.GB);
     if (wv < a.G) {
-      b0 = s0 * SAMPLE_STRIDE;
-      b1 = s1 * SAMPLE_STRIDE;
+      b0 = s0 * a.sr;
+      b1 = s1 * a.sr;
     }
-    bstride = SAMPLE_STRIDE;
+    bstride = a.sr;
   } else {
     b0 = wv * a.RB;
     b1 = min(a.n_blocks, b0 + a.RB);
@@ -1048,7 +1049,7 @@ struct TopkPlan {
   size_t part_bytes;   // legacy select partial lists (also the filter path's fallback)
   // filter path
   int64_t n_blocks, RB;
-  int GB, G, NQG, n_chunks, filter_waves;
+  int GB, G, NQG, n_chunks, filter_waves, sr;
   size_t off_tau, off_cnt, off_smax, off_cs, off_ci, off_part, total_bytes;
 };
 
@@ -1086,7 +1087,10 @@ static TopkPlan plan_topk(int B, int64_t X, int D, int k) {
   p.off_part = 0;
   if (p.filter) {
     p.n_blocks = (X + 15) / 16;
-    const int64_t n_sb = (p.n_blocks + SAMPLE_STRIDE - 1) / SAMPLE_STRIDE;
+    // (a 32-block stride at 10M items: sample 112 -> 84 us, but merge +9 us and filter
+    // +34 us from twice the candidates; no net gain, so one stride)
+    p.sr = SAMPLE_STRIDE;
+    const int64_t n_sb = (p.n_blocks + p.sr - 1) / p.sr;
     p.GB = (int)((n_sb + SAMPLE_GROUPS - 1) / SAMPLE_GROUPS);
     p.G = (int)((n_sb + p.GB - 1) / p.GB);
     p.NQG = B <= 32 ? 2 : 8;
@@ -1217,7 +1221,7 @@ extern "C" int mips_topk(const float* queries, const float* packed_items, int64_
     flag = (int*)ws;
     float* tau = (float*)(ws + p.off_tau);
     int* cnt = (int*)(ws + p.off_cnt);
-    FilterArgs f{queries, packed_items, X, D, B, p.n_blocks, p.GB, p.G, (float*)(ws + p.off_smax),
+    FilterArgs f{queries, packed_items, X, D, B, p.n_blocks, p.GB, p.G, p.sr, (float*)(ws + p.off_smax),
                  p.RB, tau, cnt, (float*)(ws + p.off_cs), (int*)(ws + p.off_ci), (int*)ws,
                  getenv("GR_MIPS_DEBUG_NOHIT") != nullptr};
     int rc = launch_filter(f, p, true, st);
