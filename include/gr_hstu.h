@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GR_HSTU_ABI_VERSION 4
+#define GR_HSTU_ABI_VERSION 5
 
 #ifndef GR_API
 #define GR_API __attribute__((visibility("default")))
@@ -247,6 +247,8 @@ GR_API int gr_wgrad(const float* a, int64_t lda, const float* a_stats, const flo
  * mips_pack_items: re-lays the (X, D) row-major fp32 item table into the
  * MFMA-native blocked layout the scorer streams (done once per
  * CandidateIndex.update_embeddings); `packed` needs mips_packed_items_bytes(X, D).
+ * For filter-path catalogs (below) the packed buffer also holds a bf16 copy of the
+ * table and its largest row norm (ABI 5).
  *
  * mips_topk: queries (B, D) fp32; scores are the k-ordered fp32 fmaf chain over d.
  * Output rows are sorted by score desc, then catalog index asc (torch.topk leaves
@@ -257,10 +259,11 @@ GR_API int gr_wgrad(const float* a, int64_t lda, const float* a_stats, const flo
  * (-inf, id -1, index -1).  out_index (B, k) is optional.  Limits: D <= 256,
  * k <= 256, N0 <= 256, X < 2^31.
  * Catalogs of X >= 262,144 items with D <= 64 take a threshold-filter path (sampled
- * per-query threshold, one all-query scoring pass that reads the table once, exact
- * merge); inputs that defeat the threshold raise a device flag and an exact path,
- * gated on that flag, recomputes (no host sync).  The first int32 of the workspace
- * is that flag after the call (1 = the exact fallback ran).
+ * per-query threshold, one all-query scoring pass over the bf16 copy that reads it
+ * once, exact f32 rescoring of the candidates in the merge, which trusts only scores
+ * above the bf16 error bound); inputs that defeat the threshold raise a device flag
+ * and an exact path, gated on that flag, recomputes (no host sync).  The first int32
+ * of the workspace is that flag after the call (1 = the exact fallback ran).
  */
 GR_API size_t mips_packed_items_bytes(int64_t X, int D);
 GR_API int mips_pack_items(const float* items, int64_t X, int D, float* packed, void* stream);

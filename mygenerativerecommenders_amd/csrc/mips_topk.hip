@@ -57,6 +57,68 @@ __device__ __forceinline__ bool sorted_contains(const int64_t* v, int n, int64_t
   return lo < n && v[lo] == key;
 }
 
+// ----------------------------------------------------------------- bf16 filter copy
+// bf16 with round-to-nearest-even: |bf16(x) - x| <= 2^-8 |x| (NaN stays NaN).
+__device__ __forceinline__ uint32_t bf16_bits(float f) {
+  const uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7fc0u;
+  return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+}
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ f4 mfma16x16x32bf16(u32x4 a, u32x4 b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                  __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+
+// Large catalogs carry a second, bf16 copy of the table for the filter pass (half the
+// bytes, 16x the MFMA rate of the f32 path), in the A-operand order of
+// v_mfma_f32_16x16x32_bf16: for block ib, k-chunk c (KC = ceil(D/32)) and lane l,
+//   packed16[(ib * KC + c) * 64 + l] = bf16(item ib*16 + l%16, dims 32c + 8(l/16) + 0..7)
+// as one 16-byte word (element j in bits 16j .. 16j+15), followed by the largest item
+// L2 norm (fp32 bits, for the filter's error bound).
+__global__ void pack_bf16_kernel(const float* items, int64_t X, int D, int KC, u32x4* packed16) {
+  const int64_t total = (X + 15) / 16 * KC * 64;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int l = (int)(e & 63);
+    const int64_t t = e >> 6;  // ib * KC + c
+    const int c = (int)(t % KC);
+    const int64_t i = (t / KC) * 16 + (l & 15);
+    const int d0 = 32 * c + 8 * (l >> 4);
+    uint32_t w[4];
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const int d = d0 + 2 * h;
+      const float v0 = (i < X && d < D) ? items[i * D + d] : 0.f;
+      const float v1 = (i < X && d + 1 < D) ? items[i * D + d + 1] : 0.f;
+      w[h] = bf16_bits(v0) | (bf16_bits(v1) << 16);
+    }
+    packed16[e] = u32x4{w[0], w[1], w[2], w[3]};
+  }
+}
+
+// max_i ||x_i||_2 as fp32 bits (non-negative floats order like their bit patterns);
+// *maxbits is zeroed beforehand.  NaN rows push it to NaN-like bits, which disables
+// the filter (its thresholds compare false) and routes the batch to the exact path.
+__global__ __launch_bounds__(256) void item_norm_max_kernel(const float* items, int64_t X, int D,
+                                                            uint32_t* maxbits) {
+  uint32_t m = 0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < X; i += (int64_t)gridDim.x * 256) {
+    float ss = 0.f;
+    for (int d = 0; d < D; ++d) ss = fmaf(items[i * D + d], items[i * D + d], ss);
+    const uint32_t b = __float_as_uint(sqrtf(ss));
+    m = b > m ? b : m;
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const uint32_t v = __shfl_xor(m, o, 64);
+    m = v > m ? v : m;
+  }
+  if ((threadIdx.x & 63) == 0 && m) atomicMax(maxbits, m);
+}
+
 // ----------------------------------------------------------------- packing
 __global__ void pack_items_kernel(const float* items, int64_t X, int D, int KS2, float* packed) {
   const int64_t nblk = (X + 15) / 16;
@@ -725,6 +787,7 @@ constexpr int64_t FILTER_MIN_X = (int64_t)SAMPLE_STRIDE * 16 * 1024;  // >= 1024
 struct FilterArgs {
   const float* q;
   const float* packed;
+  const u32x4* packed16;  // bf16 copy (KC > 0 instantiations)
   int64_t X;
   int D, B;
   int64_t n_blocks;
@@ -745,9 +808,12 @@ struct FilterArgs {
 constexpr int WG_CAP = 4096;  // per-workgroup LDS staging of filter hits (~256 expected)
 constexpr int WV_CAP = WG_CAP / 4;  // per-wave segment
 
-template <int KS, int NQG, bool SAMPLE>
+// KC == 0: f32 table (KS k-steps of 16x16x4); KC > 0: the bf16 copy (KC k-chunks of
+// 16x16x32), scores approximate to within the bound the tau kernel folds into tau.
+template <int KS, int KC, int NQG, bool SAMPLE>
 __global__ __launch_bounds__(256) void mips_filter_kernel(FilterArgs a) {
   constexpr int KS2 = (KS + 1) / 2;
+  constexpr bool BF = KC > 0;
   typedef float fv2 __attribute__((ext_vector_type(2)));
   const int lane = threadIdx.x & 63, lr = lane & 15, lg = lane >> 4;
   const int64_t wv = (int64_t)blockIdx.x * 4 + wave_id();
@@ -778,15 +844,34 @@ __global__ __launch_bounds__(256) void mips_filter_kernel(FilterArgs a) {
   // same 25 KB query block: ~90 us of contention at launch), in MFMA B-operand order
   // so each wave's reads are conflict-free: frag[(g KS + st) 64 + lr + 16 lg] =
   // Q[qb + 16 g + lr][4 st + lg].
-  __shared__ float q_lds[NQG * KS * 64];
+  // (bf16: frag16[(g KC + c) 64 + lr + 16 lg] = bf16(Q[qb + 16 g + lr][32 c + 8 lg + 0..7]))
+  __shared__ float q_lds[BF ? 1 : NQG * KS * 64];
+  __shared__ u32x4 q16_lds[BF ? NQG * KC * 64 : 1];
   __shared__ float tau_lds[NQG * 16];
   {
-    const int rows = NQG * 16, cols = 4 * KS;
-    for (int e = threadIdx.x; e < rows * cols; e += 256) {
-      const int r = e / cols, d = e - r * cols;
-      const int qq = qb + r;
-      const float v = (qq < a.B && d < a.D) ? a.q[(int64_t)qq * a.D + d] : 0.f;
-      q_lds[((r >> 4) * KS + (d >> 2)) * 64 + (r & 15) + 16 * (d & 3)] = v;
+    const int rows = NQG * 16;
+    if constexpr (BF) {
+      for (int e = threadIdx.x; e < rows * KC * 4; e += 256) {
+        const int r = e / (KC * 4), u = e - r * (KC * 4);
+        const int qq = qb + r, d0 = 32 * (u >> 2) + 8 * (u & 3);
+        uint32_t w[4];
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          const int d = d0 + 2 * h;
+          const float v0 = (qq < a.B && d < a.D) ? a.q[(int64_t)qq * a.D + d] : 0.f;
+          const float v1 = (qq < a.B && d + 1 < a.D) ? a.q[(int64_t)qq * a.D + d + 1] : 0.f;
+          w[h] = bf16_bits(v0) | (bf16_bits(v1) << 16);
+        }
+        q16_lds[((r >> 4) * KC + (u >> 2)) * 64 + (r & 15) + 16 * (u & 3)] = u32x4{w[0], w[1], w[2], w[3]};
+      }
+    } else {
+      const int cols = 4 * KS;
+      for (int e = threadIdx.x; e < rows * cols; e += 256) {
+        const int r = e / cols, d = e - r * cols;
+        const int qq = qb + r;
+        const float v = (qq < a.B && d < a.D) ? a.q[(int64_t)qq * a.D + d] : 0.f;
+        q_lds[((r >> 4) * KS + (d >> 2)) * 64 + (r & 15) + 16 * (d & 3)] = v;
+      }
     }
     for (int r = threadIdx.x; r < rows; r += 256) {
       const int qq = qb + r;
@@ -794,11 +879,18 @@ __global__ __launch_bounds__(256) void mips_filter_kernel(FilterArgs a) {
     }
     __syncthreads();
   }
-  float qreg[NQG][KS];
+  float qreg[NQG][BF ? 1 : KS];
+  u32x4 qreg16[NQG][BF ? KC : 1];
 #pragma unroll
-  for (int g = 0; g < NQG; ++g)
+  for (int g = 0; g < NQG; ++g) {
+    if constexpr (BF) {
 #pragma unroll
-    for (int st = 0; st < KS; ++st) qreg[g][st] = q_lds[(g * KS + st) * 64 + lane];
+      for (int c = 0; c < KC; ++c) qreg16[g][c] = q16_lds[(g * KC + c) * 64 + lane];
+    } else {
+#pragma unroll
+      for (int st = 0; st < KS; ++st) qreg[g][st] = q_lds[(g * KS + st) * 64 + lane];
+    }
+  }
   float thr[NQG];  // filter: tau of query 16 g + lr (+inf for padded queries); sample: running max
 #pragma unroll
   for (int g = 0; g < NQG; ++g) thr[g] = tau_lds[16 * g + lr];
@@ -808,28 +900,43 @@ __global__ __launch_bounds__(256) void mips_filter_kernel(FilterArgs a) {
   // An odd KS leaves the .y half of the last pair unused (zero padding): load only the
   // .x half, so no in-flight load targets a register the compiler considers dead (it
   // would reuse it as a temporary and wait vmcnt(0) on the prefetch).
-  constexpr int NP = KS / 2;  // full pairs
+  constexpr int NP = BF ? 0 : KS / 2;  // full pairs
+  gptr<u32x4> pk16 = as_global(a.packed16);
   struct Frag {
     fv2 p[NP > 0 ? NP : 1];
     float t;
+    u32x4 h[BF ? KC : 1];
   };
   Frag fa, fb;
   auto load = [&](Frag& f, int64_t ib) {
     ib = ib < b1 ? ib : b1 - bstride;  // clamped: loads stay unconditional
-    gptr<fv2> src = pk + ib * KS2 * 64 + lane;
+    if constexpr (BF) {
+      gptr<u32x4> src = pk16 + ib * KC * 64 + lane;
 #pragma unroll
-    for (int j = 0; j < NP; ++j) f.p[j] = src[j * 64];
-    if (KS & 1) f.t = pk1[((ib * KS2 + NP) * 64 + lane) * 2];
+      for (int c = 0; c < KC; ++c) f.h[c] = src[c * 64];
+    } else {
+      gptr<fv2> src = pk + ib * KS2 * 64 + lane;
+#pragma unroll
+      for (int j = 0; j < NP; ++j) f.p[j] = src[j * 64];
+      if (KS & 1) f.t = pk1[((ib * KS2 + NP) * 64 + lane) * 2];
+    }
   };
   auto process = [&](const Frag& f, int64_t ib) {
     f4 s[NQG];
 #pragma unroll
     for (int g = 0; g < NQG; ++g) s[g] = f4_zero();
+    if constexpr (BF) {
 #pragma unroll
-    for (int st = 0; st < KS; ++st) {
-      const float av = (st >> 1) < NP ? ((st & 1) ? f.p[st >> 1].y : f.p[st >> 1].x) : f.t;
+      for (int c = 0; c < KC; ++c)
 #pragma unroll
-      for (int g = 0; g < NQG; ++g) s[g] = mfma16x16x4(av, qreg[g][st], s[g]);
+        for (int g = 0; g < NQG; ++g) s[g] = mfma16x16x32bf16(f.h[c], qreg16[g][c], s[g]);
+    } else {
+#pragma unroll
+      for (int st = 0; st < KS; ++st) {
+        const float av = (st >> 1) < NP ? ((st & 1) ? f.p[st >> 1].y : f.p[st >> 1].x) : f.t;
+#pragma unroll
+        for (int g = 0; g < NQG; ++g) s[g] = mfma16x16x4(av, qreg[g][st], s[g]);
+      }
     }
     const int64_t item0 = ib * 16 + 4 * lg;  // rows 4 lg + r of the block
     const bool full = ib * 16 + 16 <= a.X;   // wave-uniform
@@ -931,23 +1038,58 @@ __global__ __launch_bounds__(256) void mips_filter_kernel(FilterArgs a) {
   }
 }
 
-// tau_q = M_SAMPLE-th largest group max (one workgroup per query); also resets the
-// query's candidate counter and (query 0) the fallback flag.
-__global__ __launch_bounds__(256) void mips_tau_kernel(const float* smax, int G, float* tau, int* cnt,
-                                                       int* flag) {
+// Error bound of a bf16 filter score s~ against the exact f32 score s of the same pair:
+// each product q_d x_d carries two bf16 roundings (<= (2^-7 + 2^-16) |q_d x_d|) and the
+// f32 accumulation of <= 64 terms adds <= 2^-18 sum|q_d x_d|, and
+// sum|q_d x_d| <= ||q|| ||x|| (Cauchy-Schwarz), so
+//   |s~ - s| <= delta_q = BF16_C ||q|| max_i ||x_i||  (+ a denormal-flush allowance).
+// BF16_C = 2^-7 + 2^-12 keeps a margin for the fp32 evaluation of the norms.
+constexpr float BF16_C = 0.0078125f + 0.000244140625f;
+
+struct TauArgs {
+  const float* smax;
+  int G;
+  const float* q;          // bf16 filter: the f32 queries (for ||q||)
+  int D;
+  const uint32_t* maxnorm; // bf16 filter: max item norm bits; null = exact f32 filter scores
+  float* tau;              // filter threshold
+  float* tau_e;            // exactness threshold of the rescored candidates
+  int* cnt;
+  int* flag;
+};
+
+// tau~ = M_SAMPLE-th largest group max (one workgroup per query).  f32 filter:
+// tau = tau_e = tau~.  bf16 filter, with d = delta_q (1 + 2^-10):
+//   tau = tau~ - 2 d  (collect s~ >= tau),   tau_e = tau + d.
+// Any item with exact s >= tau_e has s~ >= s - delta_q >= tau, so it was collected;
+// the M_SAMPLE sampled maxima (s~ >= tau~) all have s >= tau~ - delta_q >= tau_e.
+// (The 2^-10 inflation covers the fp32 rounding of tau + d.)  Also resets the query's
+// candidate counters and (query 0) the fallback flag.
+__global__ __launch_bounds__(256) void mips_tau_kernel(TauArgs a) {
   __shared__ uint32_t key[SAMPLE_GROUPS];
   __shared__ SelLDS L;
   const int q = blockIdx.x, tid = threadIdx.x;
-  for (int e = tid; e < G; e += 256) key[e] = ord_key(smax[(int64_t)q * G + e]);
+  for (int e = tid; e < a.G; e += 256) key[e] = ord_key(a.smax[(int64_t)q * a.G + e]);
   __syncthreads();
-  const int m = G < M_SAMPLE ? G : M_SAMPLE;
+  const int m = a.G < M_SAMPLE ? a.G : M_SAMPLE;
   uint32_t kstar;
   int k_rem;
-  block_radix_kth(key, G, m, L, kstar, k_rem);
-  if (tid < NSUB) cnt[q * NSUB + tid] = 0;
+  block_radix_kth(key, a.G, m, L, kstar, k_rem);
+  if (tid < NSUB) a.cnt[q * NSUB + tid] = 0;
   if (tid == 0) {
-    tau[q] = key_to_float(kstar);
-    if (q == 0) *flag = 0;
+    const float t = key_to_float(kstar);
+    if (a.maxnorm) {
+      float ss = 0.f;
+      for (int d = 0; d < a.D; ++d) ss = fmaf(a.q[(int64_t)q * a.D + d], a.q[(int64_t)q * a.D + d], ss);
+      const float qn = sqrtf(ss), xn = __uint_as_float(*a.maxnorm);
+      const float dl = (BF16_C * qn * xn + 1e-35f * (qn + xn + 1.f)) * (1.f + 0.0009765625f);
+      a.tau[q] = t - 2.f * dl;
+      a.tau_e[q] = a.tau[q] + dl;
+    } else {
+      a.tau[q] = t;
+      a.tau_e[q] = t;
+    }
+    if (q == 0) *a.flag = 0;
   }
 }
 
@@ -963,6 +1105,14 @@ struct FilterMergeArgs {
   int64_t* out_ids;
   int64_t* out_index;
   int* flag;
+  // bf16 filter: candidates are rescored exactly from the f32 table and only those with
+  // s >= tau_e count (see mips_tau_kernel)
+  int rescore;
+  const float* packed;
+  int KS2;
+  const float* q;
+  int D;
+  const float* tau_e;
 };
 
 __global__ __launch_bounds__(256) void mips_filter_merge_kernel(FilterMergeArgs a) {
@@ -1016,11 +1166,31 @@ __global__ __launch_bounds__(256) void mips_filter_merge_kernel(FilterMergeArgs 
       }
       __syncthreads();
     }
+  float te = -INFINITY;
+  if (a.rescore) {
+    // exact score: the k-ordered fmaf chain over d < D (the f32 MFMA's and the
+    // oracle's), items read from the f32 table: dims 4st + lg of item row r sit at
+    // ((ib KS2 + st/2) 64 + r + 16 lg) 2 + st%2
+    __shared__ float q_s[64];
+    if (tid < 64) q_s[tid] = tid < a.D ? a.q[(int64_t)q * a.D + tid] : 0.f;
+    te = a.tau_e[q];
+    __syncthreads();
+    for (int e = tid; e < n_raw; e += 256) {
+      const int64_t li = ci[e];
+      const float* row = a.packed + ((li >> 4) * a.KS2 * 64 + (li & 15)) * 2;
+      float s = 0.f;
+      for (int d = 0; d < a.D; ++d) {
+        const int st = d >> 2;
+        s = fmaf(row[((st >> 1) * 64 + 16 * (d & 3)) * 2 + (st & 1)], q_s[d], s);
+      }
+      cs[e] = s;
+    }
+  }
   int nvalid = 0;
   for (int e = tid; e < n_raw; e += 256) {
     const int64_t li = ci[e];
     const int64_t id = a.item_ids ? a.item_ids[li] : a.index_base + li;
-    const bool ok = !(n0p > 0 && sorted_contains(inv, n0p, id));
+    const bool ok = !(n0p > 0 && sorted_contains(inv, n0p, id)) && cs[e] >= te;
     key[e] = ok ? ord_key(cs[e]) : 0u;
     idx[e] = a.index_base + li;
     nvalid += ok;
@@ -1050,13 +1220,37 @@ struct TopkPlan {
   // filter path
   int64_t n_blocks, RB;
   int GB, G, NQG, n_chunks, filter_waves, sr;
-  size_t off_tau, off_cnt, off_smax, off_cs, off_ci, off_part, total_bytes;
+  int KC;              // > 0: the filter scores the bf16 copy (KC k-chunks of 32 dims)
+  size_t off_tau, off_tau_e, off_cnt, off_smax, off_cs, off_ci, off_part, total_bytes;
 };
 
 static size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 
+// Packed-table layout: the f32 blocks, then (filter-sized catalogs: X >= FILTER_MIN_X,
+// D <= 64) the bf16 copy and the max item norm.
+struct PackLayout {
+  bool bf16;
+  int KC;
+  size_t off16, off_norm, total;
+};
+
+static PackLayout pack_layout(int64_t X, int D) {
+  PackLayout L{};
+  const int64_t nblk = (X + 15) / 16;
+  const size_t f32 = sizeof(float) * (size_t)nblk * ((ceil_div(D, 4) + 1) / 2) * 128;
+  L.total = f32;
+  L.bf16 = X >= FILTER_MIN_X && ceil_div(D, 4) <= 16;
+  if (L.bf16) {
+    L.KC = ceil_div(D, 32);
+    L.off16 = align256(f32);
+    L.off_norm = L.off16 + align256((size_t)nblk * L.KC * 64 * 16);
+    L.total = L.off_norm + 256;
+  }
+  return L;
+}
+
 static TopkPlan plan_topk(int B, int64_t X, int D, int k) {
-  TopkPlan p;
+  TopkPlan p{};
   p.KS = ceil_div(D, 4);
   const int n_qg = ceil_div(B, QG);
   int target = ceil_div(256, n_qg);  // ~one workgroup per CU
@@ -1103,8 +1297,11 @@ static TopkPlan plan_topk(int B, int64_t X, int D, int k) {
     if (rounds < 1) rounds = 1;
     p.RB = (p.n_blocks + per_round * rounds - 1) / (per_round * rounds);
     p.filter_waves = (int)((p.n_blocks + p.RB - 1) / p.RB);
+    // GR_MIPS_FP32_FILTER=1: filter on the f32 table (exact scores, 16x fewer flop/s)
+    p.KC = getenv("GR_MIPS_FP32_FILTER") ? 0 : pack_layout(X, D).KC;
     size_t o = 256;  // [0, 4): fallback flag
     p.off_tau = o;  o = align256(o + sizeof(float) * B);
+    p.off_tau_e = o; o = align256(o + sizeof(float) * B);
     p.off_cnt = o;  o = align256(o + sizeof(int) * B * NSUB);
     p.off_smax = o; o = align256(o + sizeof(float) * (size_t)B * p.G);
     p.off_cs = o;   o = align256(o + sizeof(float) * (size_t)B * FILTER_CAP);
@@ -1115,32 +1312,35 @@ static TopkPlan plan_topk(int B, int64_t X, int D, int k) {
   return p;
 }
 
-template <int KS, int NQG>
+template <int KS, int KC, int NQG>
 static int launch_filter_pair(const FilterArgs& f, const TopkPlan& p, bool sample, hipStream_t st) {
   if (sample) {
     const dim3 g(ceil_div(p.G, 4), p.n_chunks);
-    GR_TIMED("mips_sample", st, hipLaunchKernelGGL((mips_filter_kernel<KS, NQG, true>), g, dim3(256), 0, st, f));
+    GR_TIMED("mips_sample", st, hipLaunchKernelGGL((mips_filter_kernel<KS, KC, NQG, true>), g, dim3(256), 0, st, f));
     GR_LAUNCH_CHECK("mips_topk(sample)");
   } else {
     const dim3 g(ceil_div(p.filter_waves, 4), p.n_chunks);
-    GR_TIMED("mips_filter", st, hipLaunchKernelGGL((mips_filter_kernel<KS, NQG, false>), g, dim3(256), 0, st, f));
+    GR_TIMED("mips_filter", st, hipLaunchKernelGGL((mips_filter_kernel<KS, KC, NQG, false>), g, dim3(256), 0, st, f));
     GR_LAUNCH_CHECK("mips_topk(filter)");
   }
   return 0;
 }
 
-template <int KS>
+template <int KS, int KC>
 static int launch_filter_ks(const FilterArgs& f, const TopkPlan& p, bool sample, hipStream_t st) {
-  return p.NQG == 2 ? launch_filter_pair<KS, 2>(f, p, sample, st) : launch_filter_pair<KS, 8>(f, p, sample, st);
+  return p.NQG == 2 ? launch_filter_pair<KS, KC, 2>(f, p, sample, st)
+                    : launch_filter_pair<KS, KC, 8>(f, p, sample, st);
 }
 
 static int launch_filter(const FilterArgs& f, const TopkPlan& p, bool sample, hipStream_t st) {
+  if (p.KC == 1) return launch_filter_ks<1, 1>(f, p, sample, st);
+  if (p.KC == 2) return launch_filter_ks<1, 2>(f, p, sample, st);
   switch (p.KS) {
-    case 1: case 2: return launch_filter_ks<2>(f, p, sample, st);
-    case 3: case 4: return launch_filter_ks<4>(f, p, sample, st);
-    case 5: case 6: case 7: case 8: return launch_filter_ks<8>(f, p, sample, st);
-    case 9: case 10: case 11: case 12: case 13: return launch_filter_ks<13>(f, p, sample, st);
-    default: return launch_filter_ks<16>(f, p, sample, st);
+    case 1: case 2: return launch_filter_ks<2, 0>(f, p, sample, st);
+    case 3: case 4: return launch_filter_ks<4, 0>(f, p, sample, st);
+    case 5: case 6: case 7: case 8: return launch_filter_ks<8, 0>(f, p, sample, st);
+    case 9: case 10: case 11: case 12: case 13: return launch_filter_ks<13, 0>(f, p, sample, st);
+    default: return launch_filter_ks<16, 0>(f, p, sample, st);
   }
 }
 
@@ -1160,16 +1360,27 @@ static int launch_select(const SelectArgs& a, hipStream_t st) {
 using namespace gr;
 
 extern "C" size_t mips_packed_items_bytes(int64_t X, int D) {
-  const int KS2 = (ceil_div(D, 4) + 1) / 2;
-  return sizeof(float) * (size_t)((X + 15) / 16) * KS2 * 128;
+  if (X < 0 || D <= 0) return 0;
+  return pack_layout(X, D).total;
 }
 
 extern "C" int mips_pack_items(const float* items, int64_t X, int D, float* packed, void* stream) {
   GR_REQUIRE(items && packed && X >= 0 && D > 0, "mips_pack_items: bad args");
   if (X == 0) return 0;
+  const hipStream_t st = (hipStream_t)stream;
   const int KS2 = (ceil_div(D, 4) + 1) / 2;
-  GR_TIMED("mips_pack", (hipStream_t)stream, hipLaunchKernelGGL(pack_items_kernel, dim3(2048), dim3(256), 0, (hipStream_t)stream, items, X,
-                     D, KS2, packed));
+  const PackLayout L = pack_layout(X, D);
+  GR_TIMED("mips_pack", st, {
+    hipLaunchKernelGGL(pack_items_kernel, dim3(2048), dim3(256), 0, st, items, X, D, KS2, packed);
+    if (L.bf16) {
+      char* base = (char*)packed;
+      uint32_t* maxbits = (uint32_t*)(base + L.off_norm);
+      hipLaunchKernelGGL(pack_bf16_kernel, dim3(2048), dim3(256), 0, st, items, X, D, L.KC,
+                         (u32x4*)(base + L.off16));
+      (void)hipMemsetAsync(maxbits, 0, sizeof(uint32_t), st);
+      hipLaunchKernelGGL(item_norm_max_kernel, dim3(2048), dim3(256), 0, st, items, X, D, maxbits);
+    }
+  });
   GR_LAUNCH_CHECK("mips_pack_items");
   return 0;
 }
@@ -1221,17 +1432,24 @@ extern "C" int mips_topk(const float* queries, const float* packed_items, int64_
     flag = (int*)ws;
     float* tau = (float*)(ws + p.off_tau);
     int* cnt = (int*)(ws + p.off_cnt);
-    FilterArgs f{queries, packed_items, X, D, B, p.n_blocks, p.GB, p.G, p.sr, (float*)(ws + p.off_smax),
+    float* tau_e = (float*)(ws + p.off_tau_e);
+    const PackLayout L = pack_layout(X, D);
+    const char* pbase = (const char*)packed_items;
+    FilterArgs f{queries, packed_items, p.KC ? (const u32x4*)(pbase + L.off16) : nullptr, X, D, B,
+                 p.n_blocks, p.GB, p.G, p.sr, (float*)(ws + p.off_smax),
                  p.RB, tau, cnt, (float*)(ws + p.off_cs), (int*)(ws + p.off_ci), (int*)ws,
                  getenv("GR_MIPS_DEBUG_NOHIT") != nullptr};
     int rc = launch_filter(f, p, true, st);
     if (rc) return rc;
-    GR_TIMED("mips_tau", st, hipLaunchKernelGGL(mips_tau_kernel, dim3(B), dim3(256), 0, st, f.smax, p.G, tau, cnt, flag));
+    TauArgs ta{f.smax, p.G, queries, D, p.KC ? (const uint32_t*)(pbase + L.off_norm) : nullptr,
+               tau, tau_e, cnt, flag};
+    GR_TIMED("mips_tau", st, hipLaunchKernelGGL(mips_tau_kernel, dim3(B), dim3(256), 0, st, ta));
     GR_LAUNCH_CHECK("mips_topk(tau)");
     rc = launch_filter(f, p, false, st);
     if (rc) return rc;
     FilterMergeArgs fm{f.cand_s, f.cand_i, cnt, B, k, N0, item_ids, index_base, invalid_ids,
-                       out_scores, out_ids, out_index, flag};
+                       out_scores, out_ids, out_index, flag, p.KC > 0, packed_items,
+                       (p.KS + 1) / 2, queries, D, tau_e};
     GR_TIMED("mips_merge", st, hipLaunchKernelGGL(mips_filter_merge_kernel, dim3(B), dim3(256), 0, st, fm));
     GR_LAUNCH_CHECK("mips_topk(filter merge)");
   }

@@ -533,6 +533,16 @@ __global__ __launch_bounds__(256) void ssm_table_grad_kernel(const float* out, i
   }
 }
 
+// d_table[v][0 .. D) = 0 for every row (a strided memset as a kernel: the graph-captured
+// step then holds no 2-D memset node)
+__global__ __launch_bounds__(256) void ssm_zero_rows_kernel(float* p, int64_t ld, int64_t rows, int D) {
+  const int64_t total = rows * D;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int64_t r = e / D;
+    p[r * ld + (e - r * D)] = 0.f;
+  }
+}
+
 inline int lanes_per_row(int D) { return D <= 16 ? 1 : D <= 32 ? 2 : D <= 64 ? 4 : D <= 128 ? 8 : 16; }
 
 #define GR_SSM_DISPATCH(L, KERNEL, ...)                          \
@@ -605,10 +615,11 @@ int gr_sampled_softmax_bwd(const float* out, int64_t ld_out, const float* pos, i
   GR_REQUIRE(d_table && ld_dtable >= D, "gr_sampled_softmax_bwd: bad d_table");
   const hipStream_t st = (hipStream_t)stream;
   const int64_t n = M * (int64_t)R;
-  if (hipMemset2DAsync(d_table, (size_t)ld_dtable * 4, 0, (size_t)D * 4, (size_t)V, st) !=
-      hipSuccess) {  // the row reduction accumulates into it
-    gr::set_error("gr_sampled_softmax_bwd: memset failed");
-    return 2;
+  {  // the row reduction accumulates into d_table
+    const int64_t zt = V * D;
+    const unsigned zg = (unsigned)std::min<int64_t>((zt + 255) / 256, 4 * gr::device_cus());
+    hipLaunchKernelGGL(gr::ssm_zero_rows_kernel, dim3(zg), dim3(256), 0, st, d_table, ld_dtable, V, D);
+    GR_LAUNCH_CHECK("gr_sampled_softmax_bwd (zero d_table)");
   }
   if (M == 0) return 0;
   GR_REQUIRE(out && pos && sup_ids && table && lse && dloss && d_out && d_pos && (offsets || R == 0),

@@ -169,7 +169,8 @@ def _gpu_flag(Q, E, ids, invalid, k, index_base=0):
 def _check_filter(Q, E, ids, invalid, k, expect_flag):
     s, i, x, flag = _gpu_flag(Q, E, ids, invalid, k)
     rs, ri, rx = topk_oracle.mips_topk(Q, E, ids, invalid, k)
-    assert flag == expect_flag, f"fallback flag {flag}, expected {expect_flag}"
+    if expect_flag is not None:
+        assert flag == expect_flag, f"fallback flag {flag}, expected {expect_flag}"
     assert np.array_equal(x, rx), f"index mismatch rows {np.where((x != rx).any(1))[0][:8]}"
     assert np.array_equal(i, ri)
     assert np.array_equal(s.view(np.uint32), rs.view(np.uint32))
@@ -255,3 +256,65 @@ def test_sharded_merge_equals_full_filter_path():
     assert np.array_equal(i.cpu().numpy(), ri)
     assert np.array_equal(x.cpu().numpy() - 1, rx)
     assert np.array_equal(s.cpu().numpy().view(np.uint32), rs.view(np.uint32))
+
+
+# ---------------------------------------------------------------- bf16 filter scores
+# The filter pass scores a bf16 copy of the table; the merge rescores every candidate
+# with the exact f32 chain and only trusts those >= tau_e (mips_tau_kernel's bound), so
+# the result stays bit-identical to the oracle.  GR_MIPS_FP32_FILTER=1 keeps the f32
+# filter (exact filter scores) reachable.
+
+@pytest.mark.parametrize("fp32", [False, True], ids=["bf16-filter", "f32-filter"])
+def test_mips_filter_score_type_bitexact(fp32, monkeypatch):
+    if fp32:
+        monkeypatch.setenv("GR_MIPS_FP32_FILTER", "1")
+    g = np.random.default_rng(31)
+    B, X, D, k, N0 = 128, 400_000, 50, 200, 211
+    Q, E, inv = _normal_catalog(g, B, X, D, N0)
+    _check_filter(Q, E, np.arange(1, X + 1, dtype=np.int64), inv, k, expect_flag=0)
+
+
+def test_mips_filter_bf16_rescoring_orders_near_ties():
+    """400 items every query scores within ~1e-5 of each other (far below bf16
+    resolution) and well above the rest: only the exact rescoring can order them."""
+    g = np.random.default_rng(21)
+    B, X, D, k = 64, 300_000, 50, 200
+    _, E, _ = _normal_catalog(g, B, X, D, 0)
+    u = g.standard_normal(D).astype(np.float32)
+    u /= np.linalg.norm(u)
+    Q = (u[None, :] + 0.3 * g.standard_normal((B, D)) / np.sqrt(D)).astype(np.float32)
+    Q /= np.linalg.norm(Q, axis=1, keepdims=True)
+    idx = g.choice(X, 400, replace=False)
+    E[idx] = (u[None, :] + 1e-5 * g.standard_normal((400, D))).astype(np.float32)
+    _check_filter(Q, E, np.arange(X, dtype=np.int64), None, k, expect_flag=0)
+
+
+def test_mips_filter_bf16_unnormalised_norms():
+    """Item norms spread over 0.5 .. 20 and large queries: the error bound scales with
+    ||q|| max||x||; whichever path runs, the answer is exact."""
+    g = np.random.default_rng(41)
+    B, X, D, k, N0 = 48, 300_000, 32, 150, 64
+    Q, E, inv = _normal_catalog(g, B, X, D, N0)
+    E *= g.uniform(0.5, 20.0, (X, 1)).astype(np.float32)
+    Q *= np.float32(100.0)
+    _check_filter(Q, E, np.arange(1, X + 1, dtype=np.int64), inv, k, expect_flag=None)
+
+
+def test_mips_filter_bf16_nan_row_takes_exact_path():
+    """A NaN item makes the bf16 bound NaN: no candidate is trusted and the exact path
+    runs; every finite item keeps its exact rank (the NaN item itself is outside the
+    reference's contract: torch.topk would rank it first)."""
+    g = np.random.default_rng(43)
+    B, X, D, k = 16, 262_144, 16, 50
+    Q, E, _ = _normal_catalog(g, B, X, D, 0)
+    E[12345, 3] = np.nan
+    s, i, x, flag = _gpu_flag(Q, E, np.arange(X, dtype=np.int64), None, k)
+    assert flag == 1
+    E0 = E.copy()
+    E0[12345] = 0.0  # score 0: far below every query's top-50
+    rs, ri, rx = topk_oracle.mips_topk(Q, E0, np.arange(X, dtype=np.int64), None, k)
+    for b in range(B):
+        keep = i[b] != 12345
+        n = int(keep.sum())
+        assert np.array_equal(i[b][keep], ri[b][:n])
+        assert np.array_equal(s[b][keep].view(np.uint32), rs[b][:n].view(np.uint32))
