@@ -243,9 +243,7 @@ def e2e_train_leg(args, device, world, lengths, ts, past_ids):
     torch.cuda.current_stream().wait_stream(side)
     torch.cuda.synchronize()
     mode, step = "eager", eager_step
-    # graph capture of this leg is opt-in (GR_E2E_GRAPH=1): its first replay faults on
-    # MI355X (under investigation; the eager steps and every kernel's tests are clean)
-    if not args.eager and os.environ.get("GR_E2E_GRAPH") == "1":
+    if not args.eager:
         try:
             reducer.zero_grad()
             g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
@@ -301,7 +299,7 @@ def main():
     ap.add_argument("--no-retrieval-leg", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no HIP-graph capture of the step")
     ap.add_argument("--e2e-steps", type=int, default=0,
-                    help="timed steps of the full training-step leg (0 = skip)")
+                    help="timed steps of the full training-step leg (0 = skip; opt-in)")
     args = ap.parse_args()
 
     from mygenerativerecommenders_amd import _lib
@@ -482,8 +480,8 @@ def main():
             sidx.get_top_k_outputs(Q, invalid_ids=inv)
         _sync_barrier(world)
         _lib.timing_enable(False)
-        rnames = ("mips_sample", "mips_tau", "mips_filter", "mips_merge", "mips_select",
-                  "mips_select_fallback", "mips_merge_fallback", "mips_pack")
+        rnames = ("mips_sample", "mips_tau", "mips_filter", "mips_rescore", "mips_merge",
+                  "mips_select", "mips_select_fallback", "mips_merge_fallback", "mips_pack")
         rt = _lib.kernel_times(rnames)
         rkern = "mips_filter" if rt["mips_filter"][1] else "mips_select"
         ktop = rt[rkern][0] / max(1, rt[rkern][1])
@@ -498,22 +496,35 @@ def main():
         dtr = _max_over_ranks(dtr, world)
         cand_per_s = B * X * args.retrieval_steps / dtr
         fl = 2.0 * B * (b - a) * D
-        ach_r = fl / (ktop * 1e-3) / 1e12 if ktop else 0.0
+        xs = b - a
+        bf16_filter = (rkern == "mips_filter" and xs >= 262_144 and D <= 64
+                       and not os.environ.get("GR_MIPS_FP32_FILTER"))
+        if bf16_filter:
+            # the filter streams the bf16 copy once: 16 items x 32 dims x 2 B per k-chunk
+            alg_bytes = float((xs + 15) // 16 * ((D + 31) // 32) * 1024)
+            ach_r = alg_bytes / (ktop * 1e-3) / 1e9 if ktop else 0.0
+            rroof = {"bound": "hbm", "achieved": round(ach_r, 1), "peak": peaks["hbm_gbs"],
+                     "unit": "GB/s", "frac": round(ach_r / peaks["hbm_gbs"], 4),
+                     "algorithmic_bytes": alg_bytes,
+                     "mfma_tflops_bf16": round(fl / (ktop * 1e-3) / 1e12, 1) if ktop else 0.0}
+        else:
+            alg_bytes = 4.0 * xs * 8 * ((D + 7) // 8)
+            ach_r = fl / (ktop * 1e-3) / 1e12 if ktop else 0.0
+            rroof = {"bound": "mfma", "achieved": round(ach_r, 3),
+                     "peak": peaks["fp32_mfma_tflops"], "unit": "TFLOP/s",
+                     "frac": round(ach_r / peaks["fp32_mfma_tflops"], 4),
+                     "algorithmic_bytes": alg_bytes}
         retrieval = {
             "metric": "top-k items scored/s", "value": cand_per_s, "unit": "items/s",
             "scaling": "strong", "ms_per_query_batch": dtr / args.retrieval_steps * 1e3,
             "config": {"workload": "C4: 10M-item catalog row-sharded, B=128 queries, k=200, "
                                    "211 invalid ids, all-gather + device merge",
-                       "items": X, "queries": B, "k": args.k, "dim": D},
+                       "items": X, "queries": B, "k": args.k, "dim": D,
+                       "filter_scores": "bf16 (exact f32 rescoring)" if bf16_filter else "f32"},
             "per_query_batch_device_ms": r_dev,
-            "roofline": {"kernel": rkern, "bound": "mfma",
-                         "achieved": round(ach_r, 3), "peak": peaks["fp32_mfma_tflops"],
-                         "unit": "TFLOP/s", "frac": round(ach_r / peaks["fp32_mfma_tflops"], 4),
-                         "traffic": r_traffic, "traffic_source": traffic_src,
-                         "algorithmic_bytes": 4.0 * (b - a) * 8 * ((D + 7) // 8),
-                         "avg_launch_ms": round(ktop, 4),
-                         "merge_avg_launch_ms": round(kmerge, 4),
-                         "flops_per_launch": fl},
+            "roofline": dict(kernel=rkern, **rroof, traffic=r_traffic,
+                             traffic_source=traffic_src, avg_launch_ms=round(ktop, 4),
+                             merge_avg_launch_ms=round(kmerge, 4), flops_per_launch=fl),
         }
 
     e2e = None

@@ -139,6 +139,19 @@ __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane
 
 __host__ __device__ inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
 
+// Zero n 32-bit words.  Used instead of hipMemsetAsync on every path a training step
+// may capture into a HIP graph: a captured memset node left a counter un-zeroed on
+// replay on MI355X (ROCm 7), which a kernel node does not.
+static __global__ __launch_bounds__(256) void zero_words_kernel(uint32_t* p, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) p[i] = 0u;
+}
+inline void zero_words_async(void* p, int64_t n, hipStream_t st) {
+  if (n <= 0) return;
+  const int64_t g = (n + 255) / 256;
+  hipLaunchKernelGGL(zero_words_kernel, dim3((unsigned)(g < 1024 ? g : 1024)), dim3(256), 0, st,
+                     (uint32_t*)p, n);
+}
+
 // CU count of the current device (cached; 256 on MI355X).
 inline int device_cus() {
   static int n = 0;

@@ -718,8 +718,8 @@ extern "C" int hstu_attn_bwd(const float* q, const float* k, const float* v, int
   hipStream_t st = (hipStream_t)stream;
   if (B == 0 || max_len == 0) {
     if (bucket_map) {
-      (void)hipMemsetAsync(dpos_w, 0, sizeof(float) * (2 * N - 1), st);
-      (void)hipMemsetAsync(dts_w, 0, sizeof(float) * (num_buckets + 1), st);
+      zero_words_async(dpos_w, 2 * N - 1, st);
+      zero_words_async(dts_w, num_buckets + 1, st);
     }
     return 0;
   }

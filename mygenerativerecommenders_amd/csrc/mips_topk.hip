@@ -99,6 +99,17 @@ __global__ void pack_bf16_kernel(const float* items, int64_t X, int D, int KC, u
   }
 }
 
+// rows[i][0 .. DP) = items[i][0 .. D), zero padded
+__global__ void pack_rows_kernel(const float* items, int64_t X, int D, int DP, float* rows) {
+  const int64_t total = X * DP;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = e / DP;
+    const int d = (int)(e - i * DP);
+    rows[e] = d < D ? items[i * D + d] : 0.f;
+  }
+}
+
 // max_i ||x_i||_2 as fp32 bits (non-negative floats order like their bit patterns);
 // *maxbits is zeroed beforehand.  NaN rows push it to NaN-like bits, which disables
 // the filter (its thresholds compare false) and routes the batch to the exact path.
@@ -996,6 +1007,22 @@ __global__ __launch_bounds__(256) void mips_filter_kernel(FilterArgs a) {
         process(f[c], jb < b1 ? jb : b1 - bstride);
       }
     }
+  } else if (!SAMPLE && b0 < b1 && BF) {
+    // bf16 blocks are 1-2 KB of HBM per ~16 MFMAs: keep PD blocks in flight per wave
+    // (a slot is refilled PD blocks ahead as soon as it is consumed)
+    constexpr int PD = 4;
+    Frag f[PD];
+#pragma unroll
+    for (int u = 0; u < PD; ++u) load(f[u], b0 + u);
+    for (int64_t ib = b0; ib < b1; ib += PD) {
+#pragma unroll
+      for (int u = 0; u < PD; ++u) {
+        if (ib + u >= b1) break;
+        const Frag cur = f[u];
+        load(f[u], ib + u + PD);
+        process(cur, ib + u);
+      }
+    }
   } else if (!SAMPLE && b0 < b1) {
     load(fa, b0);
     for (int64_t ib = b0; ib < b1; ib += 2 * bstride) {
@@ -1108,12 +1135,48 @@ struct FilterMergeArgs {
   // bf16 filter: candidates are rescored exactly from the f32 table and only those with
   // s >= tau_e count (see mips_tau_kernel)
   int rescore;
-  const float* packed;
-  int KS2;
-  const float* q;
-  int D;
   const float* tau_e;
 };
+
+// bf16 filter: every collected candidate's exact score, in place.  One workgroup per
+// (query, sub-list), one candidate per thread: the k-ordered fmaf chain over d < D (the
+// f32 MFMA's and the oracle's) over the candidate's row of the row-major copy, whose
+// DP/4 float4 loads are issued together.
+struct RescoreArgs {
+  float* cand_s;
+  const int* cand_i;
+  const int* cnt;
+  const float* rows;  // DP floats per item
+  int DP;
+  const float* q;
+  int D;
+};
+
+__global__ __launch_bounds__(SUBCAP) void mips_rescore_kernel(RescoreArgs a) {
+  __shared__ float q_s[64];
+  const int q = blockIdx.y, tid = threadIdx.x;
+  const int64_t sub = (int64_t)q * NSUB + blockIdx.x;
+  if (tid < 64) q_s[tid] = tid < a.D ? a.q[(int64_t)q * a.D + tid] : 0.f;
+  __syncthreads();
+  const int n = a.cnt[sub];
+  if (tid >= (n < SUBCAP ? n : SUBCAP)) return;
+  typedef float fv4 __attribute__((ext_vector_type(4)));
+  gptr<fv4> r = as_global(reinterpret_cast<const fv4*>(a.rows)) +
+                (int64_t)a.cand_i[sub * SUBCAP + tid] * (a.DP >> 2);
+  fv4 v[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j)
+    if (4 * j < a.DP) v[j] = r[j];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    if (4 * j < a.D) s = fmaf(v[j].x, q_s[4 * j], s);
+    if (4 * j + 1 < a.D) s = fmaf(v[j].y, q_s[4 * j + 1], s);
+    if (4 * j + 2 < a.D) s = fmaf(v[j].z, q_s[4 * j + 2], s);
+    if (4 * j + 3 < a.D) s = fmaf(v[j].w, q_s[4 * j + 3], s);
+  }
+  a.cand_s[sub * SUBCAP + tid] = s;
+}
 
 __global__ __launch_bounds__(256) void mips_filter_merge_kernel(FilterMergeArgs a) {
   __shared__ uint32_t key[FILTER_CAP];
@@ -1166,26 +1229,9 @@ __global__ __launch_bounds__(256) void mips_filter_merge_kernel(FilterMergeArgs 
       }
       __syncthreads();
     }
-  float te = -INFINITY;
-  if (a.rescore) {
-    // exact score: the k-ordered fmaf chain over d < D (the f32 MFMA's and the
-    // oracle's), items read from the f32 table: dims 4st + lg of item row r sit at
-    // ((ib KS2 + st/2) 64 + r + 16 lg) 2 + st%2
-    __shared__ float q_s[64];
-    if (tid < 64) q_s[tid] = tid < a.D ? a.q[(int64_t)q * a.D + tid] : 0.f;
-    te = a.tau_e[q];
-    __syncthreads();
-    for (int e = tid; e < n_raw; e += 256) {
-      const int64_t li = ci[e];
-      const float* row = a.packed + ((li >> 4) * a.KS2 * 64 + (li & 15)) * 2;
-      float s = 0.f;
-      for (int d = 0; d < a.D; ++d) {
-        const int st = d >> 2;
-        s = fmaf(row[((st >> 1) * 64 + 16 * (d & 3)) * 2 + (st & 1)], q_s[d], s);
-      }
-      cs[e] = s;
-    }
-  }
+  // bf16 filter: cs holds the exact scores (mips_rescore_kernel); only candidates at
+  // or above tau_e are provably complete
+  const float te = a.rescore ? a.tau_e[q] : -INFINITY;
   int nvalid = 0;
   for (int e = tid; e < n_raw; e += 256) {
     const int64_t li = ci[e];
@@ -1227,11 +1273,13 @@ struct TopkPlan {
 static size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 
 // Packed-table layout: the f32 blocks, then (filter-sized catalogs: X >= FILTER_MIN_X,
-// D <= 64) the bf16 copy and the max item norm.
+// D <= 64) the bf16 copy, the max item norm and a row-major f32 copy with rows padded
+// to DP = 4 ceil(D/4) floats (16-byte aligned: the merge's exact rescoring gathers a
+// candidate row with DP/4 float4 loads, ~4 sectors, instead of 2 D scattered floats).
 struct PackLayout {
   bool bf16;
-  int KC;
-  size_t off16, off_norm, total;
+  int KC, DP;
+  size_t off16, off_norm, off_rows, total;
 };
 
 static PackLayout pack_layout(int64_t X, int D) {
@@ -1244,7 +1292,9 @@ static PackLayout pack_layout(int64_t X, int D) {
     L.KC = ceil_div(D, 32);
     L.off16 = align256(f32);
     L.off_norm = L.off16 + align256((size_t)nblk * L.KC * 64 * 16);
-    L.total = L.off_norm + 256;
+    L.DP = 4 * ceil_div(D, 4);
+    L.off_rows = L.off_norm + 256;
+    L.total = L.off_rows + align256(sizeof(float) * (size_t)X * L.DP);
   }
   return L;
 }
@@ -1291,14 +1341,17 @@ static TopkPlan plan_topk(int B, int64_t X, int D, int k) {
     p.n_chunks = ceil_div(B, p.NQG * 16);
     // whole rounds of 2 four-wave workgroups per CU, >= ~48 blocks per wave
     const int64_t per_round = (int64_t)device_cus() * 8;
-    int64_t rounds = (p.n_blocks + per_round * 48 - 1) / (per_round * 48);
+    // GR_MIPS_FP32_FILTER=1: filter on the f32 table (exact scores, 16x fewer flop/s)
+    p.KC = getenv("GR_MIPS_FP32_FILTER") ? 0 : pack_layout(X, D).KC;
+    // f32: >= ~48 blocks per wave.  bf16 (streaming-bound): one round (10M items: 7
+    // rounds 302 us, 2 rounds 253 us, 1 round 251 us)
+    const int64_t min_rb = p.KC ? 4096 : 48;
+    int64_t rounds = (p.n_blocks + per_round * min_rb - 1) / (per_round * min_rb);
     static const char* env_rounds = getenv("GR_MIPS_FILTER_ROUNDS");  // tuning knob
     if (env_rounds) rounds = atoi(env_rounds);
     if (rounds < 1) rounds = 1;
     p.RB = (p.n_blocks + per_round * rounds - 1) / (per_round * rounds);
     p.filter_waves = (int)((p.n_blocks + p.RB - 1) / p.RB);
-    // GR_MIPS_FP32_FILTER=1: filter on the f32 table (exact scores, 16x fewer flop/s)
-    p.KC = getenv("GR_MIPS_FP32_FILTER") ? 0 : pack_layout(X, D).KC;
     size_t o = 256;  // [0, 4): fallback flag
     p.off_tau = o;  o = align256(o + sizeof(float) * B);
     p.off_tau_e = o; o = align256(o + sizeof(float) * B);
@@ -1377,8 +1430,10 @@ extern "C" int mips_pack_items(const float* items, int64_t X, int D, float* pack
       uint32_t* maxbits = (uint32_t*)(base + L.off_norm);
       hipLaunchKernelGGL(pack_bf16_kernel, dim3(2048), dim3(256), 0, st, items, X, D, L.KC,
                          (u32x4*)(base + L.off16));
-      (void)hipMemsetAsync(maxbits, 0, sizeof(uint32_t), st);
+      zero_words_async(maxbits, 1, st);
       hipLaunchKernelGGL(item_norm_max_kernel, dim3(2048), dim3(256), 0, st, items, X, D, maxbits);
+      hipLaunchKernelGGL(pack_rows_kernel, dim3(2048), dim3(256), 0, st, items, X, D, L.DP,
+                         (float*)(base + L.off_rows));
     }
   });
   GR_LAUNCH_CHECK("mips_pack_items");
@@ -1447,9 +1502,13 @@ extern "C" int mips_topk(const float* queries, const float* packed_items, int64_
     GR_LAUNCH_CHECK("mips_topk(tau)");
     rc = launch_filter(f, p, false, st);
     if (rc) return rc;
+    if (p.KC) {
+      RescoreArgs ra{f.cand_s, f.cand_i, cnt, (const float*)(pbase + L.off_rows), L.DP, queries, D};
+      GR_TIMED("mips_rescore", st, hipLaunchKernelGGL(mips_rescore_kernel, dim3(NSUB, B), dim3(SUBCAP), 0, st, ra));
+      GR_LAUNCH_CHECK("mips_topk(rescore)");
+    }
     FilterMergeArgs fm{f.cand_s, f.cand_i, cnt, B, k, N0, item_ids, index_base, invalid_ids,
-                       out_scores, out_ids, out_index, flag, p.KC > 0, packed_items,
-                       (p.KS + 1) / 2, queries, D, tau_e};
+                       out_scores, out_ids, out_index, flag, p.KC > 0, tau_e};
     GR_TIMED("mips_merge", st, hipLaunchKernelGGL(mips_filter_merge_kernel, dim3(B), dim3(256), 0, st, fm));
     GR_LAUNCH_CHECK("mips_topk(filter merge)");
   }

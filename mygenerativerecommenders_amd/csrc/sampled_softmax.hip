@@ -656,7 +656,7 @@ int gr_sampled_softmax_bwd(const float* out, int64_t ld_out, const float* pos, i
   const unsigned cgrid = lds ? (unsigned)((n + gr::kCountChunk - 1) / gr::kCountChunk)
                              : (unsigned)std::min<int64_t>((n + 1023) / 1024, 4 * gr::device_cus());
   GR_TIMED("sampled_softmax_csr", st, {
-    (void)hipMemsetAsync(cnt, 0, (size_t)K * 4, st);
+    gr::zero_words_async(cnt, K, st);
     if (lds)
       hipLaunchKernelGGL(gr::ssm_count_kernel<true>, dim3(cgrid), dim3(gr::kCountThreads),
                          (size_t)K * 4, st, rec, n, R, M, V, K, cnt, rank);

@@ -256,8 +256,8 @@ extern "C" int gr_wgrad(const float* a, int64_t lda, const float* a_stats, const
   GR_REQUIRE(Ka > 0 && Nb > 0 && B >= 0 && max_rows >= 0, "gr_wgrad: bad sizes");
   hipStream_t st = (hipStream_t)stream;
   if (max_rows == 0) {
-    (void)hipMemsetAsync(c, 0, sizeof(float) * (size_t)Ka * Nb, st);
-    if (a_colsum) (void)hipMemsetAsync(a_colsum, 0, sizeof(float) * Ka, st);
+    zero_words_async(c, (int64_t)Ka * Nb, st);
+    if (a_colsum) zero_words_async(a_colsum, Ka, st);
     return 0;
   }
   GR_REQUIRE(max_rows * (lda > ldb ? lda : ldb) * 4 < 0x7fffffffLL,

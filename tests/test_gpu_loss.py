@@ -210,3 +210,44 @@ def test_empty_batch_is_nan_like_reference():
         torch.from_numpy(sup_emb).to(dev), torch.from_numpy(weights).to(dev), s,
         DotProductSimilarity())
     assert torch.isnan(loss).item()
+
+
+def test_loss_graph_replays_match_eager():
+    """The loss forward + backward captured into one HIP graph and replayed 3 times gives
+    the eager result every time (the table-gradient counting sort keeps per-step counters
+    that must be re-zeroed inside the graph)."""
+    M, D, V, R, T = 4000, 50, 3953, 128, 0.05
+    out, sup_ids, sup_emb, weights, weight, ids, offsets = _random_case(M, D, V, R, T, 9)
+    ref = _run(out, sup_ids, sup_emb, weights, weight, ids, offsets, T, True)
+    from mygenerativerecommenders_amd.losses import SampledSoftmaxLoss
+    from mygenerativerecommenders_amd.similarity import DotProductSimilarity
+    dev = torch.device("cuda")
+    emb = _Emb(torch.as_tensor(weight).to(dev))
+    s = _sampler(True, torch.as_tensor(ids), torch.as_tensor(offsets).to(dev), emb)
+    o = torch.as_tensor(out).to(dev).requires_grad_(True)
+    p = torch.as_tensor(sup_emb).to(dev).requires_grad_(True)
+    sid = torch.as_tensor(sup_ids).to(dev)
+    wt = torch.as_tensor(weights).to(dev)
+    mod, sim = SampledSoftmaxLoss(R, T), DotProductSimilarity()
+
+    def step():
+        loss = mod.jagged_forward(o, sid, p, wt, s, sim)
+        loss.backward()
+        return loss
+
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        step()
+    torch.cuda.current_stream().wait_stream(side)
+    for t in (o, p, emb.weight):
+        t.grad = None
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        loss_static = step()
+    for _ in range(3):
+        g.replay()
+        torch.cuda.synchronize()
+        assert abs(loss_static.item() - ref[0]) <= 1e-5 * max(1.0, abs(ref[0]))
+        _close(o.grad.cpu().double().numpy(), ref[1], 1e-5, "d_out")
+        _close(emb.weight.grad.cpu().double().numpy(), ref[3], 1e-5, "d_weight")
