@@ -154,7 +154,9 @@ def _gpu_hold_fn():
 
 class _ItemEmbeddings(torch.nn.Module):
     """LocalEmbeddingModule (embedding_modules.py): (V + 1, D) table, truncated-normal
-    std 0.02, id 0 = padding."""
+    std 0.02, id 0 = padding.  Rows are gathered with index_select (backward: index_add_)
+    rather than F.embedding, whose sort-based backward faulted under HIP-graph replay
+    here for some index patterns (a permuted id list)."""
 
     def __init__(self, num_items, D):
         super().__init__()
@@ -163,7 +165,7 @@ class _ItemEmbeddings(torch.nn.Module):
         _truncated_normal_(self.weight.data, 0.0, 0.02)
 
     def get_item_embeddings(self, ids):
-        return torch.nn.functional.embedding(ids, self.weight)
+        return self.weight.index_select(0, ids.reshape(-1)).view(*ids.shape, self.weight.shape[1])
 
 
 def e2e_train_leg(args, device, world, lengths, ts, past_ids):
@@ -480,7 +482,7 @@ def main():
             sidx.get_top_k_outputs(Q, invalid_ids=inv)
         _sync_barrier(world)
         _lib.timing_enable(False)
-        rnames = ("mips_sample", "mips_tau", "mips_filter", "mips_rescore", "mips_merge",
+        rnames = ("mips_sample", "mips_tau", "mips_filter", "mips_merge",
                   "mips_select", "mips_select_fallback", "mips_merge_fallback", "mips_pack")
         rt = _lib.kernel_times(rnames)
         rkern = "mips_filter" if rt["mips_filter"][1] else "mips_select"

@@ -814,9 +814,13 @@ struct FilterArgs {
   int* cand_i;        // [B][NSUB][SUBCAP]  local item index
   int* flag;          // set when a workgroup's staging buffer overflows
   int nohit;          // profiling knob (GR_MIPS_DEBUG_NOHIT): thresholds +inf
+  // bf16 filter: hits are rescored exactly at flush time from row-major f32 copies
+  const float* rows;    // items, DP floats per row
+  const float* q_rows;  // queries, DP floats per row (workspace)
+  int DP;
 };
 
-constexpr int WG_CAP = 4096;  // per-workgroup LDS staging of filter hits (~256 expected)
+constexpr int WG_CAP = 2048;  // per-workgroup LDS staging of filter hits (~450 expected at 10M)
 constexpr int WV_CAP = WG_CAP / 4;  // per-wave segment
 
 // KC == 0: f32 table (KS k-steps of 16x16x4); KC > 0: the bf16 copy (KC k-chunks of
@@ -966,7 +970,7 @@ __global__ __launch_bounds__(256) void mips_filter_kernel(FilterArgs a) {
       for (int g = 0; g < NQG; ++g)
 #pragma unroll
         for (int r = 0; r < 4; ++r) hit |= s[g][r] >= thr[g];
-      if (__builtin_expect(__ballot(hit) != 0ull, 0)) {
+      if (__builtin_expect(__ballot(hit) != 0ull, 0) && ib < b1) {
 #pragma unroll
         for (int g = 0; g < NQG; ++g) {
           bool hg = false;
@@ -1012,15 +1016,21 @@ __global__ __launch_bounds__(256) void mips_filter_kernel(FilterArgs a) {
     // (a slot is refilled PD blocks ahead as soon as it is consumed)
     constexpr int PD = 4;
     Frag f[PD];
+    // issue order f[0], f[1], ... pinned (sched_barrier): the loop's waits count loads in
+    // that order, and a reordered prologue made hipcc drain vmcnt(0) every iteration
 #pragma unroll
-    for (int u = 0; u < PD; ++u) load(f[u], b0 + u);
+    for (int u = 0; u < PD; ++u) {
+      load(f[u], b0 + u);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // whole rounds of PD blocks, no early exit inside (a branch there let the prologue's
+    // and the loop's pending loads disagree, and hipcc drained vmcnt(0) per round);
+    // blocks past b1 are clamped re-reads that process() ignores
     for (int64_t ib = b0; ib < b1; ib += PD) {
 #pragma unroll
       for (int u = 0; u < PD; ++u) {
-        if (ib + u >= b1) break;
-        const Frag cur = f[u];
-        load(f[u], ib + u + PD);
-        process(cur, ib + u);
+        process(f[u], ib + u);
+        load(f[u], ib + u + PD);  // into the registers just consumed: no copies
       }
     }
   } else if (!SAMPLE && b0 < b1) {
@@ -1044,10 +1054,36 @@ __global__ __launch_bounds__(256) void mips_filter_kernel(FilterArgs a) {
       for (int e = threadIdx.x; e < n; e += 256) {
         const int src = w * WV_CAP + e;
         const int qq = qb + l_q[src];
+        float sc = l_s[src];
+        if constexpr (BF) {
+          // exact f32 score of the hit: the k-ordered fmaf chain over d < D (the f32
+          // MFMA's and the oracle's) from the row-major copy; the row's and the query's
+          // float4 loads are issued together
+          typedef float fv4 __attribute__((ext_vector_type(4)));
+          gptr<fv4> xr = as_global(reinterpret_cast<const fv4*>(a.rows)) +
+                         (int64_t)l_i[src] * (a.DP >> 2);
+          gptr<fv4> qr = as_global(reinterpret_cast<const fv4*>(a.q_rows)) +
+                         (int64_t)qq * (a.DP >> 2);
+          fv4 xv[16], qv[16];
+#pragma unroll
+          for (int j = 0; j < 16; ++j)
+            if (4 * j < a.DP) {
+              xv[j] = xr[j];
+              qv[j] = qr[j];
+            }
+          sc = 0.f;
+#pragma unroll
+          for (int j = 0; j < 16; ++j) {
+            if (4 * j < a.D) sc = fmaf(xv[j].x, qv[j].x, sc);
+            if (4 * j + 1 < a.D) sc = fmaf(xv[j].y, qv[j].y, sc);
+            if (4 * j + 2 < a.D) sc = fmaf(xv[j].z, qv[j].z, sc);
+            if (4 * j + 3 < a.D) sc = fmaf(xv[j].w, qv[j].w, sc);
+          }
+        }
         const int64_t sub = (int64_t)qq * NSUB + (blockIdx.x & (NSUB - 1));
         const int pos = atomicAdd(&a.cnt[sub], 1);
         if (pos < SUBCAP) {
-          a.cand_s[sub * SUBCAP + pos] = l_s[src];
+          a.cand_s[sub * SUBCAP + pos] = sc;
           a.cand_i[sub * SUBCAP + pos] = l_i[src];
         }
       }
@@ -1083,6 +1119,8 @@ struct TauArgs {
   float* tau_e;            // exactness threshold of the rescored candidates
   int* cnt;
   int* flag;
+  float* q_rows;           // bf16 filter: the queries padded to DP floats (for the rescoring)
+  int DP;
 };
 
 // tau~ = M_SAMPLE-th largest group max (one workgroup per query).  f32 filter:
@@ -1103,6 +1141,7 @@ __global__ __launch_bounds__(256) void mips_tau_kernel(TauArgs a) {
   int k_rem;
   block_radix_kth(key, a.G, m, L, kstar, k_rem);
   if (tid < NSUB) a.cnt[q * NSUB + tid] = 0;
+  if (a.q_rows && tid < a.DP) a.q_rows[(int64_t)q * a.DP + tid] = tid < a.D ? a.q[(int64_t)q * a.D + tid] : 0.f;
   if (tid == 0) {
     const float t = key_to_float(kstar);
     if (a.maxnorm) {
@@ -1137,46 +1176,6 @@ struct FilterMergeArgs {
   int rescore;
   const float* tau_e;
 };
-
-// bf16 filter: every collected candidate's exact score, in place.  One workgroup per
-// (query, sub-list), one candidate per thread: the k-ordered fmaf chain over d < D (the
-// f32 MFMA's and the oracle's) over the candidate's row of the row-major copy, whose
-// DP/4 float4 loads are issued together.
-struct RescoreArgs {
-  float* cand_s;
-  const int* cand_i;
-  const int* cnt;
-  const float* rows;  // DP floats per item
-  int DP;
-  const float* q;
-  int D;
-};
-
-__global__ __launch_bounds__(SUBCAP) void mips_rescore_kernel(RescoreArgs a) {
-  __shared__ float q_s[64];
-  const int q = blockIdx.y, tid = threadIdx.x;
-  const int64_t sub = (int64_t)q * NSUB + blockIdx.x;
-  if (tid < 64) q_s[tid] = tid < a.D ? a.q[(int64_t)q * a.D + tid] : 0.f;
-  __syncthreads();
-  const int n = a.cnt[sub];
-  if (tid >= (n < SUBCAP ? n : SUBCAP)) return;
-  typedef float fv4 __attribute__((ext_vector_type(4)));
-  gptr<fv4> r = as_global(reinterpret_cast<const fv4*>(a.rows)) +
-                (int64_t)a.cand_i[sub * SUBCAP + tid] * (a.DP >> 2);
-  fv4 v[16];
-#pragma unroll
-  for (int j = 0; j < 16; ++j)
-    if (4 * j < a.DP) v[j] = r[j];
-  float s = 0.f;
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    if (4 * j < a.D) s = fmaf(v[j].x, q_s[4 * j], s);
-    if (4 * j + 1 < a.D) s = fmaf(v[j].y, q_s[4 * j + 1], s);
-    if (4 * j + 2 < a.D) s = fmaf(v[j].z, q_s[4 * j + 2], s);
-    if (4 * j + 3 < a.D) s = fmaf(v[j].w, q_s[4 * j + 3], s);
-  }
-  a.cand_s[sub * SUBCAP + tid] = s;
-}
 
 __global__ __launch_bounds__(256) void mips_filter_merge_kernel(FilterMergeArgs a) {
   __shared__ uint32_t key[FILTER_CAP];
@@ -1229,7 +1228,7 @@ __global__ __launch_bounds__(256) void mips_filter_merge_kernel(FilterMergeArgs 
       }
       __syncthreads();
     }
-  // bf16 filter: cs holds the exact scores (mips_rescore_kernel); only candidates at
+  // bf16 filter: cs holds the exact scores (rescored at the filter's flush); only candidates at
   // or above tau_e are provably complete
   const float te = a.rescore ? a.tau_e[q] : -INFINITY;
   int nvalid = 0;
@@ -1267,7 +1266,7 @@ struct TopkPlan {
   int64_t n_blocks, RB;
   int GB, G, NQG, n_chunks, filter_waves, sr;
   int KC;              // > 0: the filter scores the bf16 copy (KC k-chunks of 32 dims)
-  size_t off_tau, off_tau_e, off_cnt, off_smax, off_cs, off_ci, off_part, total_bytes;
+  size_t off_tau, off_tau_e, off_qrows, off_cnt, off_smax, off_cs, off_ci, off_part, total_bytes;
 };
 
 static size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
@@ -1340,7 +1339,8 @@ static TopkPlan plan_topk(int B, int64_t X, int D, int k) {
     p.NQG = B <= 32 ? 2 : 8;
     p.n_chunks = ceil_div(B, p.NQG * 16);
     // whole rounds of 2 four-wave workgroups per CU, >= ~48 blocks per wave
-    const int64_t per_round = (int64_t)device_cus() * 8;
+    static const char* env_wgs = getenv("GR_MIPS_FILTER_WGS");  // tuning knob: WGs per CU
+    const int64_t per_round = (int64_t)device_cus() * 4 * (env_wgs ? atoi(env_wgs) : 2);
     // GR_MIPS_FP32_FILTER=1: filter on the f32 table (exact scores, 16x fewer flop/s)
     p.KC = getenv("GR_MIPS_FP32_FILTER") ? 0 : pack_layout(X, D).KC;
     // f32: >= ~48 blocks per wave.  bf16 (streaming-bound): one round (10M items: 7
@@ -1355,6 +1355,7 @@ static TopkPlan plan_topk(int B, int64_t X, int D, int k) {
     size_t o = 256;  // [0, 4): fallback flag
     p.off_tau = o;  o = align256(o + sizeof(float) * B);
     p.off_tau_e = o; o = align256(o + sizeof(float) * B);
+    p.off_qrows = o; o = align256(o + sizeof(float) * B * 64);  // bf16 filter: padded f32 queries
     p.off_cnt = o;  o = align256(o + sizeof(int) * B * NSUB);
     p.off_smax = o; o = align256(o + sizeof(float) * (size_t)B * p.G);
     p.off_cs = o;   o = align256(o + sizeof(float) * (size_t)B * FILTER_CAP);
@@ -1493,20 +1494,17 @@ extern "C" int mips_topk(const float* queries, const float* packed_items, int64_
     FilterArgs f{queries, packed_items, p.KC ? (const u32x4*)(pbase + L.off16) : nullptr, X, D, B,
                  p.n_blocks, p.GB, p.G, p.sr, (float*)(ws + p.off_smax),
                  p.RB, tau, cnt, (float*)(ws + p.off_cs), (int*)(ws + p.off_ci), (int*)ws,
-                 getenv("GR_MIPS_DEBUG_NOHIT") != nullptr};
+                 getenv("GR_MIPS_DEBUG_NOHIT") != nullptr,
+                 p.KC ? (const float*)(pbase + L.off_rows) : nullptr, (float*)(ws + p.off_qrows),
+                 L.DP};
     int rc = launch_filter(f, p, true, st);
     if (rc) return rc;
     TauArgs ta{f.smax, p.G, queries, D, p.KC ? (const uint32_t*)(pbase + L.off_norm) : nullptr,
-               tau, tau_e, cnt, flag};
+               tau, tau_e, cnt, flag, p.KC ? (float*)(ws + p.off_qrows) : nullptr, L.DP};
     GR_TIMED("mips_tau", st, hipLaunchKernelGGL(mips_tau_kernel, dim3(B), dim3(256), 0, st, ta));
     GR_LAUNCH_CHECK("mips_topk(tau)");
     rc = launch_filter(f, p, false, st);
     if (rc) return rc;
-    if (p.KC) {
-      RescoreArgs ra{f.cand_s, f.cand_i, cnt, (const float*)(pbase + L.off_rows), L.DP, queries, D};
-      GR_TIMED("mips_rescore", st, hipLaunchKernelGGL(mips_rescore_kernel, dim3(NSUB, B), dim3(SUBCAP), 0, st, ra));
-      GR_LAUNCH_CHECK("mips_topk(rescore)");
-    }
     FilterMergeArgs fm{f.cand_s, f.cand_i, cnt, B, k, N0, item_ids, index_base, invalid_ids,
                        out_scores, out_ids, out_index, flag, p.KC > 0, tau_e};
     GR_TIMED("mips_merge", st, hipLaunchKernelGGL(mips_filter_merge_kernel, dim3(B), dim3(256), 0, st, fm));

@@ -37,6 +37,13 @@ class _Emb(torch.nn.Module):
         return torch.nn.functional.embedding(ids, self.weight)
 
 
+class _IselEmb(_Emb):
+    """Row gather by index_select (backward: index_add_)."""
+
+    def get_item_embeddings(self, ids):
+        return self.weight.index_select(0, ids.reshape(-1)).view(*ids.shape, self.weight.shape[1])
+
+
 def _sampler(l2_norm, all_ids, offsets, emb):
     from mygenerativerecommenders_amd.negatives_sampler import LocalNegativesSampler
 
@@ -222,7 +229,7 @@ def test_loss_graph_replays_match_eager():
     from mygenerativerecommenders_amd.losses import SampledSoftmaxLoss
     from mygenerativerecommenders_amd.similarity import DotProductSimilarity
     dev = torch.device("cuda")
-    emb = _Emb(torch.as_tensor(weight).to(dev))
+    emb = _IselEmb(torch.as_tensor(weight).to(dev))
     s = _sampler(True, torch.as_tensor(ids), torch.as_tensor(offsets).to(dev), emb)
     o = torch.as_tensor(out).to(dev).requires_grad_(True)
     p = torch.as_tensor(sup_emb).to(dev).requires_grad_(True)
