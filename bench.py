@@ -152,29 +152,14 @@ def _gpu_hold_fn():
     return hold
 
 
-class _ItemEmbeddings(torch.nn.Module):
-    """LocalEmbeddingModule (embedding_modules.py): (V + 1, D) table, truncated-normal
-    std 0.02, id 0 = padding.  Rows are gathered with index_select (backward: index_add_)
-    rather than F.embedding, whose sort-based backward faulted under HIP-graph replay
-    here for some index patterns (a permuted id list)."""
-
-    def __init__(self, num_items, D):
-        super().__init__()
-        from mygenerativerecommenders_amd.preprocessors import _truncated_normal_
-        self.weight = torch.nn.Parameter(torch.empty(num_items + 1, D))
-        _truncated_normal_(self.weight.data, 0.0, 0.02)
-
-    def get_item_embeddings(self, ids):
-        return self.weight.index_select(0, ids.reshape(-1)).view(*ids.shape, self.weight.shape[1])
-
-
 def e2e_train_leg(args, device, world, lengths, ts, past_ids):
     """The whole reference training step (train.py train_fn inner loop, ml-1m config:
     SampledSoftmaxLoss with 128 local negatives, temperature 0.05, l2-normalised items):
-    item-embedding lookup -> positional preprocessor -> HSTU -> L2 postprocessor ->
+    LocalEmbeddingModule lookup -> positional preprocessor -> HSTU -> L2 postprocessor ->
     jagged sampled-softmax loss -> backward -> gradient all-reduce -> AdamW.
     Reported beside the headline, which times the encoder step the north star names."""
     from mygenerativerecommenders_amd.distributed import FlatGradAllReducer
+    from mygenerativerecommenders_amd.embeddings import LocalEmbeddingModule
     from mygenerativerecommenders_amd.losses import SampledSoftmaxLoss
     from mygenerativerecommenders_amd.negatives_sampler import LocalNegativesSampler
     from mygenerativerecommenders_amd.ops import (asynchronous_complete_cumsum,
@@ -187,7 +172,7 @@ def e2e_train_leg(args, device, world, lengths, ts, past_ids):
     N = N0 + out_len
     V = args.catalog
     enc = build_model(N0, out_len, D, blocks, device)
-    emb = _ItemEmbeddings(V, D).to(device)
+    emb = LocalEmbeddingModule(V, D).to(device)  # no year CSV: every year row is 0
     pre = Pre(N, D, 0.2).to(device).train()
     sampler = LocalNegativesSampler(True, 1e-6, all_item_ids=list(range(1, V + 1))).to(device)
     sampler._embeddings_module = emb

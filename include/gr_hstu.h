@@ -95,6 +95,23 @@ GR_API int gr_preproc_bwd(const float* dy, const int64_t* past_ids, int B, int N
                           float dropout_p, uint64_t seed, const int64_t* seed_offset, float* dx,
                           float* dpos_w, void* stream);
 
+/* ---------------------------------------------------------------- item embeddings
+ * Replaces LocalEmbeddingModule.get_item_embeddings (embeddings/embeddings.py:94-97):
+ *   out[i] = cat(w0[ids[i]], w1[map1[clamp(ids[i], 0, map_len - 1)]])     (n, d0 + d1)
+ * w0 (rows0, d0) is the item table, w1 (rows1, d1) the year table and map1 the item ->
+ * year lookup (map1 NULL: w1 is indexed by the id itself; w1 NULL: a plain gather, as
+ * CategoricalEmbeddingModule uses with its mapped ids).  Ids outside a table read 0.
+ * Backward: dw0 / dw1 (either may be NULL) are zeroed, then dW[row] += dout[i] for every
+ * gathering i, except row padding_idx (nn.Embedding padding_idx; < 0 = none); fp32
+ * atomics, unordered like index_add_. */
+GR_API int gr_item_embedding_fwd(const int64_t* ids, int64_t n, const float* w0, int64_t rows0,
+                                 int d0, const float* w1, int64_t rows1, int d1,
+                                 const int64_t* map1, int64_t map_len, float* out, void* stream);
+GR_API int gr_item_embedding_bwd(const int64_t* ids, int64_t n, const float* dout, int64_t rows0,
+                                 int d0, int64_t rows1, int d1, const int64_t* map1,
+                                 int64_t map_len, int64_t padding_idx, float* dw0, float* dw1,
+                                 void* stream);
+
 /* ---------------------------------------------------------------- sampled-softmax loss
  * Fused LocalNegativesSampler.forward (negative_sampler.py:105-131, after its randint) +
  * DotProductSimilarity.forward (dot_product.py:31-64) + SampledSoftmaxLoss.jagged_forward

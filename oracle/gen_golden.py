@@ -21,13 +21,16 @@ Fixtures written:
   * ``preproc.npz``            -- ``LearnablePositionalEmbeddingInputFeaturesPreprocessor``
     (``learnable_positional_embedding.py:42-58``), eval mode, with input / table grads.
   * ``muon.npz``               -- two ``Muon.step`` (``optimizers/muon.py:46-86``) on CPU.
+  * ``embeddings.npz``         -- ``LocalEmbeddingModule.get_item_embeddings``
+    (``embeddings/embeddings.py:94-97``) with an installed item -> year mapping, and the
+    gradients of both tables.
   * ``ssm_*.npz``              -- ``SampledSoftmaxLoss.jagged_forward``
     (``autoregressive_losses.py:259-306``) with ``LocalNegativesSampler``
     (``negative_sampler.py:66-131``) and ``DotProductSimilarity``: inputs, the seed of
     the sampling draw, the sampled ids / offsets it produced, the loss and the
     gradients of the query rows, the supervision embeddings and the embedding table.
 
-Usage:  python oracle/gen_golden.py [--only loss|preproc|muon]   (writes tests/golden/*.npz)
+Usage:  python oracle/gen_golden.py [--only loss|preproc|muon|embeddings]   (writes tests/golden/*.npz)
 """
 from __future__ import annotations
 
@@ -323,6 +326,34 @@ def gen_preprocessor():
     print(f"preproc: y {tuple(y.shape)}")
 
 
+def gen_embeddings():
+    """LocalEmbeddingModule.get_item_embeddings (embeddings/embeddings.py:94-97) and the
+    gradients of its two tables, with an item -> year mapping installed in the module's
+    ``item2year`` global (the reference fills it from a CSV that does not exist here)."""
+    if REF_SRC not in sys.path:
+        sys.path.insert(0, REF_SRC)
+    import generative_recommenders_pl.models.embeddings.embeddings as E  # noqa
+    torch.manual_seed(51)
+    num_items, dim = 2100, 50
+    g = torch.Generator().manual_seed(52)
+    years = torch.randint(1919, 2001, (num_items,), generator=g)
+    E.item2year = {i + 1: int(years[i]) for i in range(0, num_items - 300)}  # ids > 1800 unmapped
+    m = E.LocalEmbeddingModule(num_items=num_items, item_embedding_dim=dim)
+    ids = torch.randint(0, num_items + 1, (5, 37), generator=g)
+    ids[1, 20:] = 0
+    ids[3, :5] = 1799
+    out = m.get_item_embeddings(ids)
+    dout = torch.randn(out.shape, generator=g)
+    (out * dout).sum().backward()
+    np.savez_compressed(os.path.join(OUT, "embeddings.npz"), ids=ids.numpy(),
+                        item_w=m._item_emb.weight.detach().numpy(),
+                        year_w=m._year_emb.weight.detach().numpy(),
+                        year_table=m.year_lookup_table.numpy(), out=out.detach().numpy(),
+                        dout=dout.numpy(), d_item_w=m._item_emb.weight.grad.numpy(),
+                        d_year_w=m._year_emb.weight.grad.numpy())
+    print(f"embeddings: out {tuple(out.shape)}")
+
+
 def gen_muon():
     """Two steps of the reference Muon (optimizers/muon.py:46-86) on CPU over parameters of
     three shape classes (wide, tall, two square of one shape) with fixed gradients."""
@@ -366,9 +397,13 @@ def main():
     if only == "muon":
         gen_muon()
         return
+    if only == "embeddings":
+        gen_embeddings()
+        return
     gen_sampled_softmax()
     gen_preprocessor()
     gen_muon()
+    gen_embeddings()
     HSTU, CandidateIndex, MIPSBruteForceTopK, ops = _import_reference()
     gen_bucket_thresholds(HSTU)
     gen_jagged_ops(ops)

@@ -102,3 +102,23 @@ def test_bench_flop_accounting():
     # target timestamp sits at index L (features.py:53-57) and padding is 0
     assert (ts[:, 200] > 0).all() and (ts[:, 201:] == 0).all()
     assert (past_ids[:, 200:] == 0).all()
+
+
+def test_local_embedding_module_layout_and_year_table(tmp_path):
+    """embeddings.py:40-101 layout: half-width item and year tables, the item -> year
+    lookup buffer (empty mapping -> zeros of num_items + 1), CSV loading, clamping."""
+    import torch
+
+    from mygenerativerecommenders_amd.embeddings import LocalEmbeddingModule
+    m = LocalEmbeddingModule(100, 50)
+    assert m._item_emb.weight.shape == (101, 25) and m._year_emb.weight.shape == (101, 25)
+    assert m.year_lookup_table.shape == (101,) and not m.year_lookup_table.any()
+    assert m.item_embedding_dim == 50 and m.debug_str() == "local_emb_d50"
+    assert m._item_emb.weight[0].abs().sum() > 0  # reset_params re-inits the padding row too
+    csv_path = tmp_path / "movies.csv"
+    csv_path.write_text("movie_id,title,year\n1,a,1995\n7,b,2000\n")
+    m2 = LocalEmbeddingModule(100, 50, movies_csv=str(csv_path))
+    assert m2.year_lookup_table.shape == (8,)
+    assert m2.year_lookup_table[1] == 1995 and m2.year_lookup_table[7] == 2000
+    ids = torch.tensor([0, 1, 7, 50, -3])
+    assert m2.lookup_year_ids(ids).tolist() == [0, 1995, 2000, 2000, 0]

@@ -160,3 +160,16 @@ def test_preproc_oracle_matches_reference_golden():
     dx, dpos = preproc_oracle.preprocess_bwd(z["dy"], z["ids"], D ** 0.5, z["pos_w"].shape[0])
     assert np.allclose(dx, z["dx"], rtol=1e-6, atol=1e-6)
     assert np.allclose(dpos, z["dpos"], rtol=1e-5, atol=1e-6)
+
+
+# ---------------------------------------------------------------- item embeddings (N2)
+
+def test_embedding_oracle_matches_reference_golden():
+    from oracle import embedding_oracle as EO
+    z = np.load(os.path.join(GOLDEN, "embeddings.npz"))
+    out = EO.get_item_embeddings(z["ids"], z["item_w"], z["year_w"], z["year_table"])
+    assert np.array_equal(out, z["out"])  # a gather: bit-exact
+    dw0, dw1 = EO.get_item_embeddings_bwd(z["ids"], z["dout"], z["item_w"].shape[0],
+                                          z["year_w"].shape[0], z["year_table"])
+    assert np.allclose(dw0, z["d_item_w"], rtol=1e-5, atol=1e-6)
+    assert np.allclose(dw1, z["d_year_w"], rtol=1e-5, atol=1e-6)
