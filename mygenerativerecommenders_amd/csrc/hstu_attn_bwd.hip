@@ -86,10 +86,6 @@ struct AttnBwdCfg {
   static constexpr int LDV = VP + 4;
 };
 
-__device__ __forceinline__ float silu_grad_masked(const float* h, int64_t idx, bool ok) {
-  const float x = as_global(h)[idx];
-  return ok ? silu_grad_(x) : 0.f;
-}
 
 // ------------------------------------------------------------------ key-major: dK, dV
 // Per 16 x 16 (query, key) block a wave computes S and dP (A = Q / dO rows from LDS,
@@ -194,6 +190,28 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
   };
 
   const int wk_lo = k0 + w * 16;
+  // the epilogue's silu'(h) inputs, loaded now so they land during the main loop (a load
+  // at the end put one more HBM round trip on every workgroup's tail: +16 us per launch)
+  float hv_pre[4][VTILES], hk_pre[4][C::KT];
+  if (a.hv) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int key = wk_lo + 4 * lg + r;
+      const int64_t row = s0 + (key < L ? key : L - 1);
+      gptr<float> hvr = as_global(a.hv) + row * a.ld_h + h * a.dv;
+      gptr<float> hkr = as_global(a.hk) + row * a.ld_h + h * a.dqk;
+#pragma unroll
+      for (int t = 0; t < VTILES; ++t) {
+        const int c = t * 16 + lr;
+        hv_pre[r][t] = hvr[c < a.dv ? c : a.dv - 1];
+      }
+#pragma unroll
+      for (int t = 0; t < C::KT; ++t) {
+        const int c = t * 16 + lr;
+        hk_pre[r][t] = hkr[c < a.dqk ? c : a.dqk - 1];
+      }
+    }
+  }
   const int last_qt = (L - 1) / TT;
   load_tile(k0 / TT, mw);
   qst.store(Qs, C::LDQ, a.vec2);
@@ -394,7 +412,7 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
       const int c = t * 16 + lr;
       const bool ok = row_ok && c < a.dv;
       float g = dV[t][r];
-      if (a.hv) g *= silu_grad_masked(a.hv, row * a.ld_h + h * a.dv + (c < a.dv ? c : a.dv - 1), ok);
+      if (a.hv) g *= ok ? silu_grad_(hv_pre[r][t]) : 0.f;
       if (ok) a.dvv[row * a.ld_d + h * a.dv + c] = g;
     }
 #pragma unroll
@@ -402,7 +420,7 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
       const int c = t * 16 + lr;
       const bool ok = row_ok && c < a.dqk;
       float g = dK[t][r];
-      if (a.hk) g *= silu_grad_masked(a.hk, row * a.ld_h + h * a.dqk + (c < a.dqk ? c : a.dqk - 1), ok);
+      if (a.hk) g *= ok ? silu_grad_(hk_pre[r][t]) : 0.f;
       if (ok) a.dk[row * a.ld_d + h * a.dqk + c] = g;
     }
   }
@@ -477,6 +495,19 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& a, const int
 #pragma unroll
   for (int t = 0; t < C::KT; ++t) dQ[t] = f4_zero();
   const int wq_lo = q0 + w * 16;
+  float hq_pre[4][C::KT];  // the epilogue's silu'(h) inputs, prefetched (see the dK/dV body)
+  if (a.hq) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int qo = wq_lo + 4 * lg + r;
+      gptr<float> hqr = as_global(a.hq) + (s0 + (qo < L ? qo : L - 1)) * a.ld_h + h * a.dqk;
+#pragma unroll
+      for (int t = 0; t < C::KT; ++t) {
+        const int c = t * 16 + lr;
+        hq_pre[r][t] = hqr[c < a.dqk ? c : a.dqk - 1];
+      }
+    }
+  }
 
   BufTile<C::KPT, TT> kst;
   BufTile<C::VP, TT> vst;
@@ -569,7 +600,7 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& a, const int
       const int c = t * 16 + lr;
       const bool ok = row_ok && c < a.dqk;
       float g = dQ[t][r];
-      if (a.hq) g *= silu_grad_masked(a.hq, row * a.ld_h + h * a.dqk + (c < a.dqk ? c : a.dqk - 1), ok);
+      if (a.hq) g *= ok ? silu_grad_(hq_pre[r][t]) : 0.f;
       if (ok) a.dq[row * a.ld_d + h * a.dqk + c] = g;
     }
   }

@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--batch", type=int, default=0, help="override B")
     ap.add_argument("--len", type=int, default=0, help="override L (N = L + 11)")
     ap.add_argument("--nobias", action="store_true", help="no relative bias (timestamps absent)")
+    ap.add_argument("--hepi", action="store_true",
+                    help="fused silu'(h) epilogue on dQ/dK/dV (as in the training step)")
     args = ap.parse_args()
     B, N, L, d, H = SHAPES[args.shape]
     if args.batch:
@@ -77,10 +79,15 @@ def main():
                   offsets.data_ptr(), B, N, L, H, d, d, _lib.ptr(bmap), pos_w.data_ptr(),
                   ts_w.data_ptr(), 128, out.data_ptr(), hv, st)
 
+    h = torch.randn(rows, n_out, device=dev, generator=g) if args.hepi else None
+    hq = h[:, 2 * hv:3 * hv].data_ptr() if args.hepi else None
+    hk = h[:, 3 * hv:].data_ptr() if args.hepi else None
+    hvp = h[:, hv:2 * hv].data_ptr() if args.hepi else None
+
     def bwd():
         _lib.call("hstu_attn_bwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out, n_out,
                   dout.data_ptr(), hv, offsets.data_ptr(), B, N, L, H, d, d, _lib.ptr(bmap),
-                  pos_w.data_ptr(), ts_w.data_ptr(), 128, None, None, None, 0,
+                  pos_w.data_ptr(), ts_w.data_ptr(), 128, hq, hk, hvp, n_out if args.hepi else 0,
                   dq.data_ptr(), dk.data_ptr(), dvv.data_ptr(), n_out, dpw.data_ptr(),
                   dtw.data_ptr(), ws.data_ptr(), ws_n, st)
 
