@@ -94,7 +94,8 @@ struct RowWaveCfg {
 //   K, N, offsets/B (total rows = offsets[B]); weight W'(k, n) = w[k * bks() + n * bns()],
 //   K_CONTIG: bks() == 1 (staging walks k fastest);
 //   setup(total); load(src, m, lg) issues a unit's input loads; prep(src, a, m, row_ok, lg)
-//   turns them into the A quads; epi(acc, m, row_ok, lg) consumes acc[t][e] =
+//   turns them into the A quads; epi_load(es, m, row_ok, lg) issues the epilogue's row
+//   inputs before the MFMAs; epi(acc, es, m, row_ok, lg) consumes acc[t][e] =
 //   C[m][qcol(16t, lg, e)].
 template <int KG, int NT, class Op>
 __global__ __launch_bounds__(256) void rowwave_kernel(Op op) {
@@ -156,6 +157,10 @@ __global__ __launch_bounds__(256) void rowwave_kernel(Op op) {
     if (more) op.load(nxt, m + ustep * 16, lg);
     float a[KG][4];
     op.prep(cur, a, m, m < total, lg);
+    // the epilogue's own row inputs are issued now, so they land while the MFMAs run
+    // (loaded inside epi they added one dependent round trip per unit)
+    typename Op::Epi es;
+    op.epi_load(es, m, m < total, lg);
     f4 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = f4_zero();
@@ -188,12 +193,12 @@ __global__ __launch_bounds__(256) void rowwave_kernel(Op op) {
       __builtin_amdgcn_sched_barrier(0);
     }
 #ifndef GR_RW_NOSTORE
-    op.epi(acc, m, m < total, lg);
+    op.epi(acc, es, m, m < total, lg);
 #else
     float sink = 0.f;
 #pragma unroll
     for (int t = 0; t < NT; ++t) sink += acc[t][0] + acc[t][1] + acc[t][2] + acc[t][3];
-    if (sink == 1.2345f) op.epi(acc, m, m < total, lg);
+    if (sink == 1.2345f) op.epi(acc, es, m, m < total, lg);
 #endif
     if (more) cur = nxt;
   }
@@ -253,7 +258,9 @@ struct RwLnUvqk {
         a[g][e] = qcol<VEC>(16 * g, lg, e) < K ? (s.v[g][e] - mean) * rstd : 0.f;
     if (lg == 0 && row_ok) x_stats[m] = make_float2(mean, rstd);
   }
-  __device__ void epi(f4 (&acc)[NT], int64_t m, bool, int lg) const {
+  struct Epi {};
+  __device__ void epi_load(Epi&, int64_t, bool, int) const {}
+  __device__ void epi(f4 (&acc)[NT], const Epi&, int64_t m, bool, int lg) const {
     // rows past the end fall outside the descriptors (stores dropped)
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -347,11 +354,18 @@ struct RwGateO {
     }
     if (lg == 0 && row_ok) a_stats[m] = make_float2(mean, rstd);
   }
-  __device__ void epi(f4 (&acc)[NT], int64_t m, bool, int lg) const {
+  struct Epi { f4 xv[NT], bv[NT]; };
+  __device__ void epi_load(Epi& es, int64_t m, bool, int lg) const {
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      const f4 xv = ldq<VEC>(rx, m * ldx, 16 * t, lg, N);  // 0 when xres is NULL
-      const f4 bv = ldq<VEC>(rb, 0, 16 * t, lg, N);        // 0 when bias is NULL
+      es.xv[t] = ldq<VEC>(rx, m * ldx, 16 * t, lg, N);  // 0 when xres is NULL
+      es.bv[t] = ldq<VEC>(rb, 0, 16 * t, lg, N);        // 0 when bias is NULL
+    }
+  }
+  __device__ void epi(f4 (&acc)[NT], const Epi& es, int64_t m, bool, int lg) const {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const f4 xv = es.xv[t], bv = es.bv[t];
       f4 o;
 #pragma unroll
       for (int e = 0; e < 4; ++e) o[e] = (acc[t][e] + bv[e]) + xv[e];
@@ -409,15 +423,23 @@ struct RwGateOBwd {
 #pragma unroll
       for (int e = 0; e < 4; ++e) a[g][e] = s.v[g][e];  // columns >= K loaded as 0
   }
-  __device__ void epi(f4 (&acc)[NT], int64_t m, bool row_ok, int lg) const {
-    const float2 st = ld_f2(a_stats, row_ok ? m : 0);
+  struct Epi { float2 st; f4 av[NT], uv[NT], hv[NT]; };
+  __device__ void epi_load(Epi& es, int64_t m, bool row_ok, int lg) const {
+    es.st = ld_f2(a_stats, row_ok ? m : 0);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      es.av[t] = ldq<VEC>(ra, m * lda, 16 * t, lg, N);
+      es.uv[t] = ldq<VEC>(ru, m * ldu, 16 * t, lg, N);
+      es.hv[t] = ldq<VEC>(rh, m * ldh, 16 * t, lg, N);  // 0 when h_u is NULL
+    }
+  }
+  __device__ void epi(f4 (&acc)[NT], const Epi& es, int64_t m, bool row_ok, int lg) const {
+    const float2 st = es.st;
     float s1 = 0.f, s2 = 0.f;
     f4 lnv[NT], dln[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      const f4 av = ldq<VEC>(ra, m * lda, 16 * t, lg, N);
-      const f4 uv = ldq<VEC>(ru, m * ldu, 16 * t, lg, N);
-      const f4 hv = ldq<VEC>(rh, m * ldh, 16 * t, lg, N);  // 0 when h_u is NULL
+      const f4 av = es.av[t], uv = es.uv[t], hv = es.hv[t];
       f4 duv;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -486,13 +508,22 @@ struct RwLnUvqkBwd {
 #pragma unroll
       for (int e = 0; e < 4; ++e) a[g][e] = s.v[g][e];
   }
-  __device__ void epi(f4 (&acc)[NT], int64_t m, bool row_ok, int lg) const {
-    const float2 st = ld_f2(x_stats, row_ok ? m : 0);
+  struct Epi { float2 st; f4 xv[NT], dyv[NT]; };
+  __device__ void epi_load(Epi& es, int64_t m, bool row_ok, int lg) const {
+    es.st = ld_f2(x_stats, row_ok ? m : 0);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      es.xv[t] = ldq<VEC>(rx, m * ldx, 16 * t, lg, N);
+      es.dyv[t] = ldq<VEC>(rdy, m * lddy, 16 * t, lg, N);  // 0 when dy is NULL
+    }
+  }
+  __device__ void epi(f4 (&acc)[NT], const Epi& es, int64_t m, bool row_ok, int lg) const {
+    const float2 st = es.st;
     float s1 = 0.f, s2 = 0.f;
     f4 xh[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      const f4 xv = ldq<VEC>(rx, m * ldx, 16 * t, lg, N);
+      const f4 xv = es.xv[t];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const bool ok = row_ok && qcol<VEC>(16 * t, lg, e) < N;
@@ -508,7 +539,7 @@ struct RwLnUvqkBwd {
     const float mean1 = s1 * inv, mean2 = s2 * inv;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      const f4 dyv = ldq<VEC>(rdy, m * lddy, 16 * t, lg, N);  // 0 when dy is NULL
+      const f4 dyv = es.dyv[t];
       f4 o;
 #pragma unroll
       for (int e = 0; e < 4; ++e) o[e] = dyv[e] + st.y * (acc[t][e] - mean1 - xh[t][e] * mean2);
