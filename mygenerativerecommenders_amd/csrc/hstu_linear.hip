@@ -183,6 +183,10 @@ __global__ __launch_bounds__(256) void rowpanel_kernel(Op op) {
   f4 acc[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = f4_zero();
+  // the epilogue's own row inputs (LayerNorm-backward rows, residuals), issued now so
+  // they land during the K loop instead of adding a round trip at the workgroup's end
+  typename Op::template Epi<NT> es;
+  op.epi_load(es, m0 + w * 16 + 4 * lg, n0 + lr, total);
 
   load(0);
   store(0);
@@ -220,7 +224,7 @@ __global__ __launch_bounds__(256) void rowpanel_kernel(Op op) {
     }
   }
   // acc[t][r] = C[m0 + 16w + 4lg + r][n0 + 16t + lr]
-  op.epilogue(acc, m0 + w * 16 + 4 * lg, n0 + lr, total);
+  op.epilogue(acc, es, m0 + w * 16 + 4 * lg, n0 + lr, total);
 }
 
 // descriptor over rows [m0, total) of a (rows, ld) matrix (column offset folded in base)
@@ -270,7 +274,11 @@ struct OpLnUvqk {
   __device__ int bks() const { return N; }
   __device__ int bns() const { return 1; }
   template <int NT>
-  __device__ void epilogue(f4 (&acc)[NT], int64_t mrow, int ncol, int64_t total) const {
+  struct Epi {};
+  template <int NT>
+  __device__ void epi_load(Epi<NT>&, int64_t, int, int64_t) const {}
+  template <int NT>
+  __device__ void epilogue(f4 (&acc)[NT], const Epi<NT>&, int64_t mrow, int ncol, int64_t total) const {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int64_t m = mrow + r;
@@ -331,7 +339,11 @@ struct OpGateO {
   __device__ int bks() const { return 1; }
   __device__ int bns() const { return K; }
   template <int NT>
-  __device__ void epilogue(f4 (&acc)[NT], int64_t mrow, int ncol, int64_t total) const {
+  struct Epi {};
+  template <int NT>
+  __device__ void epi_load(Epi<NT>&, int64_t, int, int64_t) const {}
+  template <int NT>
+  __device__ void epilogue(f4 (&acc)[NT], const Epi<NT>&, int64_t mrow, int ncol, int64_t total) const {
     float bv[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -390,7 +402,11 @@ struct OpGateOBwd : NoStats {
   __device__ int bks() const { return N; }
   __device__ int bns() const { return 1; }
   template <int NT>
-  __device__ void epilogue(f4 (&acc)[NT], int64_t mrow, int ncol, int64_t total) const {
+  struct Epi {};
+  template <int NT>
+  __device__ void epi_load(Epi<NT>&, int64_t, int, int64_t) const {}
+  template <int NT>
+  __device__ void epilogue(f4 (&acc)[NT], const Epi<NT>&, int64_t mrow, int ncol, int64_t total) const {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int64_t m = mrow + r;
@@ -460,21 +476,34 @@ struct OpLnUvqkBwd : NoStats {
   __device__ int bks() const { return 1; }
   __device__ int bns() const { return K; }
   template <int NT>
-  __device__ void epilogue(f4 (&acc)[NT], int64_t mrow, int ncol, int64_t total) const {
+  struct Epi {
+    float2 st[4];
+    float xv[4][NT], dyv[4][NT];
+  };
+  template <int NT>
+  __device__ void epi_load(Epi<NT>& es, int64_t mrow, int ncol, int64_t total) const {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int64_t m = mrow + r;
-      const bool row_ok = m < total;
-      const int64_t mc = clamp_row(m, total);
-      const float2 st = ld_f2(x_stats, mc);
-      float xv[NT], dyv[NT];
+      const int64_t mc = clamp_row(mrow + r, total);
+      es.st[r] = ld_f2(x_stats, mc);
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         const int n = ncol + 16 * t;
         const int nc = n < N ? n : N - 1;
-        xv[t] = as_global(x)[mc * ldx + nc];
-        dyv[t] = dy ? as_global(dy)[mc * lddy + nc] : 0.f;
+        es.xv[r][t] = as_global(x)[mc * ldx + nc];
+        es.dyv[r][t] = dy ? as_global(dy)[mc * lddy + nc] : 0.f;
       }
+    }
+  }
+  template <int NT>
+  __device__ void epilogue(f4 (&acc)[NT], const Epi<NT>& es, int64_t mrow, int ncol, int64_t total) const {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t m = mrow + r;
+      const bool row_ok = m < total;
+      const float2 st = es.st[r];
+      const float* xv = es.xv[r];
+      const float* dyv = es.dyv[r];
       float s1 = 0.f, s2 = 0.f;
       float xh[NT];
 #pragma unroll
