@@ -34,31 +34,87 @@ __global__ __launch_bounds__(1024) void cumsum_kernel(const int64_t* lengths, in
   }
 }
 
-// one wave per padded row (b, p)
-__global__ __launch_bounds__(256) void dense_to_jagged_kernel(const float* dense,
-                                                              const int64_t* offsets, int B,
-                                                              int N, int D, float* jagged) {
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= (int64_t)B * N) return;
-  const int b = (int)(row / N), p = (int)(row - (int64_t)b * N);
-  const int64_t s0 = offsets[b];
-  if (p >= offsets[b + 1] - s0) return;
-  const float* src = dense + row * D;
-  float* dst = jagged + (s0 + p) * D;
-  for (int c = threadIdx.x & 63; c < D; c += 64) dst[c] = src[c];
+// Sequence b's valid rows are one contiguous span of L_b * D floats on both sides
+// (dense[b, 0:L_b, :] <-> jagged[s0_b : s0_b + L_b, :]), so each copy is a flat,
+// fully coalesced stream in units of V (float2 when D is even; rows of 4*D bytes keep
+// both sides 8-byte aligned).  Grid: x = chunks of JG_CHUNK units within a sequence,
+// y = sequences (strided for B > 65535).  Each thread issues its JG_PER loads before
+// any store.
+constexpr int JG_PER = 4;
+constexpr int JG_CHUNK = 256 * JG_PER;
+
+template <typename V>
+__global__ __launch_bounds__(256) void dense_to_jagged_kernel(const V* dense, const int64_t* offsets,
+                                                              int B, int N, int64_t row_units,
+                                                              V* jagged) {
+  for (int b = blockIdx.y; b < B; b += gridDim.y) {
+    const int64_t s0 = offsets[b];
+    const int64_t L = min(offsets[b + 1] - s0, (int64_t)N);
+    const int64_t n = L * row_units;
+    const V* src = dense + (int64_t)b * N * row_units;
+    V* dst = jagged + s0 * row_units;
+    for (int64_t base = (int64_t)blockIdx.x * JG_CHUNK; base < n; base += (int64_t)gridDim.x * JG_CHUNK) {
+      V v[JG_PER];
+#pragma unroll
+      for (int k = 0; k < JG_PER; ++k) {
+        const int64_t i = base + threadIdx.x + 256 * k;
+        if (i < n) v[k] = src[i];
+      }
+#pragma unroll
+      for (int k = 0; k < JG_PER; ++k) {
+        const int64_t i = base + threadIdx.x + 256 * k;
+        if (i < n) dst[i] = v[k];
+      }
+    }
+  }
 }
 
-__global__ __launch_bounds__(256) void jagged_to_padded_kernel(const float* jagged,
-                                                               const int64_t* offsets, int B,
-                                                               int N, int D, float* dense) {
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= (int64_t)B * N) return;
-  const int b = (int)(row / N), p = (int)(row - (int64_t)b * N);
-  const int64_t s0 = offsets[b];
-  const bool valid = p < offsets[b + 1] - s0;
-  const float* src = jagged + (s0 + p) * D;
-  float* dst = dense + row * D;
-  for (int c = threadIdx.x & 63; c < D; c += 64) dst[c] = valid ? src[c] : 0.f;
+template <typename V>
+__global__ __launch_bounds__(256) void jagged_to_padded_kernel(const V* jagged, const int64_t* offsets,
+                                                               int B, int N, int64_t row_units,
+                                                               V* dense) {
+  const int64_t n = (int64_t)N * row_units;
+  for (int b = blockIdx.y; b < B; b += gridDim.y) {
+    const int64_t s0 = offsets[b];
+    const int64_t valid = min(offsets[b + 1] - s0, (int64_t)N) * row_units;
+    const V* src = jagged + s0 * row_units;
+    V* dst = dense + (int64_t)b * n;
+    for (int64_t base = (int64_t)blockIdx.x * JG_CHUNK; base < n; base += (int64_t)gridDim.x * JG_CHUNK) {
+      V v[JG_PER];
+#pragma unroll
+      for (int k = 0; k < JG_PER; ++k) {
+        const int64_t i = base + threadIdx.x + 256 * k;
+        v[k] = i < valid ? src[i] : V{};
+      }
+#pragma unroll
+      for (int k = 0; k < JG_PER; ++k) {
+        const int64_t i = base + threadIdx.x + 256 * k;
+        if (i < n) dst[i] = v[k];
+      }
+    }
+  }
+}
+
+template <typename V>
+static void launch_jagged_copy(bool to_jagged, const float* src, const int64_t* offsets, int B, int N,
+                               int D, float* dst, hipStream_t st) {
+  const int64_t units = (int64_t)D * sizeof(float) / sizeof(V);
+  const int64_t chunks = ((int64_t)N * units + JG_CHUNK - 1) / JG_CHUNK;
+  const dim3 grid((unsigned)(chunks > 0 ? chunks : 1), (unsigned)(B < 65535 ? B : 65535));
+  if (to_jagged)
+    GR_TIMED("dense_to_jagged", st,
+             hipLaunchKernelGGL(dense_to_jagged_kernel<V>, grid, dim3(256), 0, st,
+                                reinterpret_cast<const V*>(src), offsets, B, N, units,
+                                reinterpret_cast<V*>(dst)));
+  else
+    GR_TIMED("jagged_to_padded", st,
+             hipLaunchKernelGGL(jagged_to_padded_kernel<V>, grid, dim3(256), 0, st,
+                                reinterpret_cast<const V*>(src), offsets, B, N, units,
+                                reinterpret_cast<V*>(dst)));
+}
+
+static bool aligned8(const void* a, const void* b) {
+  return ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 7) == 0;
 }
 
 // Row-wise L2 normalisation y = x / max(||x||, eps): 16 lanes per row, 4 rows per wave.
@@ -169,8 +225,10 @@ int gr_dense_to_jagged(const float* dense, const int64_t* offsets, int B, int N,
              "gr_dense_to_jagged: bad args");
   const int64_t rows = (int64_t)B * N;
   if (rows == 0) return 0;
-  GR_TIMED("dense_to_jagged", (hipStream_t)stream, hipLaunchKernelGGL(gr::dense_to_jagged_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256),
-                     0, (hipStream_t)stream, dense, offsets, B, N, D, jagged));
+  if (D % 2 == 0 && gr::aligned8(dense, jagged))
+    gr::launch_jagged_copy<float2>(true, dense, offsets, B, N, D, jagged, (hipStream_t)stream);
+  else
+    gr::launch_jagged_copy<float>(true, dense, offsets, B, N, D, jagged, (hipStream_t)stream);
   GR_LAUNCH_CHECK("gr_dense_to_jagged");
   return 0;
 }
@@ -181,8 +239,10 @@ int gr_jagged_to_padded(const float* jagged, const int64_t* offsets, int B, int 
              "gr_jagged_to_padded: bad args");
   const int64_t rows = (int64_t)B * N;
   if (rows == 0) return 0;
-  GR_TIMED("jagged_to_padded", (hipStream_t)stream, hipLaunchKernelGGL(gr::jagged_to_padded_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256),
-                     0, (hipStream_t)stream, jagged, offsets, B, N, D, dense));
+  if (D % 2 == 0 && gr::aligned8(jagged, dense))
+    gr::launch_jagged_copy<float2>(false, jagged, offsets, B, N, D, dense, (hipStream_t)stream);
+  else
+    gr::launch_jagged_copy<float>(false, jagged, offsets, B, N, D, dense, (hipStream_t)stream);
   GR_LAUNCH_CHECK("gr_jagged_to_padded");
   return 0;
 }

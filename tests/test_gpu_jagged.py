@@ -1,0 +1,90 @@
+"""GPU parity of the jagged data-movement kernels (utils/ops.py:18-114):
+``asynchronous_complete_cumsum``, ``dense_to_jagged`` and ``jagged_to_padded_dense``
+through the C-ABI, against the reference's own known answers (tests/golden/jagged_ops.npz,
+restating reference tests/test_ops.py:7-53) and a numpy restatement on seeded ragged
+inputs.  Pure copies: bit-exact."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _np_dense_to_jagged(dense, offs):
+    return np.concatenate([dense[b, : offs[b + 1] - offs[b]] for b in range(len(offs) - 1)])
+
+
+def _np_jagged_to_padded(values, offs, N):
+    out = np.zeros((len(offs) - 1, N, values.shape[1]), values.dtype)
+    for b in range(len(offs) - 1):
+        L = min(int(offs[b + 1] - offs[b]), N)
+        out[b, :L] = values[offs[b]:offs[b] + L]
+    return out
+
+
+def test_jagged_ops_reference_known_answers():
+    from mygenerativerecommenders_amd import ops
+    d = np.load(os.path.join(GOLDEN, "jagged_ops.npz"))
+    offs = ops.asynchronous_complete_cumsum(torch.from_numpy(d["lengths"]).long().cuda())
+    assert np.array_equal(offs.cpu().numpy(), d["offsets"])
+    jag = ops.dense_to_jagged(torch.from_numpy(d["dense"]).cuda(), offs,
+                              total_rows=int(d["offsets"][-1]))
+    assert np.array_equal(jag.cpu().numpy(), d["jagged"])
+    pad = ops.jagged_to_padded_dense(torch.from_numpy(d["values"]).cuda(),
+                                     torch.from_numpy(d["offsets2"]).cuda(), 3)
+    assert np.array_equal(pad.cpu().numpy(), d["padded"].astype(np.float32))
+
+
+# D even -> float2 stream, D odd -> float stream; lengths include empty and full rows
+@pytest.mark.parametrize("B,N,D", [(128, 211, 50), (5, 17, 7), (3, 1, 1), (9, 300, 256), (2, 2059, 256)])
+def test_jagged_roundtrip_ragged(B, N, D):
+    from mygenerativerecommenders_amd import ops
+    g = torch.Generator().manual_seed(B * 1000 + N + D)
+    lengths = torch.randint(0, N + 1, (B,), generator=g)
+    lengths[0] = 0
+    lengths[-1] = N
+    dense = torch.randn(B, N, D, generator=g)
+    offs_np = np.concatenate([[0], np.cumsum(lengths.numpy())]).astype(np.int64)
+    offs = ops.asynchronous_complete_cumsum(lengths.cuda())
+    assert np.array_equal(offs.cpu().numpy(), offs_np)
+    total = int(offs_np[-1])
+    jag = ops.dense_to_jagged(dense.cuda(), offs, total_rows=total)
+    ref = _np_dense_to_jagged(dense.numpy(), offs_np)
+    assert np.array_equal(jag.cpu().numpy(), ref)
+    # the output is allocated uninitialised: padded rows must be written as exact zeros
+    pad = ops.jagged_to_padded_dense(jag, offs, N)
+    assert np.array_equal(pad.cpu().numpy(), _np_jagged_to_padded(ref, offs_np, N))
+
+
+def test_jagged_unaligned_views_take_scalar_path():
+    """A dense view starting 4 bytes into its storage cannot use 8-byte vectors; the
+    result must still be exact."""
+    from mygenerativerecommenders_amd import ops
+    g = torch.Generator().manual_seed(7)
+    B, N, D = 6, 40, 50
+    storage = torch.randn(B * N * D + 1, generator=g).cuda()
+    dense = storage[1:].view(B, N, D)
+    lengths = torch.tensor([0, 40, 3, 17, 39, 1])
+    offs_np = np.concatenate([[0], np.cumsum(lengths.numpy())]).astype(np.int64)
+    offs = ops.asynchronous_complete_cumsum(lengths.cuda())
+    jag = ops.dense_to_jagged(dense, offs, total_rows=int(offs_np[-1]))
+    assert np.array_equal(jag.cpu().numpy(), _np_dense_to_jagged(dense.cpu().numpy(), offs_np))
+
+
+def test_jagged_ops_autograd():
+    """dense_to_jagged's backward is jagged_to_padded and vice versa (padding rows get 0)."""
+    from mygenerativerecommenders_amd import ops
+    g = torch.Generator().manual_seed(3)
+    B, N, D = 4, 23, 50
+    lengths = torch.tensor([23, 0, 11, 5])
+    offs = ops.asynchronous_complete_cumsum(lengths.cuda())
+    dense = torch.randn(B, N, D, generator=g).cuda().requires_grad_(True)
+    jag = ops.dense_to_jagged(dense, offs, total_rows=int(lengths.sum()))
+    w = torch.randn(jag.shape, generator=g).cuda()
+    (jag * w).sum().backward()
+    offs_np = np.concatenate([[0], np.cumsum(lengths.numpy())]).astype(np.int64)
+    assert np.array_equal(dense.grad.cpu().numpy(), _np_jagged_to_padded(w.cpu().numpy(), offs_np, N))
