@@ -10,23 +10,26 @@
 namespace gr {
 
 // single workgroup exclusive scan: offsets[0] = 0, offsets[b+1] = sum_{<=b} lengths
-__global__ __launch_bounds__(1024) void cumsum_kernel(const int64_t* lengths, int B,
-                                                     int64_t* offsets) {
-  __shared__ int64_t part[1024];
-  const int t = threadIdx.x;
-  const int per = (B + 1023) / 1024;
+__global__ __launch_bounds__(256) void cumsum_kernel(const int64_t* lengths, int B,
+                                                    int64_t* offsets) {
+  // thread t owns lengths[t*per, (t+1)*per); 64-lane shuffle scan per wave, then the
+  // four wave totals meet in LDS (one barrier)
+  __shared__ int64_t wave_tot[4];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int per = (B + 255) / 256;
   const int lo = t * per, hi = min(B, lo + per);
   int64_t s = 0;
   for (int i = lo; i < hi; ++i) s += lengths[i];
-  part[t] = s;
-  __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan
-    int64_t v = t >= o ? part[t - o] : 0;
-    __syncthreads();
-    part[t] += v;
-    __syncthreads();
+  int64_t inc = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t v = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += v;
   }
-  int64_t run = t ? part[t - 1] : 0;
+  if (lane == 63) wave_tot[wv] = inc;
+  __syncthreads();
+  int64_t run = inc - s;
+  for (int w = 0; w < wv; ++w) run += wave_tot[w];
   if (t == 0) offsets[0] = 0;
   for (int i = lo; i < hi; ++i) {
     run += lengths[i];
@@ -212,7 +215,7 @@ int gr_current_embeddings(const float* encoded, const int64_t* lengths, int B, i
 
 int gr_complete_cumsum(const int64_t* lengths, int B, int64_t* offsets, void* stream) {
   GR_REQUIRE(offsets && (B == 0 || lengths) && B >= 0, "gr_complete_cumsum: bad args");
-  GR_TIMED("cumsum", (hipStream_t)stream, hipLaunchKernelGGL(gr::cumsum_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, lengths,
+  GR_TIMED("cumsum", (hipStream_t)stream, hipLaunchKernelGGL(gr::cumsum_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, lengths,
                      B, offsets));
   GR_LAUNCH_CHECK("gr_complete_cumsum");
   return 0;

@@ -88,3 +88,14 @@ def test_jagged_ops_autograd():
     (jag * w).sum().backward()
     offs_np = np.concatenate([[0], np.cumsum(lengths.numpy())]).astype(np.int64)
     assert np.array_equal(dense.grad.cpu().numpy(), _np_jagged_to_padded(w.cpu().numpy(), offs_np, N))
+
+
+@pytest.mark.parametrize("B", [0, 1, 63, 64, 65, 256, 257, 1000, 70000])
+def test_complete_cumsum_sizes(B):
+    """Scan edges: single lane, wave and workgroup boundaries, several rows per thread."""
+    from mygenerativerecommenders_amd import ops
+    g = torch.Generator().manual_seed(B)
+    lengths = torch.randint(0, 3000, (B,), generator=g)
+    offs = ops.asynchronous_complete_cumsum(lengths.cuda())
+    ref = np.concatenate([[0], np.cumsum(lengths.numpy())]).astype(np.int64)
+    assert np.array_equal(offs.cpu().numpy(), ref)
