@@ -180,8 +180,12 @@ def e2e_train_leg(args, device, world, lengths, ts, past_ids):
     sim = DotProductSimilarity()
     params = list(enc.parameters()) + list(emb.parameters()) + list(pre.parameters())
     reducer = FlatGradAllReducer(params)
-    opt = torch.optim.AdamW(params, lr=1e-3, betas=(0.9, 0.98), weight_decay=1e-3,
-                            capturable=True)
+    try:  # one fused multi-tensor kernel per step (same AdamW math), as in the headline leg
+        opt = torch.optim.AdamW(params, lr=1e-3, betas=(0.9, 0.98), weight_decay=1e-3,
+                                fused=True, capturable=True)
+    except (RuntimeError, TypeError, ValueError):
+        opt = torch.optim.AdamW(params, lr=1e-3, betas=(0.9, 0.98), weight_decay=1e-3,
+                                capturable=True)
     # the target sits at position `length` (train.py: scatter of target_ids)
     g = torch.Generator(device=device)
     g.manual_seed(11)
