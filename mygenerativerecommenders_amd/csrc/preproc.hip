@@ -59,32 +59,47 @@ __global__ __launch_bounds__(256) void preproc_bwd_x_kernel(const float* dy, con
     dr[c] = valid ? gr_[c] * pre_keep(sd, r * D + c, p) * scale : 0.f;
 }
 
-// dpos[n][c]: one thread per (n, c), sums b = 0 .. B-1 in order (8 loads in flight)
+// dpos[n][c]: a workgroup owns 16 consecutive outputs i = n * D + c; thread (o, grp)
+// sums b = grp, grp + 16, ... in order (8 loads in flight), then the 16 partials are
+// added in grp order (deterministic, no atomics).  Splitting B over 16 groups gives
+// N * D / 16 workgroups (660 at ml-1m) instead of N * D / 256 (42), each with a
+// 16x shorter dependent chain.
+constexpr int kPosGroups = 16;
 __global__ __launch_bounds__(256) void preproc_bwd_pos_kernel(const float* dy, const int64_t* ids,
                                                               int B, int N, int D, float p,
                                                               uint64_t seed, const int64_t* seed_off,
                                                               float* dpos) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (int64_t)N * D) return;
-  const int n = (int)(i / D), c = (int)(i % D);
+  __shared__ float part[kPosGroups][17];
+  const int o = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const int64_t i = (int64_t)blockIdx.x * 16 + o;
+  const int64_t nd = (int64_t)N * D;
+  const int64_t ic = i < nd ? i : nd - 1;
+  const int n = (int)(ic / D), c = (int)(ic % D);
   const uint64_t sd = seed + (seed_off ? (uint64_t)*seed_off : 0ull);
   float acc = 0.f;
-  int b = 0;
-  for (; b + 8 <= B; b += 8) {
+  int b = grp;
+  for (; b + 7 * kPosGroups < B; b += 8 * kPosGroups) {
     float v[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const int64_t r = (int64_t)(b + u) * N + n;
+      const int64_t r = (int64_t)(b + kPosGroups * u) * N + n;
       v[u] = ids[r] != 0 ? dy[r * D + c] * pre_keep(sd, r * D + c, p) : 0.f;
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) acc += v[u];
   }
-  for (; b < B; ++b) {
+  for (; b < B; b += kPosGroups) {
     const int64_t r = (int64_t)b * N + n;
     acc += ids[r] != 0 ? dy[r * D + c] * pre_keep(sd, r * D + c, p) : 0.f;
   }
-  dpos[i] = acc;
+  part[grp][o] = acc;
+  __syncthreads();
+  if (grp == 0 && i < nd) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < kPosGroups; ++k) s += part[k][o];
+    dpos[i] = s;
+  }
 }
 
 }  // namespace gr
@@ -125,7 +140,7 @@ int gr_preproc_bwd(const float* dy, const int64_t* past_ids, int B, int N, int D
   if (dpos_w) {
     const int64_t nd = (int64_t)N * D;
     GR_TIMED("preproc", st,
-             hipLaunchKernelGGL(gr::preproc_bwd_pos_kernel, dim3((unsigned)((nd + 255) / 256)), dim3(256),
+             hipLaunchKernelGGL(gr::preproc_bwd_pos_kernel, dim3((unsigned)((nd + 15) / 16)), dim3(256),
                                 0, st, dy, past_ids, B, N, D, dropout_p, seed, seed_offset, dpos_w));
     GR_LAUNCH_CHECK("gr_preproc_bwd(dpos)");
   }
