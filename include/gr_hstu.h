@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GR_HSTU_ABI_VERSION 5
+#define GR_HSTU_ABI_VERSION 6
 
 #ifndef GR_API
 #define GR_API __attribute__((visibility("default")))
@@ -274,7 +274,11 @@ GR_API int gr_wgrad(const float* a, int64_t lda, const float* a_stats, const flo
  * the query's row of invalid_ids (B, N0) are excluded (padding zeros included, as in
  * the reference).  Rows with fewer than k valid items are padded with
  * (-inf, id -1, index -1).  out_index (B, k) is optional.  Limits: D <= 256,
- * k <= 256, N0 <= 256, X < 2^31.
+ * k <= 4096, N0 <= 8192, X < 2^31.  N0 > 256 (ml-20m validation passes past_ids of
+ * width 2059) sorts each query's list into the workspace first.  k > 256 (the
+ * reference CandidateIndex asks its top-k module for k + N0) takes a chunked exact
+ * path: all scores of a chunk of items, then a per-query radix select merged with the
+ * running top-k; same scores, ids and order, no fused fast path.
  * Catalogs of X >= 262,144 items with D <= 64 take a threshold-filter path (sampled
  * per-query threshold, one all-query scoring pass over the bf16 copy that reads it
  * once, exact f32 rescoring of the candidates in the merge, which trusts only scores
@@ -284,7 +288,7 @@ GR_API int gr_wgrad(const float* a, int64_t lda, const float* a_stats, const flo
  */
 GR_API size_t mips_packed_items_bytes(int64_t X, int D);
 GR_API int mips_pack_items(const float* items, int64_t X, int D, float* packed, void* stream);
-GR_API size_t mips_topk_workspace_size(int B, int64_t X, int D, int k);
+GR_API size_t mips_topk_workspace_size(int B, int64_t X, int D, int k, int N0);
 GR_API int mips_topk(const float* queries, const float* packed_items, int64_t X, int D,
               const int64_t* item_ids, int64_t index_base, const int64_t* invalid_ids,
               int N0, int B, int k, float* out_scores, int64_t* out_ids, int64_t* out_index,

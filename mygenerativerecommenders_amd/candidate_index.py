@@ -38,6 +38,8 @@ class CandidateIndex(torch.nn.Module):
             self._embeddings_t = embeddings.permute(2, 1, 0).squeeze(2)
         else:
             self._embeddings_t = None
+        # the table may be an inference tensor rewritten in place (no version counter)
+        self._top_k_module.invalidate()
 
     @property
     def ids(self) -> torch.Tensor:

@@ -33,8 +33,51 @@ constexpr int QG = 16;       // queries per workgroup (MFMA column block)
 constexpr int SW = 8;        // waves per select workgroup (2 per SIMD, one LDS buffer set)
 constexpr int ST = SW * 64;  // select threads
 constexpr int CAP = 512;     // per-query candidate buffer: k (<= 256) + one step (SW * STEP <= 256)
-constexpr int INV_MAX = 256; // max invalid ids per query
+constexpr int INV_MAX = 256; // invalid ids per query the select kernel keeps in LDS
+constexpr int INV_BIG = 8192; // max invalid ids per query (ml-20m validation: N0 = 2059)
 constexpr uint32_t VERIFIED = 0x80000000u;
+
+// Sorted invalid lists are padded with INT64_MAX to n0p = a power of two >= 64.
+__host__ __device__ inline int inv_pad(int N0) {
+  if (N0 <= 0) return 0;
+  int p = 64;
+  while (p < N0) p <<= 1;
+  return p;
+}
+
+// Ascending bitonic sort of v[0 .. n) in LDS (n a power of two), all threads of the
+// block (any size) joining; the caller has stored v and synchronised.
+__device__ void block_bitonic_i64(int64_t* v, int n) {
+  for (int size = 2; size <= n; size <<= 1)
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int p = threadIdx.x; p < n / 2; p += blockDim.x) {
+        const int i = 2 * p - (p & (stride - 1)), j = i + stride;
+        const bool up = (i & size) == 0;
+        const int64_t x = v[i], y = v[j];
+        if ((x > y) == up) {
+          v[i] = y;
+          v[j] = x;
+        }
+      }
+      __syncthreads();
+    }
+}
+
+// N0 > INV_MAX: each query's invalid row, sorted ascending and padded to n0p, into
+// the workspace (the select kernel binary-searches it there; 16 queries' lists do not
+// fit its LDS).  One workgroup per query, n0p * 8 B of dynamic LDS.
+__global__ __launch_bounds__(1024) void mips_sort_invalid_kernel(const int64_t* invalid, int N0,
+                                                                 int n0p, int64_t* out,
+                                                                 const int* gate) {
+  if (gate && *gate == 0) return;
+  extern __shared__ int64_t vs[];
+  const int64_t* src = invalid + (int64_t)blockIdx.x * N0;
+  for (int j = threadIdx.x; j < n0p; j += blockDim.x) vs[j] = j < N0 ? src[j] : INT64_MAX;
+  __syncthreads();
+  block_bitonic_i64(vs, n0p);
+  int64_t* dst = out + (int64_t)blockIdx.x * n0p;
+  for (int j = threadIdx.x; j < n0p; j += blockDim.x) dst[j] = vs[j];
+}
 
 __device__ __forceinline__ uint32_t ord_key(float s) {
   // monotone map float -> uint32 with -0 == +0; 0 is reserved for "dropped"
@@ -221,6 +264,7 @@ struct SelectArgs {
   float* part_score;   // [n_ranges][B][k_part]
   int64_t* part_index; // [n_ranges][B][k_part]  (global index, -1 = empty)
   const int* gate;      // non-null: run only when *gate != 0 (fallback of the filter path)
+  const int64_t* inv_sorted;  // N0 > INV_MAX: [B][n0p] sorted lists (mips_sort_invalid_kernel)
 };
 
 template <int KS, int BLOCKS>
@@ -249,9 +293,10 @@ __global__ __launch_bounds__(ST) void mips_select_kernel(SelectArgs a) {
   const int64_t x_begin = (int64_t)range * a.range_items;
   const int64_t x_end = min(a.X, x_begin + a.range_items);
 
-  // ---- prologue: sorted invalid lists, counters
-  const int n0p = a.N0 > 0 ? (a.N0 <= 64 ? 64 : (a.N0 <= 128 ? 128 : 256)) : 0;
-  for (int e = tid; e < QG * n0p; e += ST) {
+  // ---- prologue: sorted invalid lists (LDS, or the pre-sorted workspace rows), counters
+  const bool big = a.inv_sorted != nullptr;
+  const int n0p = inv_pad(a.N0);
+  for (int e = tid; e < (big ? 0 : QG * n0p); e += ST) {
     const int qq = e / n0p, j = e - qq * n0p;
     int64_t v = INT64_MAX;
     if (q0 + qq < a.B && j < a.N0) v = a.invalid[(int64_t)(q0 + qq) * a.N0 + j];
@@ -262,7 +307,7 @@ __global__ __launch_bounds__(ST) void mips_select_kernel(SelectArgs a) {
     tau_s[tid] = q0 + tid < a.B ? -INFINITY : INFINITY;  // padded queries collect nothing
   }
   __syncthreads();
-  for (int size = 2; size <= n0p; size <<= 1) {  // bitonic sort, QG independent rows
+  for (int size = 2; size <= (big ? 0 : n0p); size <<= 1) {  // bitonic sort, QG independent rows
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
       for (int e = tid; e < QG * (n0p / 2); e += ST) {
         const int qq = e / (n0p / 2), p = e - qq * (n0p / 2);
@@ -303,7 +348,8 @@ __global__ __launch_bounds__(ST) void mips_select_kernel(SelectArgs a) {
     float sc[CAP / 64];
     uint32_t ix[CAP / 64];
     const int n = cnt[qq];
-    const int64_t* qinv = inv + qq * INV_MAX;
+    const int64_t* qinv =
+        big ? a.inv_sorted + (int64_t)min(q0 + qq, a.B - 1) * n0p : inv + qq * INV_MAX;
     int nvalid = 0;
     // all LDS/global loads unconditional (clamped) so they are in flight together
     int64_t id[CAP / 64];
@@ -319,15 +365,22 @@ __global__ __launch_bounds__(ST) void mips_select_kernel(SelectArgs a) {
       id[t] = a.item_ids ? as_global(a.item_ids)[li < a.X ? li : 0] : a.index_base + li;
     }
     const int nbits = a.N0 > 0 ? 32 - __clz(n0p - 1) : 0;  // log2(n0p)
+    // branchless lower_bounds over the sorted (INT64_MAX padded) n0p-entry list, the
+    // lane's CAP/64 searches stepped together (independent probes in flight: the
+    // big-list rows are read from L2)
+    int pos[CAP / 64];
+#pragma unroll
+    for (int t = 0; t < CAP / 64; ++t) pos[t] = 0;
+    for (int bit = nbits - 1; bit >= 0; --bit) {
+      int64_t pv[CAP / 64];
+#pragma unroll
+      for (int t = 0; t < CAP / 64; ++t) pv[t] = qinv[pos[t] + (1 << bit) - 1];
+#pragma unroll
+      for (int t = 0; t < CAP / 64; ++t) pos[t] += (pv[t] < id[t]) ? (1 << bit) : 0;
+    }
 #pragma unroll
     for (int t = 0; t < CAP / 64; ++t) {
-      // branchless lower_bound over the sorted (INT64_MAX padded) n0p-entry list
-      int pos = 0;
-      for (int bit = nbits - 1; bit >= 0; --bit) {
-        const int probe = pos + (1 << bit) - 1;
-        pos += (qinv[probe] < id[t]) ? (1 << bit) : 0;
-      }
-      const bool hit = a.N0 > 0 && qinv[pos < n0p ? pos : n0p - 1] == id[t];
+      const bool hit = a.N0 > 0 && qinv[pos[t] < n0p ? pos[t] : n0p - 1] == id[t];
       const int j = lane + 64 * t;
       const bool ok = j < n && !(need[t] && hit);
       ix[t] |= VERIFIED;
@@ -765,30 +818,19 @@ struct ScoreAllArgs {
   int64_t* out_index;  // [B][X], -1 = excluded
 };
 
+// Explicit ids with N0 > 0: the query's sorted invalid list in n0p * 8 B of dynamic LDS.
 template <int KS2>
 __global__ __launch_bounds__(256) void mips_scoreall_kernel(ScoreAllArgs a) {
   __shared__ float qv[8 * KS2];
-  __shared__ int64_t inv[INV_MAX];
+  extern __shared__ int64_t inv[];
   const int q = blockIdx.x, tid = threadIdx.x;
   for (int d = tid; d < 8 * KS2; d += 256) qv[d] = d < a.D ? a.q[(int64_t)q * a.D + d] : 0.f;
   const bool search = a.item_ids && a.N0 > 0;
-  const int n0p = a.N0 <= 64 ? 64 : (a.N0 <= 128 ? 128 : 256);
+  const int n0p = inv_pad(a.N0);
   if (search) {
     for (int j = tid; j < n0p; j += 256) inv[j] = j < a.N0 ? a.invalid[(int64_t)q * a.N0 + j] : INT64_MAX;
     __syncthreads();
-    for (int size = 2; size <= n0p; size <<= 1)
-      for (int stride = size >> 1; stride > 0; stride >>= 1) {
-        for (int p = tid; p < n0p / 2; p += 256) {
-          const int i = 2 * p - (p & (stride - 1)), j = i + stride;
-          const bool up = (i & size) == 0;
-          const int64_t x = inv[i], y = inv[j];
-          if ((x > y) == up) {
-            inv[i] = y;
-            inv[j] = x;
-          }
-        }
-        __syncthreads();
-      }
+    block_bitonic_i64(inv, n0p);
   }
   __syncthreads();
   typedef float fv2 __attribute__((ext_vector_type(2)));
@@ -811,7 +853,7 @@ __global__ __launch_bounds__(256) void mips_scoreall_kernel(ScoreAllArgs a) {
 #pragma unroll
     for (int d = 0; d < 8 * KS2; ++d) sc = fmaf(qv[d], e[d], sc);  // padding adds +0 exactly
     bool ok = true;
-    if (search) ok = !sorted_contains(inv, a.N0 > 0 ? n0p : 0, a.item_ids[i]);
+    if (search) ok = !sorted_contains(inv, n0p, a.item_ids[i]);
     os[i] = ok ? sc : -INFINITY;
     oi[i] = ok ? a.index_base + i : -1;
   }
@@ -1241,7 +1283,7 @@ struct FilterMergeArgs {
 __global__ __launch_bounds__(256) void mips_filter_merge_kernel(FilterMergeArgs a) {
   __shared__ uint32_t key[FILTER_CAP];
   __shared__ int64_t idx[FILTER_CAP];
-  __shared__ int64_t inv[INV_MAX];
+  extern __shared__ int64_t inv[];  // inv_pad(N0) entries (dynamic LDS)
   __shared__ SelLDS L;
   __shared__ int sub_off[NSUB + 1];
   __shared__ float cs[FILTER_CAP];
@@ -1296,11 +1338,12 @@ __global__ __launch_bounds__(256) void mips_filter_merge_kernel(FilterMergeArgs 
       }
     }
   }
-  const int n0p = a.N0 <= 0 ? 0 : (a.N0 <= 64 ? 64 : (a.N0 <= 128 ? 128 : 256));
+  const int n0p = inv_pad(a.N0);
   for (int j = tid; j < n0p; j += 256)
     inv[j] = j < a.N0 ? a.invalid[(int64_t)q * a.N0 + j] : INT64_MAX;
   __syncthreads();
-  if (n0p > 0) block_sort_i64_asc(inv, n0p);
+  if (n0p > 256) block_bitonic_i64(inv, n0p);
+  else if (n0p > 0) block_sort_i64_asc(inv, n0p);
   // bf16 filter: cs holds the exact scores (rescored at the filter's flush); only candidates at
   // or above tau_e are provably complete
   const float te = a.rescore ? a.tau_e[q] : -INFINITY;
@@ -1330,6 +1373,210 @@ __global__ __launch_bounds__(256) void mips_filter_merge_kernel(FilterMergeArgs 
   (void)n;
 }
 
+// ----------------------------------------------------------------- wide k (k > 256)
+// torch.topk takes any k; the reference's CandidateIndex asks its top-k module for
+// k' = k + N0 (candidate_index.py:132), 2,259 at ml-20m.  The fused paths above keep
+// per-query selections of <= 256 in LDS, so k > 256 runs this chunked exact path:
+//   W1 (mips_wide_score_kernel): keys of a chunk of <= Xc items for all queries
+//      (the same k-ordered fmaf chain read from the packed layout; explicit ids are
+//      excluded here by binary search in the pre-sorted invalid rows);
+//   W2 (mips_wide_select_kernel): per query, the exact top-k of (running list ++
+//      chunk) by 8-bit radix select, ties at the k-th key by position (= catalog index:
+//      the running list holds earlier chunks, ties inside it sorted by index), then a
+//      bitonic sort (key desc, index asc) into the running list or the outputs.
+constexpr int KW_MAX = 4096;
+
+struct WideArgs {
+  const float* q;
+  const float* packed;
+  int64_t X;
+  int D, B, N0, k;
+  const int64_t* item_ids;
+  int64_t index_base;
+  const int64_t* invalid;
+  const int64_t* inv_sorted;  // explicit ids, N0 > 0: [B][n0p]
+  int n0p;
+  int64_t xc;                 // chunk row stride of ckey
+  int64_t c0, n;              // this chunk: local items [c0, c0 + n)
+  uint32_t* ckey;             // [B][xc], 0 = excluded
+  uint32_t* rkey;             // [B][k] running list (sorted), 0 = empty
+  int64_t* ridx;              // [B][k]
+  int first, last;
+  float* out_score;
+  int64_t* out_ids;
+  int64_t* out_index;
+};
+
+__global__ __launch_bounds__(256) void mips_wide_score_kernel(WideArgs a) {
+  __shared__ float qv[256];
+  const int q = blockIdx.y, tid = threadIdx.x;
+  const int KS2 = (ceil_div(a.D, 4) + 1) / 2;
+  for (int d = tid; d < 8 * KS2; d += 256) qv[d] = d < a.D ? a.q[(int64_t)q * a.D + d] : 0.f;
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * 256 + tid;
+  if (i >= a.n) return;
+  const int64_t li = a.c0 + i;
+  typedef float fv2 __attribute__((ext_vector_type(2)));
+  gptr<fv2> pk = as_global(reinterpret_cast<const fv2*>(a.packed));
+  const int64_t ib = li >> 4;
+  const int il = (int)(li & 15);
+  float sc = 0.f;
+  for (int j = 0; j < KS2; ++j) {
+    fv2 v[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[c] = pk[(ib * KS2 + j) * 64 + 16 * c + il];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) sc = fmaf(qv[8 * j + c], v[c].x, sc);      // d = 8j + c
+#pragma unroll
+    for (int c = 0; c < 4; ++c) sc = fmaf(qv[8 * j + 4 + c], v[c].y, sc);  // d = 8j + 4 + c
+  }
+  bool ok = true;
+  if (a.item_ids && a.N0 > 0)
+    ok = !sorted_contains(a.inv_sorted + (int64_t)q * a.n0p, a.n0p, a.item_ids[li]);
+  a.ckey[(int64_t)q * a.xc + i] = ok ? ord_key(sc) : 0u;
+}
+
+// k-th largest nonzero key of the virtual array key_at(0 .. M) (any block size).
+template <class KeyAt>
+__device__ void block_radix_kth_any(KeyAt key_at, int64_t M, int kk, int* hist, int* sh,
+                                    uint32_t& kstar, int& k_rem) {
+  uint32_t prefix = 0, mask = 0;
+  int need = kk;
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) hist[i] = 0;
+    __syncthreads();
+    for (int64_t e = threadIdx.x; e < M; e += blockDim.x) {
+      const uint32_t x = key_at(e);
+      if (x != 0u && (x & mask) == prefix) atomicAdd(&hist[(x >> shift) & 255], 1);
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) hist_find_digit(hist, need, &sh[0], &sh[1]);
+    __syncthreads();
+    prefix |= (uint32_t)sh[0] << shift;
+    mask |= 0xFFu << shift;
+    need -= sh[1];
+    __syncthreads();
+  }
+  kstar = prefix;
+  k_rem = need;
+}
+
+__global__ __launch_bounds__(1024) void mips_wide_select_kernel(WideArgs a) {
+  __shared__ uint32_t skey[KW_MAX];
+  __shared__ int64_t sidx[KW_MAX];
+  __shared__ int hist[256];
+  __shared__ int sh[4];
+  __shared__ int wsum[16];
+  const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  uint32_t* ck = a.ckey + (int64_t)q * a.xc;
+  uint32_t* rk = a.rkey + (int64_t)q * a.k;
+  int64_t* rx = a.ridx + (int64_t)q * a.k;
+  if (!a.item_ids && a.N0 > 0) {  // arange ids: drop the query's invalid items by index
+    for (int j = tid; j < a.N0; j += 1024) {
+      const int64_t li = a.invalid[(int64_t)q * a.N0 + j] - a.index_base - a.c0;
+      if (li >= 0 && li < a.n) ck[li] = 0u;
+    }
+    __syncthreads();
+  }
+  const int rc = a.first ? 0 : a.k;  // running list: k slots, empty ones keyed 0
+  const int64_t M = rc + a.n;
+  auto key_at = [&](int64_t e) -> uint32_t { return e < rc ? rk[e] : ck[e - rc]; };
+  auto idx_at = [&](int64_t e) -> int64_t {
+    return e < rc ? rx[e] : a.index_base + a.c0 + (e - rc);
+  };
+  int nz = 0;
+  for (int64_t e = tid; e < M; e += 1024) nz += key_at(e) != 0u;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) nz += __shfl_xor(nz, o, 64);
+  if (lane == 0) wsum[w] = nz;
+  if (tid == 0) sh[2] = 0;
+  __syncthreads();
+  int tot = 0;
+#pragma unroll
+  for (int u = 0; u < 16; ++u) tot += wsum[u];
+  __syncthreads();
+  const bool all = tot <= a.k;
+  uint32_t kstar = 0u;
+  int k_rem = 0;
+  if (!all) block_radix_kth_any(key_at, M, a.k, hist, sh, kstar, k_rem);
+  // entries above kstar (any order: sorted below)
+  for (int64_t e = tid; e < M; e += 1024) {
+    const uint32_t x = key_at(e);
+    if (x != 0u && (all || x > kstar)) {
+      const int p = atomicAdd(&sh[2], 1);
+      skey[p] = x;
+      sidx[p] = idx_at(e);
+    }
+  }
+  // ties at kstar: the first k_rem in position order, tile by tile
+  int taken = 0;
+  for (int64_t t0 = 0; !all && t0 < M && taken < k_rem; t0 += 1024) {
+    const int64_t e = t0 + tid;
+    const bool eq = e < M && key_at(e) == kstar;
+    const unsigned long long bal = __ballot(eq);
+    __syncthreads();
+    if (lane == 0) wsum[w] = __popcll(bal);
+    __syncthreads();
+    int before = 0, tile = 0;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      before += u < w ? wsum[u] : 0;
+      tile += wsum[u];
+    }
+    const int r = taken + before + __popcll(bal & ((1ull << lane) - 1ull));
+    if (eq && r < k_rem) {
+      const int p = atomicAdd(&sh[2], 1);
+      skey[p] = kstar;
+      sidx[p] = idx_at(e);
+    }
+    taken += tile;
+  }
+  __syncthreads();
+  const int nsel = sh[2];
+  int P = 2;
+  while (P < nsel) P <<= 1;
+  for (int p = nsel + tid; p < P; p += 1024) {
+    skey[p] = 0u;
+    sidx[p] = INT64_MAX;
+  }
+  __syncthreads();
+  for (int size = 2; size <= P; size <<= 1)  // key desc, index asc
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int p = tid; p < P / 2; p += 1024) {
+        const int i = 2 * p - (p & (stride - 1)), j = i + stride;
+        const bool desc = (i & size) == 0;
+        const uint32_t ki = skey[i], kj = skey[j];
+        const int64_t xi = sidx[i], xj = sidx[j];
+        const bool i_first = ki > kj || (ki == kj && xi < xj);
+        if (i_first != desc) {
+          skey[i] = kj; skey[j] = ki;
+          sidx[i] = xj; sidx[j] = xi;
+        }
+      }
+      __syncthreads();
+    }
+  if (!a.last) {
+    for (int r = tid; r < a.k; r += 1024) {
+      rk[r] = r < nsel ? skey[r] : 0u;
+      rx[r] = r < nsel ? sidx[r] : INT64_MAX;
+    }
+    return;
+  }
+  for (int r = tid; r < a.k; r += 1024) {
+    const int64_t o = (int64_t)q * a.k + r;
+    if (r < nsel) {
+      const int64_t gi = sidx[r];
+      a.out_score[o] = key_to_float(skey[r]);
+      if (a.out_index) a.out_index[o] = gi;
+      a.out_ids[o] = a.item_ids ? a.item_ids[gi - a.index_base] : gi;
+    } else {
+      a.out_score[o] = -INFINITY;
+      if (a.out_index) a.out_index[o] = -1;
+      a.out_ids[o] = -1;
+    }
+  }
+}
+
 struct TopkPlan {
   bool small, filter;
   int KS, n_ranges, k_part;
@@ -1340,6 +1587,11 @@ struct TopkPlan {
   int GB, G, NQG, n_chunks, filter_waves, sr;
   int KC;              // > 0: the filter scores the bf16 copy (KC k-chunks of 32 dims)
   size_t off_tau, off_tau_e, off_qrows, off_cnt, off_smax, off_cs, off_ci, off_part, total_bytes;
+  int n0p;             // inv_pad(N0)
+  size_t off_inv;      // N0 > INV_MAX on the select path: [B][n0p] sorted invalid lists
+  bool wide;           // k > 256: the chunked exact path
+  int64_t xc;          // its chunk (items)
+  size_t off_rkey, off_ridx;
 };
 
 static size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
@@ -1371,7 +1623,7 @@ static PackLayout pack_layout(int64_t X, int D) {
   return L;
 }
 
-static TopkPlan plan_topk(int B, int64_t X, int D, int k) {
+static TopkPlan plan_topk(int B, int64_t X, int D, int k, int N0) {
   TopkPlan p{};
   p.KS = ceil_div(D, 4);
   const int n_qg = ceil_div(B, QG);
@@ -1435,6 +1687,24 @@ static TopkPlan plan_topk(int B, int64_t X, int D, int k) {
     p.off_ci = o;   o = align256(o + sizeof(int) * (size_t)B * FILTER_CAP);
     p.off_part = o;
     p.total_bytes = o + p.part_bytes;
+  }
+  p.n0p = inv_pad(N0);
+  p.off_inv = 0;
+  p.wide = k > 256;
+  if (p.wide) {  // [B][xc] chunk keys (<= 256 MiB), [B][k] running list, sorted invalid rows
+    const int64_t cap = ((int64_t)1 << 26) / B;
+    p.xc = X < cap ? X : (cap < 4096 ? 4096 : cap);
+    p.small = p.filter = false;
+    size_t o = align256(sizeof(uint32_t) * (size_t)B * p.xc);
+    p.off_rkey = o; o = align256(o + sizeof(uint32_t) * (size_t)B * k);
+    p.off_ridx = o; o = align256(o + sizeof(int64_t) * (size_t)B * k);
+    p.off_inv = o;  o += sizeof(int64_t) * (size_t)B * p.n0p;
+    p.total_bytes = o;
+    return p;
+  }
+  if (!p.small && N0 > INV_MAX) {
+    p.off_inv = align256(p.total_bytes);
+    p.total_bytes = p.off_inv + sizeof(int64_t) * (size_t)B * p.n0p;
   }
   return p;
 }
@@ -1514,9 +1784,9 @@ extern "C" int mips_pack_items(const float* items, int64_t X, int D, float* pack
   return 0;
 }
 
-extern "C" size_t mips_topk_workspace_size(int B, int64_t X, int D, int k) {
-  if (B <= 0 || X <= 0 || D <= 0 || k <= 0) return 0;
-  return plan_topk(B, X, D, k).total_bytes;
+extern "C" size_t mips_topk_workspace_size(int B, int64_t X, int D, int k, int N0) {
+  if (B <= 0 || X <= 0 || D <= 0 || k <= 0 || N0 < 0) return 0;
+  return plan_topk(B, X, D, k, N0).total_bytes;
 }
 
 extern "C" int mips_topk(const float* queries, const float* packed_items, int64_t X, int D,
@@ -1525,23 +1795,53 @@ extern "C" int mips_topk(const float* queries, const float* packed_items, int64_
                          int64_t* out_index, void* workspace, size_t ws_bytes, void* stream) {
   GR_REQUIRE(queries && packed_items && out_scores && out_ids, "mips_topk: null pointer");
   GR_REQUIRE(B >= 0 && X >= 0 && D > 0 && D <= 256, "mips_topk: D=%d not in [1, 256]", D);
-  GR_REQUIRE(k > 0 && k <= 256, "mips_topk: k=%d not in [1, 256]", k);
-  GR_REQUIRE(N0 >= 0 && N0 <= INV_MAX && (N0 == 0 || invalid_ids),
-             "mips_topk: N0=%d not in [0, %d] (or invalid_ids null)", N0, INV_MAX);
+  GR_REQUIRE(k > 0 && k <= KW_MAX, "mips_topk: k=%d not in [1, %d]", k, KW_MAX);
+  GR_REQUIRE(N0 >= 0 && N0 <= INV_BIG && (N0 == 0 || invalid_ids),
+             "mips_topk: N0=%d not in [0, %d] (or invalid_ids null)", N0, INV_BIG);
   GR_REQUIRE(X < 0x7FFFFFFF, "mips_topk: X must be < 2^31 per shard");
   hipStream_t st = (hipStream_t)stream;
   if (B == 0) return 0;
-  TopkPlan p = plan_topk(B, X > 0 ? X : 1, D, k);
+  TopkPlan p = plan_topk(B, X > 0 ? X : 1, D, k, N0);
   GR_REQUIRE(workspace && ws_bytes >= p.total_bytes, "mips_topk: workspace %zu B < %zu B", ws_bytes,
              p.total_bytes);
+  if (p.wide) {
+    char* ws = (char*)workspace;
+    WideArgs w{queries, packed_items, X, D, B, N0, k, item_ids, index_base, invalid_ids, nullptr,
+               p.n0p, p.xc, 0, 0, (uint32_t*)ws, (uint32_t*)(ws + p.off_rkey),
+               (int64_t*)(ws + p.off_ridx), 1, 0, out_scores, out_ids, out_index};
+    if (item_ids && N0 > 0) {
+      int64_t* sorted_rows = (int64_t*)(ws + p.off_inv);
+      w.inv_sorted = sorted_rows;
+      GR_TIMED("mips_sort_invalid", st, hipLaunchKernelGGL(mips_sort_invalid_kernel, dim3(B), dim3(1024),
+                                                           sizeof(int64_t) * p.n0p, st, invalid_ids, N0,
+                                                           p.n0p, sorted_rows, nullptr));
+      GR_LAUNCH_CHECK("mips_topk(sort invalid)");
+    }
+    for (int64_t c0 = 0; c0 < X || c0 == 0; c0 += p.xc) {
+      w.c0 = c0;
+      w.n = X - c0 < p.xc ? X - c0 : p.xc;
+      w.last = c0 + p.xc >= X;
+      if (w.n > 0) {
+        GR_TIMED("mips_wide_score", st, hipLaunchKernelGGL(mips_wide_score_kernel,
+                 dim3((unsigned)((w.n + 255) / 256), B), dim3(256), 0, st, w));
+        GR_LAUNCH_CHECK("mips_topk(wide score)");
+      }
+      GR_TIMED("mips_wide_select", st, hipLaunchKernelGGL(mips_wide_select_kernel, dim3(B), dim3(1024), 0, st, w));
+      GR_LAUNCH_CHECK("mips_topk(wide select)");
+      w.first = 0;
+      if (w.last) break;
+    }
+    return 0;
+  }
   if (p.small) {
     float* sc = (float*)workspace;
     int64_t* ix = (int64_t*)(sc + (size_t)B * X);
     ScoreAllArgs s{queries, packed_items, X, D, B, N0, item_ids, index_base, invalid_ids, sc, ix};
+    const size_t inv_lds = item_ids ? sizeof(int64_t) * p.n0p : 0;
     const int KS2 = (p.KS + 1) / 2;
 #define GR_SA(K2)                                                                           \
   case K2:                                                                                  \
-    GR_TIMED("mips_select", st, hipLaunchKernelGGL(mips_scoreall_kernel<K2>, dim3(B), dim3(256), 0, st, s)); \
+    GR_TIMED("mips_select", st, hipLaunchKernelGGL(mips_scoreall_kernel<K2>, dim3(B), dim3(256), inv_lds, st, s)); \
     break;
     switch (KS2) {
       GR_SA(1) GR_SA(2) GR_SA(3) GR_SA(4) GR_SA(5) GR_SA(6) GR_SA(7) GR_SA(8)
@@ -1580,14 +1880,23 @@ extern "C" int mips_topk(const float* queries, const float* packed_items, int64_
     if (rc) return rc;
     FilterMergeArgs fm{f.cand_s, f.cand_i, cnt, B, k, N0, item_ids, index_base, invalid_ids,
                        out_scores, out_ids, out_index, flag, p.KC > 0, tau_e};
-    GR_TIMED("mips_merge", st, hipLaunchKernelGGL(mips_filter_merge_kernel, dim3(B), dim3(256), 0, st, fm));
+    GR_TIMED("mips_merge", st, hipLaunchKernelGGL(mips_filter_merge_kernel, dim3(B), dim3(256),
+                                                  sizeof(int64_t) * p.n0p, st, fm));
     GR_LAUNCH_CHECK("mips_topk(filter merge)");
   }
   // exact range-select path (the filter path's fallback, gated on its flag)
   float* part_score = (float*)(ws + p.off_part);
   int64_t* part_index = (int64_t*)(part_score + (size_t)p.n_ranges * B * p.k_part);
+  int64_t* inv_sorted = nullptr;
+  if (p.off_inv) {  // N0 > INV_MAX: sorted lists for the select kernel's binary searches
+    inv_sorted = (int64_t*)(ws + p.off_inv);
+    GR_TIMED("mips_sort_invalid", st, hipLaunchKernelGGL(mips_sort_invalid_kernel, dim3(B), dim3(1024),
+                                                         sizeof(int64_t) * p.n0p, st, invalid_ids, N0,
+                                                         p.n0p, inv_sorted, flag));
+    GR_LAUNCH_CHECK("mips_topk(sort invalid)");
+  }
   SelectArgs a{queries, packed_items, X, D, B, k, N0, p.n_ranges, p.k_part, p.range_items,
-               item_ids, index_base, invalid_ids, part_score, part_index, flag};
+               item_ids, index_base, invalid_ids, part_score, part_index, flag, inv_sorted};
   int rc;
   switch (p.KS) {
     case 1: case 2: rc = launch_select<2>(a, st); break;

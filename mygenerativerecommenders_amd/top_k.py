@@ -8,7 +8,9 @@ Differences from the reference, all deliberate:
   * the (B, X) logits are never materialised;
   * invalid-id exclusion can be fused (``invalid_ids=``), which
     ``CandidateIndex.get_top_k_outputs`` uses instead of top-(k+N0) + filtering;
-  * limits: D <= 256, k <= 256, N0 <= 256, X < 2^31 (per shard).
+  * limits: D <= 256, k <= 4096, N0 <= 8192, X < 2^31 (per shard).  k <= 256 runs
+    the fused paths; larger k (the reference CandidateIndex asks for k + N0) runs the
+    library's chunked exact path.
 """
 from __future__ import annotations
 
@@ -48,9 +50,14 @@ class PackedItems:
         self.device = items.device
 
 
-def topk_workspace_bytes(B: int, X: int, D: int, k: int) -> int:
-    """Workspace ``mips_topk`` needs for a (B, D) query batch over X items."""
-    return max(int(_lib.lib().mips_topk_workspace_size(B, X, D, k)), 16)
+K_MAX = 4096
+N0_MAX = 8192
+
+
+def topk_workspace_bytes(B: int, X: int, D: int, k: int, N0: int = 0) -> int:
+    """Workspace ``mips_topk`` needs for a (B, D) query batch over X items with N0
+    invalid ids per query."""
+    return max(int(_lib.lib().mips_topk_workspace_size(B, X, D, k, N0)), 16)
 
 
 def mips_topk(queries: torch.Tensor, packed: PackedItems, k: int,
@@ -65,8 +72,8 @@ def mips_topk(queries: torch.Tensor, packed: PackedItems, k: int,
     B, D = queries.shape
     if D != packed.D:
         raise ValueError(f"query dim {D} != item dim {packed.D}")
-    if not 0 < k <= 256:
-        raise ValueError(f"mips_topk supports 0 < k <= 256 (got {k})")
+    if not 0 < k <= K_MAX:
+        raise ValueError(f"mips_topk supports 0 < k <= {K_MAX} (got {k})")
     q = queries.contiguous().float()
     dev = q.device
     ids = None
@@ -81,12 +88,12 @@ def mips_topk(queries: torch.Tensor, packed: PackedItems, k: int,
         if inv.dim() != 2 or inv.shape[0] != B:
             raise ValueError("invalid_ids must be (B, N0)")
         N0 = inv.shape[1]
-        if N0 > 256:
-            raise ValueError(f"mips_topk supports N0 <= 256 invalid ids per row (got {N0})")
+        if N0 > N0_MAX:
+            raise ValueError(f"mips_topk supports N0 <= {N0_MAX} invalid ids per row (got {N0})")
     scores = torch.empty(B, k, dtype=torch.float32, device=dev)
     out_ids = torch.empty(B, k, dtype=torch.int64, device=dev)
     out_idx = torch.empty(B, k, dtype=torch.int64, device=dev) if return_index else None
-    ws_n = topk_workspace_bytes(B, packed.X, D, k)
+    ws_n = topk_workspace_bytes(B, packed.X, D, k, N0)
     if workspace is None:
         ws = torch.empty(ws_n, dtype=torch.uint8, device=dev)
     else:
@@ -125,8 +132,13 @@ class MIPSBruteForceTopK(TopKModule):
     """top_k.py:43-70 — (scores, ids) of the k best inner products.
 
     ``item_embeddings_t`` is the (D, X) transposed view the reference's CandidateIndex
-    keeps; the packed copy is cached per (storage, version) so a table is re-laid out
-    once per ``update_embeddings``, not once per query batch.
+    keeps.  The packed copy is cached so a table is re-laid out once per
+    ``update_embeddings``, not once per query batch.  The cache key is the view's
+    storage pointer, shape and strides plus its version counter when it has one.
+    Inference tensors have none (``Retrieval.retrieve`` is ``@torch.inference_mode``,
+    retrieval.py:19), so ``CandidateIndex.update_embeddings`` also calls
+    ``invalidate()``; a caller that rewrites an inference tensor in place without it
+    must call ``invalidate()`` itself.
     """
 
     def __init__(self) -> None:
@@ -136,9 +148,20 @@ class MIPSBruteForceTopK(TopKModule):
         self._ids_key = None
         self._ids_arange_start: Optional[int] = None
 
+    @staticmethod
+    def _key(t: torch.Tensor):
+        version = None if t.is_inference() else t._version
+        return (t.data_ptr(), tuple(t.shape), tuple(t.stride()), t.device, version)
+
+    def invalidate(self) -> None:
+        """Drops the packed table and the ids check (the table or ids changed)."""
+        self._cache_key = None
+        self._packed = None
+        self._ids_key = None
+        self._ids_arange_start = None
+
     def packed_for(self, item_embeddings_t: torch.Tensor) -> PackedItems:
-        key = (item_embeddings_t.data_ptr(), item_embeddings_t._version,
-               tuple(item_embeddings_t.shape))
+        key = self._key(item_embeddings_t)
         if self._packed is None or self._cache_key != key:
             self._packed = PackedItems(item_embeddings_t.t())
             self._cache_key = key
@@ -148,7 +171,7 @@ class MIPSBruteForceTopK(TopKModule):
         """ids == arange(s, s + X)?  Checked once per ids buffer (one host sync, like
         the reference's per-epoch index refresh); then the kernel derives ids from
         the catalog index and skips the id gathers."""
-        key = (item_ids.data_ptr(), item_ids._version, item_ids.numel())
+        key = self._key(item_ids)
         if self._ids_key != key:
             flat = item_ids.reshape(-1)
             start = int(flat[0].item()) if flat.numel() else 0

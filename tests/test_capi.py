@@ -74,7 +74,9 @@ def test_workspace_size_queries_are_host_only():
                                                 + al(4 * X * 52))
     assert L.mips_packed_items_bytes(X, 65) == 4 * nblk * 9 * 128  # D > 64: no filter copy
     assert L.gr_wgrad_workspace_size(27008, 50, 200) > 0
-    assert L.mips_topk_workspace_size(128, 10_000_000, 50, 200) > 0
+    assert L.mips_topk_workspace_size(128, 10_000_000, 50, 200, 211) > 0
+    assert L.mips_topk_workspace_size(128, 27_278, 50, 200, 2059) > L.mips_topk_workspace_size(128, 27_278, 50, 200, 211)
+    assert L.mips_topk_workspace_size(128, 3953, 50, 2259, 0) > 0
     assert L.hstu_attn_bwd_workspace_size(0, 211, 200, 1, 128) == 0
 
 

@@ -155,7 +155,8 @@ def _gpu_flag(Q, E, ids, invalid, k, index_base=0):
     from mygenerativerecommenders_amd.top_k import PackedItems, mips_topk, topk_workspace_bytes
     dev = torch.device("cuda")
     packed = PackedItems(torch.as_tensor(E).to(dev))
-    ws = torch.full((topk_workspace_bytes(Q.shape[0], E.shape[0], E.shape[1], k),), 7,
+    N0 = 0 if invalid is None else invalid.shape[1]
+    ws = torch.full((topk_workspace_bytes(Q.shape[0], E.shape[0], E.shape[1], k, N0),), 7,
                     dtype=torch.uint8, device=dev)
     s, i, x = mips_topk(torch.as_tensor(Q).to(dev), packed, k,
                         item_ids=None if ids is None else torch.as_tensor(ids).to(dev),
@@ -318,3 +319,162 @@ def test_mips_filter_bf16_nan_row_takes_exact_path():
         n = int(keep.sum())
         assert np.array_equal(i[b][keep], ri[b][:n])
         assert np.array_equal(s[b][keep].view(np.uint32), rs[b][:n].view(np.uint32))
+
+
+# ---------------------------------------------------------------- reference caller sequence
+# Retrieval.retrieve (retrieval.py:19-47) runs under @torch.inference_mode: the candidate
+# table is an inference tensor (no version counter), update_embeddings() is called on
+# first use with the L2-normalised item embeddings, and invalid_ids = past_ids (B, N)
+# with zero padding -- N0 = 211 at ml-1m and 2059 at ml-20m.
+
+def _past_ids(g, B, N0, ids):
+    inv = np.zeros((B, N0), np.int64)
+    for b in range(B):
+        L = int(g.integers(N0 // 4, N0 + 1))
+        inv[b, :L] = g.choice(ids, L)
+    return inv
+
+
+def _retrieve_like_reference(E, Q, ids, inv, k, second_epoch=True):
+    from mygenerativerecommenders_amd.candidate_index import CandidateIndex
+    from mygenerativerecommenders_amd.top_k import MIPSBruteForceTopK
+    dev = torch.device("cuda")
+    out = []
+    with torch.inference_mode():
+        table = torch.tensor(E, device=dev)
+        index = CandidateIndex(k=k, ids=torch.tensor(ids), top_k_module=MIPSBruteForceTopK()).to(dev)
+        assert index.embeddings is None
+        index.update_embeddings(table.unsqueeze(0))
+        q = torch.tensor(Q, device=dev)
+        past = torch.tensor(inv, device=dev)
+        out.append([t.cpu().numpy() for t in index.get_top_k_outputs(q, invalid_ids=past)])
+        if second_epoch:
+            # next validation epoch: the same storage rewritten in place (inference tensors
+            # carry no version counter), then update_embeddings() as on_validation_epoch_start
+            table.mul_(-1.0)
+            index.update_embeddings(table.unsqueeze(0))
+            out.append([t.cpu().numpy() for t in index.get_top_k_outputs(q, invalid_ids=past)])
+    torch.cuda.synchronize()
+    return out
+
+
+@pytest.mark.parametrize("X,N0,explicit", [
+    (3953, 211, False),      # ml-1m: small-catalog path
+    (3953, 2059, True),      # small-catalog path, explicit ids, list in dynamic LDS
+    (27_278, 211, False),    # ml-20m catalog: range-select path, LDS lists
+    (27_278, 2059, False),   # ml-20m validation: N0 = 2059, pre-sorted workspace lists
+    (27_278, 2059, True),
+    (300_000, 2059, False),  # filter path, N0 = 2059 (list in dynamic LDS of the merge)
+])
+def test_retrieve_inference_mode_bitexact(X, N0, explicit):
+    g = np.random.default_rng(X + N0)
+    B, D, k = 128, 50, 200
+    Q, E, _ = _normal_catalog(g, B, X, D, 0)
+    ids = (g.permutation(np.arange(7, 7 + 2 * X, 2, dtype=np.int64)) if explicit
+           else np.arange(1, X + 1, dtype=np.int64))
+    inv = _past_ids(g, B, N0, ids)
+    got = _retrieve_like_reference(E, Q, ids, inv, k)
+    for (top_ids, top_scores), sign in zip(got, (1.0, -1.0)):
+        rs, ri, _ = topk_oracle.mips_topk(Q, (sign * E).astype(np.float32), ids, inv, k)
+        assert np.array_equal(top_ids, ri), f"ids differ in rows {np.where((top_ids != ri).any(1))[0][:8]}"
+        assert np.array_equal(top_scores.view(np.uint32), rs.view(np.uint32))
+
+
+def _reference_filter(scores, ids, invalid, k):
+    """candidate_index.py:141-158 restated in torch: drop the row's invalid ids from the
+    top-k' list, keep the first k (nonzero + view(-1, k): needs >= k valid per row)."""
+    valid = ~(ids.unsqueeze(2) == invalid.unsqueeze(1)).max(2)[0]
+    valid = torch.logical_and(valid, torch.cumsum(valid.int(), dim=1) <= k)
+    off = torch.nonzero(valid, as_tuple=True)[1].view(-1, k)
+    return torch.gather(ids, 1, off), torch.gather(scores, 1, off)
+
+
+@pytest.mark.parametrize("X,N0,explicit", [(3953, 211, False), (27_278, 2059, False),
+                                           (27_278, 2059, True), (1000, 600, False)])
+def test_reference_k_prime_sequence_equals_fused(X, N0, explicit):
+    """The reference's CandidateIndex asks its top-k module for k' = min(k + N0, X) and
+    filters (candidate_index.py:125-158); with our MIPSBruteForceTopK that takes the
+    wide-k path (k' = 411 / 2259).  Same ids and scores as the fused exclusion."""
+    from mygenerativerecommenders_amd.candidate_index import CandidateIndex
+    from mygenerativerecommenders_amd.top_k import MIPSBruteForceTopK
+    g = np.random.default_rng(X + 3 * N0)
+    B, D, k = 64, 50, 200
+    Q, E, _ = _normal_catalog(g, B, X, D, 0)
+    ids = (g.permutation(np.arange(7, 7 + 2 * X, 2, dtype=np.int64)) if explicit
+           else np.arange(1, X + 1, dtype=np.int64))
+    inv = _past_ids(g, B, N0, ids)
+    inv[:, -1] = 0
+    dev = torch.device("cuda")
+    with torch.inference_mode():
+        table = torch.tensor(E, device=dev).unsqueeze(0)
+        mod = MIPSBruteForceTopK()
+        index = CandidateIndex(k=k, ids=torch.tensor(ids), top_k_module=mod, embeddings=table).to(dev)
+        q, past = torch.tensor(Q, device=dev), torch.tensor(inv, device=dev)
+        k_prime = min(k + N0, X)
+        s_p, i_p = mod(query_embeddings=q, item_embeddings_t=index._embeddings_t,
+                       item_ids=index.ids, k=k_prime, sorted=True)
+        ref_ids, ref_scores = _reference_filter(s_p, i_p, past, k)
+        fused_ids, fused_scores = index.get_top_k_outputs(q, invalid_ids=past)
+    assert torch.equal(ref_ids, fused_ids)
+    assert torch.equal(ref_scores, fused_scores)
+    rs, ri, _ = topk_oracle.mips_topk(Q, E, ids, None, k_prime)
+    assert np.array_equal(i_p.cpu().numpy(), ri)
+    assert np.array_equal(s_p.cpu().numpy().view(np.uint32), rs.view(np.uint32))
+
+
+@pytest.mark.parametrize("B,X,D,k,N0,explicit", [
+    (128, 3953, 50, 411, 0, False),
+    (32, 27_278, 256, 2259, 0, False),      # D = 256
+    (1024, 150_001, 16, 300, 40, False),    # 3 chunks of 65,536 (ragged last), exclusion
+    (1024, 150_001, 16, 300, 40, True),
+    (16, 500, 8, 700, 20, False),           # k > X: rows padded with -inf / -1
+])
+def test_mips_topk_wide_k_bitexact(B, X, D, k, N0, explicit):
+    g = np.random.default_rng(B + X + k)
+    Q, E, _ = _normal_catalog(g, B, X, D, 0)
+    ids = (g.permutation(np.arange(7, 7 + 2 * X, 2, dtype=np.int64)) if explicit
+           else np.arange(1, X + 1, dtype=np.int64))
+    inv = _past_ids(g, B, N0, ids) if N0 else None
+    _check_exact(Q, E, ids, inv, k)
+
+
+def test_mips_topk_wide_k_ties_across_chunks():
+    """All-equal scores over 3 chunks: the k smallest catalog indices, in index order."""
+    B, X, D, k = 1024, 140_000, 8, 333
+    Q = np.ones((B, D), np.float32)
+    E = np.full((X, D), 0.5, np.float32)
+    inv = np.tile(np.array([1, 5, 65_540, 0], np.int64)[None, :], (B, 1))
+    _check_exact(Q, E, np.arange(X, dtype=np.int64), inv, k)
+
+
+# ---------------------------------------------------------------- C4 at full size
+def test_c4_10m_single_and_8_shards_bitexact():
+    """10M items, B = 128, k = 200, 211 invalid ids; one shard, and 8 row
+    shards of 1.25M merged by mips_merge_topk (the all-gather's device merge)."""
+    from mygenerativerecommenders_amd.top_k import PackedItems, merge_topk, mips_topk
+    g = np.random.default_rng(2024)
+    B, X, D, k, N0, P = 128, 10_000_000, 50, 200, 211, 8
+    E = g.standard_normal((X, D), dtype=np.float32)
+    E /= np.linalg.norm(E, axis=1, keepdims=True)
+    Q = g.standard_normal((B, D), dtype=np.float32)
+    Q /= np.linalg.norm(Q, axis=1, keepdims=True)
+    inv = _past_ids(g, B, N0, np.arange(1, X + 1, dtype=np.int64))
+    rs, ri, rx = topk_oracle.mips_topk(Q, E, np.arange(1, X + 1, dtype=np.int64), inv, k)
+    dev = torch.device("cuda")
+    q, past = torch.tensor(Q, device=dev), torch.tensor(inv, device=dev)
+    Et = torch.tensor(E, device=dev)
+    pk = PackedItems(Et)
+    s, i, x = mips_topk(q, pk, k, invalid_ids=past, index_base=1, return_index=True)
+    assert np.array_equal(i.cpu().numpy(), ri)
+    assert np.array_equal(s.cpu().numpy().view(np.uint32), rs.view(np.uint32))
+    del pk
+    parts = []
+    for r in range(P):
+        a, b = r * X // P, (r + 1) * X // P
+        pk = PackedItems(Et[a:b])
+        parts.append(mips_topk(q, pk, k, invalid_ids=past, index_base=a + 1, return_index=True))
+        del pk
+    s, i, x = merge_topk(torch.stack([p[0] for p in parts]), torch.stack([p[2] for p in parts]),
+                         torch.stack([p[1] for p in parts]), k, return_index=True)
+    assert np.array_equal(i.cpu().numpy(), ri)
+    assert np.array_equal(s.cpu().numpy().view(np.uint32), rs.view(np.uint32))
