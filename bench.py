@@ -87,8 +87,21 @@ def peak_table():
     return {"fp32_mfma_tflops": 157.3, "bf16_mfma_tflops": 2500.0, "hbm_gbs": 8000.0}
 
 
-def cpu_baseline_hstu(B_sample, N0, out_len, D, blocks, budget_s=12.0):
-    """Times the oracle's padded-order fp32 restatement (fwd+bwd) on the host cores."""
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline_hstu(B_sample, N0, out_len, D, blocks, budget_s=20.0):
+    """Times the oracle's reference-order fp32 restatement (fwd+bwd, train mode with
+    dropout 0.2) on the host cores: within 5 % of the reference HSTU module itself in
+    the build container (profiles/r2_cpu_proxy_check.json, scripts/cpu_proxy_check.py)."""
     import numpy as np
 
     from mygenerativerecommenders_amd.bucket_table import BUCKET_THRESHOLDS
@@ -103,18 +116,22 @@ def cpu_baseline_hstu(B_sample, N0, out_len, D, blocks, budget_s=12.0):
 
     def one():
         xr = x.clone().requires_grad_(True)
-        y = O.hstu_forward_padded(lengths, xr, ts, cfg, layers, thr)
+        y = O.hstu_forward_reference_order(lengths, xr, ts, cfg, layers, 0.2, True)
         (y * dy).sum().backward()
 
+    del thr
     one()  # warm-up
-    n, t0 = 0, time.perf_counter()
+    times = []
+    t0 = time.perf_counter()
     while True:
+        t1 = time.perf_counter()
         one()
-        n += 1
-        if time.perf_counter() - t0 > budget_s / 2 or n >= 20:
+        times.append(time.perf_counter() - t1)
+        if time.perf_counter() - t0 > budget_s or len(times) >= 7:
             break
-    dt = (time.perf_counter() - t0) / n
-    return B_sample / dt, n, dt
+    times.sort()
+    dt = times[len(times) // 2]  # median
+    return B_sample / dt, len(times), dt
 
 
 def cpu_baseline_topk(B, X, D, k, N0, budget_s=8.0):
@@ -272,6 +289,138 @@ def e2e_train_leg(args, device, world, lengths, ts, past_ids):
                         "negatives, T=0.05) + backward + all-reduce + AdamW"}
 
 
+def hstu_step_flops(L, D, H, dqk, dv, blocks):
+    """SURVEY.md §8d algorithmic FLOPs of one sequence of length L, fwd + bwd (= 3 x fwd,
+    recompute not counted)."""
+    per_layer = (2.0 * L * D * (2 * H * dv + 2 * H * dqk) + 2.0 * L * H * dv * D
+                 + 2.0 * H * (dqk + dv) * L * (L + 1) / 2)
+    return 3.0 * per_layer * blocks
+
+
+def encoder_leg(B, N0, out_len, D, blocks, H, steps, warmup, device, world, seed,
+                eager=False, instrument=False):
+    """Times the encoder training step alone at one shape: HSTU fwd + bwd (input and
+    parameter grads) -> gradient all-reduce -> fused AdamW, fixed-length rows, train
+    mode, captured as two HIP graphs around the all-reduce.  Used for the C2 batch
+    sweep and the C3 (ml-20m width) leg.  ``instrument``: per-kernel device times from
+    an eager re-run with the library's event pairs."""
+    from mygenerativerecommenders_amd import _lib
+    from mygenerativerecommenders_amd.distributed import FlatGradAllReducer
+    from mygenerativerecommenders_amd.hstu import HSTU
+    N = N0 + out_len
+    torch.manual_seed(0)
+    dh = D // H
+    enc = HSTU(max_sequence_len=N0, max_output_len=out_len, embedding_dim=D,
+               item_embedding_dim=D, num_blocks=blocks, num_heads=H, linear_dim=dh,
+               attention_dim=dh, normalization="rel_bias", linear_config="uvqk",
+               linear_activation="silu", linear_dropout_rate=0.2,
+               attn_dropout_rate=0.0).to(device).train()
+    reducer = FlatGradAllReducer(list(enc.parameters()))
+    opt = torch.optim.AdamW(enc.parameters(), lr=1e-3, betas=(0.9, 0.98), weight_decay=1e-3,
+                            fused=True, capturable=True)
+    lengths, x, ts, _, dy = make_batch(B, N0, out_len, D, seed, device)
+    x.requires_grad_(True)
+
+    def fwd_bwd():
+        y, _ = enc(past_lengths=lengths, user_embeddings=x, valid_mask=None,
+                   past_payloads={"timestamps": ts}, max_len=N0)
+        y.backward(dy)
+
+    def eager_step():
+        reducer.zero_grad()
+        x.grad = None
+        fwd_bwd()
+        reducer.allreduce(world)
+        opt.step()
+
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(max(2, warmup)):
+            eager_step()
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    step = eager_step
+    if not eager:
+        reducer.zero_grad()
+        x.grad = None
+        g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g_fb):
+            fwd_bwd()
+        with torch.cuda.graph(g_opt):
+            opt.step()
+
+        def step():
+            g_fb.replay()
+            reducer.allreduce(world, inplace=True)
+            g_opt.replay()
+    for _ in range(warmup):
+        step()
+    _sync_barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    _sync_barrier(world)
+    dt = _max_over_ranks(time.perf_counter() - t0, world)
+    out = {"value": round(B * world * steps / dt, 2), "unit": "seq/s",
+           "ms_per_step": round(dt / steps * 1e3, 4), "steps": steps, "global_batch": B * world}
+    if instrument:
+        hold = _gpu_hold_fn()
+        _lib.timing_enable(True)
+        for _ in range(steps):
+            hold(5.0)
+            eager_step()
+        _sync_barrier(world)
+        _lib.timing_enable(False)
+        kt = _lib.kernel_times()
+        out["kernel_avg_ms"] = {n: t / c for n, (t, c) in kt.items() if c}
+        out["kernel_per_step_ms"] = {n: t / steps for n, (t, c) in kt.items() if c}
+        out["lengths"] = lengths.cpu()
+    del enc, opt, reducer, x, dy
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return out
+
+
+def check_retrieval(Q, shard, a, inv, ids_out, scores_out, k, world, chunk=1 << 20, tol=1e-5):
+    """Device-side check of a retrieval result over a row-sharded catalog with ids
+    a+1 .. b per rank: (1) every returned id is valid (not in its row's invalid list)
+    and unique; (2) an fp32 torch recomputation of each returned item's score agrees
+    with the returned score within tol; (3) every valid item whose recomputed score
+    exceeds the k-th returned score by more than tol is among the returned items.
+    Counts are summed over the ranks (one all-reduce)."""
+    B = Q.shape[0]
+    X_loc = shard.shape[0]
+    kth = scores_out[:, k - 1]
+    thr = kth + tol
+    n_above = torch.zeros(B, dtype=torch.int64, device=Q.device)
+    for c in range(0, X_loc, chunk):
+        C = min(chunk, X_loc - c)
+        logits = torch.empty(B, C + 1, device=Q.device)
+        logits[:, :C] = Q @ shard[c:c + C].t()
+        loc = inv - 1 - a - c
+        loc = torch.where((loc >= 0) & (loc < C), loc, torch.full_like(loc, C))
+        logits.scatter_(1, loc, float("-inf"))
+        n_above += (logits[:, :C] > thr[:, None]).sum(1)
+    loc = ids_out - 1 - a
+    mine = (loc >= 0) & (loc < X_loc)
+    rows = shard[loc.clamp(0, X_loc - 1)]
+    rescored = torch.where(mine, (rows * Q[:, None, :]).sum(-1), torch.zeros_like(scores_out))
+    if world > 1:
+        import torch.distributed as dist
+        dist.all_reduce(n_above)
+        dist.all_reduce(rescored)
+    diff = (rescored - scores_out).abs().max().item()
+    in_r_above = (rescored > thr[:, None]).sum(1)
+    valid = ~(ids_out.unsqueeze(2) == inv.unsqueeze(1)).any(2)
+    srt = ids_out.sort(1).values
+    unique = bool((srt[:, 1:] != srt[:, :-1]).all())
+    ok = bool(valid.all()) and unique and diff <= tol and bool((n_above == in_r_above).all())
+    return {"ok": ok, "all_valid": bool(valid.all()), "unique": unique,
+            "max_abs_score_diff": diff, "items_above_kth_outside_result":
+            int((n_above - in_r_above).abs().max().item()), "tol": tol}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -289,8 +438,14 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-retrieval-leg", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no HIP-graph capture of the step")
-    ap.add_argument("--e2e-steps", type=int, default=0,
-                    help="timed steps of the full training-step leg (0 = skip; opt-in)")
+    ap.add_argument("--e2e-steps", type=int, default=20,
+                    help="timed steps of the full training-step leg (0 = skip)")
+    ap.add_argument("--sweep", default="32,128,512,2048",
+                    help="C2 batch sweep of the encoder step (comma list; '' = skip)")
+    ap.add_argument("--c3-steps", type=int, default=5,
+                    help="timed steps of the C3 leg (B=32, N=2059, D=256, 8 blocks; 0 = skip)")
+    ap.add_argument("--cpu-batch", type=int, default=128,
+                    help="sequences per iteration of the CPU proxy baseline")
     args = ap.parse_args()
 
     from mygenerativerecommenders_amd import _lib
@@ -454,9 +609,10 @@ def main():
         Q = Q / Q.norm(dim=-1, keepdim=True)
         inv = torch.randint(1, X + 1, (B, N), device=device, generator=g3)
         sidx = ShardedCandidateIndex(args.k, ids_shard, shard, a)
-        del shard
         for _ in range(3):
-            sidx.get_top_k_outputs(Q, invalid_ids=inv)
+            r_ids, r_scores = sidx.get_top_k_outputs(Q, invalid_ids=inv)
+        r_check = check_retrieval(Q, shard, a, inv, r_ids, r_scores, args.k, world)
+        del shard
         _sync_barrier(world)
         t1 = time.perf_counter()
         for _ in range(args.retrieval_steps):
@@ -491,12 +647,20 @@ def main():
         bf16_filter = (rkern == "mips_filter" and xs >= 262_144 and D <= 64
                        and not os.environ.get("GR_MIPS_FP32_FILTER"))
         if bf16_filter:
-            # the filter streams the bf16 copy once: 16 items x 32 dims x 2 B per k-chunk
-            alg_bytes = float((xs + 15) // 16 * ((D + 31) // 32) * 1024)
+            # bound used: HBM, on the bf16 payload of the table (X x D x 2 B) that the
+            # filter streams once; the stored copy pads D to 32-dim chunks (padded_bytes)
+            alg_bytes = float(xs * D * 2)
+            pad_bytes = float((xs + 15) // 16 * ((D + 31) // 32) * 1024)
             ach_r = alg_bytes / (ktop * 1e-3) / 1e9 if ktop else 0.0
-            rroof = {"bound": "hbm", "achieved": round(ach_r, 1), "peak": peaks["hbm_gbs"],
+            # SURVEY §8d's bound for this workload (fp32 compute, 2BXD flop at 157.3 TF/s
+            # vs 4XD bytes at 8 TB/s): the ms per batch it allows, beside ours
+            survey_ms = max(fl / (peaks["fp32_mfma_tflops"] * 1e12),
+                            4.0 * xs * D / (peaks["hbm_gbs"] * 1e9)) * 1e3
+            rroof = {"bound": "hbm", "bound_basis": "bf16 table payload X*D*2 B, read once",
+                     "achieved": round(ach_r, 1), "peak": peaks["hbm_gbs"],
                      "unit": "GB/s", "frac": round(ach_r / peaks["hbm_gbs"], 4),
-                     "algorithmic_bytes": alg_bytes,
+                     "algorithmic_bytes": alg_bytes, "padded_bytes": pad_bytes,
+                     "survey_fp32_bound_ms_per_batch": round(survey_ms, 4),
                      "mfma_tflops_bf16": round(fl / (ktop * 1e-3) / 1e12, 1) if ktop else 0.0}
         else:
             alg_bytes = 4.0 * xs * 8 * ((D + 7) // 8)
@@ -508,15 +672,58 @@ def main():
         retrieval = {
             "metric": "top-k items scored/s", "value": cand_per_s, "unit": "items/s",
             "scaling": "strong", "ms_per_query_batch": dtr / args.retrieval_steps * 1e3,
-            "config": {"workload": "C4: 10M-item catalog row-sharded, B=128 queries, k=200, "
-                                   "211 invalid ids, all-gather + device merge",
+            "config": {"workload": ("C4: 10M-item catalog row-sharded over %d GPUs, B=128 queries, "
+                                    "k=200, 211 invalid ids, all-gather + device merge" % world)
+                                   if world > 1 else
+                                   ("C4: 10M-item catalog on 1 GPU (one shard, no merge), "
+                                    "B=128 queries, k=200, 211 invalid ids"),
                        "items": X, "queries": B, "k": args.k, "dim": D,
                        "filter_scores": "bf16 (exact f32 rescoring)" if bf16_filter else "f32"},
+            "check": r_check,
             "per_query_batch_device_ms": r_dev,
             "roofline": dict(kernel=rkern, **rroof, traffic=r_traffic,
                              traffic_source=traffic_src, avg_launch_ms=round(ktop, 4),
                              merge_avg_launch_ms=round(kmerge, 4), flops_per_launch=fl),
         }
+
+    # ---- C2 batch sweep (encoder step alone) and the C3 leg
+    sweep = None
+    if args.sweep:
+        sweep = []
+        for Bs in [int(v) for v in args.sweep.split(",") if v]:
+            r = encoder_leg(Bs, N0, out_len, D, blocks, 1, max(5, min(20, 2560 // Bs)), 3,
+                            device, world, 2000 + rank)
+            sweep.append({"batch": Bs, "seq_per_s": r["value"], "ms_per_step": r["ms_per_step"]})
+    c3 = None
+    if args.c3_steps > 0:
+        B3, N3, D3, L3 = 32, 2048, 256, 8
+        r = encoder_leg(B3, N3, out_len, D3, L3, 1, args.c3_steps, 2, device, world,
+                        3000 + rank, instrument=True)
+        step_flops = B3 * hstu_step_flops(N3, D3, 1, D3, D3, L3)
+        ach3 = step_flops / (r["ms_per_step"] * 1e-3) / 1e12
+        f3, dkv3, dq3 = attn_flops(r["lengths"], 1, D3, D3, L3)
+        rows3, nout3 = B3 * N3, 4 * D3
+        fpl3 = {"attn_fwd": f3, "attn_bwd": dkv3 + dq3, "attn_bwd_dkv": dkv3, "attn_bwd_dq": dq3,
+                "ln_uvqk_fwd": 2.0 * rows3 * D3 * nout3, "gate_o_fwd": 2.0 * rows3 * D3 * D3,
+                "gate_o_bwd": 2.0 * rows3 * D3 * D3, "ln_uvqk_bwd": 2.0 * rows3 * nout3 * D3,
+                "wgrad_partial": (2.0 * rows3 * D3 * D3 + 2.0 * rows3 * D3 * nout3) / 2.0}
+        kps = r["kernel_per_step_ms"]
+        dom3 = max(kps, key=kps.get)
+        ach_k = fpl3.get(dom3, 0.0) / (r["kernel_avg_ms"][dom3] * 1e-3) / 1e12
+        c3 = {"metric": "HSTU seq/s (fwd+bwd)", "value": r["value"], "unit": "seq/s",
+              "ms_per_step": r["ms_per_step"], "steps": args.c3_steps, "dtype": "fp32",
+              "config": {"workload": "C3: ml-20m width HSTU train step (fwd+bwd+AdamW)",
+                         "global_batch": B3 * world, "seq_len": N3, "padded_len": N3 + out_len,
+                         "dim": D3, "blocks": L3, "heads": 1},
+              "algorithmic_tflop_per_step": round(step_flops / 1e12, 4),
+              "roofline": {"bound": "mfma", "achieved": round(ach3, 2),
+                           "peak": peaks["fp32_mfma_tflops"], "unit": "TFLOP/s",
+                           "frac": round(ach3 / peaks["fp32_mfma_tflops"], 4),
+                           "basis": "whole step: SURVEY §8d 83.8 GFLOP/seq (3 x fwd) / step time"},
+              "dominant_kernel": {"kernel": dom3, "avg_launch_ms": round(r["kernel_avg_ms"][dom3], 4),
+                                  "achieved": round(ach_k, 2), "unit": "TFLOP/s",
+                                  "frac": round(ach_k / peaks["fp32_mfma_tflops"], 4)},
+              "per_step_device_ms": {k: round(v, 4) for k, v in sorted(kps.items(), key=lambda kv: -kv[1])}}
 
     e2e = None
     if args.e2e_steps > 0:
@@ -527,12 +734,15 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = torch.get_num_threads()
-        sps, n_it, dt_it = cpu_baseline_hstu(16, N0, out_len, D, blocks)
+        threads = torch.get_num_threads()  # the box's CPU share (OMP_NUM_THREADS)
+        sps, n_it, dt_it = cpu_baseline_hstu(args.cpu_batch, N0, out_len, D, blocks)
         cps, n_r, dt_r = cpu_baseline_topk(B, 200_000, D, args.k, N)
         cpu = {"value": round(sps, 2), "unit": "seq/s", "cores": threads, "kind": "port",
-               "sample": f"oracle padded-order fp32 HSTU fwd+bwd, 16 seqs x {N0} tokens, "
-                         f"{blocks} blocks, {n_it} iters ({dt_it * 1e3:.0f} ms/iter)",
+               "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
+               "sample": f"oracle reference-order fp32 HSTU fwd+bwd (train, dropout 0.2), "
+                         f"{args.cpu_batch} seqs x {N0} tokens, {blocks} blocks, median of "
+                         f"{n_it} iters ({dt_it * 1e3:.0f} ms/iter); proxy within 5 % of the "
+                         f"reference module (profiles/r2_cpu_proxy_check.json)",
                "retrieval": {"value": round(cps, 1), "unit": "items/s", "cores": threads,
                              "kind": "port",
                              "sample": f"C oracle (fmaf chain, OpenMP) B={B} X=200000 k={args.k}"
@@ -559,6 +769,8 @@ def main():
                        "parallelism": f"dp{world}"},
             "roofline": roofline,
             "retrieval": retrieval,
+            "c2_batch_sweep": sweep,
+            "c3": c3,
             "e2e_train_step": e2e,
             "cpu_baseline": cpu,
         }

@@ -100,7 +100,8 @@ KERNEL_NAMES = ("bucket_map", "attn_fwd", "attn_bwd", "attn_bwd_dkv", "attn_bwd_
                 "mips_filter", "mips_select_fallback", "mips_merge_fallback", "cumsum",
                 "dense_to_jagged", "jagged_to_padded", "l2_normalize", "current_embeddings",
                 "sampled_softmax_fwd", "sampled_softmax_bwd", "sampled_softmax_csr",
-                "sampled_softmax_table_grad", "preproc", "item_embedding")
+                "sampled_softmax_table_grad", "preproc", "item_embedding", "mips_sort_invalid",
+                "mips_wide_score", "mips_wide_select")
 
 
 def timing_enable(on: bool = True):

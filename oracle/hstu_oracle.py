@@ -186,3 +186,73 @@ def hstu_forward_padded(lengths, user_embeddings, ts, cfg: HSTUConfig, layers,
         o_in = torch.cat([u, an, u * an], -1) if cfg.concat_ua else u * an
         x = (o_in @ p["o_w"].t() + p["o_b"] + x) * valid
     return x
+
+
+# ----------------------------------------------------------------------------------
+# Reference-op-order variant: the CPU throughput proxy.
+# Same math as the two variants above, in the order the reference runs it on a CPU
+# without fbgemm: per-row Python loops for every pad / unpad (ops.py:60-114 fallbacks),
+# linear layers on the jagged rows, the (B, N, N) bias built with the pad/repeat
+# Toeplitz trick and the fp32-log bucketisation, the float mask multiply, dropout
+# before the output projection (train mode).  scripts/cpu_proxy_check.py times it
+# against the reference's own HSTU module in the build container.
+# ----------------------------------------------------------------------------------
+
+def _rows_to_jagged(dense: torch.Tensor, offsets: torch.Tensor) -> torch.Tensor:
+    """ops.py:60-73 fallback: one slice per row, then one cat."""
+    parts = []
+    for b in range(offsets.numel() - 1):
+        parts.append(dense[b, :offsets[b + 1] - offsets[b]])
+    return torch.cat(parts, 0)
+
+
+def _rows_to_padded(values: torch.Tensor, offsets: torch.Tensor, n: int) -> torch.Tensor:
+    """ops.py:104-114 fallback: a zero (B, n, ...) tensor filled row by row."""
+    B = offsets.numel() - 1
+    out = values.new_zeros((B, n) + tuple(values.shape[1:]))
+    for b in range(B):
+        s, e = offsets[b], offsets[b + 1]
+        out[b, :e - s] = values[s:e]
+    return out
+
+
+def _rel_bias_reference_order(ts: torch.Tensor, N: int, pos_w, ts_w) -> torch.Tensor:
+    """hstu.py:96-128: a (N, 3N-2) Toeplitz band from the padded, repeated pos_w, its
+    middle N columns; fp32-log buckets of ext_ts[i+1] - ts[j]; index_select of ts_w."""
+    B = ts.shape[0]
+    band = F.pad(pos_w[: 2 * N - 1], [0, N]).repeat(N)[:-N].view(1, N, 3 * N - 2)
+    r = (2 * N - 1) // 2
+    ext = torch.cat([ts, ts[:, N - 1:N]], 1)
+    bucket = bucket_reference_semantics(ext[:, 1:].unsqueeze(2) - ext[:, :-1].unsqueeze(1))
+    ts_bias = torch.index_select(ts_w, 0, bucket.view(-1)).view(B, N, N)
+    return band[:, :, r:-r] + ts_bias
+
+
+def hstu_forward_reference_order(lengths, user_embeddings, ts, cfg: HSTUConfig, layers,
+                                 dropout_p: float = 0.0, training: bool = False) -> torch.Tensor:
+    """hstu.py:633-672 -> 482-518 -> 266-413 -> 134-205 in the reference's op order."""
+    B, N, D = user_embeddings.shape
+    H, dqk, dv = cfg.H, cfg.dqk, cfg.dv
+    offsets = torch.cat([torch.zeros(1, dtype=torch.int64),
+                         torch.cumsum(lengths.to(torch.int64), 0)])
+    mask = 1.0 - torch.triu(torch.ones(N, N, dtype=torch.bool), diagonal=1).float()
+    x = _rows_to_jagged(user_embeddings, offsets)
+    for p in layers:
+        normed = F.layer_norm(x, [D], eps=cfg.eps)
+        h = F.silu(torch.mm(normed, p["uvqk"]))
+        u, v, q, k = torch.split(h, [dv * H, dv * H, dqk * H, dqk * H], dim=1)
+        pq = _rows_to_padded(q, offsets, N)
+        pk = _rows_to_padded(k, offsets, N)
+        s = torch.einsum("bnhd,bmhd->bhnm", pq.view(B, N, H, dqk), pk.view(B, N, H, dqk))
+        if ts is not None:
+            s = s + _rel_bias_reference_order(ts, N, p["pos_w"], p["ts_w"]).unsqueeze(1)
+        s = F.silu(s) / N
+        s = s * mask.unsqueeze(0).unsqueeze(0)
+        pv = _rows_to_padded(v, offsets, N).reshape(B, N, H, dv)
+        attn = _rows_to_jagged(torch.einsum("bhnm,bmhd->bnhd", s, pv).reshape(B, N, H * dv),
+                               offsets)
+        an = F.layer_norm(attn, [dv * H], eps=cfg.eps)
+        o_in = torch.cat([u, an, u * an], -1) if cfg.concat_ua else u * an
+        o_in = F.dropout(o_in, p=dropout_p, training=training)
+        x = F.linear(o_in, p["o_w"], p["o_b"]) + x
+    return _rows_to_padded(x, offsets, N)

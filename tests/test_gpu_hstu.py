@@ -74,6 +74,8 @@ def test_hstu_vs_reference_golden(name):
     (8, 200, 11, 50, 4, 1, 50, 20),     # ml-1m geometry (C2), jagged lengths U[20, 200]
     (2, 500, 11, 256, 2, 1, 256, 200),  # ml-20m-like width (C3: D = d = 256), 8 key tiles
     (2, 300, 11, 256, 1, 2, 128, 100),  # C3 variant h = 2, d = 128
+    (2, 2048, 11, 256, 2, 1, 256, 2048),  # C3 geometry: N = 2059, a full 2048-token row
+    (3, 2048, 11, 256, 2, 1, 256, 700),   # C3 ragged rows
 ])
 def test_hstu_shapes_vs_oracle(B, N0, out_len, D, blocks, H, dh, min_len):
     from mygenerativerecommenders_amd.hstu import HSTU
