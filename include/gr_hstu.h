@@ -57,9 +57,12 @@ GR_API int gr_timing_reset(void);
 GR_API int gr_complete_cumsum(const int64_t* lengths, int B, int64_t* offsets, void* stream);
 
 /* Replaces utils/ops.py:41-64 dense_to_jagged: dense (B, N, D) row-major f32 ->
- * jagged (offsets[B], D). */
+ * jagged rows, sequence b at rows offsets[b] .. offsets[b] + min(len_b, N).  Nothing is
+ * written at or past row max_rows (the jagged buffer's size).  zero_fill != 0 also
+ * zeroes the rows a sequence owns past N (lengths above N are truncated, as fbgemm's
+ * gradient of jagged_to_padded_dense) and the rows [offsets[B], max_rows). */
 GR_API int gr_dense_to_jagged(const float* dense, const int64_t* offsets, int B, int N, int D,
-                       int64_t max_rows, float* jagged, void* stream);
+                              int64_t max_rows, int zero_fill, float* jagged, void* stream);
 
 /* Replaces utils/ops.py:67-114 jagged_to_padded_dense (padding_value 0):
  * jagged (offsets[B], D) -> dense (B, N, D); rows >= length are zero. */
@@ -134,6 +137,10 @@ GR_API int gr_sampled_softmax_fwd(const float* out, int64_t ld_out, const float*
  * offsets; its summation order within a row is not fixed (integer atomics).  M*R and V must fit int32; tables
  * and row arrays must be < 2 GiB.  workspace: gr_sampled_softmax_workspace_size bytes. */
 GR_API size_t gr_sampled_softmax_workspace_size(int64_t M, int R, int64_t V, int D);
+/* Byte offset of the backward's status word inside its workspace (valid after a backward
+ * with M * R > 0): 0 = clean; bit 0 = a sample row outside [0, V); bit 1 = a counting-sort
+ * slot outside its row's range.  Flagged samples are dropped, never written out of bounds. */
+GR_API size_t gr_sampled_softmax_status_offset(int64_t M, int R, int64_t V, int D);
 GR_API int gr_sampled_softmax_bwd(const float* out, int64_t ld_out, const float* pos, int64_t ld_pos,
                                   const int64_t* sup_ids, const float* table, int64_t ld_table,
                                   int64_t V, const int64_t* all_ids, const int64_t* offsets,

@@ -46,22 +46,31 @@ __global__ __launch_bounds__(256) void cumsum_kernel(const int64_t* lengths, int
 constexpr int JG_PER = 4;
 constexpr int JG_CHUNK = 256 * JG_PER;
 
+// Bounded by max_rows (the jagged buffer's row count): nothing is written at or past it.
+// zero_fill: the rows of sequence b that the copy does not reach (a length above N is
+// truncated, as fbgemm's dense_to_jagged gradient does) and the rows [offsets[B],
+// max_rows) are zeroed -- the virtual sequence b == B covers the latter.
 template <typename V>
 __global__ __launch_bounds__(256) void dense_to_jagged_kernel(const V* dense, const int64_t* offsets,
                                                               int B, int N, int64_t row_units,
+                                                              int64_t max_rows, int zero_fill,
                                                               V* jagged) {
-  for (int b = blockIdx.y; b < B; b += gridDim.y) {
+  for (int b = blockIdx.y; b <= B; b += gridDim.y) {
     const int64_t s0 = offsets[b];
-    const int64_t L = min(offsets[b + 1] - s0, (int64_t)N);
-    const int64_t n = L * row_units;
-    const V* src = dense + (int64_t)b * N * row_units;
+    const int64_t s1 = b < B ? offsets[b + 1] : max_rows;
+    if (s0 >= max_rows || s0 < 0 || (b == B && !zero_fill)) continue;
+    const int64_t end = min(s1, max_rows);                           // rows this span owns
+    const int64_t L = b < B ? min(min(s1 - s0, (int64_t)N), end - s0) : 0;  // rows copied
+    const int64_t n_copy = L * row_units;
+    const int64_t n = (zero_fill ? end - s0 : L) * row_units;
+    const V* src = dense + (int64_t)min(b, B - 1) * N * row_units;
     V* dst = jagged + s0 * row_units;
     for (int64_t base = (int64_t)blockIdx.x * JG_CHUNK; base < n; base += (int64_t)gridDim.x * JG_CHUNK) {
       V v[JG_PER];
 #pragma unroll
       for (int k = 0; k < JG_PER; ++k) {
         const int64_t i = base + threadIdx.x + 256 * k;
-        if (i < n) v[k] = src[i];
+        v[k] = i < n_copy ? src[i] : V{};
       }
 #pragma unroll
       for (int k = 0; k < JG_PER; ++k) {
@@ -100,15 +109,17 @@ __global__ __launch_bounds__(256) void jagged_to_padded_kernel(const V* jagged, 
 
 template <typename V>
 static void launch_jagged_copy(bool to_jagged, const float* src, const int64_t* offsets, int B, int N,
-                               int D, float* dst, hipStream_t st) {
+                               int D, float* dst, hipStream_t st, int64_t max_rows = 0,
+                               int zero_fill = 0) {
   const int64_t units = (int64_t)D * sizeof(float) / sizeof(V);
   const int64_t chunks = ((int64_t)N * units + JG_CHUNK - 1) / JG_CHUNK;
-  const dim3 grid((unsigned)(chunks > 0 ? chunks : 1), (unsigned)(B < 65535 ? B : 65535));
+  const int ny = to_jagged && zero_fill ? B + 1 : B;
+  const dim3 grid((unsigned)(chunks > 0 ? chunks : 1), (unsigned)(ny < 65535 ? ny : 65535));
   if (to_jagged)
     GR_TIMED("dense_to_jagged", st,
              hipLaunchKernelGGL(dense_to_jagged_kernel<V>, grid, dim3(256), 0, st,
-                                reinterpret_cast<const V*>(src), offsets, B, N, units,
-                                reinterpret_cast<V*>(dst)));
+                                reinterpret_cast<const V*>(src), offsets, B, N, units, max_rows,
+                                zero_fill, reinterpret_cast<V*>(dst)));
   else
     GR_TIMED("jagged_to_padded", st,
              hipLaunchKernelGGL(jagged_to_padded_kernel<V>, grid, dim3(256), 0, st,
@@ -222,16 +233,21 @@ int gr_complete_cumsum(const int64_t* lengths, int B, int64_t* offsets, void* st
 }
 
 int gr_dense_to_jagged(const float* dense, const int64_t* offsets, int B, int N, int D,
-                       int64_t max_rows, float* jagged, void* stream) {
-  (void)max_rows;
-  GR_REQUIRE(dense && offsets && jagged && B >= 0 && N >= 0 && D > 0,
+                       int64_t max_rows, int zero_fill, float* jagged, void* stream) {
+  GR_REQUIRE(dense && offsets && jagged && B >= 0 && N >= 0 && D > 0 && max_rows >= 0,
              "gr_dense_to_jagged: bad args");
-  const int64_t rows = (int64_t)B * N;
-  if (rows == 0) return 0;
+  if (max_rows == 0 || (B == 0 && !zero_fill)) return 0;
+  if (B == 0 || N == 0) {
+    if (zero_fill) gr::zero_words_async(jagged, max_rows * D, (hipStream_t)stream);
+    GR_LAUNCH_CHECK("gr_dense_to_jagged");
+    return 0;
+  }
   if (D % 2 == 0 && gr::aligned8(dense, jagged))
-    gr::launch_jagged_copy<float2>(true, dense, offsets, B, N, D, jagged, (hipStream_t)stream);
+    gr::launch_jagged_copy<float2>(true, dense, offsets, B, N, D, jagged, (hipStream_t)stream,
+                                   max_rows, zero_fill);
   else
-    gr::launch_jagged_copy<float>(true, dense, offsets, B, N, D, jagged, (hipStream_t)stream);
+    gr::launch_jagged_copy<float>(true, dense, offsets, B, N, D, jagged, (hipStream_t)stream,
+                                  max_rows, zero_fill);
   GR_LAUNCH_CHECK("gr_dense_to_jagged");
   return 0;
 }

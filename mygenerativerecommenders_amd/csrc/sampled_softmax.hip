@@ -364,7 +364,8 @@ __global__ __launch_bounds__(kCountThreads) void ssm_count_kernel(const int2* re
 #pragma unroll
     for (int k = 0; k < kCountPer; ++k) {
       const int64_t p = base + (int64_t)k * kCountThreads + tid;
-      vv[k] = p < n ? sort_key(rec[p], p, R, M, V) : -1;
+      const int key = p < n ? sort_key(rec[p], p, R, M, V) : -1;
+      vv[k] = key >= 0 && key < K ? key : -1;  // out-of-range rows: dropped (fill flags them)
     }
 #pragma unroll
     for (int k = 0; k < kCountPer; ++k) lr[k] = vv[k] >= 0 ? atomicAdd(hist + vv[k], 1) : 0;
@@ -381,8 +382,10 @@ __global__ __launch_bounds__(kCountThreads) void ssm_count_kernel(const int2* re
     }
   } else {
     for (int64_t p = (int64_t)blockIdx.x * kCountThreads + threadIdx.x; p < n;
-         p += (int64_t)gridDim.x * kCountThreads)
-      rank[p] = atomicAdd(cnt + sort_key(rec[p], p, R, M, V), 1);
+         p += (int64_t)gridDim.x * kCountThreads) {
+      const int key = sort_key(rec[p], p, R, M, V);
+      rank[p] = key >= 0 && key < K ? atomicAdd(cnt + key, 1) : 0;
+    }
   }
 }
 
@@ -410,13 +413,25 @@ __global__ __launch_bounds__(1024) void ssm_scan_kernel(const int* cnt, int64_t 
   if (tid == 1023) start[V] = part[1023];
 }
 
-// Scatter: sorted[start[key] + rank[p]] = {t, c} of sample p = t * R + r.
+// Scatter: sorted[start[key] + rank[p]] = {t, c} of sample p = t * R + r.  A slot outside
+// its key's [start[key], start[key + 1]) (or a key outside [0, K)) is never written: the
+// sample is dropped and the status word flags it.
 __global__ __launch_bounds__(256) void ssm_fill_kernel(const int2* rec, int64_t n, int R, int64_t M,
-                                                       int64_t V, const int* start, const int* rank,
-                                                       int2* sorted) {
+                                                       int64_t V, int64_t K, const int* start,
+                                                       const int* rank, int2* sorted, int* status) {
   for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < n; p += (int64_t)gridDim.x * 256) {
     const int2 x = rec[p];
-    sorted[start[sort_key(x, p, R, M, V)] + rank[p]] = make_int2((int)(p / R), x.y);
+    const int key = sort_key(x, p, R, M, V);
+    if (key < 0 || key >= K || x.x < 0 || x.x >= V) {
+      atomicOr(status, 1);
+      continue;
+    }
+    const int64_t dst = (int64_t)start[key] + rank[p];
+    if (rank[p] < 0 || dst >= start[key + 1] || dst >= n) {
+      atomicOr(status, 2);
+      continue;
+    }
+    sorted[dst] = make_int2((int)(p / R), x.y);
   }
 }
 
@@ -561,7 +576,13 @@ inline size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 inline size_t ssm_ws_bytes(int64_t M, int R, int64_t V, int D) {
   (void)D;
   const int64_t n = M * (int64_t)R, K = kRanges * V;
-  return 2 * align256(n * 8) + align256(K * 4) + align256((K + 1) * 4) + align256(n * 4);
+  return 2 * align256(n * 8) + align256(K * 4) + align256((K + 1) * 4) + align256(n * 4) + 256;
+}
+// byte offset of the status word (last 256 B of the workspace): 0 after a clean backward;
+// bit 0 = a sample's catalog row outside [0, V), bit 1 = a scatter slot outside its row's
+// range (stale counters) -- such samples are dropped instead of written out of bounds
+inline size_t ssm_status_offset(int64_t M, int R, int64_t V, int D) {
+  return ssm_ws_bytes(M, R, V, D) - 256;
 }
 
 inline bool fits_buffer(int64_t rows, int64_t ld) { return rows * ld * 4 < 0x7fffffff; }
@@ -572,6 +593,10 @@ extern "C" {
 
 size_t gr_sampled_softmax_workspace_size(int64_t M, int R, int64_t V, int D) {
   return gr::ssm_ws_bytes(M, R, V, D);
+}
+
+size_t gr_sampled_softmax_status_offset(int64_t M, int R, int64_t V, int D) {
+  return gr::ssm_status_offset(M, R, V, D);
 }
 
 int gr_sampled_softmax_fwd(const float* out, int64_t ld_out, const float* pos, int64_t ld_pos,
@@ -655,8 +680,10 @@ int gr_sampled_softmax_bwd(const float* out, int64_t ld_out, const float* pos, i
   const bool lds = K <= gr::kLdsBins;
   const unsigned cgrid = lds ? (unsigned)((n + gr::kCountChunk - 1) / gr::kCountChunk)
                              : (unsigned)std::min<int64_t>((n + 1023) / 1024, 4 * gr::device_cus());
+  int* status = (int*)((char*)workspace + gr::ssm_status_offset(M, R, V, D));
   GR_TIMED("sampled_softmax_csr", st, {
     gr::zero_words_async(cnt, K, st);
+    gr::zero_words_async(status, 1, st);
     if (lds)
       hipLaunchKernelGGL(gr::ssm_count_kernel<true>, dim3(cgrid), dim3(gr::kCountThreads),
                          (size_t)K * 4, st, rec, n, R, M, V, K, cnt, rank);
@@ -664,8 +691,8 @@ int gr_sampled_softmax_bwd(const float* out, int64_t ld_out, const float* pos, i
       hipLaunchKernelGGL(gr::ssm_count_kernel<false>, dim3(cgrid), dim3(gr::kCountThreads), 0, st,
                          rec, n, R, M, V, K, cnt, rank);
     hipLaunchKernelGGL(gr::ssm_scan_kernel, dim3(1), dim3(1024), 0, st, cnt, K, start);
-    hipLaunchKernelGGL(gr::ssm_fill_kernel, dim3(sgrid), dim3(256), 0, st, rec, n, R, M, V, start,
-                       rank, sorted);
+    hipLaunchKernelGGL(gr::ssm_fill_kernel, dim3(sgrid), dim3(256), 0, st, rec, n, R, M, V, K, start,
+                       rank, sorted, status);
   });
   GR_LAUNCH_CHECK("gr_sampled_softmax_bwd (csr)");
   // every token range holds exactly (its tokens) * R samples: at most ceil(M / 8) * R

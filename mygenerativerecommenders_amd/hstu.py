@@ -222,7 +222,7 @@ class HSTUJagged(torch.nn.Module):
                 cache=None, return_cache_states=False, max_len: Optional[int] = None):
         n = invalid_attn_mask.size(1)
         if x.dim() == 3:
-            x = ops.dense_to_jagged(x, x_offsets)  # B*N capacity rows: no host sync
+            x = ops.dense_to_jagged(x, x_offsets, zero_fill=False)  # B*N capacity rows, no sync
         jagged_x, cache_states = self.jagged_forward(
             x, x_offsets, all_timestamps, invalid_attn_mask, delta_x_offsets, cache,
             return_cache_states, max_len=max_len)

@@ -76,12 +76,12 @@ def asynchronous_complete_cumsum(lengths: torch.Tensor) -> torch.Tensor:
 
 class _DenseToJagged(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, dense, offsets, total_rows):
+    def forward(ctx, dense, offsets, total_rows, zero_fill):
         B, N, D = dense.shape
         dense = dense.contiguous()
         out = torch.empty(total_rows, D, dtype=dense.dtype, device=dense.device)
         _lib.call("gr_dense_to_jagged", dense.data_ptr(), offsets.data_ptr(), B, N, D,
-                  total_rows, out.data_ptr(), _stream())
+                  total_rows, int(zero_fill), out.data_ptr(), _stream())
         ctx.save_for_backward(offsets)
         ctx.shape = (B, N, D)
         return out
@@ -94,7 +94,7 @@ class _DenseToJagged(torch.autograd.Function):
         out = torch.empty(B, N, D, dtype=g.dtype, device=g.device)
         _lib.call("gr_jagged_to_padded", g.data_ptr(), offsets.data_ptr(), B, N, D,
                   out.data_ptr(), _stream())
-        return out, None, None
+        return out, None, None, None
 
 
 class _JaggedToPadded(torch.autograd.Function):
@@ -116,23 +116,26 @@ class _JaggedToPadded(torch.autograd.Function):
         B, N, D, rows = ctx.meta
         g = g.contiguous()
         out = torch.empty(rows, D, dtype=g.dtype, device=g.device)
-        _lib.call("gr_dense_to_jagged", g.data_ptr(), offsets.data_ptr(), B, N, D, rows,
+        # rows no padded position reaches (lengths above N, rows past offsets[B]) get 0
+        _lib.call("gr_dense_to_jagged", g.data_ptr(), offsets.data_ptr(), B, N, D, rows, 1,
                   out.data_ptr(), _stream())
         return out, None, None
 
 
 def dense_to_jagged(dense_tensor: torch.Tensor, offsets: torch.Tensor,
-                    total_rows: Optional[int] = None) -> torch.Tensor:
+                    total_rows: Optional[int] = None, zero_fill: bool = True) -> torch.Tensor:
     """(B, N, D) -> (total, D) (utils/ops.py:41-64).  ``total_rows`` defaults to B*N
-    capacity (sync-free; rows past offsets[B] are scratch) — pass the exact total to
-    get an exact-size result."""
+    capacity (sync-free) — pass the exact total to get an exact-size result.  Rows past
+    offsets[B] are zero unless ``zero_fill=False`` (they are then scratch; the encoder
+    uses that for its capacity-sized activations)."""
     _lib.require_gpu(dense_tensor, offsets)
     if dense_tensor.dtype != torch.float32:
         raise TypeError("dense_to_jagged: float32 only")
     B, N, _ = dense_tensor.shape
     if total_rows is None:
         total_rows = B * N
-    return _DenseToJagged.apply(dense_tensor, offsets.to(torch.int64), int(total_rows))
+    return _DenseToJagged.apply(dense_tensor, offsets.to(torch.int64), int(total_rows),
+                                bool(zero_fill))
 
 
 def jagged_to_padded_dense(values: torch.Tensor, offsets: torch.Tensor, max_lengths: int,
@@ -438,7 +441,22 @@ class _SampledSoftmax(torch.autograd.Function):
                   temperature, lse.data_ptr(), g.data_ptr(), d_out.data_ptr(), D,
                   d_pos.data_ptr(), D, d_table.data_ptr(), D, ws.data_ptr(), ws.numel(),
                   _stream())
+        if M * R > 0:  # the backward's status word (device), read by last_sampled_softmax_status
+            off = int(_lib.lib().gr_sampled_softmax_status_offset(M, R, V, D))
+            global _LAST_SSM_STATUS
+            _LAST_SSM_STATUS = ws[off:off + 4]
         return d_out, d_pos, d_table, None, None, None, None
+
+
+_LAST_SSM_STATUS = None
+
+
+def last_sampled_softmax_status() -> int:
+    """Status word of the most recent sampled-softmax backward (host sync): 0 = clean;
+    bit 0 / bit 1 = samples dropped by the counting sort's bound checks."""
+    if _LAST_SSM_STATUS is None:
+        return 0
+    return int(_LAST_SSM_STATUS.view(torch.int32).item())
 
 
 def sampled_softmax_loss(out: torch.Tensor, pos: torch.Tensor, table: torch.Tensor,

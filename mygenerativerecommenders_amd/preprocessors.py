@@ -58,8 +58,10 @@ class _Preproc(torch.autograd.Function):
         g = dy.contiguous()
         dx = torch.empty_like(g) if ctx.needs_input_grad[0] else None
         dpos = None
-        if ctx.needs_input_grad[1]:
-            dpos = torch.zeros(pos_shape, dtype=g.dtype, device=g.device)
+        if ctx.needs_input_grad[1]:  # the kernel writes rows < N; rows >= N get no gradient
+            dpos = torch.empty(pos_shape, dtype=g.dtype, device=g.device)
+            if pos_shape[0] > N:
+                dpos[N:].zero_()
         _lib.call("gr_preproc_bwd", g.data_ptr(), ids.data_ptr(), B, N, D, scale, p, seed,
                   step.data_ptr() if has_step else None,
                   dx.data_ptr() if dx is not None else None,

@@ -99,3 +99,56 @@ def test_complete_cumsum_sizes(B):
     offs = ops.asynchronous_complete_cumsum(lengths.cuda())
     ref = np.concatenate([[0], np.cumsum(lengths.numpy())]).astype(np.int64)
     assert np.array_equal(offs.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("D", [16, 7])
+def test_dense_to_jagged_bounded_by_max_rows(D):
+    """max_rows smaller than offsets[B]: nothing at or past it is written (canary tail),
+    and the rows inside keep their values; with zero_fill the truncated tails and the
+    rows past offsets[B] are zero."""
+    from mygenerativerecommenders_amd import _lib
+    dev = torch.device("cuda")
+    B, N = 5, 12
+    lengths = torch.tensor([12, 3, 15, 0, 9])  # 15 > N: truncated to N on copy
+    offs = torch.cat([torch.zeros(1, dtype=torch.int64), torch.cumsum(lengths, 0)])
+    dense = torch.randn(B, N, D)
+    total = int(offs[-1])
+    dense_d, offs_d = dense.to(dev), offs.to(dev)
+    for max_rows, zero_fill in ((20, 0), (20, 1), (total + 6, 1)):
+        buf = torch.full((total + 10, D), 7.0, device=dev)
+        _lib.call("gr_dense_to_jagged", dense_d.data_ptr(), offs_d.data_ptr(), B, N,
+                  D, max_rows, zero_fill, buf.data_ptr(), _lib.stream_handle())
+        torch.cuda.synchronize()
+        got = buf.cpu()
+        assert torch.all(got[max_rows:] == 7.0), "wrote at or past max_rows"
+        for b in range(B):
+            s0, s1 = int(offs[b]), int(offs[b + 1])
+            L = min(s1 - s0, N)
+            for r in range(s0, min(s1, max_rows)):
+                if r - s0 < L:
+                    assert torch.equal(got[r], dense[b, r - s0])
+                elif zero_fill:
+                    assert torch.all(got[r] == 0)
+        if zero_fill and max_rows > total:
+            assert torch.all(got[total:max_rows] == 0)
+
+
+def test_jagged_to_padded_grad_truncated_rows_are_zero():
+    """Autograd through jagged_to_padded_dense with a length above N: the gradient of
+    the rows no padded position reads is 0 (fbgemm semantics), not uninitialised."""
+    from mygenerativerecommenders_amd import ops
+    dev = torch.device("cuda")
+    lengths = torch.tensor([4, 9, 2], device=dev)
+    offs = ops.asynchronous_complete_cumsum(lengths)
+    N, D = 6, 8
+    values = torch.randn(15 + 3, D, device=dev, requires_grad=True)  # 3 rows past offsets[B]
+    out = ops.jagged_to_padded_dense(values, offs, N)
+    g = torch.randn_like(out)
+    out.backward(g)
+    grad = values.grad.cpu()
+    ref = torch.zeros(18, D)
+    o = offs.cpu()
+    for b in range(3):
+        s0, L = int(o[b]), min(int(lengths[b]), N)
+        ref[s0:s0 + L] = g[b, :L].cpu()
+    assert torch.equal(grad, ref)

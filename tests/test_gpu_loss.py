@@ -258,3 +258,6 @@ def test_loss_graph_replays_match_eager():
         assert abs(loss_static.item() - ref[0]) <= 1e-5 * max(1.0, abs(ref[0]))
         _close(o.grad.cpu().double().numpy(), ref[1], 1e-5, "d_out")
         _close(emb.weight.grad.cpu().double().numpy(), ref[3], 1e-5, "d_weight")
+        # the counting sort's bound checks dropped nothing
+        from mygenerativerecommenders_amd.ops import last_sampled_softmax_status
+        assert last_sampled_softmax_status() == 0

@@ -39,8 +39,9 @@ def test_preproc_matches_reference_golden():
     assert np.allclose(m._pos_emb.weight.grad.cpu().numpy(), z["dpos"], rtol=1e-5, atol=1e-5)
 
 
-def test_preproc_c2_shape_vs_oracle():
-    B, N, D = 128, 211, 50
+@pytest.mark.parametrize("B", [1, 17, 128, 150, 300])  # 16-group dpos: unrolled + tail loops
+def test_preproc_c2_shape_vs_oracle(B):
+    N, D = 211, 50
     g = torch.Generator().manual_seed(3)
     x = torch.randn(B, N, D, generator=g)
     lengths = torch.randint(20, 201, (B,), generator=g)
@@ -79,8 +80,10 @@ def test_preproc_dropout_statistics_and_mask_agreement():
     assert abs(rate - (1 - p)) < 0.01, rate
     assert np.allclose(yv[kept], base[kept] / (1 - p), rtol=1e-5, atol=1e-5)
     mask = np.where(kept, 1 / (1 - p), 0.0)
-    dxr, _ = preproc_oracle.preprocess_bwd(dy.numpy(), ids.numpy(), D ** 0.5, N, mask=mask)
+    dxr, dposr = preproc_oracle.preprocess_bwd(dy.numpy(), ids.numpy(), D ** 0.5, N, mask=mask)
     assert np.allclose(xg.grad.cpu().numpy()[live], dxr[live], rtol=1e-5, atol=1e-5)
+    # the positional gradient sums the same regenerated mask over the batch
+    assert np.allclose(m._pos_emb.weight.grad.cpu().numpy(), dposr, rtol=1e-5, atol=1e-4)
     # a second forward draws a different mask
     _, y2, _, _ = m(None, ids.cuda(), xg, {})
     assert not torch.equal(y2, y)

@@ -100,3 +100,24 @@ def test_muon_matches_reference_golden():
             err = np.abs(p.detach().numpy() - ref).max()
             assert err <= 2e-3 * delta + 1e-7, (step, i, err, delta)
     assert all("momentum_buffer" in opt.state[p] for p in params)
+
+
+def test_retrieval_metrics_reference_known_answers():
+    """Known answers of the reference's own tests/test_metrics.py:36-47 (inputs and
+    expected values as data): targets at rank 2, 3 and absent (rank k + 1)."""
+    from mygenerativerecommenders_amd.metrics import RetrievalMetrics
+    top_k_ids = torch.tensor([[1, 2, 3], [4, 5, 6], [7, 8, 9]])
+    target_ids = torch.tensor([[2], [6], [3]])
+    m = RetrievalMetrics(k=3, at_k_list=[1, 2, 3])
+    assert m.k == 3 and m.at_k_list == [1, 2, 3]
+    m.update(top_k_ids, target_ids)
+    m.update(top_k_ids, target_ids)
+    assert len(m.top_k_ids) == 2 and len(m.target_ids) == 2
+    m.reset()
+    assert m.top_k_ids == [] and m.target_ids == []
+    m.update(top_k_ids, target_ids)
+    out = m.compute()
+    expect = {"ndcg@1": 0.0, "ndcg@2": 0.2103, "ndcg@3": 0.3770, "hr@1": 0.0,
+              "hr@2": 0.3333, "hr@3": 0.6667, "mrr": 0.3611}
+    for key, val in expect.items():
+        assert abs(float(out[key]) - val) <= 5e-5, (key, float(out[key]), val)
