@@ -298,14 +298,18 @@ def hstu_step_flops(L, D, H, dqk, dv, blocks):
 
 
 def encoder_leg(B, N0, out_len, D, blocks, H, steps, warmup, device, world, seed,
-                eager=False, instrument=False):
+                eager=False, instrument=False, muon=False):
     """Times the encoder training step alone at one shape: HSTU fwd + bwd (input and
     parameter grads) -> gradient all-reduce -> fused AdamW, fixed-length rows, train
     mode, captured as two HIP graphs around the all-reduce.  Used for the C2 batch
     sweep and the C3 (ml-20m width) leg.  ``instrument``: per-kernel device times from
-    an eager re-run with the library's event pairs."""
+    an eager re-run with the library's event pairs.  ``muon``: the C5 recipe -- the
+    reference's Muon (encoder matrices) + AdamW (the rest) split and the bucketed
+    reducer whose all-reduces overlap the backward (eager when world > 1: the
+    collectives are issued from the backward's gradient hooks)."""
     from mygenerativerecommenders_amd import _lib
-    from mygenerativerecommenders_amd.distributed import FlatGradAllReducer
+    from mygenerativerecommenders_amd.distributed import (BucketedGradReducer, FlatGradAllReducer,
+                                                          muon_adamw_split)
     from mygenerativerecommenders_amd.hstu import HSTU
     N = N0 + out_len
     torch.manual_seed(0)
@@ -315,9 +319,21 @@ def encoder_leg(B, N0, out_len, D, blocks, H, steps, warmup, device, world, seed
                attention_dim=dh, normalization="rel_bias", linear_config="uvqk",
                linear_activation="silu", linear_dropout_rate=0.2,
                attn_dropout_rate=0.0).to(device).train()
-    reducer = FlatGradAllReducer(list(enc.parameters()))
-    opt = torch.optim.AdamW(enc.parameters(), lr=1e-3, betas=(0.9, 0.98), weight_decay=1e-3,
-                            fused=True, capturable=True)
+    if muon:
+        reducer = BucketedGradReducer(list(enc.parameters()), overlap=world > 1)
+        eager = eager or world > 1
+        opts = muon_adamw_split(enc.named_parameters(),
+                                **({} if eager else {"fused": True, "capturable": True}))
+    else:
+        reducer = FlatGradAllReducer(list(enc.parameters()))
+        opts = [torch.optim.AdamW(enc.parameters(), lr=1e-3, betas=(0.9, 0.98), weight_decay=1e-3,
+                                  fused=True, capturable=True)]
+
+    class _Opt:
+        def step(self):
+            for o in opts:
+                o.step()
+    opt = _Opt()
     lengths, x, ts, _, dy = make_batch(B, N0, out_len, D, seed, device)
     x.requires_grad_(True)
 
@@ -326,11 +342,17 @@ def encoder_leg(B, N0, out_len, D, blocks, H, steps, warmup, device, world, seed
                    past_payloads={"timestamps": ts}, max_len=N0)
         y.backward(dy)
 
+    def exchange(inplace=False):
+        if muon:
+            reducer.finish()
+        else:
+            reducer.allreduce(world, inplace=inplace)
+
     def eager_step():
         reducer.zero_grad()
         x.grad = None
         fwd_bwd()
-        reducer.allreduce(world)
+        exchange()
         opt.step()
 
     side = torch.cuda.Stream()
@@ -352,7 +374,7 @@ def encoder_leg(B, N0, out_len, D, blocks, H, steps, warmup, device, world, seed
 
         def step():
             g_fb.replay()
-            reducer.allreduce(world, inplace=True)
+            exchange(inplace=True)
             g_opt.replay()
     for _ in range(warmup):
         step()
@@ -363,7 +385,8 @@ def encoder_leg(B, N0, out_len, D, blocks, H, steps, warmup, device, world, seed
     _sync_barrier(world)
     dt = _max_over_ranks(time.perf_counter() - t0, world)
     out = {"value": round(B * world * steps / dt, 2), "unit": "seq/s",
-           "ms_per_step": round(dt / steps * 1e3, 4), "steps": steps, "global_batch": B * world}
+           "ms_per_step": round(dt / steps * 1e3, 4), "steps": steps, "global_batch": B * world,
+           "execution": "eager" if eager else "hip-graph replay"}
     if instrument:
         hold = _gpu_hold_fn()
         _lib.timing_enable(True)
@@ -698,7 +721,7 @@ def main():
     if args.c3_steps > 0:
         B3, N3, D3, L3 = 32, 2048, 256, 8
         r = encoder_leg(B3, N3, out_len, D3, L3, 1, args.c3_steps, 2, device, world,
-                        3000 + rank, instrument=True)
+                        3000 + rank, instrument=True, muon=True)
         step_flops = B3 * hstu_step_flops(N3, D3, 1, D3, D3, L3)
         ach3 = step_flops / (r["ms_per_step"] * 1e-3) / 1e12
         f3, dkv3, dq3 = attn_flops(r["lengths"], 1, D3, D3, L3)
@@ -712,7 +735,11 @@ def main():
         ach_k = fpl3.get(dom3, 0.0) / (r["kernel_avg_ms"][dom3] * 1e-3) / 1e12
         c3 = {"metric": "HSTU seq/s (fwd+bwd)", "value": r["value"], "unit": "seq/s",
               "ms_per_step": r["ms_per_step"], "steps": args.c3_steps, "dtype": "fp32",
-              "config": {"workload": "C3: ml-20m width HSTU train step (fwd+bwd+AdamW)",
+              "config": {"workload": ("C3: ml-20m width HSTU train step (fwd+bwd, Muon + AdamW)"
+                                      if world == 1 else
+                                      "C5: ml-20m width HSTU DDP train step (fwd+bwd, bucketed "
+                                      "all-reduce overlapped with the backward, Muon + AdamW)"),
+                         "execution": r["execution"],
                          "global_batch": B3 * world, "seq_len": N3, "padded_len": N3 + out_len,
                          "dim": D3, "blocks": L3, "heads": 1},
               "algorithmic_tflop_per_step": round(step_flops / 1e12, 4),

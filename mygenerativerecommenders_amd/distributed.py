@@ -82,6 +82,129 @@ class FlatGradAllReducer:
             off += k
 
 
+class BucketedGradReducer:
+    """Data-parallel gradient averaging overlapped with the backward (the MI355X shape
+    of Lightning DDP's bucketed all-reduce, configs/trainer/ddp.yaml; SURVEY.md §8e:
+    ~147 MB of gradients at C5 must overlap the backward).
+
+    * Parameters are packed into buckets of ``bucket_bytes`` in REVERSE registration
+      order -- the order the layer-by-layer backward produces their gradients (last
+      block first), so the first bucket completes while earlier blocks still run.
+    * Each bucket is one persistent fp32 buffer.  A post-accumulate-grad hook scales the
+      fresh gradient by 1/world straight into the parameter's slice of its bucket (one
+      kernel, no torch.cat, no copy back) and re-points ``p.grad`` at that slice.
+    * ``overlap=True``: the hook that completes a bucket launches its all-reduce
+      (async; RCCL runs it on its own stream while the backward continues).
+      ``overlap=False``: hooks only pack (e.g. inside a captured HIP graph) and
+      ``finish()`` launches the buckets.
+    * ``finish()`` launches what is left, waits, and zero-fills the slices of
+      parameters that got no gradient this step (so every rank reduces the same bytes).
+    ``zero_grad()`` must run before each backward (set_to_none, so the backward's
+    output is stolen, not accumulated into the bucket view)."""
+
+    def __init__(self, params: List[torch.nn.Parameter], group=None,
+                 bucket_bytes: int = 25 << 20, overlap: bool = True):
+        self.params = [p for p in params if p.requires_grad]
+        self.group = group
+        self.overlap = overlap
+        dist_on = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(group) if dist_on else 1
+        self.scale = 1.0 / self.world
+        self.buckets: List[List[torch.nn.Parameter]] = []
+        cur, size = [], 0
+        for p in reversed(self.params):
+            nb = p.numel() * 4
+            if cur and size + nb > bucket_bytes:
+                self.buckets.append(cur)
+                cur, size = [], 0
+            cur.append(p)
+            size += nb
+        if cur:
+            self.buckets.append(cur)
+        self.buffers: List[torch.Tensor] = []
+        self.slot = {}
+        for bi, bucket in enumerate(self.buckets):
+            buf = torch.zeros(sum(p.numel() for p in bucket), dtype=torch.float32,
+                              device=bucket[0].device)
+            off = 0
+            for p in bucket:
+                self.slot[p] = (bi, buf[off:off + p.numel()].view_as(p))
+                off += p.numel()
+            self.buffers.append(buf)
+        self._ready = [0] * len(self.buckets)
+        self._handles: List[Optional[object]] = [None] * len(self.buckets)
+        self._seen = set()
+        self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
+
+    def zero_grad(self):
+        for p in self.params:
+            p.grad = None
+
+    def _launch(self, bi: int):
+        if self.world > 1 and self._handles[bi] is None:
+            self._handles[bi] = dist.all_reduce(self.buffers[bi], op=dist.ReduceOp.SUM,
+                                                group=self.group, async_op=True)
+
+    def _on_grad(self, p: torch.nn.Parameter):
+        bi, view = self.slot[p]
+        g = p.grad
+        if g is not view:
+            if self.scale != 1.0:
+                torch.mul(g, self.scale, out=view)
+            else:
+                view.copy_(g)
+            p.grad = view
+        if p not in self._seen:
+            self._seen.add(p)
+            self._ready[bi] += 1
+            if self.overlap and self._ready[bi] == len(self.buckets[bi]):
+                self._launch(bi)
+
+    def finish(self):
+        """Completes the step's exchange: after it every .grad is the group average."""
+        for bi, bucket in enumerate(self.buckets):
+            if self._ready[bi] < len(bucket):
+                for p in bucket:
+                    if p not in self._seen:
+                        view = self.slot[p][1]
+                        view.zero_()
+                        p.grad = view
+            self._launch(bi)
+        for h in self._handles:
+            if h is not None:
+                h.wait()
+        self._ready = [0] * len(self.buckets)
+        self._handles = [None] * len(self.buckets)
+        self._seen = set()
+
+    def remove_hooks(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+
+
+def muon_adamw_split(named_params, muon_lr=5e-3, muon_momentum=0.95, muon_wd=5e-3,
+                     adam_lr=5e-4, adam_betas=(0.8, 0.95), adam_eps=1e-10, adam_wd=5e-3,
+                     **adam_kwargs):
+    """The reference's two-optimizer split (generative_recommenders.py:297-310,
+    configs/experiment/ml-1m-hstu-muon.yaml:23-36): parameters whose name contains
+    "emb" and every parameter with ndim < 2 -> AdamW; the remaining matrices -> Muon.
+    ``named_params``: iterable of (name, parameter).  Returns [AdamW, Muon] (the
+    reference's optimizer1, optimizer2), skipping an empty group."""
+    from .muon import Muon
+    named = [(n, p) for n, p in named_params if p.requires_grad]
+    adam = [p for n, p in named if "emb" in n or p.ndim < 2]
+    ids = {id(p) for p in adam}
+    mats = [p for n, p in named if id(p) not in ids]
+    opts = []
+    if adam:
+        opts.append(torch.optim.AdamW(adam, lr=adam_lr, betas=adam_betas, eps=adam_eps,
+                                      weight_decay=adam_wd, **adam_kwargs))
+    if mats:
+        opts.append(Muon(mats, lr=muon_lr, momentum=muon_momentum, weight_decay=muon_wd))
+    return opts
+
+
 class ShardedCandidateIndex:
     """Row-sharded brute-force retrieval.  Each rank owns a contiguous
     slice of the catalog; results are identical to a single-GPU CandidateIndex over

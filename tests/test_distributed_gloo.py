@@ -97,3 +97,138 @@ def test_dp_allreduce_and_sharded_merge_world2():
         p.join(timeout=60)
     for rank, msg in results:
         assert msg == "ok", f"rank {rank}: {msg}"
+
+
+# ---------------------------------------------------------------- C5: DP HSTU training
+# The HSTU module's own parameters (same names and shapes as the drop-in), run forward on
+# the CPU through the oracle's functional restatement; the bucketed, backward-overlapped
+# reducer averages them over 2 gloo ranks each holding half the batch, Muon + AdamW
+# step (the reference's two-optimizer split).  Must equal one process on the whole batch.
+
+def _hstu_case():
+    from mygenerativerecommenders_amd.hstu import HSTU
+    torch.manual_seed(0)
+    N0, out_len, D, blocks = 16, 3, 16, 2
+    enc = HSTU(max_sequence_len=N0, max_output_len=out_len, embedding_dim=D,
+               item_embedding_dim=D, num_blocks=blocks, num_heads=1, linear_dim=D,
+               attention_dim=D, normalization="rel_bias", linear_config="uvqk",
+               linear_activation="silu", linear_dropout_rate=0.0, attn_dropout_rate=0.0)
+    with torch.no_grad():
+        for layer in enc._hstu._attention_layers:
+            layer._rel_attn_bias._ts_w.normal_(0, 0.3)
+            layer._rel_attn_bias._pos_w.normal_(0, 0.3)
+    g = torch.Generator().manual_seed(1)
+    B, N = 4, N0 + out_len
+    lengths = torch.tensor([16, 5, 11, 9])
+    x = torch.randn(2, B, N, D, generator=g)  # two steps
+    ts = torch.zeros(B, N, dtype=torch.int64)
+    for b in range(B):
+        L = int(lengths[b])
+        ts[b, :L + 1] = 1_000_000_000 + torch.cumsum((torch.rand(L + 1, generator=g) * 2e5).long(), 0)
+    dy = torch.randn(2, B, N, D, generator=g)
+    return enc, lengths, x, ts, dy, blocks
+
+
+def _hstu_loss(enc, blocks, lengths, x, ts, dy):
+    import numpy as np
+    from mygenerativerecommenders_amd.bucket_table import BUCKET_THRESHOLDS
+    from oracle import hstu_oracle as O
+    st = dict(enc.named_parameters())
+    layers = [O.layer_params_from_state(st, i) for i in range(blocks)]
+    N, D = x.shape[1], x.shape[2]
+    cfg = O.HSTUConfig(N=N, D=D, H=1, dqk=D, dv=D)
+    y = O.hstu_forward(lengths, x, ts, cfg, layers, np.asarray(BUCKET_THRESHOLDS))
+    return (y * dy).sum() / x.shape[0]  # mean over this rank's sequences
+
+
+def _hstu_train(enc, blocks, lengths, x, ts, dy, rows, reducer=None, halves=None):
+    """Two optimizer steps.  ``halves``: single-process reference that averages the two
+    half-batch gradients as 0.5 g0 + 0.5 g1 -- the same arithmetic as the reducer's
+    scaled copy + 2-rank sum, so the whole run (Muon's bf16 Newton-Schulz included,
+    which amplifies last-bit differences) must match bit for bit."""
+    from mygenerativerecommenders_amd.distributed import muon_adamw_split
+    opts = muon_adamw_split(enc.named_parameters())
+    grads = []
+    for step in range(2):
+        if reducer is not None:
+            reducer.zero_grad()
+        else:
+            for p in enc.parameters():
+                p.grad = None
+        if halves is None:
+            loss = _hstu_loss(enc, blocks, lengths[rows], x[step][rows], ts[rows], dy[step][rows])
+            loss.backward()
+        else:
+            parts = []
+            for h in halves:
+                for p in enc.parameters():
+                    p.grad = None
+                _hstu_loss(enc, blocks, lengths[h], x[step][h], ts[h], dy[step][h]).backward()
+                parts.append([p.grad.clone() for p in enc.parameters()])
+            for p, g0, g1 in zip(enc.parameters(), *parts):
+                p.grad = torch.mul(g0, 0.5) + torch.mul(g1, 0.5)
+        if reducer is not None:
+            reducer.finish()
+        grads.append([p.grad.clone() for p in enc.parameters()])
+        for o in opts:
+            o.step()
+    return grads, [p.detach().clone() for p in enc.parameters()]
+
+
+def _dp_hstu_worker(rank, world, port, q, overlap):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    try:
+        from mygenerativerecommenders_amd.distributed import BucketedGradReducer, init_from_env
+        init_from_env("gloo")
+        enc, lengths, x, ts, dy, blocks = _hstu_case()
+        B = lengths.numel()
+        copy = __import__("copy")
+        half = B // world
+        halves = [slice(r * half, (r + 1) * half) for r in range(world)]
+        full_grads, _ = _hstu_train(copy.deepcopy(enc), blocks, lengths, x, ts, dy, slice(0, B))
+        ref_grads, ref_params = _hstu_train(copy.deepcopy(enc), blocks, lengths, x, ts, dy, None,
+                                            halves=halves)
+        red = BucketedGradReducer(list(enc.parameters()), bucket_bytes=4096, overlap=overlap)
+        assert len(red.buckets) > 2  # several buckets, last block's parameters first
+        assert red.buckets[0][0] is list(enc.parameters())[-1]
+        grads, params = _hstu_train(enc, blocks, lengths, x, ts, dy, halves[rank], red)
+        # 2 ranks x B/2 == 1 process x B (first step, fp32 summation-order tolerance)
+        for g, r in zip(grads[0], full_grads[0]):
+            assert torch.allclose(g, r, rtol=1e-5, atol=1e-6), (g - r).abs().max()
+        # ... and bit-identical to the same averaging done in one process, through two
+        # Muon + AdamW steps
+        for step in range(2):
+            for g, r in zip(grads[step], ref_grads[step]):
+                assert torch.equal(g, r), (step, (g - r).abs().max())
+        for p, r in zip(params, ref_params):
+            assert torch.equal(p, r), (p - r).abs().max()
+        # .grad are views into the reducer's buckets (no copy back)
+        bufs = [(b.data_ptr(), b.data_ptr() + 4 * b.numel()) for b in red.buffers]
+        for p in enc.parameters():
+            assert any(lo <= p.grad.data_ptr() < hi for lo, hi in bufs)
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, "ok"))
+    except Exception:
+        import traceback
+        q.put((rank, traceback.format_exc()))
+        raise
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("overlap", [True, False])
+def test_dp_hstu_bucketed_overlap_world2_equals_full_batch(overlap):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dp_hstu_worker, args=(r, 2, port, q, overlap)) for r in range(2)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, msg in results:
+        assert msg == "ok", f"rank {rank}: {msg}"
