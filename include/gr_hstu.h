@@ -262,6 +262,18 @@ GR_API int gr_wgrad(const float* a, int64_t lda, const float* a_stats, const flo
              int64_t ldb, const int64_t* offsets, int B, int64_t max_rows, int Ka, int Nb,
              float* c, float* a_colsum, void* workspace, size_t ws_bytes, void* stream);
 
+/* gr_wgrad2: the two weight gradients of one STU layer in ONE launch (two independent
+ * gr_wgrad problems over the same jagged rows: problem 0 = LN(x)^T dh -> d_uvqk,
+ * problem 1 = dy^T o_in -> d_o.weight with colsum d_o.bias) and one slab reduce.
+ * Each problem as gr_wgrad; workspace: gr_wgrad2_workspace_size bytes. */
+GR_API size_t gr_wgrad2_workspace_size(int64_t max_rows, int Ka0, int Nb0, int Ka1, int Nb1);
+GR_API int gr_wgrad2(const float* a0, int64_t lda0, const float* a_stats0, const float* b0,
+                     int64_t ldb0, int Ka0, int Nb0, float* c0, float* colsum0,
+                     const float* a1, int64_t lda1, const float* a_stats1, const float* b1,
+                     int64_t ldb1, int Ka1, int Nb1, float* c1, float* colsum1,
+                     const int64_t* offsets, int B, int64_t max_rows, void* workspace,
+                     size_t ws_bytes, void* stream);
+
 /* ---------------------------------------------------------------- MIPS retrieval
  * Replaces indexing/top_k.py:44-70 (MIPSBruteForceTopK: mm + torch.topk) and
  * indexing/candidate_index.py:107-164 (get_top_k_outputs: top-(k+N0), drop the row's

@@ -5,13 +5,16 @@
 // Replaces the mm-backward weight terms of reference hstu.py:303 (_uvqk) and
 // hstu.py:404-413 (_o.weight, _o.bias).
 //
-// Split-K over rows: grid = (row splits) x (output panels of 64 ka x NT*16 nb).  A
-// workgroup streams its rows through LDS in chunks of 32 (double-buffered; the next
-// chunk is loaded into registers through buffer descriptors while the current one runs)
-// and wave w accumulates ka-tile w of the panel against all NT nb-tiles.  The column sum
-// comes for free from a ones-column appended to Bm (padding column Nb).  Each split
-// writes its panel to a workspace slab; wgrad_reduce sums the slabs in a fixed order
-// (deterministic, no atomics) with 16 slab groups per output in parallel.
+// One launch computes BOTH weight gradients of a layer (the _uvqk and _o GEMMs are
+// independent problems over the same jagged rows): grid = (row splits) x (output panels
+// of problem 0, then of problem 1), and one reduce launch sums both problems' slabs.
+// Split-K over rows: a workgroup streams its rows through LDS in chunks of 32 with the
+// loads of WG_SUPER chunks in flight together (one HBM round trip per 4 chunks instead of
+// one per chunk), and wave w accumulates ka-tile w & 3 of the panel against all NT
+// nb-tiles over the k-steps of half w >> 2.  The column sum comes for free from a
+// ones-column appended to Bm (padding column Nb).  Each split writes its panel to a
+// workspace slab; wgrad_reduce sums the slabs in a fixed order (deterministic, no
+// atomics) with 16 slab groups per output in parallel.
 #include "attn_common.h"
 
 #include "../../include/gr_hstu.h"
@@ -20,20 +23,29 @@ namespace gr {
 
 constexpr int WG_KA = 64;   // ka rows per panel (4 waves x 16)
 constexpr int WG_CH = 32;   // rows per chunk (8 MFMA k-steps)
+constexpr int WG_SUPER = 4; // chunks whose loads are issued together
 constexpr int WG_LDA = WG_KA + 16;  // == 16 mod 32: lane groups (4 rows apart) hit disjoint banks
 constexpr int WG_THREADS = 512;     // 8 waves: wave w owns ka-tile w & 3, k-steps of half w >> 2
 
-struct WgradArgs {
+struct WgradProb {
   const float* a;
   int64_t lda;
   const float2* a_stats;
   const float* bm;
   int64_t ldb;
+  int Ka, Nb, NC;     // NC = Nb (+1 with the ones column)
+  int panels, panels_nb;
+  float* slabs;       // [split][Ka][NC]
+  float* c;           // reduce outputs
+  float* colsum;
+};
+
+struct WgradArgs {
+  WgradProb p[2];
   const int64_t* offsets;
-  int B, Ka, Nb, NC;  // NC = Nb (+1 with the ones column)
+  int B;
   int64_t rows_per_split;
-  int n_splits, panels_nb;
-  float* slabs;  // [split][Ka][NC]
+  int n_splits;
 };
 
 template <int NT>
@@ -44,26 +56,33 @@ struct WgCfg {
   static constexpr int BRPP = WG_THREADS / NP2;                   // B rows per pass
   static constexpr int BPER = WG_CH / BRPP;                       // B loads per thread
   static constexpr int APER = WG_CH * WG_KA / WG_THREADS;         // A loads per thread
-  static constexpr size_t LDS = sizeof(float) * 2 * WG_CH * (WG_LDA + LDB);
+  static constexpr int SUPER = NT <= 8 ? WG_SUPER : 2;             // register budget at NT 13/16
+  static constexpr size_t LDS = sizeof(float) * 2 * WG_CH * (WG_LDA + LDB + 2);
 };
 
 template <int NT>
-__global__ __launch_bounds__(WG_THREADS) void wgrad_partial_kernel(WgradArgs g) {
+__device__ __forceinline__ void wgrad_panel(const WgradProb& g, const int64_t* offsets, int B,
+                                            int64_t rows_per_split, int split, int panel,
+                                            char* smem) {
   using C = WgCfg<NT>;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
   float (*As)[WG_CH * WG_LDA] = reinterpret_cast<float (*)[WG_CH * WG_LDA]>(smem);
   float (*Bs)[WG_CH * C::LDB] =
       reinterpret_cast<float (*)[WG_CH * C::LDB]>(smem + sizeof(float) * 2 * WG_CH * WG_LDA);
-  const int split = blockIdx.x;
-  const int pa = blockIdx.y / g.panels_nb, pb = blockIdx.y % g.panels_nb;
+  // per-row LayerNorm (mean, rstd) of the chunk, applied as A is read (rows past the
+  // split: (0, 0), so their zero A stays zero)
+  float2 (*Ss)[WG_CH] = reinterpret_cast<float2 (*)[WG_CH]>(
+      smem + sizeof(float) * 2 * WG_CH * (WG_LDA + C::LDB));
+  const int pa = panel / g.panels_nb, pb = panel % g.panels_nb;
   const int ka0 = pa * WG_KA, nb0 = pb * C::NP;
-  const int64_t total = g.offsets[g.B];
-  const int64_t r0 = (int64_t)split * g.rows_per_split;
-  const int64_t r1 = min(total, r0 + g.rows_per_split);
+  const int64_t total = offsets[B];
+  const int64_t r0 = (int64_t)split * rows_per_split;
+  const int64_t r1 = min(total, r0 + rows_per_split);
   const int tid = threadIdx.x, wv = wave_id(), lane = tid & 63;
   const int w = wv & 3, half = wv >> 2;
   const int lr = lane & 15, lg = lane >> 4;
-  const int n_ch = r1 > r0 ? (int)((r1 - r0 + WG_CH - 1) / WG_CH) : 0;
+  // wave-uniform (offsets[B] is loaded per lane; readfirstlane keeps the chunk loop and
+  // its guards scalar instead of exec-mask branches around every load)
+  const int n_ch = __builtin_amdgcn_readfirstlane(r1 > r0 ? (int)((r1 - r0 + WG_CH - 1) / WG_CH) : 0);
 
   // descriptors over this split's rows: rows past r1 load as 0
   const int64_t nrows = r1 > r0 ? r1 - r0 : 0;
@@ -78,37 +97,37 @@ __global__ __launch_bounds__(WG_THREADS) void wgrad_partial_kernel(WgradArgs g) 
   const int aka = ka0 + ac, bnb = nb0 + bc;
   const bool a_ok = aka < g.Ka;
   const bool b_in = bnb < g.Nb, b_one = bnb == g.Nb && g.NC > g.Nb;
-  float ra_v[C::APER], rb_v[C::BPER];
-  float2 st_v[C::APER];
-  auto load = [&](int ch) {
+  float ra_v[C::SUPER][C::APER], rb_v[C::SUPER][C::BPER];
+  float2 st_v[C::SUPER];
+  auto load = [&](int u, int ch) {
     const int rr0 = ch * WG_CH;
 #pragma unroll
     for (int i = 0; i < C::APER; ++i) {
       const int rr = rr0 + ar + (WG_THREADS / 64) * i;
-      ra_v[i] = buf_ld(ra, a_ok ? (int)((rr * g.lda + aka) * 4) : 0x40000000, 0);
-      if (g.a_stats) st_v[i] = ld_f2(g.a_stats, min(r0 + rr, total - 1));
+      ra_v[u][i] = buf_ld(ra, a_ok ? (int)((rr * g.lda + aka) * 4) : 0x40000000, 0);
     }
+    if (g.a_stats && tid < WG_CH) st_v[u] = ld_f2(g.a_stats, min(r0 + rr0 + tid, total - 1));
 #pragma unroll
     for (int i = 0; i < C::BPER; ++i) {
       const int rr = rr0 + br + C::BRPP * i;
-      rb_v[i] = buf_ld(rb, b_in ? (int)((rr * g.ldb + bnb) * 4) : 0x40000000, 0);
+      rb_v[u][i] = buf_ld(rb, b_in ? (int)((rr * g.ldb + bnb) * 4) : 0x40000000, 0);
     }
   };
-  auto store = [&](int buf, int ch) {
+  auto store = [&](int u, int buf, int ch) {
     const int rr0 = ch * WG_CH;
 #pragma unroll
     for (int i = 0; i < C::APER; ++i) {
       const int rr = ar + (WG_THREADS / 64) * i;
-      float v = ra_v[i];
-      if (g.a_stats) v = (v - st_v[i].x) * st_v[i].y;
-      As[buf][rr * WG_LDA + ac] = (a_ok && r0 + rr0 + rr < r1) ? v : 0.f;
+      As[buf][rr * WG_LDA + ac] = (a_ok && r0 + rr0 + rr < r1) ? ra_v[u][i] : 0.f;
     }
+    if (tid < WG_CH)
+      Ss[buf][tid] = g.a_stats && r0 + rr0 + tid < r1 ? st_v[u] : make_float2(0.f, 1.f);
     if (bc < C::NP) {
 #pragma unroll
       for (int i = 0; i < C::BPER; ++i) {
         const int rr = br + C::BRPP * i;
         const bool row_ok = r0 + rr0 + rr < r1;
-        Bs[buf][rr * C::LDB + bc] = b_one ? (row_ok ? 1.f : 0.f) : rb_v[i];
+        Bs[buf][rr * C::LDB + bc] = b_one ? (row_ok ? 1.f : 0.f) : rb_v[u][i];
       }
     }
   };
@@ -116,28 +135,49 @@ __global__ __launch_bounds__(WG_THREADS) void wgrad_partial_kernel(WgradArgs g) 
   f4 acc[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = f4_zero();
-  if (n_ch > 0) {
-    load(0);
-    store(0, 0);
-  }
-  __syncthreads();
-  for (int ch = 0; ch < n_ch; ++ch) {
-    const int buf = ch & 1;
-    if (ch + 1 < n_ch) load(ch + 1);
-    const float* Ab = As[buf];
-    const float* Bb = Bs[buf];
+  // Per super-chunk: the loads of all its chunks are issued first; chunk c is then
+  // stored to LDS buffer c & 1 and computed.  One barrier per chunk: the store into a
+  // buffer follows the barrier after the previous chunk's store, which every wave
+  // reaches only after computing on that buffer two chunks ago.
+  for (int sc = 0; sc < n_ch; sc += C::SUPER) {
 #pragma unroll
-    for (int ks = half * (WG_CH / 8); ks < (half + 1) * (WG_CH / 8); ++ks) {
-      const float av = Ab[(4 * ks + lg) * WG_LDA + 16 * w + lr];
-      float bv[NT];
+    for (int u = 0; u < C::SUPER; ++u)
+      if (sc + u < n_ch) load(u, sc + u);
 #pragma unroll
-      for (int t = 0; t < NT; ++t) bv[t] = Bb[(4 * ks + lg) * C::LDB + 16 * t + lr];
+    for (int u = 0; u < C::SUPER; ++u) {
+      if (sc + u < n_ch) {
+        const int ch = sc + u, buf = ch & 1;
+        store(u, buf, ch);
+        __syncthreads();
+        const float* Ab = As[buf];
+        const float* Bb = Bs[buf];
+        const float2* Sb = Ss[buf];
+        // operands of k-step ks + 1 are read from LDS while the MFMAs of ks run (one
+        // read -> wait -> MFMA round trip per operand otherwise)
+        constexpr int KS = WG_CH / 8;
+        const int ks0 = half * KS;
+        float av[2], bv[2][NT];
+        float2 sv[2];
+        auto rd = [&](int slot, int ks) {
+          sv[slot] = Sb[4 * ks + lg];
+          av[slot] = Ab[(4 * ks + lg) * WG_LDA + 16 * w + lr];
 #pragma unroll
-      for (int t = 0; t < NT; ++t) acc[t] = mfma16x16x4(av, bv[t], acc[t]);
+          for (int t = 0; t < NT; ++t) bv[slot][t] = Bb[(4 * ks + lg) * C::LDB + 16 * t + lr];
+        };
+        rd(0, ks0);
+#pragma unroll
+        for (int j = 0; j < KS; ++j) {
+          if (j + 1 < KS) rd((j + 1) & 1, ks0 + j + 1);
+          __builtin_amdgcn_sched_barrier(0);
+          const float a = (av[j & 1] - sv[j & 1].x) * sv[j & 1].y;
+#pragma unroll
+          for (int t = 0; t < NT; ++t) acc[t] = mfma16x16x4(a, bv[j & 1][t], acc[t]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
     }
-    if (ch + 1 < n_ch) store(buf ^ 1, ch + 1);
-    lds_barrier();
   }
+  __syncthreads();  // LDS is reused for the exchange below
   // the two halves' partial sums meet in LDS (fixed order: half 0 + half 1)
   float* xch = reinterpret_cast<float*>(smem);  // [4 waves][NT][4][64]
   if (half == 1) {
@@ -166,17 +206,31 @@ __global__ __launch_bounds__(WG_THREADS) void wgrad_partial_kernel(WgradArgs g) 
   }
 }
 
-// out = sum over splits (fixed order): a workgroup owns 16 outputs; thread (o, grp) sums
-// splits grp, grp+16, ... 8-deep, then the 16 partials are added in grp order.
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* slabs, int n_splits, int Ka,
-                                                           int Nb, int NC, float* c,
-                                                           float* colsum) {
+template <int NT0, int NT1>
+__global__ __launch_bounds__(WG_THREADS) void wgrad_partial_kernel(WgradArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int panel = blockIdx.y;
+  if (panel < g.p[0].panels)
+    wgrad_panel<NT0>(g.p[0], g.offsets, g.B, g.rows_per_split, blockIdx.x, panel, smem);
+  else
+    wgrad_panel<NT1>(g.p[1], g.offsets, g.B, g.rows_per_split, blockIdx.x, panel - g.p[0].panels,
+                     smem);
+}
+
+// out = sum over splits (fixed order): a workgroup owns 16 outputs of one problem; thread
+// (o, grp) sums splits grp, grp+16, ... 8-deep, then the 16 partials are added in grp
+// order.  Blocks [0, blocks0) reduce problem 0, the rest problem 1.
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(WgradArgs g, int blocks0) {
   __shared__ float part[16][17];
-  const int64_t ne = (int64_t)Ka * NC;
+  const bool second = (int)blockIdx.x >= blocks0;
+  const WgradProb& p = second ? g.p[1] : g.p[0];
+  const int blk = second ? blockIdx.x - blocks0 : blockIdx.x;
+  const int64_t ne = (int64_t)p.Ka * p.NC;
   const int o = threadIdx.x & 15, grp = threadIdx.x >> 4;
-  const int64_t i = (int64_t)blockIdx.x * 16 + o;
+  const int64_t i = (int64_t)blk * 16 + o;
   const int64_t ic = i < ne ? i : ne - 1;
-  gptr<float> src = as_global(slabs);
+  gptr<float> src = as_global(p.slabs);
+  const int n_splits = g.n_splits;
   float acc = 0.f;
   int j = grp;
   for (; j + 112 < n_splits; j += 128) {
@@ -193,9 +247,9 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* slabs, i
     float s = 0.f;
 #pragma unroll
     for (int k = 0; k < 16; ++k) s += part[k][o];
-    const int ka = (int)(i / NC), nb = (int)(i - (int64_t)ka * NC);
-    if (nb < Nb) c[(int64_t)ka * Nb + nb] = s;
-    else if (colsum) colsum[ka] = s;
+    const int ka = (int)(i / p.NC), nb = (int)(i - (int64_t)ka * p.NC);
+    if (nb < p.Nb) p.c[(int64_t)ka * p.Nb + nb] = s;
+    else if (p.colsum) p.colsum[ka] = s;
   }
 }
 
@@ -207,33 +261,115 @@ static int wgrad_nt(int nc) {
   return 16;
 }
 
-static int wg_num_cus() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0, v = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
-      n = v;
-    else
-      n = 256;
-  }
-  return n;
-}
+struct WgPlan {
+  int nt[2], panels[2], panels_nb[2];
+  int n_splits;
+  int64_t rps;
+  size_t slab_bytes[2];
+};
 
-// Splits so that splits x panels ~ one workgroup per CU, >= 4 chunks per split.
-static void wgrad_plan(int64_t max_rows, int Ka, int NC, int* n_splits, int64_t* rows_per_split,
-                       int* panels, int* panels_nb, int* nt) {
-  *nt = wgrad_nt(NC);
-  const int pa = ceil_div(Ka, WG_KA), pb = ceil_div(NC, *nt * 16);
-  *panels = pa * pb;
-  *panels_nb = pb;
-  int target = ceil_div(wg_num_cus(), *panels);
+// Panels cover Nb + 1 columns per problem (the workspace query has no colsum flag: the
+// ones column is only filled when a colsum is requested).  Splits so that splits x
+// panels ~ one workgroup per CU, each split a multiple of WG_CH rows.
+static WgPlan wgrad_plan(int64_t max_rows, const int Ka[2], const int Nb[2]) {
+  WgPlan pl{};
+  int total_panels = 0;
+  for (int i = 0; i < 2; ++i) {
+    if (Ka[i] <= 0) continue;
+    pl.nt[i] = wgrad_nt(Nb[i] + 1);
+    const int pa = ceil_div(Ka[i], WG_KA), pb = ceil_div(Nb[i] + 1, pl.nt[i] * 16);
+    pl.panels[i] = pa * pb;
+    pl.panels_nb[i] = pb;
+    total_panels += pl.panels[i];
+  }
+  // ~2 workgroups per CU over the launch (one resident at a time: ~190 VGPRs x 8 waves),
+  // >= 4 chunks each (C2 sweep of rows per split, grouped launch: 64 -> 33 us, 128 -> 30,
+  // 256 -> 37, 512 -> 63, 1024 -> 116; the per-CU f32 MFMA time of a chunk is ~1.4 us)
+  int target = 2 * device_cus() / (total_panels > 0 ? total_panels : 1);
+  if (target < 1) target = 1;
   int64_t rps = (max_rows + target - 1) / target;
   rps = ((rps + WG_CH - 1) / WG_CH) * WG_CH;
   if (rps < 4 * WG_CH) rps = 4 * WG_CH;
-  *rows_per_split = rps;
-  *n_splits = (int)((max_rows + rps - 1) / rps);
-  if (*n_splits < 1) *n_splits = 1;
+  pl.rps = rps;
+  pl.n_splits = (int)((max_rows + rps - 1) / rps);
+  if (pl.n_splits < 1) pl.n_splits = 1;
+  for (int i = 0; i < 2; ++i)
+    pl.slab_bytes[i] = Ka[i] > 0 ? sizeof(float) * (size_t)pl.n_splits * Ka[i] * (Nb[i] + 1) : 0;
+  return pl;
+}
+
+static size_t align256w(size_t v) { return (v + 255) & ~(size_t)255; }
+
+template <int NT0>
+static void launch_partial_nt1(int nt1, const dim3& grid, size_t lds, hipStream_t st, const WgradArgs& g) {
+  switch (nt1) {
+    case 4: hipLaunchKernelGGL((wgrad_partial_kernel<NT0, 4>), grid, dim3(WG_THREADS), lds, st, g); break;
+    case 8: hipLaunchKernelGGL((wgrad_partial_kernel<NT0, 8>), grid, dim3(WG_THREADS), lds, st, g); break;
+    case 13: hipLaunchKernelGGL((wgrad_partial_kernel<NT0, 13>), grid, dim3(WG_THREADS), lds, st, g); break;
+    default: hipLaunchKernelGGL((wgrad_partial_kernel<NT0, 16>), grid, dim3(WG_THREADS), lds, st, g); break;
+  }
+}
+
+static size_t lds_of(int nt) {
+  switch (nt) {
+    case 4: return WgCfg<4>::LDS;
+    case 8: return WgCfg<8>::LDS;
+    case 13: return WgCfg<13>::LDS;
+    default: return WgCfg<16>::LDS;
+  }
+}
+
+static int wgrad_run(const WgradProb in[2], const int64_t* offsets, int B, int64_t max_rows,
+                     void* workspace, size_t ws_bytes, hipStream_t st) {
+  const int Ka[2] = {in[0].Ka, in[1].a ? in[1].Ka : 0};
+  const int Nb[2] = {in[0].Nb, in[1].a ? in[1].Nb : 0};
+  if (max_rows == 0) {
+    for (int i = 0; i < 2; ++i) {
+      if (Ka[i] <= 0) continue;
+      zero_words_async(in[i].c, (int64_t)Ka[i] * Nb[i], st);
+      if (in[i].colsum) zero_words_async(in[i].colsum, Ka[i], st);
+    }
+    return 0;
+  }
+  const WgPlan pl = wgrad_plan(max_rows, Ka, Nb);
+  const size_t need = align256w(pl.slab_bytes[0]) + pl.slab_bytes[1];
+  GR_REQUIRE(workspace && ws_bytes >= need, "gr_wgrad: workspace %zu B < %zu B", ws_bytes, need);
+  WgradArgs g{};
+  g.offsets = offsets;
+  g.B = B;
+  g.rows_per_split = pl.rps;
+  g.n_splits = pl.n_splits;
+  char* ws = (char*)workspace;
+  int blocks[2] = {0, 0};
+  for (int i = 0; i < 2; ++i) {
+    g.p[i] = in[i];
+    if (Ka[i] <= 0) {
+      g.p[i].panels = 0;
+      continue;
+    }
+    g.p[i].NC = in[i].Nb + (in[i].colsum ? 1 : 0);
+    g.p[i].panels = pl.panels[i];
+    g.p[i].panels_nb = pl.panels_nb[i];
+    g.p[i].slabs = (float*)(ws + (i == 0 ? 0 : align256w(pl.slab_bytes[0])));
+    blocks[i] = (int)(((int64_t)Ka[i] * g.p[i].NC + 15) / 16);
+  }
+  const int nt0 = pl.nt[0], nt1 = Ka[1] > 0 ? pl.nt[1] : 4;
+  const size_t l0 = lds_of(nt0), l1 = lds_of(nt1);
+  const size_t lds = l0 > l1 ? l0 : l1;
+  const dim3 grid(pl.n_splits, g.p[0].panels + g.p[1].panels);
+  GR_TIMED("wgrad_partial", st, {
+    switch (nt0) {
+      case 4: launch_partial_nt1<4>(nt1, grid, lds, st, g); break;
+      case 8: launch_partial_nt1<8>(nt1, grid, lds, st, g); break;
+      case 13: launch_partial_nt1<13>(nt1, grid, lds, st, g); break;
+      default: launch_partial_nt1<16>(nt1, grid, lds, st, g); break;
+    }
+  });
+  GR_LAUNCH_CHECK("gr_wgrad(partial)");
+  GR_TIMED("wgrad_reduce", st, hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks[0] + blocks[1]),
+                                                  dim3(256), 0, st, g, blocks[0]));
+  GR_LAUNCH_CHECK("gr_wgrad(reduce)");
+  return 0;
 }
 
 }  // namespace gr
@@ -242,10 +378,16 @@ using namespace gr;
 
 extern "C" size_t gr_wgrad_workspace_size(int64_t max_rows, int Ka, int Nb) {
   if (max_rows <= 0 || Ka <= 0 || Nb <= 0) return 0;
-  int n_splits, panels, pnb, nt;
-  int64_t rps;
-  wgrad_plan(max_rows, Ka, Nb + 1, &n_splits, &rps, &panels, &pnb, &nt);
-  return sizeof(float) * (size_t)n_splits * (size_t)Ka * (Nb + 1);
+  const int ka[2] = {Ka, 0}, nb[2] = {Nb, 0};
+  const WgPlan pl = wgrad_plan(max_rows, ka, nb);
+  return align256w(pl.slab_bytes[0]);
+}
+
+extern "C" size_t gr_wgrad2_workspace_size(int64_t max_rows, int Ka0, int Nb0, int Ka1, int Nb1) {
+  if (max_rows <= 0 || Ka0 <= 0 || Nb0 <= 0 || Ka1 < 0 || Nb1 < 0) return 0;
+  const int ka[2] = {Ka0, Nb1 > 0 ? Ka1 : 0}, nb[2] = {Nb0, Ka1 > 0 ? Nb1 : 0};
+  const WgPlan pl = wgrad_plan(max_rows, ka, nb);
+  return align256w(pl.slab_bytes[0]) + pl.slab_bytes[1];
 }
 
 extern "C" int gr_wgrad(const float* a, int64_t lda, const float* a_stats, const float* bm,
@@ -254,35 +396,27 @@ extern "C" int gr_wgrad(const float* a, int64_t lda, const float* a_stats, const
                         void* stream) {
   GR_REQUIRE(a && bm && offsets && c, "gr_wgrad: null pointer");
   GR_REQUIRE(Ka > 0 && Nb > 0 && B >= 0 && max_rows >= 0, "gr_wgrad: bad sizes");
-  hipStream_t st = (hipStream_t)stream;
-  if (max_rows == 0) {
-    zero_words_async(c, (int64_t)Ka * Nb, st);
-    if (a_colsum) zero_words_async(a_colsum, Ka, st);
-    return 0;
-  }
   GR_REQUIRE(max_rows * (lda > ldb ? lda : ldb) * 4 < 0x7fffffffLL,
              "gr_wgrad: %lld rows exceed the 32-bit buffer range", (long long)max_rows);
-  const int NC = Nb + (a_colsum ? 1 : 0);
-  int n_splits, panels, pnb, nt;
-  int64_t rps;
-  // one plan for both column counts (the workspace query has no colsum flag): panels
-  // cover Nb + 1 columns, the ones column is only filled when a_colsum is requested
-  wgrad_plan(max_rows, Ka, Nb + 1, &n_splits, &rps, &panels, &pnb, &nt);
-  const size_t need = sizeof(float) * (size_t)n_splits * Ka * NC;
-  GR_REQUIRE(workspace && ws_bytes >= need, "gr_wgrad: workspace %zu B < %zu B", ws_bytes, need);
-  WgradArgs g{a, lda, (const float2*)a_stats, bm, ldb, offsets, B, Ka, Nb, NC, rps, n_splits, pnb,
-              (float*)workspace};
-  const dim3 grid(n_splits, panels);
-  switch (nt) {
-    case 4: GR_TIMED("wgrad_partial", st, hipLaunchKernelGGL(wgrad_partial_kernel<4>, grid, dim3(WG_THREADS), WgCfg<4>::LDS, st, g)); break;
-    case 8: GR_TIMED("wgrad_partial", st, hipLaunchKernelGGL(wgrad_partial_kernel<8>, grid, dim3(WG_THREADS), WgCfg<8>::LDS, st, g)); break;
-    case 13: GR_TIMED("wgrad_partial", st, hipLaunchKernelGGL(wgrad_partial_kernel<13>, grid, dim3(WG_THREADS), WgCfg<13>::LDS, st, g)); break;
-    default: GR_TIMED("wgrad_partial", st, hipLaunchKernelGGL(wgrad_partial_kernel<16>, grid, dim3(WG_THREADS), WgCfg<16>::LDS, st, g)); break;
-  }
-  GR_LAUNCH_CHECK("gr_wgrad(partial)");
-  const int64_t ne = (int64_t)Ka * NC;
-  GR_TIMED("wgrad_reduce", st, hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((ne + 15) / 16)), dim3(256), 0, st,
-                                                  (const float*)workspace, n_splits, Ka, Nb, NC, c, a_colsum));
-  GR_LAUNCH_CHECK("gr_wgrad(reduce)");
-  return 0;
+  WgradProb p[2] = {};
+  p[0] = WgradProb{a, lda, (const float2*)a_stats, bm, ldb, Ka, Nb, 0, 0, 0, nullptr, c, a_colsum};
+  return wgrad_run(p, offsets, B, max_rows, workspace, ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" int gr_wgrad2(const float* a0, int64_t lda0, const float* a_stats0, const float* b0,
+                         int64_t ldb0, int Ka0, int Nb0, float* c0, float* colsum0,
+                         const float* a1, int64_t lda1, const float* a_stats1, const float* b1,
+                         int64_t ldb1, int Ka1, int Nb1, float* c1, float* colsum1,
+                         const int64_t* offsets, int B, int64_t max_rows, void* workspace,
+                         size_t ws_bytes, void* stream) {
+  GR_REQUIRE(a0 && b0 && c0 && a1 && b1 && c1 && offsets, "gr_wgrad2: null pointer");
+  GR_REQUIRE(Ka0 > 0 && Nb0 > 0 && Ka1 > 0 && Nb1 > 0 && B >= 0 && max_rows >= 0,
+             "gr_wgrad2: bad sizes");
+  const int64_t ld = std::max(std::max(lda0, ldb0), std::max(lda1, ldb1));
+  GR_REQUIRE(max_rows * ld * 4 < 0x7fffffffLL,
+             "gr_wgrad2: %lld rows exceed the 32-bit buffer range", (long long)max_rows);
+  WgradProb p[2] = {};
+  p[0] = WgradProb{a0, lda0, (const float2*)a_stats0, b0, ldb0, Ka0, Nb0, 0, 0, 0, nullptr, c0, colsum0};
+  p[1] = WgradProb{a1, lda1, (const float2*)a_stats1, b1, ldb1, Ka1, Nb1, 0, 0, 0, nullptr, c1, colsum1};
+  return wgrad_run(p, offsets, B, max_rows, workspace, ws_bytes, (hipStream_t)stream);
 }

@@ -15,7 +15,6 @@ Reference map (``src/generative_recommenders_pl/models/``):
 """
 from __future__ import annotations
 
-import os
 
 from dataclasses import dataclass
 from typing import Optional
@@ -41,25 +40,6 @@ def _stream():
     return _lib.stream_handle()
 
 
-_SIDE: dict = {}
-
-
-def _side_stream(device) -> "torch.cuda.Stream":
-    """Second stream for the weight-gradient GEMMs, which are independent of the
-    attention / input-gradient chain of a layer's backward (they overlap with it)."""
-    key = device.index
-    s = _SIDE.get(key)
-    if s is None:
-        s = torch.cuda.Stream(device=device)
-        _SIDE[key] = s
-    return s
-
-
-def _overlap_enabled() -> bool:
-    # measured on MI355X (ml-1m step): 1.50 ms with the side stream vs 1.31 ms without —
-    # the concurrent weight-gradient kernels slow the attention critical path more than
-    # they hide; kept as an opt-in (GR_OVERLAP=1) for shapes with idle CUs
-    return os.environ.get("GR_OVERLAP", "0") == "1"
 
 
 # ------------------------------------------------------------------ jagged helpers
@@ -313,32 +293,6 @@ class STULayerFunction(torch.autograd.Function):
                   attn_stats.data_ptr(), _lib.ptr(h_pre), n_out, geo.dropout_p, ctx.seed,
                   _lib.ptr(ctx.seed_offset), d_uvqk.data_ptr(), n_out, d_attn.data_ptr(), hv, st)
         L = _lib.lib()
-        main = torch.cuda.current_stream(dev)
-        side = _side_stream(dev) if _overlap_enabled() else None
-
-        def on_side(fn, *tensors):
-            # run fn on the side stream after everything queued on main so far; the
-            # caching allocator is told the tensors are in use there
-            if side is None:
-                fn(st)
-                return
-            side.wait_stream(main)
-            for t in tensors:
-                if t is not None:
-                    t.record_stream(side)
-            with torch.cuda.stream(side):
-                fn(_lib.stream_handle())
-
-        d_w_o = d_b_o = None
-        if o_in is not None:
-            d_w_o = torch.empty(D, hv, dtype=torch.float32, device=dev)
-            d_b_o = torch.empty(D, dtype=torch.float32, device=dev)
-            ws_n = L.gr_wgrad_workspace_size(rows, D, hv)
-            ws = torch.empty(max(ws_n, 4), dtype=torch.uint8, device=dev)
-            on_side(lambda s_: _lib.call("gr_wgrad", dy.data_ptr(), D, None, o_in.data_ptr(), hv,
-                                         offsets.data_ptr(), B, rows, D, hv, d_w_o.data_ptr(),
-                                         d_b_o.data_ptr(), ws.data_ptr(), ws_n, s_),
-                    dy, o_in, offsets, d_w_o, d_b_o, ws)
         d_pos_w = d_ts_w = None
         ws_a = None
         ws_a_n = 0
@@ -364,22 +318,36 @@ class STULayerFunction(torch.autograd.Function):
                   _lib.ptr(bmap), _lib.ptr(pos_w), _lib.ptr(ts_w), NUM_BUCKETS,
                   hq_p, hk_p, hv_p, n_out, dq.data_ptr(), dk.data_ptr(), dvv.data_ptr(), n_out,
                   _lib.ptr(d_pos_w), _lib.ptr(d_ts_w), _lib.ptr(ws_a), ws_a_n, st)
-        d_w_uvqk = None
-        if ctx.needs_input_grad[3]:
-            d_w_uvqk = torch.empty(D, n_out, dtype=torch.float32, device=dev)
-            ws_n2 = L.gr_wgrad_workspace_size(rows, D, n_out)
-            ws2 = torch.empty(max(ws_n2, 4), dtype=torch.uint8, device=dev)
-            on_side(lambda s_: _lib.call("gr_wgrad", x.data_ptr(), x.stride(0), x_stats.data_ptr(),
-                                         d_uvqk.data_ptr(), n_out, offsets.data_ptr(), B, rows, D,
-                                         n_out, d_w_uvqk.data_ptr(), None, ws2.data_ptr(), ws_n2,
-                                         s_),
-                    x, x_stats, d_uvqk, offsets, d_w_uvqk, ws2)
         dx = torch.empty(rows, D, dtype=torch.float32, device=dev)
         _lib.call("hstu_ln_uvqk_bwd", d_uvqk.data_ptr(), n_out, offsets.data_ptr(), B, rows, D,
                   n_out, w_uvqk.data_ptr(), x.data_ptr(), x.stride(0), x_stats.data_ptr(),
                   dy.data_ptr(), D, dx.data_ptr(), D, st)
-        if side is not None:
-            main.wait_stream(side)  # the weight gradients are returned on main
+        # weight gradients (off the critical path): both GEMMs of the layer in one launch
+        # and one slab reduce (gr_wgrad2)
+        want_uvqk = ctx.needs_input_grad[3]
+        d_w_uvqk = torch.empty(D, n_out, dtype=torch.float32, device=dev) if want_uvqk else None
+        d_w_o = d_b_o = None
+        if o_in is not None:
+            d_w_o = torch.empty(D, hv, dtype=torch.float32, device=dev)
+            d_b_o = torch.empty(D, dtype=torch.float32, device=dev)
+        if want_uvqk and o_in is not None:
+            ws_n = L.gr_wgrad2_workspace_size(rows, D, n_out, D, hv)
+            ws = torch.empty(max(ws_n, 4), dtype=torch.uint8, device=dev)
+            _lib.call("gr_wgrad2", x.data_ptr(), x.stride(0), x_stats.data_ptr(), d_uvqk.data_ptr(),
+                      n_out, D, n_out, d_w_uvqk.data_ptr(), None,
+                      dy.data_ptr(), D, None, o_in.data_ptr(), hv, D, hv, d_w_o.data_ptr(),
+                      d_b_o.data_ptr(), offsets.data_ptr(), B, rows, ws.data_ptr(), ws_n, st)
+        elif want_uvqk:
+            ws_n = L.gr_wgrad_workspace_size(rows, D, n_out)
+            ws = torch.empty(max(ws_n, 4), dtype=torch.uint8, device=dev)
+            _lib.call("gr_wgrad", x.data_ptr(), x.stride(0), x_stats.data_ptr(), d_uvqk.data_ptr(),
+                      n_out, offsets.data_ptr(), B, rows, D, n_out, d_w_uvqk.data_ptr(), None,
+                      ws.data_ptr(), ws_n, st)
+        elif o_in is not None:
+            ws_n = L.gr_wgrad_workspace_size(rows, D, hv)
+            ws = torch.empty(max(ws_n, 4), dtype=torch.uint8, device=dev)
+            _lib.call("gr_wgrad", dy.data_ptr(), D, None, o_in.data_ptr(), hv, offsets.data_ptr(),
+                      B, rows, D, hv, d_w_o.data_ptr(), d_b_o.data_ptr(), ws.data_ptr(), ws_n, st)
         return (dx, None, None, d_w_uvqk, d_w_o, d_b_o, d_pos_w, d_ts_w, None, None, None)
 
 

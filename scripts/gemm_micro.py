@@ -20,6 +20,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shape", default="c2", choices=sorted(SHAPES))
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--wgrad-only", action="store_true", help="only the grouped weight gradients")
     args = ap.parse_args()
     B, N, L, D = SHAPES[args.shape]
     hv = D
@@ -52,11 +53,19 @@ def main():
     L_ = _lib.lib()
     ws1 = L_.gr_wgrad_workspace_size(cap, D, hv)
     ws2 = L_.gr_wgrad_workspace_size(cap, D, n_out)
-    ws = torch.empty(max(ws1, ws2, 4), dtype=torch.uint8, device=dev)
+    ws3 = L_.gr_wgrad2_workspace_size(cap, D, n_out, D, hv)
+    ws = torch.empty(max(ws1, ws2, ws3, 4), dtype=torch.uint8, device=dev)
     st = _lib.stream_handle()
     P = lambda t: t.data_ptr()  # noqa: E731
 
+    def run_w():
+        _lib.call("gr_wgrad2", P(x), D, P(x_stats), P(d_uvqk), n_out, D, n_out, P(dWu), None,
+                  P(dy), D, None, P(o_in), hv, D, hv, P(dWo), P(dbo), P(offsets), B, cap,
+                  P(ws), ws.numel(), st)
+
     def run():
+        if args.wgrad_only:
+            return run_w()
         _lib.call("hstu_ln_uvqk_fwd", P(x), D, P(offsets), B, cap, D, P(w_uvqk), n_out, 1e-6, 1,
                   P(x_stats), P(h_pre), P(uvqk), n_out, st)
         _lib.call("hstu_gate_o_fwd", P(uvqk), n_out, P(attn), hv, P(offsets), B, cap, hv, D,
