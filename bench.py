@@ -298,7 +298,7 @@ def hstu_step_flops(L, D, H, dqk, dv, blocks):
 
 
 def encoder_leg(B, N0, out_len, D, blocks, H, steps, warmup, device, world, seed,
-                eager=False, instrument=False, muon=False):
+                eager=False, instrument=False, muon=False, bf16=False):
     """Times the encoder training step alone at one shape: HSTU fwd + bwd (input and
     parameter grads) -> gradient all-reduce -> fused AdamW, fixed-length rows, train
     mode, captured as two HIP graphs around the all-reduce.  Used for the C2 batch
@@ -318,7 +318,8 @@ def encoder_leg(B, N0, out_len, D, blocks, H, steps, warmup, device, world, seed
                item_embedding_dim=D, num_blocks=blocks, num_heads=H, linear_dim=dh,
                attention_dim=dh, normalization="rel_bias", linear_config="uvqk",
                linear_activation="silu", linear_dropout_rate=0.2,
-               attn_dropout_rate=0.0).to(device).train()
+               attn_dropout_rate=0.0,
+               autocast_dtype=torch.bfloat16 if bf16 else None).to(device).train()
     if muon:
         reducer = BucketedGradReducer(list(enc.parameters()), overlap=world > 1)
         eager = eager or world > 1
@@ -467,6 +468,7 @@ def main():
                     help="C2 batch sweep of the encoder step (comma list; '' = skip)")
     ap.add_argument("--c3-steps", type=int, default=5,
                     help="timed steps of the C3 leg (B=32, N=2059, D=256, 8 blocks; 0 = skip)")
+    ap.add_argument("--no-bf16-leg", action="store_true", help="skip the C2 bf16-attention leg")
     ap.add_argument("--cpu-batch", type=int, default=128,
                     help="sequences per iteration of the CPU proxy baseline")
     args = ap.parse_args()
@@ -717,40 +719,58 @@ def main():
             r = encoder_leg(Bs, N0, out_len, D, blocks, 1, max(5, min(20, 2560 // Bs)), 3,
                             device, world, 2000 + rank)
             sweep.append({"batch": Bs, "seq_per_s": r["value"], "ms_per_step": r["ms_per_step"]})
-    c3 = None
-    if args.c3_steps > 0:
+    def c3_leg(bf16):
         B3, N3, D3, L3 = 32, 2048, 256, 8
         r = encoder_leg(B3, N3, out_len, D3, L3, 1, args.c3_steps, 2, device, world,
-                        3000 + rank, instrument=True, muon=True)
+                        3000 + rank, instrument=True, muon=True, bf16=bf16)
         step_flops = B3 * hstu_step_flops(N3, D3, 1, D3, D3, L3)
         ach3 = step_flops / (r["ms_per_step"] * 1e-3) / 1e12
         f3, dkv3, dq3 = attn_flops(r["lengths"], 1, D3, D3, L3)
         rows3, nout3 = B3 * N3, 4 * D3
+        # algorithmic FLOPs per layer of each kernel (x L3 layers per step)
         fpl3 = {"attn_fwd": f3, "attn_bwd": dkv3 + dq3, "attn_bwd_dkv": dkv3, "attn_bwd_dq": dq3,
                 "ln_uvqk_fwd": 2.0 * rows3 * D3 * nout3, "gate_o_fwd": 2.0 * rows3 * D3 * D3,
                 "gate_o_bwd": 2.0 * rows3 * D3 * D3, "ln_uvqk_bwd": 2.0 * rows3 * nout3 * D3,
-                "wgrad_partial": (2.0 * rows3 * D3 * D3 + 2.0 * rows3 * D3 * nout3) / 2.0}
+                "wgrad_partial": 2.0 * rows3 * D3 * D3 + 2.0 * rows3 * D3 * nout3}
         kps = r["kernel_per_step_ms"]
         dom3 = max(kps, key=kps.get)
-        ach_k = fpl3.get(dom3, 0.0) / (r["kernel_avg_ms"][dom3] * 1e-3) / 1e12
-        c3 = {"metric": "HSTU seq/s (fwd+bwd)", "value": r["value"], "unit": "seq/s",
-              "ms_per_step": r["ms_per_step"], "steps": args.c3_steps, "dtype": "fp32",
-              "config": {"workload": ("C3: ml-20m width HSTU train step (fwd+bwd, Muon + AdamW)"
-                                      if world == 1 else
-                                      "C5: ml-20m width HSTU DDP train step (fwd+bwd, bucketed "
-                                      "all-reduce overlapped with the backward, Muon + AdamW)"),
-                         "execution": r["execution"],
-                         "global_batch": B3 * world, "seq_len": N3, "padded_len": N3 + out_len,
-                         "dim": D3, "blocks": L3, "heads": 1},
-              "algorithmic_tflop_per_step": round(step_flops / 1e12, 4),
-              "roofline": {"bound": "mfma", "achieved": round(ach3, 2),
-                           "peak": peaks["fp32_mfma_tflops"], "unit": "TFLOP/s",
-                           "frac": round(ach3 / peaks["fp32_mfma_tflops"], 4),
-                           "basis": "whole step: SURVEY §8d 83.8 GFLOP/seq (3 x fwd) / step time"},
-              "dominant_kernel": {"kernel": dom3, "avg_launch_ms": round(r["kernel_avg_ms"][dom3], 4),
-                                  "achieved": round(ach_k, 2), "unit": "TFLOP/s",
-                                  "frac": round(ach_k / peaks["fp32_mfma_tflops"], 4)},
-              "per_step_device_ms": {k: round(v, 4) for k, v in sorted(kps.items(), key=lambda kv: -kv[1])}}
+        ach_k = fpl3.get(dom3, 0.0) * L3 / (kps[dom3] * 1e-3) / 1e12
+        peak = peaks["bf16_mfma_tflops"] if bf16 else peaks["fp32_mfma_tflops"]
+        wl = ("C3: ml-20m width HSTU train step (fwd+bwd, Muon + AdamW)" if world == 1 else
+              "C5: ml-20m width HSTU DDP train step (fwd+bwd, bucketed all-reduce overlapped "
+              "with the backward, Muon + AdamW)")
+        if bf16:
+            wl += "; bf16 attention operands (autocast_dtype=bfloat16), fp32 projections"
+        return {"metric": "HSTU seq/s (fwd+bwd)", "value": r["value"], "unit": "seq/s",
+                "ms_per_step": r["ms_per_step"], "steps": args.c3_steps,
+                "dtype": "bf16 attention / fp32" if bf16 else "fp32",
+                "config": {"workload": wl, "execution": r["execution"],
+                           "global_batch": B3 * world, "seq_len": N3, "padded_len": N3 + out_len,
+                           "dim": D3, "blocks": L3, "heads": 1},
+                "algorithmic_tflop_per_step": round(step_flops / 1e12, 4),
+                "roofline": {"bound": "mfma", "achieved": round(ach3, 2),
+                             "peak": peaks["fp32_mfma_tflops"], "unit": "TFLOP/s",
+                             "frac": round(ach3 / peaks["fp32_mfma_tflops"], 4),
+                             "basis": "whole step: SURVEY §8d 83.8 GFLOP/seq (3 x fwd) / step "
+                                      "time, against the fp32 MFMA peak"},
+                "dominant_kernel": {"kernel": dom3, "per_step_ms": round(kps[dom3], 4),
+                                    "achieved": round(ach_k, 2), "unit": "TFLOP/s",
+                                    "peak": peak, "frac": round(ach_k / peak, 4)},
+                "per_step_device_ms": {k: round(v, 4) for k, v in sorted(kps.items(),
+                                                                         key=lambda kv: -kv[1])}}
+
+    c3 = c3_bf16 = c2_bf16 = None
+    if args.c3_steps > 0:
+        c3 = c3_leg(False)
+        c3_bf16 = c3_leg(True)
+    if not args.no_bf16_leg:
+        r = encoder_leg(B, N0, out_len, D, blocks, 1, args.steps, 3, device, world, 2500 + rank,
+                        bf16=True)
+        c2_bf16 = {"metric": "HSTU seq/s (fwd+bwd)", "value": r["value"], "unit": "seq/s",
+                   "ms_per_step": r["ms_per_step"], "dtype": "bf16 attention / fp32",
+                   "config": {"workload": "C2 encoder train step (fwd+bwd+AdamW), bf16 attention "
+                                          "operands (autocast_dtype=bfloat16), fp32 projections",
+                              "global_batch": B * world, "seq_len": N0, "execution": r["execution"]}}
 
     e2e = None
     if args.e2e_steps > 0:
@@ -798,6 +818,8 @@ def main():
             "retrieval": retrieval,
             "c2_batch_sweep": sweep,
             "c3": c3,
+            "c3_bf16": c3_bf16,
+            "c2_bf16": c2_bf16,
             "e2e_train_step": e2e,
             "cpu_baseline": cpu,
         }

@@ -179,6 +179,16 @@ GR_API int hstu_attn_fwd(const float* q, const float* k, const float* v, int64_t
                   const float* ts_w, int num_buckets, float* out, int64_t ld_out,
                   void* stream);
 
+/* hstu_attn_fwd_bf16: hstu_attn_fwd with bf16 MFMA operands and fp32 accumulation (the
+ * opt-in bf16 compute mode): Q, K, V are rounded to bf16 as they are staged and
+ * P = silu(S + bias) / N is rounded to bf16 before P.V; S, the bias, silu and the
+ * output are fp32.  Same arguments and layout as hstu_attn_fwd. */
+GR_API int hstu_attn_fwd_bf16(const float* q, const float* k, const float* v, int64_t ld_qk,
+                              int64_t ld_v, const int64_t* offsets, int B, int N, int max_len,
+                              int H, int dqk, int dv, const uint8_t* bucket_map,
+                              const float* pos_w, const float* ts_w, int num_buckets, float* out,
+                              int64_t ld_out, void* stream);
+
 /* Backward of hstu_attn_fwd (replaces the autograd backward of hstu.py:134-205 and of
  * the bias module hstu.py:96-128, including the index_add_ into _ts_w and the
  * slice/pad backward into _pos_w).  dout: (total, H*dv), stride ld_dout.
@@ -199,6 +209,21 @@ GR_API int hstu_attn_bwd(const float* q, const float* k, const float* v, int64_t
                   int64_t ld_h, float* dq, float* dk, float* dv_out, int64_t ld_d,
                   float* dpos_w, float* dts_w, void* workspace, size_t ws_bytes,
                   void* stream);
+
+/* hstu_attn_bwd_bf16: hstu_attn_bwd with bf16 MFMA operands (Q, K, V, dO, P, dS) and
+ * fp32 accumulation / elementwise (the opt-in bf16 compute mode); the bias gradients
+ * sum fp32 dS in a fixed order.  Same arguments as hstu_attn_bwd; the workspace size
+ * also depends on the head dims. */
+GR_API size_t hstu_attn_bwd_bf16_workspace_size(int B, int N, int max_len, int H, int dqk,
+                                                int dv, int num_buckets);
+GR_API int hstu_attn_bwd_bf16(const float* q, const float* k, const float* v, int64_t ld_qk,
+                              int64_t ld_v, const float* dout, int64_t ld_dout,
+                              const int64_t* offsets, int B, int N, int max_len, int H, int dqk,
+                              int dv, const uint8_t* bucket_map, const float* pos_w,
+                              const float* ts_w, int num_buckets, const float* hq,
+                              const float* hk, const float* hv, int64_t ld_h, float* dq,
+                              float* dk, float* dvv, int64_t ld_d, float* dpos_w, float* dts_w,
+                              void* workspace, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------- STU projections
  * All take jagged rows (total = offsets[B] <= max_rows), fp32, f32 MFMA.
@@ -240,6 +265,27 @@ GR_API int hstu_gate_o_bwd(const float* dy, int64_t ld_dy, const int64_t* offset
                     const float* attn_stats, const float* h_u, int64_t ld_h,
                     float dropout_p, uint64_t seed, const int64_t* seed_offset, float* du,
                     int64_t ld_du, float* d_attn, int64_t ld_da, void* stream);
+
+/* hstu_gate_o_cat_fwd / _bwd: the concat_ua = True form of hstu_gate_o_fwd / _bwd
+ * (hstu.py:398-400): o_in = dropout_p([u, LN(attn), u * LN(attn)]) (rows, 3 hdv; the mask
+ * hashes (row, column of o_in)), y = o_in @ w_o^T + b_o + x_res.  w_pad is the (D, 3 hvp)
+ * row-major weight with w_o's three hdv-wide column blocks at column offsets 0, hvp,
+ * 2 hvp and zeros elsewhere; hvp = 16 ceil(hdv / 16) rounded up to 16, 32 or 64
+ * (hdv <= 64, D <= 128, even widths and 8-byte aligned rows).  The backward returns
+ * du (* silu'(h_u) when h_u) and d_attn = LayerNorm_backward(attn; g2 + g3 * u). */
+GR_API int hstu_gate_o_cat_fwd(const float* u, int64_t ld_u, const float* attn, int64_t ld_attn,
+                               const int64_t* offsets, int B, int64_t max_rows, int hdv, int hvp,
+                               int D, const float* w_pad, const float* b_o, const float* x_res,
+                               int64_t ld_x, float eps, float dropout_p, uint64_t seed,
+                               const int64_t* seed_offset, float* attn_stats, float* o_in,
+                               float* y, int64_t ld_y, void* stream);
+GR_API int hstu_gate_o_cat_bwd(const float* dy, int64_t ld_dy, const int64_t* offsets, int B,
+                               int64_t max_rows, int hdv, int hvp, int D, const float* w_pad,
+                               const float* u, int64_t ld_u, const float* attn, int64_t ld_attn,
+                               const float* attn_stats, const float* h_u, int64_t ld_h,
+                               float dropout_p, uint64_t seed, const int64_t* seed_offset,
+                               float* du, int64_t ld_du, float* d_attn, int64_t ld_da,
+                               void* stream);
 
 /* hstu_ln_uvqk_bwd  (backward of hstu_ln_uvqk_fwd w.r.t. x, plus the residual; D <= 256):
  *   dn = dh @ w_uvqk^T;  dx = dy_res + LayerNorm_backward(x; dn)   (dy_res may be NULL;

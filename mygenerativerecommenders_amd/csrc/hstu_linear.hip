@@ -712,6 +712,65 @@ struct RwArgsLnUvqkBwd {
   }
 };
 
+// concat_ua row-wave launches (KG / NT = 3 segments of KGH 16-column groups)
+template <class Op, int KG, int NT>
+static int rw_launch_op(const Op& op, int64_t max_rows, const char* tname, hipStream_t st) {
+  using C = RowWaveCfg<KG, NT>;
+  if constexpr (C::LDS_BYTES > RW_LDS_MAX) {
+    GR_REQUIRE(false, "%s: concat_ua weight panel (%d x %d groups) exceeds the LDS budget", tname,
+               KG, NT);
+  } else {
+    const int64_t units = (max_rows + 15) / 16;
+    int grid = (int)((units + 3) / 4);
+    const int cap = 4 * num_cus();
+    if (grid > cap) grid = cap;
+    if (grid < 1) return 0;
+    GR_TIMED(tname, st, hipLaunchKernelGGL((rowwave_kernel<KG, NT, Op>), dim3(grid), dim3(256),
+                                           C::LDS_BYTES, st, op));
+    GR_LAUNCH_CHECK(tname);
+    return 0;
+  }
+}
+
+static int cat_kgh(int hv) { return hv <= 16 ? 1 : hv <= 32 ? 2 : hv <= 64 ? 4 : -1; }
+
+template <int KGH, int NT>
+static int cat_fwd_nt(const RwArgsGateO& a, int hv, int64_t max_rows, hipStream_t st) {
+  using Op = typename RwGateOCatT<KGH, NT, 2>::template Op<3 * KGH, NT, 2>;
+  Op op;
+  a.fill(op);
+  op.hv = hv;
+  return rw_launch_op<Op, 3 * KGH, NT>(op, max_rows, "gate_o_fwd", st);
+}
+template <int KGH>
+static int cat_fwd_kgh(const RwArgsGateO& a, int hv, int nt, int64_t max_rows, hipStream_t st) {
+  switch (nt) {
+    case 1: return cat_fwd_nt<KGH, 1>(a, hv, max_rows, st);
+    case 2: return cat_fwd_nt<KGH, 2>(a, hv, max_rows, st);
+    case 4: return cat_fwd_nt<KGH, 4>(a, hv, max_rows, st);
+    case 8: return cat_fwd_nt<KGH, 8>(a, hv, max_rows, st);
+  }
+  return -1;
+}
+template <int KGH, int KG>
+static int cat_bwd_kg(const RwArgsGateOBwd& a, int hv, int64_t max_rows, hipStream_t st) {
+  using Op = typename RwGateOCatBwdT<KGH, KG, 2>::template Op<KG, 3 * KGH, 2>;
+  Op op;
+  a.fill(op);
+  op.hv = hv;
+  return rw_launch_op<Op, KG, 3 * KGH>(op, max_rows, "gate_o_bwd", st);
+}
+template <int KGH>
+static int cat_bwd_kgh(const RwArgsGateOBwd& a, int hv, int kg, int64_t max_rows, hipStream_t st) {
+  switch (kg) {
+    case 1: return cat_bwd_kg<KGH, 1>(a, hv, max_rows, st);
+    case 2: return cat_bwd_kg<KGH, 2>(a, hv, max_rows, st);
+    case 4: return cat_bwd_kg<KGH, 4>(a, hv, max_rows, st);
+    case 8: return cat_bwd_kg<KGH, 8>(a, hv, max_rows, st);
+  }
+  return -1;
+}
+
 static bool rw_enabled() {
   static int on = -1;
   if (on < 0) {
@@ -811,4 +870,53 @@ extern "C" int hstu_ln_uvqk_bwd(const float* dh, int64_t ld_dh, const int64_t* o
   op.w = w_uvqk; op.x = x; op.ldx = ld_x; op.x_stats = (const float2*)x_stats;
   op.dy = dy_res; op.lddy = ld_dy; op.dx = dx; op.lddx = ld_dx;
   return launch_rowpanel(op, max_rows, true, "hstu_ln_uvqk_bwd", (hipStream_t)stream);
+}
+
+extern "C" int hstu_gate_o_cat_fwd(const float* u, int64_t ld_u, const float* attn, int64_t ld_attn,
+                                   const int64_t* offsets, int B, int64_t max_rows, int hdv, int hvp,
+                                   int D, const float* w_pad, const float* b_o, const float* x_res,
+                                   int64_t ld_x, float eps, float dropout_p, uint64_t seed,
+                                   const int64_t* seed_offset, float* attn_stats, float* o_in,
+                                   float* y, int64_t ld_y, void* stream) {
+  GR_REQUIRE(u && attn && offsets && w_pad && y && attn_stats, "hstu_gate_o_cat_fwd: null pointer");
+  const int kgh = cat_kgh(hdv), nt = rw_bucket(D);
+  GR_REQUIRE(kgh > 0 && hvp == 16 * kgh && nt > 0 && nt <= 8 && B >= 0,
+             "hstu_gate_o_cat_fwd: hdv %d (hvp %d) / D %d unsupported (hdv <= 64, hvp = %d, D <= 128)",
+             hdv, hvp, D, 16 * kgh);
+  GR_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f, "hstu_gate_o_cat_fwd: dropout_p %f", dropout_p);
+  GR_REQUIRE(rw_vec({u, attn, x_res, o_in, y}, {ld_u, ld_attn, ld_x, ld_y, hdv, D}) > 0,
+             "hstu_gate_o_cat_fwd: rows and widths must be 8-byte aligned (even)");
+  RwArgsGateO ra{offsets, B, 3 * hvp, D, u, ld_u, attn, ld_attn, w_pad, b_o, x_res, ld_x, eps,
+                 dropout_p, seed, seed_offset, (float2*)attn_stats, o_in, y, ld_y};
+  const hipStream_t st = (hipStream_t)stream;
+  switch (kgh) {
+    case 1: return cat_fwd_kgh<1>(ra, hdv, nt, max_rows, st);
+    case 2: return cat_fwd_kgh<2>(ra, hdv, nt, max_rows, st);
+    default: return cat_fwd_kgh<4>(ra, hdv, nt, max_rows, st);
+  }
+}
+
+extern "C" int hstu_gate_o_cat_bwd(const float* dy, int64_t ld_dy, const int64_t* offsets, int B,
+                                   int64_t max_rows, int hdv, int hvp, int D, const float* w_pad,
+                                   const float* u, int64_t ld_u, const float* attn, int64_t ld_attn,
+                                   const float* attn_stats, const float* h_u, int64_t ld_h,
+                                   float dropout_p, uint64_t seed, const int64_t* seed_offset,
+                                   float* du, int64_t ld_du, float* d_attn, int64_t ld_da,
+                                   void* stream) {
+  GR_REQUIRE(dy && offsets && w_pad && u && attn && attn_stats && du && d_attn,
+             "hstu_gate_o_cat_bwd: null pointer");
+  const int kgh = cat_kgh(hdv), kg = rw_bucket(D);
+  GR_REQUIRE(kgh > 0 && hvp == 16 * kgh && kg > 0 && kg <= 8 && B >= 0,
+             "hstu_gate_o_cat_bwd: hdv %d (hvp %d) / D %d unsupported", hdv, hvp, D);
+  GR_REQUIRE(rw_vec({dy, u, attn, h_u, du, d_attn}, {ld_dy, ld_u, ld_attn, ld_h, ld_du, ld_da, hdv, D}) > 0,
+             "hstu_gate_o_cat_bwd: rows and widths must be 8-byte aligned (even)");
+  RwArgsGateOBwd ra{offsets, B, D, 3 * hvp, dy, ld_dy, w_pad, u, ld_u, attn, ld_attn,
+                    (const float2*)attn_stats, h_u, ld_h, dropout_p, seed, seed_offset, du, ld_du,
+                    d_attn, ld_da};
+  const hipStream_t st = (hipStream_t)stream;
+  switch (kgh) {
+    case 1: return cat_bwd_kgh<1>(ra, hdv, kg, max_rows, st);
+    case 2: return cat_bwd_kgh<2>(ra, hdv, kg, max_rows, st);
+    default: return cat_bwd_kgh<4>(ra, hdv, kg, max_rows, st);
+  }
 }

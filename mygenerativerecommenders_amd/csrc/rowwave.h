@@ -471,6 +471,218 @@ struct RwGateOBwd {
   }
 };
 
+// F3 with concat_ua (hstu.py:398-400): o_in = dropout([u, a, u * a]), a = LN(attn),
+// y = o_in @ W_o^T + b_o + x.  The three hdv-wide segments sit at 16-aligned k offsets
+// seg * hvp (hvp = 16 KGH >= hdv) of a zero-padded weight W' (D, 3 hvp) built by the
+// caller; the stored o_in is unpadded (rows, 3 hdv) for the weight gradient; the
+// dropout mask hashes (row, seg * hdv + c) over the 3 hdv-wide o_in.
+template <int KGH, int NT, int VEC_>
+struct RwGateOCatT {
+  template <int KG, int NT_, int V_>
+  struct Op {
+    static_assert(KG == 3 * KGH, "KG = 3 segments of KGH groups");
+    static constexpr int VEC = V_;
+    static constexpr bool K_CONTIG = true;
+    const int64_t* offsets;
+    int B, K, N;  // K = 3 hvp (padded), N = D
+    int hv;       // hdv
+    const float* u;
+    int64_t ldu;
+    const float* attn;
+    int64_t lda;
+    const float* w;
+    const float* bias;
+    const float* xres;
+    int64_t ldx;
+    float eps, p;
+    uint64_t seed;
+    const int64_t* seed_off;
+    float2* a_stats;
+    float* o_in;
+    float* y;
+    int64_t ldy;
+    __amdgpu_buffer_rsrc_t ru, ra, rx, ro, ry, rb;
+    uint64_t seed_eff;
+    struct Src { f4 v[KGH]; f4 uu[KGH]; };
+    __device__ int bks() const { return 1; }
+    __device__ int bns() const { return K; }
+    __device__ void setup(int64_t total) {
+      ru = mat_rsrc(u, ldu, total, 0);
+      ra = mat_rsrc(attn, lda, total, 0);
+      rx = mat_rsrc(xres ? xres : y, ldx, xres ? total : 0, 0);
+      ro = mat_rsrc(o_in ? o_in : y, 3 * hv, o_in ? total : 0, 0);
+      ry = mat_rsrc(y, ldy, total, 0);
+      rb = mat_rsrc(bias ? bias : y, N, bias ? 1 : 0, 0);
+      seed_eff = seed + (seed_off ? (uint64_t)*seed_off : 0ull);
+    }
+    __device__ void load(Src& s, int64_t m, int lg) const {
+#pragma unroll
+      for (int g = 0; g < KGH; ++g) {
+        s.v[g] = ldq<VEC>(ra, m * lda, 16 * g, lg, hv);
+        s.uu[g] = ldq<VEC>(ru, m * ldu, 16 * g, lg, hv);
+      }
+    }
+    __device__ void prep(const Src& s, float (&a)[KG][4], int64_t m, bool row_ok, int lg) const {
+      float sum = 0.f;
+#pragma unroll
+      for (int g = 0; g < KGH; ++g)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sum += s.v[g][e];
+      const float mean = row4_sum(sum) * (1.f / (float)hv);
+      float sq = 0.f;
+#pragma unroll
+      for (int g = 0; g < KGH; ++g)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float d = qcol<VEC>(16 * g, lg, e) < hv ? s.v[g][e] - mean : 0.f;
+          sq += d * d;
+        }
+      const float rstd = rsqrtf(row4_sum(sq) * (1.f / (float)hv) + eps);
+#pragma unroll
+      for (int seg = 0; seg < 3; ++seg)
+#pragma unroll
+        for (int g = 0; g < KGH; ++g) {
+          f4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int c = qcol<VEC>(16 * g, lg, e);
+            const float ln = (s.v[g][e] - mean) * rstd;
+            float v = seg == 0 ? s.uu[g][e] : (seg == 1 ? ln : s.uu[g][e] * ln);
+            if (p > 0.f) v *= rw_dropout_keep(seed_eff, m, seg * hv + c, 3 * hv, p);
+            a[seg * KGH + g][e] = c < hv ? v : 0.f;
+            o[e] = a[seg * KGH + g][e];
+          }
+          stq<VEC>(ro, m * 3 * hv + seg * hv, 16 * g, lg, hv, o);  // records = 0 when o_in is NULL
+        }
+      if (lg == 0 && row_ok) a_stats[m] = make_float2(mean, rstd);
+    }
+    struct Epi { f4 xv[NT_], bv[NT_]; };
+    __device__ void epi_load(Epi& es, int64_t m, bool, int lg) const {
+#pragma unroll
+      for (int t = 0; t < NT_; ++t) {
+        es.xv[t] = ldq<VEC>(rx, m * ldx, 16 * t, lg, N);
+        es.bv[t] = ldq<VEC>(rb, 0, 16 * t, lg, N);
+      }
+    }
+    __device__ void epi(f4 (&acc)[NT_], const Epi& es, int64_t m, bool, int lg) const {
+#pragma unroll
+      for (int t = 0; t < NT_; ++t) {
+        f4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = (acc[t][e] + es.bv[t][e]) + es.xv[t][e];
+        stq<VEC>(ry, m * ldy, 16 * t, lg, N, o);
+      }
+    }
+  };
+};
+
+// B1 with concat_ua: g = dy @ W' (rows, 3 hvp); per column c of the hdv-wide segments
+// g1, g2, g3 (dropout bwd), du = g1 + g3 * a (* silu'(h_u)), da = g2 + g3 * u,
+// d_attn = LayerNorm_bwd(attn; da).
+template <int KGH, int KG_, int VEC_>
+struct RwGateOCatBwdT {
+  template <int KG, int NT, int V_>
+  struct Op {
+    static_assert(NT == 3 * KGH, "NT = 3 segments of KGH tiles");
+    static constexpr int VEC = V_;
+    static constexpr bool K_CONTIG = false;
+    const int64_t* offsets;
+    int B, K, N;  // K = D, N = 3 hvp
+    int hv;
+    const float* dy;
+    int64_t lddy;
+    const float* w;
+    const float* u;
+    int64_t ldu;
+    const float* attn;
+    int64_t lda;
+    const float2* a_stats;
+    const float* h_u;
+    int64_t ldh;
+    float p;
+    uint64_t seed;
+    const int64_t* seed_off;
+    float* du;
+    int64_t lddu;
+    float* da;
+    int64_t ldda;
+    __amdgpu_buffer_rsrc_t rdy, ru, ra, rh, rdu, rda;
+    uint64_t seed_eff;
+    struct Src { f4 v[KG]; };
+    __device__ int bks() const { return N; }
+    __device__ int bns() const { return 1; }
+    __device__ void setup(int64_t total) {
+      rdy = mat_rsrc(dy, lddy, total, 0);
+      ru = mat_rsrc(u, ldu, total, 0);
+      ra = mat_rsrc(attn, lda, total, 0);
+      rh = mat_rsrc(h_u ? h_u : u, ldh, h_u ? total : 0, 0);
+      rdu = mat_rsrc(du, lddu, total, 0);
+      rda = mat_rsrc(da, ldda, total, 0);
+      seed_eff = seed + (seed_off ? (uint64_t)*seed_off : 0ull);
+    }
+    __device__ void load(Src& s, int64_t m, int lg) const {
+#pragma unroll
+      for (int g = 0; g < KG; ++g) s.v[g] = ldq<VEC>(rdy, m * lddy, 16 * g, lg, K);
+    }
+    __device__ void prep(const Src& s, float (&a)[KG][4], int64_t, bool, int) const {
+#pragma unroll
+      for (int g = 0; g < KG; ++g)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) a[g][e] = s.v[g][e];
+    }
+    struct Epi { float2 st; f4 av[KGH], uv[KGH], hv_[KGH]; };
+    __device__ void epi_load(Epi& es, int64_t m, bool row_ok, int lg) const {
+      es.st = ld_f2(a_stats, row_ok ? m : 0);
+#pragma unroll
+      for (int t = 0; t < KGH; ++t) {
+        es.av[t] = ldq<VEC>(ra, m * lda, 16 * t, lg, hv);
+        es.uv[t] = ldq<VEC>(ru, m * ldu, 16 * t, lg, hv);
+        es.hv_[t] = ldq<VEC>(rh, m * ldh, 16 * t, lg, hv);
+      }
+    }
+    __device__ void epi(f4 (&acc)[NT], const Epi& es, int64_t m, bool row_ok, int lg) const {
+      const float2 st = es.st;
+      float s1 = 0.f, s2 = 0.f;
+      f4 lnv[KGH], dln[KGH];
+#pragma unroll
+      for (int t = 0; t < KGH; ++t) {
+        f4 duv;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = qcol<VEC>(16 * t, lg, e);
+          const bool ok = row_ok && c < hv;
+          float g1 = acc[t][e], g2 = acc[KGH + t][e], g3 = acc[2 * KGH + t][e];
+          if (p > 0.f) {
+            g1 *= rw_dropout_keep(seed_eff, m, c, 3 * hv, p);
+            g2 *= rw_dropout_keep(seed_eff, m, hv + c, 3 * hv, p);
+            g3 *= rw_dropout_keep(seed_eff, m, 2 * hv + c, 3 * hv, p);
+          }
+          const float ln = (es.av[t][e] - st.x) * st.y;
+          float dd = g1 + g3 * ln;
+          if (h_u) dd *= silu_grad_(es.hv_[t][e]);
+          duv[e] = dd;
+          lnv[t][e] = ok ? ln : 0.f;
+          dln[t][e] = ok ? g2 + g3 * es.uv[t][e] : 0.f;
+          s1 += dln[t][e];
+          s2 += dln[t][e] * lnv[t][e];
+        }
+        stq<VEC>(rdu, m * lddu, 16 * t, lg, hv, duv);
+      }
+      s1 = row4_sum(s1);
+      s2 = row4_sum(s2);
+      const float inv = 1.f / (float)hv;
+      const float mean1 = s1 * inv, mean2 = s2 * inv;
+#pragma unroll
+      for (int t = 0; t < KGH; ++t) {
+        f4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = st.y * (dln[t][e] - mean1 - lnv[t][e] * mean2);
+        stq<VEC>(rda, m * ldda, 16 * t, lg, hv, o);
+      }
+    }
+  };
+};
+
 // B3: dn = dh @ W_uvqk^T (rows, D), W'(k, n) = W_uvqk[n][k]; epilogue: dx = dy + LN_bwd(x; dn).
 template <int KG, int NT, int VEC_>
 struct RwLnUvqkBwd {

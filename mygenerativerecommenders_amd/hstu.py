@@ -7,12 +7,15 @@ Same constructor arguments, parameter names / shapes / initialisation and
 state-dict keys as the reference (``hstu.py:71-128, 208-672``), so checkpoints
 round-trip.  The compute is the fused jagged path: per layer 3 launches forward
 (LN+UVQK+SiLU GEMM, attention with in-kernel relative bias, gate+LN+O GEMM+residual)
-and 6 backward; nothing of size (B, N, N) is materialised.
+and 5 backward; nothing of size (B, N, N) is materialised.  ``concat_ua=True``
+(hstu.py:398-400) runs the concatenated gate [u, LN(a), u*LN(a)] in the same fused
+kernels (linear_dim * num_heads <= 64).  ``autocast_dtype=torch.bfloat16`` (an extension
+of the reference constructor, whose HSTUJagged takes it) selects bf16 attention operands.
 
 Not supported (raise): the incremental-decoding cache path (``delta_x_offsets`` /
 ``cache``, hstu.py:293-298, 415-418 — used by no config), ``normalization=
-"softmax_rel_bias"`` (hstu.py:341-389 — used by no config), ``concat_ua=True``
-(hstu.py:398-400) and attention dropout > 0 (the reference ignores it too).
+"softmax_rel_bias"`` (hstu.py:341-389 — used by no config) and attention dropout > 0
+(the reference ignores it too).
 """
 from __future__ import annotations
 
@@ -117,6 +120,7 @@ class SequentialTransductionUnitJagged(torch.nn.Module):
         self._dropout_seed = int(torch.randint(0, 2**62, (1,)).item())
         self.register_buffer("_dropout_step", torch.zeros(1, dtype=torch.int64),
                              persistent=False)
+        self._bf16 = False  # set by HSTUJagged from its autocast_dtype
 
     def _geometry(self, n: int, max_len: int) -> ops.STUGeometry:
         if self._linear_activation == "silu":
@@ -129,13 +133,11 @@ class SequentialTransductionUnitJagged(torch.nn.Module):
             if self._normalization == "softmax_rel_bias":
                 raise NotImplementedError("normalization='softmax_rel_bias' is not supported")
             raise ValueError(f"Unknown normalization method {self._normalization}")
-        if self._concat_ua:
-            raise NotImplementedError("concat_ua=True is not supported by the fused kernels")
         return ops.STUGeometry(
             N=n, D=self._embedding_dim, H=self._num_heads, dqk=self._attention_dim,
             dv=self._linear_dim, eps=self._eps, activation=act,
             dropout_p=float(self._dropout_ratio) if self.training else 0.0,
-            max_len=max_len)
+            max_len=max_len, bf16=self._bf16, concat_ua=self._concat_ua)
 
     def forward(
         self,
@@ -187,9 +189,17 @@ class HSTUJagged(torch.nn.Module):
 
     def __init__(self, modules: List[SequentialTransductionUnitJagged],
                  autocast_dtype: Optional[torch.dtype]) -> None:
+        """autocast_dtype (hstu.py:439-480): None / float32 = the reference's fp32 path
+        (HSTU hard-wires None, hstu.py:592); torch.bfloat16 = the opt-in bf16 compute mode:
+        attention MFMA operands (Q, K, V, dO, P, dS) in bf16, fp32 accumulation,
+        elementwise and parameters (projections stay fp32)."""
         super().__init__()
         self._attention_layers = torch.nn.ModuleList(modules=modules)
+        if autocast_dtype not in (None, torch.float32, torch.bfloat16):
+            raise ValueError(f"autocast_dtype must be None, float32 or bfloat16 (got {autocast_dtype})")
         self._autocast_dtype = autocast_dtype
+        for layer in self._attention_layers:
+            layer._bf16 = autocast_dtype is torch.bfloat16
         # one device dropout counter per encoder forward (layers hash with their own seed)
         self.register_buffer("_dropout_step", torch.zeros(1, dtype=torch.int64),
                              persistent=False)
@@ -250,7 +260,11 @@ class HSTU(torch.nn.Module):
         attn_dropout_rate: float,
         enable_relative_attention_bias: bool = True,
         concat_ua: bool = False,
+        autocast_dtype: Optional[torch.dtype] = None,
     ) -> None:
+        """Reference constructor (hstu.py:532-549) plus ``autocast_dtype`` (default None =
+        the reference's hard-wired fp32; torch.bfloat16 = the opt-in bf16 attention mode,
+        see HSTUJagged)."""
         super().__init__()
         self._embedding_dim = embedding_dim
         self._item_embedding_dim = item_embedding_dim
@@ -285,7 +299,7 @@ class HSTU(torch.nn.Module):
                 )
                 for _ in range(num_blocks)
             ],
-            autocast_dtype=None,
+            autocast_dtype=autocast_dtype,
         )
         self.register_buffer(
             "_attn_mask",

@@ -217,10 +217,25 @@ class STUGeometry:
     activation: int     # 1 = silu, 0 = none
     dropout_p: float
     max_len: int        # host bound on sequence lengths (<= N)
+    bf16: bool = False  # attention with bf16 MFMA operands (HSTU autocast_dtype=bfloat16)
+    concat_ua: bool = False  # o_in = [u, LN(a), u * LN(a)] (hstu.py:398-400)
 
     @property
     def n_out(self):
         return 2 * self.H * self.dv + 2 * self.H * self.dqk
+
+
+def _pad_cat_weight(w_o: torch.Tensor, hv: int):
+    """concat_ua: _o.weight (D, 3 hv) -> (D, 3 hvp) with the u / LN(a) / u*LN(a) column
+    blocks at 16-aligned offsets 0, hvp, 2 hvp (the row-wave kernel's k groups)."""
+    hvp = 16 if hv <= 16 else (32 if hv <= 32 else 64)
+    if hv > 64:
+        raise NotImplementedError("concat_ua=True supports linear_dim * num_heads <= 64")
+    D = w_o.shape[0]
+    w = w_o.detach().reshape(D, 3, hv)
+    pad = torch.zeros(D, 3, hvp, dtype=w_o.dtype, device=w_o.device)
+    pad[:, :, :hv] = w
+    return pad.reshape(D, 3 * hvp), hvp
 
 
 class STULayerFunction(torch.autograd.Function):
@@ -254,18 +269,31 @@ class STULayerFunction(torch.autograd.Function):
         v = uvqk[:, hv:2 * hv]
         pos_w_c = pos_w.contiguous() if bmap is not None else None
         ts_w_c = ts_w.contiguous() if bmap is not None else None
-        _lib.call("hstu_attn_fwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out, n_out,
+        _lib.call("hstu_attn_fwd_bf16" if geo.bf16 else "hstu_attn_fwd", q.data_ptr(), k.data_ptr(),
+                  v.data_ptr(), n_out, n_out,
                   offsets.data_ptr(), B, geo.N, geo.max_len, H, dqk, dv, _lib.ptr(bmap),
                   _lib.ptr(pos_w_c), _lib.ptr(ts_w_c), NUM_BUCKETS, attn.data_ptr(), hv, st)
         attn_stats = torch.empty(rows, 2, dtype=torch.float32, device=dev)
         needs_w_grad = w_o.requires_grad or b_o.requires_grad
-        o_in = torch.empty(rows, hv, dtype=torch.float32, device=dev) if needs_w_grad else None
+        ow = 3 * hv if geo.concat_ua else hv  # o_in width
+        o_in = torch.empty(rows, ow, dtype=torch.float32, device=dev) if needs_w_grad else None
+        w_pad = hvp = None
+        if geo.concat_ua:
+            w_pad, hvp = _pad_cat_weight(w_o, hv)
         y = torch.empty(rows, D, dtype=torch.float32, device=dev)
         b_o_c = b_o.contiguous()
-        _lib.call("hstu_gate_o_fwd", uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
-                  offsets.data_ptr(), B, rows, hv, D, w_o.data_ptr(), b_o_c.data_ptr(),
-                  x.data_ptr(), x.stride(0), geo.eps, geo.dropout_p, seed, _lib.ptr(seed_offset),
-                  attn_stats.data_ptr(), _lib.ptr(o_in), y.data_ptr(), D, st)
+        if geo.concat_ua:
+            _lib.call("hstu_gate_o_cat_fwd", uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
+                      offsets.data_ptr(), B, rows, hv, hvp, D, w_pad.data_ptr(), b_o_c.data_ptr(),
+                      x.data_ptr(), x.stride(0), geo.eps, geo.dropout_p, seed,
+                      _lib.ptr(seed_offset), attn_stats.data_ptr(), _lib.ptr(o_in), y.data_ptr(),
+                      D, st)
+        else:
+            _lib.call("hstu_gate_o_fwd", uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
+                      offsets.data_ptr(), B, rows, hv, D, w_o.data_ptr(), b_o_c.data_ptr(),
+                      x.data_ptr(), x.stride(0), geo.eps, geo.dropout_p, seed,
+                      _lib.ptr(seed_offset), attn_stats.data_ptr(), _lib.ptr(o_in), y.data_ptr(),
+                      D, st)
         ctx.save_for_backward(x, offsets, bmap, w_uvqk, w_o, pos_w_c, ts_w_c, x_stats, uvqk,
                               h_pre, attn, attn_stats, o_in)
         ctx.geo = geo
@@ -288,10 +316,18 @@ class STULayerFunction(torch.autograd.Function):
         dy = dy.contiguous()
         d_uvqk = torch.empty(rows, n_out, dtype=torch.float32, device=dev)
         d_attn = torch.empty(rows, hv, dtype=torch.float32, device=dev)
-        _lib.call("hstu_gate_o_bwd", dy.data_ptr(), D, offsets.data_ptr(), B, rows, hv, D,
-                  w_o.data_ptr(), uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
-                  attn_stats.data_ptr(), _lib.ptr(h_pre), n_out, geo.dropout_p, ctx.seed,
-                  _lib.ptr(ctx.seed_offset), d_uvqk.data_ptr(), n_out, d_attn.data_ptr(), hv, st)
+        if geo.concat_ua:
+            w_pad, hvp = _pad_cat_weight(w_o, hv)
+            _lib.call("hstu_gate_o_cat_bwd", dy.data_ptr(), D, offsets.data_ptr(), B, rows, hv, hvp,
+                      D, w_pad.data_ptr(), uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
+                      attn_stats.data_ptr(), _lib.ptr(h_pre), n_out, geo.dropout_p, ctx.seed,
+                      _lib.ptr(ctx.seed_offset), d_uvqk.data_ptr(), n_out, d_attn.data_ptr(), hv,
+                      st)
+        else:
+            _lib.call("hstu_gate_o_bwd", dy.data_ptr(), D, offsets.data_ptr(), B, rows, hv, D,
+                      w_o.data_ptr(), uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
+                      attn_stats.data_ptr(), _lib.ptr(h_pre), n_out, geo.dropout_p, ctx.seed,
+                      _lib.ptr(ctx.seed_offset), d_uvqk.data_ptr(), n_out, d_attn.data_ptr(), hv, st)
         L = _lib.lib()
         d_pos_w = d_ts_w = None
         ws_a = None
@@ -299,7 +335,9 @@ class STULayerFunction(torch.autograd.Function):
         if bmap is not None:
             d_pos_w = torch.empty(2 * geo.N - 1, dtype=torch.float32, device=dev)
             d_ts_w = torch.empty(NUM_BUCKETS + 1, dtype=torch.float32, device=dev)
-            ws_a_n = L.hstu_attn_bwd_workspace_size(B, geo.N, geo.max_len, H, NUM_BUCKETS)
+            ws_a_n = (L.hstu_attn_bwd_bf16_workspace_size(B, geo.N, geo.max_len, H, dqk, dv,
+                                                          NUM_BUCKETS) if geo.bf16 else
+                      L.hstu_attn_bwd_workspace_size(B, geo.N, geo.max_len, H, NUM_BUCKETS))
             ws_a = torch.empty(max(ws_a_n, 4), dtype=torch.uint8, device=dev)
         q = uvqk[:, 2 * hv:2 * hv + hq]
         k = uvqk[:, 2 * hv + hq:]
@@ -313,7 +351,8 @@ class STULayerFunction(torch.autograd.Function):
         dq = d_uvqk[:, 2 * hv:2 * hv + hq]
         dk = d_uvqk[:, 2 * hv + hq:]
         dvv = d_uvqk[:, hv:2 * hv]
-        _lib.call("hstu_attn_bwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out, n_out,
+        _lib.call("hstu_attn_bwd_bf16" if geo.bf16 else "hstu_attn_bwd", q.data_ptr(), k.data_ptr(),
+                  v.data_ptr(), n_out, n_out,
                   d_attn.data_ptr(), hv, offsets.data_ptr(), B, geo.N, geo.max_len, H, dqk, dv,
                   _lib.ptr(bmap), _lib.ptr(pos_w), _lib.ptr(ts_w), NUM_BUCKETS,
                   hq_p, hk_p, hv_p, n_out, dq.data_ptr(), dk.data_ptr(), dvv.data_ptr(), n_out,
@@ -327,15 +366,16 @@ class STULayerFunction(torch.autograd.Function):
         want_uvqk = ctx.needs_input_grad[3]
         d_w_uvqk = torch.empty(D, n_out, dtype=torch.float32, device=dev) if want_uvqk else None
         d_w_o = d_b_o = None
+        ow = o_in.shape[1] if o_in is not None else hv  # 3 hv with concat_ua
         if o_in is not None:
-            d_w_o = torch.empty(D, hv, dtype=torch.float32, device=dev)
+            d_w_o = torch.empty(D, ow, dtype=torch.float32, device=dev)
             d_b_o = torch.empty(D, dtype=torch.float32, device=dev)
         if want_uvqk and o_in is not None:
-            ws_n = L.gr_wgrad2_workspace_size(rows, D, n_out, D, hv)
+            ws_n = L.gr_wgrad2_workspace_size(rows, D, n_out, D, ow)
             ws = torch.empty(max(ws_n, 4), dtype=torch.uint8, device=dev)
             _lib.call("gr_wgrad2", x.data_ptr(), x.stride(0), x_stats.data_ptr(), d_uvqk.data_ptr(),
                       n_out, D, n_out, d_w_uvqk.data_ptr(), None,
-                      dy.data_ptr(), D, None, o_in.data_ptr(), hv, D, hv, d_w_o.data_ptr(),
+                      dy.data_ptr(), D, None, o_in.data_ptr(), ow, D, ow, d_w_o.data_ptr(),
                       d_b_o.data_ptr(), offsets.data_ptr(), B, rows, ws.data_ptr(), ws_n, st)
         elif want_uvqk:
             ws_n = L.gr_wgrad_workspace_size(rows, D, n_out)
@@ -344,10 +384,10 @@ class STULayerFunction(torch.autograd.Function):
                       n_out, offsets.data_ptr(), B, rows, D, n_out, d_w_uvqk.data_ptr(), None,
                       ws.data_ptr(), ws_n, st)
         elif o_in is not None:
-            ws_n = L.gr_wgrad_workspace_size(rows, D, hv)
+            ws_n = L.gr_wgrad_workspace_size(rows, D, ow)
             ws = torch.empty(max(ws_n, 4), dtype=torch.uint8, device=dev)
-            _lib.call("gr_wgrad", dy.data_ptr(), D, None, o_in.data_ptr(), hv, offsets.data_ptr(),
-                      B, rows, D, hv, d_w_o.data_ptr(), d_b_o.data_ptr(), ws.data_ptr(), ws_n, st)
+            _lib.call("gr_wgrad", dy.data_ptr(), D, None, o_in.data_ptr(), ow, offsets.data_ptr(),
+                      B, rows, D, ow, d_w_o.data_ptr(), d_b_o.data_ptr(), ws.data_ptr(), ws_n, st)
         return (dx, None, None, d_w_uvqk, d_w_o, d_b_o, d_pos_w, d_ts_w, None, None, None)
 
 

@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--batch", type=int, default=0, help="override B")
     ap.add_argument("--len", type=int, default=0, help="override L (N = L + 11)")
     ap.add_argument("--nobias", action="store_true", help="no relative bias (timestamps absent)")
+    ap.add_argument("--bf16", action="store_true", help="bf16-operand kernels")
     ap.add_argument("--hepi", action="store_true",
                     help="fused silu'(h) epilogue on dQ/dK/dV (as in the training step)")
     args = ap.parse_args()
@@ -67,7 +68,8 @@ def main():
     dpw = torch.empty_like(pos_w)
     dtw = torch.empty_like(ts_w)
     L_ = _lib.lib()
-    ws_n = L_.hstu_attn_bwd_workspace_size(B, N, L, H, 128)
+    ws_n = (L_.hstu_attn_bwd_bf16_workspace_size(B, N, L, H, d, d, 128) if args.bf16
+            else L_.hstu_attn_bwd_workspace_size(B, N, L, H, 128))
     ws = torch.empty(max(ws_n, 4), dtype=torch.uint8, device=dev)
     st = _lib.stream_handle()
 
@@ -75,7 +77,7 @@ def main():
         bmap = None
 
     def fwd():
-        _lib.call("hstu_attn_fwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out, n_out,
+        _lib.call("hstu_attn_fwd_bf16" if args.bf16 else "hstu_attn_fwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out, n_out,
                   offsets.data_ptr(), B, N, L, H, d, d, _lib.ptr(bmap), pos_w.data_ptr(),
                   ts_w.data_ptr(), 128, out.data_ptr(), hv, st)
 
@@ -85,7 +87,7 @@ def main():
     hvp = h[:, hv:2 * hv].data_ptr() if args.hepi else None
 
     def bwd():
-        _lib.call("hstu_attn_bwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out, n_out,
+        _lib.call("hstu_attn_bwd_bf16" if args.bf16 else "hstu_attn_bwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out, n_out,
                   dout.data_ptr(), hv, offsets.data_ptr(), B, N, L, H, d, d, _lib.ptr(bmap),
                   pos_w.data_ptr(), ts_w.data_ptr(), 128, hq, hk, hvp, n_out if args.hepi else 0,
                   dq.data_ptr(), dk.data_ptr(), dvv.data_ptr(), n_out, dpw.data_ptr(),
@@ -113,7 +115,7 @@ def main():
         avg = tot / n
         res[name] = {"avg_us": round(avg * 1e3, 2),
                      "tflops": round(fl.get(name, 0) / (avg * 1e-3) / 1e12, 2) if name in fl else None}
-    print(json.dumps({"shape": args.shape, "B": B, "N": N, "L": L, "d": d, "H": H,
+    print(json.dumps({"shape": args.shape, "bf16": args.bf16, "B": B, "N": N, "L": L, "d": d, "H": H,
                       "kernels": res}))
 
 

@@ -1,0 +1,8 @@
+set -e
+cd $GRAFT_REPO_ROOT
+timeout -k 10 300 python -u -m pytest tests/test_gpu_attention.py tests/test_gpu_hstu.py -x -q -s -k bf16 --timeout 200 --timeout-method thread > gpurun_out/r2k_tests.log 2>&1
+for sh in c2 c3; do
+  timeout -k 5 90 python scripts/attn_micro.py --shape $sh --only bwd --hepi --iters 10 >> gpurun_out/r2k_micro.jsonl
+  timeout -k 5 90 python scripts/attn_micro.py --shape $sh --only bwd --hepi --iters 10 --bf16 >> gpurun_out/r2k_micro.jsonl
+done
+timeout -k 10 300 python bench.py --no-retrieval-leg --no-cpu-baseline --e2e-steps 0 --sweep "" > gpurun_out/r2k_bench.json 2> gpurun_out/r2k_bench.err

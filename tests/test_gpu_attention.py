@@ -36,7 +36,7 @@ def _case(seed, B, N, H, dqk, dv, lengths=None, with_ts=True, scale=1.0):
     return lengths, offsets, uvqk, ts, pos_w, ts_w
 
 
-def _run_gpu_fwd(offsets, uvqk, ts, pos_w, ts_w, B, N, H, dqk, dv):
+def _run_gpu_fwd(offsets, uvqk, ts, pos_w, ts_w, B, N, H, dqk, dv, entry="hstu_attn_fwd"):
     from mygenerativerecommenders_amd import _lib
     dev = torch.device("cuda")
     u = uvqk.to(dev)
@@ -53,7 +53,7 @@ def _run_gpu_fwd(offsets, uvqk, ts, pos_w, ts_w, B, N, H, dqk, dv):
     max_len = int((offsets[1:] - offsets[:-1]).max()) if B else 0
     from mygenerativerecommenders_amd import ops
     bmap = ops.bucket_map(tsd, offs, N) if tsd is not None else None
-    _lib.call("hstu_attn_fwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), u.stride(0), u.stride(0),
+    _lib.call(entry, q.data_ptr(), k.data_ptr(), v.data_ptr(), u.stride(0), u.stride(0),
               offs.data_ptr(), B, N, max_len, H, dqk, dv, _lib.ptr(bmap), pw.data_ptr(),
               tw.data_ptr(), 128, out.data_ptr(), out.stride(0), _lib.stream_handle())
     torch.cuda.synchronize()
@@ -97,7 +97,7 @@ def test_attn_fwd_full_length_and_len1():
     assert (got - ref).abs().max().item() <= 2e-5 * (1 + ref.abs().max().item())
 
 
-def _run_gpu_bwd(offsets, uvqk, dout, ts, pos_w, ts_w, B, N, H, dqk, dv, hpre=None):
+def _run_gpu_bwd(offsets, uvqk, dout, ts, pos_w, ts_w, B, N, H, dqk, dv, hpre=None, bf16=False):
     from mygenerativerecommenders_amd import _lib
     dev = torch.device("cuda")
     u = uvqk.to(dev)
@@ -115,7 +115,8 @@ def _run_gpu_bwd(offsets, uvqk, dout, ts, pos_w, ts_w, B, N, H, dqk, dv, hpre=No
     dtw = torch.full_like(tw, float("nan"))
     max_len = int((offsets[1:] - offsets[:-1]).max()) if B else 0
     L = _lib.lib()
-    ws_bytes = L.hstu_attn_bwd_workspace_size(B, N, max_len, H, 128)
+    ws_bytes = (L.hstu_attn_bwd_bf16_workspace_size(B, N, max_len, H, dqk, dv, 128) if bf16
+                else L.hstu_attn_bwd_workspace_size(B, N, max_len, H, 128))
     del thr
     ws = torch.empty(max(ws_bytes, 4), dtype=torch.uint8, device=dev)
     hd = hpre.to(dev) if hpre is not None else None
@@ -124,8 +125,8 @@ def _run_gpu_bwd(offsets, uvqk, dout, ts, pos_w, ts_w, B, N, H, dqk, dv, hpre=No
     hv_p = hd[:, hv:2 * hv].data_ptr() if hd is not None else None
     from mygenerativerecommenders_amd import ops
     bmap = ops.bucket_map(tsd, offs, N) if tsd is not None else None
-    _lib.call("hstu_attn_bwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), u.stride(0), u.stride(0),
-              do.data_ptr(), do.stride(0), offs.data_ptr(), B, N, max_len, H, dqk, dv,
+    _lib.call("hstu_attn_bwd_bf16" if bf16 else "hstu_attn_bwd", q.data_ptr(), k.data_ptr(),
+              v.data_ptr(), u.stride(0), u.stride(0), do.data_ptr(), do.stride(0), offs.data_ptr(), B, N, max_len, H, dqk, dv,
               _lib.ptr(bmap), pw.data_ptr(), tw.data_ptr(), 128,
               hq_p, hk_p, hv_p, u.stride(0) if hd is not None else 0,
               dq.data_ptr(), dk.data_ptr(), dvv.data_ptr(), d.stride(0),
@@ -250,3 +251,106 @@ def test_bucket_map_vs_reference_semantics():
                 assert qk[b, t, i % 64, jj % 64] == int(ref[jj]), (b, i, jj)
                 assert kq[b, t, jj % 64, i % 64] == int(ref[jj]), (b, i, jj)
             del j
+
+
+# ---------------------------------------------------------------- bf16 compute mode
+# hstu_attn_fwd_bf16: Q, K, V and P rounded to bf16 (MFMA operands), fp32 accumulation,
+# fp32 bias / silu / output.  Tolerance: max abs error <= 1.5e-2 * (1 + max|ref|) against
+# the fp32 oracle (bf16 keeps 8 mantissa bits: ~2^-9 relative per operand, and the
+# output sums up to N of them).
+
+BF16_FWD_TOL = 1.5e-2
+
+
+@pytest.mark.parametrize("B,N,H,dqk,dv,with_ts", [
+    (4, 43, 1, 16, 16, True),
+    (4, 43, 1, 50, 50, True),
+    (3, 75, 2, 25, 25, True),
+    (2, 211, 1, 50, 50, True),      # C2 head
+    (3, 130, 2, 8, 8, False),
+    (2, 150, 1, 64, 64, True),
+    (2, 100, 1, 128, 96, True),
+    (2, 150, 1, 256, 256, True),    # C3 head
+    (2, 90, 1, 200, 136, True),
+    (2, 70, 2, 160, 160, False),
+    (2, 2059, 1, 256, 256, True),   # C3 length
+])
+def test_attn_fwd_bf16_vs_oracle(B, N, H, dqk, dv, with_ts):
+    lengths, offsets, uvqk, ts, pos_w, ts_w = _case(B * 7 + N, B, N, H, dqk, dv,
+                                                      with_ts=with_ts)
+    hv, hq = H * dv, H * dqk
+    q = uvqk[:, 2 * hv:2 * hv + hq]
+    k = uvqk[:, 2 * hv + hq:]
+    v = uvqk[:, hv:2 * hv]
+    cfg = O.HSTUConfig(N=N, D=1, H=H, dqk=dqk, dv=dv)
+    ref = O.hstu_attention_jagged(q, k, v, offsets, ts, cfg, pos_w, ts_w, _thr())
+    got = _run_gpu_fwd(offsets, uvqk, ts, pos_w, ts_w, B, N, H, dqk, dv,
+                       entry="hstu_attn_fwd_bf16")
+    assert torch.isfinite(got).all()
+    err = (got - ref).abs().max().item()
+    scale = 1 + ref.abs().max().item()
+    print(f"bf16 fwd rel err {err / scale:.3e}")
+    assert err <= BF16_FWD_TOL * scale
+    # and it is genuinely the reduced-precision path (not the fp32 kernel)
+    assert err > 0
+
+
+# hstu_attn_bwd_bf16: bf16 MFMA operands (Q, K, V, dO, P, dS), fp32 accumulation and
+# elementwise; the bias gradients sum fp32 dS.  Tolerance: max abs error
+# <= 2e-2 * (1 + max|ref|) per gradient against the fp32 oracle.
+BF16_BWD_TOL = 2e-2
+
+
+@pytest.mark.parametrize("B,N,H,dqk,dv,with_ts", [
+    (4, 43, 1, 16, 16, True),
+    (4, 43, 1, 50, 50, True),
+    (3, 75, 2, 25, 25, True),
+    (2, 211, 1, 50, 50, True),      # C2 head
+    (3, 130, 2, 8, 8, False),
+    (2, 150, 1, 64, 64, True),
+    (2, 100, 1, 128, 96, True),
+    (2, 150, 1, 256, 256, True),    # C3 head (dV / dK split passes)
+    (2, 90, 1, 200, 136, True),
+    (2, 70, 2, 160, 160, False),
+    (2, 2059, 1, 256, 256, True),   # C3 length
+])
+def test_attn_bwd_bf16_vs_oracle(B, N, H, dqk, dv, with_ts):
+    lengths, offsets, uvqk, ts, pos_w, ts_w = _case(B * 11 + N, B, N, H, dqk, dv,
+                                                      with_ts=with_ts)
+    hv, hq = H * dv, H * dqk
+    uv = uvqk.clone().requires_grad_(True)
+    pw = pos_w.clone().requires_grad_(True)
+    tw = ts_w.clone().requires_grad_(True)
+    q, k, v = uv[:, 2 * hv:2 * hv + hq], uv[:, 2 * hv + hq:], uv[:, hv:2 * hv]
+    cfg = O.HSTUConfig(N=N, D=1, H=H, dqk=dqk, dv=dv)
+    ref = O.hstu_attention_jagged(q, k, v, offsets, ts, cfg, pw, tw, _thr())
+    g = torch.Generator().manual_seed(99)
+    dout = torch.randn(ref.shape, generator=g)
+    (ref * dout).sum().backward()
+    gq, gk, gv = (uv.grad[:, 2 * hv:2 * hv + hq], uv.grad[:, 2 * hv + hq:],
+                  uv.grad[:, hv:2 * hv])
+    dq, dk, dvv, dpw, dtw = _run_gpu_bwd(offsets, uvqk, dout, ts, pos_w, ts_w, B, N, H, dqk, dv,
+                                         bf16=True)
+    pairs = [("dq", dq, gq), ("dk", dk, gk), ("dv", dvv, gv)]
+    if with_ts:
+        pairs += [("dpos", dpw, pw.grad), ("dts", dtw, tw.grad)]
+    for name, got, want in pairs:
+        err = (got - want).abs().max().item() / (1 + want.abs().max().item())
+        print(f"bf16 bwd {name} rel err {err:.3e}")
+        _close(got, want, rel=BF16_BWD_TOL)
+
+
+def test_attn_bwd_bf16_fused_silu_grad():
+    B, N, H, d = 3, 75, 1, 32
+    lengths, offsets, uvqk, ts, pos_w, ts_w = _case(17, B, N, H, d, d)
+    g = torch.Generator().manual_seed(5)
+    hpre = torch.randn(uvqk.shape, generator=g)
+    dout = torch.randn(uvqk.shape[0], H * d, generator=g)
+    a = _run_gpu_bwd(offsets, uvqk, dout, ts, pos_w, ts_w, B, N, H, d, d, bf16=True)
+    b = _run_gpu_bwd(offsets, uvqk, dout, ts, pos_w, ts_w, B, N, H, d, d, hpre=hpre, bf16=True)
+    s = torch.sigmoid(hpre)
+    sg = s * (1 + hpre * (1 - s))
+    hv = H * d
+    for x, y, sl in ((a[0], b[0], slice(2 * hv, 3 * hv)), (a[1], b[1], slice(3 * hv, 4 * hv)),
+                     (a[2], b[2], slice(hv, 2 * hv))):
+        assert torch.allclose(y, x * sg[:, sl], rtol=1e-5, atol=1e-6)

@@ -49,13 +49,7 @@ CASES = sorted(os.path.basename(p)[5:-4] for p in glob.glob(os.path.join(GOLDEN,
 @pytest.mark.parametrize("name", CASES)
 def test_hstu_vs_reference_golden(name):
     d = np.load(os.path.join(GOLDEN, f"hstu_{name}.npz"))
-    if int(d["concat_ua"]):
-        with pytest.raises(NotImplementedError):
-            enc = _build(d).cuda().eval()
-            x = torch.tensor(d["x"]).cuda()
-            enc(torch.tensor(d["lengths"]).cuda(), x, None, {})
-        return
-    enc = _build(d).cuda().eval()
+    enc = _build(d).cuda().eval()  # concat_ua cases run the concatenated-gate kernels
     x = torch.tensor(d["x"]).cuda().requires_grad_(True)
     lengths = torch.tensor(d["lengths"]).cuda()
     payload = {"timestamps": torch.tensor(d["ts"]).cuda()} if int(d["with_ts"]) else {}
@@ -168,3 +162,133 @@ def test_hstu_train_mode_dropout_statistics():
     torch.cuda.synchronize()
     assert ((o_in2 != 0) != kept).float().mean().item() > 0.2
     del ops
+
+
+@pytest.mark.parametrize("B,N0,out_len,D,blocks,min_len", [
+    (8, 200, 11, 50, 4, 20),       # C2 geometry
+    (2, 2048, 11, 256, 2, 700),    # C3 geometry
+])
+def test_hstu_bf16_mode_vs_oracle(B, N0, out_len, D, blocks, min_len):
+    """autocast_dtype=torch.bfloat16: attention operands in bf16 (fp32 accumulation),
+    projections / LN / parameters fp32.  Stated tolerance against the fp32 oracle:
+    outputs max abs err <= 2e-2 * (1 + max|ref|), input and parameter gradients
+    <= 5e-2 * (1 + max|ref|)."""
+    from mygenerativerecommenders_amd.hstu import HSTU
+    torch.manual_seed(0)
+    N = N0 + out_len
+    enc = HSTU(max_sequence_len=N0, max_output_len=out_len, embedding_dim=D,
+               item_embedding_dim=D, num_blocks=blocks, num_heads=1, linear_dim=D,
+               attention_dim=D, normalization="rel_bias", linear_config="uvqk",
+               linear_activation="silu", linear_dropout_rate=0.2, attn_dropout_rate=0.0,
+               autocast_dtype=torch.bfloat16)
+    g = torch.Generator().manual_seed(1)
+    with torch.no_grad():
+        for layer in enc._hstu._attention_layers:
+            layer._rel_attn_bias._ts_w.normal_(0, 0.3, generator=g)
+            layer._rel_attn_bias._pos_w.normal_(0, 0.3, generator=g)
+    enc.eval()
+    lengths = torch.randint(min_len, N0 + 1, (B,), generator=g)
+    x = torch.randn(B, N, D, generator=g)
+    ts = torch.zeros(B, N, dtype=torch.int64)
+    for b in range(B):
+        L = int(lengths[b])
+        ts[b, :L + 1] = 1_000_000_000 + torch.cumsum((torch.rand(L + 1, generator=g) * 2e5).long(), 0)
+    thr = np.asarray(__import__("mygenerativerecommenders_amd.bucket_table",
+                                fromlist=["x"]).BUCKET_THRESHOLDS)
+    cfg = O.HSTUConfig(N=N, D=D, H=1, dqk=D, dv=D)
+    st = {k: v.detach().clone().requires_grad_(True) for k, v in enc.state_dict().items()
+          if k != "_attn_mask"}
+    layers = [O.layer_params_from_state(st, i) for i in range(blocks)]
+    xr = x.clone().requires_grad_(True)
+    yr = O.hstu_forward(lengths, xr, ts, cfg, layers, thr)
+    dy = torch.randn(yr.shape, generator=g)
+    (yr * dy).sum().backward()
+    enc = enc.cuda()
+    xg = x.cuda().requires_grad_(True)
+    y, _ = enc(lengths.cuda(), xg, None, {"timestamps": ts.cuda()})
+    (y * dy.cuda()).sum().backward()
+
+    def rel(got, ref):
+        return (got.detach().cpu() - ref).abs().max().item() / (1 + ref.abs().max().item())
+
+    ey = rel(y, yr)
+    print(f"bf16 encoder y rel err {ey:.3e}")
+    assert 0 < ey <= 2e-2
+    assert rel(xg.grad, xr.grad) <= 5e-2
+    for pname, p in enc.named_parameters():
+        e = rel(p.grad, st[pname].grad)
+        print(f"bf16 encoder grad {pname} rel err {e:.3e}")
+        assert e <= 5e-2, pname
+
+
+@pytest.mark.parametrize("D,dh,H", [(50, 50, 1), (32, 16, 2), (64, 64, 1)])
+def test_hstu_concat_ua_vs_oracle(D, dh, H):
+    """concat_ua=True at ml-1m-like widths (ragged lengths, relative bias) against the
+    oracle (fp32 tolerances as above)."""
+    from mygenerativerecommenders_amd.hstu import HSTU
+    torch.manual_seed(0)
+    B, N0, out_len, blocks = 6, 120, 11, 2
+    N = N0 + out_len
+    enc = HSTU(max_sequence_len=N0, max_output_len=out_len, embedding_dim=D,
+               item_embedding_dim=D, num_blocks=blocks, num_heads=H, linear_dim=dh,
+               attention_dim=dh, normalization="rel_bias", linear_config="uvqk",
+               linear_activation="silu", linear_dropout_rate=0.2, attn_dropout_rate=0.0,
+               concat_ua=True).eval()
+    g = torch.Generator().manual_seed(1)
+    lengths = torch.randint(10, N0 + 1, (B,), generator=g)
+    x = torch.randn(B, N, D, generator=g)
+    ts = torch.zeros(B, N, dtype=torch.int64)
+    for b in range(B):
+        L = int(lengths[b])
+        ts[b, :L + 1] = 1_000_000_000 + torch.cumsum((torch.rand(L + 1, generator=g) * 2e5).long(), 0)
+    thr = np.asarray(__import__("mygenerativerecommenders_amd.bucket_table",
+                                fromlist=["x"]).BUCKET_THRESHOLDS)
+    cfg = O.HSTUConfig(N=N, D=D, H=H, dqk=dh, dv=dh, concat_ua=True)
+    st = {k: v.detach().clone().requires_grad_(True) for k, v in enc.state_dict().items()
+          if k != "_attn_mask"}
+    layers = [O.layer_params_from_state(st, i) for i in range(blocks)]
+    xr = x.clone().requires_grad_(True)
+    yr = O.hstu_forward(lengths, xr, ts, cfg, layers, thr)
+    dy = torch.randn(yr.shape, generator=g)
+    (yr * dy).sum().backward()
+    enc = enc.cuda()
+    xg = x.cuda().requires_grad_(True)
+    y, _ = enc(lengths.cuda(), xg, None, {"timestamps": ts.cuda()})
+    _close(y, yr, 3e-5, "y")
+    (y * dy.cuda()).sum().backward()
+    _close(xg.grad, xr.grad, 2e-4, "dx")
+    for pname, p in enc.named_parameters():
+        _close(p.grad, st[pname].grad, 2e-4, "grad " + pname)
+
+
+def test_hstu_concat_ua_train_dropout_regenerates_mask():
+    """Train mode with dropout: d(sum(y * dy)) / dx from the kernels equals a finite
+    difference along a random direction (the backward regenerates the forward's
+    3 hdv-wide o_in mask from the same counter)."""
+    from mygenerativerecommenders_amd.hstu import HSTU
+    torch.manual_seed(4)
+    B, N0, out_len, D = 3, 40, 5, 32
+    N = N0 + out_len
+    enc = HSTU(max_sequence_len=N0, max_output_len=out_len, embedding_dim=D,
+               item_embedding_dim=D, num_blocks=1, num_heads=1, linear_dim=D, attention_dim=D,
+               normalization="rel_bias", linear_config="uvqk", linear_activation="silu",
+               linear_dropout_rate=0.3, attn_dropout_rate=0.0, concat_ua=True).cuda().train()
+    lengths = torch.tensor([40, 13, 27]).cuda()
+    x = torch.randn(B, N, D, device="cuda", dtype=torch.float64).float()
+    dy = torch.randn(B, N, D, device="cuda")
+    direction = torch.randn(B, N, D, device="cuda")
+    layer = enc._hstu._attention_layers[0]
+    step = layer._dropout_step.clone()
+
+    def f(xx):
+        layer._dropout_step.copy_(step)  # same mask every evaluation
+        y, _ = enc(lengths, xx, None, {})
+        return (y * dy).sum()
+
+    xg = x.clone().requires_grad_(True)
+    f(xg).backward()
+    eps = 1e-2
+    with torch.no_grad():
+        fd = (f(x + eps * direction) - f(x - eps * direction)) / (2 * eps)
+    an = (xg.grad * direction).sum()
+    assert abs(fd.item() - an.item()) <= 2e-2 * (1 + abs(an.item())), (fd.item(), an.item())

@@ -47,9 +47,15 @@ def test_parameter_init_statistics_match_reference():
 def test_unsupported_configurations_raise():
     with pytest.raises(ValueError):
         _hstu(linear_config="uv")
-    enc = _hstu(concat_ua=True)
+    enc = _hstu(concat_ua=True)  # supported: the geometry carries the flag
+    assert enc._hstu._attention_layers[0]._geometry(211, 211).concat_ua
+    enc = _hstu(concat_ua=True, linear_dim=96, attention_dim=96)  # o_in wider than 3 x 64
+    from mygenerativerecommenders_amd import ops
     with pytest.raises(NotImplementedError):
-        enc._hstu._attention_layers[0]._geometry(211, 211)
+        ops._pad_cat_weight(enc._hstu._attention_layers[0]._o.weight, 96)
+    with pytest.raises(ValueError):
+        _hstu(autocast_dtype=torch.float16)
+    assert _hstu(autocast_dtype=torch.bfloat16)._hstu._attention_layers[0]._geometry(211, 211).bf16
     enc = _hstu(normalization="softmax_rel_bias")
     with pytest.raises(NotImplementedError):
         enc._hstu._attention_layers[0]._geometry(211, 211)
