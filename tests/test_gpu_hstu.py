@@ -277,11 +277,11 @@ def test_hstu_concat_ua_train_dropout_regenerates_mask():
     x = torch.randn(B, N, D, device="cuda", dtype=torch.float64).float()
     dy = torch.randn(B, N, D, device="cuda")
     direction = torch.randn(B, N, D, device="cuda")
-    layer = enc._hstu._attention_layers[0]
-    step = layer._dropout_step.clone()
+    counter = enc._hstu._dropout_step  # one device counter per encoder forward
+    step = counter.clone()
 
     def f(xx):
-        layer._dropout_step.copy_(step)  # same mask every evaluation
+        counter.copy_(step)  # the forward bumps it: same mask every evaluation
         y, _ = enc(lengths, xx, None, {})
         return (y * dy).sum()
 
