@@ -321,7 +321,10 @@ def encoder_leg(B, N0, out_len, D, blocks, H, steps, warmup, device, world, seed
                attn_dropout_rate=0.0,
                autocast_dtype=torch.bfloat16 if bf16 else None).to(device).train()
     if muon:
-        reducer = BucketedGradReducer(list(enc.parameters()), overlap=world > 1)
+        # C3/C5: ~10.6 MB of gradients -> 4 MB buckets (3 all-reduces, the first two
+        # overlapping the rest of the backward)
+        reducer = BucketedGradReducer(list(enc.parameters()), bucket_bytes=4 << 20,
+                                      overlap=world > 1)
         eager = eager or world > 1
         opts = muon_adamw_split(enc.named_parameters(),
                                 **({} if eager else {"fused": True, "capturable": True}))
@@ -670,7 +673,7 @@ def main():
         fl = 2.0 * B * (b - a) * D
         xs = b - a
         bf16_filter = (rkern == "mips_filter" and xs >= 262_144 and D <= 64
-                       and not os.environ.get("GR_MIPS_FP32_FILTER"))
+                       and not _lib.get_option("MIPS_FILTER_FP32"))
         if bf16_filter:
             # bound used: HBM, on the bf16 payload of the table (X x D x 2 B) that the
             # filter streams once; the stored copy pads D to 32-dim chunks (padded_bytes)

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GR_HSTU_ABI_VERSION 6
+#define GR_HSTU_ABI_VERSION 7
 
 #ifndef GR_API
 #define GR_API __attribute__((visibility("default")))
@@ -49,6 +49,34 @@ GR_API int gr_version(void);
 GR_API int gr_timing_enable(int on);
 GR_API int gr_timing_query(const char* kernel, double* total_ms, int* launches);
 GR_API int gr_timing_reset(void);
+
+/* Process-wide launch options (the library reads no environment variables).  Set
+ * before the launches they should affect; not while a graph that used them is being
+ * captured.  gr_get_option returns the current value (or -1 for an unknown option).
+ *   GR_OPT_MIPS_FILTER_FP32   0|1  bf16 items table off: the filter pass scores on the
+ *                                  f32 table (slower, exact scores; results identical)
+ *   GR_OPT_MIPS_FILTER_WGS    >=1  filter workgroups per CU per round (default 2)
+ *   GR_OPT_MIPS_FILTER_ROUNDS >=0  filter rounds (0 = chosen from the catalog size)
+ *   GR_OPT_MIPS_FORCE_FALLBACK 0|1 thresholds forced to +inf: every query takes the
+ *                                  exact fallback scan (tests / profiling)
+ *   GR_OPT_ATTN_BWD_SPLIT     0|1  f32 attention backward as separate dK/dV and dQ
+ *                                  launches instead of the fused launch
+ *   GR_OPT_ROWWAVE            0|1  row-wave GEMM kernels (default 1) or the row-panel ones
+ *   GR_OPT_ATTN_BWD_PAIRS     0|1  f32 attention backward: workgroups take causal tile pairs
+ *                                  (p, T-1-p) when that grid fits one round (default 1)
+ */
+enum {
+  GR_OPT_MIPS_FILTER_FP32 = 1,
+  GR_OPT_MIPS_FILTER_WGS = 2,
+  GR_OPT_MIPS_FILTER_ROUNDS = 3,
+  GR_OPT_MIPS_FORCE_FALLBACK = 4,
+  GR_OPT_ATTN_BWD_SPLIT = 5,
+  GR_OPT_ROWWAVE = 6,
+  GR_OPT_ATTN_BWD_PAIRS = 7,
+  GR_OPT_COUNT_ = 8
+};
+GR_API int gr_set_option(int option, int64_t value);
+GR_API int64_t gr_get_option(int option);
 
 /* ---------------------------------------------------------------- jagged layout
  * Replaces utils/ops.py:18-38 asynchronous_complete_cumsum:
@@ -171,7 +199,7 @@ GR_API int hstu_bucket_map(const int64_t* ts, const int64_t* offsets, int B, int
  * q/k rows: (total, H*dqk) with row stride ld_qk; v rows: (total, H*dv), stride ld_v;
  * out: (total, H*dv), stride ld_out.  bucket_map: from hstu_bucket_map, or NULL for
  * NO bias at all (no timestamps, hstu.py:191).  max_len: host upper bound on the
- * sequence lengths (<= N), sizes the grid.  fp32 in / out, f32 MFMA.  dqk, dv <= 128.
+ * sequence lengths (<= N), sizes the grid.  fp32 in / out, f32 MFMA.  dqk, dv <= 256.
  */
 GR_API int hstu_attn_fwd(const float* q, const float* k, const float* v, int64_t ld_qk,
                   int64_t ld_v, const int64_t* offsets, int B, int N, int max_len, int H,

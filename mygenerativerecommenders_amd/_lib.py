@@ -6,6 +6,7 @@ missing, every op raises.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 import re
@@ -102,6 +103,36 @@ KERNEL_NAMES = ("bucket_map", "attn_fwd", "attn_bwd", "attn_bwd_dkv", "attn_bwd_
                 "sampled_softmax_fwd", "sampled_softmax_bwd", "sampled_softmax_csr",
                 "sampled_softmax_table_grad", "preproc", "item_embedding", "mips_sort_invalid",
                 "mips_wide_score", "mips_wide_select")
+
+
+def parse_options(path: str = HEADER_PATH) -> dict:
+    """{"MIPS_FILTER_FP32": 1, ...}: the GR_OPT_* launch options declared in gr_hstu.h."""
+    text = open(path).read()
+    return {m.group(1): int(m.group(2))
+            for m in re.finditer(r"\bGR_OPT_([A-Z0-9_]*[A-Z0-9])\s*=\s*(\d+)", text)}
+
+
+def set_option(name: str, value: int) -> int:
+    """Sets launch option GR_OPT_<name>; returns the previous value."""
+    opt = parse_options()[name]
+    L = lib()
+    old = L.gr_get_option(opt)
+    call("gr_set_option", opt, int(value))
+    return old
+
+
+def get_option(name: str) -> int:
+    return lib().gr_get_option(parse_options()[name])
+
+
+@contextlib.contextmanager
+def option(name: str, value: int):
+    """Scoped launch option (tests, A/B measurements)."""
+    old = set_option(name, value)
+    try:
+        yield
+    finally:
+        set_option(name, old)
 
 
 def timing_enable(on: bool = True):

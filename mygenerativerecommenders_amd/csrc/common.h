@@ -10,11 +10,15 @@
 #include <cstdio>
 #include <string>
 
+#include "../../include/gr_hstu.h"
+
 namespace gr {
 
 // ---------------------------------------------------------------- error plumbing
 void set_error(const char* fmt, ...);
 const char* last_error();
+// Launch option (gr_set_option; GR_OPT_* in gr_hstu.h).
+int64_t option(int which);
 
 #define GR_REQUIRE(cond, ...)                \
   do {                                       \
@@ -163,6 +167,15 @@ inline int device_cus() {
     else
       n = 256;
   }
+  return n;
+}
+
+// Workgroups of `kernel` (256 threads, `lds` dynamic bytes) one CU holds at once.
+template <typename K>
+inline int resident_wgs(K kernel, size_t lds) {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(kernel), 256, lds) != hipSuccess || n < 1)
+    n = 1;
   return n;
 }
 

@@ -422,7 +422,9 @@ constexpr int DIAG = 48;  // per-wave diagonal bins of one 32-query x 16-key chu
 // PART: 0 = dV, dK and the bias gradients in one pass; at the wide heads (d > 128) the
 // accumulators of both do not fit next to the fragments, so PART 1 computes dV (S, P)
 // and PART 2 dK + bias gradients (S, dP, dS): S twice, no spills.
-template <int KC, int VC, int TQ, int WAVES, bool HB, int PART>
+// PRIV: every wave keeps a private dpos_w histogram (short sequences: WAVES x (2N - 1)
+// floats fit LDS) and adds each element directly -- no per-chunk ordered pass.
+template <int KC, int VC, int TQ, int WAVES, bool HB, int PART, bool PRIV>
 __global__ __launch_bounds__(64 * WAVES) void attn_bwd_bf16_dkv_kernel(AttnBwdArgsBf16 a) {
   using C = BwdBf16Cfg<KC, VC, TQ>;
   constexpr bool DO_V = PART != 2, DO_K = PART != 1;
@@ -436,9 +438,9 @@ __global__ __launch_bounds__(64 * WAVES) void attn_bwd_bf16_dkv_kernel(AttnBwdAr
   float* tsw = reinterpret_cast<float*>(Dt + C::VP * C::LDT);
   const int npos = 2 * a.N - 1;
   float* posw = tsw + (a.nb + 1);
-  float* hpos = posw + npos;                     // workgroup dpos histogram [npos]
-  float* diag = hpos + npos;                     // [WAVES][DIAG]
-  float* hts = diag + WAVES * DIAG;              // [WAVES][nb + 1]
+  float* hpos = posw + npos;                     // dpos histogram(s) [PRIV ? WAVES : 1][npos]
+  float* diag = hpos + (PRIV ? WAVES : 1) * npos;  // [WAVES][DIAG] (ordered mode)
+  float* hts = diag + (PRIV ? 0 : WAVES * DIAG);   // [WAVES][nb + 1]
 
   const int BH = a.B * a.H;
   const int id = blockIdx.x;
@@ -460,11 +462,10 @@ __global__ __launch_bounds__(64 * WAVES) void attn_bwd_bf16_dkv_kernel(AttnBwdAr
   }
   if (HB) {
     for (int i = tid; i <= a.nb; i += NTH) tsw[i] = a.ts_w[i];
-    for (int i = tid; i < npos; i += NTH) {
-      posw[i] = a.pos_w[i];
-      hpos[i] = 0.f;
-    }
-    for (int i = tid; i < WAVES * (DIAG + a.nb + 1); i += NTH) diag[i] = 0.f;  // diag + hts
+    for (int i = tid; i < npos; i += NTH) posw[i] = a.pos_w[i];
+    // hpos, diag and hts are contiguous
+    const int nz = (PRIV ? WAVES : 1) * npos + (PRIV ? 0 : WAVES * DIAG) + WAVES * (a.nb + 1);
+    for (int i = tid; i < nz; i += NTH) hpos[i] = 0.f;
   }
   const int wk_lo = k0 + 16 * w;
   const int kj = wk_lo + lr;  // this lane's key
@@ -492,6 +493,7 @@ __global__ __launch_bounds__(64 * WAVES) void attn_bwd_bf16_dkv_kernel(AttnBwdAr
   // dts: per-lane running (bucket, sum), flushed to the wave's histogram on change
   float* whts = hts + w * (a.nb + 1);
   float* wdiag = diag + w * DIAG;
+  float* whpos = hpos + (PRIV ? w * npos : 0);
   int run_b = -1;
   float run_s = 0.f;
 
@@ -564,8 +566,11 @@ __global__ __launch_bounds__(64 * WAVES) void attn_bwd_bf16_dkv_kernel(AttnBwdAr
                 run_s = 0.f;
               }
               run_s += ds[e];
-              // diagonal kj - qi in [wk_lo - qc0 - 31, wk_lo - qc0 + 15]
-              atomicAdd(&wdiag[kj - qi - (wk_lo - qc0 - 31)], ds[e]);
+              if (PRIV) {
+                atomicAdd(&whpos[a.N - 1 + kj - qi], ds[e]);
+              } else {  // diagonal kj - qi in [wk_lo - qc0 - 31, wk_lo - qc0 + 15]
+                atomicAdd(&wdiag[kj - qi - (wk_lo - qc0 - 31)], ds[e]);
+              }
             }
           }
         }
@@ -584,7 +589,7 @@ __global__ __launch_bounds__(64 * WAVES) void attn_bwd_bf16_dkv_kernel(AttnBwdAr
             dK[t] = mfma_bf16(da, trans_frag(Qt + (16 * t + lr) * C::LDT + 32 * j + 4 * lg), dK[t]);
         }
       }
-      if (BIAS) {
+      if (BIAS && !PRIV) {
         // ordered dpos: bins N-1 + (k0 - qc0 - 31) + t, t in [0, 16 WAVES + 47): wave w's
         // diagonal bin u covers t = 16 w + u; thread t adds the waves' bins in order
         __syncthreads();
@@ -640,7 +645,12 @@ __global__ __launch_bounds__(64 * WAVES) void attn_bwd_bf16_dkv_kernel(AttnBwdAr
   if (BIAS) {
     if (run_b >= 0) atomicAdd(&whts[run_b], run_s);
     __syncthreads();
-    for (int i = tid; i < npos; i += NTH) slab[i] = hpos[i];
+    for (int i = tid; i < npos; i += NTH) {
+      float acc = hpos[i];
+      if (PRIV)
+        for (int ww = 1; ww < WAVES; ++ww) acc += hpos[ww * npos + i];  // fixed wave order
+      slab[i] = acc;
+    }
     for (int i = tid; i <= a.nb; i += NTH) {
       float acc = 0.f;
       for (int ww = 0; ww < WAVES; ++ww) acc += hts[ww * (a.nb + 1) + i];
@@ -802,11 +812,15 @@ __global__ __launch_bounds__(256) void attn_bf16_bias_reduce(const float* slabs,
 }
 
 template <int KC, int VC, int TQ, int WAVES>
-static size_t dkv_lds(const AttnBwdArgsBf16& a) {
+static size_t dkv_lds(const AttnBwdArgsBf16& a, bool priv) {
   using C = BwdBf16Cfg<KC, VC, TQ>;
+  const size_t npos = 2 * a.N - 1;
   return 2 * ((size_t)TQ * C::LDK + (size_t)C::KP * C::LDT + (size_t)TQ * C::LDV + (size_t)C::VP * C::LDT) +
-         sizeof(float) * ((a.nb + 1) + 2 * (2 * a.N - 1) + WAVES * (DIAG + a.nb + 1));
+         sizeof(float) * ((a.nb + 1) + npos + (priv ? WAVES * npos : npos + WAVES * DIAG) +
+                          WAVES * (a.nb + 1));
 }
+template <int WAVES>
+static bool dkv_priv(const AttnBwdArgsBf16& a) { return (size_t)WAVES * (2 * a.N - 1) * 4 <= 40 * 1024; }
 template <int KC, int VC, int TK>
 static size_t dq_lds(const AttnBwdArgsBf16& a) {
   using C = BwdBf16Cfg<KC, VC, TK>;
@@ -818,14 +832,19 @@ static size_t bwd_bf16_slab_bytes(int B, int N, int max_len, int H, int nb, int 
   return sizeof(float) * (size_t)ceil_div(max_len, key_tile) * B * H * (size_t)(2 * N - 1 + nb + 1);
 }
 
+template <int KC, int VC, int T, int WAVES, bool HB, bool PRIV>
+static void launch_dkv_bf16_p(const AttnBwdArgsBf16& a, int grid, size_t lds, hipStream_t st) {
+  if constexpr (KC + VC > 8) {  // wide heads: dV and dK + bias as two passes
+    GR_TIMED("attn_bwd_dkv", st, hipLaunchKernelGGL((attn_bwd_bf16_dkv_kernel<KC, VC, T, WAVES, HB, 1, PRIV>), dim3(grid), dim3(64 * WAVES), lds, st, a));
+    GR_TIMED("attn_bwd_dkv", st, hipLaunchKernelGGL((attn_bwd_bf16_dkv_kernel<KC, VC, T, WAVES, HB, 2, PRIV>), dim3(grid), dim3(64 * WAVES), lds, st, a));
+  } else {
+    GR_TIMED("attn_bwd_dkv", st, hipLaunchKernelGGL((attn_bwd_bf16_dkv_kernel<KC, VC, T, WAVES, HB, 0, PRIV>), dim3(grid), dim3(64 * WAVES), lds, st, a));
+  }
+}
 template <int KC, int VC, int T, int WAVES, bool HB>
 static void launch_dkv_bf16(const AttnBwdArgsBf16& a, int grid, size_t lds, hipStream_t st) {
-  if constexpr (KC + VC > 8) {  // wide heads: dV and dK + bias as two passes
-    GR_TIMED("attn_bwd_dkv", st, hipLaunchKernelGGL((attn_bwd_bf16_dkv_kernel<KC, VC, T, WAVES, HB, 1>), dim3(grid), dim3(64 * WAVES), lds, st, a));
-    GR_TIMED("attn_bwd_dkv", st, hipLaunchKernelGGL((attn_bwd_bf16_dkv_kernel<KC, VC, T, WAVES, HB, 2>), dim3(grid), dim3(64 * WAVES), lds, st, a));
-  } else {
-    GR_TIMED("attn_bwd_dkv", st, hipLaunchKernelGGL((attn_bwd_bf16_dkv_kernel<KC, VC, T, WAVES, HB, 0>), dim3(grid), dim3(64 * WAVES), lds, st, a));
-  }
+  if (dkv_priv<WAVES>(a)) launch_dkv_bf16_p<KC, VC, T, WAVES, HB, true>(a, grid, lds, st);
+  else launch_dkv_bf16_p<KC, VC, T, WAVES, HB, false>(a, grid, lds, st);
 }
 
 template <int KC, int VC, int T, int WAVES>
@@ -833,7 +852,7 @@ static int launch_bwd_bf16(AttnBwdArgsBf16 a, float* dpos_w, float* dts_w, hipSt
   a.n_kt = ceil_div(a.max_len, 16 * WAVES);
   a.n_qt = ceil_div(a.max_len, 16 * WAVES);
   const int grid = a.n_kt * a.B * a.H;
-  const size_t l_kv = dkv_lds<KC, VC, T, WAVES>(a), l_q = dq_lds<KC, VC, T>(a);
+  const size_t l_kv = dkv_lds<KC, VC, T, WAVES>(a, dkv_priv<WAVES>(a)), l_q = dq_lds<KC, VC, T>(a);
   GR_REQUIRE(l_kv <= 160 * 1024 && l_q <= 160 * 1024,
              "hstu_attn_bwd_bf16: LDS (%zu, %zu B) exceeds 160 KiB (N=%d)", l_kv, l_q, a.N);
   a.cus = (int64_t)grid <= 2 * device_cus() ? device_cus() : (1 << 30);

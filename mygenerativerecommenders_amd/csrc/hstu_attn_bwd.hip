@@ -43,6 +43,26 @@ __device__ __forceinline__ unsigned long long gr_stamp() {
 #define GR_ST(acc, dep) do { } while (0)
 #endif
 
+#ifdef GR_STAMP
+// Workgroup timeline (diagnostic build): [wg][entry, exit, HW_ID | XCC_ID << 32, kind]
+__device__ unsigned long long gr_tl_buf[1 << 15];
+#define GR_TL_BEGIN() const unsigned long long tl0_ = __builtin_amdgcn_s_memrealtime()
+#define GR_TL_END(slot, kind)                                                              \
+  do {                                                                                   \
+    if (threadIdx.x == 0 && (slot) * 4 + 4 <= (1 << 15)) {                               \
+      const unsigned long long hw_ = __builtin_amdgcn_s_getreg((31 << 11) | 4);          \
+      const unsigned long long xcc_ = __builtin_amdgcn_s_getreg((15 << 11) | 20);        \
+      gr_tl_buf[(slot) * 4 + 0] = tl0_;                                                  \
+      gr_tl_buf[(slot) * 4 + 1] = __builtin_amdgcn_s_memrealtime();                      \
+      gr_tl_buf[(slot) * 4 + 2] = hw_ | (xcc_ << 32);                                    \
+      gr_tl_buf[(slot) * 4 + 3] = (kind);                                                \
+    }                                                                                    \
+  } while (0)
+#else
+#define GR_TL_BEGIN() do { } while (0)
+#define GR_TL_END(slot, kind) do { } while (0)
+#endif
+
 struct AttnBwdArgs {
   const float* q;
   const float* k;
@@ -67,8 +87,10 @@ struct AttnBwdArgs {
   int64_t ld_d;
   float* slabs;  // [grid][2N-1 + nb+1]
   float inv_n;
-  int vec2;  // 8-byte pair staging (aligned rows, even widths)
-  int cus;   // CU count (snake_rank)
+  int vec2;   // 8-byte pair staging (aligned rows, even widths)
+  int cus;    // CU count (snake_rank)
+  int vec2h;  // the same for the hq / hk / hv rows
+  int paired; // workgroups run tile pairs (p, T-1-p); grid = B*H*ceil(T/2) per kind
 };
 
 // TT = rows per streamed LDS tile (queries in dK/dV, keys in dQ): 64, or 16 for the
@@ -116,20 +138,33 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
   const int wbins = npos + GR_DTS_COPIES * tss;  // per wave: dpos bins, dts copies
   float* hist = posw + npos;                   // [4 waves][wbins]
 
+#ifdef GR_STAMP
+  const unsigned long long st_entry = gr_stamp();
+#endif
   const int BH = a.B * a.H;
-  const int rank = snake_rank(id, a.cus);
-  const int kt = rank / BH;  // kt = 0 (the most query tiles) first
-  const int bh = rank % BH;
+  // paired: workgroup (p, bh) runs key tiles p and T-1-p of one sequence (the causal work
+  // of the pair is T+1 tiles for every p, so a one-round grid is balanced); otherwise one
+  // tile per workgroup, heaviest first
+  int kt_a, kt_b = -1, bh;
+  if (a.paired) {
+    kt_a = id / BH;
+    bh = id % BH;
+    kt_b = a.n_tiles - 1 - kt_a;
+    if (kt_b == kt_a) kt_b = -1;
+  } else {
+    const int rank = snake_rank(id, a.cus);
+    kt_a = rank / BH;  // kt = 0 (the most query tiles) first
+    bh = rank % BH;
+  }
   const int b = bh / a.H, h = bh % a.H;
   const int64_t s0 = a.offsets[b];
   const int L = (int)(a.offsets[b + 1] - s0);
-  const int k0 = kt * 64;
   constexpr bool has_bias = HB;  // compile-time: the 4 bias gathers of a lane issue together
   float* slab = a.slabs ? a.slabs + (int64_t)id * nbins : nullptr;
   const int tid = threadIdx.x, w = wave_id(), lane = tid & 63;
   const int lr = lane & 15, lg = lane >> 4;
 
-  if (k0 >= L) {  // this workgroup still owns a (zero) slab
+  if (kt_a * 64 >= L) {  // this workgroup still owns a (zero) slab (kt_b > kt_a: also past L)
     if (has_bias && slab)
       for (int i = tid; i < nbins; i += 256) slab[i] = 0.f;
     return;
@@ -149,12 +184,28 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
   // changes (any order stays correct: every change flushes)
   int run_b = -1;
   float run_s = 0.f;
+  const __amdgpu_buffer_rsrc_t rmap = map_rsrc(a.map_kq, b, attn_tiles_per_seq(a.N));
+  const int map_voff = ((w * 16 + lr) * 16 + lg) * 4;
+  const __amdgpu_buffer_rsrc_t rq = seq_rsrc(a.q, a.ld_qk, s0, h * a.dqk, L, a.dqk);
+  const __amdgpu_buffer_rsrc_t rdo = seq_rsrc(a.dout, a.ld_dout, s0, h * a.dv, L, a.dv);
+  const int last_qt = (L - 1) / TT;
 
+  for (int pass = 0; pass < 2; ++pass) {
+  const int kt = pass == 0 ? kt_a : kt_b;
+  const int k0 = kt * 64;
+  if (pass == 1) {
+    if (kt < 0 || k0 >= L) break;
+    lds_barrier();  // the first pass's epilogue reads of Qs / Ds
+  }
   // this lane's key (as the column of S and dP) and its K^T / V^T fragments
   const int kj = k0 + w * 16 + lr;
   const bool k_ok = kj < L;
+  // TT = 64: the workgroup's 64 key rows are staged through LDS as coalesced tiles
+  // (below); scattered per-lane row loads cost ~12K cycles of address processing when
+  // every workgroup of the launch starts together
+  constexpr bool STAGED = TT == 64;
   float kreg[KSTEPS], vreg[KSTEPS];
-  {
+  if constexpr (!STAGED) {
     const int64_t row = s0 + (k_ok ? kj : L - 1);
     gptr<float> krow = as_global(a.k) + row * a.ld_qk + h * a.dqk;
     gptr<float> vrow = as_global(a.v) + row * a.ld_v + h * a.dv;
@@ -167,11 +218,6 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
       vreg[st] = d < a.dv ? y : 0.f;
     }
   }
-  const __amdgpu_buffer_rsrc_t rmap = map_rsrc(a.map_kq, b, attn_tiles_per_seq(a.N));
-  const int map_voff = ((w * 16 + lr) * 16 + lg) * 4;
-  const __amdgpu_buffer_rsrc_t rq = seq_rsrc(a.q, a.ld_qk, s0, h * a.dqk, L, a.dqk);
-  const __amdgpu_buffer_rsrc_t rdo = seq_rsrc(a.dout, a.ld_dout, s0, h * a.dv, L, a.dv);
-
   f4 dV[VTILES], dK[C::KT];
 #pragma unroll
   for (int t = 0; t < VTILES; ++t) dV[t] = f4_zero();
@@ -190,10 +236,11 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
   };
 
   const int wk_lo = k0 + w * 16;
-  // the epilogue's silu'(h) inputs, loaded now so they land during the main loop (a load
-  // at the end put one more HBM round trip on every workgroup's tail: +16 us per launch)
-  float hv_pre[4][VTILES], hk_pre[4][C::KT];
-  if (a.hv) {
+  // the epilogue's silu'(h) inputs, loaded early so they land during the main loop (a load
+  // at the end put one more HBM round trip on every workgroup's tail: +16 us per launch);
+  // STAGED: as coalesced tiles into the stage registers during the last query tile
+  float hv_pre[4][STAGED ? 1 : VTILES], hk_pre[4][STAGED ? 1 : C::KT];
+  if (!STAGED && a.hv) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int key = wk_lo + 4 * lg + r;
@@ -201,19 +248,34 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
       gptr<float> hvr = as_global(a.hv) + row * a.ld_h + h * a.dv;
       gptr<float> hkr = as_global(a.hk) + row * a.ld_h + h * a.dqk;
 #pragma unroll
-      for (int t = 0; t < VTILES; ++t) {
+      for (int t = 0; t < (STAGED ? 1 : VTILES); ++t) {
         const int c = t * 16 + lr;
         hv_pre[r][t] = hvr[c < a.dv ? c : a.dv - 1];
       }
 #pragma unroll
-      for (int t = 0; t < C::KT; ++t) {
+      for (int t = 0; t < (STAGED ? 1 : C::KT); ++t) {
         const int c = t * 16 + lr;
         hk_pre[r][t] = hkr[c < a.dqk ? c : a.dqk - 1];
       }
     }
   }
-  const int last_qt = (L - 1) / TT;
-  load_tile(k0 / TT, mw);
+  if constexpr (STAGED) {
+    // K / V rows k0 .. k0 + 63 (rows past L and columns past dqk / dv read as 0)
+    qst.load(seq_rsrc(a.k, a.ld_qk, s0, h * a.dqk, L, a.dqk), a.ld_qk, k0, a.dqk, a.vec2);
+    dst.load(seq_rsrc(a.v, a.ld_v, s0, h * a.dv, L, a.dv), a.ld_v, k0, a.dv, a.vec2);
+    qst.store(Qs, C::LDQ, a.vec2);
+    dst.store(Ds, C::LDV, a.vec2);
+    load_tile(k0 / TT, mw);  // the first query tile's loads fly while the fragments are read
+    __syncthreads();
+#pragma unroll
+    for (int st = 0; st < KSTEPS; ++st) {
+      kreg[st] = Qs[(w * 16 + lr) * C::LDQ + 4 * st + lg];
+      vreg[st] = Ds[(w * 16 + lr) * C::LDV + 4 * st + lg];
+    }
+    lds_barrier();
+  } else {
+    load_tile(k0 / TT, mw);
+  }
   qst.store(Qs, C::LDQ, a.vec2);
   dst.store(Ds, C::LDV, a.vec2);
   __syncthreads();
@@ -225,7 +287,12 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
   for (int qt = k0 / TT; qt <= last_qt; ++qt) {
     const int q0 = qt * TT;
     const bool more = qt < last_qt;
-    if (more) load_tile(qt + 1, mwn);
+    if (more) {
+      load_tile(qt + 1, mwn);
+    } else if (STAGED && a.hv) {  // the epilogue's silu'(h) rows of this workgroup's keys
+      qst.load(seq_rsrc(a.hk, a.ld_h, s0, h * a.dqk, L, a.dqk), a.ld_h, k0, a.dqk, a.vec2h);
+      dst.load(seq_rsrc(a.hv, a.ld_h, s0, h * a.dv, L, a.dv), a.ld_h, k0, a.dv, a.vec2h);
+    }
     GR_ST(st_ld, 0);
 #pragma unroll
     for (int qb = 0; qb < C::TB; ++qb) {
@@ -388,8 +455,8 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
   }
 #ifdef GR_STAMP
   if (lane == 0) {
-    const int slot = (id * 4 + w) * 8;
-    if (slot + 8 <= (1 << 16)) {
+    const int slot = (id * 4 + w) * 12;
+    if (slot + 12 <= (1 << 16)) {
       gr_stamp_buf[slot + 0] = st_ld;
       gr_stamp_buf[slot + 1] = st_mm1;
       gr_stamp_buf[slot + 2] = st_ew;
@@ -398,9 +465,16 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
       gr_stamp_buf[slot + 5] = st_sync;
       gr_stamp_buf[slot + 6] = (unsigned long long)kt;
       gr_stamp_buf[slot + 7] = gr_stamp() - st_begin;
+      gr_stamp_buf[slot + 8] = st_begin - st_entry;
     }
   }
 #endif
+  if (STAGED && a.hv) {
+    lds_barrier();
+    qst.store(Qs, C::LDQ, a.vec2h);
+    dst.store(Ds, C::LDV, a.vec2h);
+    lds_barrier();
+  }
   // ---- epilogue: rows = keys wk_lo + 4lg + r, cols = lr + 16 t
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -412,7 +486,10 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
       const int c = t * 16 + lr;
       const bool ok = row_ok && c < a.dv;
       float g = dV[t][r];
-      if (a.hv) g *= ok ? silu_grad_(hv_pre[r][t]) : 0.f;
+      if (a.hv) {
+        const float hp = STAGED ? Ds[(w * 16 + 4 * lg + r) * C::LDV + c] : hv_pre[r][STAGED ? 0 : t];
+        g *= ok ? silu_grad_(hp) : 0.f;
+      }
       if (ok) a.dvv[row * a.ld_d + h * a.dv + c] = g;
     }
 #pragma unroll
@@ -420,7 +497,10 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
       const int c = t * 16 + lr;
       const bool ok = row_ok && c < a.dqk;
       float g = dK[t][r];
-      if (a.hk) g *= ok ? silu_grad_(hk_pre[r][t]) : 0.f;
+      if (a.hk) {
+        const float hp = STAGED ? Qs[(w * 16 + 4 * lg + r) * C::LDQ + c] : hk_pre[r][STAGED ? 0 : t];
+        g *= ok ? silu_grad_(hp) : 0.f;
+      }
       if (ok) a.dk[row * a.ld_d + h * a.dqk + c] = g;
     }
   }
@@ -428,6 +508,8 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
     const int bin = a.N - 1 + last_db - 16 + lr;
     if (bin >= 0 && bin < npos) whist[bin] += carry;
   }
+  carry = 0.f;
+  }  // pass
   if (has_bias && run_b >= 0) atomicAdd(&wts[run_b], run_s);  // the open dts run
   if (has_bias && slab) {
     __syncthreads();
@@ -440,6 +522,12 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
       slab[npos + i] = acc;
     }
   }
+#ifdef GR_STAMP
+  if (lane == 0) {
+    const int slot = (id * 4 + w) * 12;
+    if (slot + 12 <= (1 << 16)) gr_stamp_buf[slot + 9] = gr_stamp() - st_entry;
+  }
+#endif
 }
 
 // ------------------------------------------------------------------ query-major: dQ
@@ -455,14 +543,21 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& a, const int
   float* posw = tsw + (a.nb + 1);
 
   const int BH = a.B * a.H;
-  const int rank = snake_rank(id, a.cus);
-  const int qt = a.n_tiles - 1 - rank / BH;
-  const int bh = rank % BH;
+  int qt_a, qt_b = -1, bh;  // paired: query tiles p and T-1-p (see the dK/dV body)
+  if (a.paired) {
+    qt_a = id / BH;
+    bh = id % BH;
+    qt_b = a.n_tiles - 1 - qt_a;
+    if (qt_b == qt_a) qt_b = -1;
+  } else {
+    const int rank = snake_rank(id, a.cus);
+    qt_a = a.n_tiles - 1 - rank / BH;
+    bh = rank % BH;
+  }
   const int b = bh / a.H, h = bh % a.H;
   const int64_t s0 = a.offsets[b];
   const int L = (int)(a.offsets[b + 1] - s0);
-  const int q0 = qt * 64;
-  if (q0 >= L) return;
+  if (qt_a * 64 >= L && (qt_b < 0 || qt_b * 64 >= L)) return;
   const int tid = threadIdx.x, w = wave_id(), lane = tid & 63;
   const int lr = lane & 15, lg = lane >> 4;
   constexpr bool has_bias = HB;
@@ -470,10 +565,22 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& a, const int
     for (int i = tid; i <= a.nb; i += 256) tsw[i] = a.ts_w[i];
     for (int i = tid; i < 2 * a.N - 1; i += 256) posw[i] = a.pos_w[i];
   }
+  const __amdgpu_buffer_rsrc_t rmap = map_rsrc(a.map_qk, b, attn_tiles_per_seq(a.N));
+  const int map_voff = ((w * 16 + lr) * 16 + lg) * 4;
+  const __amdgpu_buffer_rsrc_t rk = seq_rsrc(a.k, a.ld_qk, s0, h * a.dqk, L, a.dqk);
+  const __amdgpu_buffer_rsrc_t rv = seq_rsrc(a.v, a.ld_v, s0, h * a.dv, L, a.dv);
+  for (int pass = 0; pass < 2; ++pass) {
+  const int qt = pass == 0 ? qt_a : qt_b;
+  const int q0 = qt * 64;
+  if (pass == 1) {
+    if (qt < 0 || q0 >= L) break;
+    lds_barrier();  // the first pass's epilogue reads of Ks
+  }
   const int qi = q0 + w * 16 + lr;
   const bool q_ok = qi < L;
+  constexpr bool STAGED = TT == 64;  // Q / dO fragments and silu'(h) through LDS (see dK/dV)
   float qreg[KSTEPS], doreg[KSTEPS];
-  {
+  if constexpr (!STAGED) {
     const int64_t row = s0 + (q_ok ? qi : L - 1);
     gptr<float> qrow = as_global(a.q) + row * a.ld_qk + h * a.dqk;
     gptr<float> drow = as_global(a.dout) + row * a.ld_dout + h * a.dv;
@@ -486,23 +593,18 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& a, const int
       doreg[st] = d < a.dv ? y : 0.f;
     }
   }
-  const __amdgpu_buffer_rsrc_t rmap = map_rsrc(a.map_qk, b, attn_tiles_per_seq(a.N));
-  const int map_voff = ((w * 16 + lr) * 16 + lg) * 4;
-  const __amdgpu_buffer_rsrc_t rk = seq_rsrc(a.k, a.ld_qk, s0, h * a.dqk, L, a.dqk);
-  const __amdgpu_buffer_rsrc_t rv = seq_rsrc(a.v, a.ld_v, s0, h * a.dv, L, a.dv);
-
   f4 dQ[C::KT];
 #pragma unroll
   for (int t = 0; t < C::KT; ++t) dQ[t] = f4_zero();
   const int wq_lo = q0 + w * 16;
-  float hq_pre[4][C::KT];  // the epilogue's silu'(h) inputs, prefetched (see the dK/dV body)
-  if (a.hq) {
+  float hq_pre[4][STAGED ? 1 : C::KT];  // the epilogue's silu'(h) inputs (see the dK/dV body)
+  if (!STAGED && a.hq) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int qo = wq_lo + 4 * lg + r;
       gptr<float> hqr = as_global(a.hq) + (s0 + (qo < L ? qo : L - 1)) * a.ld_h + h * a.dqk;
 #pragma unroll
-      for (int t = 0; t < C::KT; ++t) {
+      for (int t = 0; t < (STAGED ? 1 : C::KT); ++t) {
         const int c = t * 16 + lr;
         hq_pre[r][t] = hqr[c < a.dqk ? c : a.dqk - 1];
       }
@@ -519,7 +621,22 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& a, const int
     for (int kb = 0; kb < C::TB; ++kb)
       m[kb] = buf_ld_u32(rmap, map_voff, map_soff(q0, kt * TT + kb * 16, true));
   };
-  load_tile(0, mw);
+  if constexpr (STAGED) {
+    kst.load(seq_rsrc(a.q, a.ld_qk, s0, h * a.dqk, L, a.dqk), a.ld_qk, q0, a.dqk, a.vec2);
+    vst.load(seq_rsrc(a.dout, a.ld_dout, s0, h * a.dv, L, a.dv), a.ld_dout, q0, a.dv, a.vec2);
+    kst.store(Ks, LDK, a.vec2);
+    vst.store(Vs, LDV, a.vec2);
+    load_tile(0, mw);
+    __syncthreads();
+#pragma unroll
+    for (int st = 0; st < KSTEPS; ++st) {
+      qreg[st] = Ks[(w * 16 + lr) * LDK + 4 * st + lg];
+      doreg[st] = Vs[(w * 16 + lr) * LDV + 4 * st + lg];
+    }
+    lds_barrier();
+  } else {
+    load_tile(0, mw);
+  }
   kst.store(Ks, LDK, a.vec2);
   vst.store(Vs, LDV, a.vec2);
   __syncthreads();
@@ -528,7 +645,11 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& a, const int
   for (int kt = 0; kt <= last_kt; ++kt) {
     const int k0 = kt * TT;
     const bool more = kt < last_kt;
-    if (more) load_tile(kt + 1, mwn);
+    if (more) {
+      load_tile(kt + 1, mwn);
+    } else if (STAGED && a.hq) {
+      kst.load(seq_rsrc(a.hq, a.ld_h, s0, h * a.dqk, L, a.dqk), a.ld_h, q0, a.dqk, a.vec2h);
+    }
 #pragma unroll
     for (int kb = 0; kb < C::TB; ++kb) {
       const int kb0 = k0 + kb * 16;
@@ -590,6 +711,11 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& a, const int
       lds_barrier();
     }
   }
+  if (STAGED && a.hq) {
+    lds_barrier();
+    kst.store(Ks, LDK, a.vec2h);
+    lds_barrier();
+  }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int qo = wq_lo + 4 * lg + r;
@@ -600,20 +726,28 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& a, const int
       const int c = t * 16 + lr;
       const bool ok = row_ok && c < a.dqk;
       float g = dQ[t][r];
-      if (a.hq) g *= ok ? silu_grad_(hq_pre[r][t]) : 0.f;
+      if (a.hq) {
+        const float hp = STAGED ? Ks[(w * 16 + 4 * lg + r) * LDK + c] : hq_pre[r][STAGED ? 0 : t];
+        g *= ok ? silu_grad_(hp) : 0.f;
+      }
       if (ok) a.dq[row * a.ld_d + h * a.dqk + c] = g;
     }
   }
+  }  // pass
 }
 
 // ------------------------------------------------------------------ entry points
 template <int KSTEPS, int VTILES, int TT, bool HB>
 __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
+  GR_TL_BEGIN();
   attn_bwd_dkv_body<KSTEPS, VTILES, TT, HB>(a, blockIdx.x);
+  GR_TL_END(blockIdx.x, 0);
 }
 template <int KSTEPS, int VTILES, int TT, bool HB>
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
+  GR_TL_BEGIN();
   attn_bwd_dq_body<KSTEPS, VTILES, TT, HB>(a, blockIdx.x);
+  GR_TL_END(blockIdx.x + gridDim.x, 1);
 }
 // dK/dV and dQ in ONE launch: workgroups [0, grid) run the key-major pass (heaviest key
 // tiles first), the next grid run the query-major pass.  At narrow heads both are bound
@@ -624,10 +758,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
 template <int KSTEPS, int VTILES, int TT, bool HB>
 __global__ __launch_bounds__(256) void attn_bwd_fused_kernel(AttnBwdArgs a, int grid_kv) {
   const int id = blockIdx.x;
+  GR_TL_BEGIN();
   if (id < grid_kv)
     attn_bwd_dkv_body<KSTEPS, VTILES, TT, HB>(a, id);
   else
     attn_bwd_dq_body<KSTEPS, VTILES, TT, HB>(a, id - grid_kv);
+  GR_TL_END(id, id < grid_kv ? 0 : 1);
 }
 
 // ------------------------------------------------------------------ slab reduce
@@ -680,32 +816,40 @@ static int launch_bwd(const AttnBwdArgs& a, float* dpos_w, float* dts_w, hipStre
   const size_t lds_q = sizeof(float) * (TT * C::LDQ + TT * LDV_Q) + tail;
   GR_REQUIRE(lds_kv <= 160 * 1024 && lds_q <= 160 * 1024,
              "hstu_attn_bwd: LDS (%zu, %zu B) exceeds 160 KiB (N=%d)", lds_kv, lds_q, a.N);
-  static const bool split = getenv("GR_ATTN_BWD_SPLIT") != nullptr;  // A/B knob
+  const bool split = option(GR_OPT_ATTN_BWD_SPLIT) != 0;
+  // Tile pairs (p, T-1-p) per workgroup when the single-tile grid needs more than one
+  // round and the paired grid is resident in one: every workgroup then carries the same
+  // causal work and one prologue serves two tiles (C2: 66.8 -> 62.4 us).  Otherwise single
+  // tiles, heaviest first (LPT order).
+  const int pgrid = ceil_div(a.n_tiles, 2) * a.B * a.H;
+  const bool pairs_on = option(GR_OPT_ATTN_BWD_PAIRS) != 0 && a.n_tiles > 1;
+  int n_slabs = grid;
   if (!split && C::KT <= 8) {
     const size_t lds = lds_kv > lds_q ? lds_kv : lds_q;
-    if (a.map_kq) {
-      GR_TIMED("attn_bwd", st, hipLaunchKernelGGL((attn_bwd_fused_kernel<KS, VT, TT, true>), dim3(2 * grid), dim3(256), lds, st, a, grid));
-    } else {
-      GR_TIMED("attn_bwd", st, hipLaunchKernelGGL((attn_bwd_fused_kernel<KS, VT, TT, false>), dim3(2 * grid), dim3(256), lds, st, a, grid));
-    }
+    auto kern = a.map_kq ? attn_bwd_fused_kernel<KS, VT, TT, true> : attn_bwd_fused_kernel<KS, VT, TT, false>;
+    AttnBwdArgs af = a;
+    const int slots = device_cus() * resident_wgs(kern, lds);
+    af.paired = pairs_on && 2 * grid > slots && 2 * pgrid <= slots;
+    const int g = af.paired ? pgrid : grid;
+    n_slabs = g;
+    GR_TIMED("attn_bwd", st, hipLaunchKernelGGL(kern, dim3(2 * g), dim3(256), lds, st, af, g));
     GR_LAUNCH_CHECK("hstu_attn_bwd(fused)");
   } else {
-    if (a.map_kq) {
-      GR_TIMED("attn_bwd_dkv", st, hipLaunchKernelGGL((attn_bwd_dkv_kernel<KS, VT, TT, true>), dim3(grid), dim3(256), lds_kv, st, a));
-    } else {
-      GR_TIMED("attn_bwd_dkv", st, hipLaunchKernelGGL((attn_bwd_dkv_kernel<KS, VT, TT, false>), dim3(grid), dim3(256), lds_kv, st, a));
-    }
+    auto kkv = a.map_kq ? attn_bwd_dkv_kernel<KS, VT, TT, true> : attn_bwd_dkv_kernel<KS, VT, TT, false>;
+    auto kq = a.map_qk ? attn_bwd_dq_kernel<KS, VT, TT, true> : attn_bwd_dq_kernel<KS, VT, TT, false>;
+    AttnBwdArgs akv = a, aq = a;
+    const int s_kv = device_cus() * resident_wgs(kkv, lds_kv), s_q = device_cus() * resident_wgs(kq, lds_q);
+    akv.paired = pairs_on && grid > s_kv && pgrid <= s_kv;
+    aq.paired = pairs_on && grid > s_q && pgrid <= s_q;
+    n_slabs = akv.paired ? pgrid : grid;
+    GR_TIMED("attn_bwd_dkv", st, hipLaunchKernelGGL(kkv, dim3(n_slabs), dim3(256), lds_kv, st, akv));
     GR_LAUNCH_CHECK("hstu_attn_bwd(dkv)");
-    if (a.map_qk) {
-      GR_TIMED("attn_bwd_dq", st, hipLaunchKernelGGL((attn_bwd_dq_kernel<KS, VT, TT, true>), dim3(grid), dim3(256), lds_q, st, a));
-    } else {
-      GR_TIMED("attn_bwd_dq", st, hipLaunchKernelGGL((attn_bwd_dq_kernel<KS, VT, TT, false>), dim3(grid), dim3(256), lds_q, st, a));
-    }
+    GR_TIMED("attn_bwd_dq", st, hipLaunchKernelGGL(kq, dim3(aq.paired ? pgrid : grid), dim3(256), lds_q, st, aq));
     GR_LAUNCH_CHECK("hstu_attn_bwd(dq)");
   }
   if (a.map_kq) {
     GR_TIMED("attn_bias_reduce", st, hipLaunchKernelGGL(bias_grad_reduce_kernel, dim3(ceil_div(nbins, 16)), dim3(256), 0, st,
-                       a.slabs, grid, 2 * a.N - 1, a.nb + 1, dpos_w, dts_w));
+                       a.slabs, n_slabs, 2 * a.N - 1, a.nb + 1, dpos_w, dts_w));
     GR_LAUNCH_CHECK("hstu_attn_bwd(bias reduce)");
   }
   return 0;
@@ -716,6 +860,9 @@ static int launch_bwd(const AttnBwdArgs& a, float* dpos_w, float* dts_w, hipStre
 #ifdef GR_STAMP
 extern "C" __attribute__((visibility("default"))) int gr_stamp_read(unsigned long long* host, int n) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(gr::gr_stamp_buf), sizeof(unsigned long long) * n) == hipSuccess ? 0 : 1;
+}
+extern "C" __attribute__((visibility("default"))) int gr_timeline_read(unsigned long long* host, int n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(gr::gr_tl_buf), sizeof(unsigned long long) * n) == hipSuccess ? 0 : 1;
 }
 #endif
 
@@ -764,6 +911,7 @@ extern "C" int hstu_attn_bwd(const float* q, const float* k, const float* v, int
   // heaviest-first (dynamic dispatch = longest-processing-time order)
   a.cus = (int64_t)a.n_tiles * B * H <= 2 * device_cus() ? device_cus() : (1 << 30);
   a.vec2 = pair_aligned({q, k, v, dout}, {ld_qk, ld_v, ld_dout, dqk, dv});
+  a.vec2h = hq ? pair_aligned({hq, hk, hv}, {ld_h, dqk, dv}) : 0;
   const int d = dqk > dv ? dqk : dv;
   if (d <= 8) return launch_bwd<2, 1>(a, dpos_w, dts_w, st);
   if (d <= 16) return launch_bwd<4, 1>(a, dpos_w, dts_w, st);

@@ -771,14 +771,7 @@ static int cat_bwd_kgh(const RwArgsGateOBwd& a, int hv, int kg, int64_t max_rows
   return -1;
 }
 
-static bool rw_enabled() {
-  static int on = -1;
-  if (on < 0) {
-    const char* e = getenv("GR_ROWWAVE");
-    on = (e && e[0] == '0') ? 0 : 1;
-  }
-  return on == 1;
-}
+static bool rw_enabled() { return option(GR_OPT_ROWWAVE) != 0; }
 
 }  // namespace gr
 

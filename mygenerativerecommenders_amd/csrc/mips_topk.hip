@@ -914,7 +914,7 @@ struct FilterArgs {
   float* cand_s;      // [B][NSUB][SUBCAP]
   int* cand_i;        // [B][NSUB][SUBCAP]  local item index
   int* flag;          // set when a workgroup's staging buffer overflows
-  int nohit;          // profiling knob (GR_MIPS_DEBUG_NOHIT): thresholds +inf
+  int nohit;          // GR_OPT_MIPS_FORCE_FALLBACK: thresholds +inf
   // bf16 filter: hits are rescored exactly at flush time from row-major f32 copies
   const float* rows;    // items, DP floats per row
   const float* q_rows;  // queries, DP floats per row (workspace)
@@ -1664,16 +1664,14 @@ static TopkPlan plan_topk(int B, int64_t X, int D, int k, int N0) {
     p.NQG = B <= 32 ? 2 : 8;
     p.n_chunks = ceil_div(B, p.NQG * 16);
     // whole rounds of 2 four-wave workgroups per CU, >= ~48 blocks per wave
-    static const char* env_wgs = getenv("GR_MIPS_FILTER_WGS");  // tuning knob: WGs per CU
-    const int64_t per_round = (int64_t)device_cus() * 4 * (env_wgs ? atoi(env_wgs) : 2);
-    // GR_MIPS_FP32_FILTER=1: filter on the f32 table (exact scores, 16x fewer flop/s)
-    p.KC = getenv("GR_MIPS_FP32_FILTER") ? 0 : pack_layout(X, D).KC;
+    const int64_t per_round = (int64_t)device_cus() * 4 * option(GR_OPT_MIPS_FILTER_WGS);
+    // GR_OPT_MIPS_FILTER_FP32: filter on the f32 table (exact scores, 16x fewer flop/s)
+    p.KC = option(GR_OPT_MIPS_FILTER_FP32) ? 0 : pack_layout(X, D).KC;
     // f32: >= ~48 blocks per wave.  bf16 (streaming-bound): one round (10M items: 7
     // rounds 302 us, 2 rounds 253 us, 1 round 251 us)
     const int64_t min_rb = p.KC ? 4096 : 48;
     int64_t rounds = (p.n_blocks + per_round * min_rb - 1) / (per_round * min_rb);
-    static const char* env_rounds = getenv("GR_MIPS_FILTER_ROUNDS");  // tuning knob
-    if (env_rounds) rounds = atoi(env_rounds);
+    if (option(GR_OPT_MIPS_FILTER_ROUNDS) > 0) rounds = option(GR_OPT_MIPS_FILTER_ROUNDS);
     if (rounds < 1) rounds = 1;
     p.RB = (p.n_blocks + per_round * rounds - 1) / (per_round * rounds);
     p.filter_waves = (int)((p.n_blocks + p.RB - 1) / p.RB);
@@ -1867,7 +1865,7 @@ extern "C" int mips_topk(const float* queries, const float* packed_items, int64_
     FilterArgs f{queries, packed_items, p.KC ? (const u32x4*)(pbase + L.off16) : nullptr, X, D, B,
                  p.n_blocks, p.GB, p.G, p.sr, (float*)(ws + p.off_smax),
                  p.RB, tau, cnt, (float*)(ws + p.off_cs), (int*)(ws + p.off_ci), (int*)ws,
-                 getenv("GR_MIPS_DEBUG_NOHIT") != nullptr,
+                 option(GR_OPT_MIPS_FORCE_FALLBACK) != 0,
                  p.KC ? (const float*)(pbase + L.off_rows) : nullptr, (float*)(ws + p.off_qrows),
                  L.DP};
     int rc = launch_filter(f, p, true, st);

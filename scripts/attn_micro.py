@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--len", type=int, default=0, help="override L (N = L + 11)")
     ap.add_argument("--nobias", action="store_true", help="no relative bias (timestamps absent)")
     ap.add_argument("--bf16", action="store_true", help="bf16-operand kernels")
+    ap.add_argument("--split", action="store_true", help="f32 backward as separate dK/dV, dQ launches")
+    ap.add_argument("--nopairs", action="store_true", help="f32 backward: one tile per workgroup")
     ap.add_argument("--hepi", action="store_true",
                     help="fused silu'(h) epilogue on dQ/dK/dV (as in the training step)")
     args = ap.parse_args()
@@ -68,6 +70,8 @@ def main():
     dpw = torch.empty_like(pos_w)
     dtw = torch.empty_like(ts_w)
     L_ = _lib.lib()
+    _lib.set_option("ATTN_BWD_SPLIT", int(args.split))
+    _lib.set_option("ATTN_BWD_PAIRS", int(not args.nopairs))
     ws_n = (L_.hstu_attn_bwd_bf16_workspace_size(B, N, L, H, d, d, 128) if args.bf16
             else L_.hstu_attn_bwd_workspace_size(B, N, L, H, 128))
     ws = torch.empty(max(ws_n, 4), dtype=torch.uint8, device=dev)

@@ -262,17 +262,17 @@ def test_sharded_merge_equals_full_filter_path():
 # ---------------------------------------------------------------- bf16 filter scores
 # The filter pass scores a bf16 copy of the table; the merge rescores every candidate
 # with the exact f32 chain and only trusts those >= tau_e (mips_tau_kernel's bound), so
-# the result stays bit-identical to the oracle.  GR_MIPS_FP32_FILTER=1 keeps the f32
-# filter (exact filter scores) reachable.
+# the result stays bit-identical to the oracle.  The launch option GR_OPT_MIPS_FILTER_FP32
+# keeps the f32 filter (exact filter scores) reachable.
 
 @pytest.mark.parametrize("fp32", [False, True], ids=["bf16-filter", "f32-filter"])
-def test_mips_filter_score_type_bitexact(fp32, monkeypatch):
-    if fp32:
-        monkeypatch.setenv("GR_MIPS_FP32_FILTER", "1")
+def test_mips_filter_score_type_bitexact(fp32):
+    from mygenerativerecommenders_amd import _lib
     g = np.random.default_rng(31)
     B, X, D, k, N0 = 128, 400_000, 50, 200, 211
     Q, E, inv = _normal_catalog(g, B, X, D, N0)
-    _check_filter(Q, E, np.arange(1, X + 1, dtype=np.int64), inv, k, expect_flag=0)
+    with _lib.option("MIPS_FILTER_FP32", int(fp32)):
+        _check_filter(Q, E, np.arange(1, X + 1, dtype=np.int64), inv, k, expect_flag=0)
 
 
 def test_mips_filter_bf16_rescoring_orders_near_ties():
