@@ -246,7 +246,7 @@ class STULayerFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGeometry, seed: int,
-                seed_offset):
+                seed_offset, grad_on: bool = True):
         dev = x.device
         rows, D = x.shape
         B = offsets.numel() - 1
@@ -259,7 +259,9 @@ class STULayerFunction(torch.autograd.Function):
         w_o = w_o.contiguous()
         x_stats = torch.empty(rows, 2, dtype=torch.float32, device=dev)
         uvqk = torch.empty(rows, n_out, dtype=torch.float32, device=dev)
-        h_pre = torch.empty_like(uvqk) if geo.activation else None
+        # h_pre (pre-activation, for silu') and o_in (for the W_o gradient) exist only for
+        # the backward: inference / no_grad forwards skip both writes
+        h_pre = torch.empty_like(uvqk) if geo.activation and grad_on else None
         _lib.call("hstu_ln_uvqk_fwd", x.data_ptr(), x.stride(0), offsets.data_ptr(), B, rows, D,
                   w_uvqk.data_ptr(), n_out, geo.eps, geo.activation, x_stats.data_ptr(),
                   _lib.ptr(h_pre), uvqk.data_ptr(), n_out, st)
@@ -274,7 +276,7 @@ class STULayerFunction(torch.autograd.Function):
                   offsets.data_ptr(), B, geo.N, geo.max_len, H, dqk, dv, _lib.ptr(bmap),
                   _lib.ptr(pos_w_c), _lib.ptr(ts_w_c), NUM_BUCKETS, attn.data_ptr(), hv, st)
         attn_stats = torch.empty(rows, 2, dtype=torch.float32, device=dev)
-        needs_w_grad = w_o.requires_grad or b_o.requires_grad
+        needs_w_grad = grad_on and (w_o.requires_grad or b_o.requires_grad)
         ow = 3 * hv if geo.concat_ua else hv  # o_in width
         o_in = torch.empty(rows, ow, dtype=torch.float32, device=dev) if needs_w_grad else None
         w_pad = hvp = None
@@ -388,7 +390,7 @@ class STULayerFunction(torch.autograd.Function):
             ws = torch.empty(max(ws_n, 4), dtype=torch.uint8, device=dev)
             _lib.call("gr_wgrad", dy.data_ptr(), D, None, o_in.data_ptr(), ow, offsets.data_ptr(),
                       B, rows, D, ow, d_w_o.data_ptr(), d_b_o.data_ptr(), ws.data_ptr(), ws_n, st)
-        return (dx, None, None, d_w_uvqk, d_w_o, d_b_o, d_pos_w, d_ts_w, None, None, None)
+        return (dx, None, None, d_w_uvqk, d_w_o, d_b_o, d_pos_w, d_ts_w, None, None, None, None)
 
 
 def stu_layer(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGeometry, seed: int = 0,
@@ -399,8 +401,10 @@ def stu_layer(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGeometry,
     _lib.require_gpu(x, offsets, w_uvqk, w_o, b_o)
     if x.dtype != torch.float32:
         raise TypeError("stu_layer: float32 only (the reference runs fp32, hstu.py:592)")
+    grad_on = torch.is_grad_enabled() and any(
+        t is not None and t.requires_grad for t in (x, w_uvqk, w_o, b_o, pos_w, ts_w))
     return STULayerFunction.apply(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo, int(seed),
-                                  seed_offset)
+                                  seed_offset, grad_on)
 
 
 # ------------------------------------------------------------------ sampled-softmax loss
