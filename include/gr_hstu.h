@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GR_HSTU_ABI_VERSION 7
+#define GR_HSTU_ABI_VERSION 8
 
 #ifndef GR_API
 #define GR_API __attribute__((visibility("default")))
@@ -267,6 +267,13 @@ GR_API int hstu_ln_uvqk_fwd(const float* x, int64_t ld_x, const int64_t* offsets
                      int64_t max_rows, int D, const float* w_uvqk, int n_out, float eps,
                      int activation, float* x_stats, float* h_pre, float* uvqk,
                      int64_t ld_out, void* stream);
+/* hstu_ln_uvqk_fwd with bf16 MFMA operands (autocast_dtype = bfloat16): the transformed A
+ * values and the weights rounded to bf16, fp32 accumulation and epilogue; same
+ * arguments and outputs. */
+GR_API int hstu_ln_uvqk_fwd_bf16(const float* x, int64_t ld_x, const int64_t* offsets, int B,
+                          int64_t max_rows, int D, const float* w_uvqk, int n_out, float eps,
+                          int activation, float* x_stats, float* h_pre, float* uvqk,
+                          int64_t ld_out, void* stream);
 
 /* hstu_gate_o_fwd  (replaces hstu.py:393-413 with concat_ua = False):
  *   attn_stats[m] = (mean, rstd) of attn[m, :hdv]
@@ -282,6 +289,14 @@ GR_API int hstu_gate_o_fwd(const float* u, int64_t ld_u, const float* attn, int6
                     const float* w_o, const float* b_o, const float* x_res, int64_t ld_x,
                     float eps, float dropout_p, uint64_t seed, const int64_t* seed_offset,
                     float* attn_stats, float* o_in, float* y, int64_t ld_y, void* stream);
+/* hstu_gate_o_fwd with bf16 MFMA operands (autocast_dtype = bfloat16): the transformed A
+ * values and the weights rounded to bf16, fp32 accumulation and epilogue; same
+ * arguments and outputs. */
+GR_API int hstu_gate_o_fwd_bf16(const float* u, int64_t ld_u, const float* attn, int64_t ld_attn,
+                         const int64_t* offsets, int B, int64_t max_rows, int hdv, int D,
+                         const float* w_o, const float* b_o, const float* x_res, int64_t ld_x,
+                         float eps, float dropout_p, uint64_t seed, const int64_t* seed_offset,
+                         float* attn_stats, float* o_in, float* y, int64_t ld_y, void* stream);
 
 /* hstu_gate_o_bwd  (backward of hstu_gate_o_fwd w.r.t. u and attn; hdv <= 256):
  *   g = (dy @ w_o) * dropout mask;  du = g * LN(attn) [* silu'(h_u) if h_u];
@@ -293,6 +308,15 @@ GR_API int hstu_gate_o_bwd(const float* dy, int64_t ld_dy, const int64_t* offset
                     const float* attn_stats, const float* h_u, int64_t ld_h,
                     float dropout_p, uint64_t seed, const int64_t* seed_offset, float* du,
                     int64_t ld_du, float* d_attn, int64_t ld_da, void* stream);
+/* hstu_gate_o_bwd with bf16 MFMA operands (autocast_dtype = bfloat16): the transformed A
+ * values and the weights rounded to bf16, fp32 accumulation and epilogue; same
+ * arguments and outputs. */
+GR_API int hstu_gate_o_bwd_bf16(const float* dy, int64_t ld_dy, const int64_t* offsets, int B,
+                         int64_t max_rows, int hdv, int D, const float* w_o, const float* u,
+                         int64_t ld_u, const float* attn, int64_t ld_attn,
+                         const float* attn_stats, const float* h_u, int64_t ld_h,
+                         float dropout_p, uint64_t seed, const int64_t* seed_offset, float* du,
+                         int64_t ld_du, float* d_attn, int64_t ld_da, void* stream);
 
 /* hstu_gate_o_cat_fwd / _bwd: the concat_ua = True form of hstu_gate_o_fwd / _bwd
  * (hstu.py:398-400): o_in = dropout_p([u, LN(attn), u * LN(attn)]) (rows, 3 hdv; the mask
@@ -324,6 +348,14 @@ GR_API int hstu_ln_uvqk_bwd(const float* dh, int64_t ld_dh, const int64_t* offse
                      const float* x, int64_t ld_x, const float* x_stats,
                      const float* dy_res, int64_t ld_dy, float* dx, int64_t ld_dx,
                      void* stream);
+/* hstu_ln_uvqk_bwd with bf16 MFMA operands (autocast_dtype = bfloat16): the transformed A
+ * values and the weights rounded to bf16, fp32 accumulation and epilogue; same
+ * arguments and outputs. */
+GR_API int hstu_ln_uvqk_bwd_bf16(const float* dh, int64_t ld_dh, const int64_t* offsets, int B,
+                          int64_t max_rows, int D, int n_out, const float* w_uvqk,
+                          const float* x, int64_t ld_x, const float* x_stats,
+                          const float* dy_res, int64_t ld_dy, float* dx, int64_t ld_dx,
+                          void* stream);
 
 /* gr_wgrad: weight gradient C = A'^T B over all jagged rows (replaces the mm-backward
  * of hstu.py:303 and of the _o Linear at hstu.py:404-411):
@@ -347,6 +379,14 @@ GR_API int gr_wgrad2(const float* a0, int64_t lda0, const float* a_stats0, const
                      int64_t ldb1, int Ka1, int Nb1, float* c1, float* colsum1,
                      const int64_t* offsets, int B, int64_t max_rows, void* workspace,
                      size_t ws_bytes, void* stream);
+/* gr_wgrad2 with bf16 MFMA operands (LayerNorm applied in fp32 before rounding; fp32
+ * accumulation and slab reduce); same arguments, workspace and outputs. */
+GR_API int gr_wgrad2_bf16(const float* a0, int64_t lda0, const float* a_stats0, const float* b0,
+                          int64_t ldb0, int Ka0, int Nb0, float* c0, float* colsum0,
+                          const float* a1, int64_t lda1, const float* a_stats1, const float* b1,
+                          int64_t ldb1, int Ka1, int Nb1, float* c1, float* colsum1,
+                          const int64_t* offsets, int B, int64_t max_rows, void* workspace,
+                          size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------- MIPS retrieval
  * Replaces indexing/top_k.py:44-70 (MIPSBruteForceTopK: mm + torch.topk) and

@@ -63,6 +63,21 @@ void timing_push(const char* name, hipEvent_t start, hipEvent_t stop);
 // v_mfma_f32_16x16x4_f32: A[i=l&15][k=l>>4], B[k=l>>4][j=l&15],
 // C/D: col = l&15, row = 4*(l>>4) + reg.  Bit-exact k-ordered fmaf chain.
 typedef float f4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+
+// Two floats -> packed bf16 pair (round-to-nearest-even), lo in the low half.
+__device__ __forceinline__ uint32_t pack_bf16(float lo, float hi) {
+  const bf16x2_t v = {(__bf16)lo, (__bf16)hi};
+  return __builtin_bit_cast(uint32_t, v);
+}
+// C += A B over k = 32: a = A[row lane%16][k 8(lane/16) .. +7], b = B[k ..][col lane%16]
+__device__ __forceinline__ f4 mfma_bf16(u32x4_t a, u32x4_t b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a),
+                                                  __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
+}
 
 __device__ __forceinline__ f4 mfma16x16x4(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);

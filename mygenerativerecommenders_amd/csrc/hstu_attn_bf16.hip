@@ -20,10 +20,6 @@
 
 namespace gr {
 
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
 
 struct AttnFwdArgsBf16 {
   const float* q;
@@ -42,14 +38,6 @@ struct AttnFwdArgsBf16 {
   int cus;  // CU count (snake_rank)
 };
 
-__device__ __forceinline__ uint32_t pack_bf16(float lo, float hi) {
-  const bf16x2_t v = {(__bf16)lo, (__bf16)hi};  // round-to-nearest-even
-  return __builtin_bit_cast(uint32_t, v);
-}
-__device__ __forceinline__ f4 mfma_bf16(u32x4_t a, u32x4_t b, f4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a),
-                                                  __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
-}
 
 // Stages a ROWS x CP tile of a jagged fp32 column block as bf16 in LDS, NT threads.
 // Columns >= ncols read 0 (out-of-range buffer offset); rows past the sequence read 0

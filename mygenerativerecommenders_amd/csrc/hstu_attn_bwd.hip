@@ -190,7 +190,9 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
   const __amdgpu_buffer_rsrc_t rdo = seq_rsrc(a.dout, a.ld_dout, s0, h * a.dv, L, a.dv);
   const int last_qt = (L - 1) / TT;
 
-  for (int pass = 0; pass < 2; ++pass) {
+  // tile pairs only with LDS-staged fragments (TT = 64); the wide-head instances keep one
+  // tile per workgroup (a runtime pass loop there spilled ~1.6 KB/lane at d = 256)
+  for (int pass = 0; pass < (TT == 64 ? 2 : 1); ++pass) {
   const int kt = pass == 0 ? kt_a : kt_b;
   const int k0 = kt * 64;
   if (pass == 1) {
@@ -236,29 +238,10 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
   };
 
   const int wk_lo = k0 + w * 16;
-  // the epilogue's silu'(h) inputs, loaded early so they land during the main loop (a load
-  // at the end put one more HBM round trip on every workgroup's tail: +16 us per launch);
-  // STAGED: as coalesced tiles into the stage registers during the last query tile
-  float hv_pre[4][STAGED ? 1 : VTILES], hk_pre[4][STAGED ? 1 : C::KT];
-  if (!STAGED && a.hv) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int key = wk_lo + 4 * lg + r;
-      const int64_t row = s0 + (key < L ? key : L - 1);
-      gptr<float> hvr = as_global(a.hv) + row * a.ld_h + h * a.dv;
-      gptr<float> hkr = as_global(a.hk) + row * a.ld_h + h * a.dqk;
-#pragma unroll
-      for (int t = 0; t < (STAGED ? 1 : VTILES); ++t) {
-        const int c = t * 16 + lr;
-        hv_pre[r][t] = hvr[c < a.dv ? c : a.dv - 1];
-      }
-#pragma unroll
-      for (int t = 0; t < (STAGED ? 1 : C::KT); ++t) {
-        const int c = t * 16 + lr;
-        hk_pre[r][t] = hkr[c < a.dqk ? c : a.dqk - 1];
-      }
-    }
-  }
+  // the epilogue's silu'(h) inputs.  STAGED: coalesced tiles loaded into the stage
+  // registers during the last query tile (a load at the end put one more HBM round trip
+  // on every workgroup's tail: +16 us per launch at C2).  Wide heads: read in the
+  // epilogue (128 prefetched values per lane spilled; their workgroups run for ms)
   if constexpr (STAGED) {
     // K / V rows k0 .. k0 + 63 (rows past L and columns past dqk / dv read as 0)
     qst.load(seq_rsrc(a.k, a.ld_qk, s0, h * a.dqk, L, a.dqk), a.ld_qk, k0, a.dqk, a.vec2);
@@ -487,7 +470,8 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
       const bool ok = row_ok && c < a.dv;
       float g = dV[t][r];
       if (a.hv) {
-        const float hp = STAGED ? Ds[(w * 16 + 4 * lg + r) * C::LDV + c] : hv_pre[r][STAGED ? 0 : t];
+        const float hp = STAGED ? Ds[(w * 16 + 4 * lg + r) * C::LDV + c]
+                                : as_global(a.hv)[row * a.ld_h + h * a.dv + (c < a.dv ? c : a.dv - 1)];
         g *= ok ? silu_grad_(hp) : 0.f;
       }
       if (ok) a.dvv[row * a.ld_d + h * a.dv + c] = g;
@@ -498,7 +482,8 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
       const bool ok = row_ok && c < a.dqk;
       float g = dK[t][r];
       if (a.hk) {
-        const float hp = STAGED ? Qs[(w * 16 + 4 * lg + r) * C::LDQ + c] : hk_pre[r][STAGED ? 0 : t];
+        const float hp = STAGED ? Qs[(w * 16 + 4 * lg + r) * C::LDQ + c]
+                                : as_global(a.hk)[row * a.ld_h + h * a.dqk + (c < a.dqk ? c : a.dqk - 1)];
         g *= ok ? silu_grad_(hp) : 0.f;
       }
       if (ok) a.dk[row * a.ld_d + h * a.dqk + c] = g;
@@ -569,7 +554,7 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& a, const int
   const int map_voff = ((w * 16 + lr) * 16 + lg) * 4;
   const __amdgpu_buffer_rsrc_t rk = seq_rsrc(a.k, a.ld_qk, s0, h * a.dqk, L, a.dqk);
   const __amdgpu_buffer_rsrc_t rv = seq_rsrc(a.v, a.ld_v, s0, h * a.dv, L, a.dv);
-  for (int pass = 0; pass < 2; ++pass) {
+  for (int pass = 0; pass < (TT == 64 ? 2 : 1); ++pass) {
   const int qt = pass == 0 ? qt_a : qt_b;
   const int q0 = qt * 64;
   if (pass == 1) {
@@ -822,7 +807,7 @@ static int launch_bwd(const AttnBwdArgs& a, float* dpos_w, float* dts_w, hipStre
   // causal work and one prologue serves two tiles (C2: 66.8 -> 62.4 us).  Otherwise single
   // tiles, heaviest first (LPT order).
   const int pgrid = ceil_div(a.n_tiles, 2) * a.B * a.H;
-  const bool pairs_on = option(GR_OPT_ATTN_BWD_PAIRS) != 0 && a.n_tiles > 1;
+  const bool pairs_on = option(GR_OPT_ATTN_BWD_PAIRS) != 0 && a.n_tiles > 1 && TT == 64;
   int n_slabs = grid;
   if (!split && C::KT <= 8) {
     const size_t lds = lds_kv > lds_q ? lds_kv : lds_q;

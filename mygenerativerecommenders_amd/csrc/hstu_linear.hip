@@ -227,6 +227,138 @@ __global__ __launch_bounds__(256) void rowpanel_kernel(Op op) {
   op.epilogue(acc, es, m0 + w * 16 + 4 * lg, n0 + lr, total);
 }
 
+// bf16-operand row panel (autocast_dtype = bfloat16: the projections' matmuls in bf16
+// as torch.autocast runs them, accumulation, LN, activations and epilogues in fp32).
+// Same Op interface and output layout as rowpanel_kernel; K streams in chunks of 32
+// (one v_mfma_f32_16x16x32_bf16 k-step): the transformed A values and the weight tile
+// are rounded to bf16 when written to LDS, both as [row][k] images (A rows, weight
+// columns) so each lane's 8 k-values are one 16-byte LDS read; row stride 40 bf16 (80 B:
+// the 16 lanes of a read phase hit 16 distinct 16-byte bank groups).  Two LDS buffers:
+// chunk k+1 is written into the other buffer right after chunk k's MFMAs, so one
+// barrier per chunk.
+template <int NT, class Op>
+__global__ __launch_bounds__(256) void rowpanel_bf16_kernel(Op op) {
+  using P = PanelCfg<NT>;
+  constexpr int BKT = 32;
+  constexpr int LDK = BKT + 8;  // bf16 elements per LDS row
+  constexpr int NP2 = P::BN <= 16 ? 16 : P::BN <= 32 ? 32 : P::BN <= 64 ? 64 : P::BN <= 128 ? 128 : 256;
+  constexpr int RPB = 256 / NP2;
+  constexpr int CPP = 256 / BKT;
+  constexpr int NB = Op::B_N_CONTIG ? (BKT + RPB - 1) / RPB : (P::BN + CPP - 1) / CPP;
+  constexpr int RPA = 256 / BKT;
+  constexpr int NA = BM / RPA;
+  __shared__ __attribute__((aligned(16))) __bf16 As2[2][BM * LDK];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs2[2][P::BN * LDK];
+  __shared__ float2 stats[BM];
+  const int64_t total = op.offsets[op.B];
+  const int64_t m0 = (int64_t)blockIdx.x * BM;
+  if (m0 >= total) return;
+  const int n0 = blockIdx.y * P::BN;
+  const int tid = threadIdx.x, w = wave_id(), lane = tid & 63;
+  const int lr = lane & 15, lg = lane >> 4;
+
+  op.prologue(m0, total, stats);
+  __syncthreads();
+
+  const __amdgpu_buffer_rsrc_t ra0 = op.a_rsrc0(m0, total);
+  const __amdgpu_buffer_rsrc_t ra1 = op.a_rsrc1(m0, total);
+  const int ld0 = (int)op.a_ld0(), ld1 = (int)op.a_ld1();
+  const int a_c = tid % BKT, a_r = tid / BKT;
+  const int va0 = (a_r * ld0 + a_c) * 4, va1 = (a_r * ld1 + a_c) * 4;
+  const __amdgpu_buffer_rsrc_t rw =
+      __builtin_amdgcn_make_buffer_rsrc((void*)op.w, 0, op.K * op.N * 4, 0x00020000);
+  const int bks = op.bks(), bns = op.bns();
+  const int b_c = Op::B_N_CONTIG ? tid % NP2 : tid / BKT;
+  const int b_r = Op::B_N_CONTIG ? tid / NP2 : tid % BKT;
+  const bool b_col = Op::B_N_CONTIG ? (b_c < P::BN && n0 + b_c < op.N) : true;
+  const int vb = b_col ? (b_r * bks + (n0 + b_c) * bns) * 4 : 0x40000000;
+
+  float ra[NA], ra2[Op::NSRC == 2 ? NA : 1], rb[NB];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      ra[i] = buf_ld(ra0, va0 + k0 * 4, i * RPA * ld0 * 4);
+      if constexpr (Op::NSRC == 2) ra2[i] = buf_ld(ra1, va1 + k0 * 4, i * RPA * ld1 * 4);
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      if constexpr (Op::B_N_CONTIG)
+        rb[i] = buf_ld(rw, vb, (k0 + RPB * i) * bks * 4);
+      else
+        rb[i] = buf_ld(rw, vb, (k0 * bks + CPP * i * bns) * 4);
+    }
+  };
+  auto store = [&](int k0, int buf) {
+    __bf16* As = As2[buf];
+    __bf16* Bs = Bs2[buf];
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int r = a_r + RPA * i, k = k0 + a_c;
+      const bool ok = m0 + r < total && k < op.K;
+      const float v = op.a_xform(ra[i], Op::NSRC == 2 ? ra2[Op::NSRC == 2 ? i : 0] : 0.f, m0 + r, k,
+                                 stats[r], ok);
+      As[r * LDK + a_c] = (__bf16)(ok ? v : 0.f);
+    }
+    if constexpr (Op::B_N_CONTIG && RPB == 1) {
+      // a thread owns one weight column's 32 k-values: 16 packed pair stores
+      if (b_c < P::BN) {
+#pragma unroll
+        for (int i = 0; i < NB; i += 2) {
+          const float lo = (b_col && k0 + i < op.K) ? rb[i] : 0.f;
+          const float hi = (b_col && k0 + i + 1 < op.K) ? rb[i + 1] : 0.f;
+          *reinterpret_cast<uint32_t*>(Bs + b_c * LDK + i) = pack_bf16(lo, hi);
+        }
+      }
+    } else if constexpr (Op::B_N_CONTIG) {
+      if (b_c < P::BN) {
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+          const int kk = b_r + RPB * i;
+          if (RPB * NB == BKT || kk < BKT)
+            Bs[b_c * LDK + kk] = (__bf16)((b_col && k0 + kk < op.K) ? rb[i] : 0.f);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const int c = b_c + CPP * i;
+        if (CPP * NB == P::BN || c < P::BN)
+          Bs[c * LDK + b_r] = (__bf16)((n0 + c < op.N && k0 + b_r < op.K) ? rb[i] : 0.f);
+      }
+    }
+  };
+
+  f4 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f4_zero();
+  typename Op::template Epi<NT> es;
+  op.epi_load(es, m0 + w * 16 + 4 * lg, n0 + lr, total);
+
+  load(0);
+  store(0, 0);
+  lds_barrier();
+  int buf = 0;
+  for (int k0 = 0; k0 < op.K; k0 += BKT) {
+    const bool more = k0 + BKT < op.K;
+    if (more) load(k0 + BKT);
+    const __bf16* As = As2[buf];
+    const __bf16* Bs = Bs2[buf];
+    const u32x4_t av = *reinterpret_cast<const u32x4_t*>(As + (w * 16 + lr) * LDK + 8 * lg);
+    u32x4_t bv[2];
+    bv[0] = *reinterpret_cast<const u32x4_t*>(Bs + lr * LDK + 8 * lg);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      if (t + 1 < NT)
+        bv[(t + 1) & 1] = *reinterpret_cast<const u32x4_t*>(Bs + (16 * (t + 1) + lr) * LDK + 8 * lg);
+      acc[t] = mfma_bf16(av, bv[t & 1], acc[t]);
+    }
+    if (more) store(k0 + BKT, buf ^ 1);  // the other buffer: last read before the barrier below
+    lds_barrier();
+    buf ^= 1;
+  }
+  op.epilogue(acc, es, m0 + w * 16 + 4 * lg, n0 + lr, total);
+}
+
 // descriptor over rows [m0, total) of a (rows, ld) matrix (column offset folded in base)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const float* base, int64_t ld,
                                                            int64_t m0, int64_t total) {
@@ -571,6 +703,34 @@ static int launch_rowpanel(const Op& op, int64_t max_rows, bool full_row, const 
   return 0;
 }
 
+template <class Op>
+static int launch_rowpanel_bf16(const Op& op, int64_t max_rows, bool full_row, const char* name,
+                                hipStream_t st) {
+  const int nt_needed = ceil_div(op.N, 16);
+  GR_REQUIRE(!full_row || nt_needed <= 16,
+             "%s: %d output columns exceed one 256-column panel (row-reduction epilogue)", name,
+             op.N);
+  const int nt = nt_needed > 16 ? 16 : nt_needed;
+  const int panels = ceil_div(op.N, nt * 16);
+  dim3 grid((unsigned)((max_rows + BM - 1) / BM), (unsigned)panels);
+  if (grid.x == 0) return 0;
+  const char* tname = name + 5;
+#define GR_NT_CASE(NT_)                                                                      \
+  case NT_:                                                                                  \
+    GR_TIMED(tname, st, hipLaunchKernelGGL((rowpanel_bf16_kernel<NT_, Op>), grid, dim3(256), 0, \
+                                           st, op));                                         \
+    break;
+  switch (nt) {
+    GR_NT_CASE(1) GR_NT_CASE(2) GR_NT_CASE(3) GR_NT_CASE(4) GR_NT_CASE(5) GR_NT_CASE(6)
+    GR_NT_CASE(7) GR_NT_CASE(8) GR_NT_CASE(9) GR_NT_CASE(10) GR_NT_CASE(11) GR_NT_CASE(12)
+    GR_NT_CASE(13) GR_NT_CASE(14) GR_NT_CASE(15) GR_NT_CASE(16)
+    default: GR_REQUIRE(false, "%s: bad panel width", name);
+  }
+#undef GR_NT_CASE
+  GR_LAUNCH_CHECK(name);
+  return 0;
+}
+
 // ------------------------------------------------------------------ row-wave dispatch
 // Narrow shapes (weight panel in LDS, <= 80 KiB) run the row-wave kernel (rowwave.h);
 // everything else the row-panel kernel above.  Returns -1 when the shape / alignment
@@ -778,14 +938,14 @@ static bool rw_enabled() { return option(GR_OPT_ROWWAVE) != 0; }
 // ====================================================================== C-ABI
 using namespace gr;
 
-extern "C" int hstu_ln_uvqk_fwd(const float* x, int64_t ld_x, const int64_t* offsets, int B,
+static int hstu_ln_uvqk_fwd_impl(bool bf16, const float* x, int64_t ld_x, const int64_t* offsets, int B,
                                 int64_t max_rows, int D, const float* w_uvqk, int n_out,
                                 float eps, int activation, float* x_stats, float* h_pre,
                                 float* uvqk, int64_t ld_out, void* stream) {
   GR_REQUIRE(x && offsets && w_uvqk && uvqk && x_stats, "hstu_ln_uvqk_fwd: null pointer");
   GR_REQUIRE(D > 0 && n_out > 0 && B >= 0 && max_rows >= 0, "hstu_ln_uvqk_fwd: bad sizes");
   GR_REQUIRE(activation == 0 || activation == 1, "hstu_ln_uvqk_fwd: activation must be 0|1");
-  if (rw_enabled()) {
+  if (!bf16 && rw_enabled()) {
     RwArgsLnUvqk ra{offsets, B, D, n_out, x, ld_x, w_uvqk, eps, activation, (float2*)x_stats,
                     h_pre, uvqk, ld_out};
     const int vec = rw_vec({x, h_pre, uvqk}, {ld_x, ld_out, D, n_out});
@@ -794,10 +954,23 @@ extern "C" int hstu_ln_uvqk_fwd(const float* x, int64_t ld_x, const int64_t* off
   }
   OpLnUvqk op{offsets, B, D, n_out, x, ld_x, w_uvqk, eps, activation, (float2*)x_stats,
               h_pre, uvqk, ld_out};
-  return launch_rowpanel(op, max_rows, false, "hstu_ln_uvqk_fwd", (hipStream_t)stream);
+  return bf16 ? launch_rowpanel_bf16(op, max_rows, false, "hstu_ln_uvqk_fwd", (hipStream_t)stream)
+              : launch_rowpanel(op, max_rows, false, "hstu_ln_uvqk_fwd", (hipStream_t)stream);
+}
+extern "C" int hstu_ln_uvqk_fwd(const float* x, int64_t ld_x, const int64_t* offsets, int B,
+                                int64_t max_rows, int D, const float* w_uvqk, int n_out,
+                                float eps, int activation, float* x_stats, float* h_pre,
+                                float* uvqk, int64_t ld_out, void* stream) {
+  return hstu_ln_uvqk_fwd_impl(false, x, ld_x, offsets, B, max_rows, D, w_uvqk, n_out, eps, activation, x_stats, h_pre, uvqk, ld_out, stream);
+}
+extern "C" int hstu_ln_uvqk_fwd_bf16(const float* x, int64_t ld_x, const int64_t* offsets, int B,
+                                int64_t max_rows, int D, const float* w_uvqk, int n_out,
+                                float eps, int activation, float* x_stats, float* h_pre,
+                                float* uvqk, int64_t ld_out, void* stream) {
+  return hstu_ln_uvqk_fwd_impl(true, x, ld_x, offsets, B, max_rows, D, w_uvqk, n_out, eps, activation, x_stats, h_pre, uvqk, ld_out, stream);
 }
 
-extern "C" int hstu_gate_o_fwd(const float* u, int64_t ld_u, const float* attn, int64_t ld_attn,
+static int hstu_gate_o_fwd_impl(bool bf16, const float* u, int64_t ld_u, const float* attn, int64_t ld_attn,
                                const int64_t* offsets, int B, int64_t max_rows, int hdv, int D,
                                const float* w_o, const float* b_o, const float* x_res,
                                int64_t ld_x, float eps, float dropout_p, uint64_t seed,
@@ -806,7 +979,7 @@ extern "C" int hstu_gate_o_fwd(const float* u, int64_t ld_u, const float* attn, 
   GR_REQUIRE(u && attn && offsets && w_o && y && attn_stats, "hstu_gate_o_fwd: null pointer");
   GR_REQUIRE(hdv > 0 && D > 0 && B >= 0, "hstu_gate_o_fwd: bad sizes");
   GR_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f, "hstu_gate_o_fwd: dropout_p %f", dropout_p);
-  if (rw_enabled()) {
+  if (!bf16 && rw_enabled()) {
     RwArgsGateO ra{offsets, B, hdv, D, u, ld_u, attn, ld_attn, w_o, b_o, x_res, ld_x, eps,
                    dropout_p, seed, seed_offset, (float2*)attn_stats, o_in, y, ld_y};
     const int vec = rw_vec({u, attn, x_res, o_in, y}, {ld_u, ld_attn, ld_x, ld_y, hdv, D});
@@ -815,10 +988,27 @@ extern "C" int hstu_gate_o_fwd(const float* u, int64_t ld_u, const float* attn, 
   }
   OpGateO op{offsets, B, hdv, D, u, ld_u, attn, ld_attn, w_o, b_o, x_res, ld_x, eps, dropout_p,
              seed, seed_offset, (float2*)attn_stats, o_in, y, ld_y};
-  return launch_rowpanel(op, max_rows, false, "hstu_gate_o_fwd", (hipStream_t)stream);
+  return bf16 ? launch_rowpanel_bf16(op, max_rows, false, "hstu_gate_o_fwd", (hipStream_t)stream)
+              : launch_rowpanel(op, max_rows, false, "hstu_gate_o_fwd", (hipStream_t)stream);
+}
+extern "C" int hstu_gate_o_fwd(const float* u, int64_t ld_u, const float* attn, int64_t ld_attn,
+                               const int64_t* offsets, int B, int64_t max_rows, int hdv, int D,
+                               const float* w_o, const float* b_o, const float* x_res,
+                               int64_t ld_x, float eps, float dropout_p, uint64_t seed,
+                               const int64_t* seed_offset, float* attn_stats, float* o_in,
+                               float* y, int64_t ld_y, void* stream) {
+  return hstu_gate_o_fwd_impl(false, u, ld_u, attn, ld_attn, offsets, B, max_rows, hdv, D, w_o, b_o, x_res, ld_x, eps, dropout_p, seed, seed_offset, attn_stats, o_in, y, ld_y, stream);
+}
+extern "C" int hstu_gate_o_fwd_bf16(const float* u, int64_t ld_u, const float* attn, int64_t ld_attn,
+                               const int64_t* offsets, int B, int64_t max_rows, int hdv, int D,
+                               const float* w_o, const float* b_o, const float* x_res,
+                               int64_t ld_x, float eps, float dropout_p, uint64_t seed,
+                               const int64_t* seed_offset, float* attn_stats, float* o_in,
+                               float* y, int64_t ld_y, void* stream) {
+  return hstu_gate_o_fwd_impl(true, u, ld_u, attn, ld_attn, offsets, B, max_rows, hdv, D, w_o, b_o, x_res, ld_x, eps, dropout_p, seed, seed_offset, attn_stats, o_in, y, ld_y, stream);
 }
 
-extern "C" int hstu_gate_o_bwd(const float* dy, int64_t ld_dy, const int64_t* offsets, int B,
+static int hstu_gate_o_bwd_impl(bool bf16, const float* dy, int64_t ld_dy, const int64_t* offsets, int B,
                                int64_t max_rows, int hdv, int D, const float* w_o,
                                const float* u, int64_t ld_u, const float* attn, int64_t ld_attn,
                                const float* attn_stats, const float* h_u, int64_t ld_h,
@@ -828,7 +1018,7 @@ extern "C" int hstu_gate_o_bwd(const float* dy, int64_t ld_dy, const int64_t* of
   GR_REQUIRE(dy && offsets && w_o && u && attn && attn_stats && du && d_attn,
              "hstu_gate_o_bwd: null pointer");
   GR_REQUIRE(hdv > 0 && D > 0 && B >= 0, "hstu_gate_o_bwd: bad sizes");
-  if (rw_enabled()) {
+  if (!bf16 && rw_enabled()) {
     RwArgsGateOBwd ra{offsets, B, D, hdv, dy, ld_dy, w_o, u, ld_u, attn, ld_attn,
                       (const float2*)attn_stats, h_u, ld_h, dropout_p, seed, seed_offset, du, ld_du,
                       d_attn, ld_da};
@@ -841,17 +1031,36 @@ extern "C" int hstu_gate_o_bwd(const float* dy, int64_t ld_dy, const int64_t* of
   op.w = w_o; op.u = u; op.ldu = ld_u; op.attn = attn; op.lda = ld_attn;
   op.a_stats = (const float2*)attn_stats; op.h_u = h_u; op.ldh = ld_h; op.p = dropout_p;
   op.seed = seed; op.seed_off = seed_offset; op.du = du; op.lddu = ld_du; op.da = d_attn; op.ldda = ld_da;
-  return launch_rowpanel(op, max_rows, true, "hstu_gate_o_bwd", (hipStream_t)stream);
+  return bf16 ? launch_rowpanel_bf16(op, max_rows, true, "hstu_gate_o_bwd", (hipStream_t)stream)
+              : launch_rowpanel(op, max_rows, true, "hstu_gate_o_bwd", (hipStream_t)stream);
+}
+extern "C" int hstu_gate_o_bwd(const float* dy, int64_t ld_dy, const int64_t* offsets, int B,
+                               int64_t max_rows, int hdv, int D, const float* w_o,
+                               const float* u, int64_t ld_u, const float* attn, int64_t ld_attn,
+                               const float* attn_stats, const float* h_u, int64_t ld_h,
+                               float dropout_p, uint64_t seed, const int64_t* seed_offset,
+                               float* du, int64_t ld_du, float* d_attn, int64_t ld_da,
+                               void* stream) {
+  return hstu_gate_o_bwd_impl(false, dy, ld_dy, offsets, B, max_rows, hdv, D, w_o, u, ld_u, attn, ld_attn, attn_stats, h_u, ld_h, dropout_p, seed, seed_offset, du, ld_du, d_attn, ld_da, stream);
+}
+extern "C" int hstu_gate_o_bwd_bf16(const float* dy, int64_t ld_dy, const int64_t* offsets, int B,
+                               int64_t max_rows, int hdv, int D, const float* w_o,
+                               const float* u, int64_t ld_u, const float* attn, int64_t ld_attn,
+                               const float* attn_stats, const float* h_u, int64_t ld_h,
+                               float dropout_p, uint64_t seed, const int64_t* seed_offset,
+                               float* du, int64_t ld_du, float* d_attn, int64_t ld_da,
+                               void* stream) {
+  return hstu_gate_o_bwd_impl(true, dy, ld_dy, offsets, B, max_rows, hdv, D, w_o, u, ld_u, attn, ld_attn, attn_stats, h_u, ld_h, dropout_p, seed, seed_offset, du, ld_du, d_attn, ld_da, stream);
 }
 
-extern "C" int hstu_ln_uvqk_bwd(const float* dh, int64_t ld_dh, const int64_t* offsets, int B,
+static int hstu_ln_uvqk_bwd_impl(bool bf16, const float* dh, int64_t ld_dh, const int64_t* offsets, int B,
                                 int64_t max_rows, int D, int n_out, const float* w_uvqk,
                                 const float* x, int64_t ld_x, const float* x_stats,
                                 const float* dy_res, int64_t ld_dy, float* dx, int64_t ld_dx,
                                 void* stream) {
   GR_REQUIRE(dh && offsets && w_uvqk && x && x_stats && dx, "hstu_ln_uvqk_bwd: null pointer");
   GR_REQUIRE(D > 0 && n_out > 0 && B >= 0, "hstu_ln_uvqk_bwd: bad sizes");
-  if (rw_enabled()) {
+  if (!bf16 && rw_enabled()) {
     RwArgsLnUvqkBwd ra{offsets, B, n_out, D, dh, ld_dh, w_uvqk, x, ld_x, (const float2*)x_stats,
                        dy_res, ld_dy, dx, ld_dx};
     const int vec = rw_vec({dh, x, dy_res, dx}, {ld_dh, ld_x, ld_dy, ld_dx, n_out, D});
@@ -862,7 +1071,22 @@ extern "C" int hstu_ln_uvqk_bwd(const float* dh, int64_t ld_dh, const int64_t* o
   op.offsets = offsets; op.B = B; op.K = n_out; op.N = D; op.dh = dh; op.lddh = ld_dh;
   op.w = w_uvqk; op.x = x; op.ldx = ld_x; op.x_stats = (const float2*)x_stats;
   op.dy = dy_res; op.lddy = ld_dy; op.dx = dx; op.lddx = ld_dx;
-  return launch_rowpanel(op, max_rows, true, "hstu_ln_uvqk_bwd", (hipStream_t)stream);
+  return bf16 ? launch_rowpanel_bf16(op, max_rows, true, "hstu_ln_uvqk_bwd", (hipStream_t)stream)
+              : launch_rowpanel(op, max_rows, true, "hstu_ln_uvqk_bwd", (hipStream_t)stream);
+}
+extern "C" int hstu_ln_uvqk_bwd(const float* dh, int64_t ld_dh, const int64_t* offsets, int B,
+                                int64_t max_rows, int D, int n_out, const float* w_uvqk,
+                                const float* x, int64_t ld_x, const float* x_stats,
+                                const float* dy_res, int64_t ld_dy, float* dx, int64_t ld_dx,
+                                void* stream) {
+  return hstu_ln_uvqk_bwd_impl(false, dh, ld_dh, offsets, B, max_rows, D, n_out, w_uvqk, x, ld_x, x_stats, dy_res, ld_dy, dx, ld_dx, stream);
+}
+extern "C" int hstu_ln_uvqk_bwd_bf16(const float* dh, int64_t ld_dh, const int64_t* offsets, int B,
+                                int64_t max_rows, int D, int n_out, const float* w_uvqk,
+                                const float* x, int64_t ld_x, const float* x_stats,
+                                const float* dy_res, int64_t ld_dy, float* dx, int64_t ld_dx,
+                                void* stream) {
+  return hstu_ln_uvqk_bwd_impl(true, dh, ld_dh, offsets, B, max_rows, D, n_out, w_uvqk, x, ld_x, x_stats, dy_res, ld_dy, dx, ld_dx, stream);
 }
 
 extern "C" int hstu_gate_o_cat_fwd(const float* u, int64_t ld_u, const float* attn, int64_t ld_attn,

@@ -217,6 +217,153 @@ __global__ __launch_bounds__(WG_THREADS) void wgrad_partial_kernel(WgradArgs g) 
                      smem);
 }
 
+// ---------------------------------------------------------------------------- bf16
+// bf16-operand panel (autocast_dtype = bfloat16), v_mfma_f32_16x16x32_bf16.  Chunks of
+// WGB_CH = 64 rows; both operands are staged TRANSPOSED as bf16 images (A'^T [ka][row]
+// with the LayerNorm applied in fp32 before rounding, Bm^T [nb][row]) so a lane's 8
+// consecutive rows are one 16-byte LDS read.  A thread stages 8 consecutive rows of one
+// A column (8 coalesced row loads, one 16-byte LDS store) and RB consecutive rows of one
+// B column.  Wave w: ka-tile w & 3, k-step (rows 32 half .. +31) of half w >> 2; the
+// halves and the slab write are as in the f32 panel.
+constexpr int WGB_CH = 64;
+constexpr int WGB_LDT = WGB_CH + 8;  // bf16 per image row: 144 B, 16 lanes -> 16 bank groups
+
+template <int NT>
+struct WgCfgB {
+  static constexpr int NP = NT * 16;
+  static constexpr int NP2 = NP <= 64 ? 64 : NP <= 128 ? 128 : 256;
+  static constexpr int BG = WG_THREADS / NP2;  // row groups of the B image
+  static constexpr int RB = WGB_CH / BG;       // B rows per thread (8, 16, 32)
+  static constexpr size_t STAGE = 2 * (size_t)WGB_LDT * (WG_KA + NP);
+  static constexpr size_t XCH = sizeof(float) * 4 * NT * 4 * 64;
+  static constexpr size_t LDS = STAGE > XCH ? STAGE : XCH;
+};
+
+template <int NT>
+__device__ __forceinline__ void wgrad_panel_bf16(const WgradProb& g, const int64_t* offsets, int B,
+                                                 int64_t rows_per_split, int split, int panel,
+                                                 char* smem) {
+  using C = WgCfgB<NT>;
+  __bf16* At = reinterpret_cast<__bf16*>(smem);   // [WG_KA][WGB_LDT]
+  __bf16* Bt = At + WG_KA * WGB_LDT;               // [NP][WGB_LDT]
+  const int pa = panel / g.panels_nb, pb = panel % g.panels_nb;
+  const int ka0 = pa * WG_KA, nb0 = pb * C::NP;
+  const int64_t total = offsets[B];
+  const int64_t r0 = (int64_t)split * rows_per_split;
+  const int64_t r1 = min(total, r0 + rows_per_split);
+  const int tid = threadIdx.x, wv = wave_id(), lane = tid & 63;
+  const int w = wv & 3, half = wv >> 2;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int n_ch = __builtin_amdgcn_readfirstlane(r1 > r0 ? (int)((r1 - r0 + WGB_CH - 1) / WGB_CH) : 0);
+  const int64_t nrows = r1 > r0 ? r1 - r0 : 0;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(g.a + r0 * g.lda), 0, nrows ? (int)(((nrows - 1) * g.lda + g.Ka) * 4) : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(g.bm + r0 * g.ldb), 0, nrows ? (int)(((nrows - 1) * g.ldb + g.Nb) * 4) : 0, 0x00020000);
+  const int ac = tid & 63, ag = tid >> 6;            // A: column ka0 + ac, rows 8 ag .. +7
+  const int bc = tid % C::NP2, bg = tid / C::NP2;    // B: column nb0 + bc, rows RB bg .. +RB-1
+  const int aka = ka0 + ac, bnb = nb0 + bc;
+  const bool a_ok = aka < g.Ka;
+  const bool b_in = bnb < g.Nb, b_one = bnb == g.Nb && g.NC > g.Nb;
+  float av_[8], bv_[C::RB];
+  float2 sv_[8];
+  auto load = [&](int ch) {
+    const int rr0 = ch * WGB_CH;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int rr = rr0 + 8 * ag + i;
+      av_[i] = buf_ld(ra, a_ok ? (int)((rr * g.lda + aka) * 4) : 0x40000000, 0);
+      sv_[i] = g.a_stats ? ld_f2(g.a_stats, min(r0 + rr, total - 1)) : make_float2(0.f, 1.f);
+    }
+#pragma unroll
+    for (int i = 0; i < C::RB; ++i) {
+      const int rr = rr0 + C::RB * bg + i;
+      bv_[i] = buf_ld(rb, b_in ? (int)((rr * g.ldb + bnb) * 4) : 0x40000000, 0);
+    }
+  };
+  auto store = [&](int ch) {
+    const int rr0 = ch * WGB_CH;
+    uint32_t pk[4];
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) {
+      const bool ok0 = a_ok && r0 + rr0 + 8 * ag + i < r1, ok1 = a_ok && r0 + rr0 + 8 * ag + i + 1 < r1;
+      pk[i / 2] = pack_bf16(ok0 ? (av_[i] - sv_[i].x) * sv_[i].y : 0.f,
+                            ok1 ? (av_[i + 1] - sv_[i + 1].x) * sv_[i + 1].y : 0.f);
+    }
+    *reinterpret_cast<u32x4_t*>(At + ac * WGB_LDT + 8 * ag) = u32x4_t{pk[0], pk[1], pk[2], pk[3]};
+    if (bc < C::NP) {
+#pragma unroll
+      for (int q = 0; q < C::RB; q += 8) {
+        uint32_t pb2[4];
+#pragma unroll
+        for (int i = 0; i < 8; i += 2) {
+          const int rr = C::RB * bg + q + i;
+          const bool ok0 = r0 + rr0 + rr < r1, ok1 = r0 + rr0 + rr + 1 < r1;
+          const float lo = b_one ? (ok0 ? 1.f : 0.f) : bv_[q + i];
+          const float hi = b_one ? (ok1 ? 1.f : 0.f) : bv_[q + i + 1];
+          pb2[i / 2] = pack_bf16(lo, hi);
+        }
+        *reinterpret_cast<u32x4_t*>(Bt + bc * WGB_LDT + C::RB * bg + q) =
+            u32x4_t{pb2[0], pb2[1], pb2[2], pb2[3]};
+      }
+    }
+  };
+
+  f4 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f4_zero();
+  if (n_ch > 0) load(0);
+  for (int ch = 0; ch < n_ch; ++ch) {
+    store(ch);
+    __syncthreads();
+    if (ch + 1 < n_ch) load(ch + 1);  // next chunk's rows fly during the MFMAs
+    const int k0 = 32 * half + 8 * lg;
+    const u32x4_t a = *reinterpret_cast<const u32x4_t*>(At + (16 * w + lr) * WGB_LDT + k0);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const u32x4_t b = *reinterpret_cast<const u32x4_t*>(Bt + (16 * t + lr) * WGB_LDT + k0);
+      acc[t] = mfma_bf16(a, b, acc[t]);
+    }
+    __syncthreads();
+  }
+  // the two halves' partial sums meet in LDS (fixed order: half 0 + half 1)
+  float* xch = reinterpret_cast<float*>(smem);  // [4 waves][NT][4][64]
+  if (half == 1) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) xch[((w * NT + t) * 4 + r) * 64 + lane] = acc[t][r];
+  }
+  __syncthreads();
+  if (half == 1) return;
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[t][r] += xch[((w * NT + t) * 4 + r) * 64 + lane];
+  float* slab = g.slabs + (int64_t)split * g.Ka * g.NC;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int ka = ka0 + 16 * w + 4 * lg + r;
+    if (ka >= g.Ka) continue;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int nb = nb0 + 16 * t + lr;
+      if (nb < g.NC) slab[(int64_t)ka * g.NC + nb] = acc[t][r];
+    }
+  }
+}
+
+template <int NT0, int NT1>
+__global__ __launch_bounds__(WG_THREADS) void wgrad_partial_bf16_kernel(WgradArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int panel = blockIdx.y;
+  if (panel < g.p[0].panels)
+    wgrad_panel_bf16<NT0>(g.p[0], g.offsets, g.B, g.rows_per_split, blockIdx.x, panel, smem);
+  else
+    wgrad_panel_bf16<NT1>(g.p[1], g.offsets, g.B, g.rows_per_split, blockIdx.x,
+                          panel - g.p[0].panels, smem);
+}
+
 // out = sum over splits (fixed order): a workgroup owns 16 outputs of one problem; thread
 // (o, grp) sums splits grp, grp+16, ... 8-deep, then the 16 partials are added in grp
 // order.  Blocks [0, blocks0) reduce problem 0, the rest problem 1.
@@ -288,7 +435,7 @@ static WgPlan wgrad_plan(int64_t max_rows, const int Ka[2], const int Nb[2]) {
   int target = 2 * device_cus() / (total_panels > 0 ? total_panels : 1);
   if (target < 1) target = 1;
   int64_t rps = (max_rows + target - 1) / target;
-  rps = ((rps + WG_CH - 1) / WG_CH) * WG_CH;
+  rps = ((rps + WGB_CH - 1) / WGB_CH) * WGB_CH;  // whole chunks of either panel kind
   if (rps < 4 * WG_CH) rps = 4 * WG_CH;
   pl.rps = rps;
   pl.n_splits = (int)((max_rows + rps - 1) / rps);
@@ -310,6 +457,25 @@ static void launch_partial_nt1(int nt1, const dim3& grid, size_t lds, hipStream_
   }
 }
 
+template <int NT0>
+static void launch_partial_bf16_nt1(int nt1, const dim3& grid, size_t lds, hipStream_t st, const WgradArgs& g) {
+  switch (nt1) {
+    case 4: hipLaunchKernelGGL((wgrad_partial_bf16_kernel<NT0, 4>), grid, dim3(WG_THREADS), lds, st, g); break;
+    case 8: hipLaunchKernelGGL((wgrad_partial_bf16_kernel<NT0, 8>), grid, dim3(WG_THREADS), lds, st, g); break;
+    case 13: hipLaunchKernelGGL((wgrad_partial_bf16_kernel<NT0, 13>), grid, dim3(WG_THREADS), lds, st, g); break;
+    default: hipLaunchKernelGGL((wgrad_partial_bf16_kernel<NT0, 16>), grid, dim3(WG_THREADS), lds, st, g); break;
+  }
+}
+
+static size_t lds_of_bf16(int nt) {
+  switch (nt) {
+    case 4: return WgCfgB<4>::LDS;
+    case 8: return WgCfgB<8>::LDS;
+    case 13: return WgCfgB<13>::LDS;
+    default: return WgCfgB<16>::LDS;
+  }
+}
+
 static size_t lds_of(int nt) {
   switch (nt) {
     case 4: return WgCfg<4>::LDS;
@@ -320,7 +486,7 @@ static size_t lds_of(int nt) {
 }
 
 static int wgrad_run(const WgradProb in[2], const int64_t* offsets, int B, int64_t max_rows,
-                     void* workspace, size_t ws_bytes, hipStream_t st) {
+                     void* workspace, size_t ws_bytes, hipStream_t st, bool bf16 = false) {
   const int Ka[2] = {in[0].Ka, in[1].a ? in[1].Ka : 0};
   const int Nb[2] = {in[0].Nb, in[1].a ? in[1].Nb : 0};
   if (max_rows == 0) {
@@ -354,17 +520,28 @@ static int wgrad_run(const WgradProb in[2], const int64_t* offsets, int B, int64
     blocks[i] = (int)(((int64_t)Ka[i] * g.p[i].NC + 15) / 16);
   }
   const int nt0 = pl.nt[0], nt1 = Ka[1] > 0 ? pl.nt[1] : 4;
-  const size_t l0 = lds_of(nt0), l1 = lds_of(nt1);
+  const size_t l0 = bf16 ? lds_of_bf16(nt0) : lds_of(nt0), l1 = bf16 ? lds_of_bf16(nt1) : lds_of(nt1);
   const size_t lds = l0 > l1 ? l0 : l1;
   const dim3 grid(pl.n_splits, g.p[0].panels + g.p[1].panels);
-  GR_TIMED("wgrad_partial", st, {
-    switch (nt0) {
-      case 4: launch_partial_nt1<4>(nt1, grid, lds, st, g); break;
-      case 8: launch_partial_nt1<8>(nt1, grid, lds, st, g); break;
-      case 13: launch_partial_nt1<13>(nt1, grid, lds, st, g); break;
-      default: launch_partial_nt1<16>(nt1, grid, lds, st, g); break;
-    }
-  });
+  if (bf16) {
+    GR_TIMED("wgrad_partial", st, {
+      switch (nt0) {
+        case 4: launch_partial_bf16_nt1<4>(nt1, grid, lds, st, g); break;
+        case 8: launch_partial_bf16_nt1<8>(nt1, grid, lds, st, g); break;
+        case 13: launch_partial_bf16_nt1<13>(nt1, grid, lds, st, g); break;
+        default: launch_partial_bf16_nt1<16>(nt1, grid, lds, st, g); break;
+      }
+    });
+  } else {
+    GR_TIMED("wgrad_partial", st, {
+      switch (nt0) {
+        case 4: launch_partial_nt1<4>(nt1, grid, lds, st, g); break;
+        case 8: launch_partial_nt1<8>(nt1, grid, lds, st, g); break;
+        case 13: launch_partial_nt1<13>(nt1, grid, lds, st, g); break;
+        default: launch_partial_nt1<16>(nt1, grid, lds, st, g); break;
+      }
+    });
+  }
   GR_LAUNCH_CHECK("gr_wgrad(partial)");
   GR_TIMED("wgrad_reduce", st, hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks[0] + blocks[1]),
                                                   dim3(256), 0, st, g, blocks[0]));
@@ -403,7 +580,7 @@ extern "C" int gr_wgrad(const float* a, int64_t lda, const float* a_stats, const
   return wgrad_run(p, offsets, B, max_rows, workspace, ws_bytes, (hipStream_t)stream);
 }
 
-extern "C" int gr_wgrad2(const float* a0, int64_t lda0, const float* a_stats0, const float* b0,
+static int gr_wgrad2_impl(bool bf16, const float* a0, int64_t lda0, const float* a_stats0, const float* b0,
                          int64_t ldb0, int Ka0, int Nb0, float* c0, float* colsum0,
                          const float* a1, int64_t lda1, const float* a_stats1, const float* b1,
                          int64_t ldb1, int Ka1, int Nb1, float* c1, float* colsum1,
@@ -418,5 +595,21 @@ extern "C" int gr_wgrad2(const float* a0, int64_t lda0, const float* a_stats0, c
   WgradProb p[2] = {};
   p[0] = WgradProb{a0, lda0, (const float2*)a_stats0, b0, ldb0, Ka0, Nb0, 0, 0, 0, nullptr, c0, colsum0};
   p[1] = WgradProb{a1, lda1, (const float2*)a_stats1, b1, ldb1, Ka1, Nb1, 0, 0, 0, nullptr, c1, colsum1};
-  return wgrad_run(p, offsets, B, max_rows, workspace, ws_bytes, (hipStream_t)stream);
+  return wgrad_run(p, offsets, B, max_rows, workspace, ws_bytes, (hipStream_t)stream, bf16);
+}
+extern "C" int gr_wgrad2(const float* a0, int64_t lda0, const float* a_stats0, const float* b0,
+                         int64_t ldb0, int Ka0, int Nb0, float* c0, float* colsum0,
+                         const float* a1, int64_t lda1, const float* a_stats1, const float* b1,
+                         int64_t ldb1, int Ka1, int Nb1, float* c1, float* colsum1,
+                         const int64_t* offsets, int B, int64_t max_rows, void* workspace,
+                         size_t ws_bytes, void* stream) {
+  return gr_wgrad2_impl(false, a0, lda0, a_stats0, b0, ldb0, Ka0, Nb0, c0, colsum0, a1, lda1, a_stats1, b1, ldb1, Ka1, Nb1, c1, colsum1, offsets, B, max_rows, workspace, ws_bytes, stream);
+}
+extern "C" int gr_wgrad2_bf16(const float* a0, int64_t lda0, const float* a_stats0, const float* b0,
+                         int64_t ldb0, int Ka0, int Nb0, float* c0, float* colsum0,
+                         const float* a1, int64_t lda1, const float* a_stats1, const float* b1,
+                         int64_t ldb1, int Ka1, int Nb1, float* c1, float* colsum1,
+                         const int64_t* offsets, int B, int64_t max_rows, void* workspace,
+                         size_t ws_bytes, void* stream) {
+  return gr_wgrad2_impl(true, a0, lda0, a_stats0, b0, ldb0, Ka0, Nb0, c0, colsum0, a1, lda1, a_stats1, b1, ldb1, Ka1, Nb1, c1, colsum1, offsets, B, max_rows, workspace, ws_bytes, stream);
 }

@@ -217,7 +217,7 @@ class STUGeometry:
     activation: int     # 1 = silu, 0 = none
     dropout_p: float
     max_len: int        # host bound on sequence lengths (<= N)
-    bf16: bool = False  # attention with bf16 MFMA operands (HSTU autocast_dtype=bfloat16)
+    bf16: bool = False  # bf16 MFMA operands (HSTU autocast_dtype=bfloat16): attention, projections, weight grads
     concat_ua: bool = False  # o_in = [u, LN(a), u * LN(a)] (hstu.py:398-400)
 
     @property
@@ -262,7 +262,8 @@ class STULayerFunction(torch.autograd.Function):
         # h_pre (pre-activation, for silu') and o_in (for the W_o gradient) exist only for
         # the backward: inference / no_grad forwards skip both writes
         h_pre = torch.empty_like(uvqk) if geo.activation and grad_on else None
-        _lib.call("hstu_ln_uvqk_fwd", x.data_ptr(), x.stride(0), offsets.data_ptr(), B, rows, D,
+        sfx = "_bf16" if geo.bf16 else ""  # bf16 MFMA operands in the projections too
+        _lib.call("hstu_ln_uvqk_fwd" + sfx, x.data_ptr(), x.stride(0), offsets.data_ptr(), B, rows, D,
                   w_uvqk.data_ptr(), n_out, geo.eps, geo.activation, x_stats.data_ptr(),
                   _lib.ptr(h_pre), uvqk.data_ptr(), n_out, st)
         attn = torch.empty(rows, hv, dtype=torch.float32, device=dev)
@@ -291,7 +292,7 @@ class STULayerFunction(torch.autograd.Function):
                       _lib.ptr(seed_offset), attn_stats.data_ptr(), _lib.ptr(o_in), y.data_ptr(),
                       D, st)
         else:
-            _lib.call("hstu_gate_o_fwd", uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
+            _lib.call("hstu_gate_o_fwd" + sfx, uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
                       offsets.data_ptr(), B, rows, hv, D, w_o.data_ptr(), b_o_c.data_ptr(),
                       x.data_ptr(), x.stride(0), geo.eps, geo.dropout_p, seed,
                       _lib.ptr(seed_offset), attn_stats.data_ptr(), _lib.ptr(o_in), y.data_ptr(),
@@ -326,7 +327,8 @@ class STULayerFunction(torch.autograd.Function):
                       _lib.ptr(ctx.seed_offset), d_uvqk.data_ptr(), n_out, d_attn.data_ptr(), hv,
                       st)
         else:
-            _lib.call("hstu_gate_o_bwd", dy.data_ptr(), D, offsets.data_ptr(), B, rows, hv, D,
+            _lib.call("hstu_gate_o_bwd" + ("_bf16" if geo.bf16 else ""), dy.data_ptr(), D,
+                      offsets.data_ptr(), B, rows, hv, D,
                       w_o.data_ptr(), uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
                       attn_stats.data_ptr(), _lib.ptr(h_pre), n_out, geo.dropout_p, ctx.seed,
                       _lib.ptr(ctx.seed_offset), d_uvqk.data_ptr(), n_out, d_attn.data_ptr(), hv, st)
@@ -360,7 +362,8 @@ class STULayerFunction(torch.autograd.Function):
                   hq_p, hk_p, hv_p, n_out, dq.data_ptr(), dk.data_ptr(), dvv.data_ptr(), n_out,
                   _lib.ptr(d_pos_w), _lib.ptr(d_ts_w), _lib.ptr(ws_a), ws_a_n, st)
         dx = torch.empty(rows, D, dtype=torch.float32, device=dev)
-        _lib.call("hstu_ln_uvqk_bwd", d_uvqk.data_ptr(), n_out, offsets.data_ptr(), B, rows, D,
+        _lib.call("hstu_ln_uvqk_bwd" + ("_bf16" if geo.bf16 else ""), d_uvqk.data_ptr(), n_out,
+                  offsets.data_ptr(), B, rows, D,
                   n_out, w_uvqk.data_ptr(), x.data_ptr(), x.stride(0), x_stats.data_ptr(),
                   dy.data_ptr(), D, dx.data_ptr(), D, st)
         # weight gradients (off the critical path): both GEMMs of the layer in one launch
@@ -375,7 +378,8 @@ class STULayerFunction(torch.autograd.Function):
         if want_uvqk and o_in is not None:
             ws_n = L.gr_wgrad2_workspace_size(rows, D, n_out, D, ow)
             ws = torch.empty(max(ws_n, 4), dtype=torch.uint8, device=dev)
-            _lib.call("gr_wgrad2", x.data_ptr(), x.stride(0), x_stats.data_ptr(), d_uvqk.data_ptr(),
+            _lib.call("gr_wgrad2_bf16" if geo.bf16 else "gr_wgrad2", x.data_ptr(), x.stride(0),
+                      x_stats.data_ptr(), d_uvqk.data_ptr(),
                       n_out, D, n_out, d_w_uvqk.data_ptr(), None,
                       dy.data_ptr(), D, None, o_in.data_ptr(), ow, D, ow, d_w_o.data_ptr(),
                       d_b_o.data_ptr(), offsets.data_ptr(), B, rows, ws.data_ptr(), ws_n, st)
