@@ -10,7 +10,7 @@ round-trip.  The compute is the fused jagged path: per layer 3 launches forward
 and 5 backward; nothing of size (B, N, N) is materialised.  ``concat_ua=True``
 (hstu.py:398-400) runs the concatenated gate [u, LN(a), u*LN(a)] in the same fused
 kernels (linear_dim * num_heads <= 64).  ``autocast_dtype=torch.bfloat16`` (an extension
-of the reference constructor, whose HSTUJagged takes it) selects bf16 attention operands.
+of the reference constructor, whose HSTUJagged takes it) selects bf16 MFMA operands.
 
 Not supported (raise): the incremental-decoding cache path (``delta_x_offsets`` /
 ``cache``, hstu.py:293-298, 415-418 — used by no config), ``normalization=
@@ -191,8 +191,9 @@ class HSTUJagged(torch.nn.Module):
                  autocast_dtype: Optional[torch.dtype]) -> None:
         """autocast_dtype (hstu.py:439-480): None / float32 = the reference's fp32 path
         (HSTU hard-wires None, hstu.py:592); torch.bfloat16 = the opt-in bf16 compute mode:
-        attention MFMA operands (Q, K, V, dO, P, dS) in bf16, fp32 accumulation,
-        elementwise and parameters (projections stay fp32)."""
+        MFMA operands in bf16 (attention Q, K, V, dO, P, dS; the UVQK / O projections and
+        their weight gradients, except the concat_ua gate GEMM), fp32 accumulation, LN,
+        elementwise work and parameters."""
         super().__init__()
         self._attention_layers = torch.nn.ModuleList(modules=modules)
         if autocast_dtype not in (None, torch.float32, torch.bfloat16):
@@ -263,7 +264,7 @@ class HSTU(torch.nn.Module):
         autocast_dtype: Optional[torch.dtype] = None,
     ) -> None:
         """Reference constructor (hstu.py:532-549) plus ``autocast_dtype`` (default None =
-        the reference's hard-wired fp32; torch.bfloat16 = the opt-in bf16 attention mode,
+        the reference's hard-wired fp32; torch.bfloat16 = the opt-in bf16 MFMA mode,
         see HSTUJagged)."""
         super().__init__()
         self._embedding_dim = embedding_dim
