@@ -62,8 +62,14 @@ GR_API int gr_timing_reset(void);
  *   GR_OPT_ATTN_BWD_SPLIT     0|1  f32 attention backward as separate dK/dV and dQ
  *                                  launches instead of the fused launch
  *   GR_OPT_ROWWAVE            0|1  row-wave GEMM kernels (default 1) or the row-panel ones
- *   GR_OPT_ATTN_BWD_PAIRS     0|1  f32 attention backward: workgroups take causal tile pairs
- *                                  (p, T-1-p) when that grid fits one round (default 1)
+ *   GR_OPT_ATTN_BWD_PAIRS   0|1|2  f32 attention backward: workgroups take causal tile pairs
+ *                                  (p, T-1-p): 1 = when that grid fits one round (default),
+ *                                  2 = always (64-row tiles), 0 = never
+ *   GR_OPT_ATTN_BWD_DS        0|1  f32 attention backward at N <= 512: the dK/dV pass stores
+ *                                  dS tiles and a second launch computes dQ = dS K without
+ *                                  recompute (default 0: the one-launch form, equally fast at C2;
+ *                                  hstu_attn_bwd_workspace_size covers the dS tiles only while
+ *                                  this is on)
  */
 enum {
   GR_OPT_MIPS_FILTER_FP32 = 1,
@@ -73,7 +79,8 @@ enum {
   GR_OPT_ATTN_BWD_SPLIT = 5,
   GR_OPT_ROWWAVE = 6,
   GR_OPT_ATTN_BWD_PAIRS = 7,
-  GR_OPT_COUNT_ = 8
+  GR_OPT_ATTN_BWD_DS = 8,
+  GR_OPT_COUNT_ = 9
 };
 GR_API int gr_set_option(int option, int64_t value);
 GR_API int64_t gr_get_option(int option);

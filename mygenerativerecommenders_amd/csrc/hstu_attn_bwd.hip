@@ -91,6 +91,8 @@ struct AttnBwdArgs {
   int cus;    // CU count (snake_rank)
   int vec2h;  // the same for the hq / hk / hv rows
   int paired; // workgroups run tile pairs (p, T-1-p); grid = B*H*ceil(T/2) per kind
+  float* ds;  // non-null: the dK/dV pass stores dS as 16 x 16 tiles for the dQ pass
+  int ds_tps; // dS tiles per (sequence, head): NB (NB + 1) / 2, NB = ceil(N / 16)
 };
 
 // TT = rows per streamed LDS tile (queries in dK/dV, keys in dQ): 64, or 16 for the
@@ -327,6 +329,12 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
 #ifdef GR_STAMP
           if (r == 3) GR_ST(st_ew, ds[0] + ds[1] + ds[2] + ds[3] + p[0] + p[1] + p[2] + p[3]);
 #endif
+        }
+        if (a.ds) {  // dS tile (query block, key block), row-major [query][key]
+          const int qbi = qb0 >> 4, kbi = wk_lo >> 4;
+          float* dt = a.ds + ((int64_t)bh * a.ds_tps + qbi * (qbi + 1) / 2 + kbi) * 256;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) dt[(4 * lg + r) * 16 + lr] = ds[r];
         }
         // Relative-bias gradients.  dpos_w: element (query 4lg + r, key lr) has diagonal
         // e = lr - (4lg + r); rotating row 4lg + r left by its index inside the 16-lane
@@ -721,12 +729,120 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& a, const int
   }  // pass
 }
 
+// ------------------------------------------------------------------ query-major from dS
+// dQ = dS K from the dS tiles the key-major pass stored (no recompute of S, dP, the
+// bias or the SiLU terms): per 16 x 16 block a lane's A fragment is one float4 of the
+// row-major tile (query lr, keys 4lg .. 4lg + 3 = k-steps 0..3, the order the
+// recomputing query-major pass uses), B = the K tile staged in LDS.  Sums run in the
+// same key order as the recomputing pass, so dQ is unchanged.
+template <int KSTEPS, int VTILES, int TT>
+__device__ __forceinline__ void attn_bwd_dq_ds_body(const AttnBwdArgs& a, const int id) {
+  using C = AttnBwdCfg<KSTEPS, VTILES, TT>;
+  static_assert(TT == 64, "dQ from dS: 64-row tiles");
+  constexpr int LDK = C::LDQ;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* Ks = reinterpret_cast<float*>(smem);  // [TT][LDK]
+  const int BH = a.B * a.H;
+  const int rank = snake_rank(id, a.cus);
+  const int qt = a.n_tiles - 1 - rank / BH;
+  const int bh = rank % BH;
+  const int b = bh / a.H, h = bh % a.H;
+  const int64_t s0 = a.offsets[b];
+  const int L = (int)(a.offsets[b + 1] - s0);
+  const int q0 = qt * 64;
+  if (q0 >= L) return;
+  const int tid = threadIdx.x, w = wave_id(), lane = tid & 63;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int wq_lo = q0 + w * 16;
+  const int qbi = wq_lo >> 4;
+  const bool w_ok = wq_lo < L;  // wave-uniform: no valid query row otherwise
+  const __amdgpu_buffer_rsrc_t rk = seq_rsrc(a.k, a.ld_qk, s0, h * a.dqk, L, a.dqk);
+  const float* dsq = a.ds + ((int64_t)bh * a.ds_tps + qbi * (qbi + 1) / 2) * 256 + lr * 16 + 4 * lg;
+  f4 dQ[C::KT];
+#pragma unroll
+  for (int t = 0; t < C::KT; ++t) dQ[t] = f4_zero();
+  BufTile<C::KPT, TT> kst;
+  f4 dsv[C::TB], dsn[C::TB];
+  auto load_tile = [&](int kt, f4 (&d)[C::TB]) {
+    kst.load(rk, a.ld_qk, kt * TT, a.dqk, a.vec2);
+#pragma unroll
+    for (int kb = 0; kb < C::TB; ++kb) {
+      const int kbi = (kt * TT + kb * 16) >> 4;
+      d[kb] = (w_ok && kbi <= qbi) ? *reinterpret_cast<const f4*>(dsq + kbi * 256) : f4_zero();
+    }
+  };
+  load_tile(0, dsv);
+  kst.store(Ks, LDK, a.vec2);
+  __syncthreads();
+  const int last_kt = min(q0 + 63, L - 1) / TT;
+  for (int kt = 0; kt <= last_kt; ++kt) {
+    const int k0 = kt * TT;
+    const bool more = kt < last_kt;
+    if (more) {
+      load_tile(kt + 1, dsn);
+    } else if (a.hq) {  // the epilogue's silu'(h) rows of this workgroup's queries
+      kst.load(seq_rsrc(a.hq, a.ld_h, s0, h * a.dqk, L, a.dqk), a.ld_h, q0, a.dqk, a.vec2h);
+    }
+#pragma unroll
+    for (int kb = 0; kb < C::TB; ++kb) {
+      const int kb0 = k0 + kb * 16;
+      if (w_ok && kb0 <= wq_lo + 15 && kb0 < L) {
+        const float* kcol = Ks + (kb * 16 + 4 * lg) * LDK + lr;
+        float bk[2][C::KT];
+#pragma unroll
+        for (int t = 0; t < C::KT; ++t) bk[0][t] = kcol[t * 16];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (r + 1 < 4) {
+#pragma unroll
+            for (int t = 0; t < C::KT; ++t) bk[(r + 1) & 1][t] = kcol[(r + 1) * LDK + t * 16];
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int t = 0; t < C::KT; ++t) dQ[t] = mfma16x16x4(dsv[kb][r], bk[r & 1][t], dQ[t]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    }
+    if (more) {
+      lds_barrier();
+      kst.store(Ks, LDK, a.vec2);
+#pragma unroll
+      for (int kb = 0; kb < C::TB; ++kb) dsv[kb] = dsn[kb];
+      lds_barrier();
+    }
+  }
+  if (a.hq) {
+    lds_barrier();
+    kst.store(Ks, LDK, a.vec2h);
+    lds_barrier();
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int qo = wq_lo + 4 * lg + r;
+    const bool row_ok = qo < L;
+    const int64_t row = s0 + (row_ok ? qo : L - 1);
+#pragma unroll
+    for (int t = 0; t < C::KT; ++t) {
+      const int c = t * 16 + lr;
+      const bool ok = row_ok && c < a.dqk;
+      float g = dQ[t][r];
+      if (a.hq) g *= ok ? silu_grad_(Ks[(w * 16 + 4 * lg + r) * LDK + c]) : 0.f;
+      if (ok) a.dq[row * a.ld_d + h * a.dqk + c] = g;
+    }
+  }
+}
+
 // ------------------------------------------------------------------ entry points
 template <int KSTEPS, int VTILES, int TT, bool HB>
 __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
   GR_TL_BEGIN();
   attn_bwd_dkv_body<KSTEPS, VTILES, TT, HB>(a, blockIdx.x);
   GR_TL_END(blockIdx.x, 0);
+}
+template <int KSTEPS, int VTILES, int TT>
+__global__ __launch_bounds__(256) void attn_bwd_dq_ds_kernel(AttnBwdArgs a) {
+  if constexpr (TT == 64) attn_bwd_dq_ds_body<KSTEPS, VTILES, TT>(a, blockIdx.x);
 }
 template <int KSTEPS, int VTILES, int TT, bool HB>
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
@@ -788,6 +904,19 @@ static size_t bwd_slab_bytes(int B, int N, int max_len, int H, int nb) {
   const int n_tiles = ceil_div(max_len, 64);
   return sizeof(float) * (size_t)n_tiles * B * H * (size_t)(2 * N - 1 + nb + 1);
 }
+// dS tiles of the two-pass backward (short sequences: N <= 512), after the slabs
+constexpr int DS_MAX_N = 512;
+static int ds_tiles_per_seq(int N) {
+  const int nb = ceil_div(N, 16);
+  return nb * (nb + 1) / 2;
+}
+static size_t bwd_ds_offset(int B, int N, int max_len, int H, int nb) {
+  return (bwd_slab_bytes(B, N, max_len, H, nb) + 255) & ~(size_t)255;
+}
+static size_t bwd_ds_bytes(int B, int N, int H) {
+  return N <= DS_MAX_N && option(GR_OPT_ATTN_BWD_DS) != 0
+             ? sizeof(float) * 256 * (size_t)ds_tiles_per_seq(N) * B * H : 0;
+}
 
 template <int KS, int VT, int TT = 64>
 static int launch_bwd(const AttnBwdArgs& a, float* dpos_w, float* dts_w, hipStream_t st) {
@@ -808,13 +937,27 @@ static int launch_bwd(const AttnBwdArgs& a, float* dpos_w, float* dts_w, hipStre
   // tiles, heaviest first (LPT order).
   const int pgrid = ceil_div(a.n_tiles, 2) * a.B * a.H;
   const bool pairs_on = option(GR_OPT_ATTN_BWD_PAIRS) != 0 && a.n_tiles > 1 && TT == 64;
+  const bool pairs_force = option(GR_OPT_ATTN_BWD_PAIRS) == 2 && a.n_tiles > 1 && TT == 64;
   int n_slabs = grid;
-  if (!split && C::KT <= 8) {
+  if (TT == 64 && a.ds && !split) {
+    // two passes: dK/dV (+ dS tiles), then dQ = dS K with nothing recomputed
+    auto kkv = a.map_kq ? attn_bwd_dkv_kernel<KS, VT, TT, true> : attn_bwd_dkv_kernel<KS, VT, TT, false>;
+    AttnBwdArgs akv = a, aq = a;
+    const int s_kv = device_cus() * resident_wgs(kkv, lds_kv);
+    akv.paired = pairs_force || (pairs_on && grid > s_kv && pgrid <= s_kv);
+    n_slabs = akv.paired ? pgrid : grid;
+    GR_TIMED("attn_bwd_dkv", st, hipLaunchKernelGGL(kkv, dim3(n_slabs), dim3(256), lds_kv, st, akv));
+    GR_LAUNCH_CHECK("hstu_attn_bwd(dkv)");
+    aq.paired = 0;
+    const size_t lds_dq = sizeof(float) * TT * C::LDQ;
+    GR_TIMED("attn_bwd_dq", st, hipLaunchKernelGGL((attn_bwd_dq_ds_kernel<KS, VT, TT>), dim3(grid), dim3(256), lds_dq, st, aq));
+    GR_LAUNCH_CHECK("hstu_attn_bwd(dq from dS)");
+  } else if (!split && C::KT <= 8) {
     const size_t lds = lds_kv > lds_q ? lds_kv : lds_q;
     auto kern = a.map_kq ? attn_bwd_fused_kernel<KS, VT, TT, true> : attn_bwd_fused_kernel<KS, VT, TT, false>;
     AttnBwdArgs af = a;
     const int slots = device_cus() * resident_wgs(kern, lds);
-    af.paired = pairs_on && 2 * grid > slots && 2 * pgrid <= slots;
+    af.paired = pairs_force || (pairs_on && 2 * grid > slots && 2 * pgrid <= slots);
     const int g = af.paired ? pgrid : grid;
     n_slabs = g;
     GR_TIMED("attn_bwd", st, hipLaunchKernelGGL(kern, dim3(2 * g), dim3(256), lds, st, af, g));
@@ -824,8 +967,8 @@ static int launch_bwd(const AttnBwdArgs& a, float* dpos_w, float* dts_w, hipStre
     auto kq = a.map_qk ? attn_bwd_dq_kernel<KS, VT, TT, true> : attn_bwd_dq_kernel<KS, VT, TT, false>;
     AttnBwdArgs akv = a, aq = a;
     const int s_kv = device_cus() * resident_wgs(kkv, lds_kv), s_q = device_cus() * resident_wgs(kq, lds_q);
-    akv.paired = pairs_on && grid > s_kv && pgrid <= s_kv;
-    aq.paired = pairs_on && grid > s_q && pgrid <= s_q;
+    akv.paired = pairs_force || (pairs_on && grid > s_kv && pgrid <= s_kv);
+    aq.paired = pairs_force || (pairs_on && grid > s_q && pgrid <= s_q);
     n_slabs = akv.paired ? pgrid : grid;
     GR_TIMED("attn_bwd_dkv", st, hipLaunchKernelGGL(kkv, dim3(n_slabs), dim3(256), lds_kv, st, akv));
     GR_LAUNCH_CHECK("hstu_attn_bwd(dkv)");
@@ -854,7 +997,9 @@ extern "C" __attribute__((visibility("default"))) int gr_timeline_read(unsigned 
 extern "C" size_t hstu_attn_bwd_workspace_size(int B, int N, int max_len, int H,
                                                int num_buckets) {
   if (B <= 0 || N <= 0 || H <= 0 || max_len <= 0) return 0;
-  return gr::bwd_slab_bytes(B, N, max_len, H, num_buckets);
+  const size_t ds = gr::bwd_ds_bytes(B, N, H);
+  return ds ? gr::bwd_ds_offset(B, N, max_len, H, num_buckets) + ds
+            : gr::bwd_slab_bytes(B, N, max_len, H, num_buckets);
 }
 
 extern "C" int hstu_attn_bwd(const float* q, const float* k, const float* v, int64_t ld_qk,
@@ -897,6 +1042,12 @@ extern "C" int hstu_attn_bwd(const float* q, const float* k, const float* v, int
   a.cus = (int64_t)a.n_tiles * B * H <= 2 * device_cus() ? device_cus() : (1 << 30);
   a.vec2 = pair_aligned({q, k, v, dout}, {ld_qk, ld_v, ld_dout, dqk, dv});
   a.vec2h = hq ? pair_aligned({hq, hk, hv}, {ld_h, dqk, dv}) : 0;
+  // short sequences with a workspace large enough for the dS tiles: two-pass backward
+  if (bucket_map && bwd_ds_bytes(B, N, H) && option(GR_OPT_ATTN_BWD_DS) != 0 &&
+      ws_bytes >= bwd_ds_offset(B, N, max_len, H, num_buckets) + bwd_ds_bytes(B, N, H)) {
+    a.ds = (float*)((char*)workspace + bwd_ds_offset(B, N, max_len, H, num_buckets));
+    a.ds_tps = ds_tiles_per_seq(N);
+  }
   const int d = dqk > dv ? dqk : dv;
   if (d <= 8) return launch_bwd<2, 1>(a, dpos_w, dts_w, st);
   if (d <= 16) return launch_bwd<4, 1>(a, dpos_w, dts_w, st);

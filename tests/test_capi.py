@@ -60,7 +60,13 @@ def test_error_is_raised_as_python_exception():
 
 def test_workspace_size_queries_are_host_only():
     L = _lib.lib()
-    assert L.hstu_attn_bwd_workspace_size(128, 211, 200, 1, 128) == 4 * 128 * 4 * (2 * 211 - 1 + 129)
+    slabs = 4 * 128 * 4 * (2 * 211 - 1 + 129)
+    assert L.hstu_attn_bwd_workspace_size(128, 211, 200, 1, 128) == slabs
+    ds = 4 * 256 * 14 * 15 // 2 * 128  # dS tiles of the two-pass backward (N <= 512)
+    with _lib.option("ATTN_BWD_DS", 1):
+        assert L.hstu_attn_bwd_workspace_size(128, 211, 200, 1, 128) == (slabs + 255) // 256 * 256 + ds
+    slabs3 = 4 * 32 * 32 * (2 * 2059 - 1 + 129)
+    assert L.hstu_attn_bwd_workspace_size(32, 2059, 2048, 1, 128) == slabs3  # no dS above 512
     assert L.hstu_bucket_map_bytes(128, 211) == 2 * 128 * 10 * 4096
     assert L.mips_packed_items_bytes(3953, 50) == 4 * ((3953 + 15) // 16) * 7 * 128
     # filter-sized catalogs: f32 blocks | bf16 copy (2 k-chunks of 32 dims) | max norm |
@@ -83,7 +89,8 @@ def test_launch_options_are_explicit_not_environment():
     """Launch options go through gr_set_option; the library reads no environment."""
     opts = _lib.parse_options()
     assert set(opts) == {"MIPS_FILTER_FP32", "MIPS_FILTER_WGS", "MIPS_FILTER_ROUNDS",
-                         "MIPS_FORCE_FALLBACK", "ATTN_BWD_SPLIT", "ROWWAVE", "ATTN_BWD_PAIRS"}
+                         "MIPS_FORCE_FALLBACK", "ATTN_BWD_SPLIT", "ROWWAVE", "ATTN_BWD_PAIRS",
+                         "ATTN_BWD_DS"}
     defaults = {"MIPS_FILTER_WGS": 2, "ROWWAVE": 1, "ATTN_BWD_PAIRS": 1}
     for n in opts:
         assert _lib.get_option(n) == defaults.get(n, 0), n

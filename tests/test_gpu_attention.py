@@ -220,6 +220,38 @@ def test_attn_bwd_fused_silu_grad():
     _close(b[2], a[2] * sg[:, hv:2 * hv])
 
 
+@pytest.mark.parametrize("B,N,d", [(6, 211, 50), (5, 150, 64), (4, 300, 32)])
+def test_attn_bwd_launch_modes_bitexact(B, N, d):
+    """Every f32 backward launch form -- one fused launch (single tiles or tile pairs),
+    split dK/dV + dQ launches, and the two-pass form with stored dS -- sums dQ, dK and dV
+    in the same order: bit-identical.  The relative-bias gradients are deterministic in
+    each form, but a tile pair shares one slab (its two tiles' partials meet in LDS
+    before the slab reduce), so across forms they agree to fp32 rounding."""
+    from mygenerativerecommenders_amd import _lib
+    lengths, offsets, uvqk, ts, pos_w, ts_w = _case(31 + N, B, N, 1, d, d)
+    g = torch.Generator().manual_seed(3)
+    dout = torch.randn(uvqk.shape[0], d, generator=g)
+    hpre = torch.randn(uvqk.shape, generator=g)
+    modes = [{}, {"ATTN_BWD_PAIRS": 2}, {"ATTN_BWD_PAIRS": 0}, {"ATTN_BWD_SPLIT": 1},
+             {"ATTN_BWD_DS": 1}, {"ATTN_BWD_DS": 1, "ATTN_BWD_PAIRS": 2}]
+    outs = []
+    for m in modes:
+        old = {k: _lib.set_option(k, v) for k, v in m.items()}
+        try:
+            outs.append(_run_gpu_bwd(offsets, uvqk, dout, ts, pos_w, ts_w, B, N, 1, d, d,
+                                     hpre=hpre))
+        finally:
+            for k, v in old.items():
+                _lib.set_option(k, v)
+    for m, o in zip(modes[1:], outs[1:]):
+        for i, (x, y) in enumerate(zip(outs[0], o)):
+            assert torch.isfinite(x).all() and torch.isfinite(y).all()
+            if i < 3:
+                assert torch.equal(x, y), (m, i, (x - y).abs().max().item())
+            else:
+                _close(y, x, rel=1e-6)
+
+
 def test_bucket_map_vs_reference_semantics():
     """Every causal (i, j) bucket of the device map equals the reference bucket fn
     (hstu.py:579-581 on ts_next(i) - ts(j)), including full-length rows (ts[N-1] wrap)
