@@ -484,7 +484,14 @@ def main():
     from mygenerativerecommenders_amd.ops import get_current_embeddings
     from mygenerativerecommenders_amd.top_k import MIPSBruteForceTopK
 
-    rank, world, local = init_from_env()
+    # GR_BENCH_SHARED_GPU=1: rehearsal of the N > 1 path on a one-GPU box (every rank on
+    # cuda:0, gloo instead of RCCL); numbers from such a run are not scaling results
+    shared = os.environ.get("GR_BENCH_SHARED_GPU") == "1"
+    if shared:
+        torch.cuda.set_device(0)
+    rank, world, local = init_from_env("gloo" if shared else None)
+    if shared:
+        local = 0
     if world != args.gpus and rank == 0:
         print(f"# note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", flush=True)
     device = torch.device("cuda", local)
