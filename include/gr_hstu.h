@@ -65,11 +65,12 @@ GR_API int gr_timing_reset(void);
  *   GR_OPT_ATTN_BWD_PAIRS   0|1|2  f32 attention backward: workgroups take causal tile pairs
  *                                  (p, T-1-p): 1 = when that grid fits one round (default),
  *                                  2 = always (64-row tiles), 0 = never
- *   GR_OPT_ATTN_BWD_DS        0|1  f32 attention backward at N <= 512: the dK/dV pass stores
- *                                  dS tiles and a second launch computes dQ = dS K without
- *                                  recompute (default 0: the one-launch form, equally fast at C2;
- *                                  hstu_attn_bwd_workspace_size covers the dS tiles only while
- *                                  this is on)
+ *   GR_OPT_ATTN_BWD_DS      0|1|2  f32 attention backward at N <= 512: the dK/dV pass stores dS
+ *                                  tiles and dQ = dS K runs without recompute, 1 = in a second
+ *                                  launch, 2 = in the same launch (the dQ workgroups take each
+ *                                  key tile's dS once its producer publishes it); default 0 =
+ *                                  the recomputing one-launch form.  The workspace size
+ *                                  (hstu_attn_bwd_workspace_size) depends on this option.
  */
 enum {
   GR_OPT_MIPS_FILTER_FP32 = 1,

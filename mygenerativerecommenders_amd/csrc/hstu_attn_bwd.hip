@@ -93,6 +93,7 @@ struct AttnBwdArgs {
   int paired; // workgroups run tile pairs (p, T-1-p); grid = B*H*ceil(T/2) per kind
   float* ds;  // non-null: the dK/dV pass stores dS as 16 x 16 tiles for the dQ pass
   int ds_tps; // dS tiles per (sequence, head): NB (NB + 1) / 2, NB = ceil(N / 16)
+  uint32_t* ds_flags;  // one-launch form: [bh][key tile] = 1 once that tile's dS is published
 };
 
 // TT = rows per streamed LDS tile (queries in dK/dV, keys in dQ): 64, or 16 for the
@@ -460,6 +461,19 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
     }
   }
 #endif
+  if (a.ds_flags) {
+    // publish this key tile's dS tiles (plain stores, one agent-scope release, flag by an
+    // atomic store): every wave drains its stores before the barrier, the releasing lane
+    // waits again after the fence (cdna_hip_programming.md Guideline 16)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(a.ds_flags + (int64_t)bh * a.n_tiles + kt, 1u, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
   if (STAGED && a.hv) {
     lds_barrier();
     qst.store(Qs, C::LDQ, a.vec2h);
@@ -735,13 +749,18 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& a, const int
 // row-major tile (query lr, keys 4lg .. 4lg + 3 = k-steps 0..3, the order the
 // recomputing query-major pass uses), B = the K tile staged in LDS.  Sums run in the
 // same key order as the recomputing pass, so dQ is unchanged.
-template <int KSTEPS, int VTILES, int TT>
-__device__ __forceinline__ void attn_bwd_dq_ds_body(const AttnBwdArgs& a, const int id) {
+// WAIT (one-launch form): the key tiles are taken in DESCENDING order, each after its
+// producer workgroup's flag (one lane polls relaxed with s_sleep, then one agent-scope
+// acquire and a barrier); a spin that exceeds its bound returns false before anything
+// is written and the caller recomputes the tile instead, so no schedule can hang it.
+template <int KSTEPS, int VTILES, int TT, bool WAIT = false>
+__device__ __forceinline__ bool attn_bwd_dq_ds_body(const AttnBwdArgs& a, const int id) {
   using C = AttnBwdCfg<KSTEPS, VTILES, TT>;
   static_assert(TT == 64, "dQ from dS: 64-row tiles");
   constexpr int LDK = C::LDQ;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* Ks = reinterpret_cast<float*>(smem);  // [TT][LDK]
+  int* wstat = reinterpret_cast<int*>(Ks + TT * LDK);
   const int BH = a.B * a.H;
   const int rank = snake_rank(id, a.cus);
   const int qt = a.n_tiles - 1 - rank / BH;
@@ -750,11 +769,32 @@ __device__ __forceinline__ void attn_bwd_dq_ds_body(const AttnBwdArgs& a, const 
   const int64_t s0 = a.offsets[b];
   const int L = (int)(a.offsets[b + 1] - s0);
   const int q0 = qt * 64;
-  if (q0 >= L) return;
+  if (q0 >= L) return true;
   const int tid = threadIdx.x, w = wave_id(), lane = tid & 63;
   const int lr = lane & 15, lg = lane >> 4;
   const int wq_lo = q0 + w * 16;
   const int qbi = wq_lo >> 4;
+  // WAIT: tile j of the walk is key tile last_kt - j
+  auto wait_tile = [&](int kt) -> bool {
+    if (tid == 0) {
+      const uint32_t* f = a.ds_flags + (int64_t)bh * a.n_tiles + kt;
+      int ok = 1;
+      for (uint32_t spins = 0; __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 1u;) {
+        __builtin_amdgcn_s_sleep(4);
+        if (++spins > (1u << 20)) {  // ~ms: give up, recompute instead
+          ok = 0;
+          break;
+        }
+      }
+      if (ok) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      wstat[0] = ok;
+    }
+    __syncthreads();
+    return wstat[0] != 0;
+  };
   const bool w_ok = wq_lo < L;  // wave-uniform: no valid query row otherwise
   const __amdgpu_buffer_rsrc_t rk = seq_rsrc(a.k, a.ld_qk, s0, h * a.dqk, L, a.dqk);
   const float* dsq = a.ds + ((int64_t)bh * a.ds_tps + qbi * (qbi + 1) / 2) * 256 + lr * 16 + 4 * lg;
@@ -771,15 +811,19 @@ __device__ __forceinline__ void attn_bwd_dq_ds_body(const AttnBwdArgs& a, const 
       d[kb] = (w_ok && kbi <= qbi) ? *reinterpret_cast<const f4*>(dsq + kbi * 256) : f4_zero();
     }
   };
-  load_tile(0, dsv);
+  const int last_kt = min(q0 + 63, L - 1) / TT;
+  auto tile_of = [&](int j) { return WAIT ? last_kt - j : j; };
+  if (WAIT && !wait_tile(tile_of(0))) return false;
+  load_tile(tile_of(0), dsv);
   kst.store(Ks, LDK, a.vec2);
   __syncthreads();
-  const int last_kt = min(q0 + 63, L - 1) / TT;
-  for (int kt = 0; kt <= last_kt; ++kt) {
+  for (int j = 0; j <= last_kt; ++j) {
+    const int kt = tile_of(j);
     const int k0 = kt * TT;
-    const bool more = kt < last_kt;
+    const bool more = j < last_kt;
     if (more) {
-      load_tile(kt + 1, dsn);
+      if (WAIT && !wait_tile(tile_of(j + 1))) return false;
+      load_tile(tile_of(j + 1), dsn);
     } else if (a.hq) {  // the epilogue's silu'(h) rows of this workgroup's queries
       kst.load(seq_rsrc(a.hq, a.ld_h, s0, h * a.dqk, L, a.dqk), a.ld_h, q0, a.dqk, a.vec2h);
     }
@@ -831,6 +875,7 @@ __device__ __forceinline__ void attn_bwd_dq_ds_body(const AttnBwdArgs& a, const 
       if (ok) a.dq[row * a.ld_d + h * a.dqk + c] = g;
     }
   }
+  return true;
 }
 
 // ------------------------------------------------------------------ entry points
@@ -843,6 +888,24 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
 template <int KSTEPS, int VTILES, int TT>
 __global__ __launch_bounds__(256) void attn_bwd_dq_ds_kernel(AttnBwdArgs a) {
   if constexpr (TT == 64) attn_bwd_dq_ds_body<KSTEPS, VTILES, TT>(a, blockIdx.x);
+}
+// One launch, dS handed over inside it: workgroups [0, grid_kv) are the key-major pass
+// (publishing each key tile's dS), the rest compute dQ = dS K as the tiles appear (a
+// workgroup that times out waiting recomputes its tile, attn_bwd_dq_body).  All key-major
+// workgroups precede the dQ ones in dispatch order.
+template <int KSTEPS, int VTILES, int TT, bool HB>
+__global__ __launch_bounds__(256) void attn_bwd_fused_ds_kernel(AttnBwdArgs a, int grid_kv) {
+  const int id = blockIdx.x;
+  if constexpr (TT == 64) {
+    if (id < grid_kv) {
+      attn_bwd_dkv_body<KSTEPS, VTILES, TT, HB>(a, id);
+    } else if (!attn_bwd_dq_ds_body<KSTEPS, VTILES, TT, true>(a, id - grid_kv)) {
+      __syncthreads();
+      AttnBwdArgs aq = a;
+      aq.paired = 0;  // the dQ workgroups are single-tile whatever the key-major pairing
+      attn_bwd_dq_body<KSTEPS, VTILES, TT, HB>(aq, id - grid_kv);
+    }
+  }
 }
 template <int KSTEPS, int VTILES, int TT, bool HB>
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
@@ -917,6 +980,10 @@ static size_t bwd_ds_bytes(int B, int N, int H) {
   return N <= DS_MAX_N && option(GR_OPT_ATTN_BWD_DS) != 0
              ? sizeof(float) * 256 * (size_t)ds_tiles_per_seq(N) * B * H : 0;
 }
+// one-launch form (GR_OPT_ATTN_BWD_DS = 2): a flag word per (sequence, head, key tile)
+static size_t bwd_flag_bytes(int B, int max_len, int H) {
+  return option(GR_OPT_ATTN_BWD_DS) == 2 ? 256 + sizeof(uint32_t) * (size_t)B * H * ceil_div(max_len, 64) : 0;
+}
 
 template <int KS, int VT, int TT = 64>
 static int launch_bwd(const AttnBwdArgs& a, float* dpos_w, float* dts_w, hipStream_t st) {
@@ -939,7 +1006,18 @@ static int launch_bwd(const AttnBwdArgs& a, float* dpos_w, float* dts_w, hipStre
   const bool pairs_on = option(GR_OPT_ATTN_BWD_PAIRS) != 0 && a.n_tiles > 1 && TT == 64;
   const bool pairs_force = option(GR_OPT_ATTN_BWD_PAIRS) == 2 && a.n_tiles > 1 && TT == 64;
   int n_slabs = grid;
-  if (TT == 64 && a.ds && !split) {
+  if (TT == 64 && a.ds && a.ds_flags && !split) {
+    // one launch: the dQ workgroups consume each key tile's dS as soon as it is published
+    auto kern = a.map_kq ? attn_bwd_fused_ds_kernel<KS, VT, TT, true> : attn_bwd_fused_ds_kernel<KS, VT, TT, false>;
+    AttnBwdArgs af = a;
+    const size_t lds = (lds_kv > lds_q ? lds_kv : lds_q) + 16;
+    af.paired = pairs_force;  // key-major pairs only on request (PAIRS = 2)
+    const int g = af.paired ? pgrid : grid;
+    n_slabs = g;
+    zero_words_async(a.ds_flags, (int64_t)a.B * a.H * a.n_tiles, st);
+    GR_TIMED("attn_bwd", st, hipLaunchKernelGGL(kern, dim3(g + grid), dim3(256), lds, st, af, g));
+    GR_LAUNCH_CHECK("hstu_attn_bwd(fused dS)");
+  } else if (TT == 64 && a.ds && !split) {
     // two passes: dK/dV (+ dS tiles), then dQ = dS K with nothing recomputed
     auto kkv = a.map_kq ? attn_bwd_dkv_kernel<KS, VT, TT, true> : attn_bwd_dkv_kernel<KS, VT, TT, false>;
     AttnBwdArgs akv = a, aq = a;
@@ -998,7 +1076,7 @@ extern "C" size_t hstu_attn_bwd_workspace_size(int B, int N, int max_len, int H,
                                                int num_buckets) {
   if (B <= 0 || N <= 0 || H <= 0 || max_len <= 0) return 0;
   const size_t ds = gr::bwd_ds_bytes(B, N, H);
-  return ds ? gr::bwd_ds_offset(B, N, max_len, H, num_buckets) + ds
+  return ds ? gr::bwd_ds_offset(B, N, max_len, H, num_buckets) + ds + gr::bwd_flag_bytes(B, max_len, H)
             : gr::bwd_slab_bytes(B, N, max_len, H, num_buckets);
 }
 
@@ -1047,6 +1125,9 @@ extern "C" int hstu_attn_bwd(const float* q, const float* k, const float* v, int
       ws_bytes >= bwd_ds_offset(B, N, max_len, H, num_buckets) + bwd_ds_bytes(B, N, H)) {
     a.ds = (float*)((char*)workspace + bwd_ds_offset(B, N, max_len, H, num_buckets));
     a.ds_tps = ds_tiles_per_seq(N);
+    const size_t fo = (bwd_ds_offset(B, N, max_len, H, num_buckets) + bwd_ds_bytes(B, N, H) + 255) & ~(size_t)255;
+    if (option(GR_OPT_ATTN_BWD_DS) == 2 && ws_bytes >= fo + bwd_flag_bytes(B, max_len, H) - 256)
+      a.ds_flags = (uint32_t*)((char*)workspace + fo);
   }
   const int d = dqk > dv ? dqk : dv;
   if (d <= 8) return launch_bwd<2, 1>(a, dpos_w, dts_w, st);

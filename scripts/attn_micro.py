@@ -42,7 +42,8 @@ def main():
     ap.add_argument("--split", action="store_true", help="f32 backward as separate dK/dV, dQ launches")
     ap.add_argument("--nopairs", action="store_true", help="f32 backward: one tile per workgroup")
     ap.add_argument("--pairs", type=int, default=1, help="GR_OPT_ATTN_BWD_PAIRS (0/1/2)")
-    ap.add_argument("--ds", action="store_true", help="f32 backward: two-pass form with stored dS")
+    ap.add_argument("--ds", type=int, default=0, nargs="?", const=1,
+                    help="f32 backward dS forms: 1 = two launches, 2 = in-launch hand-off")
     ap.add_argument("--hepi", action="store_true",
                     help="fused silu'(h) epilogue on dQ/dK/dV (as in the training step)")
     args = ap.parse_args()
@@ -74,7 +75,7 @@ def main():
     L_ = _lib.lib()
     _lib.set_option("ATTN_BWD_SPLIT", int(args.split))
     _lib.set_option("ATTN_BWD_PAIRS", 0 if args.nopairs else args.pairs)
-    _lib.set_option("ATTN_BWD_DS", int(args.ds))
+    _lib.set_option("ATTN_BWD_DS", int(args.ds))  # before the workspace size query
     ws_n = (L_.hstu_attn_bwd_bf16_workspace_size(B, N, L, H, d, d, 128) if args.bf16
             else L_.hstu_attn_bwd_workspace_size(B, N, L, H, 128))
     ws = torch.empty(max(ws_n, 4), dtype=torch.uint8, device=dev)
