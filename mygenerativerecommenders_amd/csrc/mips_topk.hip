@@ -801,11 +801,14 @@ __global__ __launch_bounds__(256) void mips_merge_kernel(MergeArgs a) {
 }
 
 // ----------------------------------------------------------------- small catalogs
-// X <= MERGE_MAX: a workgroup per query scores every item (the same k-ordered fmaf chain,
-// read from the packed layout), excludes its invalid ids (arange ids: direct index
-// scatter after the scores are written; explicit ids: binary search in the sorted list)
-// and hands all X scores to the merge kernel as one candidate list.  Replaces the
-// range/threshold machinery, whose fixed per-workgroup costs dominate at ml-1m sizes.
+// X <= MERGE_MAX: workgroup (query, chunk) scores one chunk of the items (the same
+// k-ordered fmaf chain, read from the packed layout), excludes its invalid ids (arange
+// ids: direct index scatter after the scores are written; explicit ids: binary search in
+// the sorted list) and writes the scores into the query's one candidate list for the
+// merge kernel.  Replaces the range/threshold machinery, whose fixed per-workgroup costs
+// dominate at ml-1m sizes.  Chunks (blockIdx.y) spread a query over several CUs: with
+// one workgroup per query the 128 queries of a batch left half the chip idle and each
+// thread walked 16 items serially (22 us at ml-1m).
 struct ScoreAllArgs {
   const float* q;
   const float* packed;
@@ -816,6 +819,7 @@ struct ScoreAllArgs {
   const int64_t* invalid;
   float* out_score;    // [B][X]
   int64_t* out_index;  // [B][X], -1 = excluded
+  int64_t chunk;       // items per workgroup (blockIdx.y = chunk index)
 };
 
 // Explicit ids with N0 > 0: the query's sorted invalid list in n0p * 8 B of dynamic LDS.
@@ -837,7 +841,9 @@ __global__ __launch_bounds__(256) void mips_scoreall_kernel(ScoreAllArgs a) {
   gptr<fv2> pk = as_global(reinterpret_cast<const fv2*>(a.packed));
   float* os = a.out_score + (int64_t)q * a.X;
   int64_t* oi = a.out_index + (int64_t)q * a.X;
-  for (int64_t i = tid; i < a.X; i += 256) {
+  const int64_t lo = (int64_t)blockIdx.y * a.chunk;
+  const int64_t hi = lo + a.chunk < a.X ? lo + a.chunk : a.X;
+  for (int64_t i = lo + tid; i < hi; i += 256) {
     const int64_t ib = i >> 4;
     const int il = (int)(i & 15);
     float e[8 * KS2];
@@ -861,7 +867,7 @@ __global__ __launch_bounds__(256) void mips_scoreall_kernel(ScoreAllArgs a) {
     __syncthreads();
     for (int j = tid; j < a.N0; j += 256) {
       const int64_t li = a.invalid[(int64_t)q * a.N0 + j] - a.index_base;
-      if (li >= 0 && li < a.X) {
+      if (li >= lo && li < hi) {
         os[li] = -INFINITY;
         oi[li] = -1;
       }
@@ -1834,12 +1840,18 @@ extern "C" int mips_topk(const float* queries, const float* packed_items, int64_
   if (p.small) {
     float* sc = (float*)workspace;
     int64_t* ix = (int64_t*)(sc + (size_t)B * X);
-    ScoreAllArgs s{queries, packed_items, X, D, B, N0, item_ids, index_base, invalid_ids, sc, ix};
+    // ~4 workgroups per CU over the launch, chunks of whole 256-item sweeps
+    const int64_t want = std::max<int64_t>(1, (int64_t)4 * device_cus() / std::max(B, 1));
+    int64_t chunk = (X + want - 1) / want;
+    chunk = std::max<int64_t>(256, (chunk + 255) / 256 * 256);
+    const unsigned n_chunks = (unsigned)((X + chunk - 1) / chunk);
+    ScoreAllArgs s{queries, packed_items, X, D, B, N0, item_ids, index_base, invalid_ids, sc, ix,
+                   chunk};
     const size_t inv_lds = item_ids ? sizeof(int64_t) * p.n0p : 0;
     const int KS2 = (p.KS + 1) / 2;
 #define GR_SA(K2)                                                                           \
   case K2:                                                                                  \
-    GR_TIMED("mips_select", st, hipLaunchKernelGGL(mips_scoreall_kernel<K2>, dim3(B), dim3(256), inv_lds, st, s)); \
+    GR_TIMED("mips_select", st, hipLaunchKernelGGL(mips_scoreall_kernel<K2>, dim3(B, n_chunks), dim3(256), inv_lds, st, s)); \
     break;
     switch (KS2) {
       GR_SA(1) GR_SA(2) GR_SA(3) GR_SA(4) GR_SA(5) GR_SA(6) GR_SA(7) GR_SA(8)
