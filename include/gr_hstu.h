@@ -71,6 +71,8 @@ GR_API int gr_timing_reset(void);
  *                                  key tile's dS once its producer publishes it); default 0 =
  *                                  the recomputing one-launch form.  The workspace size
  *                                  (hstu_attn_bwd_workspace_size) depends on this option.
+ *   GR_OPT_DETERMINISTIC      0|1  reductions that default to fp32 atomics run in a fixed
+ *                                  order instead (gr_item_embedding_bwd: owner-computes)
  */
 enum {
   GR_OPT_MIPS_FILTER_FP32 = 1,
@@ -81,7 +83,8 @@ enum {
   GR_OPT_ROWWAVE = 6,
   GR_OPT_ATTN_BWD_PAIRS = 7,
   GR_OPT_ATTN_BWD_DS = 8,
-  GR_OPT_COUNT_ = 9
+  GR_OPT_DETERMINISTIC = 9,
+  GR_OPT_COUNT_ = 10
 };
 GR_API int gr_set_option(int option, int64_t value);
 GR_API int64_t gr_get_option(int option);

@@ -8,9 +8,12 @@
 // (CategoricalEmbeddingModule passes its mapped ids).
 //
 // Backward: dW[row] += dout[i] for every i gathering that row, skipping the tables'
-// padding row (nn.Embedding padding_idx=0: its gradient is always zero).  fp32 atomics
-// (unordered, like index_add_; the ml-1m batch gathers each item ~7 times).  The
-// gradients are zeroed by a kernel first (graph-capture safe, see common.h).
+// padding row (nn.Embedding padding_idx=0: its gradient is always zero).  Default: fp32
+// atomics (unordered, like index_add_; the ml-1m batch gathers each item ~7 times),
+// after a zeroing kernel (graph-capture safe, see common.h).  GR_OPT_DETERMINISTIC:
+// owner-computes instead -- a workgroup owns EMB_OWN rows of one table, scans every id
+// in order, compacts its matches in id order through LDS and each thread sums its
+// (row, column) in that order, so the result does not depend on scheduling.
 #include "common.h"
 
 #include "../../include/gr_hstu.h"
@@ -74,6 +77,64 @@ __global__ __launch_bounds__(256) void item_embedding_bwd_kernel(EmbArgs a) {
   }
 }
 
+// Deterministic backward: blockIdx.y = table (0 item, 1 year), blockIdx.x = row group.
+constexpr int EMB_OWN = 8;  // table rows per workgroup (thread t: row t / 32, column t % 32)
+__global__ __launch_bounds__(256) void item_embedding_bwd_owner_kernel(EmbArgs a) {
+  __shared__ int s_i[256];
+  __shared__ int s_r[256];
+  __shared__ int s_cnt[4];
+  const int tab = blockIdx.y;
+  const int d = tab ? a.d1 : a.d0, coff = tab ? a.d0 : 0, dd = a.d0 + a.d1;
+  const int64_t rows = tab ? a.rows1 : a.rows0;
+  float* dw = tab ? a.dw1 : a.dw0;
+  if (!dw || d == 0) return;
+  const int64_t r0 = (int64_t)blockIdx.x * EMB_OWN;
+  if (r0 >= rows) return;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int my_r = tid >> 5, my_c0 = tid & 31;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};  // columns my_c0 + 32 j (d <= 128)
+  for (int64_t i0 = 0; i0 < a.n; i0 += 256) {
+    const int64_t i = i0 + tid;
+    int64_t row = -1;
+    if (i < a.n) {
+      const int64_t id = a.ids[i];
+      row = tab ? emb_row1(a, id) : id;
+      if (!(row >= 0 && row < rows && row != a.padding_idx && row >= r0 && row < r0 + EMB_OWN)) row = -1;
+    }
+    // in-order compaction: wave prefix by ballot, waves in id order
+    const unsigned long long m = __ballot(row >= 0);
+    const int before = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) s_cnt[wv] = __popcll(m);
+    __syncthreads();
+    int base = 0;
+    for (int w = 0; w < wv; ++w) base += s_cnt[w];
+    const int tot = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+    if (row >= 0) {
+      s_i[base + before] = (int)(i - i0);
+      s_r[base + before] = (int)(row - r0);
+    }
+    __syncthreads();
+    for (int e = 0; e < tot; ++e) {  // every thread walks the matches in id order
+      if (s_r[e] != my_r) continue;
+      gptr<float> g = as_global(a.dout) + (i0 + s_i[e]) * dd + coff;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = my_c0 + 32 * j;
+        if (c < d) acc[j] += g[c];
+      }
+    }
+    __syncthreads();
+  }
+  const int64_t row = r0 + my_r;
+  if (row < rows) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = my_c0 + 32 * j;
+      if (c < d) dw[row * d + c] = acc[j];
+    }
+  }
+}
+
 }  // namespace gr
 
 extern "C" {
@@ -107,6 +168,22 @@ int gr_item_embedding_bwd(const int64_t* ids, int64_t n, const float* dout, int6
   GR_REQUIRE(map1 == nullptr || map_len > 0, "gr_item_embedding_bwd: empty year table");
   GR_REQUIRE(dw0 || dw1, "gr_item_embedding_bwd: no gradient requested");
   const hipStream_t st = (hipStream_t)stream;
+  if (gr::option(GR_OPT_DETERMINISTIC) != 0) {
+    GR_REQUIRE(d0 <= 128 && d1 <= 128, "gr_item_embedding_bwd: deterministic mode needs d <= 128");
+    GR_REQUIRE(n <= 0x7fffffffLL, "gr_item_embedding_bwd: n too large");
+    GR_REQUIRE(n == 0 || (ids && dout), "gr_item_embedding_bwd: null pointer");
+    gr::EmbArgs a{};
+    a.ids = ids; a.n = n; a.rows0 = rows0; a.d0 = d0;
+    a.rows1 = rows1; a.d1 = d1; a.map1 = map1; a.map_len = map_len;
+    a.dout = dout; a.dw0 = dw0; a.dw1 = d1 > 0 ? dw1 : nullptr; a.padding_idx = padding_idx;
+    const int64_t rmax = rows0 > rows1 ? rows0 : rows1;
+    GR_TIMED("item_embedding", st,
+             hipLaunchKernelGGL(gr::item_embedding_bwd_owner_kernel,
+                                dim3((unsigned)((rmax + gr::EMB_OWN - 1) / gr::EMB_OWN), 2),
+                                dim3(256), 0, st, a));
+    GR_LAUNCH_CHECK("gr_item_embedding_bwd(deterministic)");
+    return 0;
+  }
   if (dw0) gr::zero_words_async(dw0, rows0 * d0, st);
   if (dw1 && d1 > 0) gr::zero_words_async(dw1, rows1 * d1, st);
   if (n > 0) {

@@ -40,6 +40,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <hipcub/hipcub.hpp>
 
 #include "../../include/gr_hstu.h"
 
@@ -548,6 +549,67 @@ __global__ __launch_bounds__(256) void ssm_table_grad_kernel(const float* out, i
   }
 }
 
+// Deterministic mode: keys[p] = catalog row of sample p, vals[p] = p (sort input).
+__global__ __launch_bounds__(256) void ssm_det_keys_kernel(const int2* rec, int64_t n, int64_t V,
+                                                           int* keys, int* vals, int* status) {
+  for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < n; p += (int64_t)gridDim.x * 256) {
+    const int v = rec[p].x;
+    if (v < 0 || v >= V) atomicOr(status, 1);
+    keys[p] = v < 0 || v >= V ? (int)V : v;  // out-of-range rows sort past every real row
+    vals[p] = (int)p;
+  }
+}
+
+// first position e in skeys[0 .. n) with skeys[e] >= v
+__device__ __forceinline__ int64_t lower_bound_i32(const int* skeys, int64_t n, int v) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (skeys[mid] < v) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// One wave per catalog row: d_table[v] = sum over its samples, in sample order, of
+// c * out_t (lanes over the D columns; 8 samples' rows loaded ahead of their adds).
+__global__ __launch_bounds__(256) void ssm_table_grad_det_kernel(const float* out, int64_t ld_out,
+                                                                 int D, int64_t V, int R, int64_t n,
+                                                                 const int2* rec, const int* skeys,
+                                                                 const int* svals, float* d_table,
+                                                                 int64_t ld_dt) {
+  const int64_t v = (int64_t)blockIdx.x * 4 + wave_id();
+  if (v >= V) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t lo = lower_bound_i32(skeys, n, (int)v), hi = lower_bound_i32(skeys, n, (int)v + 1);
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};  // columns lane + 64 j (D <= 256)
+  constexpr int U = 8;
+  for (int64_t e0 = lo; e0 < hi; e0 += U) {
+    float c[U], x[U][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t e = e0 + u < hi ? e0 + u : hi - 1;
+      const int p = svals[e];
+      const int2 r = rec[p];
+      c[u] = e0 + u < hi ? __int_as_float(r.y) : 0.f;
+      const float* orow = out + (int64_t)(p / R) * ld_out;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int d = lane + 64 * j;
+        x[u][j] = d < D ? orow[d] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] += c[u] * x[u][j];
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int d = lane + 64 * j;
+    if (d < D) d_table[v * ld_dt + d] = acc[j];
+  }
+}
+
 // d_table[v][0 .. D) = 0 for every row (a strided memset as a kernel: the graph-captured
 // step then holds no 2-D memset node)
 __global__ __launch_bounds__(256) void ssm_zero_rows_kernel(float* p, int64_t ld, int64_t rows, int D) {
@@ -571,12 +633,28 @@ inline int lanes_per_row(int D) { return D <= 16 ? 1 : D <= 32 ? 2 : D <= 64 ? 4
 
 inline size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
-// workspace: rec[n] (int2) | sorted[n] (int2) | cnt[K] | start[K+1] | rank[n] (int32),
-// K = kRanges * V sort keys
+// GR_OPT_DETERMINISTIC: the table gradient from a STABLE radix sort of the samples by
+// catalog row (hipcub, keys = row, values = sample index in sample order), then one wave
+// per row summing its samples in sample order -- no atomics, a fixed summation order.
+inline size_t ssm_det_sort_bytes(int64_t n, int64_t V) {
+  size_t tb = 0;
+  int bits = 1;
+  while (bits < 31 && ((int64_t)1 << bits) <= V) ++bits;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const int*)nullptr, (int*)nullptr,
+                                           (const int*)nullptr, (int*)nullptr, (int)n, 0, bits);
+  return tb;
+}
+inline size_t ssm_det_bytes(int64_t n, int64_t V) {
+  return option(GR_OPT_DETERMINISTIC) != 0 ? align256(n * 4) + align256(ssm_det_sort_bytes(n, V)) : 0;
+}
+
+// workspace: rec[n] (int2) | sorted[n] (int2) | cnt[K] | start[K+1] | rank[n] (int32)
+// [| vals[n] | sort temp  (deterministic mode)] | status word, K = kRanges * V sort keys
 inline size_t ssm_ws_bytes(int64_t M, int R, int64_t V, int D) {
   (void)D;
   const int64_t n = M * (int64_t)R, K = kRanges * V;
-  return 2 * align256(n * 8) + align256(K * 4) + align256((K + 1) * 4) + align256(n * 4) + 256;
+  return 2 * align256(n * 8) + align256(K * 4) + align256((K + 1) * 4) + align256(n * 4) +
+         ssm_det_bytes(n, V) + 256;
 }
 // byte offset of the status word (last 256 B of the workspace): 0 after a clean backward;
 // bit 0 = a sample's catalog row outside [0, V), bit 1 = a scatter slot outside its row's
@@ -677,6 +755,35 @@ int gr_sampled_softmax_bwd(const float* out, int64_t ld_out, const float* pos, i
   w += gr::align256((K + 1) * 4);
   int* rank = (int*)w;
   const unsigned sgrid = (unsigned)std::min<int64_t>((n + 255) / 256, 4 * gr::device_cus());
+  if (gr::option(GR_OPT_DETERMINISTIC) != 0) {
+    GR_REQUIRE(D <= 256 && n < 0x7fffffffLL && V < 0x7fffffffLL,
+               "gr_sampled_softmax_bwd: deterministic mode needs D <= 256 and < 2^31 samples");
+    int* status = (int*)((char*)workspace + gr::ssm_status_offset(M, R, V, D));
+    int* keys_in = rank;                               // rank[n] region
+    int* vals_in = (int*)(w + gr::align256(n * 4));    // deterministic extra region
+    void* temp = (char*)vals_in + gr::align256(n * 4);
+    size_t temp_bytes = gr::ssm_det_sort_bytes(n, V);
+    int* keys_out = (int*)sorted;                      // sorted[n] (int2) region: 2 x n ints
+    int* vals_out = keys_out + n;
+    int bits = 1;
+    while (bits < 31 && ((int64_t)1 << bits) <= V) ++bits;
+    hipError_t srt = hipSuccess;
+    GR_TIMED("sampled_softmax_csr", st, {
+      gr::zero_words_async(status, 1, st);
+      hipLaunchKernelGGL(gr::ssm_det_keys_kernel, dim3(sgrid), dim3(256), 0, st, rec, n, V, keys_in,
+                         vals_in, status);
+      srt = hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys_in, keys_out, vals_in,
+                                               vals_out, (int)n, 0, bits, st);
+    });
+    GR_REQUIRE(srt == hipSuccess, "gr_sampled_softmax_bwd: radix sort failed");
+    GR_LAUNCH_CHECK("gr_sampled_softmax_bwd (deterministic sort)");
+    GR_TIMED("sampled_softmax_table_grad", st,
+             hipLaunchKernelGGL(gr::ssm_table_grad_det_kernel, dim3((unsigned)((V + 3) / 4)), dim3(256), 0,
+                                st, out, ld_out, D, V, R, n, rec, keys_out, vals_out, d_table,
+                                ld_dtable));
+    GR_LAUNCH_CHECK("gr_sampled_softmax_bwd (deterministic table grad)");
+    return 0;
+  }
   const bool lds = K <= gr::kLdsBins;
   const unsigned cgrid = lds ? (unsigned)((n + gr::kCountChunk - 1) / gr::kCountChunk)
                              : (unsigned)std::min<int64_t>((n + 1023) / 1024, 4 * gr::device_cus());

@@ -79,6 +79,41 @@ def test_categorical_embedding_vs_torch():
     torch.testing.assert_close(m._item_emb.weight.grad, w.grad, rtol=1e-5, atol=1e-6)
 
 
+def test_embedding_backward_deterministic_mode():
+    """GR_OPT_DETERMINISTIC: the owner-computes backward sums every table row's
+    contributions in id order -- equal to the reference golden, to the atomic backward
+    within fp32 rounding, and bit-identical from run to run (ml-1m-sized batch with a
+    year mapping, so both tables have heavily shared rows)."""
+    from mygenerativerecommenders_amd import _lib
+    from mygenerativerecommenders_amd.embeddings import LocalEmbeddingModule
+    z = np.load(os.path.join(GOLDEN, "embeddings.npz"))
+
+    def grads(m, ids, dout):
+        m.zero_grad(set_to_none=True)
+        (m.get_item_embeddings(ids) * dout).sum().backward()
+        return m._item_emb.weight.grad.clone(), m._year_emb.weight.grad.clone()
+    m = _module_from_golden(z)
+    ids = torch.from_numpy(z["ids"]).cuda()
+    dout = torch.from_numpy(z["dout"]).cuda()
+    with _lib.option("DETERMINISTIC", 1):
+        gi, gy = grads(m, ids, dout)
+    np.testing.assert_allclose(gi.cpu().numpy(), z["d_item_w"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(gy.cpu().numpy(), z["d_year_w"], rtol=1e-5, atol=1e-6)
+    g = torch.Generator().manual_seed(4)
+    V, D, B, N = 3953, 50, 128, 211
+    m2 = LocalEmbeddingModule(V, D, item2year={i: 1919 + i % 81 for i in range(1, V + 1)}).cuda()
+    ids2 = torch.randint(0, V + 1, (B, N), generator=g).cuda()
+    dout2 = torch.randn(B, N, D, generator=g).cuda()
+    ref = grads(m2, ids2, dout2)
+    with _lib.option("DETERMINISTIC", 1):
+        a = grads(m2, ids2, dout2)
+        b = grads(m2, ids2, dout2)
+    for x, y, r in zip(a, b, ref):
+        assert torch.equal(x, y)
+        assert (x - r).abs().max().item() <= 1e-5 * (1 + r.abs().max().item())
+        assert not x[0].any()  # padding row
+
+
 def test_embedding_graph_replay():
     from mygenerativerecommenders_amd.embeddings import LocalEmbeddingModule
     m = LocalEmbeddingModule(3952, 50).cuda()

@@ -140,6 +140,41 @@ def test_loss_random_vs_oracle(M, D, V, R, T):
             assert not got.any(), key
 
 
+@pytest.mark.parametrize("M,D,V,R", [(3000, 50, 3953, 128), (700, 64, 50, 100),
+                                     (150, 256, 40000, 128)])
+def test_table_gradient_deterministic_mode(M, D, V, R):
+    """GR_OPT_DETERMINISTIC: the table gradient from a stable radix sort of the samples
+    by row and one in-order sum per row -- equal to the oracle, bit-identical across runs
+    (the default counting-sort path flushes rows with fp32 atomics in arbitrary order)."""
+    from mygenerativerecommenders_amd import _lib, ops
+    out, sup_ids, sup_emb, weights, weight, ids, offsets = _random_case(M, D, V, R, 0.05, 7 * M + D)
+    dev = torch.device("cuda")
+    tab = torch.as_tensor(weight[ids], dtype=torch.float32).to(dev)
+    tab_n = tab / tab.norm(dim=-1, keepdim=True).clamp_min(1e-6)
+    sup = torch.as_tensor(sup_emb, dtype=torch.float32).to(dev)
+    sup_n = sup / sup.norm(dim=-1, keepdim=True).clamp_min(1e-6)
+    o = torch.as_tensor(out, dtype=torch.float32).to(dev)
+    offs = torch.as_tensor(offsets, dtype=torch.int64).to(dev)
+    sid = torch.as_tensor(sup_ids).to(dev)
+    all_ids = torch.as_tensor(ids).to(dev)
+    w = torch.as_tensor(weights).to(dev)
+
+    def grad_table():
+        t = tab_n.detach().clone().requires_grad_(True)
+        lt = ops.sampled_softmax_loss(o, sup_n, t, sid, offs, all_ids, 0.05)
+        ((lt * w).sum() / w.sum()).backward()
+        return t.grad
+    with _lib.option("DETERMINISTIC", 1):
+        g1 = grad_table()
+        g2 = grad_table()
+    g0 = grad_table()
+    assert torch.equal(g1, g2)
+    r = loss_oracle.sampled_softmax(out, sup_ids, sup_emb, weights, weight[ids], ids, offsets,
+                                    0.05, True, 1e-6)
+    _close(g1.cpu().double().numpy(), r["d_tab_norm"], 2e-4, "d_table (deterministic)")
+    _close(g0.cpu().double().numpy(), r["d_tab_norm"], 2e-4, "d_table (atomic)")
+
+
 def test_per_token_loss_vs_oracle():
     from mygenerativerecommenders_amd import ops
     out, sup_ids, sup_emb, weights, weight, ids, offsets = _random_case(2000, 50, 3953, 128,
