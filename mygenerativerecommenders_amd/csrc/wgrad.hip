@@ -15,6 +15,10 @@
 // ones-column appended to Bm (padding column Nb).  Each split writes its panel to a
 // workspace slab; wgrad_reduce sums the slabs in a fixed order (deterministic, no
 // atomics) with 16 slab groups per output in parallel.
+// The column sum (colsum, the _o bias gradient) is accumulated from the A operand the
+// waves of the first nb-panel already hold (one add per k-step, a fixed-order lane and
+// half reduction) and written as slab column Nb: no padding panel carries it (at C3 the
+// ones column of Nb = 256 + 1 cost a second, all-padding panel of 256 columns).
 #include "attn_common.h"
 
 #include "../../include/gr_hstu.h"
@@ -48,6 +52,14 @@ struct WgradArgs {
   int n_splits;
 };
 
+// sum of a lane's partial column sum over its 4 lane groups (lanes lr, lr + 16, lr + 32,
+// lr + 48 hold rows of the same column), fixed order
+__device__ __forceinline__ float wg_colsum_lanes(float v) {
+  v += __shfl_xor(v, 16);
+  v += __shfl_xor(v, 32);
+  return v;
+}
+
 template <int NT>
 struct WgCfg {
   static constexpr int NP = NT * 16;
@@ -58,6 +70,7 @@ struct WgCfg {
   static constexpr int APER = WG_CH * WG_KA / WG_THREADS;         // A loads per thread
   static constexpr int SUPER = NT <= 8 ? WG_SUPER : 2;             // register budget at NT 13/16
   static constexpr size_t LDS = sizeof(float) * 2 * WG_CH * (WG_LDA + LDB + 2);
+  static_assert(LDS >= sizeof(float) * (4 * NT * 4 * 64 + 4 * 16), "exchange area");
 };
 
 template <int NT>
@@ -96,7 +109,9 @@ __device__ __forceinline__ void wgrad_panel(const WgradProb& g, const int64_t* o
   const int bc = tid % C::NP2, br = tid / C::NP2;       // B: col nb0 + bc, rows br + BRPP i
   const int aka = ka0 + ac, bnb = nb0 + bc;
   const bool a_ok = aka < g.Ka;
-  const bool b_in = bnb < g.Nb, b_one = bnb == g.Nb && g.NC > g.Nb;
+  const bool b_in = bnb < g.Nb;
+  const bool do_cs = g.NC > g.Nb && pb == 0;  // this panel also sums A' over its rows
+  float csum = 0.f;
   float ra_v[C::SUPER][C::APER], rb_v[C::SUPER][C::BPER];
   float2 st_v[C::SUPER];
   auto load = [&](int u, int ch) {
@@ -126,8 +141,7 @@ __device__ __forceinline__ void wgrad_panel(const WgradProb& g, const int64_t* o
 #pragma unroll
       for (int i = 0; i < C::BPER; ++i) {
         const int rr = br + C::BRPP * i;
-        const bool row_ok = r0 + rr0 + rr < r1;
-        Bs[buf][rr * C::LDB + bc] = b_one ? (row_ok ? 1.f : 0.f) : rb_v[u][i];
+        Bs[buf][rr * C::LDB + bc] = rb_v[u][i];  // rows past r1 meet a zero A
       }
     }
   };
@@ -170,6 +184,7 @@ __device__ __forceinline__ void wgrad_panel(const WgradProb& g, const int64_t* o
           if (j + 1 < KS) rd((j + 1) & 1, ks0 + j + 1);
           __builtin_amdgcn_sched_barrier(0);
           const float a = (av[j & 1] - sv[j & 1].x) * sv[j & 1].y;
+          if (do_cs) csum += a;  // A'[row 4ks + lg][ka 16w + lr]
 #pragma unroll
           for (int t = 0; t < NT; ++t) acc[t] = mfma16x16x4(a, bv[j & 1][t], acc[t]);
           __builtin_amdgcn_sched_barrier(0);
@@ -179,12 +194,14 @@ __device__ __forceinline__ void wgrad_panel(const WgradProb& g, const int64_t* o
   }
   __syncthreads();  // LDS is reused for the exchange below
   // the two halves' partial sums meet in LDS (fixed order: half 0 + half 1)
-  float* xch = reinterpret_cast<float*>(smem);  // [4 waves][NT][4][64]
+  float* xch = reinterpret_cast<float*>(smem);  // [4 waves][NT][4][64], then [4][16] colsums
+  if (do_cs) csum = wg_colsum_lanes(csum);
   if (half == 1) {
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) xch[((w * NT + t) * 4 + r) * 64 + lane] = acc[t][r];
+    if (do_cs && lg == 0) xch[4 * NT * 4 * 64 + 16 * w + lr] = csum;
   }
   __syncthreads();
   if (half == 1) return;
@@ -194,6 +211,8 @@ __device__ __forceinline__ void wgrad_panel(const WgradProb& g, const int64_t* o
     for (int r = 0; r < 4; ++r) acc[t][r] += xch[((w * NT + t) * 4 + r) * 64 + lane];
   // acc[t][r] = C[ka0 + 16w + 4lg + r][nb0 + 16t + lr]
   float* slab = g.slabs + (int64_t)split * g.Ka * g.NC;
+  if (do_cs && lg == 0 && ka0 + 16 * w + lr < g.Ka)
+    slab[(int64_t)(ka0 + 16 * w + lr) * g.NC + g.Nb] = csum + xch[4 * NT * 4 * 64 + 16 * w + lr];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int ka = ka0 + 16 * w + 4 * lg + r;
@@ -235,7 +254,7 @@ struct WgCfgB {
   static constexpr int BG = WG_THREADS / NP2;  // row groups of the B image
   static constexpr int RB = WGB_CH / BG;       // B rows per thread (8, 16, 32)
   static constexpr size_t STAGE = 2 * (size_t)WGB_LDT * (WG_KA + NP);
-  static constexpr size_t XCH = sizeof(float) * 4 * NT * 4 * 64;
+  static constexpr size_t XCH = sizeof(float) * (4 * NT * 4 * 64 + 4 * 16);
   static constexpr size_t LDS = STAGE > XCH ? STAGE : XCH;
 };
 
@@ -264,7 +283,9 @@ __device__ __forceinline__ void wgrad_panel_bf16(const WgradProb& g, const int64
   const int bc = tid % C::NP2, bg = tid / C::NP2;    // B: column nb0 + bc, rows RB bg .. +RB-1
   const int aka = ka0 + ac, bnb = nb0 + bc;
   const bool a_ok = aka < g.Ka;
-  const bool b_in = bnb < g.Nb, b_one = bnb == g.Nb && g.NC > g.Nb;
+  const bool b_in = bnb < g.Nb;
+  const bool do_cs = g.NC > g.Nb && pb == 0;  // this panel also sums bf16(A') over its rows
+  float csum = 0.f;
   float av_[8], bv_[C::RB];
   float2 sv_[8];
   auto load = [&](int ch) {
@@ -297,11 +318,7 @@ __device__ __forceinline__ void wgrad_panel_bf16(const WgradProb& g, const int64
         uint32_t pb2[4];
 #pragma unroll
         for (int i = 0; i < 8; i += 2) {
-          const int rr = C::RB * bg + q + i;
-          const bool ok0 = r0 + rr0 + rr < r1, ok1 = r0 + rr0 + rr + 1 < r1;
-          const float lo = b_one ? (ok0 ? 1.f : 0.f) : bv_[q + i];
-          const float hi = b_one ? (ok1 ? 1.f : 0.f) : bv_[q + i + 1];
-          pb2[i / 2] = pack_bf16(lo, hi);
+          pb2[i / 2] = pack_bf16(bv_[q + i], bv_[q + i + 1]);  // rows past r1 meet a zero A
         }
         *reinterpret_cast<u32x4_t*>(Bt + bc * WGB_LDT + C::RB * bg + q) =
             u32x4_t{pb2[0], pb2[1], pb2[2], pb2[3]};
@@ -319,6 +336,11 @@ __device__ __forceinline__ void wgrad_panel_bf16(const WgradProb& g, const int64
     if (ch + 1 < n_ch) load(ch + 1);  // next chunk's rows fly during the MFMAs
     const int k0 = 32 * half + 8 * lg;
     const u32x4_t a = *reinterpret_cast<const u32x4_t*>(At + (16 * w + lr) * WGB_LDT + k0);
+    if (do_cs) {  // the 8 rounded values of rows k0 .. k0 + 7, column ka 16w + lr
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        csum += __uint_as_float(a[e] << 16) + __uint_as_float(a[e] & 0xffff0000u);
+    }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const u32x4_t b = *reinterpret_cast<const u32x4_t*>(Bt + (16 * t + lr) * WGB_LDT + k0);
@@ -327,12 +349,14 @@ __device__ __forceinline__ void wgrad_panel_bf16(const WgradProb& g, const int64
     __syncthreads();
   }
   // the two halves' partial sums meet in LDS (fixed order: half 0 + half 1)
-  float* xch = reinterpret_cast<float*>(smem);  // [4 waves][NT][4][64]
+  float* xch = reinterpret_cast<float*>(smem);  // [4 waves][NT][4][64], then [4][16] colsums
+  if (do_cs) csum = wg_colsum_lanes(csum);
   if (half == 1) {
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) xch[((w * NT + t) * 4 + r) * 64 + lane] = acc[t][r];
+    if (do_cs && lg == 0) xch[4 * NT * 4 * 64 + 16 * w + lr] = csum;
   }
   __syncthreads();
   if (half == 1) return;
@@ -341,6 +365,8 @@ __device__ __forceinline__ void wgrad_panel_bf16(const WgradProb& g, const int64
 #pragma unroll
     for (int r = 0; r < 4; ++r) acc[t][r] += xch[((w * NT + t) * 4 + r) * 64 + lane];
   float* slab = g.slabs + (int64_t)split * g.Ka * g.NC;
+  if (do_cs && lg == 0 && ka0 + 16 * w + lr < g.Ka)
+    slab[(int64_t)(ka0 + 16 * w + lr) * g.NC + g.Nb] = csum + xch[4 * NT * 4 * 64 + 16 * w + lr];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int ka = ka0 + 16 * w + 4 * lg + r;
@@ -415,16 +441,16 @@ struct WgPlan {
   size_t slab_bytes[2];
 };
 
-// Panels cover Nb + 1 columns per problem (the workspace query has no colsum flag: the
-// ones column is only filled when a colsum is requested).  Splits so that splits x
-// panels ~ one workgroup per CU, each split a multiple of WG_CH rows.
+// Panels cover the Nb columns of a problem; the slabs hold Nb + 1 (the workspace query has
+// no colsum flag: column Nb is only written when a colsum is requested).  Splits so that
+// splits x panels ~ one workgroup per CU, each split a multiple of WG_CH rows.
 static WgPlan wgrad_plan(int64_t max_rows, const int Ka[2], const int Nb[2]) {
   WgPlan pl{};
   int total_panels = 0;
   for (int i = 0; i < 2; ++i) {
     if (Ka[i] <= 0) continue;
-    pl.nt[i] = wgrad_nt(Nb[i] + 1);
-    const int pa = ceil_div(Ka[i], WG_KA), pb = ceil_div(Nb[i] + 1, pl.nt[i] * 16);
+    pl.nt[i] = wgrad_nt(Nb[i]);
+    const int pa = ceil_div(Ka[i], WG_KA), pb = ceil_div(Nb[i], pl.nt[i] * 16);
     pl.panels[i] = pa * pb;
     pl.panels_nb[i] = pb;
     total_panels += pl.panels[i];
