@@ -220,7 +220,7 @@ __device__ __forceinline__ void wgrad_panel(const WgradProb& g, const int64_t* o
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int nb = nb0 + 16 * t + lr;
-      if (nb < g.NC) slab[(int64_t)ka * g.NC + nb] = acc[t][r];
+      if (nb < g.Nb) slab[(int64_t)ka * g.NC + nb] = acc[t][r];  // column Nb: colsum above
     }
   }
 }
@@ -374,7 +374,7 @@ __device__ __forceinline__ void wgrad_panel_bf16(const WgradProb& g, const int64
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int nb = nb0 + 16 * t + lr;
-      if (nb < g.NC) slab[(int64_t)ka * g.NC + nb] = acc[t][r];
+      if (nb < g.Nb) slab[(int64_t)ka * g.NC + nb] = acc[t][r];  // column Nb: colsum above
     }
   }
 }
