@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GR_HSTU_ABI_VERSION 9
+#define GR_HSTU_ABI_VERSION 8
 
 #ifndef GR_API
 #define GR_API __attribute__((visibility("default")))
@@ -211,12 +211,9 @@ GR_API int hstu_bucket_map(const int64_t* ts, const int64_t* offsets, int B, int
  * out: (total, H*dv), stride ld_out.  bucket_map: from hstu_bucket_map, or NULL for
  * NO bias at all (no timestamps, hstu.py:191).  max_len: host upper bound on the
  * sequence lengths (<= N), sizes the grid.  fp32 in / out, f32 MFMA.  dqk, dv <= 256.
- * act_in = 1: q / k / v hold the PRE-activation h of the UVQK projection and the kernel
- * applies SiLU as it stages them (hstu.py:303-305 fused into the load; the caller then
- * keeps only h, ABI 9); act_in = 0: q / k / v are used as given.
  */
 GR_API int hstu_attn_fwd(const float* q, const float* k, const float* v, int64_t ld_qk,
-                  int64_t ld_v, int act_in, const int64_t* offsets, int B, int N, int max_len, int H,
+                  int64_t ld_v, const int64_t* offsets, int B, int N, int max_len, int H,
                   int dqk, int dv, const uint8_t* bucket_map, const float* pos_w,
                   const float* ts_w, int num_buckets, float* out, int64_t ld_out,
                   void* stream);
@@ -226,7 +223,7 @@ GR_API int hstu_attn_fwd(const float* q, const float* k, const float* v, int64_t
  * P = silu(S + bias) / N is rounded to bf16 before P.V; S, the bias, silu and the
  * output are fp32.  Same arguments and layout as hstu_attn_fwd. */
 GR_API int hstu_attn_fwd_bf16(const float* q, const float* k, const float* v, int64_t ld_qk,
-                              int64_t ld_v, int act_in, const int64_t* offsets, int B, int N, int max_len,
+                              int64_t ld_v, const int64_t* offsets, int B, int N, int max_len,
                               int H, int dqk, int dv, const uint8_t* bucket_map,
                               const float* pos_w, const float* ts_w, int num_buckets, float* out,
                               int64_t ld_out, void* stream);
@@ -237,15 +234,14 @@ GR_API int hstu_attn_fwd_bf16(const float* q, const float* k, const float* v, in
  * Writes dq, dk (total, H*dqk) and dv (total, H*dv), all with row stride ld_d.
  * hq/hk/hv: optional UVQK pre-activation columns (stride ld_h); when given the
  * outputs are multiplied by silu'(h) (hstu.py:303-305), i.e. they are gradients of
- * the pre-activation.  act_in as in hstu_attn_fwd (with act_in = 1 and hq/hk/hv =
- * q/k/v the call needs only the pre-activation rows).  dpos_w (2N-1) and dts_w (num_buckets+1) are OVERWRITTEN
+ * the pre-activation.  dpos_w (2N-1) and dts_w (num_buckets+1) are OVERWRITTEN
  * with this call's bias gradients (summed over heads) when bucket_map != NULL.
  * Deterministic: no global atomics; the workspace (size below, only needed with a
  * bucket map) holds one partial slab per workgroup, reduced in a fixed order.
  */
 GR_API size_t hstu_attn_bwd_workspace_size(int B, int N, int max_len, int H, int num_buckets);
 GR_API int hstu_attn_bwd(const float* q, const float* k, const float* v, int64_t ld_qk,
-                  int64_t ld_v, int act_in, const float* dout, int64_t ld_dout, const int64_t* offsets,
+                  int64_t ld_v, const float* dout, int64_t ld_dout, const int64_t* offsets,
                   int B, int N, int max_len, int H, int dqk, int dv,
                   const uint8_t* bucket_map, const float* pos_w, const float* ts_w,
                   int num_buckets, const float* hq, const float* hk, const float* hv,
@@ -260,7 +256,7 @@ GR_API int hstu_attn_bwd(const float* q, const float* k, const float* v, int64_t
 GR_API size_t hstu_attn_bwd_bf16_workspace_size(int B, int N, int max_len, int H, int dqk,
                                                 int dv, int num_buckets);
 GR_API int hstu_attn_bwd_bf16(const float* q, const float* k, const float* v, int64_t ld_qk,
-                              int64_t ld_v, int act_in, const float* dout, int64_t ld_dout,
+                              int64_t ld_v, const float* dout, int64_t ld_dout,
                               const int64_t* offsets, int B, int N, int max_len, int H, int dqk,
                               int dv, const uint8_t* bucket_map, const float* pos_w,
                               const float* ts_w, int num_buckets, const float* hq,
@@ -276,8 +272,7 @@ GR_API int hstu_attn_bwd_bf16(const float* q, const float* k, const float* v, in
  * hstu_ln_uvqk_fwd  (replaces hstu.py:300-305: layer_norm -> mm(_uvqk) -> silu):
  *   x_stats[m] = (mean, rstd) of x[m, :D];  h = LN(x) @ w_uvqk (w: (D, n_out) row-major)
  *   uvqk = activation ? silu(h) : h  (activation 1 = "silu", 0 = "none");
- *   h_pre (optional, same stride ld_out) receives h for the backward.  uvqk may be NULL
- *   when h_pre is given: only h is stored (the consumers then take act_in / act_u = 1).
+ *   h_pre (optional, same stride ld_out) receives h for the backward.
  */
 GR_API int hstu_ln_uvqk_fwd(const float* x, int64_t ld_x, const int64_t* offsets, int B,
                      int64_t max_rows, int D, const float* w_uvqk, int n_out, float eps,
@@ -298,10 +293,9 @@ GR_API int hstu_ln_uvqk_fwd_bf16(const float* x, int64_t ld_x, const int64_t* of
  *   replay then draws a fresh mask by bumping the device counter)
  *   y = o_in @ w_o^T + b_o + x_res   (w_o: (D, hdv) row-major = nn.Linear.weight)
  *   o_in (optional, contiguous (rows, hdv)) is stored for the weight gradient.
- *   b_o and x_res may be NULL.  act_u = 1: u holds the pre-activation h_u and
- *   silu(h_u) is used in its place.
+ *   b_o and x_res may be NULL.
  */
-GR_API int hstu_gate_o_fwd(const float* u, int64_t ld_u, int act_u, const float* attn, int64_t ld_attn,
+GR_API int hstu_gate_o_fwd(const float* u, int64_t ld_u, const float* attn, int64_t ld_attn,
                     const int64_t* offsets, int B, int64_t max_rows, int hdv, int D,
                     const float* w_o, const float* b_o, const float* x_res, int64_t ld_x,
                     float eps, float dropout_p, uint64_t seed, const int64_t* seed_offset,
@@ -309,7 +303,7 @@ GR_API int hstu_gate_o_fwd(const float* u, int64_t ld_u, int act_u, const float*
 /* hstu_gate_o_fwd with bf16 MFMA operands (autocast_dtype = bfloat16): the transformed A
  * values and the weights rounded to bf16, fp32 accumulation and epilogue; same
  * arguments and outputs. */
-GR_API int hstu_gate_o_fwd_bf16(const float* u, int64_t ld_u, int act_u, const float* attn, int64_t ld_attn,
+GR_API int hstu_gate_o_fwd_bf16(const float* u, int64_t ld_u, const float* attn, int64_t ld_attn,
                          const int64_t* offsets, int B, int64_t max_rows, int hdv, int D,
                          const float* w_o, const float* b_o, const float* x_res, int64_t ld_x,
                          float eps, float dropout_p, uint64_t seed, const int64_t* seed_offset,
@@ -317,8 +311,7 @@ GR_API int hstu_gate_o_fwd_bf16(const float* u, int64_t ld_u, int act_u, const f
 
 /* hstu_gate_o_bwd  (backward of hstu_gate_o_fwd w.r.t. u and attn; hdv <= 256):
  *   g = (dy @ w_o) * dropout mask;  du = g * LN(attn) [* silu'(h_u) if h_u];
- *   d_attn = LayerNorm_backward(attn; g * u).  u may be NULL when h_u is given:
- *   u = silu(h_u) is recomputed from it.
+ *   d_attn = LayerNorm_backward(attn; g * u).
  */
 GR_API int hstu_gate_o_bwd(const float* dy, int64_t ld_dy, const int64_t* offsets, int B,
                     int64_t max_rows, int hdv, int D, const float* w_o, const float* u,

@@ -104,15 +104,6 @@ struct BufTile {
       }
     }
   }
-  // SiLU of the staged values when q / k / v are handed over as the pre-activation h
-  // (act_in = 1); applied just before the LDS write, so the loads stay in flight across
-  // the previous tile's compute.  Masked (zero) entries stay zero.
-  __device__ __forceinline__ void silu_if(bool on) {
-    if (on) {
-#pragma unroll
-      for (int i = 0; i < NV; ++i) v[i] = siluf_(v[i]);
-    }
-  }
 };
 
 // Work rank of workgroup `id` (rank 0 = heaviest).  Workgroups id and id + C (C = number

@@ -36,7 +36,6 @@ struct AttnFwdArgsBf16 {
   int64_t ld_out;
   float inv_n;
   int cus;  // CU count (snake_rank)
-  int act;  // q / k / v hold the pre-activation h: SiLU applied as they are staged
 };
 
 
@@ -67,15 +66,6 @@ struct Bf16Stage {
         v[i][2 * u] = buf_ld(r, in && c < ncols ? base : 0x40000000, 0);
         v[i][2 * u + 1] = buf_ld(r, in && c + 1 < ncols ? base + 4 : 0x40000000, 0);
       }
-    }
-  }
-  // SiLU before the bf16 rounding when q / k / v are the pre-activation h (act_in = 1)
-  __device__ __forceinline__ void silu_if(bool on) {
-    if (on) {
-#pragma unroll
-      for (int i = 0; i < PER; ++i)
-#pragma unroll
-        for (int e = 0; e < 2 * RU; ++e) v[i][e] = siluf_(v[i][e]);
     }
   }
   __device__ __forceinline__ void store(__bf16* lds, int ldl) const {
@@ -149,7 +139,7 @@ __global__ __launch_bounds__(64 * WAVES) void hstu_attn_fwd_bf16_kernel(AttnFwdA
       for (int e = 0; e < 8; ++e) {
         const int d = 32 * c + 8 * lg + e;
         const float y = qrow[d < a.dqk ? d : a.dqk - 1];
-        x[e] = d < a.dqk ? (a.act ? siluf_(y) : y) : 0.f;
+        x[e] = d < a.dqk ? y : 0.f;
       }
       qf[c] = u32x4_t{pack_bf16(x[0], x[1]), pack_bf16(x[2], x[3]), pack_bf16(x[4], x[5]),
                       pack_bf16(x[6], x[7])};
@@ -169,8 +159,6 @@ __global__ __launch_bounds__(64 * WAVES) void hstu_attn_fwd_bf16_kernel(AttnFwdA
   Bf16Stage<C::VP, TK, true, NTH> vst;
   kst.load(rk, a.ld_qk, 0, a.dqk);
   vst.load(rv, a.ld_v, 0, a.dv);
-  kst.silu_if(a.act);
-  vst.silu_if(a.act);
   kst.store(Ks, C::LDK);
   vst.store(Vt, C::LDV);
   __syncthreads();  // also publishes tsw / posw
@@ -235,8 +223,6 @@ __global__ __launch_bounds__(64 * WAVES) void hstu_attn_fwd_bf16_kernel(AttnFwdA
     }
     if (more) {
       lds_barrier();
-      kst.silu_if(a.act);
-      vst.silu_if(a.act);
       kst.store(Ks, C::LDK);
       vst.store(Vt, C::LDV);
       lds_barrier();
@@ -277,7 +263,7 @@ static int launch_fwd_bf16(AttnFwdArgsBf16 a, hipStream_t st) {
 }  // namespace gr
 
 extern "C" int hstu_attn_fwd_bf16(const float* q, const float* k, const float* v, int64_t ld_qk,
-                                  int64_t ld_v, int act_in, const int64_t* offsets, int B, int N, int max_len,
+                                  int64_t ld_v, const int64_t* offsets, int B, int N, int max_len,
                                   int H, int dqk, int dv, const uint8_t* bucket_map,
                                   const float* pos_w, const float* ts_w, int num_buckets,
                                   float* out, int64_t ld_out, void* stream) {
@@ -288,12 +274,10 @@ extern "C" int hstu_attn_fwd_bf16(const float* q, const float* k, const float* v
   GR_REQUIRE(dqk <= 256 && dv <= 256, "hstu_attn_fwd_bf16: dqk/dv > 256 unsupported (%d, %d)", dqk, dv);
   GR_REQUIRE(!bucket_map || (pos_w && ts_w && num_buckets > 0 && num_buckets < 256),
              "hstu_attn_fwd_bf16: bucket_map given without pos_w/ts_w");
-  GR_REQUIRE(act_in == 0 || act_in == 1, "hstu_attn_fwd_bf16: act_in %d not 0 / 1", act_in);
   if (B == 0 || max_len == 0) return 0;
   AttnFwdArgsBf16 a{q, k, v, ld_qk, ld_v, offsets, B, N, H, dqk, dv, max_len,
                     bucket_map, pos_w, ts_w, bucket_map ? num_buckets : 0, out, ld_out,
                     1.0f / (float)N, 0};
-  a.act = act_in;
   hipStream_t st = (hipStream_t)stream;
   const int d = dqk > dv ? dqk : dv;
   if (d <= 32) return launch_fwd_bf16<1, 2, 64, 4>(a, st);
@@ -346,7 +330,6 @@ struct AttnBwdArgsBf16 {
   float inv_n;
   int n_kt, n_qt;  // key / query tiles of the two passes
   int cus;
-  int act;  // q / k / v hold the pre-activation h: SiLU applied as they are staged
 };
 
 // A ROWS x CP fp32 tile loaded once, stored as bf16 row-major and / or transposed.
@@ -371,15 +354,6 @@ struct DualStage {
       }
     }
   }
-  // SiLU before the bf16 rounding when q / k / v are the pre-activation h (act_in = 1)
-  __device__ __forceinline__ void silu_if(bool on) {
-    if (on) {
-#pragma unroll
-      for (int i = 0; i < PER; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[i][e] = siluf_(v[i][e]);
-    }
-  }
   __device__ __forceinline__ void store_rows(__bf16* lds, int ldl) const {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
@@ -402,14 +376,14 @@ struct DualStage {
   }
 };
 
-// 8 bf16 of a row from global, zero past `n` (fragments held in VGPRs); act: SiLU first
-__device__ __forceinline__ u32x4_t row_frag(gptr<float> row, int d0, int n, bool act = false) {
+// 8 bf16 of a row from global, zero past `n` (fragments held in VGPRs)
+__device__ __forceinline__ u32x4_t row_frag(gptr<float> row, int d0, int n) {
   float x[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const int d = d0 + e;
     const float y = row[d < n ? d : n - 1];
-    x[e] = d < n ? (act ? siluf_(y) : y) : 0.f;
+    x[e] = d < n ? y : 0.f;
   }
   return u32x4_t{pack_bf16(x[0], x[1]), pack_bf16(x[2], x[3]), pack_bf16(x[4], x[5]),
                  pack_bf16(x[6], x[7])};
@@ -490,10 +464,9 @@ __global__ __launch_bounds__(64 * WAVES) void attn_bwd_bf16_dkv_kernel(AttnBwdAr
     gptr<float> krow = as_global(a.k) + row * a.ld_qk + h * a.dqk;
     gptr<float> vrow = as_global(a.v) + row * a.ld_v + h * a.dv;
 #pragma unroll
-    for (int c = 0; c < KC; ++c) kf[c] = row_frag(krow, 32 * c + 8 * lg, a.dqk, a.act);
+    for (int c = 0; c < KC; ++c) kf[c] = row_frag(krow, 32 * c + 8 * lg, a.dqk);
 #pragma unroll
-    for (int c = 0; c < VC; ++c)
-      vf[c] = DO_K ? row_frag(vrow, 32 * c + 8 * lg, a.dv, a.act) : u32x4_t{};
+    for (int c = 0; c < VC; ++c) vf[c] = DO_K ? row_frag(vrow, 32 * c + 8 * lg, a.dv) : u32x4_t{};
   }
   const __amdgpu_buffer_rsrc_t rmap = map_rsrc(a.map_kq, b, attn_tiles_per_seq(a.N));
   const int map_voff = (((wk_lo & 63) + lr) * 16 + lg) * 4;  // key-major 64 x 64 tiles
@@ -518,7 +491,6 @@ __global__ __launch_bounds__(64 * WAVES) void attn_bwd_bf16_dkv_kernel(AttnBwdAr
   qst.load(rq, a.ld_qk, qt0 * TQ, a.dqk);
   dst.load(rdo, a.ld_dout, qt0 * TQ, a.dv);
   auto store_tiles = [&]() {
-    qst.silu_if(a.act);
     qst.store_rows(Qs, C::LDK);
     if (DO_K) qst.store_trans(Qt, C::LDT);
     if (DO_K) dst.store_rows(Ds, C::LDV);
@@ -710,7 +682,7 @@ __global__ __launch_bounds__(64 * WAVES) void attn_bwd_bf16_dq_kernel(AttnBwdArg
     gptr<float> qrow = as_global(a.q) + row * a.ld_qk + h * a.dqk;
     gptr<float> drow = as_global(a.dout) + row * a.ld_dout + h * a.dv;
 #pragma unroll
-    for (int c = 0; c < KC; ++c) qf[c] = row_frag(qrow, 32 * c + 8 * lg, a.dqk, a.act);
+    for (int c = 0; c < KC; ++c) qf[c] = row_frag(qrow, 32 * c + 8 * lg, a.dqk);
 #pragma unroll
     for (int c = 0; c < VC; ++c) df[c] = row_frag(drow, 32 * c + 8 * lg, a.dv);
   }
@@ -726,8 +698,6 @@ __global__ __launch_bounds__(64 * WAVES) void attn_bwd_bf16_dq_kernel(AttnBwdArg
   DualStage<C::VP, TK, NTH> vst;
   kst.load(rk, a.ld_qk, 0, a.dqk);
   vst.load(rv, a.ld_v, 0, a.dv);
-  kst.silu_if(a.act);
-  vst.silu_if(a.act);
   kst.store_rows(Ks, C::LDK);
   kst.store_trans(Kt, C::LDT);
   vst.store_rows(Vs, C::LDV);
@@ -786,8 +756,6 @@ __global__ __launch_bounds__(64 * WAVES) void attn_bwd_bf16_dq_kernel(AttnBwdArg
     }
     if (more) {
       lds_barrier();
-      kst.silu_if(a.act);
-      vst.silu_if(a.act);
       kst.store_rows(Ks, C::LDK);
       kst.store_trans(Kt, C::LDT);
       vst.store_rows(Vs, C::LDV);
@@ -905,7 +873,7 @@ extern "C" size_t hstu_attn_bwd_bf16_workspace_size(int B, int N, int max_len, i
 }
 
 extern "C" int hstu_attn_bwd_bf16(const float* q, const float* k, const float* v, int64_t ld_qk,
-                                  int64_t ld_v, int act_in, const float* dout, int64_t ld_dout,
+                                  int64_t ld_v, const float* dout, int64_t ld_dout,
                                   const int64_t* offsets, int B, int N, int max_len, int H,
                                   int dqk, int dv, const uint8_t* bucket_map, const float* pos_w,
                                   const float* ts_w, int num_buckets, const float* hq,
@@ -919,7 +887,6 @@ extern "C" int hstu_attn_bwd_bf16(const float* q, const float* k, const float* v
   GR_REQUIRE(dqk <= 256 && dv <= 256, "hstu_attn_bwd_bf16: dqk/dv > 256 unsupported (%d, %d)", dqk, dv);
   GR_REQUIRE((hq == nullptr) == (hk == nullptr) && (hk == nullptr) == (hv == nullptr),
              "hstu_attn_bwd_bf16: hq/hk/hv must be all given or all NULL");
-  GR_REQUIRE(act_in == 0 || act_in == 1, "hstu_attn_bwd_bf16: act_in %d not 0 / 1", act_in);
   const int d = dqk > dv ? dqk : dv;
   if (bucket_map) {
     GR_REQUIRE(pos_w && ts_w && dpos_w && dts_w && num_buckets > 0 && num_buckets < 256,
@@ -941,7 +908,6 @@ extern "C" int hstu_attn_bwd_bf16(const float* q, const float* k, const float* v
                     bucket_map, map_kq, pos_w, ts_w, bucket_map ? num_buckets : 0, hq, hk, hv,
                     ld_h, dq, dk, dvv, ld_d, bucket_map ? (float*)workspace : nullptr,
                     1.0f / (float)N, 0, 0, 0};
-  a.act = act_in;
   if (d <= 32) return launch_bwd_bf16<1, 1, 64, 4>(a, dpos_w, dts_w, st);
   if (d <= 64) return launch_bwd_bf16<2, 2, 64, 4>(a, dpos_w, dts_w, st);
   if (d <= 128) return launch_bwd_bf16<4, 4, 32, 8>(a, dpos_w, dts_w, st);

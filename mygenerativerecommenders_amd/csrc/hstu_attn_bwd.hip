@@ -94,7 +94,6 @@ struct AttnBwdArgs {
   float* ds;  // non-null: the dK/dV pass stores dS as 16 x 16 tiles for the dQ pass
   int ds_tps; // dS tiles per (sequence, head): NB (NB + 1) / 2, NB = ceil(N / 16)
   uint32_t* ds_flags;  // one-launch form: [bh][key tile] = 1 once that tile's dS is published
-  int act;    // q / k / v hold the pre-activation h: SiLU applied as they are loaded
 };
 
 // TT = rows per streamed LDS tile (queries in dK/dV, keys in dQ): 64, or 16 for the
@@ -219,9 +218,9 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
     for (int st = 0; st < KSTEPS; ++st) {
       const int d = 4 * st + lg;
       const float x = krow[d < a.dqk ? d : a.dqk - 1];
-      kreg[st] = d < a.dqk ? (a.act ? siluf_(x) : x) : 0.f;
+      kreg[st] = d < a.dqk ? x : 0.f;
       const float y = vrow[d < a.dv ? d : a.dv - 1];
-      vreg[st] = d < a.dv ? (a.act ? siluf_(y) : y) : 0.f;
+      vreg[st] = d < a.dv ? y : 0.f;
     }
   }
   f4 dV[VTILES], dK[C::KT];
@@ -250,8 +249,6 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
     // K / V rows k0 .. k0 + 63 (rows past L and columns past dqk / dv read as 0)
     qst.load(seq_rsrc(a.k, a.ld_qk, s0, h * a.dqk, L, a.dqk), a.ld_qk, k0, a.dqk, a.vec2);
     dst.load(seq_rsrc(a.v, a.ld_v, s0, h * a.dv, L, a.dv), a.ld_v, k0, a.dv, a.vec2);
-    qst.silu_if(a.act);
-    dst.silu_if(a.act);
     qst.store(Qs, C::LDQ, a.vec2);
     dst.store(Ds, C::LDV, a.vec2);
     load_tile(k0 / TT, mw);  // the first query tile's loads fly while the fragments are read
@@ -265,7 +262,6 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
   } else {
     load_tile(k0 / TT, mw);
   }
-  qst.silu_if(a.act);
   qst.store(Qs, C::LDQ, a.vec2);
   dst.store(Ds, C::LDV, a.vec2);
   __syncthreads();
@@ -441,7 +437,6 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
     }
     if (more) {
       lds_barrier();
-      qst.silu_if(a.act);
       qst.store(Qs, C::LDQ, a.vec2);
       dst.store(Ds, C::LDV, a.vec2);
 #pragma unroll
@@ -600,7 +595,7 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& a, const int
     for (int st = 0; st < KSTEPS; ++st) {
       const int d = 4 * st + lg;
       const float x = qrow[d < a.dqk ? d : a.dqk - 1];
-      qreg[st] = d < a.dqk ? (a.act ? siluf_(x) : x) : 0.f;
+      qreg[st] = d < a.dqk ? x : 0.f;
       const float y = drow[d < a.dv ? d : a.dv - 1];
       doreg[st] = d < a.dv ? y : 0.f;
     }
@@ -636,7 +631,6 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& a, const int
   if constexpr (STAGED) {
     kst.load(seq_rsrc(a.q, a.ld_qk, s0, h * a.dqk, L, a.dqk), a.ld_qk, q0, a.dqk, a.vec2);
     vst.load(seq_rsrc(a.dout, a.ld_dout, s0, h * a.dv, L, a.dv), a.ld_dout, q0, a.dv, a.vec2);
-    kst.silu_if(a.act);
     kst.store(Ks, LDK, a.vec2);
     vst.store(Vs, LDV, a.vec2);
     load_tile(0, mw);
@@ -650,8 +644,6 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& a, const int
   } else {
     load_tile(0, mw);
   }
-  kst.silu_if(a.act);
-  vst.silu_if(a.act);
   kst.store(Ks, LDK, a.vec2);
   vst.store(Vs, LDV, a.vec2);
   __syncthreads();
@@ -719,8 +711,6 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& a, const int
     }
     if (more) {
       lds_barrier();
-      kst.silu_if(a.act);
-      vst.silu_if(a.act);
       kst.store(Ks, LDK, a.vec2);
       vst.store(Vs, LDV, a.vec2);
 #pragma unroll
@@ -825,7 +815,6 @@ __device__ __forceinline__ bool attn_bwd_dq_ds_body(const AttnBwdArgs& a, const 
   auto tile_of = [&](int j) { return WAIT ? last_kt - j : j; };
   if (WAIT && !wait_tile(tile_of(0))) return false;
   load_tile(tile_of(0), dsv);
-  kst.silu_if(a.act);
   kst.store(Ks, LDK, a.vec2);
   __syncthreads();
   for (int j = 0; j <= last_kt; ++j) {
@@ -861,7 +850,6 @@ __device__ __forceinline__ bool attn_bwd_dq_ds_body(const AttnBwdArgs& a, const 
     }
     if (more) {
       lds_barrier();
-      kst.silu_if(a.act);
       kst.store(Ks, LDK, a.vec2);
 #pragma unroll
       for (int kb = 0; kb < C::TB; ++kb) dsv[kb] = dsn[kb];
@@ -1093,7 +1081,7 @@ extern "C" size_t hstu_attn_bwd_workspace_size(int B, int N, int max_len, int H,
 }
 
 extern "C" int hstu_attn_bwd(const float* q, const float* k, const float* v, int64_t ld_qk,
-                             int64_t ld_v, int act_in, const float* dout, int64_t ld_dout,
+                             int64_t ld_v, const float* dout, int64_t ld_dout,
                              const int64_t* offsets, int B, int N, int max_len, int H, int dqk,
                              int dv, const uint8_t* bucket_map, const float* pos_w,
                              const float* ts_w, int num_buckets, const float* hq,
@@ -1107,7 +1095,6 @@ extern "C" int hstu_attn_bwd(const float* q, const float* k, const float* v, int
   GR_REQUIRE(dqk <= 256 && dv <= 256, "hstu_attn_bwd: dqk/dv > 256 unsupported (%d, %d)", dqk, dv);
   GR_REQUIRE((hq == nullptr) == (hk == nullptr) && (hk == nullptr) == (hv == nullptr),
              "hstu_attn_bwd: hq/hk/hv must be all given or all NULL");
-  GR_REQUIRE(act_in == 0 || act_in == 1, "hstu_attn_bwd: act_in %d not 0 / 1", act_in);
   if (bucket_map) {
     GR_REQUIRE(pos_w && ts_w && dpos_w && dts_w && num_buckets > 0 && num_buckets < 256,
                "hstu_attn_bwd: bucket_map given without pos_w/ts_w/dpos_w/dts_w");
@@ -1133,7 +1120,6 @@ extern "C" int hstu_attn_bwd(const float* q, const float* k, const float* v, int
   a.cus = (int64_t)a.n_tiles * B * H <= 2 * device_cus() ? device_cus() : (1 << 30);
   a.vec2 = pair_aligned({q, k, v, dout}, {ld_qk, ld_v, ld_dout, dqk, dv});
   a.vec2h = hq ? pair_aligned({hq, hk, hv}, {ld_h, dqk, dv}) : 0;
-  a.act = act_in;
   // short sequences with a workspace large enough for the dS tiles: two-pass backward
   if (bucket_map && bwd_ds_bytes(B, N, H) && option(GR_OPT_ATTN_BWD_DS) != 0 &&
       ws_bytes >= bwd_ds_offset(B, N, max_len, H, num_buckets) + bwd_ds_bytes(B, N, H)) {

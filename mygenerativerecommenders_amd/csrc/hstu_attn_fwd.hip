@@ -37,7 +37,6 @@ struct AttnFwdArgs {
   float inv_n;
   int vec2;  // 8-byte pair staging (aligned rows, even widths)
   int cus;   // CU count (snake_rank)
-  int act;   // q / k / v hold the pre-activation h: SiLU applied as they are loaded
 };
 
 // TK = keys per LDS tile (64, or 16 for the wide head dims where a 64-key register
@@ -91,7 +90,7 @@ __global__ __launch_bounds__(256) void hstu_attn_fwd_kernel(AttnFwdArgs a) {
     for (int st = 0; st < KSTEPS; ++st) {
       const int d = 4 * st + lg;
       const float x = qrow[d < a.dqk ? d : a.dqk - 1];
-      qreg[st] = d < a.dqk ? (a.act ? siluf_(x) : x) : 0.f;
+      qreg[st] = d < a.dqk ? x : 0.f;
     }
   }
   const __amdgpu_buffer_rsrc_t rmap = map_rsrc(a.map_qk, b, attn_tiles_per_seq(a.N));
@@ -115,8 +114,6 @@ __global__ __launch_bounds__(256) void hstu_attn_fwd_kernel(AttnFwdArgs a) {
   };
 
   load_tile(0, mw);
-  kst.silu_if(a.act);
-  vst.silu_if(a.act);
   kst.store(Ks, C::LDK, a.vec2);
   vst.store(Vs, C::LDV, a.vec2);
   __syncthreads();  // also publishes tsw / posw
@@ -180,8 +177,6 @@ __global__ __launch_bounds__(256) void hstu_attn_fwd_kernel(AttnFwdArgs a) {
     }
     if (more) {
       lds_barrier();
-      kst.silu_if(a.act);
-      vst.silu_if(a.act);
       kst.store(Ks, C::LDK, a.vec2);
       vst.store(Vs, C::LDV, a.vec2);
 #pragma unroll
@@ -221,7 +216,7 @@ static int launch_fwd(const AttnFwdArgs& a, int grid, hipStream_t st) {
 }  // namespace gr
 
 extern "C" int hstu_attn_fwd(const float* q, const float* k, const float* v, int64_t ld_qk,
-                             int64_t ld_v, int act_in, const int64_t* offsets, int B, int N, int max_len,
+                             int64_t ld_v, const int64_t* offsets, int B, int N, int max_len,
                              int H, int dqk, int dv, const uint8_t* bucket_map,
                              const float* pos_w, const float* ts_w, int num_buckets, float* out,
                              int64_t ld_out, void* stream) {
@@ -232,7 +227,6 @@ extern "C" int hstu_attn_fwd(const float* q, const float* k, const float* v, int
   GR_REQUIRE(dqk <= 256 && dv <= 256, "hstu_attn_fwd: dqk/dv > 256 unsupported (%d, %d)", dqk, dv);
   GR_REQUIRE(!bucket_map || (pos_w && ts_w && num_buckets > 0 && num_buckets < 256),
              "hstu_attn_fwd: bucket_map given without pos_w/ts_w");
-  GR_REQUIRE(act_in == 0 || act_in == 1, "hstu_attn_fwd: act_in %d not 0 / 1", act_in);
   if (B == 0 || max_len == 0) return 0;
   AttnFwdArgs a{q, k, v, ld_qk, ld_v, offsets, B, N, H, dqk, dv, ceil_div(max_len, 64),
                 bucket_map, pos_w, ts_w, bucket_map ? num_buckets : 0, out, ld_out,
@@ -241,7 +235,6 @@ extern "C" int hstu_attn_fwd(const float* q, const float* k, const float* v, int
   // heaviest-first (dynamic dispatch = longest-processing-time order)
   a.cus = (int64_t)a.n_qtiles * B * H <= 2 * device_cus() ? device_cus() : (1 << 30);
   a.vec2 = pair_aligned({q, k, v}, {ld_qk, ld_v, dqk, dv});
-  a.act = act_in;
   const int grid = a.n_qtiles * B * H;
   hipStream_t st = (hipStream_t)stream;
   const int d = dqk > dv ? dqk : dv;

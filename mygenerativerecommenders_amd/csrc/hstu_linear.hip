@@ -421,7 +421,7 @@ struct OpLnUvqk {
         if (n >= N) continue;
         const float v = acc[t][r];
         if (h_pre) h_pre[m * ld_out + n] = v;
-        if (out) out[m * ld_out + n] = act ? siluf_(v) : v;
+        out[m * ld_out + n] = act ? siluf_(v) : v;
       }
     }
   }
@@ -441,7 +441,6 @@ struct OpGateO {
   int B, K, N;  // K = hdv, N = D
   const float* u;
   int64_t ldu;
-  int act_u;  // u holds the pre-activation h_u: u = silu(h_u)
   const float* attn;
   int64_t lda;
   const float* w;
@@ -464,7 +463,7 @@ struct OpGateO {
   __device__ int64_t a_ld0() const { return ldu; }
   __device__ int64_t a_ld1() const { return lda; }
   __device__ float a_xform(float uv, float av, int64_t m, int k, float2 st, bool valid) const {
-    float v = (act_u ? siluf_(uv) : uv) * ((av - st.x) * st.y);
+    float v = uv * ((av - st.x) * st.y);
     if (p > 0.f) v *= dropout_keep(seed + (seed_off ? (uint64_t)*seed_off : 0ull), m, k, K, p);
     if (valid && o_in && blockIdx.y == 0) o_in[m * K + k] = v;
     return v;
@@ -552,8 +551,8 @@ struct OpGateOBwd : NoStats {
         const int n = ncol + 16 * t;
         const int nc = n < N ? n : N - 1;
         av[t] = as_global(attn)[mc * lda + nc];
+        uv[t] = as_global(u)[mc * ldu + nc];
         hv[t] = h_u ? as_global(h_u)[mc * ldh + nc] : 0.f;
-        uv[t] = u ? as_global(u)[mc * ldu + nc] : siluf_(hv[t]);  // u NULL: u = silu(h_u)
       }
       float s1 = 0.f, s2 = 0.f;
       float lnv[NT], dln[NT];
@@ -845,12 +844,11 @@ struct RwArgsLnUvqk {
   }
 };
 struct RwArgsGateO {
-  const int64_t* offsets; int B, K, N; const float* u; int64_t ldu; int act_u; const float* attn; int64_t lda;
+  const int64_t* offsets; int B, K, N; const float* u; int64_t ldu; const float* attn; int64_t lda;
   const float* w; const float* bias; const float* xres; int64_t ldx; float eps, p; uint64_t seed;
   const int64_t* seed_off; float2* a_stats; float* o_in; float* y; int64_t ldy;
   template <class Op> void fill(Op& o) const {
-    o.offsets = offsets; o.B = B; o.K = K; o.N = N; o.u = u; o.ldu = ldu; o.act_u = act_u;
-    o.attn = attn; o.lda = lda;
+    o.offsets = offsets; o.B = B; o.K = K; o.N = N; o.u = u; o.ldu = ldu; o.attn = attn; o.lda = lda;
     o.w = w; o.bias = bias; o.xres = xres; o.ldx = ldx; o.eps = eps; o.p = p; o.seed = seed;
     o.seed_off = seed_off; o.a_stats = a_stats; o.o_in = o_in; o.y = y; o.ldy = ldy;
   }
@@ -944,7 +942,7 @@ static int hstu_ln_uvqk_fwd_impl(bool bf16, const float* x, int64_t ld_x, const 
                                 int64_t max_rows, int D, const float* w_uvqk, int n_out,
                                 float eps, int activation, float* x_stats, float* h_pre,
                                 float* uvqk, int64_t ld_out, void* stream) {
-  GR_REQUIRE(x && offsets && w_uvqk && (uvqk || h_pre) && x_stats, "hstu_ln_uvqk_fwd: null pointer");
+  GR_REQUIRE(x && offsets && w_uvqk && uvqk && x_stats, "hstu_ln_uvqk_fwd: null pointer");
   GR_REQUIRE(D > 0 && n_out > 0 && B >= 0 && max_rows >= 0, "hstu_ln_uvqk_fwd: bad sizes");
   GR_REQUIRE(activation == 0 || activation == 1, "hstu_ln_uvqk_fwd: activation must be 0|1");
   if (!bf16 && rw_enabled()) {
@@ -972,43 +970,42 @@ extern "C" int hstu_ln_uvqk_fwd_bf16(const float* x, int64_t ld_x, const int64_t
   return hstu_ln_uvqk_fwd_impl(true, x, ld_x, offsets, B, max_rows, D, w_uvqk, n_out, eps, activation, x_stats, h_pre, uvqk, ld_out, stream);
 }
 
-static int hstu_gate_o_fwd_impl(bool bf16, const float* u, int64_t ld_u, int act_u, const float* attn, int64_t ld_attn,
+static int hstu_gate_o_fwd_impl(bool bf16, const float* u, int64_t ld_u, const float* attn, int64_t ld_attn,
                                const int64_t* offsets, int B, int64_t max_rows, int hdv, int D,
                                const float* w_o, const float* b_o, const float* x_res,
                                int64_t ld_x, float eps, float dropout_p, uint64_t seed,
                                const int64_t* seed_offset, float* attn_stats, float* o_in,
                                float* y, int64_t ld_y, void* stream) {
   GR_REQUIRE(u && attn && offsets && w_o && y && attn_stats, "hstu_gate_o_fwd: null pointer");
-  GR_REQUIRE(act_u == 0 || act_u == 1, "hstu_gate_o_fwd: act_u %d not 0 / 1", act_u);
   GR_REQUIRE(hdv > 0 && D > 0 && B >= 0, "hstu_gate_o_fwd: bad sizes");
   GR_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f, "hstu_gate_o_fwd: dropout_p %f", dropout_p);
   if (!bf16 && rw_enabled()) {
-    RwArgsGateO ra{offsets, B, hdv, D, u, ld_u, act_u, attn, ld_attn, w_o, b_o, x_res, ld_x, eps,
+    RwArgsGateO ra{offsets, B, hdv, D, u, ld_u, attn, ld_attn, w_o, b_o, x_res, ld_x, eps,
                    dropout_p, seed, seed_offset, (float2*)attn_stats, o_in, y, ld_y};
     const int vec = rw_vec({u, attn, x_res, o_in, y}, {ld_u, ld_attn, ld_x, ld_y, hdv, D});
     const int rc = rw_dispatch<RwGateO>(ra, hdv, D, vec, max_rows, "gate_o_fwd", (hipStream_t)stream);
     if (rc >= 0) return rc;
   }
-  OpGateO op{offsets, B, hdv, D, u, ld_u, act_u, attn, ld_attn, w_o, b_o, x_res, ld_x, eps, dropout_p,
+  OpGateO op{offsets, B, hdv, D, u, ld_u, attn, ld_attn, w_o, b_o, x_res, ld_x, eps, dropout_p,
              seed, seed_offset, (float2*)attn_stats, o_in, y, ld_y};
   return bf16 ? launch_rowpanel_bf16(op, max_rows, false, "hstu_gate_o_fwd", (hipStream_t)stream)
               : launch_rowpanel(op, max_rows, false, "hstu_gate_o_fwd", (hipStream_t)stream);
 }
-extern "C" int hstu_gate_o_fwd(const float* u, int64_t ld_u, int act_u, const float* attn, int64_t ld_attn,
+extern "C" int hstu_gate_o_fwd(const float* u, int64_t ld_u, const float* attn, int64_t ld_attn,
                                const int64_t* offsets, int B, int64_t max_rows, int hdv, int D,
                                const float* w_o, const float* b_o, const float* x_res,
                                int64_t ld_x, float eps, float dropout_p, uint64_t seed,
                                const int64_t* seed_offset, float* attn_stats, float* o_in,
                                float* y, int64_t ld_y, void* stream) {
-  return hstu_gate_o_fwd_impl(false, u, ld_u, act_u, attn, ld_attn, offsets, B, max_rows, hdv, D, w_o, b_o, x_res, ld_x, eps, dropout_p, seed, seed_offset, attn_stats, o_in, y, ld_y, stream);
+  return hstu_gate_o_fwd_impl(false, u, ld_u, attn, ld_attn, offsets, B, max_rows, hdv, D, w_o, b_o, x_res, ld_x, eps, dropout_p, seed, seed_offset, attn_stats, o_in, y, ld_y, stream);
 }
-extern "C" int hstu_gate_o_fwd_bf16(const float* u, int64_t ld_u, int act_u, const float* attn, int64_t ld_attn,
+extern "C" int hstu_gate_o_fwd_bf16(const float* u, int64_t ld_u, const float* attn, int64_t ld_attn,
                                const int64_t* offsets, int B, int64_t max_rows, int hdv, int D,
                                const float* w_o, const float* b_o, const float* x_res,
                                int64_t ld_x, float eps, float dropout_p, uint64_t seed,
                                const int64_t* seed_offset, float* attn_stats, float* o_in,
                                float* y, int64_t ld_y, void* stream) {
-  return hstu_gate_o_fwd_impl(true, u, ld_u, act_u, attn, ld_attn, offsets, B, max_rows, hdv, D, w_o, b_o, x_res, ld_x, eps, dropout_p, seed, seed_offset, attn_stats, o_in, y, ld_y, stream);
+  return hstu_gate_o_fwd_impl(true, u, ld_u, attn, ld_attn, offsets, B, max_rows, hdv, D, w_o, b_o, x_res, ld_x, eps, dropout_p, seed, seed_offset, attn_stats, o_in, y, ld_y, stream);
 }
 
 static int hstu_gate_o_bwd_impl(bool bf16, const float* dy, int64_t ld_dy, const int64_t* offsets, int B,
@@ -1018,7 +1015,7 @@ static int hstu_gate_o_bwd_impl(bool bf16, const float* dy, int64_t ld_dy, const
                                float dropout_p, uint64_t seed, const int64_t* seed_offset,
                                float* du, int64_t ld_du, float* d_attn, int64_t ld_da,
                                void* stream) {
-  GR_REQUIRE(dy && offsets && w_o && (u || h_u) && attn && attn_stats && du && d_attn,
+  GR_REQUIRE(dy && offsets && w_o && u && attn && attn_stats && du && d_attn,
              "hstu_gate_o_bwd: null pointer");
   GR_REQUIRE(hdv > 0 && D > 0 && B >= 0, "hstu_gate_o_bwd: bad sizes");
   if (!bf16 && rw_enabled()) {
@@ -1106,7 +1103,7 @@ extern "C" int hstu_gate_o_cat_fwd(const float* u, int64_t ld_u, const float* at
   GR_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f, "hstu_gate_o_cat_fwd: dropout_p %f", dropout_p);
   GR_REQUIRE(rw_vec({u, attn, x_res, o_in, y}, {ld_u, ld_attn, ld_x, ld_y, hdv, D}) > 0,
              "hstu_gate_o_cat_fwd: rows and widths must be 8-byte aligned (even)");
-  RwArgsGateO ra{offsets, B, 3 * hvp, D, u, ld_u, 0, attn, ld_attn, w_pad, b_o, x_res, ld_x, eps,
+  RwArgsGateO ra{offsets, B, 3 * hvp, D, u, ld_u, attn, ld_attn, w_pad, b_o, x_res, ld_x, eps,
                  dropout_p, seed, seed_offset, (float2*)attn_stats, o_in, y, ld_y};
   const hipStream_t st = (hipStream_t)stream;
   switch (kgh) {

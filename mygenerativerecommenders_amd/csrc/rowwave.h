@@ -228,7 +228,7 @@ struct RwLnUvqk {
   __device__ void setup(int64_t total) {
     rx = mat_rsrc(x, ldx, total, 0);
     rh = mat_rsrc(h_pre ? h_pre : out, ld_out, h_pre ? total : 0, 0);
-    ro = mat_rsrc(out ? out : h_pre, ld_out, out ? total : 0, 0);  // out NULL: h_pre only
+    ro = mat_rsrc(out, ld_out, total, 0);
   }
   __device__ void load(Src& s, int64_t m, int lg) const {
 #pragma unroll
@@ -289,7 +289,6 @@ struct RwGateO {
   int B, K, N;  // K = hdv, N = D
   const float* u;
   int64_t ldu;
-  int act_u;  // u holds the pre-activation h_u: u = silu(h_u)
   const float* attn;
   int64_t lda;
   const float* w;
@@ -346,8 +345,7 @@ struct RwGateO {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int k = qcol<VEC>(16 * g, lg, e);
-        const float uu = act_u ? siluf_(s.uu[g][e]) : s.uu[g][e];
-        float v = uu * ((s.v[g][e] - mean) * rstd);
+        float v = s.uu[g][e] * ((s.v[g][e] - mean) * rstd);
         if (p > 0.f) v *= rw_dropout_keep(seed_eff, m, k, K, p);
         a[g][e] = k < K ? v : 0.f;
         o[e] = a[g][e];
@@ -408,7 +406,7 @@ struct RwGateOBwd {
   __device__ int bns() const { return 1; }
   __device__ void setup(int64_t total) {
     rdy = mat_rsrc(dy, lddy, total, 0);
-    ru = mat_rsrc(u ? u : h_u, ldu, u ? total : 0, 0);  // u NULL: u = silu(h_u)
+    ru = mat_rsrc(u, ldu, total, 0);
     ra = mat_rsrc(attn, lda, total, 0);
     rh = mat_rsrc(h_u ? h_u : u, ldh, h_u ? total : 0, 0);
     rdu = mat_rsrc(du, lddu, total, 0);
@@ -431,7 +429,7 @@ struct RwGateOBwd {
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       es.av[t] = ldq<VEC>(ra, m * lda, 16 * t, lg, N);
-      if (u) es.uv[t] = ldq<VEC>(ru, m * ldu, 16 * t, lg, N);
+      es.uv[t] = ldq<VEC>(ru, m * ldu, 16 * t, lg, N);
       es.hv[t] = ldq<VEC>(rh, m * ldh, 16 * t, lg, N);  // 0 when h_u is NULL
     }
   }
@@ -453,7 +451,7 @@ struct RwGateOBwd {
         if (h_u) dd *= silu_grad_(hv[e]);
         duv[e] = dd;
         lnv[t][e] = ok ? ln : 0.f;
-        dln[t][e] = ok ? gg * (u ? uv[e] : siluf_(hv[e])) : 0.f;
+        dln[t][e] = ok ? gg * uv[e] : 0.f;
         s1 += dln[t][e];
         s2 += dln[t][e] * lnv[t][e];
       }
@@ -490,7 +488,6 @@ struct RwGateOCatT {
     int hv;       // hdv
     const float* u;
     int64_t ldu;
-    int act_u;  // always 0: concat_ua takes u after the activation
     const float* attn;
     int64_t lda;
     const float* w;

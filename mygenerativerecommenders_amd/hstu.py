@@ -121,10 +121,6 @@ class SequentialTransductionUnitJagged(torch.nn.Module):
         self.register_buffer("_dropout_step", torch.zeros(1, dtype=torch.int64),
                              persistent=False)
         self._bf16 = False  # set by HSTUJagged from its autocast_dtype
-        # memory-saving mode (not in the reference): keep only the pre-activation UVQK rows
-        # per layer and let the attention / gate kernels apply SiLU as they load them
-        # (one (rows, n_out) buffer less per layer; slower)
-        self.store_preactivation_only = False
 
     def _geometry(self, n: int, max_len: int) -> ops.STUGeometry:
         if self._linear_activation == "silu":
@@ -141,8 +137,7 @@ class SequentialTransductionUnitJagged(torch.nn.Module):
             N=n, D=self._embedding_dim, H=self._num_heads, dqk=self._attention_dim,
             dv=self._linear_dim, eps=self._eps, activation=act,
             dropout_p=float(self._dropout_ratio) if self.training else 0.0,
-            max_len=max_len, bf16=self._bf16, concat_ua=self._concat_ua,
-            preact_only=self.store_preactivation_only)
+            max_len=max_len, bf16=self._bf16, concat_ua=self._concat_ua)
 
     def forward(
         self,

@@ -219,7 +219,6 @@ class STUGeometry:
     max_len: int        # host bound on sequence lengths (<= N)
     bf16: bool = False  # bf16 MFMA operands (HSTU autocast_dtype=bfloat16): attention, projections, weight grads
     concat_ua: bool = False  # o_in = [u, LN(a), u * LN(a)] (hstu.py:398-400)
-    preact_only: bool = False  # store only h; consumers apply SiLU on load (act_in / act_u)
 
     @property
     def n_out(self):
@@ -259,39 +258,25 @@ class STULayerFunction(torch.autograd.Function):
         w_uvqk = w_uvqk.contiguous()
         w_o = w_o.contiguous()
         x_stats = torch.empty(rows, 2, dtype=torch.float32, device=dev)
-        # preact_only (memory-saving mode): with the silu activation (hstu.py:303-305) only
-        # the pre-activation h is stored; the attention and gate kernels apply SiLU as they
-        # load it (act_in / act_u = 1) and the backward takes silu'(h) from the same rows:
-        # one (rows, n_out) buffer instead of two.  Not the default: the attention kernels
-        # re-stage every K / V tile once per query tile, so SiLU is recomputed many times
-        # over (measured: C2 +4 us attn_fwd / +2 us attn_bwd per layer against -2 us in
-        # ln_uvqk_fwd; C3 +170 / +130 us), DESIGN.md 4b.  concat_ua keeps the post-activation
-        # copy (its kernels take u as stored).
-        act_in = 1 if geo.activation and geo.preact_only and not geo.concat_ua else 0
-        if act_in:
-            h_pre = torch.empty(rows, n_out, dtype=torch.float32, device=dev)
-            uvqk = None
-        else:
-            uvqk = torch.empty(rows, n_out, dtype=torch.float32, device=dev)
-            # h_pre (for silu') exists only for the backward
-            h_pre = torch.empty_like(uvqk) if geo.activation and grad_on else None
-        src = h_pre if act_in else uvqk  # rows the attention / gate kernels read
+        uvqk = torch.empty(rows, n_out, dtype=torch.float32, device=dev)
+        # h_pre (pre-activation, for silu') and o_in (for the W_o gradient) exist only for
+        # the backward: inference / no_grad forwards skip both writes
+        h_pre = torch.empty_like(uvqk) if geo.activation and grad_on else None
         sfx = "_bf16" if geo.bf16 else ""  # bf16 MFMA operands in the projections too
         _lib.call("hstu_ln_uvqk_fwd" + sfx, x.data_ptr(), x.stride(0), offsets.data_ptr(), B, rows, D,
                   w_uvqk.data_ptr(), n_out, geo.eps, geo.activation, x_stats.data_ptr(),
-                  _lib.ptr(h_pre), _lib.ptr(uvqk), n_out, st)
+                  _lib.ptr(h_pre), uvqk.data_ptr(), n_out, st)
         attn = torch.empty(rows, hv, dtype=torch.float32, device=dev)
-        q = src[:, 2 * hv:2 * hv + hq]
-        k = src[:, 2 * hv + hq:]
-        v = src[:, hv:2 * hv]
+        q = uvqk[:, 2 * hv:2 * hv + hq]
+        k = uvqk[:, 2 * hv + hq:]
+        v = uvqk[:, hv:2 * hv]
         pos_w_c = pos_w.contiguous() if bmap is not None else None
         ts_w_c = ts_w.contiguous() if bmap is not None else None
         _lib.call("hstu_attn_fwd_bf16" if geo.bf16 else "hstu_attn_fwd", q.data_ptr(), k.data_ptr(),
-                  v.data_ptr(), n_out, n_out, act_in,
+                  v.data_ptr(), n_out, n_out,
                   offsets.data_ptr(), B, geo.N, geo.max_len, H, dqk, dv, _lib.ptr(bmap),
                   _lib.ptr(pos_w_c), _lib.ptr(ts_w_c), NUM_BUCKETS, attn.data_ptr(), hv, st)
         attn_stats = torch.empty(rows, 2, dtype=torch.float32, device=dev)
-        # o_in (for the W_o gradient) only when a backward will run
         needs_w_grad = grad_on and (w_o.requires_grad or b_o.requires_grad)
         ow = 3 * hv if geo.concat_ua else hv  # o_in width
         o_in = torch.empty(rows, ow, dtype=torch.float32, device=dev) if needs_w_grad else None
@@ -307,7 +292,7 @@ class STULayerFunction(torch.autograd.Function):
                       _lib.ptr(seed_offset), attn_stats.data_ptr(), _lib.ptr(o_in), y.data_ptr(),
                       D, st)
         else:
-            _lib.call("hstu_gate_o_fwd" + sfx, src.data_ptr(), n_out, act_in, attn.data_ptr(), hv,
+            _lib.call("hstu_gate_o_fwd" + sfx, uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
                       offsets.data_ptr(), B, rows, hv, D, w_o.data_ptr(), b_o_c.data_ptr(),
                       x.data_ptr(), x.stride(0), geo.eps, geo.dropout_p, seed,
                       _lib.ptr(seed_offset), attn_stats.data_ptr(), _lib.ptr(o_in), y.data_ptr(),
@@ -315,7 +300,6 @@ class STULayerFunction(torch.autograd.Function):
         ctx.save_for_backward(x, offsets, bmap, w_uvqk, w_o, pos_w_c, ts_w_c, x_stats, uvqk,
                               h_pre, attn, attn_stats, o_in)
         ctx.geo = geo
-        ctx.act_in = act_in
         ctx.seed = seed
         ctx.seed_offset = seed_offset
         return y
@@ -342,10 +326,10 @@ class STULayerFunction(torch.autograd.Function):
                       attn_stats.data_ptr(), _lib.ptr(h_pre), n_out, geo.dropout_p, ctx.seed,
                       _lib.ptr(ctx.seed_offset), d_uvqk.data_ptr(), n_out, d_attn.data_ptr(), hv,
                       st)
-        else:  # act_in: u = NULL, recomputed as silu(h_u)
+        else:
             _lib.call("hstu_gate_o_bwd" + ("_bf16" if geo.bf16 else ""), dy.data_ptr(), D,
                       offsets.data_ptr(), B, rows, hv, D,
-                      w_o.data_ptr(), _lib.ptr(uvqk), n_out, attn.data_ptr(), hv,
+                      w_o.data_ptr(), uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
                       attn_stats.data_ptr(), _lib.ptr(h_pre), n_out, geo.dropout_p, ctx.seed,
                       _lib.ptr(ctx.seed_offset), d_uvqk.data_ptr(), n_out, d_attn.data_ptr(), hv, st)
         L = _lib.lib()
@@ -359,11 +343,9 @@ class STULayerFunction(torch.autograd.Function):
                                                           NUM_BUCKETS) if geo.bf16 else
                       L.hstu_attn_bwd_workspace_size(B, geo.N, geo.max_len, H, NUM_BUCKETS))
             ws_a = torch.empty(max(ws_a_n, 4), dtype=torch.uint8, device=dev)
-        act_in = ctx.act_in
-        src = h_pre if act_in else uvqk
-        q = src[:, 2 * hv:2 * hv + hq]
-        k = src[:, 2 * hv + hq:]
-        v = src[:, hv:2 * hv]
+        q = uvqk[:, 2 * hv:2 * hv + hq]
+        k = uvqk[:, 2 * hv + hq:]
+        v = uvqk[:, hv:2 * hv]
         if h_pre is not None:
             hq_p = h_pre[:, 2 * hv:2 * hv + hq].data_ptr()
             hk_p = h_pre[:, 2 * hv + hq:].data_ptr()
@@ -374,7 +356,7 @@ class STULayerFunction(torch.autograd.Function):
         dk = d_uvqk[:, 2 * hv + hq:]
         dvv = d_uvqk[:, hv:2 * hv]
         _lib.call("hstu_attn_bwd_bf16" if geo.bf16 else "hstu_attn_bwd", q.data_ptr(), k.data_ptr(),
-                  v.data_ptr(), n_out, n_out, act_in,
+                  v.data_ptr(), n_out, n_out,
                   d_attn.data_ptr(), hv, offsets.data_ptr(), B, geo.N, geo.max_len, H, dqk, dv,
                   _lib.ptr(bmap), _lib.ptr(pos_w), _lib.ptr(ts_w), NUM_BUCKETS,
                   hq_p, hk_p, hv_p, n_out, dq.data_ptr(), dk.data_ptr(), dvv.data_ptr(), n_out,

@@ -42,8 +42,6 @@ def main():
     ap.add_argument("--split", action="store_true", help="f32 backward as separate dK/dV, dQ launches")
     ap.add_argument("--nopairs", action="store_true", help="f32 backward: one tile per workgroup")
     ap.add_argument("--pairs", type=int, default=1, help="GR_OPT_ATTN_BWD_PAIRS (0/1/2)")
-    ap.add_argument("--act", action="store_true",
-                    help="q/k/v as the pre-activation h (act_in = 1, h rows = q/k/v rows)")
     ap.add_argument("--ds", type=int, default=0, nargs="?", const=1,
                     help="f32 backward dS forms: 1 = two launches, 2 = in-launch hand-off")
     ap.add_argument("--hepi", action="store_true",
@@ -87,19 +85,17 @@ def main():
         bmap = None
 
     def fwd():
-        _lib.call("hstu_attn_fwd_bf16" if args.bf16 else "hstu_attn_fwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out, n_out, int(args.act),
+        _lib.call("hstu_attn_fwd_bf16" if args.bf16 else "hstu_attn_fwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out, n_out,
                   offsets.data_ptr(), B, N, L, H, d, d, _lib.ptr(bmap), pos_w.data_ptr(),
                   ts_w.data_ptr(), 128, out.data_ptr(), hv, st)
 
     h = torch.randn(rows, n_out, device=dev, generator=g) if args.hepi else None
-    if args.act:  # the product path: silu'(h) from the same rows as q / k / v
-        args.hepi, h = True, uvqk
     hq = h[:, 2 * hv:3 * hv].data_ptr() if args.hepi else None
     hk = h[:, 3 * hv:].data_ptr() if args.hepi else None
     hvp = h[:, hv:2 * hv].data_ptr() if args.hepi else None
 
     def bwd():
-        _lib.call("hstu_attn_bwd_bf16" if args.bf16 else "hstu_attn_bwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out, n_out, int(args.act),
+        _lib.call("hstu_attn_bwd_bf16" if args.bf16 else "hstu_attn_bwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out, n_out,
                   dout.data_ptr(), hv, offsets.data_ptr(), B, N, L, H, d, d, _lib.ptr(bmap),
                   pos_w.data_ptr(), ts_w.data_ptr(), 128, hq, hk, hvp, n_out if args.hepi else 0,
                   dq.data_ptr(), dk.data_ptr(), dvv.data_ptr(), n_out, dpw.data_ptr(),

@@ -68,7 +68,7 @@ def main():
             return run_w()
         _lib.call("hstu_ln_uvqk_fwd", P(x), D, P(offsets), B, cap, D, P(w_uvqk), n_out, 1e-6, 1,
                   P(x_stats), P(h_pre), P(uvqk), n_out, st)
-        _lib.call("hstu_gate_o_fwd", P(uvqk), n_out, 0, P(attn), hv, P(offsets), B, cap, hv, D,
+        _lib.call("hstu_gate_o_fwd", P(uvqk), n_out, P(attn), hv, P(offsets), B, cap, hv, D,
                   P(w_o), P(b_o), P(x), D, 1e-6, 0.2, 7, P(seed_off), P(attn_stats), P(o_in),
                   P(y), D, st)
         _lib.call("hstu_gate_o_bwd", P(dy), D, P(offsets), B, cap, hv, D, P(w_o), P(uvqk),

@@ -37,7 +37,7 @@ Lb = _lib.lib()
 ws_n = Lb.hstu_attn_bwd_workspace_size(B, N, L, H, 128)
 ws = torch.empty(ws_n, dtype=torch.uint8, device=dev)
 for _ in range(3):
-    _lib.call("hstu_attn_bwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out, n_out, 0,
+    _lib.call("hstu_attn_bwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out, n_out,
               dout.data_ptr(), hv, offsets.data_ptr(), B, N, L, H, d, d, bmap.data_ptr(),
               pos_w.data_ptr(), ts_w.data_ptr(), 128, hp(2 * hv), hp(3 * hv), hp(hv), n_out,
               dd[:, 2 * hv:].data_ptr(), dd[:, 3 * hv:].data_ptr(), dd[:, hv:].data_ptr(), n_out,

@@ -47,7 +47,7 @@ n_wg = 2 * grid  # dQ workgroups in slots [grid, 2 grid)
 
 
 def run():
-    _lib.call("hstu_attn_bwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out, n_out, 0,
+    _lib.call("hstu_attn_bwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out, n_out,
               dout.data_ptr(), hv, offsets.data_ptr(), B, N, L, H, d, d, _lib.ptr(bmap),
               pos_w.data_ptr(), ts_w.data_ptr(), 128, hpre[:, 2 * hv:].data_ptr(),
               hpre[:, 3 * hv:].data_ptr(), hpre[:, hv:].data_ptr(), n_out,

@@ -36,7 +36,7 @@ def test_every_declared_symbol_resolves_with_signature():
         assert len(fn.argtypes) == len(args), name
 
 
-@pytest.mark.parametrize("name,nargs", [("hstu_attn_fwd", 20), ("mips_topk", 16),
+@pytest.mark.parametrize("name,nargs", [("hstu_attn_fwd", 19), ("mips_topk", 16),
                                         ("hstu_ln_uvqk_fwd", 15), ("gr_wgrad", 15)])
 def test_null_pointer_is_an_error_not_a_crash(name, nargs):
     L = _lib.lib()

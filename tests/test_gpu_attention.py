@@ -36,8 +36,7 @@ def _case(seed, B, N, H, dqk, dv, lengths=None, with_ts=True, scale=1.0):
     return lengths, offsets, uvqk, ts, pos_w, ts_w
 
 
-def _run_gpu_fwd(offsets, uvqk, ts, pos_w, ts_w, B, N, H, dqk, dv, entry="hstu_attn_fwd",
-                 act_in=0):
+def _run_gpu_fwd(offsets, uvqk, ts, pos_w, ts_w, B, N, H, dqk, dv, entry="hstu_attn_fwd"):
     from mygenerativerecommenders_amd import _lib
     dev = torch.device("cuda")
     u = uvqk.to(dev)
@@ -54,7 +53,7 @@ def _run_gpu_fwd(offsets, uvqk, ts, pos_w, ts_w, B, N, H, dqk, dv, entry="hstu_a
     max_len = int((offsets[1:] - offsets[:-1]).max()) if B else 0
     from mygenerativerecommenders_amd import ops
     bmap = ops.bucket_map(tsd, offs, N) if tsd is not None else None
-    _lib.call(entry, q.data_ptr(), k.data_ptr(), v.data_ptr(), u.stride(0), u.stride(0), act_in,
+    _lib.call(entry, q.data_ptr(), k.data_ptr(), v.data_ptr(), u.stride(0), u.stride(0),
               offs.data_ptr(), B, N, max_len, H, dqk, dv, _lib.ptr(bmap), pw.data_ptr(),
               tw.data_ptr(), 128, out.data_ptr(), out.stride(0), _lib.stream_handle())
     torch.cuda.synchronize()
@@ -98,8 +97,7 @@ def test_attn_fwd_full_length_and_len1():
     assert (got - ref).abs().max().item() <= 2e-5 * (1 + ref.abs().max().item())
 
 
-def _run_gpu_bwd(offsets, uvqk, dout, ts, pos_w, ts_w, B, N, H, dqk, dv, hpre=None, bf16=False,
-                 act_in=0):
+def _run_gpu_bwd(offsets, uvqk, dout, ts, pos_w, ts_w, B, N, H, dqk, dv, hpre=None, bf16=False):
     from mygenerativerecommenders_amd import _lib
     dev = torch.device("cuda")
     u = uvqk.to(dev)
@@ -128,7 +126,7 @@ def _run_gpu_bwd(offsets, uvqk, dout, ts, pos_w, ts_w, B, N, H, dqk, dv, hpre=No
     from mygenerativerecommenders_amd import ops
     bmap = ops.bucket_map(tsd, offs, N) if tsd is not None else None
     _lib.call("hstu_attn_bwd_bf16" if bf16 else "hstu_attn_bwd", q.data_ptr(), k.data_ptr(),
-              v.data_ptr(), u.stride(0), u.stride(0), act_in, do.data_ptr(), do.stride(0), offs.data_ptr(), B, N, max_len, H, dqk, dv,
+              v.data_ptr(), u.stride(0), u.stride(0), do.data_ptr(), do.stride(0), offs.data_ptr(), B, N, max_len, H, dqk, dv,
               _lib.ptr(bmap), pw.data_ptr(), tw.data_ptr(), 128,
               hq_p, hk_p, hv_p, u.stride(0) if hd is not None else 0,
               dq.data_ptr(), dk.data_ptr(), dvv.data_ptr(), d.stride(0),

@@ -129,7 +129,7 @@ def test_hstu_train_mode_dropout_statistics():
     stats = torch.empty(rows, 2, device=dev)
     o_in = torch.empty(rows, hv, device=dev)
     y = torch.empty(rows, D, device=dev)
-    _lib.call("hstu_gate_o_fwd", u.data_ptr(), u.stride(0), 0, attn.data_ptr(), hv,
+    _lib.call("hstu_gate_o_fwd", u.data_ptr(), u.stride(0), attn.data_ptr(), hv,
               offsets.data_ptr(), 1, rows, hv, D, w.data_ptr(), b.data_ptr(), None, 0, 1e-6,
               0.2, 1234, None, stats.data_ptr(), o_in.data_ptr(), y.data_ptr(), D,
               _lib.stream_handle())
@@ -155,7 +155,7 @@ def test_hstu_train_mode_dropout_statistics():
     # a device seed offset changes the mask
     off = torch.tensor([7], dtype=torch.int64, device=dev)
     o_in2 = torch.empty_like(o_in)
-    _lib.call("hstu_gate_o_fwd", u.data_ptr(), u.stride(0), 0, attn.data_ptr(), hv,
+    _lib.call("hstu_gate_o_fwd", u.data_ptr(), u.stride(0), attn.data_ptr(), hv,
               offsets.data_ptr(), 1, rows, hv, D, w.data_ptr(), b.data_ptr(), None, 0, 1e-6,
               0.2, 1234, off.data_ptr(), stats.data_ptr(), o_in2.data_ptr(), y.data_ptr(), D,
               _lib.stream_handle())

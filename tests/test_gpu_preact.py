@@ -184,12 +184,13 @@ def test_encoder_preact_only_matches_default(bf16, B, N0, D, H, dh, blocks):
                item_embedding_dim=D, num_blocks=blocks, num_heads=H, linear_dim=dh,
                attention_dim=dh, normalization="rel_bias", linear_config="uvqk",
                linear_activation="silu", linear_dropout_rate=0.2, attn_dropout_rate=0.0,
-               **({"autocast_dtype": torch.bfloat16} if bf16 else {})).cuda().train()
+               **({"autocast_dtype": torch.bfloat16} if bf16 else {}))
     g = torch.Generator().manual_seed(5)
     with torch.no_grad():
         for layer in enc._hstu._attention_layers:
             layer._rel_attn_bias._ts_w.normal_(0, 0.3, generator=g)
             layer._rel_attn_bias._pos_w.normal_(0, 0.3, generator=g)
+    enc = enc.cuda().train()
     lengths = torch.randint(20, N0 + 1, (B,), generator=g).cuda()
     x = torch.randn(B, N, D, generator=g).cuda()
     ts = (1_000_000_000 + torch.cumsum(torch.randint(0, 200_000, (B, N), generator=g), 1)).cuda()
