@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GR_HSTU_ABI_VERSION 8
+#define GR_HSTU_ABI_VERSION 10
 
 #ifndef GR_API
 #define GR_API __attribute__((visibility("default")))
@@ -145,7 +145,8 @@ GR_API int gr_preproc_bwd(const float* dy, const int64_t* past_ids, int B, int N
  * CategoricalEmbeddingModule uses with its mapped ids).  Ids outside a table read 0.
  * Backward: dw0 / dw1 (either may be NULL) are zeroed, then dW[row] += dout[i] for every
  * gathering i, except row padding_idx (nn.Embedding padding_idx; < 0 = none); fp32
- * atomics, unordered like index_add_. */
+ * atomics, unordered like index_add_.  GR_OPT_DETERMINISTIC: owner-computes in id order,
+ * limited to ceil(max(rows0, rows1) / 8) * n <= 2^33. */
 GR_API int gr_item_embedding_fwd(const int64_t* ids, int64_t n, const float* w0, int64_t rows0,
                                  int d0, const float* w1, int64_t rows1, int d1,
                                  const int64_t* map1, int64_t map_len, float* out, void* stream);

@@ -87,9 +87,18 @@ class GrError(RuntimeError):
 
 
 def call(name: str, *args):
-    """Calls a C-ABI entry point; raises GrError(gr_last_error()) on non-zero status."""
+    """Calls a C-ABI entry point; raises GrError(gr_last_error()) on non-zero status.
+
+    The argument count must equal the header's: ctypes would pass surplus arguments as
+    varargs, so a caller written against another ABI version would shift every later
+    pointer and size silently.
+    """
     L = lib()
-    rc = getattr(L, name)(*args)
+    fn = getattr(L, name)
+    if len(args) != len(fn.argtypes):
+        raise GrError(f"{name} takes {len(fn.argtypes)} arguments (gr_hstu.h, ABI "
+                      f"{L.gr_version()}), got {len(args)}")
+    rc = fn(*args)
     if rc != 0:
         msg = L.gr_last_error().decode(errors="replace")
         raise GrError(f"{name} failed (status {rc}): {msg}")

@@ -172,6 +172,14 @@ int gr_item_embedding_bwd(const int64_t* ids, int64_t n, const float* dout, int6
     GR_REQUIRE(d0 <= 128 && d1 <= 128, "gr_item_embedding_bwd: deterministic mode needs d <= 128");
     GR_REQUIRE(n <= 0x7fffffffLL, "gr_item_embedding_bwd: n too large");
     GR_REQUIRE(n == 0 || (ids && dout), "gr_item_embedding_bwd: null pointer");
+    {
+      // every owner workgroup scans all n ids: bound the scan work (the mode is a
+      // reproducibility check, not a production path; 2^33 id reads is ~C5 size)
+      const int64_t rm = rows0 > rows1 ? rows0 : rows1;
+      GR_REQUIRE((rm + gr::EMB_OWN - 1) / gr::EMB_OWN * (double)n <= 8589934592.0,
+                 "gr_item_embedding_bwd: deterministic mode limited to ceil(rows/8) * n <= 2^33 "
+                 "(rows=%lld n=%lld)", (long long)rm, (long long)n);
+    }
     gr::EmbArgs a{};
     a.ids = ids; a.n = n; a.rows0 = rows0; a.d0 = d0;
     a.rows1 = rows1; a.d1 = d1; a.map1 = map1; a.map_len = map_len;

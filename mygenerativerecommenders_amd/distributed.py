@@ -93,27 +93,53 @@ class BucketedGradReducer:
     * Each bucket is one persistent fp32 buffer.  A post-accumulate-grad hook scales the
       fresh gradient by 1/world straight into the parameter's slice of its bucket (one
       kernel, no torch.cat, no copy back) and re-points ``p.grad`` at that slice.
-    * ``overlap=True``: the hook that completes a bucket launches its all-reduce
-      (async; RCCL runs it on its own stream while the backward continues).
-      ``overlap=False``: hooks only pack (e.g. inside a captured HIP graph) and
-      ``finish()`` launches the buckets.
-    * ``finish()`` launches what is left, waits, and zero-fills the slices of
-      parameters that got no gradient this step (so every rank reduces the same bytes).
+    * Collectives are issued strictly in bucket order on every rank (as DDP does): a
+      completed bucket is launched only once every bucket before it has been, so ranks
+      whose hooks fire in different orders still pair the same buffers.
+      ``overlap=True``: hooks launch the ready prefix during the backward (async; RCCL
+      runs it on its own stream).  ``overlap=False``: hooks only pack (e.g. inside a
+      captured HIP graph) and ``finish()`` launches every bucket.
+    * ``row_support={param: rows}`` (embedding tables): the caller guarantees that the
+      gradient of ``param`` is zero outside ``rows`` on every rank -- e.g. the year
+      table of ``LocalEmbeddingModule``, whose gradient can only land on the years the
+      item -> year map produces (``LocalEmbeddingModule.grad_row_support``).  Only those
+      rows travel; the result is identical to the dense exchange.
+    * ``finish()`` launches what is left, waits, and writes the averages back where
+      needed.  A parameter that got no gradient on this rank contributes zeros.  With
+      ``find_unused_parameters=True`` one extra small all-reduce counts, per parameter,
+      the ranks that produced a gradient; parameters no rank touched get ``grad = None``
+      (as DDP leaves them), so the optimizer skips them.  Without it (DDP's default,
+      which would raise on such a parameter) they get a zero gradient.
     ``zero_grad()`` must run before each backward (set_to_none, so the backward's
     output is stolen, not accumulated into the bucket view)."""
 
     def __init__(self, params: List[torch.nn.Parameter], group=None,
-                 bucket_bytes: int = 25 << 20, overlap: bool = True):
+                 bucket_bytes: int = 25 << 20, overlap: bool = True,
+                 row_support: Optional[dict] = None, find_unused_parameters: bool = False):
         self.params = [p for p in params if p.requires_grad]
         self.group = group
         self.overlap = overlap
+        self.find_unused = find_unused_parameters
         dist_on = dist.is_available() and dist.is_initialized()
         self.world = dist.get_world_size(group) if dist_on else 1
         self.scale = 1.0 / self.world
+        self.rows = {}
+        for p, r in (row_support or {}).items():
+            if p.dim() < 1:
+                raise ValueError("row_support: parameter must have a row dimension")
+            r = torch.as_tensor(r, dtype=torch.int64).reshape(-1).unique()  # sorted, unique
+            if r.numel() and (int(r[0]) < 0 or int(r[-1]) >= p.shape[0]):
+                raise ValueError("row_support: row index outside the parameter")
+            self.rows[p] = r.to(p.device)
+
+        def exch_numel(p):
+            r = self.rows.get(p)
+            return p.numel() if r is None else r.numel() * (p.numel() // max(1, p.shape[0]))
+
         self.buckets: List[List[torch.nn.Parameter]] = []
         cur, size = [], 0
         for p in reversed(self.params):
-            nb = p.numel() * 4
+            nb = exch_numel(p) * 4
             if cur and size + nb > bucket_bytes:
                 self.buckets.append(cur)
                 cur, size = [], 0
@@ -124,31 +150,48 @@ class BucketedGradReducer:
         self.buffers: List[torch.Tensor] = []
         self.slot = {}
         for bi, bucket in enumerate(self.buckets):
-            buf = torch.zeros(sum(p.numel() for p in bucket), dtype=torch.float32,
+            buf = torch.zeros(sum(exch_numel(p) for p in bucket), dtype=torch.float32,
                               device=bucket[0].device)
             off = 0
             for p in bucket:
-                self.slot[p] = (bi, buf[off:off + p.numel()].view_as(p))
-                off += p.numel()
+                n = exch_numel(p)
+                shape = p.shape if p not in self.rows else (self.rows[p].numel(),) + tuple(p.shape[1:])
+                self.slot[p] = (bi, buf[off:off + n].view(shape))
+                off += n
             self.buffers.append(buf)
+        self.index = {p: i for i, p in enumerate(self.params)}
+        self.exchange_bytes = sum(4 * b.numel() for b in self.buffers)
+        self._reset()
+        self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
+
+    def _reset(self):
         self._ready = [0] * len(self.buckets)
         self._handles: List[Optional[object]] = [None] * len(self.buckets)
+        self._next = 0
         self._seen = set()
-        self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
 
     def zero_grad(self):
         for p in self.params:
             p.grad = None
 
-    def _launch(self, bi: int):
-        if self.world > 1 and self._handles[bi] is None:
-            self._handles[bi] = dist.all_reduce(self.buffers[bi], op=dist.ReduceOp.SUM,
-                                                group=self.group, async_op=True)
+    def _launch_ready(self, upto_all: bool = False):
+        """Launches buckets in index order: the consecutive run of complete buckets from
+        the next unlaunched one (every remaining bucket when ``upto_all``)."""
+        while self._next < len(self.buckets) and (
+                upto_all or self._ready[self._next] == len(self.buckets[self._next])):
+            if self.world > 1:
+                self._handles[self._next] = dist.all_reduce(
+                    self.buffers[self._next], op=dist.ReduceOp.SUM, group=self.group,
+                    async_op=True)
+            self._next += 1
 
     def _on_grad(self, p: torch.nn.Parameter):
         bi, view = self.slot[p]
         g = p.grad
-        if g is not view:
+        rows = self.rows.get(p)
+        if rows is not None:  # only the supported rows travel; p.grad stays dense
+            torch.mul(g.index_select(0, rows), self.scale, out=view)
+        elif g is not view:
             if self.scale != 1.0:
                 torch.mul(g, self.scale, out=view)
             else:
@@ -158,24 +201,39 @@ class BucketedGradReducer:
             self._seen.add(p)
             self._ready[bi] += 1
             if self.overlap and self._ready[bi] == len(self.buckets[bi]):
-                self._launch(bi)
+                self._launch_ready()
 
     def finish(self):
         """Completes the step's exchange: after it every .grad is the group average."""
-        for bi, bucket in enumerate(self.buckets):
-            if self._ready[bi] < len(bucket):
-                for p in bucket:
-                    if p not in self._seen:
-                        view = self.slot[p][1]
-                        view.zero_()
-                        p.grad = view
-            self._launch(bi)
+        unseen = [p for p in self.params if p not in self._seen]
+        for p in unseen:
+            view = self.slot[p][1]
+            view.zero_()
+            if p not in self.rows:
+                p.grad = view
+            else:
+                p.grad = torch.zeros_like(p)
+        self._launch_ready(upto_all=True)
+        used = None
+        if self.find_unused and self.world > 1:
+            used = torch.ones(len(self.params), dtype=torch.float32, device=self.buffers[0].device)
+            for p in unseen:
+                used[self.index[p]] = 0.0
+            dist.all_reduce(used, op=dist.ReduceOp.SUM, group=self.group)
         for h in self._handles:
             if h is not None:
                 h.wait()
-        self._ready = [0] * len(self.buckets)
-        self._handles = [None] * len(self.buckets)
-        self._seen = set()
+        if self.world > 1:  # scatter the averaged rows into the dense gradients
+            for p, rows in self.rows.items():
+                p.grad.index_copy_(0, rows, self.slot[p][1])
+        if used is not None:
+            for p, u in zip(self.params, used.tolist()):
+                if u == 0.0:
+                    p.grad = None
+        elif self.find_unused:
+            for p in unseen:
+                p.grad = None
+        self._reset()
 
     def remove_hooks(self):
         for h in self._hooks:

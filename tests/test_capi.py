@@ -58,6 +58,19 @@ def test_error_is_raised_as_python_exception():
         _lib.call("hstu_attn_fwd", *vals)
 
 
+def test_call_rejects_wrong_argument_count():
+    """ctypes passes surplus arguments as varargs; _lib.call must refuse them (and short
+    lists) before anything reaches the library."""
+    _, args = _lib.parse_header()["hstu_attn_fwd"]
+    vals = [None if a.endswith("*") else 1 for a in args]
+    with pytest.raises(_lib.GrError, match="takes 19 arguments"):
+        _lib.call("hstu_attn_fwd", *vals, 0)
+    with pytest.raises(_lib.GrError, match="takes 19 arguments"):
+        _lib.call("hstu_attn_fwd", *vals[:-1])
+    with pytest.raises(_lib.GrError, match="got 0"):
+        _lib.call("gr_wgrad")
+
+
 def test_workspace_size_queries_are_host_only():
     L = _lib.lib()
     slabs = 4 * 128 * 4 * (2 * 211 - 1 + 129)

@@ -232,3 +232,182 @@ def test_dp_hstu_bucketed_overlap_world2_equals_full_batch(overlap):
         p.join(timeout=60)
     for rank, msg in results:
         assert msg == "ok", f"rank {rank}: {msg}"
+
+
+# ---------------------------------------------------------------- C5 with item tables
+# LocalEmbeddingModule's two (num_items + 1, D/2) tables join the exchange (reference DDP
+# all-reduces every parameter, configs/trainer/ddp.yaml).  The year table goes through
+# the reducer's row_support (only the rows the item -> year map can reach travel).  The
+# table gathers run test-side with torch ops on the CPU (the module's own gather is a
+# HIP kernel); a second gather of random "negative" rows touches most item rows.
+
+def _tables_case():
+    from mygenerativerecommenders_amd.embeddings import LocalEmbeddingModule
+    enc, lengths, x, ts, dy, blocks = _hstu_case()
+    V, D = 97, x.shape[-1]
+    torch.manual_seed(3)
+    item2year = {i: 1990 + (i % 7) for i in range(1, V + 1)}  # years index the year table
+    emb = LocalEmbeddingModule(2100, D, item2year=item2year)
+    g = torch.Generator().manual_seed(4)
+    B, N = x.shape[1], x.shape[2]
+    ids = torch.randint(1, V + 1, (2, B, N), generator=g)
+    ids[:, :, -2:] = 0  # padding ids: no table gradient (padding_idx 0)
+    neg = torch.randint(0, V + 1, (2, B, 64), generator=g)
+    wneg = torch.randn(2, B, 64, D // 2, generator=g)
+    return enc, emb, lengths, ids, neg, wneg, ts, dy, blocks
+
+
+def _tables_loss(enc, emb, blocks, lengths, ids, neg, wneg, ts, dy, x_noise):
+    item_w, year_w = emb._item_emb.weight, emb._year_emb.weight
+    yid = emb.year_lookup_table[ids.clamp(0, emb.year_lookup_table.numel() - 1)]
+    xe = torch.cat([torch.nn.functional.embedding(ids, item_w, padding_idx=0),
+                    torch.nn.functional.embedding(yid, year_w, padding_idx=0)], -1)
+    loss = _hstu_loss(enc, blocks, lengths, xe + x_noise, ts, dy)
+    negs = torch.nn.functional.embedding(neg, item_w, padding_idx=0)
+    return loss + (negs * wneg).sum() / ids.shape[0]
+
+
+def _tables_train(enc, emb, blocks, case, rows, reducer=None, halves=None):
+    from mygenerativerecommenders_amd.distributed import muon_adamw_split
+    lengths, ids, neg, wneg, ts, dy, x_noise = case
+    named = list(emb.named_parameters(prefix="_embedding_module")) + list(enc.named_parameters())
+    params = [p for _, p in named]
+    opts = muon_adamw_split(named)
+    grads = []
+    for step in range(2):
+        for p in params:
+            p.grad = None
+        if halves is None:
+            _tables_loss(enc, emb, blocks, lengths[rows], ids[step][rows], neg[step][rows],
+                         wneg[step][rows], ts[rows], dy[step][rows], x_noise[step][rows]).backward()
+        else:
+            parts = []
+            for h in halves:
+                for p in params:
+                    p.grad = None
+                _tables_loss(enc, emb, blocks, lengths[h], ids[step][h], neg[step][h],
+                             wneg[step][h], ts[h], dy[step][h], x_noise[step][h]).backward()
+                parts.append([p.grad.clone() for p in params])
+            for p, g0, g1 in zip(params, *parts):
+                p.grad = torch.mul(g0, 0.5) + torch.mul(g1, 0.5)
+        if reducer is not None:
+            reducer.finish()
+        grads.append([p.grad.clone() for p in params])
+        for o in opts:
+            o.step()
+    return grads, [p.detach().clone() for p in params]
+
+
+def _dp_tables_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    try:
+        import copy
+        from mygenerativerecommenders_amd.distributed import BucketedGradReducer, init_from_env
+        init_from_env("gloo")
+        enc, emb, lengths, ids, neg, wneg, ts, dy, blocks = _tables_case()
+        x_noise = torch.randn(2, *ids.shape[1:], enc._embedding_dim,
+                              generator=torch.Generator().manual_seed(9)) * 0.01
+        case = (lengths, ids, neg, wneg, ts, dy, x_noise)
+        B = lengths.numel()
+        halves = [slice(r * B // world, (r + 1) * B // world) for r in range(world)]
+        full_g, _ = _tables_train(copy.deepcopy(enc), copy.deepcopy(emb), blocks, case, slice(0, B))
+        ref_g, ref_p = _tables_train(copy.deepcopy(enc), copy.deepcopy(emb), blocks, case, None,
+                                     halves=halves)
+        params = list(emb.parameters()) + list(enc.parameters())
+        support = emb.grad_row_support()
+        yrows = support[emb._year_emb.weight]
+        assert yrows.tolist() == list(range(1990, 1997))
+        red = BucketedGradReducer(params, bucket_bytes=16 << 10, overlap=True,
+                                  row_support=support)
+        dense_bytes = 4 * sum(p.numel() for p in params)
+        assert red.exchange_bytes == dense_bytes - 4 * (emb._year_emb.weight.numel()
+                                                        - yrows.numel() * emb._year_emb.weight.shape[1])
+        got_g, got_p = _tables_train(enc, emb, blocks, case, halves[rank], red)
+        # 2 ranks x B/2 == 1 process x B, tables included (fp32 summation tolerance)
+        for g, r in zip(got_g[0], full_g[0]):
+            assert torch.allclose(g, r, rtol=1e-5, atol=1e-6), (g - r).abs().max()
+        # the item table gradient touches most rows; the year table only the mapped years
+        assert (got_g[0][0].abs().sum(1) > 0).sum() > 80
+        ynz = (got_g[0][1].abs().sum(1) > 0).nonzero().reshape(-1)
+        assert set(ynz.tolist()) <= set(yrows.tolist()) and ynz.numel() > 0
+        # bit-identical to the same 0.5 g0 + 0.5 g1 averaging in one process, 2 steps
+        for step in range(2):
+            for g, r in zip(got_g[step], ref_g[step]):
+                assert torch.equal(g, r), (step, (g - r).abs().max())
+        for p, r in zip(got_p, ref_p):
+            assert torch.equal(p, r), (p - r).abs().max()
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, "ok"))
+    except Exception:
+        import traceback
+        q.put((rank, traceback.format_exc()))
+        raise
+
+
+def _spawn(target, world=2, timeout=300):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=timeout) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, msg in results:
+        assert msg == "ok", f"rank {rank}: {msg}"
+
+
+def test_dp_with_item_tables_world2_equals_full_batch():
+    _spawn(_dp_tables_worker)
+
+
+def _unused_worker(rank, world, port, q):
+    """A parameter that only rank 0 uses sits in the FIRST bucket; on rank 1 the later
+    buckets complete first.  Launching in bucket order keeps the collectives paired;
+    find_unused_parameters leaves a parameter no rank used at grad None."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    try:
+        from mygenerativerecommenders_amd.distributed import BucketedGradReducer, init_from_env
+        init_from_env("gloo")
+        torch.manual_seed(0)
+        a = torch.nn.Parameter(torch.randn(6, 5))
+        b = torch.nn.Parameter(torch.randn(5, 4))
+        c = torch.nn.Parameter(torch.randn(40))   # used by rank 0 only
+        never = torch.nn.Parameter(torch.randn(3))
+        for find_unused in (True, False):
+            red = BucketedGradReducer([a, b, never, c], bucket_bytes=64, overlap=True,
+                                      find_unused_parameters=find_unused)
+            assert red.buckets[0] == [c]
+            x = torch.randn(3, 6, generator=torch.Generator().manual_seed(rank))
+            red.zero_grad()
+            loss = (x @ a @ b).square().sum()
+            if rank == 0:
+                loss = loss + c.sin().sum()
+            loss.backward()
+            red.finish()
+            ga = [torch.empty_like(a) for _ in range(world)]
+            xa = (x @ a @ b)
+            ref_a = torch.autograd.grad(xa.square().sum(), a)[0]
+            dist.all_gather(ga, ref_a)
+            assert torch.allclose(a.grad, sum(ga) / world, atol=1e-5)
+            assert torch.allclose(c.grad, c.detach().cos() / world, atol=1e-6)
+            if find_unused:
+                assert never.grad is None
+            else:
+                assert torch.equal(never.grad, torch.zeros(3))
+            red.remove_hooks()
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, "ok"))
+    except Exception:
+        import traceback
+        q.put((rank, traceback.format_exc()))
+        raise
+
+
+def test_bucket_order_with_rank_dependent_unused_parameter_world2():
+    _spawn(_unused_worker, timeout=120)
