@@ -169,14 +169,22 @@ def _gpu_hold_fn():
     return hold
 
 
-def e2e_train_leg(args, device, world, lengths, ts, past_ids):
-    """The whole reference training step (train.py train_fn inner loop, ml-1m config:
-    SampledSoftmaxLoss with 128 local negatives, temperature 0.05, l2-normalised items):
+def e2e_train_leg(args, device, world, lengths, ts, past_ids, N0=None, D=None, blocks=None,
+                  V=None, steps=None, c5=False):
+    """The whole reference training step (train.py train_fn inner loop: SampledSoftmaxLoss
+    with 128 local negatives, temperature 0.05, l2-normalised items):
     LocalEmbeddingModule lookup -> positional preprocessor -> HSTU -> L2 postprocessor ->
-    jagged sampled-softmax loss -> backward -> gradient all-reduce -> AdamW.
+    jagged sampled-softmax loss -> backward -> gradient exchange -> optimizer.
+    Default (C2 shapes): one flat all-reduce + fused AdamW, captured as two graphs.
+    ``c5``: the ml-20m-width recipe -- the item tables join the exchange through the
+    bucketed reducer (reverse-order buckets launched in index order during the backward;
+    the year table by row_support), Muon + AdamW split (generative_recommenders.py:297-310);
+    eager at N > 1 (collectives issued from gradient hooks), graphs at N = 1.
     Reported beside the headline, which times the encoder step the north star names."""
-    from mygenerativerecommenders_amd.distributed import FlatGradAllReducer
+    from mygenerativerecommenders_amd.distributed import (BucketedGradReducer, FlatGradAllReducer,
+                                                          muon_adamw_split)
     from mygenerativerecommenders_amd.embeddings import LocalEmbeddingModule
+    from mygenerativerecommenders_amd.hstu import HSTU
     from mygenerativerecommenders_amd.losses import SampledSoftmaxLoss
     from mygenerativerecommenders_amd.negatives_sampler import LocalNegativesSampler
     from mygenerativerecommenders_amd.ops import (asynchronous_complete_cumsum,
@@ -185,24 +193,60 @@ def e2e_train_leg(args, device, world, lengths, ts, past_ids):
         LearnablePositionalEmbeddingInputFeaturesPreprocessor as Pre)
     from mygenerativerecommenders_amd.similarity import DotProductSimilarity
 
-    B, N0, out_len, D, blocks = args.batch, args.seq, args.out_len, args.dim, args.blocks
+    B = lengths.numel()
+    N0 = N0 or args.seq
+    D = D or args.dim
+    blocks = blocks or args.blocks
+    V = V or args.catalog
+    steps = steps or args.e2e_steps
+    out_len = args.out_len
     N = N0 + out_len
-    V = args.catalog
-    enc = build_model(N0, out_len, D, blocks, device)
-    emb = LocalEmbeddingModule(V, D).to(device)  # no year CSV: every year row is 0
+    torch.manual_seed(0)
+    enc = HSTU(max_sequence_len=N0, max_output_len=out_len, embedding_dim=D,
+               item_embedding_dim=D, num_blocks=blocks, num_heads=1, linear_dim=D,
+               attention_dim=D, normalization="rel_bias", linear_config="uvqk",
+               linear_activation="silu", linear_dropout_rate=0.2,
+               attn_dropout_rate=0.0).to(device).train()
+    # C2: no year CSV (every year row 0, as the reference without its file); C5: a
+    # synthetic item -> year map (years 1919..2015) so the year table carries gradients
+    item2year = {i: 1919 + (i * 7919) % 97 for i in range(1, V + 1)} if c5 else None
+    emb = LocalEmbeddingModule(V, D, item2year=item2year).to(device)
     pre = Pre(N, D, 0.2).to(device).train()
     sampler = LocalNegativesSampler(True, 1e-6, all_item_ids=list(range(1, V + 1))).to(device)
     sampler._embeddings_module = emb
     loss_mod = SampledSoftmaxLoss(128, 0.05)
     sim = DotProductSimilarity()
-    params = list(enc.parameters()) + list(emb.parameters()) + list(pre.parameters())
-    reducer = FlatGradAllReducer(params)
-    try:  # one fused multi-tensor kernel per step (same AdamW math), as in the headline leg
-        opt = torch.optim.AdamW(params, lr=1e-3, betas=(0.9, 0.98), weight_decay=1e-3,
-                                fused=True, capturable=True)
-    except (RuntimeError, TypeError, ValueError):
-        opt = torch.optim.AdamW(params, lr=1e-3, betas=(0.9, 0.98), weight_decay=1e-3,
-                                capturable=True)
+    named = (list(emb.named_parameters(prefix="_embedding_module"))
+             + list(pre.named_parameters(prefix="_input_preproc_module"))
+             + list(enc.named_parameters(prefix="_hstu")))
+    params = [p for _, p in named]
+    eager = args.eager
+    if c5:
+        support = emb.grad_row_support()
+        reducer = BucketedGradReducer(params, bucket_bytes=25 << 20, overlap=world > 1,
+                                      row_support=support)
+        eager = eager or world > 1
+        opts = muon_adamw_split(named, **({} if eager else {"fused": True, "capturable": True}))
+        xbytes = reducer.exchange_bytes
+    else:
+        reducer = FlatGradAllReducer(params)
+        try:  # one fused multi-tensor kernel per step (same AdamW math), as in the headline leg
+            opts = [torch.optim.AdamW(params, lr=1e-3, betas=(0.9, 0.98), weight_decay=1e-3,
+                                      fused=True, capturable=True)]
+        except (RuntimeError, TypeError, ValueError):
+            opts = [torch.optim.AdamW(params, lr=1e-3, betas=(0.9, 0.98), weight_decay=1e-3,
+                                      capturable=True)]
+        xbytes = 4 * sum(p.numel() for p in params)
+
+    def opt_step():
+        for o in opts:
+            o.step()
+
+    def exchange(inplace=False):
+        if c5:
+            reducer.finish()
+        else:
+            reducer.allreduce(world, inplace=inplace)
     # the target sits at position `length` (train.py: scatter of target_ids)
     g = torch.Generator(device=device)
     g.manual_seed(11)
@@ -231,8 +275,8 @@ def e2e_train_leg(args, device, world, lengths, ts, past_ids):
     def eager_step():
         reducer.zero_grad()
         loss = fwd_bwd()
-        reducer.allreduce(world)
-        opt.step()
+        exchange()
+        opt_step()
         return loss
 
     diag = os.environ.get("GR_E2E_DIAG") == "1"
@@ -251,20 +295,26 @@ def e2e_train_leg(args, device, world, lengths, ts, past_ids):
     torch.cuda.current_stream().wait_stream(side)
     torch.cuda.synchronize()
     mode, step = "eager", eager_step
-    if not args.eager:
+    if not eager:
         try:
             reducer.zero_grad()
             g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             with torch.cuda.graph(g_fb):
                 fwd_bwd()
             chk("capture fwd+bwd")
+            if c5:
+                exchange()  # world 1: packs the bucket views, no collective
             with torch.cuda.graph(g_opt):
-                opt.step()
+                opt_step()
             chk("capture optimizer")
 
             def replay():
                 g_fb.replay()
-                reducer.allreduce(world, inplace=True)
+                if c5:
+                    if world > 1:
+                        raise RuntimeError("c5 graphs are single-rank only")
+                else:
+                    reducer.allreduce(world, inplace=True)
                 g_opt.replay()
             replay()
             torch.cuda.synchronize()
@@ -272,8 +322,7 @@ def e2e_train_leg(args, device, world, lengths, ts, past_ids):
         except Exception as e:  # report eager numbers rather than none
             print(f"# e2e: graph capture failed ({type(e).__name__}: {e}); eager", flush=True)
             torch.cuda.synchronize()
-    steps = args.e2e_steps
-    for i in range(3):
+    for i in range(3 if not c5 else 1):
         step()
         chk(f"{mode} warm-up step {i}")
     _sync_barrier(world)
@@ -282,11 +331,20 @@ def e2e_train_leg(args, device, world, lengths, ts, past_ids):
         step()
     _sync_barrier(world)
     dt = _max_over_ranks(time.perf_counter() - t0, world)
-    return {"value": round(B * world * steps / dt, 2), "unit": "seq/s",
-            "ms_per_step": round(dt / steps * 1e3, 4), "steps": steps, "execution": mode,
-            "workload": "full train step: embedding lookup + positional preprocessor + "
-                        "HSTU 4 blocks + L2 postprocessor + sampled softmax (128 local "
-                        "negatives, T=0.05) + backward + all-reduce + AdamW"}
+    out = {"value": round(B * world * steps / dt, 2), "unit": "seq/s",
+           "ms_per_step": round(dt / steps * 1e3, 4), "steps": steps, "execution": mode,
+           "global_batch": B * world,
+           "workload": (f"full train step: embedding lookup ({V} items) + positional "
+                        f"preprocessor + HSTU {blocks} blocks d={D} N0={N0} + L2 postprocessor + "
+                        f"sampled softmax (128 local negatives, T=0.05) + backward + "
+                        + ("bucketed all-reduce (tables included) + Muon/AdamW" if c5 else
+                           "all-reduce + AdamW")),
+           "exchange_bytes_per_step": xbytes,
+           "dense_grad_bytes_per_step": 4 * sum(p.numel() for p in params)}
+    del enc, emb, pre, sampler, opts, reducer
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return out
 
 
 def hstu_step_flops(L, D, H, dqk, dv, blocks):
@@ -472,6 +530,8 @@ def main():
     ap.add_argument("--c3-steps", type=int, default=5,
                     help="timed steps of the C3 leg (B=32, N=2059, D=256, 8 blocks; 0 = skip)")
     ap.add_argument("--no-bf16-leg", action="store_true", help="skip the C2 bf16-attention leg")
+    ap.add_argument("--c5-steps", type=int, default=3,
+                    help="timed steps of the full C5-shaped train step (tables, Muon; 0 = skip)")
     ap.add_argument("--cpu-batch", type=int, default=128,
                     help="sequences per iteration of the CPU proxy baseline")
     args = ap.parse_args()
@@ -648,10 +708,38 @@ def main():
             r_ids, r_scores = sidx.get_top_k_outputs(Q, invalid_ids=inv)
         r_check = check_retrieval(Q, shard, a, inv, r_ids, r_scores, args.k, world)
         del shard
+        # the local top-k (no collective, no host sync) is replayed as a HIP graph; the
+        # all-gather + merge of N > 1 runs eagerly after it
+        r_exec = "eager"
+        r_step = lambda: sidx.get_top_k_outputs(Q, invalid_ids=inv)  # noqa: E731
+        if not args.eager:
+            side_r = torch.cuda.Stream()
+            side_r.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side_r):
+                sidx.local_top_k(Q, inv)
+            torch.cuda.current_stream().wait_stream(side_r)
+            torch.cuda.synchronize()
+            g_r = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g_r):
+                gs_, gi_, gx_ = sidx.local_top_k(Q, inv)
+
+            def r_step():
+                g_r.replay()
+                if world > 1:
+                    from mygenerativerecommenders_amd.distributed import gather_and_merge
+                    return gather_and_merge(gs_, gi_, gx_, args.k)
+                return gi_, gs_
+            gi_chk, gs_chk = r_step()
+            torch.cuda.synchronize()
+            if not (torch.equal(gi_chk, r_ids) and torch.equal(gs_chk, r_scores)):
+                raise RuntimeError("retrieval: graph replay differs from the eager result")
+            r_exec = "hip-graph replay (local top-k)" + (" + eager all-gather/merge" if world > 1 else "")
+        for _ in range(3):
+            r_step()
         _sync_barrier(world)
         t1 = time.perf_counter()
         for _ in range(args.retrieval_steps):
-            sidx.get_top_k_outputs(Q, invalid_ids=inv)
+            r_step()
         _sync_barrier(world)
         dtr = time.perf_counter() - t1
         # per-kernel durations from a separate instrumented pass (the timed loop above
@@ -712,7 +800,7 @@ def main():
                                    if world > 1 else
                                    ("C4: 10M-item catalog on 1 GPU (one shard, no merge), "
                                     "B=128 queries, k=200, 211 invalid ids"),
-                       "items": X, "queries": B, "k": args.k, "dim": D,
+                       "items": X, "queries": B, "k": args.k, "dim": D, "execution": r_exec,
                        "filter_scores": "bf16 (exact f32 rescoring)" if bf16_filter else "f32"},
             "check": r_check,
             "per_query_batch_device_ms": r_dev,
@@ -790,6 +878,19 @@ def main():
         except Exception as e:  # the headline line must still print
             e2e = {"error": f"{type(e).__name__}: {e}"}
 
+    c5_full = None
+    if args.c5_steps > 0:
+        try:
+            B5, N5, D5, L5, V5 = 32, 2048, 256, 8, 131_262
+            l5, _, t5, p5, _ = make_batch(B5, N5, args.out_len, 1, 4000 + rank, device)
+            p5 = torch.where(p5 > 0, (p5 * 33) % V5 + 1, p5)  # ids over the ml-20m catalog
+            c5_full = e2e_train_leg(args, device, world, l5, t5, p5, N0=N5, D=D5, blocks=L5,
+                                    V=V5, steps=args.c5_steps, c5=True)
+            c5_full["config"] = ("C5 shapes" if world > 1 else "C5 shapes on one GPU") + \
+                f": B={B5}/rank, N0={N5}, D={D5}, {L5} blocks, {V5} items (item + year tables)"
+        except Exception as e:  # the headline line must still print
+            c5_full = {"error": f"{type(e).__name__}: {e}"}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = torch.get_num_threads()  # the box's CPU share (OMP_NUM_THREADS)
@@ -832,6 +933,7 @@ def main():
             "c3_bf16": c3_bf16,
             "c2_bf16": c2_bf16,
             "e2e_train_step": e2e,
+            "c5_train_step": c5_full,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -38,6 +38,11 @@ static std::atomic<bool> g_tm_on{false};
 
 bool timing_enabled() { return g_tm_on.load(std::memory_order_relaxed); }
 
+const char*& timing_region() {
+  static thread_local const char* name = nullptr;
+  return name;
+}
+
 void timing_push(const char* name, hipEvent_t start, hipEvent_t stop) {
   std::lock_guard<std::mutex> lk(g_tm_mu);
   g_tm.push_back({name, start, stop});

@@ -1,6 +1,7 @@
 // Shared device/host helpers for the gfx950 HSTU + MIPS library.
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -11,6 +12,11 @@
 #include <string>
 
 #include "../../include/gr_hstu.h"
+
+// Every hipLaunchKernelGGL in this library's sources goes through gr::launch_kernel (timed
+// inside GR_TIMED regions when timing is on).
+#undef hipLaunchKernelGGL
+#define hipLaunchKernelGGL(kernelName, ...) ::gr::launch_kernel((kernelName), __VA_ARGS__)
 
 namespace gr {
 
@@ -29,25 +35,37 @@ int64_t option(int which);
   } while (0)
 
 // ---------------------------------------------------------------- live kernel timing
-// When enabled (gr_timing_enable), every launch site records a HIP event pair on the
-// launch stream; gr_timing_query drains and sums them per kernel name.
+// When enabled (gr_timing_enable), every kernel launched inside a GR_TIMED region is
+// dispatched through hipExtLaunchKernel with a start / stop event pair that the dispatch
+// packet itself timestamps (the same begin / end a rocprofv3 kernel trace reports; no
+// separate event-record packets around the launch); gr_timing_query drains and sums
+// them per kernel name.
 bool timing_enabled();
 void timing_push(const char* name, hipEvent_t start, hipEvent_t stop);
+const char*& timing_region();  // name of the enclosing GR_TIMED region (thread-local)
 
-#define GR_TIMED(name, stream, ...)                                          \
-  do {                                                                       \
-    hipEvent_t e0_ = nullptr, e1_ = nullptr;                                 \
-    const bool tm_ = ::gr::timing_enabled();                                 \
-    if (tm_) {                                                               \
-      (void)hipEventCreate(&e0_);                                            \
-      (void)hipEventCreate(&e1_);                                            \
-      (void)hipEventRecord(e0_, (stream));                                   \
-    }                                                                        \
-    __VA_ARGS__;                                                             \
-    if (tm_) {                                                               \
-      (void)hipEventRecord(e1_, (stream));                                   \
-      ::gr::timing_push((name), e0_, e1_);                                   \
-    }                                                                        \
+template <typename F, typename... Args>
+inline void launch_kernel(F kernel, const dim3& grid, const dim3& block, uint32_t shmem,
+                          hipStream_t st, Args... args) {
+  const char* name = timing_region();
+  if (name && timing_enabled()) {
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    hipExtLaunchKernelGGL(kernel, grid, block, shmem, st, e0, e1, 0, args...);
+    timing_push(name, e0, e1);
+  } else {
+    kernel<<<grid, block, shmem, st>>>(args...);
+  }
+}
+
+#define GR_TIMED(name, stream, ...)                 \
+  do {                                              \
+    const char* prev_ = ::gr::timing_region();      \
+    ::gr::timing_region() = (name);                 \
+    (void)(stream);                                 \
+    __VA_ARGS__;                                    \
+    ::gr::timing_region() = prev_;                  \
   } while (0)
 
 #define GR_LAUNCH_CHECK(what)                                                   \

@@ -281,18 +281,25 @@ class ShardedCandidateIndex:
         self.group = group
         self.packed = PackedItems(emb_shard.float().contiguous())
 
-    def get_top_k_outputs(self, query_embeddings: torch.Tensor,
-                          invalid_ids: Optional[torch.Tensor] = None, k: Optional[int] = None):
-        from .top_k import merge_topk, mips_topk
+    def local_top_k(self, query_embeddings: torch.Tensor,
+                    invalid_ids: Optional[torch.Tensor] = None, k: Optional[int] = None):
+        """This rank's (scores, ids, global index) (B, k): no collective, no host sync,
+        so it can be captured in a HIP graph."""
+        from .top_k import mips_topk
         k = k or self.k
         if self.arange_base is not None:  # global index = id (monotone in the row)
-            s, i, x = mips_topk(query_embeddings, self.packed, k, item_ids=None,
-                                invalid_ids=invalid_ids, index_base=self.arange_base,
-                                return_index=True)
-        else:
-            s, i, x = mips_topk(query_embeddings, self.packed, k, item_ids=self.ids,
-                                invalid_ids=invalid_ids, index_base=self.row_offset,
-                                return_index=True)
+            return mips_topk(query_embeddings, self.packed, k, item_ids=None,
+                             invalid_ids=invalid_ids, index_base=self.arange_base,
+                             return_index=True)
+        return mips_topk(query_embeddings, self.packed, k, item_ids=self.ids,
+                         invalid_ids=invalid_ids, index_base=self.row_offset,
+                         return_index=True)
+
+    def get_top_k_outputs(self, query_embeddings: torch.Tensor,
+                          invalid_ids: Optional[torch.Tensor] = None, k: Optional[int] = None):
+        from .top_k import merge_topk
+        k = k or self.k
+        s, i, x = self.local_top_k(query_embeddings, invalid_ids, k)
         return gather_and_merge(s, i, x, k, self.group, merge_topk)
 
 

@@ -48,6 +48,18 @@ class PackedItems:
         _lib.call("mips_pack_items", items.data_ptr(), self.X, self.D, self.buf.data_ptr(),
                   _lib.stream_handle())
         self.device = items.device
+        self._ws = {}  # (B, k, N0) -> (bytes, reusable workspace): no per-call allocation
+
+    def workspace(self, B: int, k: int, N0: int):
+        """The cached workspace for a (B, k, N0) call (stream-ordered reuse: calls on one
+        stream never overlap)."""
+        key = (B, k, N0)
+        ent = self._ws.get(key)
+        if ent is None:
+            n = topk_workspace_bytes(B, self.X, self.D, k, N0)
+            ent = (n, torch.empty(n, dtype=torch.uint8, device=self.device))
+            self._ws[key] = ent
+        return ent
 
 
 K_MAX = 4096
@@ -74,17 +86,22 @@ def mips_topk(queries: torch.Tensor, packed: PackedItems, k: int,
         raise ValueError(f"query dim {D} != item dim {packed.D}")
     if not 0 < k <= K_MAX:
         raise ValueError(f"mips_topk supports 0 < k <= {K_MAX} (got {k})")
-    q = queries.contiguous().float()
+    q = queries if queries.dtype == torch.float32 and queries.is_contiguous() else \
+        queries.contiguous().float()
     dev = q.device
     ids = None
     if item_ids is not None:
-        ids = item_ids.reshape(-1).to(device=dev, dtype=torch.int64).contiguous()
+        ids = item_ids.reshape(-1)
+        if ids.dtype != torch.int64 or ids.device != dev or not ids.is_contiguous():
+            ids = ids.to(device=dev, dtype=torch.int64).contiguous()
         if ids.numel() != packed.X:
             raise ValueError(f"item_ids has {ids.numel()} entries, table has {packed.X}")
     inv = None
     N0 = 0
     if invalid_ids is not None:
-        inv = invalid_ids.to(device=dev, dtype=torch.int64).contiguous()
+        inv = invalid_ids
+        if inv.dtype != torch.int64 or inv.device != dev or not inv.is_contiguous():
+            inv = inv.to(device=dev, dtype=torch.int64).contiguous()
         if inv.dim() != 2 or inv.shape[0] != B:
             raise ValueError("invalid_ids must be (B, N0)")
         N0 = inv.shape[1]
@@ -93,10 +110,10 @@ def mips_topk(queries: torch.Tensor, packed: PackedItems, k: int,
     scores = torch.empty(B, k, dtype=torch.float32, device=dev)
     out_ids = torch.empty(B, k, dtype=torch.int64, device=dev)
     out_idx = torch.empty(B, k, dtype=torch.int64, device=dev) if return_index else None
-    ws_n = topk_workspace_bytes(B, packed.X, D, k, N0)
     if workspace is None:
-        ws = torch.empty(ws_n, dtype=torch.uint8, device=dev)
+        ws_n, ws = packed.workspace(B, k, N0)
     else:
+        ws_n = topk_workspace_bytes(B, packed.X, D, k, N0)
         if workspace.dtype != torch.uint8 or workspace.numel() < ws_n or workspace.device != dev:
             raise ValueError(f"workspace must be a uint8 tensor of >= {ws_n} bytes on {dev}")
         ws = workspace
