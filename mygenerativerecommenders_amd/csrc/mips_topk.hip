@@ -117,18 +117,27 @@ __device__ __forceinline__ f4 mfma16x16x32bf16(u32x4 a, u32x4 b, f4 c) {
 
 // Large catalogs carry a second, bf16 copy of the table for the filter pass (half the
 // bytes, 16x the MFMA rate of the f32 path), in the A-operand order of
-// v_mfma_f32_16x16x32_bf16: for block ib, k-chunk c (KC = ceil(D/32)) and lane l,
-//   packed16[(ib * KC + c) * 64 + l] = bf16(item ib*16 + l%16, dims 32c + 8(l/16) + 0..7)
-// as one 16-byte word (element j in bits 16j .. 16j+15), followed by the largest item
-// L2 norm (fp32 bits, for the filter's error bound).
+// v_mfma_f32_16x16x32_bf16: for block ib, k-chunk c (KC = ceil(D/32)) and lane l, one
+// 16-byte word (element j in bits 16j .. 16j+15) = bf16(item ib*16 + l%16, dims
+// 32c + 8(l/16) + 0..7).  The last chunk stores only its first LG = ceil((D - 32(KC-1))/8)
+// lane groups (dims past D would be zero): a block is BB = 1024 (KC-1) + 256 LG bytes
+// (D = 50: 1,792 B instead of 2,048), word (ib, c, l) at byte ib BB + 1024 c + 16 l.  The
+// filter's lanes of the unstored groups re-read group 0's word (same address: no extra
+// bytes) against zero query dims.  The largest item L2 norm (fp32 bits, for the filter's
+// error bound) follows the copy.
+__host__ __device__ inline int bf16_last_groups(int D, int KC) { return (D - 32 * (KC - 1) + 7) / 8; }
+__host__ __device__ inline int bf16_block_bytes(int D, int KC) {
+  return 1024 * (KC - 1) + 256 * bf16_last_groups(D, KC);
+}
 __global__ void pack_bf16_kernel(const float* items, int64_t X, int D, int KC, u32x4* packed16) {
-  const int64_t total = (X + 15) / 16 * KC * 64;
+  const int words = bf16_block_bytes(D, KC) / 16;  // 16-byte words per block
+  const int64_t total = (X + 15) / 16 * words;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * blockDim.x) {
-    const int l = (int)(e & 63);
-    const int64_t t = e >> 6;  // ib * KC + c
-    const int c = (int)(t % KC);
-    const int64_t i = (t / KC) * 16 + (l & 15);
+    const int64_t ib = e / words;
+    const int u = (int)(e - ib * words);
+    const int c = u >> 6, l = u & 63;
+    const int64_t i = ib * 16 + (l & 15);
     const int d0 = 32 * c + 8 * (l >> 4);
     uint32_t w[4];
 #pragma unroll
@@ -906,6 +915,7 @@ struct FilterArgs {
   const float* q;
   const float* packed;
   const u32x4* packed16;  // bf16 copy (KC > 0 instantiations)
+  int BB, LG;             // its block bytes and stored lane groups of the last chunk
   int64_t X;
   int D, B;
   int64_t n_blocks;
@@ -1023,7 +1033,8 @@ __global__ __launch_bounds__(256) void mips_filter_kernel(FilterArgs a) {
   // .x half, so no in-flight load targets a register the compiler considers dead (it
   // would reuse it as a temporary and wait vmcnt(0) on the prefetch).
   constexpr int NP = BF ? 0 : KS / 2;  // full pairs
-  gptr<u32x4> pk16 = as_global(a.packed16);
+  // bf16 copy: lanes of the last chunk's unstored lane groups read group 0's word
+  const int last_lane = lg < a.LG ? lane : lr;
   struct Frag {
     fv2 p[NP > 0 ? NP : 1];
     float t;
@@ -1033,11 +1044,13 @@ __global__ __launch_bounds__(256) void mips_filter_kernel(FilterArgs a) {
   auto load = [&](Frag& f, int64_t ib) {
     ib = ib < b1 ? ib : b1 - bstride;  // clamped: loads stay unconditional
     if constexpr (BF) {
-      gptr<u32x4> src = pk16 + ib * KC * 64 + lane;
-#pragma unroll
+      gptr<u32x4> src = as_global(reinterpret_cast<const u32x4*>(
+          reinterpret_cast<const char*>(a.packed16) + ib * a.BB));
       // the table streams once: non-temporal loads (10M items: filter 259 -> 233 us;
       // no-hit streaming 227 -> 202 us = 6.3 TB/s)
-      for (int c = 0; c < KC; ++c) f.h[c] = __builtin_nontemporal_load(&src[c * 64]);
+#pragma unroll
+      for (int c = 0; c < KC; ++c)
+        f.h[c] = __builtin_nontemporal_load(&src[c * 64 + (c == KC - 1 ? last_lane : lane)]);
     } else {
       gptr<fv2> src = pk + ib * KS2 * 64 + lane;
 #pragma unroll
@@ -1074,11 +1087,18 @@ __global__ __launch_bounds__(256) void mips_filter_kernel(FilterArgs a) {
       // hits are rare (~1e-4 of scores): one wave-wide OR per block; a block with any
       // hit appends them to this wave's private LDS segment at positions from
       // ballots and a wave-uniform (scalar) counter: no atomics, no waits
-      bool hit = false;
+      // screen: max over the 4 rows, minus the query's threshold, max over the query
+      // groups, one compare (~30 VALU and one ballot per block instead of a compare and a
+      // mask OR per score).  m - t >= 0 holds whenever m >= t (a flushed denormal
+      // difference reads +-0: at worst a false positive, which the exact per-score test
+      // below drops); +inf - +inf (a padded query's threshold) is NaN and never a hit
+      float dmax = -INFINITY;
 #pragma unroll
-      for (int g = 0; g < NQG; ++g)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) hit |= s[g][r] >= thr[g];
+      for (int g = 0; g < NQG; ++g) {
+        const float m = fmaxf(fmaxf(s[g][0], s[g][1]), fmaxf(s[g][2], s[g][3]));
+        dmax = fmaxf(dmax, m - thr[g]);
+      }
+      const bool hit = dmax >= 0.f;
       if (__builtin_expect(__ballot(hit) != 0ull, 0) && ib < b1) {
 #pragma unroll
         for (int g = 0; g < NQG; ++g) {
@@ -1621,7 +1641,7 @@ static PackLayout pack_layout(int64_t X, int D) {
   if (L.bf16) {
     L.KC = ceil_div(D, 32);
     L.off16 = align256(f32);
-    L.off_norm = L.off16 + align256((size_t)nblk * L.KC * 64 * 16);
+    L.off_norm = L.off16 + align256((size_t)nblk * bf16_block_bytes(D, L.KC));
     L.DP = 4 * ceil_div(D, 4);
     L.off_rows = L.off_norm + 256;
     L.total = L.off_rows + align256(sizeof(float) * (size_t)X * L.DP);
@@ -1874,7 +1894,8 @@ extern "C" int mips_topk(const float* queries, const float* packed_items, int64_
     float* tau_e = (float*)(ws + p.off_tau_e);
     const PackLayout L = pack_layout(X, D);
     const char* pbase = (const char*)packed_items;
-    FilterArgs f{queries, packed_items, p.KC ? (const u32x4*)(pbase + L.off16) : nullptr, X, D, B,
+    FilterArgs f{queries, packed_items, p.KC ? (const u32x4*)(pbase + L.off16) : nullptr,
+                 p.KC ? bf16_block_bytes(D, p.KC) : 0, p.KC ? bf16_last_groups(D, p.KC) : 0, X, D, B,
                  p.n_blocks, p.GB, p.G, p.sr, (float*)(ws + p.off_smax),
                  p.RB, tau, cnt, (float*)(ws + p.off_cs), (int*)(ws + p.off_ci), (int*)ws,
                  option(GR_OPT_MIPS_FORCE_FALLBACK) != 0,
