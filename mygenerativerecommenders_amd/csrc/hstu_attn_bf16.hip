@@ -865,9 +865,20 @@ static int bwd_bf16_waves(int d) { return d <= 64 ? 4 : 8; }
 
 }  // namespace gr
 
+// wide heads (128 < d <= 256, dqk == dv): hstu_attn_bf16w.hip
+size_t gr_attn_bwd_bf16w_workspace(int B, int N, int max_len, int H, int num_buckets);
+int gr_attn_bwd_bf16w(const float* q, const float* k, const float* v, int64_t ld_qk, int64_t ld_v,
+                      const float* dout, int64_t ld_dout, const int64_t* offsets, int B, int N,
+                      int max_len, int H, int d, const uint8_t* map_kq, const float* pos_w,
+                      const float* ts_w, int num_buckets, const float* hq, const float* hk,
+                      const float* hv, int64_t ld_h, float* dq, float* dk, float* dvv, int64_t ld_d,
+                      float* dpos_w, float* dts_w, void* workspace, hipStream_t st);
+static bool bwd_bf16_wide(int dqk, int dv) { return dqk == dv && dqk > 128 && dqk <= 256; }
+
 extern "C" size_t hstu_attn_bwd_bf16_workspace_size(int B, int N, int max_len, int H, int dqk,
                                                     int dv, int num_buckets) {
   if (B <= 0 || N <= 0 || H <= 0 || max_len <= 0 || dqk <= 0 || dv <= 0) return 0;
+  if (bwd_bf16_wide(dqk, dv)) return gr_attn_bwd_bf16w_workspace(B, N, max_len, H, num_buckets);
   const int d = dqk > dv ? dqk : dv;
   return gr::bwd_bf16_slab_bytes(B, N, max_len, H, num_buckets, 16 * gr::bwd_bf16_waves(d));
 }
@@ -888,11 +899,18 @@ extern "C" int hstu_attn_bwd_bf16(const float* q, const float* k, const float* v
   GR_REQUIRE((hq == nullptr) == (hk == nullptr) && (hk == nullptr) == (hv == nullptr),
              "hstu_attn_bwd_bf16: hq/hk/hv must be all given or all NULL");
   const int d = dqk > dv ? dqk : dv;
+  // wide heads need the workspace with or without the bias (the dS blocks live there)
+  const bool wide = bwd_bf16_wide(dqk, dv) &&
+                    pair_aligned({q, k, v, dout}, {ld_qk, ld_v, ld_dout, (int64_t)dqk, hq ? ld_h : 0});
   if (bucket_map) {
     GR_REQUIRE(pos_w && ts_w && dpos_w && dts_w && num_buckets > 0 && num_buckets < 256,
                "hstu_attn_bwd_bf16: bucket_map given without pos_w/ts_w/dpos_w/dts_w");
-    const size_t need = bwd_bf16_slab_bytes(B, N, max_len, H, num_buckets, 16 * bwd_bf16_waves(d));
-    GR_REQUIRE(workspace && ws_bytes >= need, "hstu_attn_bwd_bf16: workspace %zu B < %zu B", ws_bytes, need);
+  }
+  if (bucket_map || wide) {
+    const size_t need = wide ? gr_attn_bwd_bf16w_workspace(B, N, max_len, H, num_buckets)
+                             : bwd_bf16_slab_bytes(B, N, max_len, H, num_buckets, 16 * bwd_bf16_waves(d));
+    GR_REQUIRE(B == 0 || max_len == 0 || (workspace && ws_bytes >= need),
+               "hstu_attn_bwd_bf16: workspace %zu B < %zu B", ws_bytes, need);
   }
   hipStream_t st = (hipStream_t)stream;
   if (B == 0 || max_len == 0) {
@@ -904,6 +922,10 @@ extern "C" int hstu_attn_bwd_bf16(const float* q, const float* k, const float* v
   }
   const uint8_t* map_kq =
       bucket_map ? bucket_map + (size_t)B * attn_tiles_per_seq(N) * 4096 : nullptr;
+  if (wide)
+    return gr_attn_bwd_bf16w(q, k, v, ld_qk, ld_v, dout, ld_dout, offsets, B, N, max_len, H, dqk,
+                             map_kq, pos_w, ts_w, num_buckets, hq, hk, hv, ld_h, dq, dk, dvv, ld_d,
+                             dpos_w, dts_w, workspace, st);
   AttnBwdArgsBf16 a{q, k, v, ld_qk, ld_v, dout, ld_dout, offsets, B, N, H, dqk, dv, max_len,
                     bucket_map, map_kq, pos_w, ts_w, bucket_map ? num_buckets : 0, hq, hk, hv,
                     ld_h, dq, dk, dvv, ld_d, bucket_map ? (float*)workspace : nullptr,

@@ -344,9 +344,11 @@ BF16_BWD_TOL = 2e-2
     (3, 130, 2, 8, 8, False),
     (2, 150, 1, 64, 64, True),
     (2, 100, 1, 128, 96, True),
-    (2, 150, 1, 256, 256, True),    # C3 head (dV / dK split passes)
-    (2, 90, 1, 200, 136, True),
+    (2, 150, 1, 256, 256, True),    # C3 head (wide 32x32x16 path, hstu_attn_bf16w.hip)
+    (2, 90, 1, 200, 136, True),     # dqk != dv: split dV / dK passes
     (2, 70, 2, 160, 160, False),
+    (2, 300, 2, 192, 192, True),    # wide path, two heads, ragged 128-key tiles
+    (3, 100, 1, 130, 130, True),    # wide path, 130 of 160 padded dims
     (2, 2059, 1, 256, 256, True),   # C3 length
 ])
 def test_attn_bwd_bf16_vs_oracle(B, N, H, dqk, dv, with_ts):
@@ -375,8 +377,9 @@ def test_attn_bwd_bf16_vs_oracle(B, N, H, dqk, dv, with_ts):
         _close(got, want, rel=BF16_BWD_TOL)
 
 
-def test_attn_bwd_bf16_fused_silu_grad():
-    B, N, H, d = 3, 75, 1, 32
+@pytest.mark.parametrize("d", [32, 256])
+def test_attn_bwd_bf16_fused_silu_grad(d):
+    B, N, H = 3, 75, 1
     lengths, offsets, uvqk, ts, pos_w, ts_w = _case(17, B, N, H, d, d)
     g = torch.Generator().manual_seed(5)
     hpre = torch.randn(uvqk.shape, generator=g)
