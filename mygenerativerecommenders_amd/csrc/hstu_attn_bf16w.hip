@@ -19,15 +19,17 @@
 //     register operand implies.
 //   * query-major pass (dQ = dS K), 4 waves x 32 queries: A = the stored dS block, read
 //     back transposed; B = the K tile, transposed reads.  Nothing is recomputed.
+// Operands reach LDS as bf16 through LDS-DMA (global_load_lds_dwordx4, no registers):
+// a conversion pass first writes bf16 copies of Q, K, V and dO, [row][head][32 D32] with
+// zero padding; LDS tiles are chunk-major, [16-byte column chunk][row][8 bf16], so that
+// the DMA's lane-linear image is the tile and both the A-fragment reads (ds_read_b128,
+// lanes = consecutive rows) and the transposed B reads need no per-lane address math.
 // Relative-bias gradients stay fp32 and deterministic: dpos_w per wave as plain stores of
 // each diagonal bin (a chunk's wrapped diagonals are carried into the next chunk, whose
 // main diagonals are the same bins), dts_w per lane as running (bucket, sum) flushed to
 // per-wave LDS histograms; one slab per wave, reduced in a fixed order.
 #include "attn_common.h"
 
-#ifndef W_ABL
-#define W_ABL 0  // ablation builds only (scripts/attn_micro.py against vlib/ variants)
-#endif
 
 #include "../../include/gr_hstu.h"
 
@@ -71,6 +73,41 @@ __device__ __forceinline__ u32x4_t trB_nat(const __bf16* tile, int rs, int s, in
   const u32x2_t lo = tr16(base), hi = tr16(base + 4 * rs);
   return u32x4_t{lo.x, lo.y, hi.x, hi.y};
 }
+// Chunk-major tiles: element (row r, column c) at byte ((c >> 3) * 32 + r) * 16 + (c & 7) * 2.
+// trB_acc / trB_nat on such a tile (rows = k): k-step s, columns 32 t .. 32 t + 31.
+__device__ __forceinline__ u32x4_t trB_acc_cm(const char* tile, int s, int t, int lane) {
+  const int g = lane >> 4, h = lane >> 5, q = (lane & 15) >> 2, p = lane & 3;
+  const char* base = tile + ((4 * t + 2 * (g & 1) + (p >> 1)) * 32 + 16 * s + 4 * h + q) * 16 + 8 * (p & 1);
+  const u32x2_t lo = tr16(reinterpret_cast<const __bf16*>(base)),
+                hi = tr16(reinterpret_cast<const __bf16*>(base + 8 * 16));
+  return u32x4_t{lo.x, lo.y, hi.x, hi.y};
+}
+__device__ __forceinline__ u32x4_t trB_nat_cm(const char* tile, int s, int t, int lane) {
+  const int g = lane >> 4, h = lane >> 5, q = (lane & 15) >> 2, p = lane & 3;
+  const char* base = tile + ((4 * t + 2 * (g & 1) + (p >> 1)) * 32 + 16 * s + 8 * h + q) * 16 + 8 * (p & 1);
+  const u32x2_t lo = tr16(reinterpret_cast<const __bf16*>(base)),
+                hi = tr16(reinterpret_cast<const __bf16*>(base + 4 * 16));
+  return u32x4_t{lo.x, lo.y, hi.x, hi.y};
+}
+// A fragment (row lane % 32, k-step ks) of a chunk-major tile: 16 bytes
+__device__ __forceinline__ u32x4_t frag_cm(const char* tile, int ks, int lane) {
+  return *reinterpret_cast<const u32x4_t*>(tile + ((2 * ks + (lane >> 5)) * 32 + (lane & 31)) * 16);
+}
+// One 32-row tile of a bf16 copy into chunk-major LDS by LDS-DMA: DMA instruction i moves
+// chunks 2i, 2i + 1 (lane l: row l % 32, chunk 2i + l / 32, LDS byte 1024 i + 16 l); the
+// workgroup's 4 waves take i = w, w + 4, ...; rows >= L read the zero row.
+template <int D32>
+__device__ __forceinline__ void dma_tile(char* tile, const __bf16* rows, int64_t rsb, int r0, int L,
+                                         const __bf16* zrow, int w, int lane) {
+  const int r = r0 + (lane & 31);
+  const __bf16* src = (r < L ? rows + (int64_t)r * rsb : zrow) + 8 * (lane >> 5);
+#pragma unroll
+  for (int i = 0; i < 2 * D32; i += 4)
+    if (i + w < 2 * D32)
+      __builtin_amdgcn_global_load_lds((const void*)(src + 16 * (i + w)),
+                                       (__attribute__((address_space(3))) void*)(tile + 1024 * (i + w)), 16, 0, 0);
+}
+
 // The accumulator's registers 8s .. 8s+7 as a bf16 A / B fragment (k-step s)
 __device__ __forceinline__ u32x4_t acc_frag(const float (&x)[16], int s) {
   return u32x4_t{pack_bf16(x[8 * s], x[8 * s + 1]), pack_bf16(x[8 * s + 2], x[8 * s + 3]),
@@ -100,6 +137,12 @@ struct AttnBwdArgsW {
   int64_t ld_d;
   float* slabs;    // [grid_k][4 waves][2N-1 + nb+1]
   __bf16* ds;      // dS blocks: [bh][tri(qb, kb)][32 keys][32 queries]
+  __bf16* qb;      // bf16 copies [row][head][32 D32] of Q, K, V, dO
+  __bf16* kb;
+  __bf16* vb;
+  __bf16* ob;
+  __bf16* zrow;    // 32 D32 zeros
+  int64_t total_rows;  // B N (upper bound of offsets[B])
   int nbt;         // dS blocks per (sequence, head): NB (NB + 1) / 2, NB = ceil(N / 32)
   float inv_n;
   int n_kt;        // 128-key tiles
@@ -110,54 +153,50 @@ constexpr int WK = 128;  // keys (queries) per workgroup: 4 waves x 32
 constexpr int kDtsCopies = 4;  // dts histogram copies per wave (lane % copies)
 __host__ __device__ constexpr int w_dts_stride(int nb1) { return ((nb1 + 30) / 32) * 32 + 1; }
 
-// fp32 rows -> bf16 LDS tile, 32 rows x DP columns: thread t owns the column pair
-// 2 (t % 128) of rows t / 128 + 2 i (one voffset per thread, the row step in soffset);
-// rows past the sequence read 0 (descriptor range), columns >= ncols read 0 (offset)
-template <int DP>
-struct StageW {
-  static constexpr int PER = 16;
-  float2 v[PER];
-  int voff;
-  __device__ __forceinline__ void init(int64_t ld, int ncols) {
-    const int c = 2 * (threadIdx.x & 127), rr = threadIdx.x >> 7;
-    voff = c < ncols ? (rr * (int)ld + c) * 4 : 0x40000000;
-  }
-  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t r, int64_t ld, int r0) {
-    typedef unsigned int u2_ __attribute__((ext_vector_type(2)));
+// fp32 -> bf16 copies [row][head][32 D32] of Q, K, V, dO (blockIdx.y = tensor), zero
+// padding past d; one thread per 16-byte chunk; block (0, 0) also writes the zero row.
+__global__ __launch_bounds__(256) void attn_bf16w_convert(AttnBwdArgsW a, int nch) {
+  const float* src = blockIdx.y == 0 ? a.q : blockIdx.y == 1 ? a.k : blockIdx.y == 2 ? a.v : a.dout;
+  const int64_t ld = blockIdx.y < 2 ? a.ld_qk : blockIdx.y == 2 ? a.ld_v : a.ld_dout;
+  __bf16* dst = blockIdx.y == 0 ? a.qb : blockIdx.y == 1 ? a.kb : blockIdx.y == 2 ? a.vb : a.ob;
+  if (blockIdx.x == 0 && blockIdx.y == 0 && (int)threadIdx.x < nch)
+    *reinterpret_cast<u32x4_t*>(a.zrow + 8 * threadIdx.x) = u32x4_t{0u, 0u, 0u, 0u};
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int c = (int)(idx % nch);
+  const int64_t rh = idx / nch;
+  const int h = (int)(rh % a.H);
+  const int64_t row = rh / a.H;
+  if (row >= a.offsets[a.B]) return;
+  const float* p = src + row * ld + h * a.d + 8 * c;
+  float x[8];
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const u2_ x = __builtin_amdgcn_raw_buffer_load_b64(r, voff, (r0 + 2 * i) * (int)ld * 4, 0);
-      v[i] = make_float2(__uint_as_float(x.x), __uint_as_float(x.y));
-    }
+  for (int j = 0; j < 8; j += 2) {
+    float2 v = make_float2(0.f, 0.f);
+    if (8 * c + j < a.d) v = *reinterpret_cast<const float2*>(p + j);  // d, ld even
+    x[j] = v.x;
+    x[j + 1] = v.y;
   }
-  __device__ __forceinline__ void store(__bf16* lds, int rs) const {
-    const int c = 2 * (threadIdx.x & 127), rr = threadIdx.x >> 7;
-    if (DP == 256 || c < DP) {
-#pragma unroll
-      for (int i = 0; i < PER; ++i)
-        *reinterpret_cast<uint32_t*>(lds + (rr + 2 * i) * rs + c) = pack_bf16(v[i].x, v[i].y);
-    }
-  }
-};
+  *reinterpret_cast<u32x4_t*>(dst + (row * a.H + h) * (8 * nch) + 8 * c) =
+      u32x4_t{pack_bf16(x[0], x[1]), pack_bf16(x[2], x[3]), pack_bf16(x[4], x[5]), pack_bf16(x[6], x[7])};
+}
 
 // ------------------------------------------------------------------ key-major pass
 // KIND_K = false: dV += P^T dO;  true: dK += dS^T Q, bias gradients, dS blocks.
 template <int D32, bool HB, bool KIND_K>
-__device__ __forceinline__ void kv_body(const AttnBwdArgsW& a, char* smem, int rank) {
+__device__ __forceinline__ void kv_body(const AttnBwdArgsW& a, char* smem, int kt, int bh) {
   constexpr int DP = 32 * D32;   // padded head dim
   constexpr int KS = DP / 16;    // k-steps of the S / dP products
-  constexpr int RS = DP + 8;     // LDS row stride (bf16): 16-byte aligned rows
+  constexpr int TB = 64 * DP;    // bytes of one chunk-major 32-row tile
   constexpr bool BIAS = HB && KIND_K;
-  __bf16* tiles = reinterpret_cast<__bf16*>(smem);  // [2 buffers][Q, dO][32][RS]
-  float* tsw = reinterpret_cast<float*>(tiles + 4 * 32 * RS);
+  char* tiles = smem;  // [2 buffers][Q, dO][TB]
+  float* tsw = reinterpret_cast<float*>(tiles + 4 * TB);
   const int npos = 2 * a.N - 1;
   float* posw = tsw + (a.nb + 1);
   const int tss = w_dts_stride(a.nb + 1);
   float* hts = posw + npos;  // [4 waves][kDtsCopies][tss]
 
   const int BH = a.B * a.H;
-  const int kt = rank / BH;  // heaviest (first) key tiles first
-  const int bh = rank % BH;
+  const int rank = kt * BH + bh;  // slab index
   const int b = bh / a.H, h = bh % a.H;
   const int64_t s0 = a.offsets[b];
   const int L = (int)(a.offsets[b + 1] - s0);
@@ -180,30 +219,19 @@ __device__ __forceinline__ void kv_body(const AttnBwdArgsW& a, char* smem, int r
   const int k0w = k0 + 32 * w;   // this wave's first key
   const int kj = k0w + lr;       // this lane's key (column of S / dP)
   const bool k_ok = kj < L;
+  // bf16 copies of this (sequence, head): row r at rows + r * rsb
+  const int64_t rsb = (int64_t)a.H * DP;
+  const int64_t hoff = s0 * rsb + (int64_t)h * DP;
   // K^T / V^T fragments of the wave's keys: element j of k-step ks = dim 16 ks + 8 lh + j
-  // (keys >= L read 0 through the descriptor range; dims >= d are masked)
   u32x4_t kf[KS], vf[KS];
   {
-    auto frag = [&](__amdgpu_buffer_rsrc_t r, int64_t ld, int ks) {
-      const int c0 = 16 * ks + 8 * lh;
-      const int off = (kj * (int)ld + c0) * 4;
-      const u32x4_t lo = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
-      const u32x4_t hi = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(r, off + 16, 0, 0));
-      float x[8];
+    const __bf16* krow = k_ok ? a.kb + hoff + (int64_t)kj * rsb : a.zrow;
+    const __bf16* vrow = k_ok ? a.vb + hoff + (int64_t)kj * rsb : a.zrow;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        x[j] = c0 + j < a.d ? __uint_as_float(lo[j]) : 0.f;
-        x[4 + j] = c0 + 4 + j < a.d ? __uint_as_float(hi[j]) : 0.f;
-      }
-      return u32x4_t{pack_bf16(x[0], x[1]), pack_bf16(x[2], x[3]), pack_bf16(x[4], x[5]), pack_bf16(x[6], x[7])};
-    };
-    const __amdgpu_buffer_rsrc_t rk = seq_rsrc(a.k, a.ld_qk, s0, h * a.d, L, a.d);
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) kf[ks] = frag(rk, a.ld_qk, ks);
+    for (int ks = 0; ks < KS; ++ks) kf[ks] = *reinterpret_cast<const u32x4_t*>(krow + 16 * ks + 8 * lh);
     if (KIND_K) {
-      const __amdgpu_buffer_rsrc_t rv = seq_rsrc(a.v, a.ld_v, s0, h * a.d, L, a.d);
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) vf[ks] = frag(rv, a.ld_v, ks);
+      for (int ks = 0; ks < KS; ++ks) vf[ks] = *reinterpret_cast<const u32x4_t*>(vrow + 16 * ks + 8 * lh);
     }
   }
   // output accumulators: tile t = columns 32 t .. 32 t + 31, rows = the wave's keys
@@ -211,8 +239,6 @@ __device__ __forceinline__ void kv_body(const AttnBwdArgsW& a, char* smem, int r
 #pragma unroll
   for (int t = 0; t < D32; ++t) acc[t] = f16_zero();
 
-  const __amdgpu_buffer_rsrc_t rq = seq_rsrc(a.q, a.ld_qk, s0, h * a.d, L, a.d);
-  const __amdgpu_buffer_rsrc_t rdo = seq_rsrc(a.dout, a.ld_dout, s0, h * a.d, L, a.d);
   const __amdgpu_buffer_rsrc_t rmap = map_rsrc(a.map_kq, b, attn_tiles_per_seq(a.N));
   // dts: running (bucket, sum) of this lane, flushed into per-wave LDS histogram copies
   // when the bucket changes
@@ -223,9 +249,6 @@ __device__ __forceinline__ void kv_body(const AttnBwdArgsW& a, char* smem, int r
   // wrapped diagonals of the previous chunk (carry), see the file header
   float carry = 0.f;
 
-  StageW<DP> stq, std_;
-  stq.init(a.ld_qk, a.d);
-  std_.init(a.ld_dout, a.d);
   const int n_chunks = (L - k0 + 31) / 32;  // the workgroup's chunks: queries k0, k0 + 32, ...
   const bool w_on = k0w < L;
   const int map_w = (kj & 63) * 16;
@@ -240,58 +263,72 @@ __device__ __forceinline__ void kv_body(const AttnBwdArgsW& a, char* smem, int r
   };
   uint32_t mw_next[4] = {0u, 0u, 0u, 0u};
   if (HB && w_on) map_words(k0w, mw_next);
-  stq.load(rq, a.ld_qk, k0);
-  std_.load(rdo, a.ld_dout, k0);
-  stq.store(tiles, RS);
-  std_.store(tiles + 32 * RS, RS);
+  // the chunk's Q and dO rows by LDS-DMA, one chunk ahead (drained by the chunk's barrier)
+  auto dma = [&](int buf, int r0) {
+    dma_tile<D32>(tiles + buf * 2 * TB, a.qb + hoff, rsb, r0, L, a.zrow, w, lane);
+    dma_tile<D32>(tiles + buf * 2 * TB + TB, a.ob + hoff, rsb, r0, L, a.zrow, w, lane);
+  };
+  dma(0, k0);
   __syncthreads();
   for (int ci = 0; ci < n_chunks; ++ci) {
     const int qc0 = k0 + 32 * ci;
-    const __bf16* Qs = tiles + (ci & 1) * 64 * RS;
-    const __bf16* Ds = Qs + 32 * RS;
-    __bf16* Qn = tiles + ((ci + 1) & 1) * 64 * RS;
+    const char* Qs = tiles + (ci & 1) * 2 * TB;
+    const char* Ds = Qs + TB;
     const bool more = ci + 1 < n_chunks;
-    // the next chunk's rows: loaded now, written to the other buffer after this chunk
-    if (W_ABL != 2 && more) {
-      stq.load(rq, a.ld_qk, qc0 + 32);
-      std_.load(rdo, a.ld_dout, qc0 + 32);
-    }
+    if (more) dma((ci + 1) & 1, qc0 + 32);
     const bool act = w_on && qc0 >= k0w;  // wave-uniform: the chunk reaches the wave's keys
     if (act) {
       uint32_t mw[4];
 #pragma unroll
       for (int m = 0; m < 4; ++m) mw[m] = mw_next[m];
       if (HB && more) map_words(qc0 + 32, mw_next);
-      // two independent chains per kind (S, dP or the even / odd k-steps of S)
+      // relative bias of the chunk's elements, looked up before the products so the LDS
+      // latency hides under them: element rr = query qc0 + (rr & 3) + 8 (rr >> 2) + 4 lh
+      float bias[16];
+      if (HB) {
+        const float* pw = posw + (a.N - 1 + kj - qc0 - 4 * lh);  // minus the row (rr & 3) + 8 (rr >> 2)
+#pragma unroll
+        for (int rr = 0; rr < 16; ++rr) {
+          const int bk = (mw[rr >> 2] >> (8 * (rr & 3))) & 0xFF;
+          bias[rr] = pw[-((rr & 3) + 8 * (rr >> 2))] + tsw[bk];
+        }
+      }
+      // S (and dP) with the A fragments read PF k-steps ahead; two independent chains per
+      // kind (S, dP or the even / odd k-steps of S)
+      constexpr int PF = 4;
+      u32x4_t qa[PF], da[PF];
+#pragma unroll
+      for (int i = 0; i < PF; ++i) {
+        qa[i] = frag_cm(Qs, i, lane);
+        if (KIND_K) da[i] = frag_cm(Ds, i, lane);
+      }
       f32x16 S = f16_zero(), dP = f16_zero();
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        const u32x4_t qa = *reinterpret_cast<const u32x4_t*>(Qs + lr * RS + 16 * ks + 8 * lh);
+        const u32x4_t a0 = qa[ks % PF];
+        u32x4_t a1 = da[ks % PF];
+        if (ks + PF < KS) {
+          qa[ks % PF] = frag_cm(Qs, ks + PF, lane);
+          if (KIND_K) da[ks % PF] = frag_cm(Ds, ks + PF, lane);
+        }
         if (KIND_K) {
-          S = mfma32(qa, kf[ks], S);
-          dP = mfma32(*reinterpret_cast<const u32x4_t*>(Ds + lr * RS + 16 * ks + 8 * lh), vf[ks], dP);
+          S = mfma32(a0, kf[ks], S);
+          dP = mfma32(a1, vf[ks], dP);
         } else if (ks & 1) {
-          dP = mfma32(qa, kf[ks], dP);
+          dP = mfma32(a0, kf[ks], dP);
         } else {
-          S = mfma32(qa, kf[ks], S);
+          S = mfma32(a0, kf[ks], S);
         }
       }
       if (!KIND_K) S += dP;
-      // element rr: query qc0 + (rr & 3) + 8 (rr >> 2) + 4 lh, key kj
       float x16[16];
 #pragma unroll
       for (int rr = 0; rr < 16; ++rr) {
         const int qi = qc0 + (rr & 3) + 8 * (rr >> 2) + 4 * lh;
         const bool ok = k_ok && qi < L && kj <= qi;
         float x = S[rr];
-        int bk = 0;
-        if (HB) {
-          bk = (mw[rr >> 2] >> (8 * (rr & 3))) & 0xFF;
-          int pi = a.N - 1 + kj - qi;
-          pi = pi < 0 ? 0 : (pi > npos - 1 ? npos - 1 : pi);
-          x = x + (posw[pi] + tsw[bk]);
-        }
-        const float sg = W_ABL == 1 ? x : sigmoidf_(x);
+        if (HB) x = x + bias[rr];
+        const float sg = sigmoidf_(x);
         const uint32_t msk = ok ? 0xffffffffu : 0u;
         if (!KIND_K) {
           x16[rr] = __uint_as_float(__float_as_uint(x * sg * a.inv_n) & msk);
@@ -303,11 +340,19 @@ __device__ __forceinline__ void kv_body(const AttnBwdArgsW& a, char* smem, int r
       }
       const u32x4_t f0 = acc_frag(x16, 0), f1 = acc_frag(x16, 1);
       // acc += X^T B, B = dO (dV) or Q (dK) rows of the chunk, transposed reads
-      const __bf16* Bt = KIND_K ? Qs : Ds;
+      const char* Bt = KIND_K ? Qs : Ds;
+      // 2 D32 products (k-step s = u / D32, tile t = u % D32), B fragments read PB ahead
+      constexpr int NU = 2 * D32, PB = 4;
+      u32x4_t bq[PB];
 #pragma unroll
-      for (int t = 0; t < (W_ABL == 3 ? 1 : D32); ++t) acc[t] = mfma32(f0, trB_acc(Bt, RS, 0, 32 * t, lane), acc[t]);
+      for (int u = 0; u < PB; ++u) bq[u] = trB_acc_cm(Bt, u / D32, u % D32, lane);
 #pragma unroll
-      for (int t = 0; t < (W_ABL == 3 ? 1 : D32); ++t) acc[t] = mfma32(f1, trB_acc(Bt, RS, 1, 32 * t, lane), acc[t]);
+      for (int u = 0; u < NU; ++u) {
+        const u32x4_t b0 = bq[u % PB];
+        if (u + PB < NU) bq[u % PB] = trB_acc_cm(Bt, (u + PB) / D32, (u + PB) % D32, lane);
+        const int t = u % D32;
+        acc[t] = mfma32(u < D32 ? f0 : f1, b0, acc[t]);
+      }
       if (KIND_K) {
         // dS block for the query-major pass: [key][query] image, registers 4g .. 4g+3 =
         // queries 8g + 4lh + 0..3 (8-byte stores)
@@ -320,7 +365,7 @@ __device__ __forceinline__ void kv_body(const AttnBwdArgsW& a, char* smem, int r
           *reinterpret_cast<u32x2_t*>(blk + lr * 32 + 8 * g + 4 * lh) = v2;
         }
       }
-      if (BIAS && W_ABL != 4 && W_ABL != 6) {
+      if (BIAS) {
         // dts run (a lane's queries ascend with rr), after the math so that the branches
         // do not split its schedule; the accumulator MFMAs above run meanwhile
 #pragma unroll
@@ -336,7 +381,7 @@ __device__ __forceinline__ void kv_body(const AttnBwdArgsW& a, char* smem, int r
           run_s += x16[rr];  // 0 where !ok
         }
       }
-      if (BIAS && W_ABL != 5 && W_ABL != 6) {
+      if (BIAS) {
         // dpos: rotate register rr (row R = (rr & 3) + 8 (rr >> 2) + 4 lh) left by R in
         // the 32-lane half: lane c then holds diagonal c (main) or c - 32 (wrapped)
         float dmain = 0.f, dwrap = 0.f;
@@ -357,13 +402,7 @@ __device__ __forceinline__ void kv_body(const AttnBwdArgsW& a, char* smem, int r
         carry = dwrap;
       }
     }
-    if (more) {
-      if (W_ABL != 2) {
-        stq.store(Qn, RS);
-        std_.store(Qn + 32 * RS, RS);
-      }
-      __syncthreads();
-    }
+    if (more) __syncthreads();
   }
   // ---- epilogue: acc[t][rr] = (dV or dK)[key k0w + (rr & 3) + 8 (rr >> 2) + 4 lh][32 t + lr]
   float* outp = KIND_K ? a.dk : a.dvv;
@@ -406,29 +445,44 @@ __device__ __forceinline__ void kv_body(const AttnBwdArgsW& a, char* smem, int r
   }
 }
 
-// even workgroups: dK (+ bias, dS), odd: dV; pairs in heaviest-first order
+// workgroup i -> (sequence-head bh, slot j of per_seq): XCD x = i % 8 takes the
+// sequence-heads x, x + 8, ... in turn (the grid is padded to a multiple of 8 of them)
+__device__ __forceinline__ void xcd_slot(const AttnBwdArgsW& a, int per_seq, int& bh, int& j) {
+  const int x = blockIdx.x & 7, sl = blockIdx.x >> 3;
+  bh = (sl / per_seq) * 8 + x;
+  j = sl % per_seq;
+}
+
 template <int D32, bool HB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void attn_bwd_bf16w_kv_kernel(AttnBwdArgsW a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  if ((blockIdx.x & 1) == 0) kv_body<D32, HB, true>(a, smem, blockIdx.x >> 1);
-  else kv_body<D32, HB, false>(a, smem, blockIdx.x >> 1);
+  // XCD-aware order (workgroup i runs on XCD i % 8): every workgroup of one (sequence,
+  // head) lands on one XCD, so its Q / dO rows, re-read by each key tile and by both
+  // kinds, come from that XCD's L2; within it dK / dV pairs, heaviest key tiles first
+  int bh, j;
+  xcd_slot(a, 2 * a.n_kt, bh, j);
+  if (bh >= a.B * a.H) return;
+  if ((j & 1) == 0) kv_body<D32, HB, true>(a, smem, j >> 1, bh);
+  else kv_body<D32, HB, false>(a, smem, j >> 1, bh);
 }
 
 // ------------------------------------------------------------------ query-major pass
 // dQ[q][:] = sum over key blocks of dS block (A: transposed reads of the [key][query] image,
-// natural k order) times the K tile (B: transposed reads of the row-major bf16 tile).
+// natural k order) times the K tile (B: transposed reads of the chunk-major tile).  K tiles
+// and the waves' dS blocks arrive by LDS-DMA one block ahead.
 template <int D32>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2)))
 void attn_bwd_bf16w_dq_kernel(AttnBwdArgsW a) {
   constexpr int DP = 32 * D32;
-  constexpr int RS = DP + 8;
+  constexpr int TB = 64 * DP;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  __bf16* kt_l = reinterpret_cast<__bf16*>(smem);  // [2][32][RS]
-  __bf16* dsl = kt_l + 2 * 32 * RS;                // [4 waves][2][32 x 32]
-  const int BH = a.B * a.H;
-  const int qt = a.n_qt - 1 - (int)blockIdx.x / BH;  // heaviest tiles first
-  const int bh = blockIdx.x % BH;
+  char* kt_l = smem;             // [2][TB]
+  char* dsl = smem + 2 * TB;     // [4 waves][2][2048 B]
+  int bh, j;
+  xcd_slot(a, a.n_qt, bh, j);  // one (sequence, head) per XCD at a time: K rows from L2
+  if (bh >= a.B * a.H) return;
+  const int qt = a.n_qt - 1 - j;  // heaviest tiles first
   const int b = bh / a.H, h = bh % a.H;
   const int64_t s0 = a.offsets[b];
   const int L = (int)(a.offsets[b + 1] - s0);
@@ -441,51 +495,45 @@ void attn_bwd_bf16w_dq_kernel(AttnBwdArgsW a) {
   f32x16 acc[D32];
 #pragma unroll
   for (int t = 0; t < D32; ++t) acc[t] = f16_zero();
-  const __amdgpu_buffer_rsrc_t rk = seq_rsrc(a.k, a.ld_qk, s0, h * a.d, L, a.d);
-  StageW<DP> stk;
-  stk.init(a.ld_qk, a.d);
+  const int64_t rsb = (int64_t)a.H * DP;
+  const __bf16* krows = a.kb + s0 * rsb + (int64_t)h * DP;
   const int n_kb = (min(q0 + WK, L) + 31) / 32;  // key blocks the workgroup needs
-  __bf16* mydl = dsl + w * 2 * 1024;
+  char* mydl = dsl + w * 2 * 2048;
   const bool w_on = q0w < L;
-  auto load_ds = [&](int kb, u32x4_t (&v)[2]) {
-    // the wave's 2 KB block (qb, kb): 64 lanes x 2 x 16 B
-    const __bf16* src = a.ds + ((int64_t)bh * a.nbt + qb * (qb + 1) / 2 + kb) * 1024;
+  const __bf16* dsrow = a.ds + ((int64_t)bh * a.nbt + qb * (qb + 1) / 2) * 1024;
+  auto dma = [&](int kb, int buf) {
+    dma_tile<D32>(kt_l + buf * TB, krows, rsb, 32 * kb, L, a.zrow, w, lane);
+    // the wave's 2 KB dS block (qb, kb): two 1 KB pieces, lane-linear
+    const bool ok = w_on && kb <= qb;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-      v[i] = (w_on && kb <= qb) ? *reinterpret_cast<const u32x4_t*>(src + 8 * (lane + 64 * i))
-                                : u32x4_t{0u, 0u, 0u, 0u};
+    for (int i = 0; i < 2; ++i) {
+      const __bf16* src = ok ? dsrow + kb * 1024 + 512 * i + 8 * lane : a.zrow;
+      __builtin_amdgcn_global_load_lds((const void*)src,
+                                       (__attribute__((address_space(3))) void*)(mydl + buf * 2048 + 1024 * i), 16, 0, 0);
+    }
   };
-  u32x4_t dsv[2];
-  stk.load(rk, a.ld_qk, 0);
-  load_ds(0, dsv);
-  stk.store(kt_l, RS);
-#pragma unroll
-  for (int i = 0; i < 2; ++i) *reinterpret_cast<u32x4_t*>(mydl + 8 * (lane + 64 * i)) = dsv[i];
+  dma(0, 0);
   __syncthreads();
   for (int kb = 0; kb < n_kb; ++kb) {
-    const __bf16* Kl = kt_l + (kb & 1) * 32 * RS;
-    const __bf16* Dl = mydl + (kb & 1) * 1024;
+    const char* Kl = kt_l + (kb & 1) * TB;
+    const __bf16* Dl = reinterpret_cast<const __bf16*>(mydl + (kb & 1) * 2048);
     const bool more = kb + 1 < n_kb;
-    if (more) {
-      stk.load(rk, a.ld_qk, 32 * (kb + 1));
-      load_ds(kb + 1, dsv);
-    }
+    if (more) dma(kb + 1, (kb + 1) & 1);
     if (w_on && kb <= qb) {  // wave-uniform causal skip
       // A: dS[q = lane % 32][keys 16 s + 8 lh + 0..7] from the [key][query] image
       const u32x4_t a0 = trB_nat(Dl, 32, 0, 0, lane), a1 = trB_nat(Dl, 32, 1, 0, lane);
+      constexpr int NU = 2 * D32, PB = 4;
+      u32x4_t bq[PB];
 #pragma unroll
-      for (int t = 0; t < D32; ++t) {
-        acc[t] = mfma32(a0, trB_nat(Kl, RS, 0, 32 * t, lane), acc[t]);
-        acc[t] = mfma32(a1, trB_nat(Kl, RS, 1, 32 * t, lane), acc[t]);
+      for (int u = 0; u < PB; ++u) bq[u] = trB_nat_cm(Kl, u / D32, u % D32, lane);
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        const u32x4_t b0 = bq[u % PB];
+        if (u + PB < NU) bq[u % PB] = trB_nat_cm(Kl, (u + PB) / D32, (u + PB) % D32, lane);
+        acc[u % D32] = mfma32(u < D32 ? a0 : a1, b0, acc[u % D32]);
       }
     }
-    if (more) {
-      stk.store(kt_l + ((kb + 1) & 1) * 32 * RS, RS);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-        *reinterpret_cast<u32x4_t*>(mydl + ((kb + 1) & 1) * 1024 + 8 * (lane + 64 * i)) = dsv[i];
-      __syncthreads();
-    }
+    if (more) __syncthreads();
   }
   if (!w_on) return;
   const int lh = lane >> 5;
@@ -536,21 +584,30 @@ static size_t bf16w_ds_bytes(int B, int N, int H) {
   const size_t nb32 = (size_t)ceil_div(N, 32);
   return 2048 * (nb32 * (nb32 + 1) / 2) * (size_t)B * H;
 }
+static size_t al256(size_t v) { return (v + 255) & ~(size_t)255; }
+// one bf16 copy [B N rows][H][DPA], DPA = d rounded up to 32
+static size_t bf16w_copy_bytes(int B, int N, int H, int d) {
+  return al256((size_t)B * N * H * ceil_div(d, 32) * 32 * 2);
+}
 
 template <int D32>
 static int launch_bwd_bf16w(AttnBwdArgsW a, float* dpos_w, float* dts_w, hipStream_t st) {
-  constexpr int DP = 32 * D32, RS = DP + 8;
+  constexpr int DP = 32 * D32, TB = 64 * DP;
   const size_t npos = 2 * a.N - 1;
   const int tss = w_dts_stride(a.nb + 1);
-  const size_t lds_kv = 2 * 4 * 32 * RS + sizeof(float) * ((a.nb + 1) + npos + 4 * kDtsCopies * tss);
-  const size_t lds_q = 2 * (2 * 32 * RS + 4 * 2 * 1024);
+  const size_t lds_kv = 4 * TB + sizeof(float) * ((a.nb + 1) + npos + 4 * kDtsCopies * tss);
+  const size_t lds_q = 2 * TB + 4 * 2 * 2048;
+  const int nch = 4 * D32;
+  const int64_t conv_threads = a.total_rows * a.H * nch;
+  GR_TIMED("attn_bwd_convert", st, hipLaunchKernelGGL(attn_bf16w_convert, dim3((unsigned)((conv_threads + 255) / 256), 4), dim3(256), 0, st, a, nch));
+  GR_LAUNCH_CHECK("hstu_attn_bwd_bf16(wide convert)");
   GR_REQUIRE(lds_kv <= 160 * 1024, "hstu_attn_bwd_bf16: LDS %zu B exceeds 160 KiB (N=%d)", lds_kv, a.N);
   const int grid = a.n_kt * a.B * a.H;
   auto kkv = a.map_kq ? attn_bwd_bf16w_kv_kernel<D32, true> : attn_bwd_bf16w_kv_kernel<D32, false>;
-  GR_TIMED("attn_bwd_dkv", st, hipLaunchKernelGGL(kkv, dim3(2 * grid), dim3(256), lds_kv, st, a));
+  const int bh8 = ceil_div(a.B * a.H, 8) * 8;  // XCD-aware order: see xcd_slot
+  GR_TIMED("attn_bwd_dkv", st, hipLaunchKernelGGL(kkv, dim3(2 * a.n_kt * bh8), dim3(256), lds_kv, st, a));
   GR_LAUNCH_CHECK("hstu_attn_bwd_bf16(wide dkv)");
-  const int grid_q = a.n_qt * a.B * a.H;
-  GR_TIMED("attn_bwd_dq", st, hipLaunchKernelGGL(attn_bwd_bf16w_dq_kernel<D32>, dim3(grid_q), dim3(256), lds_q, st, a));
+  GR_TIMED("attn_bwd_dq", st, hipLaunchKernelGGL(attn_bwd_bf16w_dq_kernel<D32>, dim3(a.n_qt * bh8), dim3(256), lds_q, st, a));
   GR_LAUNCH_CHECK("hstu_attn_bwd_bf16(wide dq)");
   if (a.map_kq) {
     const int nbins = (int)npos + a.nb + 1;
@@ -567,9 +624,10 @@ static int launch_bwd_bf16w(AttnBwdArgsW a, float* dpos_w, float* dts_w, hipStre
 }  // namespace gr
 
 // Wide-head entry (called by hstu_attn_bwd_bf16 for 128 < d <= 256, dqk == dv).
-size_t gr_attn_bwd_bf16w_workspace(int B, int N, int max_len, int H, int num_buckets) {
-  return ((gr::bf16w_slab_bytes(B, N, max_len, H, num_buckets) + 255) & ~(size_t)255) +
-         gr::bf16w_ds_bytes(B, N, H);
+size_t gr_attn_bwd_bf16w_workspace(int B, int N, int max_len, int H, int d, int num_buckets) {
+  using namespace gr;
+  return al256(bf16w_slab_bytes(B, N, max_len, H, num_buckets)) + al256(bf16w_ds_bytes(B, N, H)) +
+         4 * bf16w_copy_bytes(B, N, H, d) + 256;
 }
 
 int gr_attn_bwd_bf16w(const float* q, const float* k, const float* v, int64_t ld_qk, int64_t ld_v,
@@ -579,7 +637,9 @@ int gr_attn_bwd_bf16w(const float* q, const float* k, const float* v, int64_t ld
                       const float* hv, int64_t ld_h, float* dq, float* dk, float* dvv, int64_t ld_d,
                       float* dpos_w, float* dts_w, void* workspace, hipStream_t st) {
   using namespace gr;
-  const size_t slab_b = (bf16w_slab_bytes(B, N, max_len, H, num_buckets) + 255) & ~(size_t)255;
+  const size_t slab_b = al256(bf16w_slab_bytes(B, N, max_len, H, num_buckets));
+  const size_t ds_b = al256(bf16w_ds_bytes(B, N, H));
+  const size_t cp_b = bf16w_copy_bytes(B, N, H, d);
   AttnBwdArgsW a{};
   a.q = q; a.k = k; a.v = v; a.ld_qk = ld_qk; a.ld_v = ld_v; a.dout = dout; a.ld_dout = ld_dout;
   a.offsets = offsets; a.B = B; a.N = N; a.H = H; a.d = d;
@@ -588,6 +648,13 @@ int gr_attn_bwd_bf16w(const float* q, const float* k, const float* v, int64_t ld
   a.dq = dq; a.dk = dk; a.dvv = dvv; a.ld_d = ld_d;
   a.slabs = (float*)workspace;
   a.ds = (__bf16*)((char*)workspace + slab_b);
+  char* cp = (char*)workspace + slab_b + ds_b;
+  a.qb = (__bf16*)cp;
+  a.kb = (__bf16*)(cp + cp_b);
+  a.vb = (__bf16*)(cp + 2 * cp_b);
+  a.ob = (__bf16*)(cp + 3 * cp_b);
+  a.zrow = (__bf16*)(cp + 4 * cp_b);
+  a.total_rows = (int64_t)B * N;
   const int nb32 = ceil_div(N, 32);
   a.nbt = nb32 * (nb32 + 1) / 2;
   a.inv_n = 1.0f / (float)N;

@@ -114,7 +114,7 @@ def main():
             bwd()
     torch.cuda.synchronize()
     _lib.timing_enable(False)
-    kt = _lib.kernel_times(("attn_fwd", "attn_bwd", "attn_bwd_dkv", "attn_bwd_dq", "attn_bias_reduce"))
+    kt = _lib.kernel_times(("attn_fwd", "attn_bwd", "attn_bwd_dkv", "attn_bwd_dq", "attn_bias_reduce", "attn_bwd_convert"))
     fl = flops(B, L, d, H)
     res = {}
     for name, (tot, n) in kt.items():
