@@ -284,15 +284,17 @@ __device__ __forceinline__ void kv_body(const AttnBwdArgsW& a, char* smem, int k
       if (HB && more) map_words(qc0 + 32, mw_next);
       // relative bias of the chunk's elements, looked up before the products so the LDS
       // latency hides under them: element rr = query qc0 + (rr & 3) + 8 (rr >> 2) + 4 lh
-      float bias[16];
+      float bias_p[16], bias_t[16];
       if (HB) {
         const float* pw = posw + (a.N - 1 + kj - qc0 - 4 * lh);  // minus the row (rr & 3) + 8 (rr >> 2)
 #pragma unroll
         for (int rr = 0; rr < 16; ++rr) {
           const int bk = (mw[rr >> 2] >> (8 * (rr & 3))) & 0xFF;
-          bias[rr] = pw[-((rr & 3) + 8 * (rr >> 2))] + tsw[bk];
+          bias_p[rr] = pw[-((rr & 3) + 8 * (rr >> 2))];
+          bias_t[rr] = tsw[bk];
         }
       }
+      __builtin_amdgcn_sched_barrier(0);
       // S (and dP) with the A fragments read PF k-steps ahead; two independent chains per
       // kind (S, dP or the even / odd k-steps of S)
       constexpr int PF = 4;
@@ -320,6 +322,16 @@ __device__ __forceinline__ void kv_body(const AttnBwdArgsW& a, char* smem, int k
           S = mfma32(a0, kf[ks], S);
         }
       }
+      // schedule: the PF reads first, then one MFMA (S, dP) per read group, so PF groups
+      // of A-fragment reads stay in flight under the products
+      constexpr int GR = KIND_K ? 2 : 1;
+#pragma unroll
+      for (int i = 0; i < PF; ++i) __builtin_amdgcn_sched_group_barrier(0x100, GR, 0);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        __builtin_amdgcn_sched_group_barrier(0x008, GR, 0);
+        if (ks + PF < KS) __builtin_amdgcn_sched_group_barrier(0x100, GR, 0);
+      }
       if (!KIND_K) S += dP;
       float x16[16];
 #pragma unroll
@@ -327,7 +339,11 @@ __device__ __forceinline__ void kv_body(const AttnBwdArgsW& a, char* smem, int k
         const int qi = qc0 + (rr & 3) + 8 * (rr >> 2) + 4 * lh;
         const bool ok = k_ok && qi < L && kj <= qi;
         float x = S[rr];
-        if (HB) x = x + bias[rr];
+        if (HB) {
+          float bp = bias_p[rr], bt = bias_t[rr];
+          asm volatile("" : "+v"(bp), "+v"(bt));  // keep the add here, after the products
+          x = x + (bp + bt);
+        }
         const float sg = sigmoidf_(x);
         const uint32_t msk = ok ? 0xffffffffu : 0u;
         if (!KIND_K) {
@@ -339,6 +355,7 @@ __device__ __forceinline__ void kv_body(const AttnBwdArgsW& a, char* smem, int k
         }
       }
       const u32x4_t f0 = acc_frag(x16, 0), f1 = acc_frag(x16, 1);
+      __builtin_amdgcn_sched_barrier(0);
       // acc += X^T B, B = dO (dV) or Q (dK) rows of the chunk, transposed reads
       const char* Bt = KIND_K ? Qs : Ds;
       // 2 D32 products (k-step s = u / D32, tile t = u % D32), B fragments read PB ahead
@@ -352,6 +369,13 @@ __device__ __forceinline__ void kv_body(const AttnBwdArgsW& a, char* smem, int k
         if (u + PB < NU) bq[u % PB] = trB_acc_cm(Bt, (u + PB) / D32, (u + PB) % D32, lane);
         const int t = u % D32;
         acc[t] = mfma32(u < D32 ? f0 : f1, b0, acc[t]);
+      }
+#pragma unroll
+      for (int u = 0; u < PB; ++u) __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+        if (u + PB < NU) __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
       }
       if (KIND_K) {
         // dS block for the query-major pass: [key][query] image, registers 4g .. 4g+3 =
@@ -531,6 +555,13 @@ void attn_bwd_bf16w_dq_kernel(AttnBwdArgsW a) {
         const u32x4_t b0 = bq[u % PB];
         if (u + PB < NU) bq[u % PB] = trB_nat_cm(Kl, (u + PB) / D32, (u + PB) % D32, lane);
         acc[u % D32] = mfma32(u < D32 ? a0 : a1, b0, acc[u % D32]);
+      }
+#pragma unroll
+      for (int u = 0; u < PB + 2; ++u) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if (u + PB < NU) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
       }
     }
     if (more) __syncthreads();
