@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GR_HSTU_ABI_VERSION 10
+#define GR_HSTU_ABI_VERSION 11
 
 #ifndef GR_API
 #define GR_API __attribute__((visibility("default")))
@@ -222,12 +222,19 @@ GR_API int hstu_attn_fwd(const float* q, const float* k, const float* v, int64_t
 /* hstu_attn_fwd_bf16: hstu_attn_fwd with bf16 MFMA operands and fp32 accumulation (the
  * opt-in bf16 compute mode): Q, K, V are rounded to bf16 as they are staged and
  * P = silu(S + bias) / N is rounded to bf16 before P.V; S, the bias, silu and the
- * output are fp32.  Same arguments and layout as hstu_attn_fwd. */
+ * output are fp32.  Same arguments and layout as hstu_attn_fwd, plus `copies`:
+ * NULL, or (wide heads only: dqk == dv in (128, 256], even strides) the bf16 copies of
+ * Q, K, V made by hstu_attn_bf16_copies, which the wide kernels stage into LDS by DMA.
+ * The same copies can be passed to hstu_attn_bwd_bf16 (saved with the activations). */
+GR_API size_t hstu_attn_bf16_copies_bytes(int B, int N, int H, int dqk, int dv);
+GR_API int hstu_attn_bf16_copies(const float* q, const float* k, const float* v, int64_t ld_qk,
+                                 int64_t ld_v, const int64_t* offsets, int B, int N, int H,
+                                 int dqk, int dv, void* copies, void* stream);
 GR_API int hstu_attn_fwd_bf16(const float* q, const float* k, const float* v, int64_t ld_qk,
                               int64_t ld_v, const int64_t* offsets, int B, int N, int max_len,
                               int H, int dqk, int dv, const uint8_t* bucket_map,
                               const float* pos_w, const float* ts_w, int num_buckets, float* out,
-                              int64_t ld_out, void* stream);
+                              int64_t ld_out, const void* copies, void* stream);
 
 /* Backward of hstu_attn_fwd (replaces the autograd backward of hstu.py:134-205 and of
  * the bias module hstu.py:96-128, including the index_add_ into _ts_w and the
@@ -252,8 +259,9 @@ GR_API int hstu_attn_bwd(const float* q, const float* k, const float* v, int64_t
 
 /* hstu_attn_bwd_bf16: hstu_attn_bwd with bf16 MFMA operands (Q, K, V, dO, P, dS) and
  * fp32 accumulation / elementwise (the opt-in bf16 compute mode); the bias gradients
- * sum fp32 dS in a fixed order.  Same arguments as hstu_attn_bwd; the workspace size
- * also depends on the head dims. */
+ * sum fp32 dS in a fixed order.  Same arguments as hstu_attn_bwd plus `copies` (NULL or
+ * the forward's hstu_attn_bf16_copies, wide heads); the workspace size also depends on
+ * the head dims and is needed at wide heads with or without a bucket map. */
 GR_API size_t hstu_attn_bwd_bf16_workspace_size(int B, int N, int max_len, int H, int dqk,
                                                 int dv, int num_buckets);
 GR_API int hstu_attn_bwd_bf16(const float* q, const float* k, const float* v, int64_t ld_qk,
@@ -263,7 +271,7 @@ GR_API int hstu_attn_bwd_bf16(const float* q, const float* k, const float* v, in
                               const float* ts_w, int num_buckets, const float* hq,
                               const float* hk, const float* hv, int64_t ld_h, float* dq,
                               float* dk, float* dvv, int64_t ld_d, float* dpos_w, float* dts_w,
-                              void* workspace, size_t ws_bytes, void* stream);
+                              const void* copies, void* workspace, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------- STU projections
  * All take jagged rows (total = offsets[B] <= max_rows), fp32, f32 MFMA.

@@ -262,11 +262,38 @@ static int launch_fwd_bf16(AttnFwdArgsBf16 a, hipStream_t st) {
 
 }  // namespace gr
 
+// wide heads (128 < d <= 256, dqk == dv): hstu_attn_bf16w.hip
+size_t gr_attn_bf16w_copies_bytes(int B, int N, int H, int d);
+int gr_attn_bf16w_copies(const float* q, const float* k, const float* v, int64_t ld_qk, int64_t ld_v,
+                         const int64_t* offsets, int B, int N, int H, int d, void* copies,
+                         hipStream_t st);
+int gr_attn_fwd_bf16w(const void* copies, const int64_t* offsets, int B, int N, int max_len, int H,
+                      int d, const uint8_t* map_qk, const float* pos_w, const float* ts_w,
+                      int num_buckets, float* out, int64_t ld_out, hipStream_t st);
+static bool bf16_wide(int dqk, int dv) { return dqk == dv && dqk > 128 && dqk <= 256; }
+
+extern "C" size_t hstu_attn_bf16_copies_bytes(int B, int N, int H, int dqk, int dv) {
+  if (B <= 0 || N <= 0 || H <= 0 || !bf16_wide(dqk, dv) || dqk % 2) return 0;
+  return gr_attn_bf16w_copies_bytes(B, N, H, dqk);
+}
+
+extern "C" int hstu_attn_bf16_copies(const float* q, const float* k, const float* v, int64_t ld_qk,
+                                     int64_t ld_v, const int64_t* offsets, int B, int N, int H,
+                                     int dqk, int dv, void* copies, void* stream) {
+  using namespace gr;
+  GR_REQUIRE(q && k && v && offsets && copies, "hstu_attn_bf16_copies: null pointer");
+  GR_REQUIRE(B >= 0 && N > 0 && H > 0, "hstu_attn_bf16_copies: bad sizes");
+  GR_REQUIRE(bf16_wide(dqk, dv) && pair_aligned({q, k, v}, {ld_qk, ld_v, (int64_t)dqk}),
+             "hstu_attn_bf16_copies: needs dqk == dv in (128, 256], even strides (dqk %d, dv %d)", dqk, dv);
+  if (B == 0) return 0;
+  return gr_attn_bf16w_copies(q, k, v, ld_qk, ld_v, offsets, B, N, H, dqk, copies, (hipStream_t)stream);
+}
+
 extern "C" int hstu_attn_fwd_bf16(const float* q, const float* k, const float* v, int64_t ld_qk,
                                   int64_t ld_v, const int64_t* offsets, int B, int N, int max_len,
                                   int H, int dqk, int dv, const uint8_t* bucket_map,
                                   const float* pos_w, const float* ts_w, int num_buckets,
-                                  float* out, int64_t ld_out, void* stream) {
+                                  float* out, int64_t ld_out, const void* copies, void* stream) {
   using namespace gr;
   GR_REQUIRE(q && k && v && offsets && out, "hstu_attn_fwd_bf16: null pointer");
   GR_REQUIRE(B >= 0 && N > 0 && H > 0 && dqk > 0 && dv > 0, "hstu_attn_fwd_bf16: bad sizes");
@@ -274,7 +301,12 @@ extern "C" int hstu_attn_fwd_bf16(const float* q, const float* k, const float* v
   GR_REQUIRE(dqk <= 256 && dv <= 256, "hstu_attn_fwd_bf16: dqk/dv > 256 unsupported (%d, %d)", dqk, dv);
   GR_REQUIRE(!bucket_map || (pos_w && ts_w && num_buckets > 0 && num_buckets < 256),
              "hstu_attn_fwd_bf16: bucket_map given without pos_w/ts_w");
+  GR_REQUIRE(!copies || bf16_wide(dqk, dv),
+             "hstu_attn_fwd_bf16: copies are for dqk == dv in (128, 256] (dqk %d, dv %d)", dqk, dv);
   if (B == 0 || max_len == 0) return 0;
+  if (copies)
+    return gr_attn_fwd_bf16w(copies, offsets, B, N, max_len, H, dqk, bucket_map, pos_w, ts_w,
+                             num_buckets, out, ld_out, (hipStream_t)stream);
   AttnFwdArgsBf16 a{q, k, v, ld_qk, ld_v, offsets, B, N, H, dqk, dv, max_len,
                     bucket_map, pos_w, ts_w, bucket_map ? num_buckets : 0, out, ld_out,
                     1.0f / (float)N, 0};
@@ -872,8 +904,8 @@ int gr_attn_bwd_bf16w(const float* q, const float* k, const float* v, int64_t ld
                       int max_len, int H, int d, const uint8_t* map_kq, const float* pos_w,
                       const float* ts_w, int num_buckets, const float* hq, const float* hk,
                       const float* hv, int64_t ld_h, float* dq, float* dk, float* dvv, int64_t ld_d,
-                      float* dpos_w, float* dts_w, void* workspace, hipStream_t st);
-static bool bwd_bf16_wide(int dqk, int dv) { return dqk == dv && dqk > 128 && dqk <= 256; }
+                      float* dpos_w, float* dts_w, const void* copies, void* workspace, hipStream_t st);
+static bool bwd_bf16_wide(int dqk, int dv) { return bf16_wide(dqk, dv); }
 
 extern "C" size_t hstu_attn_bwd_bf16_workspace_size(int B, int N, int max_len, int H, int dqk,
                                                     int dv, int num_buckets) {
@@ -890,7 +922,8 @@ extern "C" int hstu_attn_bwd_bf16(const float* q, const float* k, const float* v
                                   const float* ts_w, int num_buckets, const float* hq,
                                   const float* hk, const float* hv, int64_t ld_h, float* dq,
                                   float* dk, float* dvv, int64_t ld_d, float* dpos_w,
-                                  float* dts_w, void* workspace, size_t ws_bytes, void* stream) {
+                                  float* dts_w, const void* copies, void* workspace, size_t ws_bytes,
+                                  void* stream) {
   using namespace gr;
   GR_REQUIRE(q && k && v && dout && offsets && dq && dk && dvv, "hstu_attn_bwd_bf16: null pointer");
   GR_REQUIRE(B >= 0 && N > 0 && H > 0 && dqk > 0 && dv > 0, "hstu_attn_bwd_bf16: bad sizes");
@@ -925,7 +958,7 @@ extern "C" int hstu_attn_bwd_bf16(const float* q, const float* k, const float* v
   if (wide)
     return gr_attn_bwd_bf16w(q, k, v, ld_qk, ld_v, dout, ld_dout, offsets, B, N, max_len, H, dqk,
                              map_kq, pos_w, ts_w, num_buckets, hq, hk, hv, ld_h, dq, dk, dvv, ld_d,
-                             dpos_w, dts_w, workspace, st);
+                             dpos_w, dts_w, copies, workspace, st);
   AttnBwdArgsBf16 a{q, k, v, ld_qk, ld_v, dout, ld_dout, offsets, B, N, H, dqk, dv, max_len,
                     bucket_map, map_kq, pos_w, ts_w, bucket_map ? num_buckets : 0, hq, hk, hv,
                     ld_h, dq, dk, dvv, ld_d, bucket_map ? (float*)workspace : nullptr,

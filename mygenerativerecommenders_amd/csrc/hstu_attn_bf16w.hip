@@ -153,31 +153,227 @@ constexpr int WK = 128;  // keys (queries) per workgroup: 4 waves x 32
 constexpr int kDtsCopies = 4;  // dts histogram copies per wave (lane % copies)
 __host__ __device__ constexpr int w_dts_stride(int nb1) { return ((nb1 + 30) / 32) * 32 + 1; }
 
-// fp32 -> bf16 copies [row][head][32 D32] of Q, K, V, dO (blockIdx.y = tensor), zero
-// padding past d; one thread per 16-byte chunk; block (0, 0) also writes the zero row.
-__global__ __launch_bounds__(256) void attn_bf16w_convert(AttnBwdArgsW a, int nch) {
-  const float* src = blockIdx.y == 0 ? a.q : blockIdx.y == 1 ? a.k : blockIdx.y == 2 ? a.v : a.dout;
-  const int64_t ld = blockIdx.y < 2 ? a.ld_qk : blockIdx.y == 2 ? a.ld_v : a.ld_dout;
-  __bf16* dst = blockIdx.y == 0 ? a.qb : blockIdx.y == 1 ? a.kb : blockIdx.y == 2 ? a.vb : a.ob;
-  if (blockIdx.x == 0 && blockIdx.y == 0 && (int)threadIdx.x < nch)
-    *reinterpret_cast<u32x4_t*>(a.zrow + 8 * threadIdx.x) = u32x4_t{0u, 0u, 0u, 0u};
+// fp32 -> bf16 copies [row][head][32 D32] (blockIdx.y = tensor of the set), zero padding
+// past d; one thread per 16-byte chunk; block (0, 0) also writes the zero row.
+struct ConvSet {
+  const float* src[4];
+  int64_t ld[4];
+  __bf16* dst[4];
+  __bf16* zrow;
+  const int64_t* offsets;
+  int B, H, d, nch;
+};
+__global__ __launch_bounds__(256) void attn_bf16w_convert(ConvSet cs) {
+  const int y = blockIdx.y;
+  const float* src = y == 0 ? cs.src[0] : y == 1 ? cs.src[1] : y == 2 ? cs.src[2] : cs.src[3];
+  const int64_t ld = y == 0 ? cs.ld[0] : y == 1 ? cs.ld[1] : y == 2 ? cs.ld[2] : cs.ld[3];
+  __bf16* dst = y == 0 ? cs.dst[0] : y == 1 ? cs.dst[1] : y == 2 ? cs.dst[2] : cs.dst[3];
+  if (cs.zrow && blockIdx.x == 0 && y == 0 && (int)threadIdx.x < cs.nch)
+    *reinterpret_cast<u32x4_t*>(cs.zrow + 8 * threadIdx.x) = u32x4_t{0u, 0u, 0u, 0u};
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int c = (int)(idx % nch);
-  const int64_t rh = idx / nch;
-  const int h = (int)(rh % a.H);
-  const int64_t row = rh / a.H;
-  if (row >= a.offsets[a.B]) return;
-  const float* p = src + row * ld + h * a.d + 8 * c;
+  const int c = (int)(idx % cs.nch);
+  const int64_t rh = idx / cs.nch;
+  const int h = (int)(rh % cs.H);
+  const int64_t row = rh / cs.H;
+  if (row >= cs.offsets[cs.B]) return;
+  const float* p = src + row * ld + h * cs.d + 8 * c;
   float x[8];
 #pragma unroll
   for (int j = 0; j < 8; j += 2) {
     float2 v = make_float2(0.f, 0.f);
-    if (8 * c + j < a.d) v = *reinterpret_cast<const float2*>(p + j);  // d, ld even
+    if (8 * c + j < cs.d) v = *reinterpret_cast<const float2*>(p + j);  // d, ld even
     x[j] = v.x;
     x[j + 1] = v.y;
   }
-  *reinterpret_cast<u32x4_t*>(dst + (row * a.H + h) * (8 * nch) + 8 * c) =
+  *reinterpret_cast<u32x4_t*>(dst + (row * cs.H + h) * (8 * cs.nch) + 8 * c) =
       u32x4_t{pack_bf16(x[0], x[1]), pack_bf16(x[2], x[3]), pack_bf16(x[4], x[5]), pack_bf16(x[6], x[7])};
+}
+static int launch_convert(ConvSet cs, int n, int64_t total_rows, hipStream_t st) {
+  if (n == 0) return 0;
+  const int64_t threads = total_rows * cs.H * cs.nch;
+  GR_TIMED("attn_bf16_copies", st, hipLaunchKernelGGL(attn_bf16w_convert, dim3((unsigned)((threads + 255) / 256), n), dim3(256), 0, st, cs));
+  GR_LAUNCH_CHECK("hstu_attn_bf16 copies");
+  return 0;
+}
+
+// ------------------------------------------------------------------ forward
+// out = P V, P = silu(S + bias) / N: 4 waves x 32 queries per workgroup.  Per 32-key
+// chunk a wave computes S^T = K Q^T (A = K rows from the chunk-major LDS tile, B = its
+// queries' Q^T fragments in registers), so the accumulator holds keys in registers and
+// queries on lanes -- as an A operand that is P [query][key] -- and out += P V takes B
+// from the V tile by transposed reads.  K / V tiles arrive by LDS-DMA one chunk ahead.
+struct AttnFwdArgsW {
+  const __bf16* qb;
+  const __bf16* kb;
+  const __bf16* vb;
+  const __bf16* zrow;
+  const int64_t* offsets;
+  int B, N, H, d;
+  const uint8_t* map_qk;  // query-major bucket map (null: no bias)
+  const float* pos_w;
+  const float* ts_w;
+  int nb;
+  float* out;
+  int64_t ld_out;
+  float inv_n;
+  int n_qt;
+};
+
+template <int D32, bool HB>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void attn_fwd_bf16w_kernel(AttnFwdArgsW a) {
+  constexpr int DP = 32 * D32, KS = 2 * D32, TB = 64 * DP;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* tiles = smem;  // [2 buffers][K, V][TB]
+  float* tsw = reinterpret_cast<float*>(smem + 4 * TB);
+  const int npos = 2 * a.N - 1;
+  float* posw = tsw + (a.nb + 1);
+  // XCD-aware order: the query tiles of one (sequence, head) on one XCD, heaviest first
+  const int x = blockIdx.x & 7, sl = blockIdx.x >> 3;
+  const int bh = (sl / a.n_qt) * 8 + x;
+  if (bh >= a.B * a.H) return;
+  const int qt = a.n_qt - 1 - sl % a.n_qt;
+  const int b = bh / a.H, h = bh % a.H;
+  const int64_t s0 = a.offsets[b];
+  const int L = (int)(a.offsets[b + 1] - s0);
+  const int q0 = qt * WK;
+  if (q0 >= L) return;
+  const int tid = threadIdx.x, w = wave_id(), lane = tid & 63;
+  const int lr = lane & 31, lh = lane >> 5;
+  if (HB) {
+    for (int i = tid; i <= a.nb; i += 256) tsw[i] = a.ts_w[i];
+    for (int i = tid; i < npos; i += 256) posw[i] = a.pos_w[i];
+  }
+  const int q0w = q0 + 32 * w;
+  const int qi = q0w + lr;  // this lane's query (column of S^T)
+  const bool q_ok = qi < L;
+  const int64_t rsb = (int64_t)a.H * DP;
+  const int64_t hoff = s0 * rsb + (int64_t)h * DP;
+  // Q^T fragments of the wave's queries: element j of k-step ks = dim 16 ks + 8 lh + j
+  u32x4_t qf[KS];
+  {
+    const __bf16* qrow = q_ok ? a.qb + hoff + (int64_t)qi * rsb : a.zrow;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) qf[ks] = *reinterpret_cast<const u32x4_t*>(qrow + 16 * ks + 8 * lh);
+  }
+  f32x16 acc[D32];
+#pragma unroll
+  for (int t = 0; t < D32; ++t) acc[t] = f16_zero();
+  const __amdgpu_buffer_rsrc_t rmap = map_rsrc(a.map_qk, b, attn_tiles_per_seq(a.N));
+  const int map_w = (qi & 63) * 16;
+  // bucket words of chunk kc: query qi, keys kc + 8m + 4lh .. +3 (query-major 64 x 64 tiles)
+  auto map_words = [&](int kc, uint32_t (&mw)[4]) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int kk = kc + 8 * m + 4 * lh;
+      mw[m] = buf_ld_u32(rmap, (attn_tile_id(q0w >> 6, kk >> 6) * 1024 + map_w + ((kk & 63) >> 2)) * 4, 0);
+    }
+  };
+  const int n_chunks = (min(q0 + WK, L) + 31) / 32;  // key chunks 0, 32, ... the tile needs
+  const bool w_on = q0w < L;
+  auto dma = [&](int buf, int r0) {
+    dma_tile<D32>(tiles + buf * 2 * TB, a.kb + hoff, rsb, r0, L, a.zrow, w, lane);
+    dma_tile<D32>(tiles + buf * 2 * TB + TB, a.vb + hoff, rsb, r0, L, a.zrow, w, lane);
+  };
+  uint32_t mw_next[4] = {0u, 0u, 0u, 0u};
+  if (HB && w_on) map_words(0, mw_next);
+  dma(0, 0);
+  __syncthreads();
+  for (int ci = 0; ci < n_chunks; ++ci) {
+    const int kc0 = 32 * ci;
+    const char* Ks = tiles + (ci & 1) * 2 * TB;
+    const char* Vs = Ks + TB;
+    const bool more = ci + 1 < n_chunks;
+    if (more) dma((ci + 1) & 1, kc0 + 32);
+    const bool act = w_on && kc0 <= q0w + 31;  // wave-uniform causal skip
+    if (act) {
+      uint32_t mw[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) mw[m] = mw_next[m];
+      if (HB && more && kc0 + 32 <= q0w + 31) map_words(kc0 + 32, mw_next);
+      // bias of element rr = key kc0 + (rr & 3) + 8 (rr >> 2) + 4 lh, query qi
+      float bias_p[16], bias_t[16];
+      if (HB) {
+        const float* pw = posw + (a.N - 1 + kc0 + 4 * lh - qi);  // plus the key row
+#pragma unroll
+        for (int rr = 0; rr < 16; ++rr) {
+          const int bk = (mw[rr >> 2] >> (8 * (rr & 3))) & 0xFF;
+          bias_p[rr] = pw[(rr & 3) + 8 * (rr >> 2)];
+          bias_t[rr] = tsw[bk];
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // S^T: A = K rows (k-step ks), B = qf[ks]; two chains (even / odd k-steps)
+      constexpr int PF = 4;
+      u32x4_t ka[PF];
+#pragma unroll
+      for (int i = 0; i < PF; ++i) ka[i] = frag_cm(Ks, i, lane);
+      f32x16 S0 = f16_zero(), S1 = f16_zero();
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const u32x4_t a0 = ka[ks % PF];
+        if (ks + PF < KS) ka[ks % PF] = frag_cm(Ks, ks + PF, lane);
+        if (ks & 1) S1 = mfma32(a0, qf[ks], S1);
+        else S0 = mfma32(a0, qf[ks], S0);
+      }
+#pragma unroll
+      for (int i = 0; i < PF; ++i) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if (ks + PF < KS) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      S0 += S1;
+      float x16[16];
+#pragma unroll
+      for (int rr = 0; rr < 16; ++rr) {
+        const int kj = kc0 + (rr & 3) + 8 * (rr >> 2) + 4 * lh;
+        const bool ok = q_ok && kj <= qi;
+        float xv = S0[rr];
+        if (HB) {
+          float bp = bias_p[rr], bt = bias_t[rr];
+          asm volatile("" : "+v"(bp), "+v"(bt));  // keep the add here, after the products
+          xv = xv + (bp + bt);
+        }
+        const float sg = sigmoidf_(xv);
+        x16[rr] = __uint_as_float(__float_as_uint(xv * sg * a.inv_n) & (ok ? 0xffffffffu : 0u));
+      }
+      const u32x4_t f0 = acc_frag(x16, 0), f1 = acc_frag(x16, 1);
+      __builtin_amdgcn_sched_barrier(0);
+      // out += P V: B = V rows of the chunk (k = keys), transposed reads 4 ahead
+      constexpr int NU = 2 * D32, PB = 4;
+      u32x4_t bq[PB];
+#pragma unroll
+      for (int u = 0; u < PB; ++u) bq[u] = trB_acc_cm(Vs, u / D32, u % D32, lane);
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        const u32x4_t b0 = bq[u % PB];
+        if (u + PB < NU) bq[u % PB] = trB_acc_cm(Vs, (u + PB) / D32, (u + PB) % D32, lane);
+        acc[u % D32] = mfma32(u < D32 ? f0 : f1, b0, acc[u % D32]);
+      }
+#pragma unroll
+      for (int u = 0; u < PB; ++u) __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+        if (u + PB < NU) __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
+      }
+    }
+    if (more) __syncthreads();
+  }
+  if (!w_on) return;
+  // acc[t][rr] = out[query q0w + (rr & 3) + 8 (rr >> 2) + 4 lh][32 t + lr]
+#pragma unroll
+  for (int rr = 0; rr < 16; ++rr) {
+    const int qo = q0w + (rr & 3) + 8 * (rr >> 2) + 4 * lh;
+    if (qo >= L) continue;
+    float* orow = a.out + (s0 + qo) * a.ld_out + h * a.d;
+#pragma unroll
+    for (int t = 0; t < D32; ++t) {
+      const int c = 32 * t + lr;
+      if (c < a.d) orow[c] = acc[t][rr];
+    }
+  }
 }
 
 // ------------------------------------------------------------------ key-major pass
@@ -621,6 +817,32 @@ static size_t bf16w_copy_bytes(int B, int N, int H, int d) {
   return al256((size_t)B * N * H * ceil_div(d, 32) * 32 * 2);
 }
 
+// Q, K, V copies: [Q][K][V][zero row], each copy al256(B N H DPA 2) bytes
+static size_t bf16w_copies_bytes(int B, int N, int H, int d) {
+  return 3 * bf16w_copy_bytes(B, N, H, d) + al256(ceil_div(d, 32) * 64);
+}
+struct CopyPtrs {
+  __bf16 *q, *k, *v, *zrow;
+};
+static CopyPtrs copy_ptrs(const void* copies, int B, int N, int H, int d) {
+  const size_t cp_b = bf16w_copy_bytes(B, N, H, d);
+  char* c = (char*)copies;
+  return {(__bf16*)c, (__bf16*)(c + cp_b), (__bf16*)(c + 2 * cp_b), (__bf16*)(c + 3 * cp_b)};
+}
+
+template <int D32>
+static int launch_fwd_bf16w(AttnFwdArgsW a, hipStream_t st, int max_len) {
+  constexpr int TB = 64 * 32 * D32;
+  const size_t lds = 4 * TB + sizeof(float) * ((a.nb + 1) + (2 * a.N - 1));
+  GR_REQUIRE(lds <= 160 * 1024, "hstu_attn_fwd_bf16: LDS %zu B exceeds 160 KiB (N=%d)", lds, a.N);
+  a.n_qt = ceil_div(max_len, WK);
+  const int bh8 = ceil_div(a.B * a.H, 8) * 8;
+  auto k = a.map_qk ? attn_fwd_bf16w_kernel<D32, true> : attn_fwd_bf16w_kernel<D32, false>;
+  GR_TIMED("attn_fwd", st, hipLaunchKernelGGL(k, dim3(a.n_qt * bh8), dim3(256), lds, st, a));
+  GR_LAUNCH_CHECK("hstu_attn_fwd_bf16(wide)");
+  return 0;
+}
+
 template <int D32>
 static int launch_bwd_bf16w(AttnBwdArgsW a, float* dpos_w, float* dts_w, hipStream_t st) {
   constexpr int DP = 32 * D32, TB = 64 * DP;
@@ -628,10 +850,6 @@ static int launch_bwd_bf16w(AttnBwdArgsW a, float* dpos_w, float* dts_w, hipStre
   const int tss = w_dts_stride(a.nb + 1);
   const size_t lds_kv = 4 * TB + sizeof(float) * ((a.nb + 1) + npos + 4 * kDtsCopies * tss);
   const size_t lds_q = 2 * TB + 4 * 2 * 2048;
-  const int nch = 4 * D32;
-  const int64_t conv_threads = a.total_rows * a.H * nch;
-  GR_TIMED("attn_bwd_convert", st, hipLaunchKernelGGL(attn_bf16w_convert, dim3((unsigned)((conv_threads + 255) / 256), 4), dim3(256), 0, st, a, nch));
-  GR_LAUNCH_CHECK("hstu_attn_bwd_bf16(wide convert)");
   GR_REQUIRE(lds_kv <= 160 * 1024, "hstu_attn_bwd_bf16: LDS %zu B exceeds 160 KiB (N=%d)", lds_kv, a.N);
   const int grid = a.n_kt * a.B * a.H;
   auto kkv = a.map_kq ? attn_bwd_bf16w_kv_kernel<D32, true> : attn_bwd_bf16w_kv_kernel<D32, false>;
@@ -654,11 +872,44 @@ static int launch_bwd_bf16w(AttnBwdArgsW a, float* dpos_w, float* dts_w, hipStre
 
 }  // namespace gr
 
-// Wide-head entry (called by hstu_attn_bwd_bf16 for 128 < d <= 256, dqk == dv).
+// Wide-head entries (called by hstu_attn_{fwd,bwd}_bf16 for 128 < d <= 256, dqk == dv).
+size_t gr_attn_bf16w_copies_bytes(int B, int N, int H, int d) {
+  return gr::bf16w_copies_bytes(B, N, H, d);
+}
+
+int gr_attn_bf16w_copies(const float* q, const float* k, const float* v, int64_t ld_qk, int64_t ld_v,
+                         const int64_t* offsets, int B, int N, int H, int d, void* copies,
+                         hipStream_t st) {
+  using namespace gr;
+  const CopyPtrs c = copy_ptrs(copies, B, N, H, d);
+  ConvSet cs{{q, k, v, nullptr}, {ld_qk, ld_qk, ld_v, 0}, {c.q, c.k, c.v, nullptr}, c.zrow,
+             offsets, B, H, d, 4 * ceil_div(d, 32)};
+  return launch_convert(cs, 3, (int64_t)B * N, st);
+}
+
+int gr_attn_fwd_bf16w(const void* copies, const int64_t* offsets, int B, int N, int max_len, int H,
+                      int d, const uint8_t* map_qk, const float* pos_w, const float* ts_w,
+                      int num_buckets, float* out, int64_t ld_out, hipStream_t st) {
+  using namespace gr;
+  const CopyPtrs c = copy_ptrs(copies, B, N, H, d);
+  AttnFwdArgsW a{};
+  a.qb = c.q; a.kb = c.k; a.vb = c.v; a.zrow = c.zrow;
+  a.offsets = offsets; a.B = B; a.N = N; a.H = H; a.d = d;
+  a.map_qk = map_qk; a.pos_w = pos_w; a.ts_w = ts_w; a.nb = map_qk ? num_buckets : 0;
+  a.out = out; a.ld_out = ld_out; a.inv_n = 1.0f / (float)N;
+  const int D32 = ceil_div(d, 32);
+  if (D32 <= 5) return launch_fwd_bf16w<5>(a, st, max_len);
+  if (D32 == 6) return launch_fwd_bf16w<6>(a, st, max_len);
+  if (D32 == 7) return launch_fwd_bf16w<7>(a, st, max_len);
+  return launch_fwd_bf16w<8>(a, st, max_len);
+}
+
+// workspace: slabs | dS blocks | dO copy + zero row | Q, K, V copies (used when the caller
+// passes none)
 size_t gr_attn_bwd_bf16w_workspace(int B, int N, int max_len, int H, int d, int num_buckets) {
   using namespace gr;
   return al256(bf16w_slab_bytes(B, N, max_len, H, num_buckets)) + al256(bf16w_ds_bytes(B, N, H)) +
-         4 * bf16w_copy_bytes(B, N, H, d) + 256;
+         bf16w_copy_bytes(B, N, H, d) + al256(ceil_div(d, 32) * 64) + bf16w_copies_bytes(B, N, H, d);
 }
 
 int gr_attn_bwd_bf16w(const float* q, const float* k, const float* v, int64_t ld_qk, int64_t ld_v,
@@ -666,11 +917,12 @@ int gr_attn_bwd_bf16w(const float* q, const float* k, const float* v, int64_t ld
                       int max_len, int H, int d, const uint8_t* map_kq, const float* pos_w,
                       const float* ts_w, int num_buckets, const float* hq, const float* hk,
                       const float* hv, int64_t ld_h, float* dq, float* dk, float* dvv, int64_t ld_d,
-                      float* dpos_w, float* dts_w, void* workspace, hipStream_t st) {
+                      float* dpos_w, float* dts_w, const void* copies, void* workspace, hipStream_t st) {
   using namespace gr;
   const size_t slab_b = al256(bf16w_slab_bytes(B, N, max_len, H, num_buckets));
   const size_t ds_b = al256(bf16w_ds_bytes(B, N, H));
   const size_t cp_b = bf16w_copy_bytes(B, N, H, d);
+  const int nch = 4 * ceil_div(d, 32);
   AttnBwdArgsW a{};
   a.q = q; a.k = k; a.v = v; a.ld_qk = ld_qk; a.ld_v = ld_v; a.dout = dout; a.ld_dout = ld_dout;
   a.offsets = offsets; a.B = B; a.N = N; a.H = H; a.d = d;
@@ -680,12 +932,24 @@ int gr_attn_bwd_bf16w(const float* q, const float* k, const float* v, int64_t ld
   a.slabs = (float*)workspace;
   a.ds = (__bf16*)((char*)workspace + slab_b);
   char* cp = (char*)workspace + slab_b + ds_b;
-  a.qb = (__bf16*)cp;
-  a.kb = (__bf16*)(cp + cp_b);
-  a.vb = (__bf16*)(cp + 2 * cp_b);
-  a.ob = (__bf16*)(cp + 3 * cp_b);
-  a.zrow = (__bf16*)(cp + 4 * cp_b);
+  a.ob = (__bf16*)cp;
+  __bf16* ozrow = (__bf16*)(cp + cp_b);
+  char* own = cp + cp_b + al256(nch * 16);
+  ConvSet cs{{dout, q, k, v}, {ld_dout, ld_qk, ld_qk, ld_v}, {a.ob, nullptr, nullptr, nullptr}, ozrow,
+             offsets, B, H, d, nch};
+  int n = 1;
+  if (copies) {  // Q, K, V copies from the forward
+    const CopyPtrs c = copy_ptrs(copies, B, N, H, d);
+    a.qb = c.q; a.kb = c.k; a.vb = c.v;
+  } else {
+    const CopyPtrs c = copy_ptrs(own, B, N, H, d);
+    a.qb = c.q; a.kb = c.k; a.vb = c.v;
+    cs.dst[1] = c.q; cs.dst[2] = c.k; cs.dst[3] = c.v;
+    n = 4;
+  }
+  a.zrow = ozrow;
   a.total_rows = (int64_t)B * N;
+  if (launch_convert(cs, n, a.total_rows, st)) return -1;
   const int nb32 = ceil_div(N, 32);
   a.nbt = nb32 * (nb32 + 1) / 2;
   a.inv_n = 1.0f / (float)N;

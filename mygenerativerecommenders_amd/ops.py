@@ -272,10 +272,24 @@ class STULayerFunction(torch.autograd.Function):
         v = uvqk[:, hv:2 * hv]
         pos_w_c = pos_w.contiguous() if bmap is not None else None
         ts_w_c = ts_w.contiguous() if bmap is not None else None
-        _lib.call("hstu_attn_fwd_bf16" if geo.bf16 else "hstu_attn_fwd", q.data_ptr(), k.data_ptr(),
-                  v.data_ptr(), n_out, n_out,
-                  offsets.data_ptr(), B, geo.N, geo.max_len, H, dqk, dv, _lib.ptr(bmap),
-                  _lib.ptr(pos_w_c), _lib.ptr(ts_w_c), NUM_BUCKETS, attn.data_ptr(), hv, st)
+        # wide bf16 heads: bf16 copies of Q, K, V that the attention kernels stage into LDS
+        # by DMA, made once here and kept for the backward
+        copies = None
+        if geo.bf16 and n_out % 2 == 0:
+            cb = _lib.lib().hstu_attn_bf16_copies_bytes(B, geo.N, H, dqk, dv)
+            if cb:
+                copies = torch.empty(cb, dtype=torch.uint8, device=dev)
+                _lib.call("hstu_attn_bf16_copies", q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out,
+                          n_out, offsets.data_ptr(), B, geo.N, H, dqk, dv, copies.data_ptr(), st)
+        if geo.bf16:
+            _lib.call("hstu_attn_fwd_bf16", q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out, n_out,
+                      offsets.data_ptr(), B, geo.N, geo.max_len, H, dqk, dv, _lib.ptr(bmap),
+                      _lib.ptr(pos_w_c), _lib.ptr(ts_w_c), NUM_BUCKETS, attn.data_ptr(), hv,
+                      _lib.ptr(copies), st)
+        else:
+            _lib.call("hstu_attn_fwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out, n_out,
+                      offsets.data_ptr(), B, geo.N, geo.max_len, H, dqk, dv, _lib.ptr(bmap),
+                      _lib.ptr(pos_w_c), _lib.ptr(ts_w_c), NUM_BUCKETS, attn.data_ptr(), hv, st)
         attn_stats = torch.empty(rows, 2, dtype=torch.float32, device=dev)
         needs_w_grad = grad_on and (w_o.requires_grad or b_o.requires_grad)
         ow = 3 * hv if geo.concat_ua else hv  # o_in width
@@ -298,7 +312,7 @@ class STULayerFunction(torch.autograd.Function):
                       _lib.ptr(seed_offset), attn_stats.data_ptr(), _lib.ptr(o_in), y.data_ptr(),
                       D, st)
         ctx.save_for_backward(x, offsets, bmap, w_uvqk, w_o, pos_w_c, ts_w_c, x_stats, uvqk,
-                              h_pre, attn, attn_stats, o_in)
+                              h_pre, attn, attn_stats, o_in, copies if grad_on else None)
         ctx.geo = geo
         ctx.seed = seed
         ctx.seed_offset = seed_offset
@@ -307,7 +321,7 @@ class STULayerFunction(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         (x, offsets, bmap, w_uvqk, w_o, pos_w, ts_w, x_stats, uvqk, h_pre, attn, attn_stats,
-         o_in) = ctx.saved_tensors
+         o_in, copies) = ctx.saved_tensors
         geo = ctx.geo
         dev = x.device
         rows, D = x.shape
@@ -339,6 +353,7 @@ class STULayerFunction(torch.autograd.Function):
         if bmap is not None:
             d_pos_w = torch.empty(2 * geo.N - 1, dtype=torch.float32, device=dev)
             d_ts_w = torch.empty(NUM_BUCKETS + 1, dtype=torch.float32, device=dev)
+        if bmap is not None or geo.bf16:  # wide bf16 heads use the workspace without a map too
             ws_a_n = (L.hstu_attn_bwd_bf16_workspace_size(B, geo.N, geo.max_len, H, dqk, dv,
                                                           NUM_BUCKETS) if geo.bf16 else
                       L.hstu_attn_bwd_workspace_size(B, geo.N, geo.max_len, H, NUM_BUCKETS))
@@ -355,12 +370,15 @@ class STULayerFunction(torch.autograd.Function):
         dq = d_uvqk[:, 2 * hv:2 * hv + hq]
         dk = d_uvqk[:, 2 * hv + hq:]
         dvv = d_uvqk[:, hv:2 * hv]
-        _lib.call("hstu_attn_bwd_bf16" if geo.bf16 else "hstu_attn_bwd", q.data_ptr(), k.data_ptr(),
-                  v.data_ptr(), n_out, n_out,
-                  d_attn.data_ptr(), hv, offsets.data_ptr(), B, geo.N, geo.max_len, H, dqk, dv,
-                  _lib.ptr(bmap), _lib.ptr(pos_w), _lib.ptr(ts_w), NUM_BUCKETS,
-                  hq_p, hk_p, hv_p, n_out, dq.data_ptr(), dk.data_ptr(), dvv.data_ptr(), n_out,
-                  _lib.ptr(d_pos_w), _lib.ptr(d_ts_w), _lib.ptr(ws_a), ws_a_n, st)
+        bwd_args = (q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out, n_out,
+                    d_attn.data_ptr(), hv, offsets.data_ptr(), B, geo.N, geo.max_len, H, dqk, dv,
+                    _lib.ptr(bmap), _lib.ptr(pos_w), _lib.ptr(ts_w), NUM_BUCKETS,
+                    hq_p, hk_p, hv_p, n_out, dq.data_ptr(), dk.data_ptr(), dvv.data_ptr(), n_out,
+                    _lib.ptr(d_pos_w), _lib.ptr(d_ts_w))
+        if geo.bf16:
+            _lib.call("hstu_attn_bwd_bf16", *bwd_args, _lib.ptr(copies), _lib.ptr(ws_a), ws_a_n, st)
+        else:
+            _lib.call("hstu_attn_bwd", *bwd_args, _lib.ptr(ws_a), ws_a_n, st)
         dx = torch.empty(rows, D, dtype=torch.float32, device=dev)
         _lib.call("hstu_ln_uvqk_bwd" + ("_bf16" if geo.bf16 else ""), d_uvqk.data_ptr(), n_out,
                   offsets.data_ptr(), B, rows, D,

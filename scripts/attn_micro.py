@@ -83,11 +83,18 @@ def main():
 
     if args.nobias:
         bmap = None
+    # wide bf16 heads: the forward's bf16 Q / K / V copies (made per step, as in training)
+    cb = L_.hstu_attn_bf16_copies_bytes(B, N, H, d, d) if args.bf16 else 0
+    copies = torch.empty(cb, dtype=torch.uint8, device=dev) if cb else None
 
     def fwd():
+        if copies is not None:
+            _lib.call("hstu_attn_bf16_copies", q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out,
+                      n_out, offsets.data_ptr(), B, N, H, d, d, copies.data_ptr(), st)
+        extra = (_lib.ptr(copies),) if args.bf16 else ()
         _lib.call("hstu_attn_fwd_bf16" if args.bf16 else "hstu_attn_fwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out, n_out,
                   offsets.data_ptr(), B, N, L, H, d, d, _lib.ptr(bmap), pos_w.data_ptr(),
-                  ts_w.data_ptr(), 128, out.data_ptr(), hv, st)
+                  ts_w.data_ptr(), 128, out.data_ptr(), hv, *extra, st)
 
     h = torch.randn(rows, n_out, device=dev, generator=g) if args.hepi else None
     hq = h[:, 2 * hv:3 * hv].data_ptr() if args.hepi else None
@@ -99,7 +106,7 @@ def main():
                   dout.data_ptr(), hv, offsets.data_ptr(), B, N, L, H, d, d, _lib.ptr(bmap),
                   pos_w.data_ptr(), ts_w.data_ptr(), 128, hq, hk, hvp, n_out if args.hepi else 0,
                   dq.data_ptr(), dk.data_ptr(), dvv.data_ptr(), n_out, dpw.data_ptr(),
-                  dtw.data_ptr(), ws.data_ptr(), ws_n, st)
+                  dtw.data_ptr(), *((_lib.ptr(copies),) if args.bf16 else ()), ws.data_ptr(), ws_n, st)
 
     for _ in range(3):
         fwd()
@@ -114,7 +121,7 @@ def main():
             bwd()
     torch.cuda.synchronize()
     _lib.timing_enable(False)
-    kt = _lib.kernel_times(("attn_fwd", "attn_bwd", "attn_bwd_dkv", "attn_bwd_dq", "attn_bias_reduce", "attn_bwd_convert"))
+    kt = _lib.kernel_times(("attn_fwd", "attn_bwd", "attn_bwd_dkv", "attn_bwd_dq", "attn_bias_reduce", "attn_bf16_copies"))
     fl = flops(B, L, d, H)
     res = {}
     for name, (tot, n) in kt.items():

@@ -36,7 +36,22 @@ def _case(seed, B, N, H, dqk, dv, lengths=None, with_ts=True, scale=1.0):
     return lengths, offsets, uvqk, ts, pos_w, ts_w
 
 
-def _run_gpu_fwd(offsets, uvqk, ts, pos_w, ts_w, B, N, H, dqk, dv, entry="hstu_attn_fwd"):
+def _make_copies(u, offs, B, N, H, dqk, dv):
+    """bf16 Q, K, V copies for the wide bf16 kernels (None where they do not apply)."""
+    from mygenerativerecommenders_amd import _lib
+    hv, hq = H * dv, H * dqk
+    cb = _lib.lib().hstu_attn_bf16_copies_bytes(B, N, H, dqk, dv)
+    if not cb or u.stride(0) % 2:
+        return None
+    c = torch.empty(cb, dtype=torch.uint8, device=u.device)
+    _lib.call("hstu_attn_bf16_copies", u[:, 2 * hv:].data_ptr(), u[:, 2 * hv + hq:].data_ptr(),
+              u[:, hv:].data_ptr(), u.stride(0), u.stride(0), offs.data_ptr(), B, N, H, dqk, dv,
+              c.data_ptr(), _lib.stream_handle())
+    return c
+
+
+def _run_gpu_fwd(offsets, uvqk, ts, pos_w, ts_w, B, N, H, dqk, dv, entry="hstu_attn_fwd",
+                 copies=False):
     from mygenerativerecommenders_amd import _lib
     dev = torch.device("cuda")
     u = uvqk.to(dev)
@@ -53,9 +68,12 @@ def _run_gpu_fwd(offsets, uvqk, ts, pos_w, ts_w, B, N, H, dqk, dv, entry="hstu_a
     max_len = int((offsets[1:] - offsets[:-1]).max()) if B else 0
     from mygenerativerecommenders_amd import ops
     bmap = ops.bucket_map(tsd, offs, N) if tsd is not None else None
+    extra = ()
+    if entry == "hstu_attn_fwd_bf16":
+        extra = (_lib.ptr(_make_copies(u, offs, B, N, H, dqk, dv) if copies else None),)
     _lib.call(entry, q.data_ptr(), k.data_ptr(), v.data_ptr(), u.stride(0), u.stride(0),
               offs.data_ptr(), B, N, max_len, H, dqk, dv, _lib.ptr(bmap), pw.data_ptr(),
-              tw.data_ptr(), 128, out.data_ptr(), out.stride(0), _lib.stream_handle())
+              tw.data_ptr(), 128, out.data_ptr(), out.stride(0), *extra, _lib.stream_handle())
     torch.cuda.synchronize()
     return out.cpu()
 
@@ -97,7 +115,8 @@ def test_attn_fwd_full_length_and_len1():
     assert (got - ref).abs().max().item() <= 2e-5 * (1 + ref.abs().max().item())
 
 
-def _run_gpu_bwd(offsets, uvqk, dout, ts, pos_w, ts_w, B, N, H, dqk, dv, hpre=None, bf16=False):
+def _run_gpu_bwd(offsets, uvqk, dout, ts, pos_w, ts_w, B, N, H, dqk, dv, hpre=None, bf16=False,
+                 copies=False):
     from mygenerativerecommenders_amd import _lib
     dev = torch.device("cuda")
     u = uvqk.to(dev)
@@ -130,7 +149,9 @@ def _run_gpu_bwd(offsets, uvqk, dout, ts, pos_w, ts_w, B, N, H, dqk, dv, hpre=No
               _lib.ptr(bmap), pw.data_ptr(), tw.data_ptr(), 128,
               hq_p, hk_p, hv_p, u.stride(0) if hd is not None else 0,
               dq.data_ptr(), dk.data_ptr(), dvv.data_ptr(), d.stride(0),
-              dpw.data_ptr(), dtw.data_ptr(), ws.data_ptr(), ws_bytes, _lib.stream_handle())
+              dpw.data_ptr(), dtw.data_ptr(),
+              *((_lib.ptr(_make_copies(u, offs, B, N, H, dqk, dv) if copies else None),) if bf16 else ()),
+              ws.data_ptr(), ws_bytes, _lib.stream_handle())
     torch.cuda.synchronize()
     return dq.cpu(), dk.cpu(), dvv.cpu(), dpw.cpu(), dtw.cpu()
 
@@ -319,15 +340,20 @@ def test_attn_fwd_bf16_vs_oracle(B, N, H, dqk, dv, with_ts):
     v = uvqk[:, hv:2 * hv]
     cfg = O.HSTUConfig(N=N, D=1, H=H, dqk=dqk, dv=dv)
     ref = O.hstu_attention_jagged(q, k, v, offsets, ts, cfg, pos_w, ts_w, _thr())
-    got = _run_gpu_fwd(offsets, uvqk, ts, pos_w, ts_w, B, N, H, dqk, dv,
-                       entry="hstu_attn_fwd_bf16")
-    assert torch.isfinite(got).all()
-    err = (got - ref).abs().max().item()
-    scale = 1 + ref.abs().max().item()
-    print(f"bf16 fwd rel err {err / scale:.3e}")
-    assert err <= BF16_FWD_TOL * scale
-    # and it is genuinely the reduced-precision path (not the fp32 kernel)
-    assert err > 0
+    from mygenerativerecommenders_amd import _lib
+    modes = [False]
+    if _lib.lib().hstu_attn_bf16_copies_bytes(B, N, H, dqk, dv):
+        modes.append(True)  # wide heads: the DMA-staged kernel on the bf16 copies
+    for copies in modes:
+        got = _run_gpu_fwd(offsets, uvqk, ts, pos_w, ts_w, B, N, H, dqk, dv,
+                           entry="hstu_attn_fwd_bf16", copies=copies)
+        assert torch.isfinite(got).all()
+        err = (got - ref).abs().max().item()
+        scale = 1 + ref.abs().max().item()
+        print(f"bf16 fwd (copies={copies}) rel err {err / scale:.3e}")
+        assert err <= BF16_FWD_TOL * scale
+        # and it is genuinely the reduced-precision path (not the fp32 kernel)
+        assert err > 0
 
 
 # hstu_attn_bwd_bf16: bf16 MFMA operands (Q, K, V, dO, P, dS), fp32 accumulation and
@@ -375,6 +401,19 @@ def test_attn_bwd_bf16_vs_oracle(B, N, H, dqk, dv, with_ts):
         err = (got - want).abs().max().item() / (1 + want.abs().max().item())
         print(f"bf16 bwd {name} rel err {err:.3e}")
         _close(got, want, rel=BF16_BWD_TOL)
+
+
+@pytest.mark.parametrize("B,N,H,d,with_ts", [(2, 300, 2, 192, True), (2, 150, 1, 256, False)])
+def test_attn_bwd_bf16_forward_copies_bitexact(B, N, H, d, with_ts):
+    """The backward on the forward's bf16 copies equals the backward that converts its own
+    operands, bit for bit (same rounding, same kernels)."""
+    lengths, offsets, uvqk, ts, pos_w, ts_w = _case(B * 5 + N, B, N, H, d, d, with_ts=with_ts)
+    g = torch.Generator().manual_seed(3)
+    dout = torch.randn(uvqk.shape[0], H * d, generator=g)
+    a = _run_gpu_bwd(offsets, uvqk, dout, ts, pos_w, ts_w, B, N, H, d, d, bf16=True)
+    b = _run_gpu_bwd(offsets, uvqk, dout, ts, pos_w, ts_w, B, N, H, d, d, bf16=True, copies=True)
+    for x, y in zip(a[:3] if not with_ts else a, b):  # no bias: dpos / dts are not written
+        assert torch.equal(x, y)
 
 
 @pytest.mark.parametrize("d", [32, 256])
