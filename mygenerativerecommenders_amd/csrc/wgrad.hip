@@ -20,6 +20,7 @@
 // half reduction) and written as slab column Nb: no padding panel carries it (at C3 the
 // ones column of Nb = 256 + 1 cost a second, all-padding panel of 256 columns).
 #include "attn_common.h"
+#include "mfma32.h"
 
 #include "../../include/gr_hstu.h"
 
@@ -390,6 +391,146 @@ __global__ __launch_bounds__(WG_THREADS) void wgrad_partial_bf16_kernel(WgradArg
                           panel - g.p[0].panels, smem);
 }
 
+// ------------------------------------------------------------------ bf16, wide (Ka <= 256)
+// 256 (ka) x 256 (nb) output tile per workgroup, v_mfma_f32_32x32x16_bf16: A is read once
+// per nb tile instead of once per 64-wide ka panel and B once instead of once per ka panel
+// (C3 _uvqk: 0.67 GB of operand traffic per layer instead of 1.7 GB).  Chunks of 32 rows:
+// each thread loads 4 float4 of A and 4 of B (one chunk ahead, in registers), applies the
+// LayerNorm to A in fp32, rounds both to bf16 and writes row-major LDS tiles; the MFMA
+// operands are transposed reads of those tiles (A^T: lanes = ka; B: lanes = nb, both with
+// k = rows).  Wave w: ka rows 64 (w & 3) .. +63, nb columns 128 (w >> 2) .. +127 (8 tiles).
+constexpr int WGW_T = 256;            // tile edge
+constexpr int WGW_RS = WGW_T + 8;     // LDS row stride (bf16)
+constexpr size_t WGW_LDS = 2 * 2 * 32 * WGW_RS * 2;
+
+__device__ __forceinline__ void wgrad_tile_bf16w(const WgradProb& g, const int64_t* offsets, int B,
+                                                 int64_t rows_per_split, int split, int tile,
+                                                 char* smem) {
+  __bf16* lds = reinterpret_cast<__bf16*>(smem);  // [2 buffers][A, B][32][WGW_RS]
+  const int nb0 = tile * WGW_T;
+  const int64_t total = offsets[B];
+  const int64_t r0 = (int64_t)split * rows_per_split;
+  const int64_t r1 = min(total, r0 + rows_per_split);
+  const int tid = threadIdx.x, wv = wave_id(), lane = tid & 63;
+  const int n_ch = __builtin_amdgcn_readfirstlane(r1 > r0 ? (int)((r1 - r0 + 31) / 32) : 0);
+  const int64_t nrows = r1 > r0 ? r1 - r0 : 0;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(g.a + r0 * g.lda), 0, nrows ? (int)(((nrows - 1) * g.lda + g.Ka) * 4) : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(g.bm + r0 * g.ldb), 0, nrows ? (int)(((nrows - 1) * g.ldb + g.Nb) * 4) : 0, 0x00020000);
+  // staging: thread t owns columns 4 (t % 64) .. +3 of rows t / 64 + 8 i (i < 4)
+  const int sc = 4 * (tid & 63), sr = tid >> 6;
+  const bool a_ok = sc < g.Ka, b_ok = nb0 + sc < g.Nb;  // Ka, Nb multiples of 4 (host check)
+  const int aoff = a_ok ? sc * 4 : 0x40000000, boff = b_ok ? (nb0 + sc) * 4 : 0x40000000;
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  f4v av[4], bv[4];
+  float2 stv[4];
+  auto load = [&](int ch) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rr = 32 * ch + sr + 8 * i;
+      av[i] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(ra, aoff + rr * (int)g.lda * 4, 0, 0));
+      bv[i] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rb, boff + rr * (int)g.ldb * 4, 0, 0));
+      stv[i] = g.a_stats ? ld_f2(g.a_stats, min(r0 + rr, total - 1)) : make_float2(0.f, 1.f);
+    }
+  };
+  const bool do_cs = g.NC > g.Nb && tile == 0;
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};  // bf16(A') column sums of this thread's 4 columns
+  auto store = [&](int ch, int buf) {
+    __bf16* At = lds + buf * 2 * 32 * WGW_RS;
+    __bf16* Bt = At + 32 * WGW_RS;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rr = sr + 8 * i;
+      const bool ok = r0 + 32 * ch + rr < r1;
+      float x[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[e] = ok ? (av[i][e] - stv[i].x) * stv[i].y : 0.f;
+      const uint32_t p0 = pack_bf16(x[0], x[1]), p1 = pack_bf16(x[2], x[3]);
+      if (do_cs) {
+        cs[0] += __uint_as_float(p0 << 16);
+        cs[1] += __uint_as_float(p0 & 0xffff0000u);
+        cs[2] += __uint_as_float(p1 << 16);
+        cs[3] += __uint_as_float(p1 & 0xffff0000u);
+      }
+      *reinterpret_cast<u32x2_t*>(At + rr * WGW_RS + sc) = u32x2_t{p0, p1};
+      *reinterpret_cast<u32x2_t*>(Bt + rr * WGW_RS + sc) =
+          u32x2_t{pack_bf16(bv[i][0], bv[i][1]), pack_bf16(bv[i][2], bv[i][3])};  // rows past r1 meet a zero A
+    }
+  };
+  const int wka = 64 * (wv & 3), wnb = 128 * (wv >> 2);
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f16_zero();
+  if (n_ch > 0) {
+    load(0);
+    store(0, 0);
+  }
+  __syncthreads();
+  for (int ch = 0; ch < n_ch; ++ch) {
+    const bool more = ch + 1 < n_ch;
+    if (more) load(ch + 1);  // the next chunk's rows fly during the MFMAs
+    const __bf16* At = lds + (ch & 1) * 2 * 32 * WGW_RS;
+    const __bf16* Bt = At + 32 * WGW_RS;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      u32x4_t af[2], bf[4];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = trB_nat(At, WGW_RS, s, wka + 32 * i, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bf[j] = trB_nat(Bt, WGW_RS, s, wnb + 32 * j, lane);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma32(af[i], bf[j], acc[i][j]);
+    }
+    if (more) store(ch + 1, (ch + 1) & 1);
+    __syncthreads();
+  }
+  // acc[i][j][rr] = C[ka wka + 32 i + (rr & 3) + 8 (rr >> 2) + 4 (lane >> 5)][nb nb0 + wnb + 32 j + lane % 32]
+  float* slab = g.slabs + (int64_t)split * g.Ka * g.NC;
+  const int lr = lane & 31, lh = lane >> 5;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int rr = 0; rr < 16; ++rr) {
+      const int ka = wka + 32 * i + (rr & 3) + 8 * (rr >> 2) + 4 * lh;
+      if (ka >= g.Ka) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int nb = nb0 + wnb + 32 * j + lr;
+        if (nb < g.Nb) slab[(int64_t)ka * g.NC + nb] = acc[i][j][rr];
+      }
+    }
+  if (do_cs) {  // the 8 row groups' partial column sums, added in wave order
+    float* xs = reinterpret_cast<float*>(smem);  // [8][256]
+#pragma unroll
+    for (int e = 0; e < 4; ++e) xs[sr * WGW_T + sc + e] = cs[e];
+    __syncthreads();
+    if (tid < WGW_T && tid < g.Ka) {
+      float t = 0.f;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) t += xs[r * WGW_T + tid];
+      slab[(int64_t)tid * g.NC + g.Nb] = t;
+    }
+  }
+}
+
+// grid: XCD-aware, all tiles of one split on one XCD (A shared through its L2)
+__global__ __launch_bounds__(WG_THREADS) void wgrad_partial_bf16w_kernel(WgradArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int P = g.p[0].panels + g.p[1].panels;
+  const int x = blockIdx.x & 7, sl = blockIdx.x >> 3;
+  const int split = (sl / P) * 8 + x, tile = sl % P;
+  if (split >= g.n_splits) return;
+  if (tile < g.p[0].panels)
+    wgrad_tile_bf16w(g.p[0], g.offsets, g.B, g.rows_per_split, split, tile, smem);
+  else
+    wgrad_tile_bf16w(g.p[1], g.offsets, g.B, g.rows_per_split, split, tile - g.p[0].panels, smem);
+}
+
 // out = sum over splits (fixed order): a workgroup owns 16 outputs of one problem; thread
 // (o, grp) sums splits grp, grp+16, ... 8-deep, then the 16 partials are added in grp
 // order.  Blocks [0, blocks0) reduce problem 0, the rest problem 1.
@@ -511,6 +652,40 @@ static size_t lds_of(int nt) {
   }
 }
 
+// bf16 wide plan (wgrad_tile_bf16w): Ka <= 256, one 256-wide tile per 256 columns of Nb;
+// splits a multiple of 8 (XCD groups) with ~one workgroup per CU over the launch.
+static bool wgrad_wide_ok(const WgradProb in[2]) {
+  int kmax = 0;
+  for (int i = 0; i < 2; ++i) {
+    if (!in[i].a) continue;
+    const WgradProb& p = in[i];
+    if (p.Ka > WGW_T || p.Ka % 4 || p.Nb % 4 || p.lda % 4 || p.ldb % 4 ||
+        (uintptr_t)p.a % 16 || (uintptr_t)p.bm % 16)
+      return false;
+    kmax = std::max(kmax, p.Ka);
+  }
+  return kmax > 128;
+}
+static WgPlan wgrad_plan_wide(int64_t max_rows, const int Ka[2], const int Nb[2]) {
+  WgPlan pl{};
+  int tiles = 0;
+  for (int i = 0; i < 2; ++i) {
+    if (Ka[i] <= 0) continue;
+    pl.panels[i] = ceil_div(Nb[i], WGW_T);
+    pl.panels_nb[i] = pl.panels[i];
+    tiles += pl.panels[i];
+  }
+  int target = device_cus() / (tiles > 0 ? tiles : 1);
+  target = std::max(8, (target / 8) * 8);
+  int64_t rps = (max_rows + target - 1) / target;
+  rps = std::max<int64_t>(((rps + 31) / 32) * 32, 128);
+  pl.rps = rps;
+  pl.n_splits = std::max(1, (int)((max_rows + rps - 1) / rps));
+  for (int i = 0; i < 2; ++i)
+    pl.slab_bytes[i] = Ka[i] > 0 ? sizeof(float) * (size_t)pl.n_splits * Ka[i] * (Nb[i] + 1) : 0;
+  return pl;
+}
+
 static int wgrad_run(const WgradProb in[2], const int64_t* offsets, int B, int64_t max_rows,
                      void* workspace, size_t ws_bytes, hipStream_t st, bool bf16 = false) {
   const int Ka[2] = {in[0].Ka, in[1].a ? in[1].Ka : 0};
@@ -523,7 +698,8 @@ static int wgrad_run(const WgradProb in[2], const int64_t* offsets, int B, int64
     }
     return 0;
   }
-  const WgPlan pl = wgrad_plan(max_rows, Ka, Nb);
+  const bool wide = bf16 && wgrad_wide_ok(in);
+  const WgPlan pl = wide ? wgrad_plan_wide(max_rows, Ka, Nb) : wgrad_plan(max_rows, Ka, Nb);
   const size_t need = align256w(pl.slab_bytes[0]) + pl.slab_bytes[1];
   GR_REQUIRE(workspace && ws_bytes >= need, "gr_wgrad: workspace %zu B < %zu B", ws_bytes, need);
   WgradArgs g{};
@@ -544,6 +720,16 @@ static int wgrad_run(const WgradProb in[2], const int64_t* offsets, int B, int64
     g.p[i].panels_nb = pl.panels_nb[i];
     g.p[i].slabs = (float*)(ws + (i == 0 ? 0 : align256w(pl.slab_bytes[0])));
     blocks[i] = (int)(((int64_t)Ka[i] * g.p[i].NC + 15) / 16);
+  }
+  if (wide) {
+    const int P = g.p[0].panels + g.p[1].panels;
+    GR_TIMED("wgrad_partial", st, hipLaunchKernelGGL(wgrad_partial_bf16w_kernel, dim3(ceil_div(pl.n_splits, 8) * 8 * P),
+                                                     dim3(WG_THREADS), WGW_LDS, st, g));
+    GR_LAUNCH_CHECK("gr_wgrad(partial, wide bf16)");
+    GR_TIMED("wgrad_reduce", st, hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks[0] + blocks[1]),
+                                                    dim3(256), 0, st, g, blocks[0]));
+    GR_LAUNCH_CHECK("gr_wgrad(reduce)");
+    return 0;
   }
   const int nt0 = pl.nt[0], nt1 = Ka[1] > 0 ? pl.nt[1] : 4;
   const size_t l0 = bf16 ? lds_of_bf16(nt0) : lds_of(nt0), l1 = bf16 ? lds_of_bf16(nt1) : lds_of(nt1);
@@ -590,7 +776,12 @@ extern "C" size_t gr_wgrad2_workspace_size(int64_t max_rows, int Ka0, int Nb0, i
   if (max_rows <= 0 || Ka0 <= 0 || Nb0 <= 0 || Ka1 < 0 || Nb1 < 0) return 0;
   const int ka[2] = {Ka0, Nb1 > 0 ? Ka1 : 0}, nb[2] = {Nb0, Ka1 > 0 ? Nb1 : 0};
   const WgPlan pl = wgrad_plan(max_rows, ka, nb);
-  return align256w(pl.slab_bytes[0]) + pl.slab_bytes[1];
+  size_t need = align256w(pl.slab_bytes[0]) + pl.slab_bytes[1];
+  if (std::max(ka[0], ka[1]) <= WGW_T) {  // the wide bf16 plan may split differently
+    const WgPlan pw = wgrad_plan_wide(max_rows, ka, nb);
+    need = std::max(need, align256w(pw.slab_bytes[0]) + pw.slab_bytes[1]);
+  }
+  return need;
 }
 
 extern "C" int gr_wgrad(const float* a, int64_t lda, const float* a_stats, const float* bm,
