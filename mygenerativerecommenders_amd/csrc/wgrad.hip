@@ -518,17 +518,137 @@ __device__ __forceinline__ void wgrad_tile_bf16w(const WgradProb& g, const int64
   }
 }
 
-// grid: XCD-aware, all tiles of one split on one XCD (A shared through its L2)
-__global__ __launch_bounds__(WG_THREADS) void wgrad_partial_bf16w_kernel(WgradArgs g) {
+// fp32 form of the same tile (gr_wgrad2 at wide heads): v_mfma_f32_32x32x2_f32 straight
+// from fp32 LDS tiles (A' with the LayerNorm applied, B), 16-row chunks; an A (B) fragment
+// is one float per lane: row 2 s + lane / 32, column lane % 32 of the tile.
+constexpr int WGF_CH = 16;
+constexpr size_t WGF_LDS = 2 * 2 * WGF_CH * WGW_T * 4;
+
+__device__ __forceinline__ f32x16 mfma32f(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ void wgrad_tile_f32w(const WgradProb& g, const int64_t* offsets, int B,
+                                                int64_t rows_per_split, int split, int tile,
+                                                char* smem) {
+  float* lds = reinterpret_cast<float*>(smem);  // [2 buffers][A, B][WGF_CH][256]
+  const int nb0 = tile * WGW_T;
+  const int64_t total = offsets[B];
+  const int64_t r0 = (int64_t)split * rows_per_split;
+  const int64_t r1 = min(total, r0 + rows_per_split);
+  const int tid = threadIdx.x, wv = wave_id(), lane = tid & 63;
+  const int n_ch = __builtin_amdgcn_readfirstlane(r1 > r0 ? (int)((r1 - r0 + WGF_CH - 1) / WGF_CH) : 0);
+  const int64_t nrows = r1 > r0 ? r1 - r0 : 0;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(g.a + r0 * g.lda), 0, nrows ? (int)(((nrows - 1) * g.lda + g.Ka) * 4) : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(g.bm + r0 * g.ldb), 0, nrows ? (int)(((nrows - 1) * g.ldb + g.Nb) * 4) : 0, 0x00020000);
+  // staging: thread t owns columns 4 (t % 64) .. +3 of rows t / 64 + 8 i (i < 2)
+  const int sc = 4 * (tid & 63), sr = tid >> 6;
+  const bool a_ok = sc < g.Ka, b_ok = nb0 + sc < g.Nb;
+  const int aoff = a_ok ? sc * 4 : 0x40000000, boff = b_ok ? (nb0 + sc) * 4 : 0x40000000;
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  f4v av[2], bv[2];
+  float2 stv[2];
+  auto load = [&](int ch) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int rr = WGF_CH * ch + sr + 8 * i;
+      av[i] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(ra, aoff + rr * (int)g.lda * 4, 0, 0));
+      bv[i] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rb, boff + rr * (int)g.ldb * 4, 0, 0));
+      stv[i] = g.a_stats ? ld_f2(g.a_stats, min(r0 + rr, total - 1)) : make_float2(0.f, 1.f);
+    }
+  };
+  const bool do_cs = g.NC > g.Nb && tile == 0;
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};
+  auto store = [&](int ch, int buf) {
+    float* At = lds + buf * 2 * WGF_CH * WGW_T;
+    float* Bt = At + WGF_CH * WGW_T;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int rr = sr + 8 * i;
+      const bool ok = r0 + WGF_CH * ch + rr < r1;
+      f4v x;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        x[e] = ok ? (av[i][e] - stv[i].x) * stv[i].y : 0.f;
+        if (do_cs) cs[e] += x[e];
+      }
+      *reinterpret_cast<f4v*>(At + rr * WGW_T + sc) = x;
+      *reinterpret_cast<f4v*>(Bt + rr * WGW_T + sc) = bv[i];  // rows past r1 meet a zero A
+    }
+  };
+  const int wka = 64 * (wv & 3), wnb = 128 * (wv >> 2);
+  const int lr = lane & 31, lh = lane >> 5;
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f16_zero();
+  if (n_ch > 0) {
+    load(0);
+    store(0, 0);
+  }
+  __syncthreads();
+  for (int ch = 0; ch < n_ch; ++ch) {
+    const bool more = ch + 1 < n_ch;
+    if (more) load(ch + 1);
+    const float* At = lds + (ch & 1) * 2 * WGF_CH * WGW_T + lh * WGW_T + lr;
+    const float* Bt = At + WGF_CH * WGW_T;
+#pragma unroll
+    for (int s = 0; s < WGF_CH / 2; ++s) {
+      float af[2], bf[4];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = At[2 * s * WGW_T + wka + 32 * i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bf[j] = Bt[2 * s * WGW_T + wnb + 32 * j];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma32f(af[i], bf[j], acc[i][j]);
+    }
+    if (more) store(ch + 1, (ch + 1) & 1);
+    __syncthreads();
+  }
+  float* slab = g.slabs + (int64_t)split * g.Ka * g.NC;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int rr = 0; rr < 16; ++rr) {
+      const int ka = wka + 32 * i + (rr & 3) + 8 * (rr >> 2) + 4 * lh;
+      if (ka >= g.Ka) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int nb = nb0 + wnb + 32 * j + lr;
+        if (nb < g.Nb) slab[(int64_t)ka * g.NC + nb] = acc[i][j][rr];
+      }
+    }
+  if (do_cs) {
+    float* xs = reinterpret_cast<float*>(smem);  // [8][256]
+#pragma unroll
+    for (int e = 0; e < 4; ++e) xs[sr * WGW_T + sc + e] = cs[e];
+    __syncthreads();
+    if (tid < WGW_T && tid < g.Ka) {
+      float t = 0.f;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) t += xs[r * WGW_T + tid];
+      slab[(int64_t)tid * g.NC + g.Nb] = t;
+    }
+  }
+}
+
+template <bool BF16>
+__global__ __launch_bounds__(WG_THREADS) void wgrad_partial_wide_kernel(WgradArgs g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int P = g.p[0].panels + g.p[1].panels;
   const int x = blockIdx.x & 7, sl = blockIdx.x >> 3;
   const int split = (sl / P) * 8 + x, tile = sl % P;
   if (split >= g.n_splits) return;
-  if (tile < g.p[0].panels)
-    wgrad_tile_bf16w(g.p[0], g.offsets, g.B, g.rows_per_split, split, tile, smem);
-  else
-    wgrad_tile_bf16w(g.p[1], g.offsets, g.B, g.rows_per_split, split, tile - g.p[0].panels, smem);
+  const bool second = tile >= g.p[0].panels;
+  const WgradProb& p = second ? g.p[1] : g.p[0];
+  const int t = second ? tile - g.p[0].panels : tile;
+  if (BF16) wgrad_tile_bf16w(p, g.offsets, g.B, g.rows_per_split, split, t, smem);
+  else wgrad_tile_f32w(p, g.offsets, g.B, g.rows_per_split, split, t, smem);
 }
 
 // out = sum over splits (fixed order): a workgroup owns 16 outputs of one problem; thread
@@ -698,7 +818,7 @@ static int wgrad_run(const WgradProb in[2], const int64_t* offsets, int B, int64
     }
     return 0;
   }
-  const bool wide = bf16 && wgrad_wide_ok(in);
+  const bool wide = wgrad_wide_ok(in);
   const WgPlan pl = wide ? wgrad_plan_wide(max_rows, Ka, Nb) : wgrad_plan(max_rows, Ka, Nb);
   const size_t need = align256w(pl.slab_bytes[0]) + pl.slab_bytes[1];
   GR_REQUIRE(workspace && ws_bytes >= need, "gr_wgrad: workspace %zu B < %zu B", ws_bytes, need);
@@ -723,9 +843,12 @@ static int wgrad_run(const WgradProb in[2], const int64_t* offsets, int B, int64
   }
   if (wide) {
     const int P = g.p[0].panels + g.p[1].panels;
-    GR_TIMED("wgrad_partial", st, hipLaunchKernelGGL(wgrad_partial_bf16w_kernel, dim3(ceil_div(pl.n_splits, 8) * 8 * P),
-                                                     dim3(WG_THREADS), WGW_LDS, st, g));
-    GR_LAUNCH_CHECK("gr_wgrad(partial, wide bf16)");
+    const dim3 grid(ceil_div(pl.n_splits, 8) * 8 * P);  // XCD groups, see wgrad_partial_wide_kernel
+    if (bf16)
+      GR_TIMED("wgrad_partial", st, hipLaunchKernelGGL(wgrad_partial_wide_kernel<true>, grid, dim3(WG_THREADS), WGW_LDS, st, g));
+    else
+      GR_TIMED("wgrad_partial", st, hipLaunchKernelGGL(wgrad_partial_wide_kernel<false>, grid, dim3(WG_THREADS), WGF_LDS, st, g));
+    GR_LAUNCH_CHECK("gr_wgrad(partial, wide)");
     GR_TIMED("wgrad_reduce", st, hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks[0] + blocks[1]),
                                                     dim3(256), 0, st, g, blocks[0]));
     GR_LAUNCH_CHECK("gr_wgrad(reduce)");
