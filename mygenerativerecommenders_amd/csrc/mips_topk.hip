@@ -1271,11 +1271,16 @@ __global__ __launch_bounds__(256) void mips_tau_kernel(TauArgs a) {
   block_radix_kth(key, a.G, m, L, kstar, k_rem);
   if (tid < NSUB) a.cnt[q * NSUB + tid] = 0;
   if (a.q_rows && tid < a.DP) a.q_rows[(int64_t)q * a.DP + tid] = tid < a.D ? a.q[(int64_t)q * a.D + tid] : 0.f;
+  // |q|^2 by wave 0 (lane-strided partial sums, fixed-order butterfly)
+  float ss = 0.f;
+  if (tid < 64) {
+    for (int d = tid; d < a.D; d += 64) ss = fmaf(a.q[(int64_t)q * a.D + d], a.q[(int64_t)q * a.D + d], ss);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) ss += __shfl_xor(ss, o, 64);
+  }
   if (tid == 0) {
     const float t = key_to_float(kstar);
     if (a.maxnorm) {
-      float ss = 0.f;
-      for (int d = 0; d < a.D; ++d) ss = fmaf(a.q[(int64_t)q * a.D + d], a.q[(int64_t)q * a.D + d], ss);
       const float qn = sqrtf(ss), xn = __uint_as_float(*a.maxnorm);
       const float dl = (BF16_C * qn * xn + 1e-35f * (qn + xn + 1.f)) * (1.f + 0.0009765625f);
       a.tau[q] = t - 2.f * dl;
