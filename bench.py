@@ -520,6 +520,8 @@ def main():
     ap.add_argument("--k", type=int, default=200)
     ap.add_argument("--retrieval-items", type=int, default=10_000_000)
     ap.add_argument("--retrieval-steps", type=int, default=20)
+    ap.add_argument("--retrieval-d256-items", type=int, default=10_000_000,
+                    help="C4 variant D = 256 (SURVEY §8d): catalog size, 0 = skip")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-retrieval-leg", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no HIP-graph capture of the step")
@@ -822,6 +824,61 @@ def main():
                              merge_avg_launch_ms=round(kmerge, 4), flops_per_launch=fl),
         }
 
+    # ---- C4 variant D = 256: the bf16 filter path beyond D = 64
+    retrieval_d256 = None
+    if not args.no_retrieval_leg and args.retrieval_d256_items > 0:
+        X2, D2 = args.retrieval_d256_items, 256
+        a2, b2 = shard_bounds(X2, world, rank)
+        g4 = torch.Generator(device=device)
+        g4.manual_seed(200 + rank)
+        shard2 = torch.randn(b2 - a2, D2, device=device, generator=g4)
+        shard2 = shard2 / shard2.norm(dim=-1, keepdim=True).clamp_min(1e-6)
+        g5 = torch.Generator(device=device)
+        g5.manual_seed(6)
+        Q2 = torch.randn(B, D2, device=device, generator=g5)
+        Q2 = Q2 / Q2.norm(dim=-1, keepdim=True)
+        inv2 = torch.randint(1, X2 + 1, (B, N), device=device, generator=g5)
+        sidx2 = ShardedCandidateIndex(args.k, torch.arange(a2 + 1, b2 + 1, device=device), shard2, a2)
+        for _ in range(3):
+            r_ids2, r_scores2 = sidx2.get_top_k_outputs(Q2, invalid_ids=inv2)
+        r_check2 = check_retrieval(Q2, shard2, a2, inv2, r_ids2, r_scores2, args.k, world)
+        del shard2
+        _sync_barrier(world)
+        t1 = time.perf_counter()
+        for _ in range(args.retrieval_steps):
+            sidx2.get_top_k_outputs(Q2, invalid_ids=inv2)
+        _sync_barrier(world)
+        dtr2 = _max_over_ranks(time.perf_counter() - t1, world)
+        _lib.timing_enable(True)
+        for _ in range(args.retrieval_steps):
+            hold(5.0)
+            sidx2.get_top_k_outputs(Q2, invalid_ids=inv2)
+        _sync_barrier(world)
+        _lib.timing_enable(False)
+        rt2 = _lib.kernel_times(("mips_sample", "mips_tau", "mips_filter", "mips_merge",
+                                 "mips_select", "mips_select_fallback", "mips_merge_fallback"))
+        kf = rt2["mips_filter"][0] / max(1, rt2["mips_filter"][1])
+        xs2 = b2 - a2
+        ach2 = xs2 * D2 * 2 / (kf * 1e-3) / 1e9 if kf else 0.0
+        retrieval_d256 = {
+            "metric": "top-k items scored/s", "unit": "items/s",
+            "value": B * X2 * args.retrieval_steps / dtr2,
+            "ms_per_query_batch": dtr2 / args.retrieval_steps * 1e3,
+            "config": {"workload": "C4 variant D = 256: %d-item catalog%s, B=%d, k=%d, %d invalid ids"
+                                   % (X2, " row-sharded over %d GPUs" % world if world > 1 else " on 1 GPU",
+                                      B, args.k, N),
+                       "items": X2, "dim": D2, "execution": "eager launches",
+                       "filter_scores": "bf16 (exact f32 rescoring)" if rt2["mips_filter"][1] else "f32 select"},
+            "check": r_check2,
+            "per_query_batch_device_ms": {n: round(v[0] / max(1, args.retrieval_steps), 4)
+                                          for n, v in rt2.items() if v[1]},
+            "roofline": {"kernel": "mips_filter", "bound": "hbm",
+                         "bound_basis": "bf16 table payload X*D*2 B, read once",
+                         "achieved": round(ach2, 1), "peak": peaks["hbm_gbs"], "unit": "GB/s",
+                         "frac": round(ach2 / peaks["hbm_gbs"], 4), "avg_launch_ms": round(kf, 4)},
+        }
+        del sidx2
+
     # ---- C2 batch sweep (encoder step alone) and the C3 leg
     sweep = None
     if args.sweep:
@@ -944,6 +1001,7 @@ def main():
             "c2_batch_sweep": sweep,
             "c3": c3,
             "c3_bf16": c3_bf16,
+            "retrieval_d256": retrieval_d256,
             "c2_bf16": c2_bf16,
             "e2e_train_step": e2e,
             "c5_train_step": c5_full,

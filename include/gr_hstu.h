@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GR_HSTU_ABI_VERSION 11
+#define GR_HSTU_ABI_VERSION 12
 
 #ifndef GR_API
 #define GR_API __attribute__((visibility("default")))
@@ -358,6 +358,25 @@ GR_API int hstu_gate_o_cat_bwd(const float* dy, int64_t ld_dy, const int64_t* of
                                float dropout_p, uint64_t seed, const int64_t* seed_offset,
                                float* du, int64_t ld_du, float* d_attn, int64_t ld_da,
                                void* stream);
+
+/* hstu_gate_o_cat_wide_fwd / _bwd: concat_ua at any width (the forms above need
+ * hdv <= 64, D <= 128): o_in (REQUIRED, (rows, 3 hdv), the GEMM operand) is built by an
+ * elementwise pass and y = o_in @ w_o^T + b_o + x_res streams the unpadded w_o (D, 3 hdv)
+ * through the row-panel GEMM.  Same dropout mask (hash of the o_in row and column).  The
+ * backward takes g: a (max_rows, 3 hdv) fp32 scratch for dy @ w_o. */
+GR_API int hstu_gate_o_cat_wide_fwd(const float* u, int64_t ld_u, const float* attn, int64_t ld_attn,
+                                    const int64_t* offsets, int B, int64_t max_rows, int hdv, int D,
+                                    const float* w_o, const float* b_o, const float* x_res,
+                                    int64_t ld_x, float eps, float dropout_p, uint64_t seed,
+                                    const int64_t* seed_offset, float* attn_stats, float* o_in,
+                                    float* y, int64_t ld_y, void* stream);
+GR_API int hstu_gate_o_cat_wide_bwd(const float* dy, int64_t ld_dy, const int64_t* offsets, int B,
+                                    int64_t max_rows, int hdv, int D, const float* w_o,
+                                    const float* u, int64_t ld_u, const float* attn, int64_t ld_attn,
+                                    const float* attn_stats, const float* h_u, int64_t ld_h,
+                                    float dropout_p, uint64_t seed, const int64_t* seed_offset,
+                                    float* g, float* du, int64_t ld_du, float* d_attn, int64_t ld_da,
+                                    void* stream);
 
 /* hstu_ln_uvqk_bwd  (backward of hstu_ln_uvqk_fwd w.r.t. x, plus the residual; D <= 256):
  *   dn = dh @ w_uvqk^T;  dx = dy_res + LayerNorm_backward(x; dn)   (dy_res may be NULL;

@@ -1137,3 +1137,219 @@ extern "C" int hstu_gate_o_cat_bwd(const float* dy, int64_t ld_dy, const int64_t
     default: return cat_bwd_kgh<4>(ra, hdv, kg, max_rows, st);
   }
 }
+
+// ------------------------------------------------------------------ concat_ua, any width
+// hstu.py:398-400 at widths the LDS-resident row-wave form cannot hold (h dv > 64 or
+// D > 128, e.g. C3): o_in = dropout([u, LN(attn), u * LN(attn)]) is materialised by an
+// elementwise pass (one wave per row), and the projection runs through the row-panel GEMM
+// with W_o streamed through LDS in k-chunks (no resident weight).  Backward: g = dy @ W_o
+// (dropout applied as it is stored) into a (rows, 3 hdv) scratch, then one wave per row
+// forms du and the LayerNorm backward of the attention branch.
+namespace gr {
+
+__global__ __launch_bounds__(256) void cat_oin_kernel(const float* u, int64_t ldu, const float* attn,
+                                                      int64_t lda, const int64_t* offsets, int B,
+                                                      int hv, float eps, float p, uint64_t seed,
+                                                      const int64_t* seed_off, float2* a_stats,
+                                                      float* o_in) {
+  const int64_t total = offsets[B];
+  const int64_t m = (int64_t)blockIdx.x * 4 + wave_id();
+  if (m >= total) return;
+  const int lane = threadIdx.x & 63;
+  gptr<float> arow = as_global(attn) + m * lda;
+  gptr<float> urow = as_global(u) + m * ldu;
+  float s = 0.f;
+  for (int c = lane; c < hv; c += 64) s += arow[c];
+  const float mean = wave_sum(s) / (float)hv;
+  float q = 0.f;
+  for (int c = lane; c < hv; c += 64) {
+    const float d = arow[c] - mean;
+    q += d * d;
+  }
+  const float rstd = rsqrtf(wave_sum(q) / (float)hv + eps);
+  if (lane == 0) a_stats[m] = make_float2(mean, rstd);
+  const uint64_t se = seed + (seed_off ? (uint64_t)*seed_off : 0ull);
+  float* orow = o_in + m * 3 * hv;
+  for (int c = lane; c < hv; c += 64) {
+    const float uv = urow[c], ln = (arow[c] - mean) * rstd;
+    float v0 = uv, v1 = ln, v2 = uv * ln;
+    if (p > 0.f) {
+      v0 *= dropout_keep(se, m, c, 3 * hv, p);
+      v1 *= dropout_keep(se, m, hv + c, 3 * hv, p);
+      v2 *= dropout_keep(se, m, 2 * hv + c, 3 * hv, p);
+    }
+    orow[c] = v0;
+    orow[hv + c] = v1;
+    orow[2 * hv + c] = v2;
+  }
+}
+
+// y = o_in @ W_o^T + b_o + x_res   (K = 3 hdv, N = D; W_o row-major (D, K))
+struct OpLinRes : NoStats {
+  static constexpr bool B_N_CONTIG = false;
+  const int64_t* offsets;
+  int B, K, N;
+  const float* a;
+  int64_t lda;
+  const float* w;
+  const float* bias;
+  const float* xres;
+  int64_t ldx;
+  float* y;
+  int64_t ldy;
+  static constexpr int NSRC = 1;
+  __device__ __amdgpu_buffer_rsrc_t a_rsrc0(int64_t m0, int64_t t) const { return rows_rsrc(a, lda, m0, t); }
+  __device__ __amdgpu_buffer_rsrc_t a_rsrc1(int64_t m0, int64_t t) const { return rows_rsrc(a, lda, m0, t); }
+  __device__ int64_t a_ld0() const { return lda; }
+  __device__ int64_t a_ld1() const { return lda; }
+  __device__ float a_xform(float v, float, int64_t, int, float2, bool) const { return v; }
+  __device__ int bks() const { return 1; }
+  __device__ int bns() const { return K; }
+  template <int NT>
+  struct Epi {};
+  template <int NT>
+  __device__ void epi_load(Epi<NT>&, int64_t, int, int64_t) const {}
+  template <int NT>
+  __device__ void epilogue(f4 (&acc)[NT], const Epi<NT>&, int64_t mrow, int ncol, int64_t total) const {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t m = mrow + r;
+      if (m >= total) continue;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int n = ncol + 16 * t;
+        if (n >= N) continue;
+        const float bv = bias ? as_global(bias)[n] : 0.f;
+        const float xv = xres ? as_global(xres)[m * ldx + n] : 0.f;
+        y[m * ldy + n] = (acc[t][r] + bv) + xv;
+      }
+    }
+  }
+};
+
+// g = (dy @ W_o) * dropout mask   (K = D, N = 3 hdv; W_o row-major (D, N))
+struct OpCatG : NoStats {
+  static constexpr bool B_N_CONTIG = true;
+  const int64_t* offsets;
+  int B, K, N;
+  const float* dy;
+  int64_t lddy;
+  const float* w;
+  float p;
+  uint64_t seed;
+  const int64_t* seed_off;
+  float* g;
+  static constexpr int NSRC = 1;
+  __device__ __amdgpu_buffer_rsrc_t a_rsrc0(int64_t m0, int64_t t) const { return rows_rsrc(dy, lddy, m0, t); }
+  __device__ __amdgpu_buffer_rsrc_t a_rsrc1(int64_t m0, int64_t t) const { return rows_rsrc(dy, lddy, m0, t); }
+  __device__ int64_t a_ld0() const { return lddy; }
+  __device__ int64_t a_ld1() const { return lddy; }
+  __device__ float a_xform(float v, float, int64_t, int, float2, bool) const { return v; }
+  __device__ int bks() const { return N; }
+  __device__ int bns() const { return 1; }
+  template <int NT>
+  struct Epi {};
+  template <int NT>
+  __device__ void epi_load(Epi<NT>&, int64_t, int, int64_t) const {}
+  template <int NT>
+  __device__ void epilogue(f4 (&acc)[NT], const Epi<NT>&, int64_t mrow, int ncol, int64_t total) const {
+    const uint64_t se = seed + (seed_off ? (uint64_t)*seed_off : 0ull);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t m = mrow + r;
+      if (m >= total) continue;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int n = ncol + 16 * t;
+        if (n >= N) continue;
+        g[m * N + n] = p > 0.f ? acc[t][r] * dropout_keep(se, m, n, N, p) : acc[t][r];
+      }
+    }
+  }
+};
+
+// du = (g0 + g2 LN(a)) (* silu'(h_u)),  d_attn = LayerNorm_bwd(a; g1 + g2 u)
+__global__ __launch_bounds__(256) void cat_bwd_rows_kernel(const float* g, const float* u, int64_t ldu,
+                                                           const float* attn, int64_t lda,
+                                                           const float2* a_stats, const float* h_u,
+                                                           int64_t ldh, const int64_t* offsets, int B,
+                                                           int hv, float* du, int64_t lddu, float* da,
+                                                           int64_t ldda) {
+  const int64_t total = offsets[B];
+  const int64_t m = (int64_t)blockIdx.x * 4 + wave_id();
+  if (m >= total) return;
+  const int lane = threadIdx.x & 63;
+  const float2 st = ld_f2(a_stats, m);
+  gptr<float> grow = as_global(g) + m * 3 * hv;
+  float s1 = 0.f, s2 = 0.f;
+  for (int c = lane; c < hv; c += 64) {
+    const float ln = (as_global(attn)[m * lda + c] - st.x) * st.y;
+    const float uv = as_global(u)[m * ldu + c];
+    const float g0 = grow[c], g1 = grow[hv + c], g2 = grow[2 * hv + c];
+    float d = g0 + g2 * ln;
+    if (h_u) d *= silu_grad_(as_global(h_u)[m * ldh + c]);
+    du[m * lddu + c] = d;
+    const float dln = g1 + g2 * uv;
+    s1 += dln;
+    s2 += dln * ln;
+  }
+  const float mean1 = wave_sum(s1) / (float)hv, mean2 = wave_sum(s2) / (float)hv;
+  for (int c = lane; c < hv; c += 64) {
+    const float ln = (as_global(attn)[m * lda + c] - st.x) * st.y;
+    const float uv = as_global(u)[m * ldu + c];
+    const float dln = grow[hv + c] + grow[2 * hv + c] * uv;
+    da[m * ldda + c] = st.y * (dln - mean1 - ln * mean2);
+  }
+}
+
+}  // namespace gr
+
+extern "C" int hstu_gate_o_cat_wide_fwd(const float* u, int64_t ld_u, const float* attn, int64_t ld_attn,
+                                        const int64_t* offsets, int B, int64_t max_rows, int hdv, int D,
+                                        const float* w_o, const float* b_o, const float* x_res,
+                                        int64_t ld_x, float eps, float dropout_p, uint64_t seed,
+                                        const int64_t* seed_offset, float* attn_stats, float* o_in,
+                                        float* y, int64_t ld_y, void* stream) {
+  using namespace gr;
+  GR_REQUIRE(u && attn && offsets && w_o && o_in && y && attn_stats,
+             "hstu_gate_o_cat_wide_fwd: null pointer (o_in is required: the GEMM operand)");
+  GR_REQUIRE(hdv > 0 && D > 0 && B >= 0 && max_rows >= 0, "hstu_gate_o_cat_wide_fwd: bad sizes");
+  GR_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f, "hstu_gate_o_cat_wide_fwd: dropout_p %f", dropout_p);
+  if (max_rows == 0 || B == 0) return 0;
+  const hipStream_t st = (hipStream_t)stream;
+  GR_TIMED("gate_o_fwd", st, hipLaunchKernelGGL(cat_oin_kernel, dim3((unsigned)((max_rows + 3) / 4)), dim3(256), 0, st,
+                                                u, ld_u, attn, ld_attn, offsets, B, hdv, eps, dropout_p, seed,
+                                                seed_offset, (float2*)attn_stats, o_in));
+  GR_LAUNCH_CHECK("hstu_gate_o_cat_wide_fwd(o_in)");
+  OpLinRes op{};
+  op.offsets = offsets; op.B = B; op.K = 3 * hdv; op.N = D;
+  op.a = o_in; op.lda = 3 * hdv; op.w = w_o; op.bias = b_o; op.xres = x_res; op.ldx = ld_x;
+  op.y = y; op.ldy = ld_y;
+  return launch_rowpanel(op, max_rows, false, "hstu_gate_o_fwd", st);
+}
+
+extern "C" int hstu_gate_o_cat_wide_bwd(const float* dy, int64_t ld_dy, const int64_t* offsets, int B,
+                                        int64_t max_rows, int hdv, int D, const float* w_o,
+                                        const float* u, int64_t ld_u, const float* attn, int64_t ld_attn,
+                                        const float* attn_stats, const float* h_u, int64_t ld_h,
+                                        float dropout_p, uint64_t seed, const int64_t* seed_offset,
+                                        float* g, float* du, int64_t ld_du, float* d_attn, int64_t ld_da,
+                                        void* stream) {
+  using namespace gr;
+  GR_REQUIRE(dy && offsets && w_o && u && attn && attn_stats && g && du && d_attn,
+             "hstu_gate_o_cat_wide_bwd: null pointer");
+  GR_REQUIRE(hdv > 0 && D > 0 && B >= 0 && max_rows >= 0, "hstu_gate_o_cat_wide_bwd: bad sizes");
+  if (max_rows == 0 || B == 0) return 0;
+  const hipStream_t st = (hipStream_t)stream;
+  OpCatG op{};
+  op.offsets = offsets; op.B = B; op.K = D; op.N = 3 * hdv;
+  op.dy = dy; op.lddy = ld_dy; op.w = w_o; op.p = dropout_p; op.seed = seed; op.seed_off = seed_offset;
+  op.g = g;
+  const int rc = launch_rowpanel(op, max_rows, false, "hstu_gate_o_bwd", st);
+  if (rc) return rc;
+  GR_TIMED("gate_o_bwd", st, hipLaunchKernelGGL(cat_bwd_rows_kernel, dim3((unsigned)((max_rows + 3) / 4)), dim3(256), 0, st,
+                                                g, u, ld_u, attn, ld_attn, (const float2*)attn_stats, h_u, ld_h,
+                                                offsets, B, hdv, du, ld_du, d_attn, ld_da));
+  GR_LAUNCH_CHECK("hstu_gate_o_cat_wide_bwd(rows)");
+  return 0;
+}

@@ -162,24 +162,37 @@ __global__ void pack_rows_kernel(const float* items, int64_t X, int D, int DP, f
   }
 }
 
-// max_i ||x_i||_2 as fp32 bits (non-negative floats order like their bit patterns);
-// *maxbits is zeroed beforehand.  NaN rows push it to NaN-like bits, which disables
-// the filter (its thresholds compare false) and routes the batch to the exact path.
+__device__ __forceinline__ float bf16_round(float f) { return __uint_as_float(bf16_bits(f) << 16); }
+
+// The filter's error-bound inputs, as fp32 bits (non-negative floats order like their bit
+// patterns; both words zeroed beforehand):
+//   maxbits[0] = max_i ||bf16(x_i)||_2,   maxbits[1] = max_i ||bf16(x_i) - x_i||_2.
+// NaN / inf rows push them to NaN-like bits, which disables the filter (its thresholds
+// compare false) and routes the batch to the exact path.
 __global__ __launch_bounds__(256) void item_norm_max_kernel(const float* items, int64_t X, int D,
                                                             uint32_t* maxbits) {
-  uint32_t m = 0;
+  uint32_t m = 0, me = 0;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < X; i += (int64_t)gridDim.x * 256) {
-    float ss = 0.f;
-    for (int d = 0; d < D; ++d) ss = fmaf(items[i * D + d], items[i * D + d], ss);
-    const uint32_t b = __float_as_uint(sqrtf(ss));
+    float ss = 0.f, se = 0.f;
+    for (int d = 0; d < D; ++d) {
+      const float v = items[i * D + d], r = bf16_round(v), e = r - v;
+      ss = fmaf(r, r, ss);
+      se = fmaf(e, e, se);
+    }
+    const uint32_t b = __float_as_uint(sqrtf(ss)), be = __float_as_uint(sqrtf(se));
     m = b > m ? b : m;
+    me = be > me ? be : me;
   }
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) {
-    const uint32_t v = __shfl_xor(m, o, 64);
+    const uint32_t v = __shfl_xor(m, o, 64), ve = __shfl_xor(me, o, 64);
     m = v > m ? v : m;
+    me = ve > me ? ve : me;
   }
-  if ((threadIdx.x & 63) == 0 && m) atomicMax(maxbits, m);
+  if ((threadIdx.x & 63) == 0) {
+    if (m) atomicMax(maxbits, m);
+    if (me) atomicMax(maxbits + 1, me);
+  }
 }
 
 // ----------------------------------------------------------------- packing
@@ -1129,7 +1142,7 @@ __global__ __launch_bounds__(256) void mips_filter_kernel(FilterArgs a) {
   if (SAMPLE && b0 < b1) {
     // a few sample blocks per wave at a 16-block stride: issue a chunk's loads
     // together, then score them (duplicated clamped blocks leave the max unchanged)
-    constexpr int CH = 4;
+    constexpr int CH = KC <= 2 ? 4 : 2;
     for (int64_t ib = b0; ib < b1; ib += CH * bstride) {
       Frag f[CH];
 #pragma unroll
@@ -1143,7 +1156,7 @@ __global__ __launch_bounds__(256) void mips_filter_kernel(FilterArgs a) {
   } else if (!SAMPLE && b0 < b1 && BF) {
     // bf16 blocks are 1-2 KB of HBM per ~16 MFMAs: keep PD blocks in flight per wave
     // (a slot is refilled PD blocks ahead as soon as it is consumed)
-    constexpr int PD = 4;
+    constexpr int PD = KC <= 2 ? 4 : 2;
     Frag f[PD];
     // issue order f[0], f[1], ... pinned (sched_barrier): the loop's waits count loads in
     // that order, and a reordered prologue made hipcc drain vmcnt(0) every iteration
@@ -1193,20 +1206,23 @@ __global__ __launch_bounds__(256) void mips_filter_kernel(FilterArgs a) {
                          (int64_t)l_i[src] * (a.DP >> 2);
           gptr<fv4> qr = as_global(reinterpret_cast<const fv4*>(a.q_rows)) +
                          (int64_t)qq * (a.DP >> 2);
-          fv4 xv[16], qv[16];
-#pragma unroll
-          for (int j = 0; j < 16; ++j)
-            if (4 * j < a.DP) {
-              xv[j] = xr[j];
-              qv[j] = qr[j];
-            }
           sc = 0.f;
+          for (int j0 = 0; j0 < a.DP; j0 += 64) {  // 64 dims per round (D <= 256: <= 4)
+            fv4 xv[16], qv[16];
 #pragma unroll
-          for (int j = 0; j < 16; ++j) {
-            if (4 * j < a.D) sc = fmaf(xv[j].x, qv[j].x, sc);
-            if (4 * j + 1 < a.D) sc = fmaf(xv[j].y, qv[j].y, sc);
-            if (4 * j + 2 < a.D) sc = fmaf(xv[j].z, qv[j].z, sc);
-            if (4 * j + 3 < a.D) sc = fmaf(xv[j].w, qv[j].w, sc);
+            for (int j = 0; j < 16; ++j)
+              if (j0 + 4 * j < a.DP) {
+                xv[j] = xr[(j0 >> 2) + j];
+                qv[j] = qr[(j0 >> 2) + j];
+              }
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+              const int d = j0 + 4 * j;
+              if (d < a.D) sc = fmaf(xv[j].x, qv[j].x, sc);
+              if (d + 1 < a.D) sc = fmaf(xv[j].y, qv[j].y, sc);
+              if (d + 2 < a.D) sc = fmaf(xv[j].z, qv[j].z, sc);
+              if (d + 3 < a.D) sc = fmaf(xv[j].w, qv[j].w, sc);
+            }
           }
         }
         const int64_t sub = (int64_t)qq * NSUB + (blockIdx.x & (NSUB - 1));
@@ -1230,20 +1246,25 @@ __global__ __launch_bounds__(256) void mips_filter_kernel(FilterArgs a) {
   }
 }
 
-// Error bound of a bf16 filter score s~ against the exact f32 score s of the same pair:
-// each product q_d x_d carries two bf16 roundings (<= (2^-7 + 2^-16) |q_d x_d|) and the
-// f32 accumulation of <= 64 terms adds <= 2^-18 sum|q_d x_d|, and
-// sum|q_d x_d| <= ||q|| ||x|| (Cauchy-Schwarz), so
-//   |s~ - s| <= delta_q = BF16_C ||q|| max_i ||x_i||  (+ a denormal-flush allowance).
-// BF16_C = 2^-7 + 2^-12 keeps a margin for the fp32 evaluation of the norms.
-constexpr float BF16_C = 0.0078125f + 0.000244140625f;
-
+// Error bound of a bf16 filter score s~ against the exact f32 score s of the same pair,
+// with q~ = bf16(q), x~ = bf16(x) (round to nearest even, as the filter converts them):
+//   s~ - s = sum (q~_d x~_d - q_d x_d) + (f32 accumulation error)
+//          = (q~ - q).x~ + q.(x~ - x) + acc,
+//   |(q~ - q).x~| <= ||q~ - q|| max_i ||x~_i||,   |q.(x~ - x)| <= ||q|| max_i ||x~_i - x_i||
+// (Cauchy-Schwarz), and |acc| <= gamma_D sum|q~_d x~_d| <= 2^-15 ||q~|| max_i ||x~_i||
+// (bf16 products are exact in f32; D <= 256 additions).  So
+//   |s~ - s| <= delta_q = ||q~ - q|| XN + ||q|| EX + 2^-15 ||q~|| XN  (+ a denormal-flush
+// allowance), XN / EX from item_norm_max_kernel, the query terms measured here.  The
+// rounding error norms are what bf16 actually did (about 2^-9.2 of the norm for random
+// data) rather than the worst case 2^-8 per factor, so delta_q is about 2.2x smaller
+// than ||q|| max ||x|| (2^-7 + 2^-16): fewer candidates, and none of the sub-list
+// overflows at D = 256 that the worst-case bound caused.
 struct TauArgs {
   const float* smax;
   int G;
   const float* q;          // bf16 filter: the f32 queries (for ||q||)
   int D;
-  const uint32_t* maxnorm; // bf16 filter: max item norm bits; null = exact f32 filter scores
+  const uint32_t* maxnorm; // bf16 filter: {XN, EX} bits (item_norm_max_kernel); null = exact f32 scores
   float* tau;              // filter threshold
   float* tau_e;            // exactness threshold of the rescored candidates
   int* cnt;
@@ -1271,18 +1292,31 @@ __global__ __launch_bounds__(256) void mips_tau_kernel(TauArgs a) {
   block_radix_kth(key, a.G, m, L, kstar, k_rem);
   if (tid < NSUB) a.cnt[q * NSUB + tid] = 0;
   if (a.q_rows && tid < a.DP) a.q_rows[(int64_t)q * a.DP + tid] = tid < a.D ? a.q[(int64_t)q * a.D + tid] : 0.f;
-  // |q|^2 by wave 0 (lane-strided partial sums, fixed-order butterfly)
-  float ss = 0.f;
+  // ||q||^2, ||q~||^2, ||q~ - q||^2 by wave 0 (lane-strided partial sums, fixed-order
+  // butterfly)
+  float ss = 0.f, sr = 0.f, se = 0.f;
   if (tid < 64) {
-    for (int d = tid; d < a.D; d += 64) ss = fmaf(a.q[(int64_t)q * a.D + d], a.q[(int64_t)q * a.D + d], ss);
+    for (int d = tid; d < a.D; d += 64) {
+      const float v = a.q[(int64_t)q * a.D + d], r = bf16_round(v), e = r - v;
+      ss = fmaf(v, v, ss);
+      sr = fmaf(r, r, sr);
+      se = fmaf(e, e, se);
+    }
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) ss += __shfl_xor(ss, o, 64);
+    for (int o = 32; o >= 1; o >>= 1) {
+      ss += __shfl_xor(ss, o, 64);
+      sr += __shfl_xor(sr, o, 64);
+      se += __shfl_xor(se, o, 64);
+    }
   }
   if (tid == 0) {
     const float t = key_to_float(kstar);
     if (a.maxnorm) {
-      const float qn = sqrtf(ss), xn = __uint_as_float(*a.maxnorm);
-      const float dl = (BF16_C * qn * xn + 1e-35f * (qn + xn + 1.f)) * (1.f + 0.0009765625f);
+      const float qn = sqrtf(ss), qrn = sqrtf(sr), qen = sqrtf(se);
+      const float xn = __uint_as_float(a.maxnorm[0]), xen = __uint_as_float(a.maxnorm[1]);
+      // (1 + 2^-10) covers the f32 evaluation of the norms and of this sum
+      const float dl = (qen * xn + qn * xen + 0.000030517578125f * qrn * xn +
+                        1e-35f * (qn + xn + 1.f)) * (1.f + 0.0009765625f);
       a.tau[q] = t - 2.f * dl;
       a.tau_e[q] = a.tau[q] + dl;
     } else {
@@ -1642,7 +1676,7 @@ static PackLayout pack_layout(int64_t X, int D) {
   const int64_t nblk = (X + 15) / 16;
   const size_t f32 = sizeof(float) * (size_t)nblk * ((ceil_div(D, 4) + 1) / 2) * 128;
   L.total = f32;
-  L.bf16 = X >= FILTER_MIN_X && ceil_div(D, 4) <= 16;
+  L.bf16 = X >= FILTER_MIN_X && ceil_div(D, 4) <= 64;  // D <= 256: KC <= 8 k-chunks
   if (L.bf16) {
     L.KC = ceil_div(D, 32);
     L.off16 = align256(f32);
@@ -1681,7 +1715,10 @@ static TopkPlan plan_topk(int B, int64_t X, int D, int k, int N0) {
     const size_t sb = (size_t)B * X * (sizeof(float) + sizeof(int64_t));
     if (sb > p.part_bytes) p.part_bytes = sb;
   }
-  p.filter = !p.small && X >= FILTER_MIN_X && p.KS <= 16;
+  // the f32 filter holds every query fragment in registers (D <= 64); the bf16 filter runs
+  // to D = 256 with fewer queries per workgroup beyond D = 64
+  const int kc_bf = option(GR_OPT_MIPS_FILTER_FP32) ? 0 : pack_layout(X, D).KC;
+  p.filter = !p.small && X >= FILTER_MIN_X && (p.KS <= 16 || kc_bf > 0);
   p.total_bytes = p.part_bytes;
   p.off_part = 0;
   if (p.filter) {
@@ -1692,12 +1729,12 @@ static TopkPlan plan_topk(int B, int64_t X, int D, int k, int N0) {
     const int64_t n_sb = (p.n_blocks + p.sr - 1) / p.sr;
     p.GB = (int)((n_sb + SAMPLE_GROUPS - 1) / SAMPLE_GROUPS);
     p.G = (int)((n_sb + p.GB - 1) / p.GB);
-    p.NQG = B <= 32 ? 2 : 8;
+    p.NQG = B <= 32 ? 2 : (kc_bf > 2 ? 4 : 8);
     p.n_chunks = ceil_div(B, p.NQG * 16);
     // whole rounds of 2 four-wave workgroups per CU, >= ~48 blocks per wave
     const int64_t per_round = (int64_t)device_cus() * 4 * option(GR_OPT_MIPS_FILTER_WGS);
     // GR_OPT_MIPS_FILTER_FP32: filter on the f32 table (exact scores, 16x fewer flop/s)
-    p.KC = option(GR_OPT_MIPS_FILTER_FP32) ? 0 : pack_layout(X, D).KC;
+    p.KC = kc_bf;
     // f32: >= ~48 blocks per wave.  bf16 (streaming-bound): one round (10M items: 7
     // rounds 302 us, 2 rounds 253 us, 1 round 251 us)
     const int64_t min_rb = p.KC ? 4096 : 48;
@@ -1709,7 +1746,7 @@ static TopkPlan plan_topk(int B, int64_t X, int D, int k, int N0) {
     size_t o = 256;  // [0, 4): fallback flag
     p.off_tau = o;  o = align256(o + sizeof(float) * B);
     p.off_tau_e = o; o = align256(o + sizeof(float) * B);
-    p.off_qrows = o; o = align256(o + sizeof(float) * B * 64);  // bf16 filter: padded f32 queries
+    p.off_qrows = o; o = align256(o + sizeof(float) * B * 4 * p.KS);  // bf16 filter: padded f32 queries
     p.off_cnt = o;  o = align256(o + sizeof(int) * B * NSUB);
     p.off_smax = o; o = align256(o + sizeof(float) * (size_t)B * p.G);
     p.off_cs = o;   o = align256(o + sizeof(float) * (size_t)B * FILTER_CAP);
@@ -1754,13 +1791,26 @@ static int launch_filter_pair(const FilterArgs& f, const TopkPlan& p, bool sampl
 
 template <int KS, int KC>
 static int launch_filter_ks(const FilterArgs& f, const TopkPlan& p, bool sample, hipStream_t st) {
-  return p.NQG == 2 ? launch_filter_pair<KS, KC, 2>(f, p, sample, st)
-                    : launch_filter_pair<KS, KC, 8>(f, p, sample, st);
+  if constexpr (KC > 2)  // D > 64: 2 or 4 query tiles per workgroup (register budget)
+    return p.NQG == 2 ? launch_filter_pair<KS, KC, 2>(f, p, sample, st)
+                      : launch_filter_pair<KS, KC, 4>(f, p, sample, st);
+  else
+    return p.NQG == 2 ? launch_filter_pair<KS, KC, 2>(f, p, sample, st)
+                      : launch_filter_pair<KS, KC, 8>(f, p, sample, st);
 }
 
 static int launch_filter(const FilterArgs& f, const TopkPlan& p, bool sample, hipStream_t st) {
-  if (p.KC == 1) return launch_filter_ks<1, 1>(f, p, sample, st);
-  if (p.KC == 2) return launch_filter_ks<1, 2>(f, p, sample, st);
+  switch (p.KC) {
+    case 1: return launch_filter_ks<1, 1>(f, p, sample, st);
+    case 2: return launch_filter_ks<1, 2>(f, p, sample, st);
+    case 3: return launch_filter_ks<1, 3>(f, p, sample, st);
+    case 4: return launch_filter_ks<1, 4>(f, p, sample, st);
+    case 5: return launch_filter_ks<1, 5>(f, p, sample, st);
+    case 6: return launch_filter_ks<1, 6>(f, p, sample, st);
+    case 7: return launch_filter_ks<1, 7>(f, p, sample, st);
+    case 8: return launch_filter_ks<1, 8>(f, p, sample, st);
+    default: break;
+  }
   switch (p.KS) {
     case 1: case 2: return launch_filter_ks<2, 0>(f, p, sample, st);
     case 3: case 4: return launch_filter_ks<4, 0>(f, p, sample, st);
@@ -1803,7 +1853,7 @@ extern "C" int mips_pack_items(const float* items, int64_t X, int D, float* pack
       uint32_t* maxbits = (uint32_t*)(base + L.off_norm);
       hipLaunchKernelGGL(pack_bf16_kernel, dim3(2048), dim3(256), 0, st, items, X, D, L.KC,
                          (u32x4*)(base + L.off16));
-      zero_words_async(maxbits, 1, st);
+      zero_words_async(maxbits, 2, st);
       hipLaunchKernelGGL(item_norm_max_kernel, dim3(2048), dim3(256), 0, st, items, X, D, maxbits);
       hipLaunchKernelGGL(pack_rows_kernel, dim3(2048), dim3(256), 0, st, items, X, D, L.DP,
                          (float*)(base + L.off_rows));

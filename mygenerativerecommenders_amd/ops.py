@@ -225,6 +225,12 @@ class STUGeometry:
         return 2 * self.H * self.dv + 2 * self.H * self.dqk
 
 
+def _cat_wide(hv: int, D: int) -> bool:
+    """concat_ua beyond the LDS-resident row-wave form (hdv <= 64, D <= 128): o_in
+    materialised and W_o streamed (hstu_gate_o_cat_wide_fwd / _bwd)."""
+    return hv > 64 or D > 128
+
+
 def _pad_cat_weight(w_o: torch.Tensor, hv: int):
     """concat_ua: _o.weight (D, 3 hv) -> (D, 3 hvp) with the u / LN(a) / u*LN(a) column
     blocks at 16-aligned offsets 0, hvp, 2 hvp (the row-wave kernel's k groups)."""
@@ -293,13 +299,23 @@ class STULayerFunction(torch.autograd.Function):
         attn_stats = torch.empty(rows, 2, dtype=torch.float32, device=dev)
         needs_w_grad = grad_on and (w_o.requires_grad or b_o.requires_grad)
         ow = 3 * hv if geo.concat_ua else hv  # o_in width
-        o_in = torch.empty(rows, ow, dtype=torch.float32, device=dev) if needs_w_grad else None
+        cat_wide = geo.concat_ua and _cat_wide(hv, D)
+        o_in = (torch.empty(rows, ow, dtype=torch.float32, device=dev)
+                if needs_w_grad or cat_wide else None)
         w_pad = hvp = None
-        if geo.concat_ua:
+        if geo.concat_ua and not cat_wide:
             w_pad, hvp = _pad_cat_weight(w_o, hv)
         y = torch.empty(rows, D, dtype=torch.float32, device=dev)
         b_o_c = b_o.contiguous()
-        if geo.concat_ua:
+        if cat_wide:
+            _lib.call("hstu_gate_o_cat_wide_fwd", uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
+                      offsets.data_ptr(), B, rows, hv, D, w_o.data_ptr(), b_o_c.data_ptr(),
+                      x.data_ptr(), x.stride(0), geo.eps, geo.dropout_p, seed,
+                      _lib.ptr(seed_offset), attn_stats.data_ptr(), o_in.data_ptr(), y.data_ptr(),
+                      D, st)
+            if not needs_w_grad:
+                o_in = None
+        elif geo.concat_ua:
             _lib.call("hstu_gate_o_cat_fwd", uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
                       offsets.data_ptr(), B, rows, hv, hvp, D, w_pad.data_ptr(), b_o_c.data_ptr(),
                       x.data_ptr(), x.stride(0), geo.eps, geo.dropout_p, seed,
@@ -333,7 +349,15 @@ class STULayerFunction(torch.autograd.Function):
         dy = dy.contiguous()
         d_uvqk = torch.empty(rows, n_out, dtype=torch.float32, device=dev)
         d_attn = torch.empty(rows, hv, dtype=torch.float32, device=dev)
-        if geo.concat_ua:
+        if geo.concat_ua and _cat_wide(hv, D):
+            g_cat = torch.empty(rows, 3 * hv, dtype=torch.float32, device=dev)
+            _lib.call("hstu_gate_o_cat_wide_bwd", dy.data_ptr(), D, offsets.data_ptr(), B, rows, hv,
+                      D, w_o.data_ptr(), uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
+                      attn_stats.data_ptr(), _lib.ptr(h_pre), n_out, geo.dropout_p, ctx.seed,
+                      _lib.ptr(ctx.seed_offset), g_cat.data_ptr(), d_uvqk.data_ptr(), n_out,
+                      d_attn.data_ptr(), hv, st)
+            del g_cat
+        elif geo.concat_ua:
             w_pad, hvp = _pad_cat_weight(w_o, hv)
             _lib.call("hstu_gate_o_cat_bwd", dy.data_ptr(), D, offsets.data_ptr(), B, rows, hv, hvp,
                       D, w_pad.data_ptr(), uvqk.data_ptr(), n_out, attn.data_ptr(), hv,

@@ -93,7 +93,10 @@ def test_workspace_size_queries_are_host_only():
                                                 + al(4 * X * 52))
     assert L.mips_packed_items_bytes(X, 64) == (al(4 * nblk * 8 * 128) + al(nblk * 2048) + 256
                                                 + al(4 * X * 64))
-    assert L.mips_packed_items_bytes(X, 65) == 4 * nblk * 9 * 128  # D > 64: no filter copy
+    # D = 65: three k-chunks, the last with one stored lane group (2,304 B per 16 items)
+    assert L.mips_packed_items_bytes(X, 65) == (al(4 * nblk * 9 * 128) + al(nblk * 2304) + 256
+                                                + al(4 * X * 68))
+    assert L.mips_packed_items_bytes(X, 257) == 4 * nblk * 33 * 128  # D > 256: no filter copy
     assert L.gr_wgrad_workspace_size(27008, 50, 200) > 0
     assert L.mips_topk_workspace_size(128, 10_000_000, 50, 200, 211) > 0
     assert L.mips_topk_workspace_size(128, 27_278, 50, 200, 2059) > L.mips_topk_workspace_size(128, 27_278, 50, 200, 211)

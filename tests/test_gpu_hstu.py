@@ -221,7 +221,8 @@ def test_hstu_bf16_mode_vs_oracle(B, N0, out_len, D, blocks, min_len):
         assert e <= 5e-2, pname
 
 
-@pytest.mark.parametrize("D,dh,H", [(50, 50, 1), (32, 16, 2), (64, 64, 1)])
+@pytest.mark.parametrize("D,dh,H", [(50, 50, 1), (32, 16, 2), (64, 64, 1),
+                                    (256, 256, 1), (192, 48, 2), (160, 40, 1)])
 def test_hstu_concat_ua_vs_oracle(D, dh, H):
     """concat_ua=True at ml-1m-like widths (ragged lengths, relative bias) against the
     oracle (fp32 tolerances as above)."""

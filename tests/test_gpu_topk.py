@@ -213,6 +213,19 @@ def test_mips_filter_bf16_layouts_bitexact(D):
     _check_filter(Q, E, np.arange(1, X + 1, dtype=np.int64), inv, k, expect_flag=0)
 
 
+@pytest.mark.parametrize("D,B,X", [(256, 32, 1_000_000), (256, 128, 1_000_000), (256, 64, 300_001),
+                                   (96, 40, 262_144 + 77), (130, 24, 300_001)])
+def test_mips_filter_wide_d_bitexact(D, B, X):
+    """The bf16 filter beyond D = 64 (k-chunks of 32 dims, 4 or 2 query tiles per
+    workgroup, exact f32 rescoring in 64-dim rounds): bit-exact against the oracle,
+    including the SURVEY C4 variant D = 256 at X = 1 M with its B = 128 (no fallback:
+    the measured-norm error bound keeps the candidate sub-lists from overflowing)."""
+    g = np.random.default_rng(D + B)
+    k, N0 = (200, 211) if D == 256 else (64, 33)
+    Q, E, inv = _normal_catalog(g, B, X, D, N0)
+    _check_filter(Q, E, np.arange(1, X + 1, dtype=np.int64), inv, k, expect_flag=0)
+
+
 def test_mips_filter_path_explicit_ids():
     g = np.random.default_rng(5)
     B, X, D, k, N0 = 96, 300_000, 50, 200, 211
