@@ -138,4 +138,41 @@ __device__ __forceinline__ int map_soff(int q, int k, bool query_major) {
   return (t * 1024 + sub * 4) * 4;
 }
 
+// Epilogue store of NR x NT accumulator values (row i, column tile t) as
+// out[row][c] = v * silu'(hp[row][c]) (plain v when hp is null), rows past L and columns
+// >= width skipped.  The silu'(h) loads are issued branch-free (clamped addresses) for all
+// NR x NT values before any is used: with a per-element `if (valid) load; use; store` the
+// compiler waited for each load in turn (vmcnt(0) per element: ~50 us of serial latency
+// per workgroup at d = 256).
+//   row_of(i): the element row (sequence-relative), col_of(t): the column
+template <int NR, int NT, typename V, typename RowF, typename ColF>
+__device__ __forceinline__ void store_scaled(const V& val, int L, int width, int64_t s0,
+                                             float* out, int64_t ld_out, const float* hp,
+                                             int64_t ld_h, int c0, RowF row_of, ColF col_of) {
+  float hv[NR][NT];
+  if (hp) {
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int r = row_of(i);
+      const int64_t row = s0 + (r < L ? r : 0);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int c = col_of(t);
+        hv[i][t] = as_global(hp)[row * ld_h + c0 + (c < width ? c : 0)];
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {
+    const int r = row_of(i);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int c = col_of(t);
+      float g = val(i, t);
+      if (hp) g *= silu_grad_(hv[i][t]);
+      if (r < L && c < width) out[(s0 + r) * ld_out + c0 + c] = g;
+    }
+  }
+}
+
 }  // namespace gr

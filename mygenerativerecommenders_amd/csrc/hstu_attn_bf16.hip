@@ -639,29 +639,15 @@ __global__ __launch_bounds__(64 * WAVES) void attn_bwd_bf16_dkv_kernel(AttnBwdAr
     }
   }
   // ---- epilogue: rows = keys wk_lo + 4lg + r, cols = 16 t + lr (the silu'(h) inputs are
-  // loaded here, per element: no room to prefetch them beside the accumulators)
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int key = wk_lo + 4 * lg + r;
-    if (key >= L) continue;
-    const int64_t row = s0 + key;
-    if (DO_V) {
-      gptr<float> hvr = a.hv ? as_global(a.hv) + row * a.ld_h + h * a.dv : nullptr;
-#pragma unroll
-      for (int t = 0; t < C::VT; ++t) {
-        const int c = 16 * t + lr;
-        if (c < a.dv) a.dvv[row * a.ld_d + h * a.dv + c] = a.hv ? dV[t][r] * silu_grad_(hvr[c]) : dV[t][r];
-      }
-    }
-    if (DO_K) {
-      gptr<float> hkr = a.hk ? as_global(a.hk) + row * a.ld_h + h * a.dqk : nullptr;
-#pragma unroll
-      for (int t = 0; t < C::KT; ++t) {
-        const int c = 16 * t + lr;
-        if (c < a.dqk) a.dk[row * a.ld_d + h * a.dqk + c] = a.hk ? dK[t][r] * silu_grad_(hkr[c]) : dK[t][r];
-      }
-    }
-  }
+  // loaded here, all of a tensor's before any is used)
+  if (DO_V)
+    store_scaled<4, C::VT>([&](int i, int t) { return dV[t][i]; }, L, a.dv, s0, a.dvv, a.ld_d, a.hv,
+                           a.ld_h, h * a.dv, [&](int i) { return wk_lo + 4 * lg + i; },
+                           [&](int t) { return 16 * t + lr; });
+  if (DO_K)
+    store_scaled<4, C::KT>([&](int i, int t) { return dK[t][i]; }, L, a.dqk, s0, a.dk, a.ld_d, a.hk,
+                           a.ld_h, h * a.dqk, [&](int i) { return wk_lo + 4 * lg + i; },
+                           [&](int t) { return 16 * t + lr; });
   if (BIAS) {
     if (run_b >= 0) atomicAdd(&whts[run_b], run_s);
     __syncthreads();
@@ -794,18 +780,9 @@ __global__ __launch_bounds__(64 * WAVES) void attn_bwd_bf16_dq_kernel(AttnBwdArg
       lds_barrier();
     }
   }
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int qo = wq_lo + 4 * lg + r;
-    if (qo >= L) continue;
-    const int64_t row = s0 + qo;
-    gptr<float> hqr = a.hq ? as_global(a.hq) + row * a.ld_h + h * a.dqk : nullptr;
-#pragma unroll
-    for (int t = 0; t < C::KT; ++t) {
-      const int c = 16 * t + lr;
-      if (c < a.dqk) a.dq[row * a.ld_d + h * a.dqk + c] = a.hq ? dQ[t][r] * silu_grad_(hqr[c]) : dQ[t][r];
-    }
-  }
+  store_scaled<4, C::KT>([&](int i, int t) { return dQ[t][i]; }, L, a.dqk, s0, a.dq, a.ld_d, a.hq,
+                         a.ld_h, h * a.dqk, [&](int i) { return wq_lo + 4 * lg + i; },
+                         [&](int t) { return 16 * t + lr; });
 }
 
 // Deterministic slab reduction (fixed order): a workgroup owns 16 bins; thread (bin, g)

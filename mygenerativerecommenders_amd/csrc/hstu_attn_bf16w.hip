@@ -591,19 +591,11 @@ __device__ __forceinline__ void kv_body(const AttnBwdArgsW& a, char* smem, int k
   float* outp = KIND_K ? a.dk : a.dvv;
   const float* hp = KIND_K ? a.hk : a.hv;
 #pragma unroll
-  for (int rr = 0; rr < 16; ++rr) {
-    const int key = k0w + (rr & 3) + 8 * (rr >> 2) + 4 * lh;
-    const int64_t row = s0 + (key < L ? key : 0);
-#pragma unroll
-    for (int t = 0; t < D32; ++t) {
-      const int c = 32 * t + lr;
-      float g = acc[t][rr];
-      if (key < L && c < a.d) {
-        if (hp) g *= silu_grad_(as_global(hp)[row * a.ld_h + h * a.d + c]);
-        outp[row * a.ld_d + h * a.d + c] = g;
-      }
-    }
-  }
+  for (int g = 0; g < 16; g += 8)  // 8 rows (8 D32 silu'(h) loads) in flight at a time
+    store_scaled<8, D32>([&](int i, int t) { return acc[t][g + i]; }, L, a.d, s0, outp, a.ld_d,
+                         hp, a.ld_h, h * a.d,
+                         [&](int i) { return k0w + ((g + i) & 3) + 8 * ((g + i) >> 2) + 4 * lh; },
+                         [&](int t) { return 32 * t + lr; });
   if (BIAS) {
     // the last chunk's wrapped diagonals; zero every bin this wave never wrote: written
     // bins N-1 + d0 + [-32, 31] over d0 = k0w - qc0, qc0 = k0w .. last chunk
@@ -728,19 +720,11 @@ void attn_bwd_bf16w_dq_kernel(AttnBwdArgsW a) {
   if (!w_on) return;
   const int lh = lane >> 5;
 #pragma unroll
-  for (int rr = 0; rr < 16; ++rr) {
-    const int qo = q0w + (rr & 3) + 8 * (rr >> 2) + 4 * lh;
-    if (qo >= L) continue;
-    const int64_t row = s0 + qo;
-#pragma unroll
-    for (int t = 0; t < D32; ++t) {
-      const int c = 32 * t + lr;
-      if (c >= a.d) continue;
-      float g = acc[t][rr];
-      if (a.hq) g *= silu_grad_(as_global(a.hq)[row * a.ld_h + h * a.d + c]);
-      a.dq[row * a.ld_d + h * a.d + c] = g;
-    }
-  }
+  for (int g = 0; g < 16; g += 8)
+    store_scaled<8, D32>([&](int i, int t) { return acc[t][g + i]; }, L, a.d, s0, a.dq, a.ld_d,
+                         a.hq, a.ld_h, h * a.d,
+                         [&](int i) { return q0w + ((g + i) & 3) + 8 * ((g + i) >> 2) + 4 * lh; },
+                         [&](int t) { return 32 * t + lr; });
 }
 
 // slabs: [n][2N-1 + nb+1]; fixed-order reduce in two coalesced stages: stage 1 sums slabs

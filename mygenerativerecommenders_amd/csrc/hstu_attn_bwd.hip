@@ -127,8 +127,10 @@ struct AttnBwdCfg {
 // mod 32.
 __host__ __device__ constexpr int dts_stride(int nb1) { return ((nb1 + 30) / 32) * 32 + 1; }
 
-template <int KSTEPS, int VTILES, int TT, bool HB>
+template <int KSTEPS, int VTILES, int TT, bool HB, bool V2>
 __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const int id) {
+  // V2: 8-byte pair staging known at compile time (see BWD_V2 below)
+  const bool v2 = V2 || a.vec2, v2h = V2 || a.vec2h;
   using C = AttnBwdCfg<KSTEPS, VTILES, TT>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* Qs = reinterpret_cast<float*>(smem);  // [TT][LDQ]
@@ -233,8 +235,8 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
   BufTile<C::VP, TT> dst;
   uint32_t mw[C::TB], mwn[C::TB];
   auto load_tile = [&](int qt, uint32_t (&m)[C::TB]) {
-    qst.load(rq, a.ld_qk, qt * TT, a.dqk, a.vec2);
-    dst.load(rdo, a.ld_dout, qt * TT, a.dv, a.vec2);
+    qst.load(rq, a.ld_qk, qt * TT, a.dqk, v2);
+    dst.load(rdo, a.ld_dout, qt * TT, a.dv, v2);
 #pragma unroll
     for (int qb = 0; qb < C::TB; ++qb)
       m[qb] = buf_ld_u32(rmap, map_voff, map_soff(qt * TT + qb * 16, k0, false));
@@ -247,10 +249,10 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
   // epilogue (128 prefetched values per lane spilled; their workgroups run for ms)
   if constexpr (STAGED) {
     // K / V rows k0 .. k0 + 63 (rows past L and columns past dqk / dv read as 0)
-    qst.load(seq_rsrc(a.k, a.ld_qk, s0, h * a.dqk, L, a.dqk), a.ld_qk, k0, a.dqk, a.vec2);
-    dst.load(seq_rsrc(a.v, a.ld_v, s0, h * a.dv, L, a.dv), a.ld_v, k0, a.dv, a.vec2);
-    qst.store(Qs, C::LDQ, a.vec2);
-    dst.store(Ds, C::LDV, a.vec2);
+    qst.load(seq_rsrc(a.k, a.ld_qk, s0, h * a.dqk, L, a.dqk), a.ld_qk, k0, a.dqk, v2);
+    dst.load(seq_rsrc(a.v, a.ld_v, s0, h * a.dv, L, a.dv), a.ld_v, k0, a.dv, v2);
+    qst.store(Qs, C::LDQ, v2);
+    dst.store(Ds, C::LDV, v2);
     load_tile(k0 / TT, mw);  // the first query tile's loads fly while the fragments are read
     __syncthreads();
 #pragma unroll
@@ -262,22 +264,28 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
   } else {
     load_tile(k0 / TT, mw);
   }
-  qst.store(Qs, C::LDQ, a.vec2);
-  dst.store(Ds, C::LDV, a.vec2);
+  qst.store(Qs, C::LDQ, v2);
+  dst.store(Ds, C::LDV, v2);
   __syncthreads();
 #ifdef GR_STAMP
   unsigned long long st_t0 = gr_stamp(), st_ld = 0, st_mm1 = 0, st_ew = 0, st_bias = 0,
                      st_mm2 = 0, st_sync = 0;
   const unsigned long long st_begin = st_t0;
 #endif
+  // The first tile's map words were loaded just before the loop: consume them here.  A
+  // load still pending at the loop entry is merged into the loop-header state by the
+  // waitcnt pass, which then makes block qb of EVERY tile wait for all but the last
+  // (3 - qb) loads issued so far -- the whole next-tile prefetch.
+#pragma unroll
+  for (int qb = 0; qb < C::TB; ++qb) asm volatile("" ::"v"(mw[qb]));
   for (int qt = k0 / TT; qt <= last_qt; ++qt) {
     const int q0 = qt * TT;
     const bool more = qt < last_qt;
     if (more) {
       load_tile(qt + 1, mwn);
     } else if (STAGED && a.hv) {  // the epilogue's silu'(h) rows of this workgroup's keys
-      qst.load(seq_rsrc(a.hk, a.ld_h, s0, h * a.dqk, L, a.dqk), a.ld_h, k0, a.dqk, a.vec2h);
-      dst.load(seq_rsrc(a.hv, a.ld_h, s0, h * a.dv, L, a.dv), a.ld_h, k0, a.dv, a.vec2h);
+      qst.load(seq_rsrc(a.hk, a.ld_h, s0, h * a.dqk, L, a.dqk), a.ld_h, k0, a.dqk, v2h);
+      dst.load(seq_rsrc(a.hv, a.ld_h, s0, h * a.dv, L, a.dv), a.ld_h, k0, a.dv, v2h);
     }
     GR_ST(st_ld, 0);
 #pragma unroll
@@ -437,8 +445,8 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
     }
     if (more) {
       lds_barrier();
-      qst.store(Qs, C::LDQ, a.vec2);
-      dst.store(Ds, C::LDV, a.vec2);
+      qst.store(Qs, C::LDQ, v2);
+      dst.store(Ds, C::LDV, v2);
 #pragma unroll
       for (int qb = 0; qb < C::TB; ++qb) mw[qb] = mwn[qb];
       lds_barrier();
@@ -476,8 +484,8 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
   }
   if (STAGED && a.hv) {
     lds_barrier();
-    qst.store(Qs, C::LDQ, a.vec2h);
-    dst.store(Ds, C::LDV, a.vec2h);
+    qst.store(Qs, C::LDQ, v2h);
+    dst.store(Ds, C::LDV, v2h);
     lds_barrier();
   }
   // ---- epilogue: rows = keys wk_lo + 4lg + r, cols = lr + 16 t
@@ -538,8 +546,9 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
 }
 
 // ------------------------------------------------------------------ query-major: dQ
-template <int KSTEPS, int VTILES, int TT, bool HB>
+template <int KSTEPS, int VTILES, int TT, bool HB, bool V2>
 __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& a, const int id) {
+  const bool v2 = V2 || a.vec2, v2h = V2 || a.vec2h;
   using C = AttnBwdCfg<KSTEPS, VTILES, TT>;
   constexpr int LDK = C::LDQ;
   constexpr int LDV = 32 * ((C::VP - 2 + 31) / 32) + 2;  // A-operand reads only
@@ -622,17 +631,17 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& a, const int
   BufTile<C::VP, TT> vst;
   uint32_t mw[C::TB], mwn[C::TB];
   auto load_tile = [&](int kt, uint32_t (&m)[C::TB]) {
-    kst.load(rk, a.ld_qk, kt * TT, a.dqk, a.vec2);
-    vst.load(rv, a.ld_v, kt * TT, a.dv, a.vec2);
+    kst.load(rk, a.ld_qk, kt * TT, a.dqk, v2);
+    vst.load(rv, a.ld_v, kt * TT, a.dv, v2);
 #pragma unroll
     for (int kb = 0; kb < C::TB; ++kb)
       m[kb] = buf_ld_u32(rmap, map_voff, map_soff(q0, kt * TT + kb * 16, true));
   };
   if constexpr (STAGED) {
-    kst.load(seq_rsrc(a.q, a.ld_qk, s0, h * a.dqk, L, a.dqk), a.ld_qk, q0, a.dqk, a.vec2);
-    vst.load(seq_rsrc(a.dout, a.ld_dout, s0, h * a.dv, L, a.dv), a.ld_dout, q0, a.dv, a.vec2);
-    kst.store(Ks, LDK, a.vec2);
-    vst.store(Vs, LDV, a.vec2);
+    kst.load(seq_rsrc(a.q, a.ld_qk, s0, h * a.dqk, L, a.dqk), a.ld_qk, q0, a.dqk, v2);
+    vst.load(seq_rsrc(a.dout, a.ld_dout, s0, h * a.dv, L, a.dv), a.ld_dout, q0, a.dv, v2);
+    kst.store(Ks, LDK, v2);
+    vst.store(Vs, LDV, v2);
     load_tile(0, mw);
     __syncthreads();
 #pragma unroll
@@ -644,18 +653,20 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& a, const int
   } else {
     load_tile(0, mw);
   }
-  kst.store(Ks, LDK, a.vec2);
-  vst.store(Vs, LDV, a.vec2);
+  kst.store(Ks, LDK, v2);
+  vst.store(Vs, LDV, v2);
   __syncthreads();
 
   const int last_kt = min(q0 + 63, L - 1) / TT;
+#pragma unroll
+  for (int kb = 0; kb < C::TB; ++kb) asm volatile("" ::"v"(mw[kb]));  // see the dK/dV body
   for (int kt = 0; kt <= last_kt; ++kt) {
     const int k0 = kt * TT;
     const bool more = kt < last_kt;
     if (more) {
       load_tile(kt + 1, mwn);
     } else if (STAGED && a.hq) {
-      kst.load(seq_rsrc(a.hq, a.ld_h, s0, h * a.dqk, L, a.dqk), a.ld_h, q0, a.dqk, a.vec2h);
+      kst.load(seq_rsrc(a.hq, a.ld_h, s0, h * a.dqk, L, a.dqk), a.ld_h, q0, a.dqk, v2h);
     }
 #pragma unroll
     for (int kb = 0; kb < C::TB; ++kb) {
@@ -711,8 +722,8 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& a, const int
     }
     if (more) {
       lds_barrier();
-      kst.store(Ks, LDK, a.vec2);
-      vst.store(Vs, LDV, a.vec2);
+      kst.store(Ks, LDK, v2);
+      vst.store(Vs, LDV, v2);
 #pragma unroll
       for (int kb = 0; kb < C::TB; ++kb) mw[kb] = mwn[kb];
       lds_barrier();
@@ -720,7 +731,7 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& a, const int
   }
   if (STAGED && a.hq) {
     lds_barrier();
-    kst.store(Ks, LDK, a.vec2h);
+    kst.store(Ks, LDK, v2h);
     lds_barrier();
   }
 #pragma unroll
@@ -753,8 +764,9 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& a, const int
 // producer workgroup's flag (one lane polls relaxed with s_sleep, then one agent-scope
 // acquire and a barrier); a spin that exceeds its bound returns false before anything
 // is written and the caller recomputes the tile instead, so no schedule can hang it.
-template <int KSTEPS, int VTILES, int TT, bool WAIT = false>
+template <int KSTEPS, int VTILES, int TT, bool V2, bool WAIT = false>
 __device__ __forceinline__ bool attn_bwd_dq_ds_body(const AttnBwdArgs& a, const int id) {
+  const bool v2 = V2 || a.vec2, v2h = V2 || a.vec2h;
   using C = AttnBwdCfg<KSTEPS, VTILES, TT>;
   static_assert(TT == 64, "dQ from dS: 64-row tiles");
   constexpr int LDK = C::LDQ;
@@ -804,7 +816,7 @@ __device__ __forceinline__ bool attn_bwd_dq_ds_body(const AttnBwdArgs& a, const 
   BufTile<C::KPT, TT> kst;
   f4 dsv[C::TB], dsn[C::TB];
   auto load_tile = [&](int kt, f4 (&d)[C::TB]) {
-    kst.load(rk, a.ld_qk, kt * TT, a.dqk, a.vec2);
+    kst.load(rk, a.ld_qk, kt * TT, a.dqk, v2);
 #pragma unroll
     for (int kb = 0; kb < C::TB; ++kb) {
       const int kbi = (kt * TT + kb * 16) >> 4;
@@ -815,8 +827,10 @@ __device__ __forceinline__ bool attn_bwd_dq_ds_body(const AttnBwdArgs& a, const 
   auto tile_of = [&](int j) { return WAIT ? last_kt - j : j; };
   if (WAIT && !wait_tile(tile_of(0))) return false;
   load_tile(tile_of(0), dsv);
-  kst.store(Ks, LDK, a.vec2);
+  kst.store(Ks, LDK, v2);
   __syncthreads();
+#pragma unroll
+  for (int kb = 0; kb < C::TB; ++kb) asm volatile("" ::"v"(dsv[kb]));  // see the dK/dV body
   for (int j = 0; j <= last_kt; ++j) {
     const int kt = tile_of(j);
     const int k0 = kt * TT;
@@ -825,7 +839,7 @@ __device__ __forceinline__ bool attn_bwd_dq_ds_body(const AttnBwdArgs& a, const 
       if (WAIT && !wait_tile(tile_of(j + 1))) return false;
       load_tile(tile_of(j + 1), dsn);
     } else if (a.hq) {  // the epilogue's silu'(h) rows of this workgroup's queries
-      kst.load(seq_rsrc(a.hq, a.ld_h, s0, h * a.dqk, L, a.dqk), a.ld_h, q0, a.dqk, a.vec2h);
+      kst.load(seq_rsrc(a.hq, a.ld_h, s0, h * a.dqk, L, a.dqk), a.ld_h, q0, a.dqk, v2h);
     }
 #pragma unroll
     for (int kb = 0; kb < C::TB; ++kb) {
@@ -850,7 +864,7 @@ __device__ __forceinline__ bool attn_bwd_dq_ds_body(const AttnBwdArgs& a, const 
     }
     if (more) {
       lds_barrier();
-      kst.store(Ks, LDK, a.vec2);
+      kst.store(Ks, LDK, v2);
 #pragma unroll
       for (int kb = 0; kb < C::TB; ++kb) dsv[kb] = dsn[kb];
       lds_barrier();
@@ -858,7 +872,7 @@ __device__ __forceinline__ bool attn_bwd_dq_ds_body(const AttnBwdArgs& a, const 
   }
   if (a.hq) {
     lds_barrier();
-    kst.store(Ks, LDK, a.vec2h);
+    kst.store(Ks, LDK, v2h);
     lds_barrier();
   }
 #pragma unroll
@@ -879,38 +893,53 @@ __device__ __forceinline__ bool attn_bwd_dq_ds_body(const AttnBwdArgs& a, const 
 }
 
 // ------------------------------------------------------------------ entry points
+// BWD_V2: every kernel body is instantiated twice, with the pair staging fixed at compile
+// time when all rows qualify.  With a runtime flag the unused dword path's load
+// destinations stayed live across the join, and the waitcnt pass made each tile's first
+// block wait for the whole next-tile prefetch (vmcnt(3) of ~20) before writing them.
+#define BWD_V2(a) ((a).vec2 && ((a).vec2h || !(a).hq))
 template <int KSTEPS, int VTILES, int TT, bool HB>
 __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
   GR_TL_BEGIN();
-  attn_bwd_dkv_body<KSTEPS, VTILES, TT, HB>(a, blockIdx.x);
+  if (BWD_V2(a)) attn_bwd_dkv_body<KSTEPS, VTILES, TT, HB, true>(a, blockIdx.x);
+  else attn_bwd_dkv_body<KSTEPS, VTILES, TT, HB, false>(a, blockIdx.x);
   GR_TL_END(blockIdx.x, 0);
 }
 template <int KSTEPS, int VTILES, int TT>
 __global__ __launch_bounds__(256) void attn_bwd_dq_ds_kernel(AttnBwdArgs a) {
-  if constexpr (TT == 64) attn_bwd_dq_ds_body<KSTEPS, VTILES, TT>(a, blockIdx.x);
+  if constexpr (TT == 64) {
+    if (BWD_V2(a)) attn_bwd_dq_ds_body<KSTEPS, VTILES, TT, true>(a, blockIdx.x);
+    else attn_bwd_dq_ds_body<KSTEPS, VTILES, TT, false>(a, blockIdx.x);
+  }
 }
 // One launch, dS handed over inside it: workgroups [0, grid_kv) are the key-major pass
 // (publishing each key tile's dS), the rest compute dQ = dS K as the tiles appear (a
 // workgroup that times out waiting recomputes its tile, attn_bwd_dq_body).  All key-major
 // workgroups precede the dQ ones in dispatch order.
+template <int KSTEPS, int VTILES, int TT, bool HB, bool V2>
+__device__ __forceinline__ void attn_bwd_fused_ds_run(const AttnBwdArgs& a, int grid_kv) {
+  const int id = blockIdx.x;
+  if (id < grid_kv) {
+    attn_bwd_dkv_body<KSTEPS, VTILES, TT, HB, V2>(a, id);
+  } else if (!attn_bwd_dq_ds_body<KSTEPS, VTILES, TT, V2, true>(a, id - grid_kv)) {
+    __syncthreads();
+    AttnBwdArgs aq = a;
+    aq.paired = 0;  // the dQ workgroups are single-tile whatever the key-major pairing
+    attn_bwd_dq_body<KSTEPS, VTILES, TT, HB, V2>(aq, id - grid_kv);
+  }
+}
 template <int KSTEPS, int VTILES, int TT, bool HB>
 __global__ __launch_bounds__(256) void attn_bwd_fused_ds_kernel(AttnBwdArgs a, int grid_kv) {
-  const int id = blockIdx.x;
   if constexpr (TT == 64) {
-    if (id < grid_kv) {
-      attn_bwd_dkv_body<KSTEPS, VTILES, TT, HB>(a, id);
-    } else if (!attn_bwd_dq_ds_body<KSTEPS, VTILES, TT, true>(a, id - grid_kv)) {
-      __syncthreads();
-      AttnBwdArgs aq = a;
-      aq.paired = 0;  // the dQ workgroups are single-tile whatever the key-major pairing
-      attn_bwd_dq_body<KSTEPS, VTILES, TT, HB>(aq, id - grid_kv);
-    }
+    if (BWD_V2(a)) attn_bwd_fused_ds_run<KSTEPS, VTILES, TT, HB, true>(a, grid_kv);
+    else attn_bwd_fused_ds_run<KSTEPS, VTILES, TT, HB, false>(a, grid_kv);
   }
 }
 template <int KSTEPS, int VTILES, int TT, bool HB>
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   GR_TL_BEGIN();
-  attn_bwd_dq_body<KSTEPS, VTILES, TT, HB>(a, blockIdx.x);
+  if (BWD_V2(a)) attn_bwd_dq_body<KSTEPS, VTILES, TT, HB, true>(a, blockIdx.x);
+  else attn_bwd_dq_body<KSTEPS, VTILES, TT, HB, false>(a, blockIdx.x);
   GR_TL_END(blockIdx.x + gridDim.x, 1);
 }
 // dK/dV and dQ in ONE launch: workgroups [0, grid) run the key-major pass (heaviest key
@@ -923,10 +952,13 @@ template <int KSTEPS, int VTILES, int TT, bool HB>
 __global__ __launch_bounds__(256) void attn_bwd_fused_kernel(AttnBwdArgs a, int grid_kv) {
   const int id = blockIdx.x;
   GR_TL_BEGIN();
-  if (id < grid_kv)
-    attn_bwd_dkv_body<KSTEPS, VTILES, TT, HB>(a, id);
-  else
-    attn_bwd_dq_body<KSTEPS, VTILES, TT, HB>(a, id - grid_kv);
+  if (BWD_V2(a)) {
+    if (id < grid_kv) attn_bwd_dkv_body<KSTEPS, VTILES, TT, HB, true>(a, id);
+    else attn_bwd_dq_body<KSTEPS, VTILES, TT, HB, true>(a, id - grid_kv);
+  } else {
+    if (id < grid_kv) attn_bwd_dkv_body<KSTEPS, VTILES, TT, HB, false>(a, id);
+    else attn_bwd_dq_body<KSTEPS, VTILES, TT, HB, false>(a, id - grid_kv);
+  }
   GR_TL_END(id, id < grid_kv ? 0 : 1);
 }
 

@@ -51,9 +51,11 @@ struct AttnFwdCfg {
   static constexpr int KB = TK / 16;                         // 16-key blocks per tile
 };
 
-template <int KSTEPS, int VTILES, int TK, bool HB>
-__global__ __launch_bounds__(256) void hstu_attn_fwd_kernel(AttnFwdArgs a) {
+// V2: pair staging fixed at compile time (see BWD_V2 in hstu_attn_bwd.hip)
+template <int KSTEPS, int VTILES, int TK, bool HB, bool V2>
+__device__ __forceinline__ void hstu_attn_fwd_body(const AttnFwdArgs& a) {
   using C = AttnFwdCfg<KSTEPS, VTILES, TK>;
+  const bool v2 = V2 || a.vec2;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* Ks = reinterpret_cast<float*>(smem);
   float* Vs = Ks + TK * C::LDK;
@@ -106,20 +108,24 @@ __global__ __launch_bounds__(256) void hstu_attn_fwd_kernel(AttnFwdArgs a) {
   BufTile<C::VP, TK> vst;
   uint32_t mw[C::KB], mwn[C::KB];
   auto load_tile = [&](int kt, uint32_t (&m)[C::KB]) {
-    kst.load(rk, a.ld_qk, kt * TK, a.dqk, a.vec2);
-    vst.load(rv, a.ld_v, kt * TK, a.dv, a.vec2);
+    kst.load(rk, a.ld_qk, kt * TK, a.dqk, v2);
+    vst.load(rv, a.ld_v, kt * TK, a.dv, v2);
 #pragma unroll
     for (int kb = 0; kb < C::KB; ++kb)
       m[kb] = buf_ld_u32(rmap, map_voff, map_soff(q0, kt * TK + kb * 16, true));
   };
 
   load_tile(0, mw);
-  kst.store(Ks, C::LDK, a.vec2);
-  vst.store(Vs, C::LDV, a.vec2);
+  kst.store(Ks, C::LDK, v2);
+  vst.store(Vs, C::LDV, v2);
   __syncthreads();  // also publishes tsw / posw
 
   const int wq_lo = q0 + w * 16;  // first query of this wave
   const int last_kt = min(q0 + 63, L - 1) / TK;
+  // consume the first tile's map words before the loop (see the dK/dV body of the backward:
+  // a load pending at the loop entry makes every tile's blocks wait for the next prefetch)
+#pragma unroll
+  for (int kb = 0; kb < C::KB; ++kb) asm volatile("" ::"v"(mw[kb]));
   for (int kt = 0; kt <= last_kt; ++kt) {
     const int k0 = kt * TK;
     const bool more = kt < last_kt;
@@ -177,8 +183,8 @@ __global__ __launch_bounds__(256) void hstu_attn_fwd_kernel(AttnFwdArgs a) {
     }
     if (more) {
       lds_barrier();
-      kst.store(Ks, C::LDK, a.vec2);
-      vst.store(Vs, C::LDV, a.vec2);
+      kst.store(Ks, C::LDK, v2);
+      vst.store(Vs, C::LDV, v2);
 #pragma unroll
       for (int kb = 0; kb < C::KB; ++kb) mw[kb] = mwn[kb];
       lds_barrier();
@@ -197,6 +203,12 @@ __global__ __launch_bounds__(256) void hstu_attn_fwd_kernel(AttnFwdArgs a) {
       if (c < a.dv) orow[c] = acc[ct][r];
     }
   }
+}
+
+template <int KSTEPS, int VTILES, int TK, bool HB>
+__global__ __launch_bounds__(256) void hstu_attn_fwd_kernel(AttnFwdArgs a) {
+  if (a.vec2) hstu_attn_fwd_body<KSTEPS, VTILES, TK, HB, true>(a);
+  else hstu_attn_fwd_body<KSTEPS, VTILES, TK, HB, false>(a);
 }
 
 template <int KS, int VT, int TK = 64>
