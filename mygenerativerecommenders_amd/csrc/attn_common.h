@@ -74,14 +74,13 @@ struct BufTile {
         v[2 * i + 1] = __uint_as_float(x.y);
       }
     } else {
+      // columns past ncols read out of range (0 from the range check): no select after
+      // the load, so all PER loads stay in flight
       const int c = tid % CPR, rr = tid / CPR;
-      const int voff = ((r0 + rr) * (int)ld + c) * 4;
+      const int voff = c < ncols ? ((r0 + rr) * (int)ld + c) * 4 : 0x40000000;
       const int step = RPP * (int)ld * 4;
 #pragma unroll
-      for (int i = 0; i < PER; ++i) {
-        const float x = buf_ld(r, voff, i * step);
-        v[i] = c < ncols ? x : 0.f;
-      }
+      for (int i = 0; i < PER; ++i) v[i] = buf_ld(r, voff, i * step);
     }
   }
   __device__ __forceinline__ void store(float* lds, int ldl, bool vec2) const {

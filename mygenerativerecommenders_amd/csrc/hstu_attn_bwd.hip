@@ -489,6 +489,14 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
     lds_barrier();
   }
   // ---- epilogue: rows = keys wk_lo + 4lg + r, cols = lr + 16 t
+  if constexpr (!STAGED) {  // silu'(h) from global: every load issued before any store
+    store_scaled<4, VTILES>([&](int i, int t) { return dV[t][i]; }, L, a.dv, s0, a.dvv, a.ld_d, a.hv,
+                            a.ld_h, h * a.dv, [&](int i) { return wk_lo + 4 * lg + i; },
+                            [&](int t) { return 16 * t + lr; });
+    store_scaled<4, C::KT>([&](int i, int t) { return dK[t][i]; }, L, a.dqk, s0, a.dk, a.ld_d, a.hk,
+                           a.ld_h, h * a.dqk, [&](int i) { return wk_lo + 4 * lg + i; },
+                           [&](int t) { return 16 * t + lr; });
+  } else
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int key = wk_lo + 4 * lg + r;

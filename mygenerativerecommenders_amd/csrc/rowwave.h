@@ -126,6 +126,12 @@ __global__ __launch_bounds__(256) void rowwave_kernel(Op op) {
     constexpr int ITER = SP / SSTEP;
     constexpr int BATCH = ITER < 16 ? ITER : 16;
     const int f = tid % FP2, s0 = tid / FP2;
+    // W through a buffer descriptor: entries outside K x N read as 0 from the range check
+    // (a select after a plain load let hipcc sink each load into a branch and wait for it
+    // there: ITER serial round trips per workgroup)
+    const int64_t wlast = (int64_t)(op.K - 1) * op.bks() + (int64_t)(op.N - 1) * op.bns() + 1;
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)op.w, 0, (int)(wlast * 4 < 0x7fffffff ? wlast * 4 : 0x7fffffff), 0x00020000);
     if (f < FP) {
 #pragma unroll 1
       for (int i0 = 0; i0 < ITER; i0 += BATCH) {
@@ -137,9 +143,9 @@ __global__ __launch_bounds__(256) void rowwave_kernel(Op op) {
           const int k = Op::K_CONTIG ? f : sl;
           const int p = Op::K_CONTIG ? sl : f;  // LDS column
           const int n = (p & ~15) + qcol<VEC>(0, (p & 15) >> 2, p & 3);
-          const int kc = k < op.K ? k : op.K - 1, nc = n < op.N ? n : op.N - 1;
-          const float x = as_global(op.w)[(int64_t)kc * op.bks() + (int64_t)nc * op.bns()];
-          v[i] = (k < op.K && n < op.N) ? x : 0.f;
+          const bool ok = k < op.K && n < op.N;
+          v[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+              rw, ok ? (int)(((int64_t)k * op.bks() + (int64_t)n * op.bns()) * 4) : OOB, 0, 0));
           kk[i] = k;
           pp[i] = p;
         }
