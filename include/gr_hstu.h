@@ -73,6 +73,9 @@ GR_API int gr_timing_reset(void);
  *                                  (hstu_attn_bwd_workspace_size) depends on this option.
  *   GR_OPT_DETERMINISTIC      0|1  reductions that default to fp32 atomics run in a fixed
  *                                  order instead (gr_item_embedding_bwd: owner-computes)
+ *   GR_OPT_WGRAD_ROWS         >=0  f32 / bf16 weight gradients (64-wide panels): rows per
+ *                                  split (0 = chosen from the row count; rounded up to 64).
+ *                                  The workspace size (gr_wgrad*_workspace_size) depends on it.
  */
 enum {
   GR_OPT_MIPS_FILTER_FP32 = 1,
@@ -84,7 +87,8 @@ enum {
   GR_OPT_ATTN_BWD_PAIRS = 7,
   GR_OPT_ATTN_BWD_DS = 8,
   GR_OPT_DETERMINISTIC = 9,
-  GR_OPT_COUNT_ = 10
+  GR_OPT_WGRAD_ROWS = 10,
+  GR_OPT_COUNT_ = 11
 };
 GR_API int gr_set_option(int option, int64_t value);
 GR_API int64_t gr_get_option(int option);

@@ -124,7 +124,9 @@ __global__ __launch_bounds__(256) void rowwave_kernel(Op op) {
     constexpr int FP2 = FP <= 16 ? 16 : FP <= 32 ? 32 : FP <= 64 ? 64 : FP <= 128 ? 128 : 256;
     constexpr int SSTEP = 256 / FP2;
     constexpr int ITER = SP / SSTEP;
-    constexpr int BATCH = ITER < 16 ? ITER : 16;
+    // the whole panel's loads in flight at once (one L2 round trip per workgroup; batches
+    // of 16 cost C2's 400 one-unit-per-wave workgroups three extra trips before any MFMA)
+    constexpr int BATCH = ITER < 64 ? ITER : 64;
     const int f = tid % FP2, s0 = tid / FP2;
     // W through a buffer descriptor: entries outside K x N read as 0 from the range check
     // (a select after a plain load let hipcc sink each load into a branch and wait for it
@@ -136,7 +138,6 @@ __global__ __launch_bounds__(256) void rowwave_kernel(Op op) {
 #pragma unroll 1
       for (int i0 = 0; i0 < ITER; i0 += BATCH) {
         float v[BATCH];
-        int kk[BATCH], pp[BATCH];
 #pragma unroll
         for (int i = 0; i < BATCH; ++i) {
           const int sl = s0 + (i0 + i) * SSTEP;
@@ -146,12 +147,12 @@ __global__ __launch_bounds__(256) void rowwave_kernel(Op op) {
           const bool ok = k < op.K && n < op.N;
           v[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
               rw, ok ? (int)(((int64_t)k * op.bks() + (int64_t)n * op.bns()) * 4) : OOB, 0, 0));
-          kk[i] = k;
-          pp[i] = p;
         }
 #pragma unroll
-        for (int i = 0; i < BATCH; ++i)
-          if (i0 + i < ITER) Wl[kk[i] * C::LDW + pp[i]] = v[i];
+        for (int i = 0; i < BATCH; ++i) {
+          const int sl = s0 + (i0 + i) * SSTEP;
+          if (i0 + i < ITER) Wl[(Op::K_CONTIG ? f : sl) * C::LDW + (Op::K_CONTIG ? sl : f)] = v[i];
+        }
       }
     }
   }

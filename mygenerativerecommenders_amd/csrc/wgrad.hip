@@ -150,19 +150,24 @@ __device__ __forceinline__ void wgrad_panel(const WgradProb& g, const int64_t* o
   f4 acc[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = f4_zero();
-  // Per super-chunk: the loads of all its chunks are issued first; chunk c is then
-  // stored to LDS buffer c & 1 and computed.  One barrier per chunk: the store into a
-  // buffer follows the barrier after the previous chunk's store, which every wave
-  // reaches only after computing on that buffer two chunks ago.
-  for (int sc = 0; sc < n_ch; sc += C::SUPER) {
+  // SUPER register slots rotate over the chunks: chunk c is staged from slot c % SUPER
+  // into LDS buffer c & 1, and the slot is refilled with chunk c + SUPER right away, so
+  // SUPER - 1 chunks of compute cover each load (issuing a whole super-chunk's loads only
+  // after the previous one was computed exposed one HBM round trip per SUPER chunks:
+  // C2 rows-per-split sweeps showed ~4.6 us per chunk against ~1.4 us of MFMA).  One
+  // barrier per chunk: the store into a buffer follows the barrier after the previous
+  // chunk's store, which every wave reaches only after computing on that buffer two
+  // chunks ago.
 #pragma unroll
-    for (int u = 0; u < C::SUPER; ++u)
-      if (sc + u < n_ch) load(u, sc + u);
+  for (int u = 0; u < C::SUPER; ++u)
+    if (u < n_ch) load(u, u);
+  for (int sc = 0; sc < n_ch; sc += C::SUPER) {
 #pragma unroll
     for (int u = 0; u < C::SUPER; ++u) {
       if (sc + u < n_ch) {
         const int ch = sc + u, buf = ch & 1;
         store(u, buf, ch);
+        if (ch + C::SUPER < n_ch) load(u, ch + C::SUPER);
         __syncthreads();
         const float* Ab = As[buf];
         const float* Bb = Bs[buf];
@@ -722,6 +727,7 @@ static WgPlan wgrad_plan(int64_t max_rows, const int Ka[2], const int Nb[2]) {
   int target = 2 * device_cus() / (total_panels > 0 ? total_panels : 1);
   if (target < 1) target = 1;
   int64_t rps = (max_rows + target - 1) / target;
+  if (option(GR_OPT_WGRAD_ROWS) > 0) rps = option(GR_OPT_WGRAD_ROWS);
   rps = ((rps + WGB_CH - 1) / WGB_CH) * WGB_CH;  // whole chunks of either panel kind
   if (rps < 4 * WG_CH) rps = 4 * WG_CH;
   pl.rps = rps;

@@ -21,7 +21,10 @@ def main():
     ap.add_argument("--shape", default="c2", choices=sorted(SHAPES))
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--wgrad-only", action="store_true", help="only the grouped weight gradients")
+    ap.add_argument("--wgrad-rows", type=int, default=0, help="GR_OPT_WGRAD_ROWS (0 = auto)")
+    ap.add_argument("--bf16", action="store_true", help="bf16 weight gradients (gr_wgrad2_bf16)")
     args = ap.parse_args()
+    _lib.set_option("WGRAD_ROWS", args.wgrad_rows)  # before the workspace queries
     B, N, L, D = SHAPES[args.shape]
     hv = D
     n_out = 4 * D
@@ -59,7 +62,7 @@ def main():
     P = lambda t: t.data_ptr()  # noqa: E731
 
     def run_w():
-        _lib.call("gr_wgrad2", P(x), D, P(x_stats), P(d_uvqk), n_out, D, n_out, P(dWu), None,
+        _lib.call("gr_wgrad2_bf16" if args.bf16 else "gr_wgrad2", P(x), D, P(x_stats), P(d_uvqk), n_out, D, n_out, P(dWu), None,
                   P(dy), D, None, P(o_in), hv, D, hv, P(dWo), P(dbo), P(offsets), B, cap,
                   P(ws), ws.numel(), st)
 
