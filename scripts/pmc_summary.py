@@ -13,6 +13,8 @@ FETCH_SIZE and WRITE_SIZE are in KB and come from separate --pmc passes; on gfx9
 FETCH_SIZE reports half the bytes of a wide coalesced read, so
     hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.
 Kernel names are mapped to the names the library's live timing uses (gr_timing_query).
+    python scripts/pmc_summary.py gpurun_out/<tag> <tag> --no-latest   leaves pmc_latest.json
+(for profiles of other legs than the headline).
 """
 import collections
 import csv
@@ -26,6 +28,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 _MAP = [
     (r"bucket_map_kernel", "bucket_map"),
+    (r"attn_bwd_bf16w_kv_kernel|attn_bwd_bf16_dkv_kernel", "attn_bwd_dkv"),
+    (r"attn_bwd_bf16w_dq_kernel|attn_bwd_bf16_dq_kernel", "attn_bwd_dq"),
+    (r"attn_fwd_bf16w_kernel|attn_fwd_bf16_kernel", "attn_fwd"),
+    (r"attn_bf16w_convert", "attn_bf16_copies"),
+    (r"attn_bf16w_bias_reduce", "attn_bias_reduce"),
+    (r"wgrad_partial_(wide|bf16)_kernel", "wgrad_partial"),
     (r"attn_fwd_kernel", "attn_fwd"),
     (r"attn_bwd_fused_kernel", "attn_bwd"),
     (r"attn_bwd_dkv_kernel", "attn_bwd_dkv"),
@@ -53,7 +61,8 @@ _MAP = [
 def short_name(full: str):
     for pat, name in _MAP:
         if re.search(pat, full):
-            return name
+            # bf16-operand kernels get their own entries (same timing names, same grids)
+            return name + "_bf16" if re.search(r"bf16|wide_kernel<true>", full) else name
     return None
 
 
@@ -112,7 +121,7 @@ def main():
     out = {"source": f"profiles/{tag}_pmc.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, "
                      "separate passes; hbm = (2*FETCH+WRITE) KB*1024, gfx950 FETCH correction)",
            "kernels": kernels, "per_grid": per_grid}
-    for name in (f"{tag}_pmc.json", "pmc_latest.json"):
+    for name in (f"{tag}_pmc.json",) + (() if "--no-latest" in sys.argv else ("pmc_latest.json",)):
         with open(os.path.join(prof, name), "w") as fh:
             json.dump(out, fh, indent=1, sort_keys=True)
     for k, e in sorted(kernels.items()):
