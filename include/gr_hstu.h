@@ -76,6 +76,9 @@ GR_API int gr_timing_reset(void);
  *   GR_OPT_WGRAD_ROWS         >=0  f32 / bf16 weight gradients (64-wide panels): rows per
  *                                  split (0 = chosen from the row count; rounded up to 64).
  *                                  The workspace size (gr_wgrad*_workspace_size) depends on it.
+ *   GR_OPT_PANEL_VEC          0|1  bf16 projection GEMMs at K % 32 == 0 with 16-byte aligned
+ *                                  rows and 256-column panels: float4 operand staging
+ *                                  (default 1) or the scalar-staged row panel
  */
 enum {
   GR_OPT_MIPS_FILTER_FP32 = 1,
@@ -88,7 +91,8 @@ enum {
   GR_OPT_ATTN_BWD_DS = 8,
   GR_OPT_DETERMINISTIC = 9,
   GR_OPT_WGRAD_ROWS = 10,
-  GR_OPT_COUNT_ = 11
+  GR_OPT_PANEL_VEC = 11,
+  GR_OPT_COUNT_ = 12
 };
 GR_API int gr_set_option(int option, int64_t value);
 GR_API int64_t gr_get_option(int option);

@@ -359,6 +359,137 @@ __global__ __launch_bounds__(256) void rowpanel_bf16_kernel(Op op) {
   op.epilogue(acc, es, m0 + w * 16 + 4 * lg, n0 + lr, total);
 }
 
+// Wide-shape bf16 row panel (K % 32 == 0, 16-byte aligned rows, 256-column panels: the
+// C3 projections).  Same tile, LDS images and epilogue as rowpanel_bf16_kernel, with
+//  * float4 operand loads: 10 vector-memory instructions per thread per 32-wide chunk
+//    instead of 40 (the scalar staging, not the MFMAs, set the chunk time at D = 256);
+//  * the epilogue's row inputs issued under the last chunk's MFMAs instead of before the
+//    loop, so their registers are not live across it (the LayerNorm-backward panel held
+//    128 of them: 256 VGPRs, one workgroup per CU).
+// Staging maps (t = thread):
+//  A        : k-quad t & 7 of rows t >> 3 and + 32            -> 8-byte LDS stores
+//  B k-contig (W'(k, n) = w[k + n bns]): k-quad t & 7 of columns t >> 3 + 32 i, i < 8
+//  B n-contig (W'(k, n) = w[k bks + n]): n-quad (lane >> 2) + 16 w of k-rows
+//             8 i + 2 (lane & 3) + {0, 1}, i < 4              -> packed (k, k+1) stores
+template <class Op>
+__global__ __launch_bounds__(256) void rowpanel_bf16v_kernel(Op op) {
+  constexpr int NT = 16, BN = 256, BKT = 32, LDK = BKT + 8;
+  __shared__ __attribute__((aligned(16))) __bf16 As2[2][BM * LDK];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs2[2][BN * LDK];
+  __shared__ float2 stats[BM];
+  const int64_t total = op.offsets[op.B];
+  const int64_t m0 = (int64_t)blockIdx.x * BM;
+  if (m0 >= total) return;
+  const int n0 = blockIdx.y * BN;
+  const int tid = threadIdx.x, w = wave_id(), lane = tid & 63;
+  const int lr = lane & 15, lg = lane >> 4;
+
+  op.prologue(m0, total, stats);
+  __syncthreads();
+
+  const __amdgpu_buffer_rsrc_t ra0 = op.a_rsrc0(m0, total);
+  const __amdgpu_buffer_rsrc_t ra1 = op.a_rsrc1(m0, total);
+  const int ld0 = (int)op.a_ld0(), ld1 = (int)op.a_ld1();
+  const int aq = tid & 7, ar = tid >> 3;
+  const int va0 = (ar * ld0 + 4 * aq) * 4, va1 = (ar * ld1 + 4 * aq) * 4;
+  const __amdgpu_buffer_rsrc_t rw =
+      __builtin_amdgcn_make_buffer_rsrc((void*)op.w, 0, op.K * op.N * 4, 0x00020000);
+  const int bks = op.bks(), bns = op.bns();
+  // k-contiguous: column bc + 32 i, k-quad bq; n-contiguous: n-quad bn, k-pair bp
+  const int bq = tid & 7, bc = tid >> 3;
+  const int bp = lane & 3, bn = (lane >> 2) + 16 * w;
+  int vb;
+  if constexpr (Op::B_N_CONTIG)
+    vb = n0 + 4 * bn < op.N ? (2 * bp * bks + n0 + 4 * bn) * 4 : 0x40000000;
+  else
+    vb = (4 * bq + (n0 + bc) * bns) * 4;
+
+  f4 ra[2], ra2[Op::NSRC == 2 ? 2 : 1], rb[8];
+  auto ld4 = [](__amdgpu_buffer_rsrc_t r, int v, int s) {
+    return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, v, s, 0));
+  };
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      ra[i] = ld4(ra0, va0 + k0 * 4, i * 32 * ld0 * 4);
+      if constexpr (Op::NSRC == 2) ra2[Op::NSRC == 2 ? i : 0] = ld4(ra1, va1 + k0 * 4, i * 32 * ld1 * 4);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if constexpr (Op::B_N_CONTIG)
+        rb[i] = ld4(rw, vb, (k0 + 8 * (i >> 1) + (i & 1)) * bks * 4);
+      else
+        rb[i] = ld4(rw, vb, (k0 + 32 * i * bns) * 4);  // columns >= N: past the range, 0
+    }
+  };
+  auto store = [&](int k0, int buf) {
+    __bf16* As = As2[buf];
+    __bf16* Bs = Bs2[buf];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = ar + 32 * i;
+      const bool rok = m0 + r < total;
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = k0 + 4 * aq + j;
+        const float x = op.a_xform(ra[i][j], Op::NSRC == 2 ? ra2[Op::NSRC == 2 ? i : 0][j] : 0.f,
+                                   m0 + r, k, stats[r], rok);
+        v[j] = rok ? x : 0.f;
+      }
+      *reinterpret_cast<u32x2_t*>(As + r * LDK + 4 * aq) =
+          u32x2_t{pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3])};
+    }
+    if constexpr (Op::B_N_CONTIG) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          *reinterpret_cast<uint32_t*>(Bs + (4 * bn + j) * LDK + 8 * i + 2 * bp) =
+              pack_bf16(rb[2 * i][j], rb[2 * i + 1][j]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        *reinterpret_cast<u32x2_t*>(Bs + (bc + 32 * i) * LDK + 4 * bq) =
+            u32x2_t{pack_bf16(rb[i][0], rb[i][1]), pack_bf16(rb[i][2], rb[i][3])};
+    }
+  };
+
+  f4 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f4_zero();
+  auto mfmas = [&](int buf) {
+    const __bf16* As = As2[buf];
+    const __bf16* Bs = Bs2[buf];
+    const u32x4_t av = *reinterpret_cast<const u32x4_t*>(As + (w * 16 + lr) * LDK + 8 * lg);
+    u32x4_t bv[2];
+    bv[0] = *reinterpret_cast<const u32x4_t*>(Bs + lr * LDK + 8 * lg);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      if (t + 1 < NT)
+        bv[(t + 1) & 1] = *reinterpret_cast<const u32x4_t*>(Bs + (16 * (t + 1) + lr) * LDK + 8 * lg);
+      acc[t] = mfma_bf16(av, bv[t & 1], acc[t]);
+    }
+  };
+
+  load(0);
+  store(0, 0);
+  lds_barrier();
+  int buf = 0;
+  const int klast = op.K - BKT;
+  for (int k0 = 0; k0 < klast; k0 += BKT) {
+    load(k0 + BKT);
+    mfmas(buf);
+    store(k0 + BKT, buf ^ 1);
+    lds_barrier();
+    buf ^= 1;
+  }
+  typename Op::template Epi<NT> es;
+  op.epi_load(es, m0 + w * 16 + 4 * lg, n0 + lr, total);
+  mfmas(buf);
+  op.epilogue(acc, es, m0 + w * 16 + 4 * lg, n0 + lr, total);
+}
+
 // descriptor over rows [m0, total) of a (rows, ld) matrix (column offset folded in base)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const float* base, int64_t ld,
                                                            int64_t m0, int64_t total) {
@@ -703,9 +834,12 @@ static int launch_rowpanel(const Op& op, int64_t max_rows, bool full_row, const 
   return 0;
 }
 
+// vec: operand rows 16-byte aligned (caller-checked); the float4 form also needs K a
+// multiple of the 32-wide chunk, full 256-column panels and, for n-contiguous weights,
+// N a multiple of 4 (a float4 never straddles the end of the weight)
 template <class Op>
 static int launch_rowpanel_bf16(const Op& op, int64_t max_rows, bool full_row, const char* name,
-                                hipStream_t st) {
+                                hipStream_t st, bool vec = false) {
   const int nt_needed = ceil_div(op.N, 16);
   GR_REQUIRE(!full_row || nt_needed <= 16,
              "%s: %d output columns exceed one 256-column panel (row-reduction epilogue)", name,
@@ -715,6 +849,12 @@ static int launch_rowpanel_bf16(const Op& op, int64_t max_rows, bool full_row, c
   dim3 grid((unsigned)((max_rows + BM - 1) / BM), (unsigned)panels);
   if (grid.x == 0) return 0;
   const char* tname = name + 5;
+  if (vec && option(GR_OPT_PANEL_VEC) != 0 && nt == 16 && op.K % 32 == 0 &&
+      (!Op::B_N_CONTIG || op.N % 4 == 0) && (int64_t)op.K * op.N * 4 <= 0x7fffffffLL) {
+    GR_TIMED(tname, st, hipLaunchKernelGGL((rowpanel_bf16v_kernel<Op>), grid, dim3(256), 0, st, op));
+    GR_LAUNCH_CHECK(name);
+    return 0;
+  }
 #define GR_NT_CASE(NT_)                                                                      \
   case NT_:                                                                                  \
     GR_TIMED(tname, st, hipLaunchKernelGGL((rowpanel_bf16_kernel<NT_, Op>), grid, dim3(256), 0, \
@@ -954,7 +1094,8 @@ static int hstu_ln_uvqk_fwd_impl(bool bf16, const float* x, int64_t ld_x, const 
   }
   OpLnUvqk op{offsets, B, D, n_out, x, ld_x, w_uvqk, eps, activation, (float2*)x_stats,
               h_pre, uvqk, ld_out};
-  return bf16 ? launch_rowpanel_bf16(op, max_rows, false, "hstu_ln_uvqk_fwd", (hipStream_t)stream)
+  return bf16 ? launch_rowpanel_bf16(op, max_rows, false, "hstu_ln_uvqk_fwd", (hipStream_t)stream,
+                                     rw_vec({x, w_uvqk}, {ld_x, n_out}) == 4)
               : launch_rowpanel(op, max_rows, false, "hstu_ln_uvqk_fwd", (hipStream_t)stream);
 }
 extern "C" int hstu_ln_uvqk_fwd(const float* x, int64_t ld_x, const int64_t* offsets, int B,
@@ -988,7 +1129,8 @@ static int hstu_gate_o_fwd_impl(bool bf16, const float* u, int64_t ld_u, const f
   }
   OpGateO op{offsets, B, hdv, D, u, ld_u, attn, ld_attn, w_o, b_o, x_res, ld_x, eps, dropout_p,
              seed, seed_offset, (float2*)attn_stats, o_in, y, ld_y};
-  return bf16 ? launch_rowpanel_bf16(op, max_rows, false, "hstu_gate_o_fwd", (hipStream_t)stream)
+  return bf16 ? launch_rowpanel_bf16(op, max_rows, false, "hstu_gate_o_fwd", (hipStream_t)stream,
+                                     rw_vec({u, attn, w_o}, {ld_u, ld_attn, hdv}) == 4)
               : launch_rowpanel(op, max_rows, false, "hstu_gate_o_fwd", (hipStream_t)stream);
 }
 extern "C" int hstu_gate_o_fwd(const float* u, int64_t ld_u, const float* attn, int64_t ld_attn,
@@ -1031,7 +1173,8 @@ static int hstu_gate_o_bwd_impl(bool bf16, const float* dy, int64_t ld_dy, const
   op.w = w_o; op.u = u; op.ldu = ld_u; op.attn = attn; op.lda = ld_attn;
   op.a_stats = (const float2*)attn_stats; op.h_u = h_u; op.ldh = ld_h; op.p = dropout_p;
   op.seed = seed; op.seed_off = seed_offset; op.du = du; op.lddu = ld_du; op.da = d_attn; op.ldda = ld_da;
-  return bf16 ? launch_rowpanel_bf16(op, max_rows, true, "hstu_gate_o_bwd", (hipStream_t)stream)
+  return bf16 ? launch_rowpanel_bf16(op, max_rows, true, "hstu_gate_o_bwd", (hipStream_t)stream,
+                                     rw_vec({dy, w_o}, {ld_dy, hdv}) == 4)
               : launch_rowpanel(op, max_rows, true, "hstu_gate_o_bwd", (hipStream_t)stream);
 }
 extern "C" int hstu_gate_o_bwd(const float* dy, int64_t ld_dy, const int64_t* offsets, int B,
@@ -1071,7 +1214,8 @@ static int hstu_ln_uvqk_bwd_impl(bool bf16, const float* dh, int64_t ld_dh, cons
   op.offsets = offsets; op.B = B; op.K = n_out; op.N = D; op.dh = dh; op.lddh = ld_dh;
   op.w = w_uvqk; op.x = x; op.ldx = ld_x; op.x_stats = (const float2*)x_stats;
   op.dy = dy_res; op.lddy = ld_dy; op.dx = dx; op.lddx = ld_dx;
-  return bf16 ? launch_rowpanel_bf16(op, max_rows, true, "hstu_ln_uvqk_bwd", (hipStream_t)stream)
+  return bf16 ? launch_rowpanel_bf16(op, max_rows, true, "hstu_ln_uvqk_bwd", (hipStream_t)stream,
+                                     rw_vec({dh, w_uvqk}, {ld_dh, D}) == 4)
               : launch_rowpanel(op, max_rows, true, "hstu_ln_uvqk_bwd", (hipStream_t)stream);
 }
 extern "C" int hstu_ln_uvqk_bwd(const float* dh, int64_t ld_dh, const int64_t* offsets, int B,

@@ -221,6 +221,51 @@ def test_hstu_bf16_mode_vs_oracle(B, N0, out_len, D, blocks, min_len):
         assert e <= 5e-2, pname
 
 
+@pytest.mark.parametrize("D,H,N0", [(256, 1, 700), (192, 2, 300)])
+def test_hstu_bf16_panel_vec_bitexact(D, H, N0):
+    """The float4-staged bf16 row panel (GR_OPT_PANEL_VEC=1, K % 32 == 0) stages the same
+    bf16 operands in the same k order as the scalar-staged one: encoder output and every
+    gradient bit-identical between the two (ragged rows, partial last row tile; D = 192,
+    H = 2 has a half-filled second UVQK column panel)."""
+    from mygenerativerecommenders_amd.hstu import HSTU
+    torch.manual_seed(0)
+    B, out_len = 3, 11
+    N = N0 + out_len
+    enc = HSTU(max_sequence_len=N0, max_output_len=out_len, embedding_dim=D,
+               item_embedding_dim=D, num_blocks=2, num_heads=H, linear_dim=D // H,
+               attention_dim=D // H, normalization="rel_bias", linear_config="uvqk",
+               linear_activation="silu", linear_dropout_rate=0.2, attn_dropout_rate=0.0,
+               autocast_dtype=torch.bfloat16).cuda()
+    g = torch.Generator().manual_seed(3)
+    lengths = torch.tensor([N0 - 37, 19, N0 // 2])
+    x = torch.randn(B, N, D, generator=g)
+    ts = torch.zeros(B, N, dtype=torch.int64)
+    for b in range(B):
+        L = int(lengths[b])
+        ts[b, :L + 1] = 1_000_000_000 + torch.cumsum((torch.rand(L + 1, generator=g) * 2e5).long(), 0)
+    dy = torch.randn(B, N, D, generator=g).cuda()
+
+    from mygenerativerecommenders_amd import _lib
+
+    def run(vec):
+        prev = _lib.set_option("PANEL_VEC", vec)
+        try:
+            enc.zero_grad(set_to_none=True)
+            enc._hstu._dropout_step.zero_()  # same dropout masks in both runs
+            xg = x.cuda().requires_grad_(True)
+            y, _ = enc(lengths.cuda(), xg, None, {"timestamps": ts.cuda()})
+            (y * dy).sum().backward()
+            torch.cuda.synchronize()
+        finally:
+            _lib.set_option("PANEL_VEC", prev)
+        return [y.detach().clone(), xg.grad.clone()] + [p.grad.clone() for p in enc.parameters()]
+
+    a, b = run(1), run(0)
+    assert torch.isfinite(a[0]).all()
+    for i, (u, v) in enumerate(zip(a, b)):
+        assert torch.equal(u, v), i
+
+
 @pytest.mark.parametrize("D,dh,H", [(50, 50, 1), (32, 16, 2), (64, 64, 1),
                                     (256, 256, 1), (192, 48, 2), (160, 40, 1)])
 def test_hstu_concat_ua_vs_oracle(D, dh, H):
