@@ -125,6 +125,7 @@ struct ConvSet {
   __bf16* zrow;
   const int64_t* offsets;
   int B, H, d, nch;
+  int vec4;  // set by launch_convert
 };
 __global__ __launch_bounds__(256) void attn_bf16w_convert(ConvSet cs) {
   const int y = blockIdx.y;
@@ -133,20 +134,31 @@ __global__ __launch_bounds__(256) void attn_bf16w_convert(ConvSet cs) {
   __bf16* dst = y == 0 ? cs.dst[0] : y == 1 ? cs.dst[1] : y == 2 ? cs.dst[2] : cs.dst[3];
   if (cs.zrow && blockIdx.x == 0 && y == 0 && (int)threadIdx.x < cs.nch)
     *reinterpret_cast<u32x4_t*>(cs.zrow + 8 * threadIdx.x) = u32x4_t{0u, 0u, 0u, 0u};
-  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int c = (int)(idx % cs.nch);
-  const int64_t rh = idx / cs.nch;
-  const int h = (int)(rh % cs.H);
-  const int64_t row = rh / cs.H;
+  // 32-bit index math (the launcher checks rows * H * nch < 2^31): the 64-bit divisions
+  // cost more issue slots than the 48 bytes a thread moves
+  const uint32_t idx = blockIdx.x * 256u + threadIdx.x;
+  const uint32_t nch = (uint32_t)cs.nch, H = (uint32_t)cs.H;
+  const uint32_t rh = idx / nch, c = idx - rh * nch;
+  const uint32_t row32 = rh / H, h = rh - row32 * H;
+  const int64_t row = row32;
   if (row >= cs.offsets[cs.B]) return;
   const float* p = src + row * ld + h * cs.d + 8 * c;
   float x[8];
+  if (cs.vec4) {  // d == 8 nch, 16-byte aligned rows: two float4 loads, no guards
+    const f4 lo = *reinterpret_cast<const f4*>(p), hi = *reinterpret_cast<const f4*>(p + 4);
 #pragma unroll
-  for (int j = 0; j < 8; j += 2) {
-    float2 v = make_float2(0.f, 0.f);
-    if (8 * c + j < cs.d) v = *reinterpret_cast<const float2*>(p + j);  // d, ld even
-    x[j] = v.x;
-    x[j + 1] = v.y;
+    for (int j = 0; j < 4; ++j) {
+      x[j] = lo[j];
+      x[j + 4] = hi[j];
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      float2 v = make_float2(0.f, 0.f);
+      if (8 * (int)c + j < cs.d) v = *reinterpret_cast<const float2*>(p + j);  // d, ld even
+      x[j] = v.x;
+      x[j + 1] = v.y;
+    }
   }
   *reinterpret_cast<u32x4_t*>(dst + (row * cs.H + h) * (8 * cs.nch) + 8 * c) =
       u32x4_t{pack_bf16(x[0], x[1]), pack_bf16(x[2], x[3]), pack_bf16(x[4], x[5]), pack_bf16(x[6], x[7])};
@@ -154,6 +166,11 @@ __global__ __launch_bounds__(256) void attn_bf16w_convert(ConvSet cs) {
 static int launch_convert(ConvSet cs, int n, int64_t total_rows, hipStream_t st) {
   if (n == 0) return 0;
   const int64_t threads = total_rows * cs.H * cs.nch;
+  GR_REQUIRE(threads + 256 < 0x7fffffffLL, "hstu_attn_bf16 copies: %lld rows x heads too many",
+             (long long)(total_rows * cs.H));
+  cs.vec4 = cs.d == 8 * cs.nch;  // no padding chunk (d % 32 == 0)
+  for (int i = 0; i < n; ++i)
+    if ((uintptr_t)cs.src[i] % 16 != 0 || cs.ld[i] % 4 != 0) cs.vec4 = 0;
   GR_TIMED("attn_bf16_copies", st, hipLaunchKernelGGL(attn_bf16w_convert, dim3((unsigned)((threads + 255) / 256), n), dim3(256), 0, st, cs));
   GR_LAUNCH_CHECK("hstu_attn_bf16 copies");
   return 0;

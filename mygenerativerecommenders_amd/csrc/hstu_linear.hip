@@ -49,6 +49,53 @@ __device__ __forceinline__ void panel_row_stats(const float* base, int64_t ld, i
   const int sub = lane & 15, rq = lane >> 4;
   const int64_t mlast = total - 1;
   const float invk = 1.f / (float)K;
+  if (K <= 256) {
+    // all 4 x 16 values of the lane's 4 rows issued before any reduction (the loop form
+    // below is a chain of 2 x 4 x K/64 dependent round trips: ~30 us per workgroup at
+    // K = 256); padding columns are 0, so the sums — in the same order — are unchanged
+    float v[4][16];
+#pragma unroll
+    for (int pass = 0; pass < 4; ++pass) {
+      const int64_t m = m0 + w * 16 + pass * 4 + rq;
+      gptr<float> row = src + (m < mlast ? m : mlast) * ld;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int k = 16 * j + sub;
+        v[pass][j] = row[k < K ? k : K - 1];
+      }
+    }
+#pragma unroll
+    for (int pass = 0; pass < 4; ++pass) {
+      const int r = w * 16 + pass * 4 + rq;
+      const int64_t m = m0 + r;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v[pass][j] = 16 * j + sub < K ? v[pass][j] : 0.f;
+      float s = 0.f;
+#pragma unroll
+      for (int it = 0; it < 4; ++it)
+        s += (v[pass][4 * it] + v[pass][4 * it + 1]) + (v[pass][4 * it + 2] + v[pass][4 * it + 3]);
+      s = sum16(s);
+      const float mean = s * invk;
+      float q = 0.f;
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        float d[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int j = 4 * it + u;
+          d[u] = 16 * j + sub < K ? v[pass][j] - mean : 0.f;
+        }
+        q += (d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]);
+      }
+      q = sum16(q);
+      const float rstd = rsqrtf(q * invk + eps);
+      if (sub == 0) {
+        st_lds[r] = make_float2(mean, rstd);
+        if (st_glob && m < total) st_glob[m] = make_float2(mean, rstd);
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int pass = 0; pass < 4; ++pass) {
     const int r = w * 16 + pass * 4 + rq;
@@ -613,21 +660,26 @@ struct OpGateO {
       const int n = ncol + 16 * t;
       bv[t] = bias ? as_global(bias)[n < N ? n : N - 1] : 0.f;
     }
+    // every residual load issued before the first store (y may alias xres for hipcc,
+    // which otherwise waits for each row's loads after the previous row's stores)
+    float xv[4][NT];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int64_t m = mrow + r;
-      const int64_t mc = clamp_row(m, total);
-      float xv[NT];
+      const int64_t mc = clamp_row(mrow + r, total);
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         const int n = ncol + 16 * t;
-        xv[t] = xres ? as_global(xres)[mc * ldx + (n < N ? n : N - 1)] : 0.f;
+        xv[r][t] = xres ? as_global(xres)[mc * ldx + (n < N ? n : N - 1)] : 0.f;
       }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t m = mrow + r;
       if (m >= total) continue;
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         const int n = ncol + 16 * t;
-        if (n < N) y[m * ldy + n] = (acc[t][r] + bv[t]) + xv[t];
+        if (n < N) y[m * ldy + n] = (acc[t][r] + bv[t]) + xv[r][t];
       }
     }
   }
