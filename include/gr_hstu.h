@@ -76,9 +76,9 @@ GR_API int gr_timing_reset(void);
  *   GR_OPT_WGRAD_ROWS         >=0  f32 / bf16 weight gradients (64-wide panels): rows per
  *                                  split (0 = chosen from the row count; rounded up to 64).
  *                                  The workspace size (gr_wgrad*_workspace_size) depends on it.
- *   GR_OPT_PANEL_VEC          0|1  bf16 projection GEMMs at K % 32 == 0 with 16-byte aligned
- *                                  rows and 256-column panels: float4 operand staging
- *                                  (default 1) or the scalar-staged row panel
+ *   GR_OPT_PANEL_VEC          0|1  bf16 backward projection GEMMs at K % 32 == 0 with
+ *                                  16-byte aligned rows and 256-column panels: float4
+ *                                  operand staging (default 1) or the scalar-staged row panel
  */
 enum {
   GR_OPT_MIPS_FILTER_FP32 = 1,

@@ -407,7 +407,7 @@ __global__ __launch_bounds__(256) void rowpanel_bf16_kernel(Op op) {
 }
 
 // Wide-shape bf16 row panel (K % 32 == 0, 16-byte aligned rows, 256-column panels: the
-// C3 projections).  Same tile, LDS images and epilogue as rowpanel_bf16_kernel, with
+// C3 backward projections).  Same tile, LDS images and epilogue as rowpanel_bf16_kernel, with
 //  * float4 operand loads: 10 vector-memory instructions per thread per 32-wide chunk
 //    instead of 40 (the scalar staging, not the MFMAs, set the chunk time at D = 256);
 //  * the epilogue's row inputs issued under the last chunk's MFMAs instead of before the
@@ -811,36 +811,35 @@ struct OpLnUvqkBwd : NoStats {
     }
   }
   template <int NT>
+  __device__ void row_out(const f4 (&acc)[NT], int r, float2 st, const float* xv, const float* dyv,
+                          int64_t m, int ncol, int64_t total) const {
+    const bool row_ok = m < total;
+    float s1 = 0.f, s2 = 0.f;
+    float xh[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int n = ncol + 16 * t;
+      const bool ok = row_ok && n < N;
+      xh[t] = ok ? (xv[t] - st.x) * st.y : 0.f;
+      const float dn = ok ? acc[t][r] : 0.f;
+      s1 += dn;
+      s2 += dn * xh[t];
+    }
+    s1 = sum16(s1);
+    s2 = sum16(s2);
+    const float inv = 1.f / (float)N;
+    const float mean1 = s1 * inv, mean2 = s2 * inv;
+    if (!row_ok) return;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int n = ncol + 16 * t;
+      if (n < N) dx[m * lddx + n] = dyv[t] + st.y * (acc[t][r] - mean1 - xh[t] * mean2);
+    }
+  }
+  template <int NT>
   __device__ void epilogue(f4 (&acc)[NT], const Epi<NT>& es, int64_t mrow, int ncol, int64_t total) const {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t m = mrow + r;
-      const bool row_ok = m < total;
-      const float2 st = es.st[r];
-      const float* xv = es.xv[r];
-      const float* dyv = es.dyv[r];
-      float s1 = 0.f, s2 = 0.f;
-      float xh[NT];
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        const int n = ncol + 16 * t;
-        const bool ok = row_ok && n < N;
-        xh[t] = ok ? (xv[t] - st.x) * st.y : 0.f;
-        const float dn = ok ? acc[t][r] : 0.f;
-        s1 += dn;
-        s2 += dn * xh[t];
-      }
-      s1 = sum16(s1);
-      s2 = sum16(s2);
-      const float inv = 1.f / (float)N;
-      const float mean1 = s1 * inv, mean2 = s2 * inv;
-      if (!row_ok) continue;
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        const int n = ncol + 16 * t;
-        if (n < N) dx[m * lddx + n] = dyv[t] + st.y * (acc[t][r] - mean1 - xh[t] * mean2);
-      }
-    }
+    for (int r = 0; r < 4; ++r) row_out(acc, r, es.st[r], es.xv[r], es.dyv[r], mrow + r, ncol, total);
   }
 };
 
@@ -1146,8 +1145,10 @@ static int hstu_ln_uvqk_fwd_impl(bool bf16, const float* x, int64_t ld_x, const 
   }
   OpLnUvqk op{offsets, B, D, n_out, x, ld_x, w_uvqk, eps, activation, (float2*)x_stats,
               h_pre, uvqk, ld_out};
-  return bf16 ? launch_rowpanel_bf16(op, max_rows, false, "hstu_ln_uvqk_fwd", (hipStream_t)stream,
-                                     rw_vec({x, w_uvqk}, {ld_x, n_out}) == 4)
+  // forward panels keep the scalar staging: measured faster at C3 (210 vs 219 us; gate_o
+  // 132 vs 139 us, scripts/gemm_micro.py --bf16-panels); the float4 form pays off in the
+  // backward panels, whose epilogue inputs otherwise hold the registers
+  return bf16 ? launch_rowpanel_bf16(op, max_rows, false, "hstu_ln_uvqk_fwd", (hipStream_t)stream)
               : launch_rowpanel(op, max_rows, false, "hstu_ln_uvqk_fwd", (hipStream_t)stream);
 }
 extern "C" int hstu_ln_uvqk_fwd(const float* x, int64_t ld_x, const int64_t* offsets, int B,
@@ -1181,8 +1182,7 @@ static int hstu_gate_o_fwd_impl(bool bf16, const float* u, int64_t ld_u, const f
   }
   OpGateO op{offsets, B, hdv, D, u, ld_u, attn, ld_attn, w_o, b_o, x_res, ld_x, eps, dropout_p,
              seed, seed_offset, (float2*)attn_stats, o_in, y, ld_y};
-  return bf16 ? launch_rowpanel_bf16(op, max_rows, false, "hstu_gate_o_fwd", (hipStream_t)stream,
-                                     rw_vec({u, attn, w_o}, {ld_u, ld_attn, hdv}) == 4)
+  return bf16 ? launch_rowpanel_bf16(op, max_rows, false, "hstu_gate_o_fwd", (hipStream_t)stream)
               : launch_rowpanel(op, max_rows, false, "hstu_gate_o_fwd", (hipStream_t)stream);
 }
 extern "C" int hstu_gate_o_fwd(const float* u, int64_t ld_u, const float* attn, int64_t ld_attn,

@@ -23,8 +23,12 @@ def main():
     ap.add_argument("--wgrad-only", action="store_true", help="only the grouped weight gradients")
     ap.add_argument("--wgrad-rows", type=int, default=0, help="GR_OPT_WGRAD_ROWS (0 = auto)")
     ap.add_argument("--bf16", action="store_true", help="bf16 weight gradients (gr_wgrad2_bf16)")
+    ap.add_argument("--bf16-panels", action="store_true", help="bf16 projection GEMMs (*_bf16)")
+    ap.add_argument("--panel-vec", type=int, default=1, help="GR_OPT_PANEL_VEC")
     args = ap.parse_args()
     _lib.set_option("WGRAD_ROWS", args.wgrad_rows)  # before the workspace queries
+    _lib.set_option("PANEL_VEC", args.panel_vec)
+    sfx = "_bf16" if args.bf16_panels else ""
     B, N, L, D = SHAPES[args.shape]
     hv = D
     n_out = 4 * D
@@ -69,19 +73,20 @@ def main():
     def run():
         if args.wgrad_only:
             return run_w()
-        _lib.call("hstu_ln_uvqk_fwd", P(x), D, P(offsets), B, cap, D, P(w_uvqk), n_out, 1e-6, 1,
+        _lib.call("hstu_ln_uvqk_fwd" + sfx, P(x), D, P(offsets), B, cap, D, P(w_uvqk), n_out, 1e-6, 1,
                   P(x_stats), P(h_pre), P(uvqk), n_out, st)
-        _lib.call("hstu_gate_o_fwd", P(uvqk), n_out, P(attn), hv, P(offsets), B, cap, hv, D,
+        _lib.call("hstu_gate_o_fwd" + sfx, P(uvqk), n_out, P(attn), hv, P(offsets), B, cap, hv, D,
                   P(w_o), P(b_o), P(x), D, 1e-6, 0.2, 7, P(seed_off), P(attn_stats), P(o_in),
                   P(y), D, st)
-        _lib.call("hstu_gate_o_bwd", P(dy), D, P(offsets), B, cap, hv, D, P(w_o), P(uvqk),
+        _lib.call("hstu_gate_o_bwd" + sfx, P(dy), D, P(offsets), B, cap, hv, D, P(w_o), P(uvqk),
                   n_out, P(attn), hv, P(attn_stats), P(h_pre), n_out, 0.2, 7, P(seed_off),
                   P(d_uvqk), n_out, P(d_attn), hv, st)
-        _lib.call("gr_wgrad", P(dy), D, None, P(o_in), hv, P(offsets), B, cap, D, hv, P(dWo),
-                  P(dbo), P(ws), ws.numel(), st)
-        _lib.call("gr_wgrad", P(x), D, P(x_stats), P(d_uvqk), n_out, P(offsets), B, cap, D,
-                  n_out, P(dWu), None, P(ws), ws.numel(), st)
-        _lib.call("hstu_ln_uvqk_bwd", P(d_uvqk), n_out, P(offsets), B, cap, D, n_out, P(w_uvqk),
+        if not args.bf16_panels:
+            _lib.call("gr_wgrad", P(dy), D, None, P(o_in), hv, P(offsets), B, cap, D, hv, P(dWo),
+                      P(dbo), P(ws), ws.numel(), st)
+            _lib.call("gr_wgrad", P(x), D, P(x_stats), P(d_uvqk), n_out, P(offsets), B, cap, D,
+                      n_out, P(dWu), None, P(ws), ws.numel(), st)
+        _lib.call("hstu_ln_uvqk_bwd" + sfx, P(d_uvqk), n_out, P(offsets), B, cap, D, n_out, P(w_uvqk),
                   P(x), D, P(x_stats), P(dy), D, P(dx), D, st)
 
     for _ in range(3):
@@ -112,7 +117,8 @@ def main():
         res[n] = {"avg_us": round(avg * 1e3, 2), "launches_per_iter": c // args.iters}
         if n in bytes_:
             res[n]["GBps"] = round(bytes_[n] / (avg * 1e-3) / 1e9, 1)
-    print(json.dumps({"shape": args.shape, "rows": rows, "kernels": res}))
+    print(json.dumps({"shape": args.shape, "rows": rows, "bf16_panels": args.bf16_panels,
+                      "panel_vec": args.panel_vec, "kernels": res}))
 
 
 if __name__ == "__main__":
