@@ -230,16 +230,16 @@ __global__ __launch_bounds__(256) void rowpanel_kernel(Op op) {
   f4 acc[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = f4_zero();
-  // the epilogue's own row inputs (LayerNorm-backward rows, residuals), issued now so
-  // they land during the K loop instead of adding a round trip at the workgroup's end
+  // the epilogue's own row inputs (LayerNorm-backward rows, residuals), issued before the
+  // K loop so they land during it instead of adding a round trip at the workgroup's end;
+  // when they are many (more than 64 per lane: the C3 LayerNorm-backward panel holds 136,
+  // ~300 registers with the accumulators, one wave per SIMD) the epilogue streams them
+  // row by row after the loop instead
+  constexpr bool STREAM_EPI = sizeof(typename Op::template Epi<NT>) > 64 * sizeof(float);
   typename Op::template Epi<NT> es;
-  op.epi_load(es, m0 + w * 16 + 4 * lg, n0 + lr, total);
+  if constexpr (!STREAM_EPI) op.epi_load(es, m0 + w * 16 + 4 * lg, n0 + lr, total);
 
-  load(0);
-  store(0);
-  lds_barrier();
-  for (int k0 = 0; k0 < op.K; k0 += BKT) {
-    const bool more = k0 + BKT < op.K;
+  auto chunk = [&](int k0, bool more) {
     if (more) load(k0 + BKT);
     const float* arow = As + (w * 16 + lr) * LDAT + lg;
     // operands of k-step ks+1 read from LDS while the MFMAs of step ks run; steps past
@@ -269,9 +269,19 @@ __global__ __launch_bounds__(256) void rowpanel_kernel(Op op) {
       store(k0 + BKT);
       lds_barrier();
     }
-  }
+  };
+
+  load(0);
+  store(0);
+  lds_barrier();
+  int k0 = 0;
+  for (; k0 + BKT < op.K; k0 += BKT) chunk(k0, true);
+  chunk(k0, false);
   // acc[t][r] = C[m0 + 16w + 4lg + r][n0 + 16t + lr]
-  op.epilogue(acc, es, m0 + w * 16 + 4 * lg, n0 + lr, total);
+  if constexpr (STREAM_EPI)
+    op.epilogue_stream(acc, m0 + w * 16 + 4 * lg, n0 + lr, total);
+  else
+    op.epilogue(acc, es, m0 + w * 16 + 4 * lg, n0 + lr, total);
 }
 
 // bf16-operand row panel (autocast_dtype = bfloat16: the projections' matmuls in bf16
@@ -811,6 +821,19 @@ struct OpLnUvqkBwd : NoStats {
     }
   }
   template <int NT>
+  __device__ void row_in(float2& st, float (&xv)[NT], float (&dyv)[NT], int64_t m, int ncol,
+                         int64_t total) const {
+    const int64_t mc = clamp_row(m, total);
+    st = ld_f2(x_stats, mc);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int n = ncol + 16 * t;
+      const int nc = n < N ? n : N - 1;
+      xv[t] = as_global(x)[mc * ldx + nc];
+      dyv[t] = dy ? as_global(dy)[mc * lddy + nc] : 0.f;
+    }
+  }
+  template <int NT>
   __device__ void row_out(const f4 (&acc)[NT], int r, float2 st, const float* xv, const float* dyv,
                           int64_t m, int ncol, int64_t total) const {
     const bool row_ok = m < total;
@@ -840,6 +863,19 @@ struct OpLnUvqkBwd : NoStats {
   __device__ void epilogue(f4 (&acc)[NT], const Epi<NT>& es, int64_t mrow, int ncol, int64_t total) const {
 #pragma unroll
     for (int r = 0; r < 4; ++r) row_out(acc, r, es.st[r], es.xv[r], es.dyv[r], mrow + r, ncol, total);
+  }
+  // streamed form (f32 row panel at 256 columns): row r + 1's inputs in flight while row r
+  // is reduced and stored, two rows of registers instead of four
+  template <int NT>
+  __device__ void epilogue_stream(f4 (&acc)[NT], int64_t mrow, int ncol, int64_t total) const {
+    float2 st[2];
+    float xv[2][NT], dyv[2][NT];
+    row_in(st[0], xv[0], dyv[0], mrow, ncol, total);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (r + 1 < 4) row_in(st[(r + 1) & 1], xv[(r + 1) & 1], dyv[(r + 1) & 1], mrow + r + 1, ncol, total);
+      row_out(acc, r, st[r & 1], xv[r & 1], dyv[r & 1], mrow + r, ncol, total);
+    }
   }
 };
 

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--bf16", action="store_true", help="bf16 weight gradients (gr_wgrad2_bf16)")
     ap.add_argument("--bf16-panels", action="store_true", help="bf16 projection GEMMs (*_bf16)")
     ap.add_argument("--panel-vec", type=int, default=1, help="GR_OPT_PANEL_VEC")
+    ap.add_argument("--with-wgrad", action="store_true", help="also the per-matrix gr_wgrad calls")
     args = ap.parse_args()
     _lib.set_option("WGRAD_ROWS", args.wgrad_rows)  # before the workspace queries
     _lib.set_option("PANEL_VEC", args.panel_vec)
@@ -81,7 +82,7 @@ def main():
         _lib.call("hstu_gate_o_bwd" + sfx, P(dy), D, P(offsets), B, cap, hv, D, P(w_o), P(uvqk),
                   n_out, P(attn), hv, P(attn_stats), P(h_pre), n_out, 0.2, 7, P(seed_off),
                   P(d_uvqk), n_out, P(d_attn), hv, st)
-        if not args.bf16_panels:
+        if args.with_wgrad:
             _lib.call("gr_wgrad", P(dy), D, None, P(o_in), hv, P(offsets), B, cap, D, hv, P(dWo),
                       P(dbo), P(ws), ws.numel(), st)
             _lib.call("gr_wgrad", P(x), D, P(x_stats), P(d_uvqk), n_out, P(offsets), B, cap, D,
