@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GR_HSTU_ABI_VERSION 12
+#define GR_HSTU_ABI_VERSION 13
 
 #ifndef GR_API
 #define GR_API __attribute__((visibility("default")))
@@ -211,6 +211,22 @@ GR_API size_t hstu_bucket_map_bytes(int B, int N);
 GR_API int hstu_bucket_map(const int64_t* ts, const int64_t* offsets, int B, int N,
                     const int64_t* bucket_thr, int num_buckets, uint8_t* map, void* stream);
 
+/* hstu_rel_bias_fwd / _bwd (ABI 13) — replaces RelativeBucketedTimeAndPositionBasedBias
+ * .forward (sequential_encoders/hstu.py:96-128) for callers that materialise the bias
+ * (the module called on its own); the attention kernels never need it.
+ *   out[b, i, j] = pos_w[N - 1 + j - i] + ts_w[bucket(ts_next(b, i) - ts(b, j))]
+ * for ALL 0 <= i, j < N (causal or not, as the reference), out (B, N, N) fp32.
+ * Backward: d_pos_w (2N - 1), d_ts_w (num_buckets + 1), both overwritten, summed in a
+ * fixed order (deterministic); workspace hstu_rel_bias_bwd_workspace_size bytes.
+ */
+GR_API int hstu_rel_bias_fwd(const int64_t* ts, int B, int N, const int64_t* bucket_thr,
+                    int num_buckets, const float* pos_w, const float* ts_w, float* out,
+                    void* stream);
+GR_API size_t hstu_rel_bias_bwd_workspace_size(int B, int N, int num_buckets);
+GR_API int hstu_rel_bias_bwd(const int64_t* ts, int B, int N, const int64_t* bucket_thr,
+                    int num_buckets, const float* dout, float* d_pos_w, float* d_ts_w,
+                    void* workspace, size_t ws_bytes, void* stream);
+
 /* hstu_attn_fwd — replaces sequential_encoders/hstu.py:134-205
  * (_hstu_attention_maybe_from_cache, non-cache branch) fused with the relative bias of
  * hstu.py:96-128 (RelativeBucketedTimeAndPositionBasedBias.forward):
@@ -272,6 +288,10 @@ GR_API int hstu_attn_bwd(const float* q, const float* k, const float* v, int64_t
  * the head dims and is needed at wide heads with or without a bucket map. */
 GR_API size_t hstu_attn_bwd_bf16_workspace_size(int B, int N, int max_len, int H, int dqk,
                                                 int dv, int num_buckets);
+/* ABI 13: the workspace when `copies` (the forward's hstu_attn_bf16_copies) is passed:
+ * the wide form then needs no Q/K/V copies of its own (~100 MB per layer at C3). */
+GR_API size_t hstu_attn_bwd_bf16_workspace_size_copies(int B, int N, int max_len, int H, int dqk,
+                    int dv, int num_buckets);
 GR_API int hstu_attn_bwd_bf16(const float* q, const float* k, const float* v, int64_t ld_qk,
                               int64_t ld_v, const float* dout, int64_t ld_dout,
                               const int64_t* offsets, int B, int N, int max_len, int H, int dqk,
@@ -459,7 +479,7 @@ GR_API int gr_wgrad2_bf16(const float* a0, int64_t lda0, const float* a_stats0, 
  * reference CandidateIndex asks its top-k module for k + N0) takes a chunked exact
  * path: all scores of a chunk of items, then a per-query radix select merged with the
  * running top-k; same scores, ids and order, no fused fast path.
- * Catalogs of X >= 262,144 items with D <= 64 take a threshold-filter path (sampled
+ * Catalogs of X >= 262,144 items with D <= 256 take a threshold-filter path (sampled
  * per-query threshold, one all-query scoring pass over the bf16 copy that reads it
  * once, exact f32 rescoring of the candidates in the merge, which trusts only scores
  * above the bf16 error bound); inputs that defeat the threshold raise a device flag

@@ -875,7 +875,8 @@ static int bwd_bf16_waves(int d) { return d <= 64 ? 4 : 8; }
 }  // namespace gr
 
 // wide heads (128 < d <= 256, dqk == dv): hstu_attn_bf16w.hip
-size_t gr_attn_bwd_bf16w_workspace(int B, int N, int max_len, int H, int d, int num_buckets);
+size_t gr_attn_bwd_bf16w_workspace(int B, int N, int max_len, int H, int d, int num_buckets,
+                                   bool with_copies);
 int gr_attn_bwd_bf16w(const float* q, const float* k, const float* v, int64_t ld_qk, int64_t ld_v,
                       const float* dout, int64_t ld_dout, const int64_t* offsets, int B, int N,
                       int max_len, int H, int d, const uint8_t* map_kq, const float* pos_w,
@@ -887,9 +888,16 @@ static bool bwd_bf16_wide(int dqk, int dv) { return bf16_wide(dqk, dv); }
 extern "C" size_t hstu_attn_bwd_bf16_workspace_size(int B, int N, int max_len, int H, int dqk,
                                                     int dv, int num_buckets) {
   if (B <= 0 || N <= 0 || H <= 0 || max_len <= 0 || dqk <= 0 || dv <= 0) return 0;
-  if (bwd_bf16_wide(dqk, dv)) return gr_attn_bwd_bf16w_workspace(B, N, max_len, H, dqk, num_buckets);
+  if (bwd_bf16_wide(dqk, dv)) return gr_attn_bwd_bf16w_workspace(B, N, max_len, H, dqk, num_buckets, false);
   const int d = dqk > dv ? dqk : dv;
   return gr::bwd_bf16_slab_bytes(B, N, max_len, H, num_buckets, 16 * gr::bwd_bf16_waves(d));
+}
+
+extern "C" size_t hstu_attn_bwd_bf16_workspace_size_copies(int B, int N, int max_len, int H, int dqk,
+                                                           int dv, int num_buckets) {
+  if (B <= 0 || N <= 0 || H <= 0 || max_len <= 0 || dqk <= 0 || dv <= 0) return 0;
+  if (bwd_bf16_wide(dqk, dv)) return gr_attn_bwd_bf16w_workspace(B, N, max_len, H, dqk, num_buckets, true);
+  return hstu_attn_bwd_bf16_workspace_size(B, N, max_len, H, dqk, dv, num_buckets);
 }
 
 extern "C" int hstu_attn_bwd_bf16(const float* q, const float* k, const float* v, int64_t ld_qk,
@@ -917,7 +925,8 @@ extern "C" int hstu_attn_bwd_bf16(const float* q, const float* k, const float* v
                "hstu_attn_bwd_bf16: bucket_map given without pos_w/ts_w/dpos_w/dts_w");
   }
   if (bucket_map || wide) {
-    const size_t need = wide ? gr_attn_bwd_bf16w_workspace(B, N, max_len, H, dqk, num_buckets)
+    const size_t need = wide ? gr_attn_bwd_bf16w_workspace(B, N, max_len, H, dqk, num_buckets,
+                                                           copies != nullptr)
                              : bwd_bf16_slab_bytes(B, N, max_len, H, num_buckets, 16 * bwd_bf16_waves(d));
     GR_REQUIRE(B == 0 || max_len == 0 || (workspace && ws_bytes >= need),
                "hstu_attn_bwd_bf16: workspace %zu B < %zu B", ws_bytes, need);

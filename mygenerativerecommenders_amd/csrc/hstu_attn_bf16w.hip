@@ -870,10 +870,13 @@ int gr_attn_fwd_bf16w(const void* copies, const int64_t* offsets, int B, int N, 
 
 // workspace: slabs | dS blocks | dO copy + zero row | Q, K, V copies (used when the caller
 // passes none)
-size_t gr_attn_bwd_bf16w_workspace(int B, int N, int max_len, int H, int d, int num_buckets) {
+// own Q/K/V copies sit at the end: a caller passing the forward's copies needs none
+size_t gr_attn_bwd_bf16w_workspace(int B, int N, int max_len, int H, int d, int num_buckets,
+                                   bool with_copies) {
   using namespace gr;
   return al256(bf16w_slab_bytes(B, N, max_len, H, num_buckets)) + al256(bf16w_ds_bytes(B, N, H)) +
-         bf16w_copy_bytes(B, N, H, d) + al256(ceil_div(d, 32) * 64) + bf16w_copies_bytes(B, N, H, d);
+         bf16w_copy_bytes(B, N, H, d) + al256(ceil_div(d, 32) * 64) +
+         (with_copies ? 0 : bf16w_copies_bytes(B, N, H, d));
 }
 
 int gr_attn_bwd_bf16w(const float* q, const float* k, const float* v, int64_t ld_qk, int64_t ld_v,

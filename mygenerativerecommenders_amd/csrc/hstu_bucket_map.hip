@@ -105,3 +105,136 @@ extern "C" int hstu_bucket_map(const int64_t* ts, const int64_t* offsets, int B,
   GR_LAUNCH_CHECK("hstu_bucket_map");
   return 0;
 }
+
+// ------------------------------------------------------------------ materialised bias
+// RelativeBucketedTimeAndPositionBasedBias.forward (hstu.py:96-128) for callers that
+// want the (B, N, N) tensor itself (debug hooks, the module called on its own); the
+// attention kernels never use it.  bias[b, i, j] = pos_w[N - 1 + j - i]
+//   + ts_w[bucket(ts_next(b, i) - ts(b, j))] over ALL (i, j), causal or not, as the
+// reference computes it.  Backward: d_pos_w by diagonal (one thread per offset, b and i
+// in order) and d_ts_w by per-row bucket sums (slabs, then a fixed-order reduce): both
+// deterministic, no float atomics.
+namespace gr {
+
+__global__ __launch_bounds__(256) void rel_bias_fwd_kernel(const int64_t* ts, int B, int N,
+                                                           const int64_t* thr_g, int nb,
+                                                           const float* pos_w, const float* ts_w,
+                                                           float* out) {
+  __shared__ int64_t thr[256];
+  for (int i = threadIdx.x; i <= nb; i += 256) thr[i] = thr_g[i];
+  __syncthreads();
+  const int64_t row = blockIdx.x;  // (b, i)
+  const int b = (int)(row / N), i = (int)(row % N);
+  const int64_t tq = ts[(int64_t)b * N + (i + 1 < N ? i + 1 : N - 1)];
+  for (int j = threadIdx.x; j < N; j += 256) {
+    const int bk = time_bucket(tq - ts[(int64_t)b * N + j], thr, nb);
+    out[row * N + j] = pos_w[N - 1 + j - i] + ts_w[bk];
+  }
+}
+
+__global__ __launch_bounds__(256) void rel_bias_dpos_kernel(const float* dout, int B, int N,
+                                                            float* d_pos) {
+  const int r = blockIdx.x * 256 + threadIdx.x;  // j - i + N - 1
+  if (r >= 2 * N - 1) return;
+  const int dlt = r - (N - 1);
+  const int i0 = dlt < 0 ? -dlt : 0, i1 = dlt < 0 ? N : N - dlt;
+  float acc = 0.f;
+  for (int b = 0; b < B; ++b)
+    for (int i = i0; i < i1; ++i) acc += dout[((int64_t)b * N + i) * N + i + dlt];
+  d_pos[r] = acc;
+}
+
+// one workgroup per (b, i) row: bucket sums of the row in j order -> slab[row][nb + 1]
+__global__ __launch_bounds__(256) void rel_bias_dts_rows_kernel(const int64_t* ts, const float* dout,
+                                                                int B, int N, const int64_t* thr_g,
+                                                                int nb, float* slabs) {
+  __shared__ int64_t thr[256];
+  __shared__ uint8_t bk[1024];
+  __shared__ float val[1024];
+  for (int i = threadIdx.x; i <= nb; i += 256) thr[i] = thr_g[i];
+  const int64_t row = blockIdx.x;
+  const int b = (int)(row / N), i = (int)(row % N);
+  const int64_t tq = ts[(int64_t)b * N + (i + 1 < N ? i + 1 : N - 1)];
+  float acc = 0.f;  // thread t <= nb: bucket t
+  for (int j0 = 0; j0 < N; j0 += 1024) {
+    __syncthreads();
+    for (int j = threadIdx.x; j < 1024 && j0 + j < N; j += 256) {
+      bk[j] = (uint8_t)time_bucket(tq - ts[(int64_t)b * N + j0 + j], thr, nb);
+      val[j] = dout[row * N + j0 + j];
+    }
+    __syncthreads();
+    if ((int)threadIdx.x <= nb) {
+      const int n = N - j0 < 1024 ? N - j0 : 1024;
+      for (int j = 0; j < n; ++j)
+        if (bk[j] == threadIdx.x) acc += val[j];
+    }
+  }
+  if ((int)threadIdx.x <= nb) slabs[row * (nb + 1) + threadIdx.x] = acc;
+}
+
+// one workgroup per bucket: thread t sums slab rows t, t + 256, ... in order, then a
+// fixed-order tree over the 256 partials
+__global__ __launch_bounds__(256) void rel_bias_dts_reduce_kernel(const float* slabs, int64_t rows,
+                                                                  int nb, float* d_ts) {
+  __shared__ float part[256];
+  const int c = blockIdx.x;
+  float acc = 0.f;
+  for (int64_t r = threadIdx.x; r < rows; r += 256) acc += slabs[r * (nb + 1) + c];
+  part[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) part[threadIdx.x] += part[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) d_ts[c] = part[0];
+}
+
+}  // namespace gr
+
+extern "C" int hstu_rel_bias_fwd(const int64_t* ts, int B, int N, const int64_t* bucket_thr,
+                                 int num_buckets, const float* pos_w, const float* ts_w,
+                                 float* out, void* stream) {
+  GR_REQUIRE(ts && bucket_thr && pos_w && ts_w && out, "hstu_rel_bias_fwd: null pointer");
+  GR_REQUIRE(B >= 0 && N > 0 && num_buckets > 0 && num_buckets < 256,
+             "hstu_rel_bias_fwd: bad sizes (num_buckets must be < 256)");
+  GR_REQUIRE((int64_t)B * N < 0x7fffffff, "hstu_rel_bias_fwd: B * N too large");
+  if (B == 0) return 0;
+  hipLaunchKernelGGL(gr::rel_bias_fwd_kernel, dim3(B * N), dim3(256), 0, (hipStream_t)stream, ts,
+                     B, N, bucket_thr, num_buckets, pos_w, ts_w, out);
+  GR_LAUNCH_CHECK("hstu_rel_bias_fwd");
+  return 0;
+}
+
+extern "C" size_t hstu_rel_bias_bwd_workspace_size(int B, int N, int num_buckets) {
+  if (B <= 0 || N <= 0 || num_buckets <= 0) return 0;
+  return sizeof(float) * (size_t)B * N * (num_buckets + 1);
+}
+
+extern "C" int hstu_rel_bias_bwd(const int64_t* ts, int B, int N, const int64_t* bucket_thr,
+                                 int num_buckets, const float* dout, float* d_pos_w,
+                                 float* d_ts_w, void* workspace, size_t ws_bytes, void* stream) {
+  GR_REQUIRE(ts && bucket_thr && dout && d_pos_w && d_ts_w, "hstu_rel_bias_bwd: null pointer");
+  GR_REQUIRE(B >= 0 && N > 0 && num_buckets > 0 && num_buckets < 256,
+             "hstu_rel_bias_bwd: bad sizes (num_buckets must be < 256)");
+  GR_REQUIRE((int64_t)B * N < 0x7fffffff, "hstu_rel_bias_bwd: B * N too large");
+  const hipStream_t st = (hipStream_t)stream;
+  if (B == 0) {
+    gr::zero_words_async(d_pos_w, 2 * N - 1, st);
+    gr::zero_words_async(d_ts_w, num_buckets + 1, st);
+    return 0;
+  }
+  const size_t need = hstu_rel_bias_bwd_workspace_size(B, N, num_buckets);
+  GR_REQUIRE(workspace && ws_bytes >= need, "hstu_rel_bias_bwd: workspace %zu B < %zu B",
+             ws_bytes, need);
+  float* slabs = (float*)workspace;
+  hipLaunchKernelGGL(gr::rel_bias_dpos_kernel, dim3((2 * N - 1 + 255) / 256), dim3(256), 0, st,
+                     dout, B, N, d_pos_w);
+  GR_LAUNCH_CHECK("hstu_rel_bias_bwd(dpos)");
+  hipLaunchKernelGGL(gr::rel_bias_dts_rows_kernel, dim3(B * N), dim3(256), 0, st, ts, dout, B, N,
+                     bucket_thr, num_buckets, slabs);
+  GR_LAUNCH_CHECK("hstu_rel_bias_bwd(dts rows)");
+  hipLaunchKernelGGL(gr::rel_bias_dts_reduce_kernel, dim3(num_buckets + 1), dim3(256), 0, st,
+                     slabs, (int64_t)B * N, num_buckets, d_ts_w);
+  GR_LAUNCH_CHECK("hstu_rel_bias_bwd(dts reduce)");
+  return 0;
+}

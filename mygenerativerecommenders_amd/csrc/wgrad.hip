@@ -898,7 +898,12 @@ extern "C" size_t gr_wgrad_workspace_size(int64_t max_rows, int Ka, int Nb) {
   if (max_rows <= 0 || Ka <= 0 || Nb <= 0) return 0;
   const int ka[2] = {Ka, 0}, nb[2] = {Nb, 0};
   const WgPlan pl = wgrad_plan(max_rows, ka, nb);
-  return align256w(pl.slab_bytes[0]);
+  size_t need = align256w(pl.slab_bytes[0]);
+  if (Ka <= WGW_T) {  // gr_wgrad takes the wide plan at 128 < Ka <= 256 (wgrad_wide_ok)
+    const WgPlan pw = wgrad_plan_wide(max_rows, ka, nb);
+    need = std::max(need, align256w(pw.slab_bytes[0]));
+  }
+  return need;
 }
 
 extern "C" size_t gr_wgrad2_workspace_size(int64_t max_rows, int Ka0, int Nb0, int Ka1, int Nb1) {

@@ -10,7 +10,8 @@ Here:
     ``bucket_bytes`` are used when the flat buffer is large (ml-20m scale).
   * ``ShardedCandidateIndex``: the item table is row-sharded (rank r holds rows
     [r*X/P, (r+1)*X/P)); each rank runs the fused local top-k, the (B, k) score /
-    index / id lists are all-gathered (12 B x B x k per rank) and merged on device.
+    index / id lists are all-gathered as one packed (B, k, 20 B) buffer and merged on
+    device.
 """
 from __future__ import annotations
 
@@ -223,9 +224,14 @@ class BucketedGradReducer:
         for h in self._handles:
             if h is not None:
                 h.wait()
-        if self.world > 1:  # scatter the averaged rows into the dense gradients
+        if self.world > 1:  # the averaged rows into an otherwise zero dense gradient:
+            # rows outside the support are zero by the caller's promise, so a broken
+            # promise shows as a gradient that differs from the dense exchange rather than
+            # as ranks that silently keep different local rows
             for p, rows in self.rows.items():
-                p.grad.index_copy_(0, rows, self.slot[p][1])
+                g = torch.zeros_like(p)
+                g.index_copy_(0, rows, self.slot[p][1])
+                p.grad = g
         if used is not None:
             for p, u in zip(self.params, used.tolist()):
                 if u == 0.0:
@@ -313,13 +319,22 @@ def gather_and_merge(scores, ids, index, k, group=None, merge_fn=None):
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
         return ids, scores
     P = dist.get_world_size(group)
-    gs = [torch.empty_like(scores) for _ in range(P)]
-    gi = [torch.empty_like(ids) for _ in range(P)]
-    gx = [torch.empty_like(index) for _ in range(P)]
-    dist.all_gather(gs, scores.contiguous(), group=group)
-    dist.all_gather(gi, ids.contiguous(), group=group)
-    dist.all_gather(gx, index.contiguous(), group=group)
-    ms, mi = merge_fn(torch.stack(gs), torch.stack(gx), torch.stack(gi), k)
+    B, kk = scores.shape
+    # ONE collective: (score f32 | id i64 | index i64) packed as 5 int32 words per entry
+    # (20 B x B x k per rank) instead of three all-gathers of 4 + 8 + 8 B
+    packed = torch.cat([scores.float().contiguous().view(torch.int32).unsqueeze(-1),
+                        ids.to(torch.int64).contiguous().view(torch.int32).view(B, kk, 2),
+                        index.to(torch.int64).contiguous().view(torch.int32).view(B, kk, 2)],
+                       dim=-1).contiguous()
+    out = torch.empty((P,) + tuple(packed.shape), dtype=torch.int32, device=packed.device)
+    try:
+        dist.all_gather_into_tensor(out, packed, group=group)
+    except (RuntimeError, NotImplementedError, AttributeError):  # backends without it
+        dist.all_gather(list(out.unbind(0)), packed, group=group)
+    gs = out[..., 0].contiguous().view(torch.float32)
+    gi = out[..., 1:3].contiguous().view(torch.int64).squeeze(-1)
+    gx = out[..., 3:5].contiguous().view(torch.int64).squeeze(-1)
+    ms, mi = merge_fn(gs, gx, gi, k)
     return mi, ms
 
 

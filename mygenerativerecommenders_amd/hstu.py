@@ -8,8 +8,9 @@ state-dict keys as the reference (``hstu.py:71-128, 208-672``), so checkpoints
 round-trip.  The compute is the fused jagged path: per layer 3 launches forward
 (LN+UVQK+SiLU GEMM, attention with in-kernel relative bias, gate+LN+O GEMM+residual)
 and 5 backward; nothing of size (B, N, N) is materialised.  ``concat_ua=True``
-(hstu.py:398-400) runs the concatenated gate [u, LN(a), u*LN(a)] in the same fused
-kernels (linear_dim * num_heads <= 64).  ``autocast_dtype=torch.bfloat16`` (an extension
+(hstu.py:398-400) runs the concatenated gate [u, LN(a), u*LN(a)] at any width (the
+row-wave kernels with W_o in LDS up to linear_dim * num_heads = 64 and D = 128, the
+streamed-W_o form beyond).  ``autocast_dtype=torch.bfloat16`` (an extension
 of the reference constructor, whose HSTUJagged takes it) selects bf16 MFMA operands.
 
 Not supported (raise): the incremental-decoding cache path (``delta_x_offsets`` /
@@ -46,10 +47,11 @@ class RelativeAttentionBiasModule(torch.nn.Module):
 
 
 class RelativeBucketedTimeAndPositionBasedBias(RelativeAttentionBiasModule):
-    """Parameter holder for the relative position + time bias (hstu.py:71-128).
+    """Relative position + time bias (hstu.py:71-128).
 
     ``_ts_w`` (num_buckets + 1) and ``_pos_w`` (2 * max_seq_len - 1), N(0, 0.02).
-    The bias itself is never materialised: ``hstu_attn_fwd`` rebuilds it per tile.
+    Inside the encoder the bias is never materialised (the attention kernels rebuild it
+    per tile); ``forward`` materialises it for callers that use the module on its own.
     """
 
     def __init__(self, max_seq_len: int, num_buckets: int,
@@ -67,8 +69,10 @@ class RelativeBucketedTimeAndPositionBasedBias(RelativeAttentionBiasModule):
         self._bucketization_fn = bucketization_fn
 
     def forward(self, all_timestamps: torch.Tensor) -> torch.Tensor:
-        raise NotImplementedError(
-            "the (B, N, N) bias is fused into hstu_attn_fwd and never materialised")
+        """(B, N) int64 timestamps -> (B, N, N) bias, N = max_seq_len (hstu.py:96-128),
+        materialised by ``hstu_rel_bias_fwd`` with gradients to ``_pos_w`` / ``_ts_w``.
+        The encoder never calls this: its attention rebuilds the bias per tile."""
+        return ops.rel_bias(all_timestamps, self._max_seq_len, self._pos_w, self._ts_w)
 
 
 class SequentialTransductionUnitJagged(torch.nn.Module):

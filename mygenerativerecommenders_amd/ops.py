@@ -204,6 +204,54 @@ def bucket_map(timestamps: torch.Tensor, offsets: torch.Tensor, N: int) -> torch
     return out
 
 
+class _RelBias(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ts, N, pos_w, ts_w):
+        B = ts.shape[0]
+        thr = bucket_thresholds(ts.device)
+        out = torch.empty(B, N, N, dtype=torch.float32, device=ts.device)
+        pw, tw = pos_w.detach().float().contiguous(), ts_w.detach().float().contiguous()
+        _lib.call("hstu_rel_bias_fwd", ts.data_ptr(), B, N, thr.data_ptr(), NUM_BUCKETS,
+                  pw.data_ptr(), tw.data_ptr(), out.data_ptr(), _stream())
+        ctx.save_for_backward(ts)
+        ctx.N = N
+        ctx.shapes = (pos_w.shape, ts_w.shape)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (ts,) = ctx.saved_tensors
+        N = ctx.N
+        B = ts.shape[0]
+        g = g.float().contiguous()
+        d_pos = torch.empty(2 * N - 1, dtype=torch.float32, device=g.device)
+        d_ts = torch.empty(NUM_BUCKETS + 1, dtype=torch.float32, device=g.device)
+        ws_n = _lib.lib().hstu_rel_bias_bwd_workspace_size(B, N, NUM_BUCKETS)
+        ws = torch.empty(max(ws_n, 4), dtype=torch.uint8, device=g.device)
+        _lib.call("hstu_rel_bias_bwd", ts.data_ptr(), B, N, bucket_thresholds(g.device).data_ptr(),
+                  NUM_BUCKETS, g.data_ptr(), d_pos.data_ptr(), d_ts.data_ptr(), ws.data_ptr(),
+                  ws_n, _stream())
+        pshape, tshape = ctx.shapes
+        d_pos_full = d_pos
+        if pshape[0] != 2 * N - 1:  # pos_w longer than 2N - 1: only its head is used
+            d_pos_full = torch.zeros(pshape, dtype=torch.float32, device=g.device)
+            d_pos_full[:2 * N - 1] = d_pos
+        return None, None, d_pos_full, d_ts
+
+
+def rel_bias(timestamps: torch.Tensor, N: int, pos_w: torch.Tensor,
+             ts_w: torch.Tensor) -> torch.Tensor:
+    """RelativeBucketedTimeAndPositionBasedBias.forward (hstu.py:96-128): (B, N) int64
+    timestamps -> (B, N, N) fp32 bias over all (i, j), differentiable in pos_w / ts_w."""
+    _lib.require_gpu(timestamps, pos_w, ts_w)
+    ts = timestamps.to(torch.int64).contiguous()
+    if ts.dim() != 2 or ts.shape[1] != N:
+        raise ValueError(f"timestamps must be (B, {N}), got {tuple(ts.shape)}")
+    if pos_w.numel() < 2 * N - 1 or ts_w.numel() != NUM_BUCKETS + 1:
+        raise ValueError("rel_bias: pos_w needs >= 2N - 1 entries and ts_w num_buckets + 1")
+    return _RelBias.apply(ts, int(N), pos_w, ts_w)
+
+
 # ------------------------------------------------------------------ fused STU layer
 
 @dataclass
@@ -378,8 +426,9 @@ class STULayerFunction(torch.autograd.Function):
             d_pos_w = torch.empty(2 * geo.N - 1, dtype=torch.float32, device=dev)
             d_ts_w = torch.empty(NUM_BUCKETS + 1, dtype=torch.float32, device=dev)
         if bmap is not None or geo.bf16:  # wide bf16 heads use the workspace without a map too
-            ws_a_n = (L.hstu_attn_bwd_bf16_workspace_size(B, geo.N, geo.max_len, H, dqk, dv,
-                                                          NUM_BUCKETS) if geo.bf16 else
+            ws_fn = (L.hstu_attn_bwd_bf16_workspace_size_copies if copies is not None else
+                     L.hstu_attn_bwd_bf16_workspace_size)
+            ws_a_n = (ws_fn(B, geo.N, geo.max_len, H, dqk, dv, NUM_BUCKETS) if geo.bf16 else
                       L.hstu_attn_bwd_workspace_size(B, geo.N, geo.max_len, H, NUM_BUCKETS))
             ws_a = torch.empty(max(ws_a_n, 4), dtype=torch.uint8, device=dev)
         q = uvqk[:, 2 * hv:2 * hv + hq]

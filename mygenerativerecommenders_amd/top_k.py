@@ -48,18 +48,33 @@ class PackedItems:
         _lib.call("mips_pack_items", items.data_ptr(), self.X, self.D, self.buf.data_ptr(),
                   _lib.stream_handle())
         self.device = items.device
-        self._ws = {}  # (B, k, N0) -> (bytes, reusable workspace): no per-call allocation
+        # one grow-only workspace per stream (stream-ordered reuse: calls on one stream
+        # never overlap; two streams get two buffers).  A grown buffer's predecessor is
+        # kept alive (a captured graph may still point at it); growth at least doubles,
+        # so few are ever retired.
+        self._ws = {}        # stream handle -> (bytes, workspace)
+        self._retired = []
+        self._need = {}      # (B, k, N0) -> bytes
 
     def workspace(self, B: int, k: int, N0: int):
-        """The cached workspace for a (B, k, N0) call (stream-ordered reuse: calls on one
-        stream never overlap)."""
+        """(bytes needed, a workspace of at least that many bytes) for a (B, k, N0) call
+        on the current stream."""
         key = (B, k, N0)
-        ent = self._ws.get(key)
-        if ent is None:
+        n = self._need.get(key)
+        if n is None:
             n = topk_workspace_bytes(B, self.X, self.D, k, N0)
-            ent = (n, torch.empty(n, dtype=torch.uint8, device=self.device))
-            self._ws[key] = ent
-        return ent
+            self._need[key] = n
+        sk = _lib.stream_handle() or 0
+        ent = self._ws.get(sk)
+        if ent is None or ent[1].numel() < n:
+            if ent is not None:
+                self._retired.append(ent[1])
+                n_alloc = max(n, 2 * ent[1].numel())
+            else:
+                n_alloc = n
+            ent = (n_alloc, torch.empty(n_alloc, dtype=torch.uint8, device=self.device))
+            self._ws[sk] = ent
+        return n, ent[1]
 
 
 K_MAX = 4096

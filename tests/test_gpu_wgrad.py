@@ -107,3 +107,24 @@ def test_wgrad2_layer_shapes(bf16, D, n_out, hv):
     _check(c0, r0, "C0")
     _check(c1, r1, "C1")
     _check(cs1, rcs, "colsum1")
+
+
+@pytest.mark.parametrize("Ka,Nb", [(256, 1024), (256, 256)])
+def test_wgrad_single_wide_many_rows(Ka, Nb):
+    """gr_wgrad at 128 < Ka <= 256 takes the wide plan; at C3 row counts (~65K rows) its
+    slabs are larger than the narrow plan's, so gr_wgrad_workspace_size must size for it
+    (the single-GEMM paths: frozen _o or frozen _uvqk at D = 256)."""
+    L = _lib()
+    offs, total, cap, a, b, st = _case([2059] * 32, Ka, Nb, 7 + Ka + Nb)
+    lib = L.lib()
+    ws_n = lib.gr_wgrad_workspace_size(cap, Ka, Nb)
+    ws = torch.empty(max(ws_n, 4), dtype=torch.uint8, device="cuda")
+    c = torch.full((Ka, Nb), float("nan"), device="cuda")
+    cs = torch.full((Ka,), float("nan"), device="cuda")
+    L.call("gr_wgrad", a.data_ptr(), Ka, st.data_ptr(), b.data_ptr(), Nb, offs.data_ptr(),
+           offs.numel() - 1, cap, Ka, Nb, c.data_ptr(), cs.data_ptr(), ws.data_ptr(), ws_n,
+           L.stream_handle())
+    torch.cuda.synchronize()
+    rc, rcs = _ref(a, b, st, total)
+    _check(c, rc, "C")
+    _check(cs, rcs, "colsum")
