@@ -455,6 +455,18 @@ GR_API int gr_wgrad2_bf16(const float* a0, int64_t lda0, const float* a_stats0, 
                           const int64_t* offsets, int B, int64_t max_rows, void* workspace,
                           size_t ws_bytes, void* stream);
 
+/* gr_wgrad_multi (ABI 13) — the weight gradients of several problems in ONE partial
+ * launch and ONE fixed-order reduce (the encoder's backward defers every layer's _uvqk
+ * and _o gradients to one call: 2 launches per step instead of 2 per layer).
+ * desc: n_problems (1..16) x 9 int64 {a, lda, a_stats, b, ldb, Ka, Nb, c, colsum} with
+ * the meaning of gr_wgrad's arguments (pointers as integers; a_stats, colsum may be 0).
+ * All problems share the jagged rows (offsets, B, max_rows); at most two distinct panel
+ * widths (the narrow kernels' classes).  bf16: bf16 operands as gr_wgrad2_bf16.
+ * Deterministic (fixed-order slab reduce, no atomics). */
+GR_API size_t gr_wgrad_multi_workspace_size(const int64_t* desc, int n_problems, int64_t max_rows);
+GR_API int gr_wgrad_multi(const int64_t* desc, int n_problems, const int64_t* offsets, int B,
+                    int64_t max_rows, int bf16, void* workspace, size_t ws_bytes, void* stream);
+
 /* ---------------------------------------------------------------- MIPS retrieval
  * Replaces indexing/top_k.py:44-70 (MIPSBruteForceTopK: mm + torch.topk) and
  * indexing/candidate_index.py:107-164 (get_top_k_outputs: top-(k+N0), drop the row's

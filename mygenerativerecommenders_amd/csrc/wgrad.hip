@@ -45,13 +45,28 @@ struct WgradProb {
   float* colsum;
 };
 
+// Up to WG_MAXP problems per launch (a layer's two, or every layer's of an encoder at
+// once: gr_wgrad_multi).  Problems come in two panel classes (kind 0 / 1: NT0 / NT1 of
+// the narrow kernels); pan0 / blk0 are the prefix sums of panels / reduce blocks.
+constexpr int WG_MAXP = 16;
 struct WgradArgs {
-  WgradProb p[2];
+  WgradProb p[WG_MAXP];
+  int np;
+  int kind[WG_MAXP];
+  int pan0[WG_MAXP + 1];
+  int blk0[WG_MAXP + 1];
   const int64_t* offsets;
   int B;
   int64_t rows_per_split;
   int n_splits;
 };
+
+// problem owning item x of a prefix table (scalar: kernel arguments are wave-uniform)
+__device__ __forceinline__ int wg_find(const int* pre, int np, int x) {
+  int i = 0;
+  while (i + 1 < np && x >= pre[i + 1]) ++i;
+  return i;
+}
 
 // sum of a lane's partial column sum over its 4 lane groups (lanes lr, lr + 16, lr + 32,
 // lr + 48 hold rows of the same column), fixed order
@@ -235,11 +250,11 @@ template <int NT0, int NT1>
 __global__ __launch_bounds__(WG_THREADS) void wgrad_partial_kernel(WgradArgs g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int panel = blockIdx.y;
-  if (panel < g.p[0].panels)
-    wgrad_panel<NT0>(g.p[0], g.offsets, g.B, g.rows_per_split, blockIdx.x, panel, smem);
+  const int i = wg_find(g.pan0, g.np, panel);
+  if (g.kind[i] == 0)
+    wgrad_panel<NT0>(g.p[i], g.offsets, g.B, g.rows_per_split, blockIdx.x, panel - g.pan0[i], smem);
   else
-    wgrad_panel<NT1>(g.p[1], g.offsets, g.B, g.rows_per_split, blockIdx.x, panel - g.p[0].panels,
-                     smem);
+    wgrad_panel<NT1>(g.p[i], g.offsets, g.B, g.rows_per_split, blockIdx.x, panel - g.pan0[i], smem);
 }
 
 // ---------------------------------------------------------------------------- bf16
@@ -389,11 +404,11 @@ template <int NT0, int NT1>
 __global__ __launch_bounds__(WG_THREADS) void wgrad_partial_bf16_kernel(WgradArgs g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int panel = blockIdx.y;
-  if (panel < g.p[0].panels)
-    wgrad_panel_bf16<NT0>(g.p[0], g.offsets, g.B, g.rows_per_split, blockIdx.x, panel, smem);
+  const int i = wg_find(g.pan0, g.np, panel);
+  if (g.kind[i] == 0)
+    wgrad_panel_bf16<NT0>(g.p[i], g.offsets, g.B, g.rows_per_split, blockIdx.x, panel - g.pan0[i], smem);
   else
-    wgrad_panel_bf16<NT1>(g.p[1], g.offsets, g.B, g.rows_per_split, blockIdx.x,
-                          panel - g.p[0].panels, smem);
+    wgrad_panel_bf16<NT1>(g.p[i], g.offsets, g.B, g.rows_per_split, blockIdx.x, panel - g.pan0[i], smem);
 }
 
 // ------------------------------------------------------------------ bf16, wide (Ka <= 256)
@@ -645,25 +660,25 @@ __device__ __forceinline__ void wgrad_tile_f32w(const WgradProb& g, const int64_
 template <bool BF16>
 __global__ __launch_bounds__(WG_THREADS) void wgrad_partial_wide_kernel(WgradArgs g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int P = g.p[0].panels + g.p[1].panels;
+  const int P = g.pan0[g.np];
   const int x = blockIdx.x & 7, sl = blockIdx.x >> 3;
   const int split = (sl / P) * 8 + x, tile = sl % P;
   if (split >= g.n_splits) return;
-  const bool second = tile >= g.p[0].panels;
-  const WgradProb& p = second ? g.p[1] : g.p[0];
-  const int t = second ? tile - g.p[0].panels : tile;
+  const int i = wg_find(g.pan0, g.np, tile);
+  const WgradProb& p = g.p[i];
+  const int t = tile - g.pan0[i];
   if (BF16) wgrad_tile_bf16w(p, g.offsets, g.B, g.rows_per_split, split, t, smem);
   else wgrad_tile_f32w(p, g.offsets, g.B, g.rows_per_split, split, t, smem);
 }
 
 // out = sum over splits (fixed order): a workgroup owns 16 outputs of one problem; thread
 // (o, grp) sums splits grp, grp+16, ... 8-deep, then the 16 partials are added in grp
-// order.  Blocks [0, blocks0) reduce problem 0, the rest problem 1.
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(WgradArgs g, int blocks0) {
+// order.  Blocks [blk0[i], blk0[i + 1]) reduce problem i.
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(WgradArgs g) {
   __shared__ float part[16][17];
-  const bool second = (int)blockIdx.x >= blocks0;
-  const WgradProb& p = second ? g.p[1] : g.p[0];
-  const int blk = second ? blockIdx.x - blocks0 : blockIdx.x;
+  const int pi = wg_find(g.blk0, g.np, blockIdx.x);
+  const WgradProb& p = g.p[pi];
+  const int blk = blockIdx.x - g.blk0[pi];
   const int64_t ne = (int64_t)p.Ka * p.NC;
   const int o = threadIdx.x & 15, grp = threadIdx.x >> 4;
   const int64_t i = (int64_t)blk * 16 + o;
@@ -701,26 +716,50 @@ static int wgrad_nt(int nc) {
 }
 
 struct WgPlan {
-  int nt[2], panels[2], panels_nb[2];
+  int nt[2];                       // narrow panel width class of kind 0 / 1
+  int np, kind[WG_MAXP], panels[WG_MAXP], panels_nb[WG_MAXP];
   int n_splits;
   int64_t rps;
-  size_t slab_bytes[2];
+  size_t slab_bytes[WG_MAXP];
+  size_t need;                     // workspace bytes (slab regions, 256-aligned)
+  bool ok;                         // the problems fit two narrow panel classes
 };
+
+static void wg_finish(WgPlan& pl, int64_t max_rows, int64_t rps, const int* Ka, const int* Nb) {
+  pl.rps = rps;
+  pl.n_splits = (int)((max_rows + rps - 1) / rps);
+  if (pl.n_splits < 1) pl.n_splits = 1;
+  pl.need = 0;
+  for (int i = 0; i < pl.np; ++i) {
+    pl.slab_bytes[i] = Ka[i] > 0 ? sizeof(float) * (size_t)pl.n_splits * Ka[i] * (Nb[i] + 1) : 0;
+    pl.need += (pl.slab_bytes[i] + 255) & ~(size_t)255;
+  }
+}
 
 // Panels cover the Nb columns of a problem; the slabs hold Nb + 1 (the workspace query has
 // no colsum flag: column Nb is only written when a colsum is requested).  Splits so that
 // splits x panels ~ one workgroup per CU, each split a multiple of WG_CH rows.
-static WgPlan wgrad_plan(int64_t max_rows, const int Ka[2], const int Nb[2]) {
+// Problems with Ka <= 0 are absent (no panels, no slabs).
+static WgPlan wgrad_plan(int64_t max_rows, const int* Ka, const int* Nb, int np) {
   WgPlan pl{};
+  pl.np = np;
+  pl.ok = true;
+  pl.nt[0] = pl.nt[1] = 0;
   int total_panels = 0;
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < np; ++i) {
     if (Ka[i] <= 0) continue;
-    pl.nt[i] = wgrad_nt(Nb[i]);
-    const int pa = ceil_div(Ka[i], WG_KA), pb = ceil_div(Nb[i], pl.nt[i] * 16);
+    const int nt = wgrad_nt(Nb[i]);
+    int k = nt == pl.nt[0] ? 0 : nt == pl.nt[1] ? 1 : pl.nt[0] == 0 ? 0 : pl.nt[1] == 0 ? 1 : -1;
+    if (k < 0) { pl.ok = false; k = 0; }
+    pl.nt[k] = nt;
+    pl.kind[i] = k;
+    const int pa = ceil_div(Ka[i], WG_KA), pb = ceil_div(Nb[i], nt * 16);
     pl.panels[i] = pa * pb;
     pl.panels_nb[i] = pb;
     total_panels += pl.panels[i];
   }
+  if (pl.nt[0] == 0) pl.nt[0] = 4;
+  if (pl.nt[1] == 0) pl.nt[1] = 4;
   // ~2 workgroups per CU over the launch (one resident at a time: ~190 VGPRs x 8 waves),
   // >= 4 chunks each (C2 sweep of rows per split, grouped launch: 64 -> 33 us, 128 -> 30,
   // 256 -> 37, 512 -> 63, 1024 -> 116; the per-CU f32 MFMA time of a chunk is ~1.4 us)
@@ -730,11 +769,7 @@ static WgPlan wgrad_plan(int64_t max_rows, const int Ka[2], const int Nb[2]) {
   if (option(GR_OPT_WGRAD_ROWS) > 0) rps = option(GR_OPT_WGRAD_ROWS);
   rps = ((rps + WGB_CH - 1) / WGB_CH) * WGB_CH;  // whole chunks of either panel kind
   if (rps < 4 * WG_CH) rps = 4 * WG_CH;
-  pl.rps = rps;
-  pl.n_splits = (int)((max_rows + rps - 1) / rps);
-  if (pl.n_splits < 1) pl.n_splits = 1;
-  for (int i = 0; i < 2; ++i)
-    pl.slab_bytes[i] = Ka[i] > 0 ? sizeof(float) * (size_t)pl.n_splits * Ka[i] * (Nb[i] + 1) : 0;
+  wg_finish(pl, max_rows, rps, Ka, Nb);
   return pl;
 }
 
@@ -778,11 +813,11 @@ static size_t lds_of(int nt) {
   }
 }
 
-// bf16 wide plan (wgrad_tile_bf16w): Ka <= 256, one 256-wide tile per 256 columns of Nb;
+// wide plan (wgrad_tile_bf16w / _f32w): Ka <= 256, one 256-wide tile per 256 columns of Nb;
 // splits a multiple of 8 (XCD groups) with ~one workgroup per CU over the launch.
-static bool wgrad_wide_ok(const WgradProb in[2]) {
+static bool wgrad_wide_ok(const WgradProb* in, int np) {
   int kmax = 0;
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < np; ++i) {
     if (!in[i].a) continue;
     const WgradProb& p = in[i];
     if (p.Ka > WGW_T || p.Ka % 4 || p.Nb % 4 || p.lda % 4 || p.ldb % 4 ||
@@ -792,10 +827,12 @@ static bool wgrad_wide_ok(const WgradProb in[2]) {
   }
   return kmax > 128;
 }
-static WgPlan wgrad_plan_wide(int64_t max_rows, const int Ka[2], const int Nb[2]) {
+static WgPlan wgrad_plan_wide(int64_t max_rows, const int* Ka, const int* Nb, int np) {
   WgPlan pl{};
+  pl.np = np;
+  pl.ok = true;
   int tiles = 0;
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < np; ++i) {
     if (Ka[i] <= 0) continue;
     pl.panels[i] = ceil_div(Nb[i], WGW_T);
     pl.panels_nb[i] = pl.panels[i];
@@ -805,89 +842,102 @@ static WgPlan wgrad_plan_wide(int64_t max_rows, const int Ka[2], const int Nb[2]
   target = std::max(8, (target / 8) * 8);
   int64_t rps = (max_rows + target - 1) / target;
   rps = std::max<int64_t>(((rps + 31) / 32) * 32, 128);
-  pl.rps = rps;
-  pl.n_splits = std::max(1, (int)((max_rows + rps - 1) / rps));
-  for (int i = 0; i < 2; ++i)
-    pl.slab_bytes[i] = Ka[i] > 0 ? sizeof(float) * (size_t)pl.n_splits * Ka[i] * (Nb[i] + 1) : 0;
+  wg_finish(pl, max_rows, rps, Ka, Nb);
   return pl;
 }
 
-static int wgrad_run(const WgradProb in[2], const int64_t* offsets, int B, int64_t max_rows,
+static int wgrad_run(const WgradProb* in, int np, const int64_t* offsets, int B, int64_t max_rows,
                      void* workspace, size_t ws_bytes, hipStream_t st, bool bf16 = false) {
-  const int Ka[2] = {in[0].Ka, in[1].a ? in[1].Ka : 0};
-  const int Nb[2] = {in[0].Nb, in[1].a ? in[1].Nb : 0};
+  GR_REQUIRE(np >= 1 && np <= WG_MAXP, "gr_wgrad: %d problems (1..%d)", np, WG_MAXP);
+  int Ka[WG_MAXP], Nb[WG_MAXP];
+  for (int i = 0; i < np; ++i) {
+    Ka[i] = in[i].a ? in[i].Ka : 0;
+    Nb[i] = in[i].a ? in[i].Nb : 0;
+  }
   if (max_rows == 0) {
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < np; ++i) {
       if (Ka[i] <= 0) continue;
       zero_words_async(in[i].c, (int64_t)Ka[i] * Nb[i], st);
       if (in[i].colsum) zero_words_async(in[i].colsum, Ka[i], st);
     }
     return 0;
   }
-  const bool wide = wgrad_wide_ok(in);
-  const WgPlan pl = wide ? wgrad_plan_wide(max_rows, Ka, Nb) : wgrad_plan(max_rows, Ka, Nb);
-  const size_t need = align256w(pl.slab_bytes[0]) + pl.slab_bytes[1];
-  GR_REQUIRE(workspace && ws_bytes >= need, "gr_wgrad: workspace %zu B < %zu B", ws_bytes, need);
+  const bool wide = wgrad_wide_ok(in, np);
+  const WgPlan pl = wide ? wgrad_plan_wide(max_rows, Ka, Nb, np) : wgrad_plan(max_rows, Ka, Nb, np);
+  GR_REQUIRE(pl.ok, "gr_wgrad: the problems need more than two panel widths");
+  GR_REQUIRE(workspace && ws_bytes >= pl.need, "gr_wgrad: workspace %zu B < %zu B", ws_bytes, pl.need);
   WgradArgs g{};
   g.offsets = offsets;
   g.B = B;
   g.rows_per_split = pl.rps;
   g.n_splits = pl.n_splits;
+  g.np = np;
   char* ws = (char*)workspace;
-  int blocks[2] = {0, 0};
-  for (int i = 0; i < 2; ++i) {
+  size_t off = 0;
+  g.pan0[0] = g.blk0[0] = 0;
+  for (int i = 0; i < np; ++i) {
     g.p[i] = in[i];
+    g.kind[i] = pl.kind[i];
+    int blocks = 0;
     if (Ka[i] <= 0) {
       g.p[i].panels = 0;
-      continue;
+    } else {
+      g.p[i].NC = in[i].Nb + (in[i].colsum ? 1 : 0);
+      g.p[i].panels = pl.panels[i];
+      g.p[i].panels_nb = pl.panels_nb[i];
+      g.p[i].slabs = (float*)(ws + off);
+      off += align256w(pl.slab_bytes[i]);
+      blocks = (int)(((int64_t)Ka[i] * g.p[i].NC + 15) / 16);
     }
-    g.p[i].NC = in[i].Nb + (in[i].colsum ? 1 : 0);
-    g.p[i].panels = pl.panels[i];
-    g.p[i].panels_nb = pl.panels_nb[i];
-    g.p[i].slabs = (float*)(ws + (i == 0 ? 0 : align256w(pl.slab_bytes[0])));
-    blocks[i] = (int)(((int64_t)Ka[i] * g.p[i].NC + 15) / 16);
+    g.pan0[i + 1] = g.pan0[i] + g.p[i].panels;
+    g.blk0[i + 1] = g.blk0[i] + blocks;
   }
+  const int P = g.pan0[np];
   if (wide) {
-    const int P = g.p[0].panels + g.p[1].panels;
     const dim3 grid(ceil_div(pl.n_splits, 8) * 8 * P);  // XCD groups, see wgrad_partial_wide_kernel
     if (bf16)
       GR_TIMED("wgrad_partial", st, hipLaunchKernelGGL(wgrad_partial_wide_kernel<true>, grid, dim3(WG_THREADS), WGW_LDS, st, g));
     else
       GR_TIMED("wgrad_partial", st, hipLaunchKernelGGL(wgrad_partial_wide_kernel<false>, grid, dim3(WG_THREADS), WGF_LDS, st, g));
     GR_LAUNCH_CHECK("gr_wgrad(partial, wide)");
-    GR_TIMED("wgrad_reduce", st, hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks[0] + blocks[1]),
-                                                    dim3(256), 0, st, g, blocks[0]));
-    GR_LAUNCH_CHECK("gr_wgrad(reduce)");
-    return 0;
-  }
-  const int nt0 = pl.nt[0], nt1 = Ka[1] > 0 ? pl.nt[1] : 4;
-  const size_t l0 = bf16 ? lds_of_bf16(nt0) : lds_of(nt0), l1 = bf16 ? lds_of_bf16(nt1) : lds_of(nt1);
-  const size_t lds = l0 > l1 ? l0 : l1;
-  const dim3 grid(pl.n_splits, g.p[0].panels + g.p[1].panels);
-  if (bf16) {
-    GR_TIMED("wgrad_partial", st, {
-      switch (nt0) {
-        case 4: launch_partial_bf16_nt1<4>(nt1, grid, lds, st, g); break;
-        case 8: launch_partial_bf16_nt1<8>(nt1, grid, lds, st, g); break;
-        case 13: launch_partial_bf16_nt1<13>(nt1, grid, lds, st, g); break;
-        default: launch_partial_bf16_nt1<16>(nt1, grid, lds, st, g); break;
-      }
-    });
   } else {
-    GR_TIMED("wgrad_partial", st, {
-      switch (nt0) {
-        case 4: launch_partial_nt1<4>(nt1, grid, lds, st, g); break;
-        case 8: launch_partial_nt1<8>(nt1, grid, lds, st, g); break;
-        case 13: launch_partial_nt1<13>(nt1, grid, lds, st, g); break;
-        default: launch_partial_nt1<16>(nt1, grid, lds, st, g); break;
-      }
-    });
+    const int nt0 = pl.nt[0], nt1 = pl.nt[1];
+    const size_t l0 = bf16 ? lds_of_bf16(nt0) : lds_of(nt0), l1 = bf16 ? lds_of_bf16(nt1) : lds_of(nt1);
+    const size_t lds = l0 > l1 ? l0 : l1;
+    const dim3 grid(pl.n_splits, P);
+    if (bf16) {
+      GR_TIMED("wgrad_partial", st, {
+        switch (nt0) {
+          case 4: launch_partial_bf16_nt1<4>(nt1, grid, lds, st, g); break;
+          case 8: launch_partial_bf16_nt1<8>(nt1, grid, lds, st, g); break;
+          case 13: launch_partial_bf16_nt1<13>(nt1, grid, lds, st, g); break;
+          default: launch_partial_bf16_nt1<16>(nt1, grid, lds, st, g); break;
+        }
+      });
+    } else {
+      GR_TIMED("wgrad_partial", st, {
+        switch (nt0) {
+          case 4: launch_partial_nt1<4>(nt1, grid, lds, st, g); break;
+          case 8: launch_partial_nt1<8>(nt1, grid, lds, st, g); break;
+          case 13: launch_partial_nt1<13>(nt1, grid, lds, st, g); break;
+          default: launch_partial_nt1<16>(nt1, grid, lds, st, g); break;
+        }
+      });
+    }
+    GR_LAUNCH_CHECK("gr_wgrad(partial)");
   }
-  GR_LAUNCH_CHECK("gr_wgrad(partial)");
-  GR_TIMED("wgrad_reduce", st, hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks[0] + blocks[1]),
-                                                  dim3(256), 0, st, g, blocks[0]));
+  GR_TIMED("wgrad_reduce", st, hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(g.blk0[np]), dim3(256), 0, st, g));
   GR_LAUNCH_CHECK("gr_wgrad(reduce)");
   return 0;
+}
+
+// workspace of a problem list: the larger of the narrow and (when it may be taken) wide plans
+static size_t wgrad_ws_need(const int* Ka, const int* Nb, int np, int64_t max_rows) {
+  size_t need = wgrad_plan(max_rows, Ka, Nb, np).need;
+  int kmax = 0;
+  for (int i = 0; i < np; ++i) kmax = std::max(kmax, Ka[i]);
+  if (kmax <= WGW_T) need = std::max(need, wgrad_plan_wide(max_rows, Ka, Nb, np).need);
+  return need;
 }
 
 }  // namespace gr
@@ -896,26 +946,14 @@ using namespace gr;
 
 extern "C" size_t gr_wgrad_workspace_size(int64_t max_rows, int Ka, int Nb) {
   if (max_rows <= 0 || Ka <= 0 || Nb <= 0) return 0;
-  const int ka[2] = {Ka, 0}, nb[2] = {Nb, 0};
-  const WgPlan pl = wgrad_plan(max_rows, ka, nb);
-  size_t need = align256w(pl.slab_bytes[0]);
-  if (Ka <= WGW_T) {  // gr_wgrad takes the wide plan at 128 < Ka <= 256 (wgrad_wide_ok)
-    const WgPlan pw = wgrad_plan_wide(max_rows, ka, nb);
-    need = std::max(need, align256w(pw.slab_bytes[0]));
-  }
-  return need;
+  const int ka[1] = {Ka}, nb[1] = {Nb};
+  return wgrad_ws_need(ka, nb, 1, max_rows);
 }
 
 extern "C" size_t gr_wgrad2_workspace_size(int64_t max_rows, int Ka0, int Nb0, int Ka1, int Nb1) {
   if (max_rows <= 0 || Ka0 <= 0 || Nb0 <= 0 || Ka1 < 0 || Nb1 < 0) return 0;
   const int ka[2] = {Ka0, Nb1 > 0 ? Ka1 : 0}, nb[2] = {Nb0, Ka1 > 0 ? Nb1 : 0};
-  const WgPlan pl = wgrad_plan(max_rows, ka, nb);
-  size_t need = align256w(pl.slab_bytes[0]) + pl.slab_bytes[1];
-  if (std::max(ka[0], ka[1]) <= WGW_T) {  // the wide bf16 plan may split differently
-    const WgPlan pw = wgrad_plan_wide(max_rows, ka, nb);
-    need = std::max(need, align256w(pw.slab_bytes[0]) + pw.slab_bytes[1]);
-  }
-  return need;
+  return wgrad_ws_need(ka, nb, 2, max_rows);
 }
 
 extern "C" int gr_wgrad(const float* a, int64_t lda, const float* a_stats, const float* bm,
@@ -926,9 +964,9 @@ extern "C" int gr_wgrad(const float* a, int64_t lda, const float* a_stats, const
   GR_REQUIRE(Ka > 0 && Nb > 0 && B >= 0 && max_rows >= 0, "gr_wgrad: bad sizes");
   GR_REQUIRE(max_rows * (lda > ldb ? lda : ldb) * 4 < 0x7fffffffLL,
              "gr_wgrad: %lld rows exceed the 32-bit buffer range", (long long)max_rows);
-  WgradProb p[2] = {};
+  WgradProb p[1] = {};
   p[0] = WgradProb{a, lda, (const float2*)a_stats, bm, ldb, Ka, Nb, 0, 0, 0, nullptr, c, a_colsum};
-  return wgrad_run(p, offsets, B, max_rows, workspace, ws_bytes, (hipStream_t)stream);
+  return wgrad_run(p, 1, offsets, B, max_rows, workspace, ws_bytes, (hipStream_t)stream);
 }
 
 static int gr_wgrad2_impl(bool bf16, const float* a0, int64_t lda0, const float* a_stats0, const float* b0,
@@ -946,7 +984,7 @@ static int gr_wgrad2_impl(bool bf16, const float* a0, int64_t lda0, const float*
   WgradProb p[2] = {};
   p[0] = WgradProb{a0, lda0, (const float2*)a_stats0, b0, ldb0, Ka0, Nb0, 0, 0, 0, nullptr, c0, colsum0};
   p[1] = WgradProb{a1, lda1, (const float2*)a_stats1, b1, ldb1, Ka1, Nb1, 0, 0, 0, nullptr, c1, colsum1};
-  return wgrad_run(p, offsets, B, max_rows, workspace, ws_bytes, (hipStream_t)stream, bf16);
+  return wgrad_run(p, 2, offsets, B, max_rows, workspace, ws_bytes, (hipStream_t)stream, bf16);
 }
 extern "C" int gr_wgrad2(const float* a0, int64_t lda0, const float* a_stats0, const float* b0,
                          int64_t ldb0, int Ka0, int Nb0, float* c0, float* colsum0,
@@ -963,4 +1001,47 @@ extern "C" int gr_wgrad2_bf16(const float* a0, int64_t lda0, const float* a_stat
                          const int64_t* offsets, int B, int64_t max_rows, void* workspace,
                          size_t ws_bytes, void* stream) {
   return gr_wgrad2_impl(true, a0, lda0, a_stats0, b0, ldb0, Ka0, Nb0, c0, colsum0, a1, lda1, a_stats1, b1, ldb1, Ka1, Nb1, c1, colsum1, offsets, B, max_rows, workspace, ws_bytes, stream);
+}
+
+// ---------------------------------------------------------------- many problems at once
+// desc: 9 int64 per problem {a, lda, a_stats, b, ldb, Ka, Nb, c, colsum} (pointers as
+// integers, a_stats / colsum may be 0).
+static int wg_parse(const int64_t* desc, int np, WgradProb* p, int* Ka, int* Nb, int64_t* ldmax) {
+  GR_REQUIRE(desc && np >= 1 && np <= WG_MAXP, "gr_wgrad_multi: %d problems (1..%d)", np, WG_MAXP);
+  *ldmax = 0;
+  for (int i = 0; i < np; ++i) {
+    const int64_t* d = desc + 9 * i;
+    p[i] = WgradProb{(const float*)d[0], d[1], (const float2*)d[2], (const float*)d[3], d[4],
+                     (int)d[5], (int)d[6], 0, 0, 0, nullptr, (float*)d[7], (float*)d[8]};
+    GR_REQUIRE(p[i].a && p[i].bm && p[i].c && p[i].Ka > 0 && p[i].Nb > 0,
+               "gr_wgrad_multi: problem %d has a null pointer or an empty shape", i);
+    Ka[i] = p[i].Ka;
+    Nb[i] = p[i].Nb;
+    *ldmax = std::max(*ldmax, std::max(d[1], d[4]));
+  }
+  return 0;
+}
+
+extern "C" size_t gr_wgrad_multi_workspace_size(const int64_t* desc, int n_problems, int64_t max_rows) {
+  if (!desc || n_problems < 1 || n_problems > WG_MAXP || max_rows <= 0) return 0;
+  int Ka[WG_MAXP], Nb[WG_MAXP];
+  for (int i = 0; i < n_problems; ++i) {
+    Ka[i] = (int)desc[9 * i + 5];
+    Nb[i] = (int)desc[9 * i + 6];
+  }
+  return wgrad_ws_need(Ka, Nb, n_problems, max_rows);
+}
+
+extern "C" int gr_wgrad_multi(const int64_t* desc, int n_problems, const int64_t* offsets, int B,
+                              int64_t max_rows, int bf16, void* workspace, size_t ws_bytes,
+                              void* stream) {
+  WgradProb p[WG_MAXP] = {};
+  int Ka[WG_MAXP], Nb[WG_MAXP];
+  int64_t ld = 0;
+  if (const int rc = wg_parse(desc, n_problems, p, Ka, Nb, &ld)) return rc;
+  GR_REQUIRE(offsets && B >= 0 && max_rows >= 0, "gr_wgrad_multi: bad sizes");
+  GR_REQUIRE(max_rows * ld * 4 < 0x7fffffffLL,
+             "gr_wgrad_multi: %lld rows exceed the 32-bit buffer range", (long long)max_rows);
+  return wgrad_run(p, n_problems, offsets, B, max_rows, workspace, ws_bytes, (hipStream_t)stream,
+                   bf16 != 0);
 }
