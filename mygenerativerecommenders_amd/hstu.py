@@ -205,6 +205,9 @@ class HSTUJagged(torch.nn.Module):
         self._autocast_dtype = autocast_dtype
         for layer in self._attention_layers:
             layer._bf16 = autocast_dtype is torch.bfloat16
+        # the layers as one autograd node (ops.stu_stack: every layer's weight gradients in
+        # one launch pair); False = one node per layer (ops.stu_layer), as the reference
+        self._use_stack = True
         # one device dropout counter per encoder forward (layers hash with their own seed)
         self.register_buffer("_dropout_step", torch.zeros(1, dtype=torch.int64),
                              persistent=False)
@@ -223,6 +226,11 @@ class HSTUJagged(torch.nn.Module):
         if self.training and any(layer._dropout_ratio > 0 for layer in self._attention_layers):
             self._dropout_step.add_(1)
             step = self._dropout_step
+        stack = self._stack_params(n, max_len, bmap, return_cache_states)
+        if stack is not None:
+            geo, params, seeds = stack
+            x = ops.stu_stack(x, x_offsets, bmap, params, geo, seeds, step)
+            return x, cache_states
         for layer in self._attention_layers:
             x, cs = layer(x=x, x_offsets=x_offsets, all_timestamps=all_timestamps,
                           invalid_attn_mask=invalid_attn_mask,
@@ -232,6 +240,27 @@ class HSTUJagged(torch.nn.Module):
             if return_cache_states:
                 cache_states.append(cs)
         return x, cache_states
+
+    def _stack_params(self, n, max_len, bmap, return_cache_states):
+        """(geometry, per-layer params, dropout seeds) when the layers can run as one
+        ``ops.stu_stack`` node (same geometry, no concat_ua, no cache states), else None."""
+        if return_cache_states or not self._use_stack:
+            return None
+        layers = list(self._attention_layers)
+        geos = [layer._geometry(n, n if max_len is None else max_len) for layer in layers]
+        if any(g != geos[0] for g in geos) or geos[0].concat_ua:
+            return None
+        params = []
+        for layer in layers:
+            rab = layer._rel_attn_bias
+            has_bias = bmap is not None and rab is not None
+            if (bmap is not None) != has_bias:
+                return None  # some layers without a bias module: per-layer path
+            if has_bias and rab._pos_w.numel() != 2 * n - 1:
+                raise ValueError(f"_pos_w has {rab._pos_w.numel()} entries, expected {2 * n - 1}")
+            params.append((layer._uvqk, layer._o.weight, layer._o.bias,
+                           rab._pos_w if has_bias else None, rab._ts_w if has_bias else None))
+        return geos[0], params, [layer._dropout_seed for layer in layers]
 
     def forward(self, x, x_offsets, all_timestamps, invalid_attn_mask, delta_x_offsets=None,
                 cache=None, return_cache_states=False, max_len: Optional[int] = None):

@@ -292,6 +292,207 @@ def _pad_cat_weight(w_o: torch.Tensor, hv: int):
     return pad.reshape(D, 3 * hvp), hvp
 
 
+def _stu_forward(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGeometry, seed: int,
+                 seed_offset, grad_on: bool, needs_w_grad: bool):
+    """One STU layer forward (hstu.py:266-413): 3 launches.  Returns (y, saved) with the
+    tensors its backward needs (``_stu_backward``)."""
+    dev = x.device
+    rows, D = x.shape
+    B = offsets.numel() - 1
+    H, dv, dqk = geo.H, geo.dv, geo.dqk
+    hv, hq = H * dv, H * dqk
+    n_out = geo.n_out
+    st = _stream()
+    x = x.contiguous()
+    w_uvqk = w_uvqk.contiguous()
+    w_o = w_o.contiguous()
+    x_stats = torch.empty(rows, 2, dtype=torch.float32, device=dev)
+    uvqk = torch.empty(rows, n_out, dtype=torch.float32, device=dev)
+    # h_pre (pre-activation, for silu') and o_in (for the W_o gradient) exist only for
+    # the backward: inference / no_grad forwards skip both writes
+    h_pre = torch.empty_like(uvqk) if geo.activation and grad_on else None
+    sfx = "_bf16" if geo.bf16 else ""  # bf16 MFMA operands in the projections too
+    _lib.call("hstu_ln_uvqk_fwd" + sfx, x.data_ptr(), x.stride(0), offsets.data_ptr(), B, rows, D,
+              w_uvqk.data_ptr(), n_out, geo.eps, geo.activation, x_stats.data_ptr(),
+              _lib.ptr(h_pre), uvqk.data_ptr(), n_out, st)
+    attn = torch.empty(rows, hv, dtype=torch.float32, device=dev)
+    q = uvqk[:, 2 * hv:2 * hv + hq]
+    k = uvqk[:, 2 * hv + hq:]
+    v = uvqk[:, hv:2 * hv]
+    pos_w_c = pos_w.contiguous() if bmap is not None else None
+    ts_w_c = ts_w.contiguous() if bmap is not None else None
+    # wide bf16 heads: bf16 copies of Q, K, V that the attention kernels stage into LDS
+    # by DMA, made once here and kept for the backward
+    copies = None
+    if geo.bf16 and n_out % 2 == 0:
+        cb = _lib.lib().hstu_attn_bf16_copies_bytes(B, geo.N, H, dqk, dv)
+        if cb:
+            copies = torch.empty(cb, dtype=torch.uint8, device=dev)
+            _lib.call("hstu_attn_bf16_copies", q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out,
+                      n_out, offsets.data_ptr(), B, geo.N, H, dqk, dv, copies.data_ptr(), st)
+    if geo.bf16:
+        _lib.call("hstu_attn_fwd_bf16", q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out, n_out,
+                  offsets.data_ptr(), B, geo.N, geo.max_len, H, dqk, dv, _lib.ptr(bmap),
+                  _lib.ptr(pos_w_c), _lib.ptr(ts_w_c), NUM_BUCKETS, attn.data_ptr(), hv,
+                  _lib.ptr(copies), st)
+    else:
+        _lib.call("hstu_attn_fwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out, n_out,
+                  offsets.data_ptr(), B, geo.N, geo.max_len, H, dqk, dv, _lib.ptr(bmap),
+                  _lib.ptr(pos_w_c), _lib.ptr(ts_w_c), NUM_BUCKETS, attn.data_ptr(), hv, st)
+    attn_stats = torch.empty(rows, 2, dtype=torch.float32, device=dev)
+    needs_w_grad = grad_on and needs_w_grad
+    ow = 3 * hv if geo.concat_ua else hv  # o_in width
+    cat_wide = geo.concat_ua and _cat_wide(hv, D)
+    o_in = (torch.empty(rows, ow, dtype=torch.float32, device=dev)
+            if needs_w_grad or cat_wide else None)
+    w_pad = hvp = None
+    if geo.concat_ua and not cat_wide:
+        w_pad, hvp = _pad_cat_weight(w_o, hv)
+    y = torch.empty(rows, D, dtype=torch.float32, device=dev)
+    b_o_c = b_o.contiguous()
+    if cat_wide:
+        _lib.call("hstu_gate_o_cat_wide_fwd", uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
+                  offsets.data_ptr(), B, rows, hv, D, w_o.data_ptr(), b_o_c.data_ptr(),
+                  x.data_ptr(), x.stride(0), geo.eps, geo.dropout_p, seed,
+                  _lib.ptr(seed_offset), attn_stats.data_ptr(), o_in.data_ptr(), y.data_ptr(),
+                  D, st)
+        if not needs_w_grad:
+            o_in = None
+    elif geo.concat_ua:
+        _lib.call("hstu_gate_o_cat_fwd", uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
+                  offsets.data_ptr(), B, rows, hv, hvp, D, w_pad.data_ptr(), b_o_c.data_ptr(),
+                  x.data_ptr(), x.stride(0), geo.eps, geo.dropout_p, seed,
+                  _lib.ptr(seed_offset), attn_stats.data_ptr(), _lib.ptr(o_in), y.data_ptr(),
+                  D, st)
+    else:
+        _lib.call("hstu_gate_o_fwd" + sfx, uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
+                  offsets.data_ptr(), B, rows, hv, D, w_o.data_ptr(), b_o_c.data_ptr(),
+                  x.data_ptr(), x.stride(0), geo.eps, geo.dropout_p, seed,
+                  _lib.ptr(seed_offset), attn_stats.data_ptr(), _lib.ptr(o_in), y.data_ptr(),
+                  D, st)
+    saved = (x, offsets, bmap, w_uvqk, w_o, pos_w_c, ts_w_c, x_stats, uvqk, h_pre, attn,
+             attn_stats, o_in, copies if grad_on else None)
+    return y, saved
+
+
+def _stu_backward(saved, dy, geo: STUGeometry, seed: int, seed_offset, want_uvqk: bool,
+                  defer_wgrad: bool = False):
+    """One STU layer backward: gate_o_bwd, attention backward (+ bias reduce), ln_uvqk_bwd,
+    then the two weight-gradient GEMMs (gr_wgrad2), or -- ``defer_wgrad`` -- their
+    gr_wgrad_multi problem rows, left for the caller to launch with other layers'.
+    Returns (dx, d_w_uvqk, d_w_o, d_b_o, d_pos_w, d_ts_w, problems)."""
+    (x, offsets, bmap, w_uvqk, w_o, pos_w, ts_w, x_stats, uvqk, h_pre, attn, attn_stats,
+     o_in, copies) = saved
+    dev = x.device
+    rows, D = x.shape
+    B = offsets.numel() - 1
+    H, dv, dqk = geo.H, geo.dv, geo.dqk
+    hv, hq = H * dv, H * dqk
+    n_out = geo.n_out
+    st = _stream()
+    dy = dy.contiguous()
+    d_uvqk = torch.empty(rows, n_out, dtype=torch.float32, device=dev)
+    d_attn = torch.empty(rows, hv, dtype=torch.float32, device=dev)
+    if geo.concat_ua and _cat_wide(hv, D):
+        g_cat = torch.empty(rows, 3 * hv, dtype=torch.float32, device=dev)
+        _lib.call("hstu_gate_o_cat_wide_bwd", dy.data_ptr(), D, offsets.data_ptr(), B, rows, hv,
+                  D, w_o.data_ptr(), uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
+                  attn_stats.data_ptr(), _lib.ptr(h_pre), n_out, geo.dropout_p, seed,
+                  _lib.ptr(seed_offset), g_cat.data_ptr(), d_uvqk.data_ptr(), n_out,
+                  d_attn.data_ptr(), hv, st)
+        del g_cat
+    elif geo.concat_ua:
+        w_pad, hvp = _pad_cat_weight(w_o, hv)
+        _lib.call("hstu_gate_o_cat_bwd", dy.data_ptr(), D, offsets.data_ptr(), B, rows, hv, hvp,
+                  D, w_pad.data_ptr(), uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
+                  attn_stats.data_ptr(), _lib.ptr(h_pre), n_out, geo.dropout_p, seed,
+                  _lib.ptr(seed_offset), d_uvqk.data_ptr(), n_out, d_attn.data_ptr(), hv,
+                  st)
+    else:
+        _lib.call("hstu_gate_o_bwd" + ("_bf16" if geo.bf16 else ""), dy.data_ptr(), D,
+                  offsets.data_ptr(), B, rows, hv, D,
+                  w_o.data_ptr(), uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
+                  attn_stats.data_ptr(), _lib.ptr(h_pre), n_out, geo.dropout_p, seed,
+                  _lib.ptr(seed_offset), d_uvqk.data_ptr(), n_out, d_attn.data_ptr(), hv, st)
+    L = _lib.lib()
+    d_pos_w = d_ts_w = None
+    ws_a = None
+    ws_a_n = 0
+    if bmap is not None:
+        d_pos_w = torch.empty(2 * geo.N - 1, dtype=torch.float32, device=dev)
+        d_ts_w = torch.empty(NUM_BUCKETS + 1, dtype=torch.float32, device=dev)
+    if bmap is not None or geo.bf16:  # wide bf16 heads use the workspace without a map too
+        ws_fn = (L.hstu_attn_bwd_bf16_workspace_size_copies if copies is not None else
+                 L.hstu_attn_bwd_bf16_workspace_size)
+        ws_a_n = (ws_fn(B, geo.N, geo.max_len, H, dqk, dv, NUM_BUCKETS) if geo.bf16 else
+                  L.hstu_attn_bwd_workspace_size(B, geo.N, geo.max_len, H, NUM_BUCKETS))
+        ws_a = torch.empty(max(ws_a_n, 4), dtype=torch.uint8, device=dev)
+    q = uvqk[:, 2 * hv:2 * hv + hq]
+    k = uvqk[:, 2 * hv + hq:]
+    v = uvqk[:, hv:2 * hv]
+    if h_pre is not None:
+        hq_p = h_pre[:, 2 * hv:2 * hv + hq].data_ptr()
+        hk_p = h_pre[:, 2 * hv + hq:].data_ptr()
+        hv_p = h_pre[:, hv:2 * hv].data_ptr()
+    else:
+        hq_p = hk_p = hv_p = None
+    dq = d_uvqk[:, 2 * hv:2 * hv + hq]
+    dk = d_uvqk[:, 2 * hv + hq:]
+    dvv = d_uvqk[:, hv:2 * hv]
+    bwd_args = (q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out, n_out,
+                d_attn.data_ptr(), hv, offsets.data_ptr(), B, geo.N, geo.max_len, H, dqk, dv,
+                _lib.ptr(bmap), _lib.ptr(pos_w), _lib.ptr(ts_w), NUM_BUCKETS,
+                hq_p, hk_p, hv_p, n_out, dq.data_ptr(), dk.data_ptr(), dvv.data_ptr(), n_out,
+                _lib.ptr(d_pos_w), _lib.ptr(d_ts_w))
+    if geo.bf16:
+        _lib.call("hstu_attn_bwd_bf16", *bwd_args, _lib.ptr(copies), _lib.ptr(ws_a), ws_a_n, st)
+    else:
+        _lib.call("hstu_attn_bwd", *bwd_args, _lib.ptr(ws_a), ws_a_n, st)
+    dx = torch.empty(rows, D, dtype=torch.float32, device=dev)
+    _lib.call("hstu_ln_uvqk_bwd" + ("_bf16" if geo.bf16 else ""), d_uvqk.data_ptr(), n_out,
+              offsets.data_ptr(), B, rows, D,
+              n_out, w_uvqk.data_ptr(), x.data_ptr(), x.stride(0), x_stats.data_ptr(),
+              dy.data_ptr(), D, dx.data_ptr(), D, st)
+    # weight gradients (off the critical path): both GEMMs of the layer in one launch
+    # and one slab reduce (gr_wgrad2), or deferred to the caller's gr_wgrad_multi
+    d_w_uvqk = torch.empty(D, n_out, dtype=torch.float32, device=dev) if want_uvqk else None
+    d_w_o = d_b_o = None
+    ow = o_in.shape[1] if o_in is not None else hv  # 3 hv with concat_ua
+    if o_in is not None:
+        d_w_o = torch.empty(D, ow, dtype=torch.float32, device=dev)
+        d_b_o = torch.empty(D, dtype=torch.float32, device=dev)
+    problems = []
+    if defer_wgrad:
+        # rows of gr_wgrad_multi's descriptor {a, lda, a_stats, b, ldb, Ka, Nb, c, colsum}
+        # plus the tensors that must stay alive until the launch
+        if want_uvqk:
+            problems.append(((x.data_ptr(), x.stride(0), x_stats.data_ptr(), d_uvqk.data_ptr(),
+                              n_out, D, n_out, d_w_uvqk.data_ptr(), 0), (x, x_stats, d_uvqk)))
+        if o_in is not None:
+            problems.append(((dy.data_ptr(), D, 0, o_in.data_ptr(), ow, D, ow, d_w_o.data_ptr(),
+                              d_b_o.data_ptr()), (dy, o_in)))
+    elif want_uvqk and o_in is not None:
+        ws_n = L.gr_wgrad2_workspace_size(rows, D, n_out, D, ow)
+        ws = torch.empty(max(ws_n, 4), dtype=torch.uint8, device=dev)
+        _lib.call("gr_wgrad2_bf16" if geo.bf16 else "gr_wgrad2", x.data_ptr(), x.stride(0),
+                  x_stats.data_ptr(), d_uvqk.data_ptr(),
+                  n_out, D, n_out, d_w_uvqk.data_ptr(), None,
+                  dy.data_ptr(), D, None, o_in.data_ptr(), ow, D, ow, d_w_o.data_ptr(),
+                  d_b_o.data_ptr(), offsets.data_ptr(), B, rows, ws.data_ptr(), ws_n, st)
+    elif want_uvqk:
+        ws_n = L.gr_wgrad_workspace_size(rows, D, n_out)
+        ws = torch.empty(max(ws_n, 4), dtype=torch.uint8, device=dev)
+        _lib.call("gr_wgrad", x.data_ptr(), x.stride(0), x_stats.data_ptr(), d_uvqk.data_ptr(),
+                  n_out, offsets.data_ptr(), B, rows, D, n_out, d_w_uvqk.data_ptr(), None,
+                  ws.data_ptr(), ws_n, st)
+    elif o_in is not None:
+        ws_n = L.gr_wgrad_workspace_size(rows, D, ow)
+        ws = torch.empty(max(ws_n, 4), dtype=torch.uint8, device=dev)
+        _lib.call("gr_wgrad", dy.data_ptr(), D, None, o_in.data_ptr(), ow, offsets.data_ptr(),
+                  B, rows, D, ow, d_w_o.data_ptr(), d_b_o.data_ptr(), ws.data_ptr(), ws_n, st)
+    return dx, d_w_uvqk, d_w_o, d_b_o, d_pos_w, d_ts_w, problems
+
+
 class STULayerFunction(torch.autograd.Function):
     """One SequentialTransductionUnitJagged (hstu.py:266-413) as 3 fused launches
     forward and 6 backward.  Inputs: jagged x (rows, D), offsets (B+1), the batch's
@@ -301,82 +502,9 @@ class STULayerFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGeometry, seed: int,
                 seed_offset, grad_on: bool = True):
-        dev = x.device
-        rows, D = x.shape
-        B = offsets.numel() - 1
-        H, dv, dqk = geo.H, geo.dv, geo.dqk
-        hv, hq = H * dv, H * dqk
-        n_out = geo.n_out
-        st = _stream()
-        x = x.contiguous()
-        w_uvqk = w_uvqk.contiguous()
-        w_o = w_o.contiguous()
-        x_stats = torch.empty(rows, 2, dtype=torch.float32, device=dev)
-        uvqk = torch.empty(rows, n_out, dtype=torch.float32, device=dev)
-        # h_pre (pre-activation, for silu') and o_in (for the W_o gradient) exist only for
-        # the backward: inference / no_grad forwards skip both writes
-        h_pre = torch.empty_like(uvqk) if geo.activation and grad_on else None
-        sfx = "_bf16" if geo.bf16 else ""  # bf16 MFMA operands in the projections too
-        _lib.call("hstu_ln_uvqk_fwd" + sfx, x.data_ptr(), x.stride(0), offsets.data_ptr(), B, rows, D,
-                  w_uvqk.data_ptr(), n_out, geo.eps, geo.activation, x_stats.data_ptr(),
-                  _lib.ptr(h_pre), uvqk.data_ptr(), n_out, st)
-        attn = torch.empty(rows, hv, dtype=torch.float32, device=dev)
-        q = uvqk[:, 2 * hv:2 * hv + hq]
-        k = uvqk[:, 2 * hv + hq:]
-        v = uvqk[:, hv:2 * hv]
-        pos_w_c = pos_w.contiguous() if bmap is not None else None
-        ts_w_c = ts_w.contiguous() if bmap is not None else None
-        # wide bf16 heads: bf16 copies of Q, K, V that the attention kernels stage into LDS
-        # by DMA, made once here and kept for the backward
-        copies = None
-        if geo.bf16 and n_out % 2 == 0:
-            cb = _lib.lib().hstu_attn_bf16_copies_bytes(B, geo.N, H, dqk, dv)
-            if cb:
-                copies = torch.empty(cb, dtype=torch.uint8, device=dev)
-                _lib.call("hstu_attn_bf16_copies", q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out,
-                          n_out, offsets.data_ptr(), B, geo.N, H, dqk, dv, copies.data_ptr(), st)
-        if geo.bf16:
-            _lib.call("hstu_attn_fwd_bf16", q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out, n_out,
-                      offsets.data_ptr(), B, geo.N, geo.max_len, H, dqk, dv, _lib.ptr(bmap),
-                      _lib.ptr(pos_w_c), _lib.ptr(ts_w_c), NUM_BUCKETS, attn.data_ptr(), hv,
-                      _lib.ptr(copies), st)
-        else:
-            _lib.call("hstu_attn_fwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out, n_out,
-                      offsets.data_ptr(), B, geo.N, geo.max_len, H, dqk, dv, _lib.ptr(bmap),
-                      _lib.ptr(pos_w_c), _lib.ptr(ts_w_c), NUM_BUCKETS, attn.data_ptr(), hv, st)
-        attn_stats = torch.empty(rows, 2, dtype=torch.float32, device=dev)
-        needs_w_grad = grad_on and (w_o.requires_grad or b_o.requires_grad)
-        ow = 3 * hv if geo.concat_ua else hv  # o_in width
-        cat_wide = geo.concat_ua and _cat_wide(hv, D)
-        o_in = (torch.empty(rows, ow, dtype=torch.float32, device=dev)
-                if needs_w_grad or cat_wide else None)
-        w_pad = hvp = None
-        if geo.concat_ua and not cat_wide:
-            w_pad, hvp = _pad_cat_weight(w_o, hv)
-        y = torch.empty(rows, D, dtype=torch.float32, device=dev)
-        b_o_c = b_o.contiguous()
-        if cat_wide:
-            _lib.call("hstu_gate_o_cat_wide_fwd", uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
-                      offsets.data_ptr(), B, rows, hv, D, w_o.data_ptr(), b_o_c.data_ptr(),
-                      x.data_ptr(), x.stride(0), geo.eps, geo.dropout_p, seed,
-                      _lib.ptr(seed_offset), attn_stats.data_ptr(), o_in.data_ptr(), y.data_ptr(),
-                      D, st)
-            if not needs_w_grad:
-                o_in = None
-        elif geo.concat_ua:
-            _lib.call("hstu_gate_o_cat_fwd", uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
-                      offsets.data_ptr(), B, rows, hv, hvp, D, w_pad.data_ptr(), b_o_c.data_ptr(),
-                      x.data_ptr(), x.stride(0), geo.eps, geo.dropout_p, seed,
-                      _lib.ptr(seed_offset), attn_stats.data_ptr(), _lib.ptr(o_in), y.data_ptr(),
-                      D, st)
-        else:
-            _lib.call("hstu_gate_o_fwd" + sfx, uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
-                      offsets.data_ptr(), B, rows, hv, D, w_o.data_ptr(), b_o_c.data_ptr(),
-                      x.data_ptr(), x.stride(0), geo.eps, geo.dropout_p, seed,
-                      _lib.ptr(seed_offset), attn_stats.data_ptr(), _lib.ptr(o_in), y.data_ptr(),
-                      D, st)
-        ctx.save_for_backward(x, offsets, bmap, w_uvqk, w_o, pos_w_c, ts_w_c, x_stats, uvqk,
-                              h_pre, attn, attn_stats, o_in, copies if grad_on else None)
+        y, saved = _stu_forward(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo, seed,
+                                seed_offset, grad_on, w_o.requires_grad or b_o.requires_grad)
+        ctx.save_for_backward(*saved)
         ctx.geo = geo
         ctx.seed = seed
         ctx.seed_offset = seed_offset
@@ -384,108 +512,96 @@ class STULayerFunction(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        (x, offsets, bmap, w_uvqk, w_o, pos_w, ts_w, x_stats, uvqk, h_pre, attn, attn_stats,
-         o_in, copies) = ctx.saved_tensors
-        geo = ctx.geo
-        dev = x.device
-        rows, D = x.shape
-        B = offsets.numel() - 1
-        H, dv, dqk = geo.H, geo.dv, geo.dqk
-        hv, hq = H * dv, H * dqk
-        n_out = geo.n_out
-        st = _stream()
-        dy = dy.contiguous()
-        d_uvqk = torch.empty(rows, n_out, dtype=torch.float32, device=dev)
-        d_attn = torch.empty(rows, hv, dtype=torch.float32, device=dev)
-        if geo.concat_ua and _cat_wide(hv, D):
-            g_cat = torch.empty(rows, 3 * hv, dtype=torch.float32, device=dev)
-            _lib.call("hstu_gate_o_cat_wide_bwd", dy.data_ptr(), D, offsets.data_ptr(), B, rows, hv,
-                      D, w_o.data_ptr(), uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
-                      attn_stats.data_ptr(), _lib.ptr(h_pre), n_out, geo.dropout_p, ctx.seed,
-                      _lib.ptr(ctx.seed_offset), g_cat.data_ptr(), d_uvqk.data_ptr(), n_out,
-                      d_attn.data_ptr(), hv, st)
-            del g_cat
-        elif geo.concat_ua:
-            w_pad, hvp = _pad_cat_weight(w_o, hv)
-            _lib.call("hstu_gate_o_cat_bwd", dy.data_ptr(), D, offsets.data_ptr(), B, rows, hv, hvp,
-                      D, w_pad.data_ptr(), uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
-                      attn_stats.data_ptr(), _lib.ptr(h_pre), n_out, geo.dropout_p, ctx.seed,
-                      _lib.ptr(ctx.seed_offset), d_uvqk.data_ptr(), n_out, d_attn.data_ptr(), hv,
-                      st)
-        else:
-            _lib.call("hstu_gate_o_bwd" + ("_bf16" if geo.bf16 else ""), dy.data_ptr(), D,
-                      offsets.data_ptr(), B, rows, hv, D,
-                      w_o.data_ptr(), uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
-                      attn_stats.data_ptr(), _lib.ptr(h_pre), n_out, geo.dropout_p, ctx.seed,
-                      _lib.ptr(ctx.seed_offset), d_uvqk.data_ptr(), n_out, d_attn.data_ptr(), hv, st)
-        L = _lib.lib()
-        d_pos_w = d_ts_w = None
-        ws_a = None
-        ws_a_n = 0
-        if bmap is not None:
-            d_pos_w = torch.empty(2 * geo.N - 1, dtype=torch.float32, device=dev)
-            d_ts_w = torch.empty(NUM_BUCKETS + 1, dtype=torch.float32, device=dev)
-        if bmap is not None or geo.bf16:  # wide bf16 heads use the workspace without a map too
-            ws_fn = (L.hstu_attn_bwd_bf16_workspace_size_copies if copies is not None else
-                     L.hstu_attn_bwd_bf16_workspace_size)
-            ws_a_n = (ws_fn(B, geo.N, geo.max_len, H, dqk, dv, NUM_BUCKETS) if geo.bf16 else
-                      L.hstu_attn_bwd_workspace_size(B, geo.N, geo.max_len, H, NUM_BUCKETS))
-            ws_a = torch.empty(max(ws_a_n, 4), dtype=torch.uint8, device=dev)
-        q = uvqk[:, 2 * hv:2 * hv + hq]
-        k = uvqk[:, 2 * hv + hq:]
-        v = uvqk[:, hv:2 * hv]
-        if h_pre is not None:
-            hq_p = h_pre[:, 2 * hv:2 * hv + hq].data_ptr()
-            hk_p = h_pre[:, 2 * hv + hq:].data_ptr()
-            hv_p = h_pre[:, hv:2 * hv].data_ptr()
-        else:
-            hq_p = hk_p = hv_p = None
-        dq = d_uvqk[:, 2 * hv:2 * hv + hq]
-        dk = d_uvqk[:, 2 * hv + hq:]
-        dvv = d_uvqk[:, hv:2 * hv]
-        bwd_args = (q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out, n_out,
-                    d_attn.data_ptr(), hv, offsets.data_ptr(), B, geo.N, geo.max_len, H, dqk, dv,
-                    _lib.ptr(bmap), _lib.ptr(pos_w), _lib.ptr(ts_w), NUM_BUCKETS,
-                    hq_p, hk_p, hv_p, n_out, dq.data_ptr(), dk.data_ptr(), dvv.data_ptr(), n_out,
-                    _lib.ptr(d_pos_w), _lib.ptr(d_ts_w))
-        if geo.bf16:
-            _lib.call("hstu_attn_bwd_bf16", *bwd_args, _lib.ptr(copies), _lib.ptr(ws_a), ws_a_n, st)
-        else:
-            _lib.call("hstu_attn_bwd", *bwd_args, _lib.ptr(ws_a), ws_a_n, st)
-        dx = torch.empty(rows, D, dtype=torch.float32, device=dev)
-        _lib.call("hstu_ln_uvqk_bwd" + ("_bf16" if geo.bf16 else ""), d_uvqk.data_ptr(), n_out,
-                  offsets.data_ptr(), B, rows, D,
-                  n_out, w_uvqk.data_ptr(), x.data_ptr(), x.stride(0), x_stats.data_ptr(),
-                  dy.data_ptr(), D, dx.data_ptr(), D, st)
-        # weight gradients (off the critical path): both GEMMs of the layer in one launch
-        # and one slab reduce (gr_wgrad2)
-        want_uvqk = ctx.needs_input_grad[3]
-        d_w_uvqk = torch.empty(D, n_out, dtype=torch.float32, device=dev) if want_uvqk else None
-        d_w_o = d_b_o = None
-        ow = o_in.shape[1] if o_in is not None else hv  # 3 hv with concat_ua
-        if o_in is not None:
-            d_w_o = torch.empty(D, ow, dtype=torch.float32, device=dev)
-            d_b_o = torch.empty(D, dtype=torch.float32, device=dev)
-        if want_uvqk and o_in is not None:
-            ws_n = L.gr_wgrad2_workspace_size(rows, D, n_out, D, ow)
-            ws = torch.empty(max(ws_n, 4), dtype=torch.uint8, device=dev)
-            _lib.call("gr_wgrad2_bf16" if geo.bf16 else "gr_wgrad2", x.data_ptr(), x.stride(0),
-                      x_stats.data_ptr(), d_uvqk.data_ptr(),
-                      n_out, D, n_out, d_w_uvqk.data_ptr(), None,
-                      dy.data_ptr(), D, None, o_in.data_ptr(), ow, D, ow, d_w_o.data_ptr(),
-                      d_b_o.data_ptr(), offsets.data_ptr(), B, rows, ws.data_ptr(), ws_n, st)
-        elif want_uvqk:
-            ws_n = L.gr_wgrad_workspace_size(rows, D, n_out)
-            ws = torch.empty(max(ws_n, 4), dtype=torch.uint8, device=dev)
-            _lib.call("gr_wgrad", x.data_ptr(), x.stride(0), x_stats.data_ptr(), d_uvqk.data_ptr(),
-                      n_out, offsets.data_ptr(), B, rows, D, n_out, d_w_uvqk.data_ptr(), None,
-                      ws.data_ptr(), ws_n, st)
-        elif o_in is not None:
-            ws_n = L.gr_wgrad_workspace_size(rows, D, ow)
-            ws = torch.empty(max(ws_n, 4), dtype=torch.uint8, device=dev)
-            _lib.call("gr_wgrad", dy.data_ptr(), D, None, o_in.data_ptr(), ow, offsets.data_ptr(),
-                      B, rows, D, ow, d_w_o.data_ptr(), d_b_o.data_ptr(), ws.data_ptr(), ws_n, st)
+        dx, d_w_uvqk, d_w_o, d_b_o, d_pos_w, d_ts_w, _ = _stu_backward(
+            ctx.saved_tensors, dy, ctx.geo, ctx.seed, ctx.seed_offset, ctx.needs_input_grad[3])
         return (dx, None, None, d_w_uvqk, d_w_o, d_b_o, d_pos_w, d_ts_w, None, None, None, None)
+
+
+_SAVED_PER_LAYER = 14  # entries of _stu_forward's saved tuple
+
+
+def launch_wgrad_multi(problems, offsets, rows, bf16: bool):
+    """Launches the deferred weight-gradient problems (``_stu_backward(defer_wgrad=True)``)
+    through gr_wgrad_multi, up to 16 per launch."""
+    import numpy as np
+    if not problems:
+        return
+    L = _lib.lib()
+    B = offsets.numel() - 1
+    dev = offsets.device
+    for c0 in range(0, len(problems), 16):
+        chunk = problems[c0:c0 + 16]
+        desc = np.ascontiguousarray(np.array([p[0] for p in chunk], dtype=np.int64))
+        n = len(chunk)
+        ws_n = int(L.gr_wgrad_multi_workspace_size(desc.ctypes.data, n, rows))
+        ws = torch.empty(max(ws_n, 4), dtype=torch.uint8, device=dev)
+        _lib.call("gr_wgrad_multi", desc.ctypes.data, n, offsets.data_ptr(), B, rows,
+                  1 if bf16 else 0, ws.data_ptr(), ws_n, _stream())
+
+
+class STUStackFunction(torch.autograd.Function):
+    """Every STU layer of an encoder (HSTUJagged.jagged_forward's loop, hstu.py:467-478)
+    as ONE autograd node.  Forward: the per-layer launches of ``_stu_forward``.  Backward:
+    the per-layer critical path (gate_o_bwd, attention backward, ln_uvqk_bwd) layer by
+    layer, and the weight gradients of ALL layers afterwards in one gr_wgrad_multi (one
+    partial + one reduce launch for the encoder instead of two per layer: at ml-1m each
+    layer's pair is latency-bound, 4 x 32 us).
+    params: per layer (_uvqk, _o.weight, _o.bias, _pos_w or None, _ts_w or None)."""
+
+    @staticmethod
+    def forward(ctx, x, offsets, bmap, geo: STUGeometry, seeds, seed_offset, grad_on: bool,
+                *params):
+        n_layers = len(seeds)
+        saved_all = []
+        for l in range(n_layers):
+            w_uvqk, w_o, b_o, pos_w, ts_w = params[5 * l:5 * l + 5]
+            x, saved = _stu_forward(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo,
+                                    seeds[l], seed_offset, grad_on,
+                                    w_o.requires_grad or b_o.requires_grad)
+            if grad_on:
+                saved_all.extend(saved)
+        if grad_on:
+            ctx.save_for_backward(*saved_all)
+        ctx.geo = geo
+        ctx.seeds = seeds
+        ctx.seed_offset = seed_offset
+        return x
+
+    @staticmethod
+    def backward(ctx, dy):
+        saved = ctx.saved_tensors
+        geo = ctx.geo
+        n_layers = len(ctx.seeds)
+        grads = [None] * (5 * n_layers)
+        problems = []
+        offsets = saved[1]
+        rows = saved[0].shape[0]
+        for l in reversed(range(n_layers)):
+            sl = saved[_SAVED_PER_LAYER * l:_SAVED_PER_LAYER * (l + 1)]
+            want_uvqk = ctx.needs_input_grad[7 + 5 * l]
+            dx, d_w_uvqk, d_w_o, d_b_o, d_pos_w, d_ts_w, probs = _stu_backward(
+                sl, dy, geo, ctx.seeds[l], ctx.seed_offset, want_uvqk, defer_wgrad=True)
+            grads[5 * l:5 * l + 5] = [d_w_uvqk, d_w_o, d_b_o, d_pos_w, d_ts_w]
+            problems.extend(probs)
+            dy = dx
+        launch_wgrad_multi(problems, offsets, rows, geo.bf16)
+        return (dy, None, None, None, None, None, None, *grads)
+
+
+def stu_stack(x, offsets, bmap, layer_params, geo: STUGeometry, seeds, seed_offset=None):
+    """All layers at once (``STUStackFunction``).  layer_params: per layer (_uvqk,
+    _o.weight, _o.bias, _pos_w, _ts_w) with the bias tables None when bmap is None.
+    Not for concat_ua (the per-layer ``stu_layer`` covers it)."""
+    if geo.concat_ua:
+        raise ValueError("stu_stack: concat_ua layers run through stu_layer")
+    flat = [t for lp in layer_params for t in lp]
+    _lib.require_gpu(x, offsets, *flat)
+    if x.dtype != torch.float32:
+        raise TypeError("stu_stack: float32 only (the reference runs fp32, hstu.py:592)")
+    grad_on = torch.is_grad_enabled() and any(
+        t is not None and t.requires_grad for t in [x] + flat)
+    return STUStackFunction.apply(x, offsets, bmap, geo, tuple(int(s) for s in seeds),
+                                  seed_offset, grad_on, *flat)
 
 
 def stu_layer(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGeometry, seed: int = 0,

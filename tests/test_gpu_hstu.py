@@ -338,3 +338,59 @@ def test_hstu_concat_ua_train_dropout_regenerates_mask():
         fd = (f(x + eps * direction) - f(x - eps * direction)) / (2 * eps)
     an = (xg.grad * direction).sum()
     assert abs(fd.item() - an.item()) <= 2e-2 * (1 + abs(an.item())), (fd.item(), an.item())
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+@pytest.mark.parametrize("B,N0,D,blocks,freeze", [(8, 200, 50, 4, None), (2, 500, 256, 2, None),
+                                                 (4, 200, 50, 3, "_o"), (4, 200, 50, 2, "_uvqk")])
+def test_hstu_stack_node_matches_per_layer_nodes(bf16, B, N0, D, blocks, freeze):
+    """The encoder as one autograd node (ops.stu_stack: every layer's weight gradients in
+    one gr_wgrad_multi launch pair) against one node per layer (ops.stu_layer), train
+    mode with dropout: the forward and the input gradient are bit-identical (same
+    kernels, same masks), the weight gradients agree to fp32 summation order
+    (1e-5 relative), frozen parameters get no gradient."""
+    from mygenerativerecommenders_amd.hstu import HSTU
+    torch.manual_seed(0)
+    out_len = 11
+    N = N0 + out_len
+    enc = HSTU(max_sequence_len=N0, max_output_len=out_len, embedding_dim=D,
+               item_embedding_dim=D, num_blocks=blocks, num_heads=1, linear_dim=D,
+               attention_dim=D, normalization="rel_bias", linear_config="uvqk",
+               linear_activation="silu", linear_dropout_rate=0.2, attn_dropout_rate=0.0,
+               autocast_dtype=torch.bfloat16 if bf16 else None).cuda().train()
+    if freeze:
+        for name, p in enc.named_parameters():
+            if freeze in name:
+                p.requires_grad_(False)
+    g = torch.Generator().manual_seed(5)
+    lengths = torch.randint(N0 // 3, N0 + 1, (B,), generator=g)
+    x = torch.randn(B, N, D, generator=g).cuda()
+    ts = torch.zeros(B, N, dtype=torch.int64)
+    for b in range(B):
+        L = int(lengths[b])
+        ts[b, :L + 1] = 1_000_000_000 + torch.cumsum((torch.rand(L + 1, generator=g) * 2e5).long(), 0)
+    dy = torch.randn(B, N, D, generator=g).cuda()
+    outs = []
+    for use_stack in (True, False):
+        enc._hstu._use_stack = use_stack
+        enc._hstu._dropout_step.zero_()  # same dropout masks in both runs
+        enc.zero_grad(set_to_none=True)
+        xg = x.clone().requires_grad_(True)
+        y, _ = enc(lengths.cuda(), xg, None, {"timestamps": ts.cuda()})
+        (y * dy).sum().backward()
+        outs.append((y.detach(), xg.grad, {n: (p.grad.clone() if p.grad is not None else None)
+                                           for n, p in enc.named_parameters()}))
+    enc._hstu._use_stack = True
+    (y0, dx0, g0), (y1, dx1, g1) = outs
+    assert torch.equal(y0, y1)
+    assert torch.equal(dx0, dx1)
+    for n in g0:
+        if g1[n] is None:
+            assert g0[n] is None, n
+            continue
+        assert g0[n] is not None, n
+        err = (g0[n] - g1[n]).abs().max().item()
+        # bf16 mode with one weight frozen: the per-layer node's single GEMM (gr_wgrad)
+        # has fp32 operands, the stack's gr_wgrad_multi bf16 ones (the mode's operand type)
+        tol = 5e-3 if (bf16 and freeze) else 1e-5
+        assert err <= tol * (1 + g1[n].abs().max().item()), (n, err)
