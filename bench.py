@@ -669,6 +669,8 @@ def main():
         "ln_uvqk_fwd": 2.0 * rows * D * nout, "gate_o_fwd": 2.0 * rows * D * D,
         "gate_o_bwd": 2.0 * rows * D * D, "ln_uvqk_bwd": 2.0 * rows * nout * D,
         "wgrad_partial": (2.0 * rows * D * D + 2.0 * rows * D * nout) / 2.0,
+        "boundary_fwd": 2.0 * rows * D * D + 2.0 * rows * D * nout,
+        "boundary_bwd": 2.0 * rows * D * D + 2.0 * rows * nout * D,
     }
     dominant = max(kern_total, key=kern_total.get)
     ach = flops_per_launch.get(dominant, 0.0) / (kern[dominant] * 1e-3) / 1e12 if kern[dominant] else 0.0

@@ -424,6 +424,32 @@ GR_API int hstu_ln_uvqk_bwd_bf16(const float* dh, int64_t ld_dh, const int64_t* 
                           const float* dy_res, int64_t ld_dy, float* dx, int64_t ld_dx,
                           void* stream);
 
+/* hstu_boundary_fwd / _bwd (ABI 13) — one encoder layer boundary as ONE launch (the
+ * encoder's autograd node, ops.STUStackFunction, calls them between layers):
+ *   fwd: hstu_gate_o_fwd of layer l (y = x_res + dropout(u * LN(attn)) W_o^T + b_o) then
+ *        hstu_ln_uvqk_fwd of layer l + 1 on y (x_stats, h_pre, uvqk of layer l + 1);
+ *   bwd: hstu_ln_uvqk_bwd of layer l (dx = dy_res + LN_bwd(dh W_uvqk^T)) then
+ *        hstu_gate_o_bwd of layer l - 1 with dy = dx (du, d_attn of layer l - 1).
+ * Arguments: those of the two calls it replaces (the second call's row input is the
+ * first one's output, y / dx, which is still stored).  Results are identical to the two
+ * calls; shapes the fused form does not cover (D or h dv > 64, n_out > 256, unaligned
+ * rows) run exactly those two calls.  fp32 only. */
+GR_API int hstu_boundary_fwd(const float* u, int64_t ld_u, const float* attn, int64_t ld_attn,
+                    const int64_t* offsets, int B, int64_t max_rows, int hdv, int D,
+                    const float* w_o, const float* b_o, const float* x_res, int64_t ld_x,
+                    float eps, float dropout_p, uint64_t seed, const int64_t* seed_offset,
+                    float* attn_stats, float* o_in, float* y, int64_t ld_y,
+                    const float* w_uvqk, int n_out, int activation, float* x_stats,
+                    float* h_pre, float* uvqk, int64_t ld_out, void* stream);
+GR_API int hstu_boundary_bwd(const float* dh, int64_t ld_dh, const int64_t* offsets, int B,
+                    int64_t max_rows, int D, int n_out, const float* w_uvqk, const float* x,
+                    int64_t ld_x, const float* x_stats, const float* dy_res, int64_t ld_dy,
+                    float* dx, int64_t ld_dx, int hdv, const float* w_o, const float* u,
+                    int64_t ld_u, const float* attn, int64_t ld_attn, const float* attn_stats,
+                    const float* h_u, int64_t ld_h, float dropout_p, uint64_t seed,
+                    const int64_t* seed_offset, float* du, int64_t ld_du, float* d_attn,
+                    int64_t ld_da, void* stream);
+
 /* gr_wgrad: weight gradient C = A'^T B over all jagged rows (replaces the mm-backward
  * of hstu.py:303 and of the _o Linear at hstu.py:404-411):
  *   C[ka, nb] = sum_m A'[m, ka] * Bm[m, nb],  A' = A or (A - mean_m) * rstd_m when

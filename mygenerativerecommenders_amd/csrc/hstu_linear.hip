@@ -1585,3 +1585,162 @@ extern "C" int hstu_gate_o_cat_wide_bwd(const float* dy, int64_t ld_dy, const in
   GR_LAUNCH_CHECK("hstu_gate_o_cat_wide_bwd(rows)");
   return 0;
 }
+
+// ------------------------------------------------------------------ layer boundaries
+// gate_o(l) + ln_uvqk(l + 1) and ln_uvqk_bwd(l) + gate_o_bwd(l - 1) as ONE row-wave launch
+// each (rowwave2_kernel): at ml-1m every projection launch is latency-bound (a 16-row
+// unit per wave and ~1.6 units per SIMD), so the boundary's two launches cost about twice
+// one, and the boundary rows (y, dx) are handed over in registers.  Shapes outside the
+// instantiated set (D, h dv <= 64, n_out <= 256) fall back to the two separate launches,
+// with identical results either way (same per-unit arithmetic).
+namespace gr {
+
+static int rw2_bucket_small(int x) {  // the boundary's shared width (D and h dv) in 16-col groups
+  const int g = ceil_div(x, 16);
+  return g <= 1 ? 1 : g <= 2 ? 2 : g <= 4 ? 4 : -1;
+}
+
+template <int KG1, int NT1, int NT2, class Op1, class Op2>
+static int rw2_launch(const Op1& op1, const Op2& op2, int64_t max_rows, const char* tname,
+                      hipStream_t st) {
+  using C1 = RowWaveCfg<KG1, NT1>;
+  using C2 = RowWaveCfg<NT1, NT2>;
+  constexpr size_t lds = C1::LDS_BYTES + C2::LDS_BYTES;
+  if constexpr (lds > 150 * 1024) {
+    return -1;
+  } else {
+    const int64_t units = (max_rows + 15) / 16;
+    int grid = (int)((units + 3) / 4);
+    const int per_cu = (int)((160 * 1024) / lds);
+    const int cap = (per_cu < 1 ? 1 : per_cu > 4 ? 4 : per_cu) * num_cus();
+    if (grid > cap) grid = cap;
+    if (grid < 1) return 0;
+    GR_TIMED(tname, st, hipLaunchKernelGGL((rowwave2_kernel<KG1, NT1, NT2, Op1, Op2>), dim3(grid),
+                                           dim3(256), lds, st, op1, op2));
+    GR_LAUNCH_CHECK(tname);
+    return 0;
+  }
+}
+
+template <int W, int NT2>
+static int bfwd_launch(const RwArgsGateO& a1, const RwArgsLnUvqk& a2, int64_t max_rows, hipStream_t st) {
+  RwGateO<W, W, 2> o1;
+  RwLnUvqk<W, NT2, 2> o2;
+  a1.fill(o1);
+  a2.fill(o2);
+  return rw2_launch<W, W, NT2>(o1, o2, max_rows, "boundary_fwd", st);
+}
+template <int W>
+static int bfwd_nt(const RwArgsGateO& a1, const RwArgsLnUvqk& a2, int nt2, int64_t max_rows, hipStream_t st) {
+  switch (nt2) {
+    case 4: return bfwd_launch<W, 4>(a1, a2, max_rows, st);
+    case 8: return bfwd_launch<W, 8>(a1, a2, max_rows, st);
+    case 13: return bfwd_launch<W, 13>(a1, a2, max_rows, st);
+    case 16: return bfwd_launch<W, 16>(a1, a2, max_rows, st);
+  }
+  return -1;
+}
+
+template <int KG1, int W>
+static int bbwd_launch(const RwArgsLnUvqkBwd& a1, const RwArgsGateOBwd& a2, int64_t max_rows, hipStream_t st) {
+  RwLnUvqkBwd<KG1, W, 2> o1;
+  RwGateOBwd<W, W, 2> o2;
+  a1.fill(o1);
+  a2.fill(o2);
+  return rw2_launch<KG1, W, W>(o1, o2, max_rows, "boundary_bwd", st);
+}
+template <int W>
+static int bbwd_kg(const RwArgsLnUvqkBwd& a1, const RwArgsGateOBwd& a2, int kg1, int64_t max_rows, hipStream_t st) {
+  switch (kg1) {
+    case 4: return bbwd_launch<4, W>(a1, a2, max_rows, st);
+    case 8: return bbwd_launch<8, W>(a1, a2, max_rows, st);
+    case 13: return bbwd_launch<13, W>(a1, a2, max_rows, st);
+    case 16: return bbwd_launch<16, W>(a1, a2, max_rows, st);
+  }
+  return -1;
+}
+
+}  // namespace gr
+
+extern "C" int hstu_boundary_fwd(const float* u, int64_t ld_u, const float* attn, int64_t ld_attn,
+                                 const int64_t* offsets, int B, int64_t max_rows, int hdv, int D,
+                                 const float* w_o, const float* b_o, const float* x_res,
+                                 int64_t ld_x, float eps, float dropout_p, uint64_t seed,
+                                 const int64_t* seed_offset, float* attn_stats, float* o_in,
+                                 float* y, int64_t ld_y, const float* w_uvqk, int n_out,
+                                 int activation, float* x_stats, float* h_pre, float* uvqk,
+                                 int64_t ld_out, void* stream) {
+  GR_REQUIRE(u && attn && offsets && w_o && y && attn_stats && w_uvqk && uvqk && x_stats,
+             "hstu_boundary_fwd: null pointer");
+  GR_REQUIRE(hdv > 0 && D > 0 && n_out > 0 && B >= 0, "hstu_boundary_fwd: bad sizes");
+  GR_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f, "hstu_boundary_fwd: dropout_p %f", dropout_p);
+  GR_REQUIRE(activation == 0 || activation == 1, "hstu_boundary_fwd: activation must be 0|1");
+  const hipStream_t st = (hipStream_t)stream;
+  if (rw_enabled()) {
+    RwArgsGateO a1{offsets, B, hdv, D, u, ld_u, attn, ld_attn, w_o, b_o, x_res, ld_x, eps,
+                   dropout_p, seed, seed_offset, (float2*)attn_stats, o_in, y, ld_y};
+    RwArgsLnUvqk a2{offsets, B, D, n_out, y, ld_y, w_uvqk, eps, activation, (float2*)x_stats,
+                    h_pre, uvqk, ld_out};
+    const int w = std::max(rw2_bucket_small(hdv), rw2_bucket_small(D));
+    const int nt2 = rw_bucket(n_out);
+    const int vec = rw_vec({u, attn, x_res, o_in, y, h_pre, uvqk},
+                           {ld_u, ld_attn, ld_x, ld_y, ld_out, hdv, D, n_out});
+    const bool fits = rw2_bucket_small(hdv) > 0 && rw2_bucket_small(D) > 0 && nt2 >= 4 && vec &&
+                      max_rows * 4 * 1024 <= 0x7fffffffLL;
+    if (fits) {
+      int rc = -1;
+      if (w == 1) rc = bfwd_nt<1>(a1, a2, nt2, max_rows, st);
+      else if (w == 2) rc = bfwd_nt<2>(a1, a2, nt2, max_rows, st);
+      else rc = bfwd_nt<4>(a1, a2, nt2, max_rows, st);
+      if (rc >= 0) return rc;
+    }
+  }
+  if (int rc = hstu_gate_o_fwd(u, ld_u, attn, ld_attn, offsets, B, max_rows, hdv, D, w_o, b_o, x_res,
+                               ld_x, eps, dropout_p, seed, seed_offset, attn_stats, o_in, y, ld_y,
+                               stream))
+    return rc;
+  return hstu_ln_uvqk_fwd(y, ld_y, offsets, B, max_rows, D, w_uvqk, n_out, eps, activation, x_stats,
+                          h_pre, uvqk, ld_out, stream);
+}
+
+extern "C" int hstu_boundary_bwd(const float* dh, int64_t ld_dh, const int64_t* offsets, int B,
+                                 int64_t max_rows, int D, int n_out, const float* w_uvqk,
+                                 const float* x, int64_t ld_x, const float* x_stats,
+                                 const float* dy_res, int64_t ld_dy, float* dx, int64_t ld_dx,
+                                 int hdv, const float* w_o, const float* u, int64_t ld_u,
+                                 const float* attn, int64_t ld_attn, const float* attn_stats,
+                                 const float* h_u, int64_t ld_h, float dropout_p, uint64_t seed,
+                                 const int64_t* seed_offset, float* du, int64_t ld_du,
+                                 float* d_attn, int64_t ld_da, void* stream) {
+  GR_REQUIRE(dh && offsets && w_uvqk && x && x_stats && dx && w_o && u && attn && attn_stats && du &&
+                 d_attn,
+             "hstu_boundary_bwd: null pointer");
+  GR_REQUIRE(D > 0 && n_out > 0 && hdv > 0 && B >= 0, "hstu_boundary_bwd: bad sizes");
+  const hipStream_t st = (hipStream_t)stream;
+  if (rw_enabled()) {
+    RwArgsLnUvqkBwd a1{offsets, B, n_out, D, dh, ld_dh, w_uvqk, x, ld_x, (const float2*)x_stats,
+                       dy_res, ld_dy, dx, ld_dx};
+    RwArgsGateOBwd a2{offsets, B, D, hdv, dx, ld_dx, w_o, u, ld_u, attn, ld_attn,
+                      (const float2*)attn_stats, h_u, ld_h, dropout_p, seed, seed_offset, du, ld_du,
+                      d_attn, ld_da};
+    const int w = std::max(rw2_bucket_small(hdv), rw2_bucket_small(D));
+    const int kg1 = rw_bucket(n_out);
+    const int vec = rw_vec({dh, x, dy_res, dx, u, attn, h_u, du, d_attn},
+                           {ld_dh, ld_x, ld_dy, ld_dx, ld_u, ld_attn, ld_h, ld_du, ld_da, n_out, D, hdv});
+    const bool fits = rw2_bucket_small(hdv) > 0 && rw2_bucket_small(D) > 0 && kg1 >= 4 && vec &&
+                      max_rows * 4 * 1024 <= 0x7fffffffLL;
+    if (fits) {
+      int rc = -1;
+      if (w == 1) rc = bbwd_kg<1>(a1, a2, kg1, max_rows, st);
+      else if (w == 2) rc = bbwd_kg<2>(a1, a2, kg1, max_rows, st);
+      else rc = bbwd_kg<4>(a1, a2, kg1, max_rows, st);
+      if (rc >= 0) return rc;
+    }
+  }
+  if (int rc = hstu_ln_uvqk_bwd(dh, ld_dh, offsets, B, max_rows, D, n_out, w_uvqk, x, ld_x, x_stats,
+                                dy_res, ld_dy, dx, ld_dx, stream))
+    return rc;
+  return hstu_gate_o_bwd(dx, ld_dx, offsets, B, max_rows, hdv, D, w_o, u, ld_u, attn, ld_attn,
+                         attn_stats, h_u, ld_h, dropout_p, seed, seed_offset, du, ld_du, d_attn,
+                         ld_da, stream);
+}

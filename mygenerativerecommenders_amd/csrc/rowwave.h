@@ -97,6 +97,125 @@ struct RowWaveCfg {
 //   turns them into the A quads; epi_load(es, m, row_ok, lg) issues the epilogue's row
 //   inputs before the MFMAs; epi(acc, es, m, row_ok, lg) consumes acc[t][e] =
 //   C[m][qcol(16t, lg, e)].
+// Stage an Op's weight panel W' (KG*16 x NT*16, LDS row stride LDW) into LDS once per
+// workgroup (the same layout and load order as rowwave_kernel's staging below).
+template <int KG, int NT, class Op>
+__device__ __forceinline__ void rw_stage_w(const Op& op, float* Wl) {
+  using C = RowWaveCfg<KG, NT>;
+  constexpr int VEC = Op::VEC;
+  const int tid = threadIdx.x;
+  constexpr int FP = Op::K_CONTIG ? C::KP : C::NP;
+  constexpr int SP = Op::K_CONTIG ? C::NP : C::KP;
+  constexpr int FP2 = FP <= 16 ? 16 : FP <= 32 ? 32 : FP <= 64 ? 64 : FP <= 128 ? 128 : 256;
+  constexpr int SSTEP = 256 / FP2;
+  constexpr int ITER = SP / SSTEP;
+  constexpr int BATCH = ITER < 64 ? ITER : 64;
+  const int f = tid % FP2, s0 = tid / FP2;
+  const int64_t wlast = (int64_t)(op.K - 1) * op.bks() + (int64_t)(op.N - 1) * op.bns() + 1;
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)op.w, 0, (int)(wlast * 4 < 0x7fffffff ? wlast * 4 : 0x7fffffff), 0x00020000);
+  if (f < FP) {
+#pragma unroll 1
+    for (int i0 = 0; i0 < ITER; i0 += BATCH) {
+      float v[BATCH];
+#pragma unroll
+      for (int i = 0; i < BATCH; ++i) {
+        const int sl = s0 + (i0 + i) * SSTEP;
+        const int k = Op::K_CONTIG ? f : sl;
+        const int p = Op::K_CONTIG ? sl : f;
+        const int n = (p & ~15) + qcol<VEC>(0, (p & 15) >> 2, p & 3);
+        const bool ok = k < op.K && n < op.N;
+        v[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+            rw, ok ? (int)(((int64_t)k * op.bks() + (int64_t)n * op.bns()) * 4) : OOB, 0, 0));
+      }
+#pragma unroll
+      for (int i = 0; i < BATCH; ++i) {
+        const int sl = s0 + (i0 + i) * SSTEP;
+        if (i0 + i < ITER) Wl[(Op::K_CONTIG ? f : sl) * C::LDW + (Op::K_CONTIG ? sl : f)] = v[i];
+      }
+    }
+  }
+}
+
+// acc[t] = sum_k W'(k, 16 t + .) a(k): the row-wave k-step loop of rowwave_kernel
+template <int KG, int NT, int VEC>
+__device__ __forceinline__ void rw_mma(const float* Wl, const float (&a)[KG][4], f4 (&acc)[NT],
+                                       int lr, int lg) {
+  using C = RowWaveCfg<KG, NT>;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f4_zero();
+  int wofs = 0;
+  asm volatile("" : "+v"(wofs));
+  const float* wbase = Wl + wofs + lr;
+  float wv[2][NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) wv[0][t] = wbase[qcol<VEC>(0, lg, 0) * C::LDW + 16 * t];
+#pragma unroll
+  for (int s = 0; s < 4 * KG; ++s) {
+    const int g = s >> 2, e = s & 3;
+    if (s + 1 < 4 * KG) {
+      const float* wrow = wbase + qcol<VEC>(16 * ((s + 1) >> 2), lg, (s + 1) & 3) * C::LDW;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) wv[(s + 1) & 1][t] = wrow[16 * t];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = mfma16x16x4(wv[s & 1][t], a[g][e], acc[t]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// Two row-wave GEMMs chained per 16-row unit (a layer boundary of the encoder): Op1's
+// epilogue stores its output rows AND hands the quads, still in registers, to Op2 as its
+// A operand (Op1's NT == Op2's KG: one lane's 4 consecutive output columns are exactly
+// its 4 k values of the next product).  Both weight panels stay in LDS.  The forward
+// boundary is gate_o(l) -> ln_uvqk(l + 1) (y = x + o W_o^T + b, then silu(LN(y) W_uvqk)),
+// the backward one ln_uvqk_bwd(l) -> gate_o_bwd(l - 1) (dx_l is the dy of layer l - 1):
+// one launch and no re-read of the boundary rows instead of two launches.
+template <int KG1, int NT1, int NT2, class Op1, class Op2>
+__global__ __launch_bounds__(256) void rowwave2_kernel(Op1 op1, Op2 op2) {
+  using C1 = RowWaveCfg<KG1, NT1>;
+  constexpr int VEC = Op1::VEC;
+  static_assert(Op2::VEC == VEC, "one quad layout");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* W1 = reinterpret_cast<float*>(smem);
+  float* W2 = W1 + C1::KP * C1::LDW;
+  const int tid = threadIdx.x, w = wave_id(), lane = tid & 63;
+  const int lr = lane & 15, lg = lane >> 4;
+  (void)tid;
+  const int64_t total = op1.offsets[op1.B];
+  op1.setup(total);
+  op2.setup(total);
+  const int64_t n_units = (total + 15) / 16;
+  int64_t u = (int64_t)blockIdx.x * 4 + w;
+  const int64_t ustep = (int64_t)gridDim.x * 4;
+  typename Op1::Src cur;
+  if (u < n_units) op1.load(cur, u * 16 + lr, lg);
+  rw_stage_w<KG1, NT1>(op1, W1);
+  rw_stage_w<NT1, NT2>(op2, W2);
+  __syncthreads();
+  for (; u < n_units; u += ustep) {
+    const int64_t m = u * 16 + lr;
+    const bool ok = m < total;
+    float a1[KG1][4];
+    op1.prep(cur, a1, m, ok, lg);
+    typename Op1::Epi es1;
+    op1.epi_load(es1, m, ok, lg);
+    typename Op2::Epi es2;
+    op2.epi_load(es2, m, ok, lg);
+    f4 acc1[NT1];
+    rw_mma<KG1, NT1, VEC>(W1, a1, acc1, lr, lg);
+    typename Op2::Src s2;
+    op1.epi(acc1, es1, m, ok, lg, s2.v);
+    if (u + ustep < n_units) op1.load(cur, m + ustep * 16, lg);  // the next unit's rows
+    float a2[NT1][4];
+    op2.prep(s2, a2, m, ok, lg);
+    f4 acc2[NT2];
+    rw_mma<NT1, NT2, VEC>(W2, a2, acc2, lr, lg);
+    op2.epi(acc2, es2, m, ok, lg);
+  }
+}
+
 template <int KG, int NT, class Op>
 __global__ __launch_bounds__(256) void rowwave_kernel(Op op) {
   using C = RowWaveCfg<KG, NT>;
@@ -369,7 +488,8 @@ struct RwGateO {
       es.bv[t] = ldq<VEC>(rb, 0, 16 * t, lg, N);        // 0 when bias is NULL
     }
   }
-  __device__ void epi(f4 (&acc)[NT], const Epi& es, int64_t m, bool, int lg) const {
+  // out (optional): the stored y quads, for a fused consumer (rowwave2_kernel)
+  __device__ void epi(f4 (&acc)[NT], const Epi& es, int64_t m, bool, int lg, f4* out = nullptr) const {
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const f4 xv = es.xv[t], bv = es.bv[t];
@@ -377,6 +497,7 @@ struct RwGateO {
 #pragma unroll
       for (int e = 0; e < 4; ++e) o[e] = (acc[t][e] + bv[e]) + xv[e];
       stq<VEC>(ry, m * ldy, 16 * t, lg, N, o);
+      if (out) out[t] = o;
     }
   }
 };
@@ -736,7 +857,9 @@ struct RwLnUvqkBwd {
       es.dyv[t] = ldq<VEC>(rdy, m * lddy, 16 * t, lg, N);  // 0 when dy is NULL
     }
   }
-  __device__ void epi(f4 (&acc)[NT], const Epi& es, int64_t m, bool row_ok, int lg) const {
+  // out (optional): the stored dx quads, for a fused consumer (rowwave2_kernel)
+  __device__ void epi(f4 (&acc)[NT], const Epi& es, int64_t m, bool row_ok, int lg,
+                      f4* out = nullptr) const {
     const float2 st = es.st;
     float s1 = 0.f, s2 = 0.f;
     f4 xh[NT];
@@ -763,6 +886,10 @@ struct RwLnUvqkBwd {
 #pragma unroll
       for (int e = 0; e < 4; ++e) o[e] = dyv[e] + st.y * (acc[t][e] - mean1 - xh[t][e] * mean2);
       stq<VEC>(rdx, m * lddx, 16 * t, lg, N, o);
+      if (out) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) out[t][e] = qcol<VEC>(16 * t, lg, e) < N ? o[e] : 0.f;
+      }
     }
   }
 };

@@ -293,9 +293,14 @@ def _pad_cat_weight(w_o: torch.Tensor, hv: int):
 
 
 def _stu_forward(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGeometry, seed: int,
-                 seed_offset, grad_on: bool, needs_w_grad: bool):
-    """One STU layer forward (hstu.py:266-413): 3 launches.  Returns (y, saved) with the
-    tensors its backward needs (``_stu_backward``)."""
+                 seed_offset, grad_on: bool, needs_w_grad: bool, pre=None, next_w_uvqk=None):
+    """One STU layer forward (hstu.py:266-413): 3 launches.  Returns (y, saved, pre_next)
+    with the tensors its backward needs (``_stu_backward``).
+    Layer boundaries (``_fuse_boundaries``): ``pre`` = (x_stats, uvqk, h_pre) of this layer
+    already made by the previous layer's hstu_boundary_fwd (the LN + UVQK launch is
+    skipped); ``next_w_uvqk`` = the next layer's _uvqk: this layer's gate_o and the next
+    layer's LN + UVQK run as one hstu_boundary_fwd launch, whose (x_stats, uvqk, h_pre) are
+    returned as ``pre_next``."""
     dev = x.device
     rows, D = x.shape
     B = offsets.numel() - 1
@@ -306,15 +311,14 @@ def _stu_forward(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGeomet
     x = x.contiguous()
     w_uvqk = w_uvqk.contiguous()
     w_o = w_o.contiguous()
-    x_stats = torch.empty(rows, 2, dtype=torch.float32, device=dev)
-    uvqk = torch.empty(rows, n_out, dtype=torch.float32, device=dev)
-    # h_pre (pre-activation, for silu') and o_in (for the W_o gradient) exist only for
-    # the backward: inference / no_grad forwards skip both writes
-    h_pre = torch.empty_like(uvqk) if geo.activation and grad_on else None
     sfx = "_bf16" if geo.bf16 else ""  # bf16 MFMA operands in the projections too
-    _lib.call("hstu_ln_uvqk_fwd" + sfx, x.data_ptr(), x.stride(0), offsets.data_ptr(), B, rows, D,
-              w_uvqk.data_ptr(), n_out, geo.eps, geo.activation, x_stats.data_ptr(),
-              _lib.ptr(h_pre), uvqk.data_ptr(), n_out, st)
+    if pre is not None:
+        x_stats, uvqk, h_pre = pre
+    else:
+        x_stats, uvqk, h_pre = _ln_uvqk_outputs(rows, n_out, geo, grad_on, dev)
+        _lib.call("hstu_ln_uvqk_fwd" + sfx, x.data_ptr(), x.stride(0), offsets.data_ptr(), B,
+                  rows, D, w_uvqk.data_ptr(), n_out, geo.eps, geo.activation,
+                  x_stats.data_ptr(), _lib.ptr(h_pre), uvqk.data_ptr(), n_out, st)
     attn = torch.empty(rows, hv, dtype=torch.float32, device=dev)
     q = uvqk[:, 2 * hv:2 * hv + hq]
     k = uvqk[:, 2 * hv + hq:]
@@ -350,7 +354,20 @@ def _stu_forward(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGeomet
         w_pad, hvp = _pad_cat_weight(w_o, hv)
     y = torch.empty(rows, D, dtype=torch.float32, device=dev)
     b_o_c = b_o.contiguous()
-    if cat_wide:
+    pre_next = None
+    if next_w_uvqk is not None:
+        if geo.concat_ua or geo.bf16:
+            raise ValueError("hstu_boundary_fwd: fp32, no concat_ua")
+        w_next = next_w_uvqk.contiguous()
+        pre_next = _ln_uvqk_outputs(rows, n_out, geo, grad_on, dev)
+        nx_stats, nx_uvqk, nx_h_pre = pre_next
+        _lib.call("hstu_boundary_fwd", uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
+                  offsets.data_ptr(), B, rows, hv, D, w_o.data_ptr(), b_o_c.data_ptr(),
+                  x.data_ptr(), x.stride(0), geo.eps, geo.dropout_p, seed,
+                  _lib.ptr(seed_offset), attn_stats.data_ptr(), _lib.ptr(o_in), y.data_ptr(),
+                  D, w_next.data_ptr(), n_out, geo.activation, nx_stats.data_ptr(),
+                  _lib.ptr(nx_h_pre), nx_uvqk.data_ptr(), n_out, st)
+    elif cat_wide:
         _lib.call("hstu_gate_o_cat_wide_fwd", uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
                   offsets.data_ptr(), B, rows, hv, D, w_o.data_ptr(), b_o_c.data_ptr(),
                   x.data_ptr(), x.stride(0), geo.eps, geo.dropout_p, seed,
@@ -372,15 +389,28 @@ def _stu_forward(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGeomet
                   D, st)
     saved = (x, offsets, bmap, w_uvqk, w_o, pos_w_c, ts_w_c, x_stats, uvqk, h_pre, attn,
              attn_stats, o_in, copies if grad_on else None)
-    return y, saved
+    return y, saved, pre_next
+
+
+def _ln_uvqk_outputs(rows, n_out, geo: STUGeometry, grad_on: bool, dev):
+    """(x_stats, uvqk, h_pre) of one layer's LN + UVQK.  h_pre (pre-activation, for
+    silu') exists only for the backward: inference / no_grad forwards skip its write."""
+    x_stats = torch.empty(rows, 2, dtype=torch.float32, device=dev)
+    uvqk = torch.empty(rows, n_out, dtype=torch.float32, device=dev)
+    h_pre = torch.empty_like(uvqk) if geo.activation and grad_on else None
+    return x_stats, uvqk, h_pre
 
 
 def _stu_backward(saved, dy, geo: STUGeometry, seed: int, seed_offset, want_uvqk: bool,
-                  defer_wgrad: bool = False):
+                  defer_wgrad: bool = False, pre_d=None, prev=None):
     """One STU layer backward: gate_o_bwd, attention backward (+ bias reduce), ln_uvqk_bwd,
     then the two weight-gradient GEMMs (gr_wgrad2), or -- ``defer_wgrad`` -- their
     gr_wgrad_multi problem rows, left for the caller to launch with other layers'.
-    Returns (dx, d_w_uvqk, d_w_o, d_b_o, d_pos_w, d_ts_w, problems)."""
+    Layer boundaries: ``pre_d`` = (d_uvqk, d_attn) already made by the next layer's
+    hstu_boundary_bwd (gate_o_bwd is skipped); ``prev`` = (saved, seed) of the previous
+    layer: this layer's ln_uvqk_bwd and the previous layer's gate_o_bwd run as one
+    hstu_boundary_bwd launch, whose (d_uvqk, d_attn) are returned as ``pre_d_prev``.
+    Returns (dx, d_w_uvqk, d_w_o, d_b_o, d_pos_w, d_ts_w, problems, pre_d_prev)."""
     (x, offsets, bmap, w_uvqk, w_o, pos_w, ts_w, x_stats, uvqk, h_pre, attn, attn_stats,
      o_in, copies) = saved
     dev = x.device
@@ -391,9 +421,14 @@ def _stu_backward(saved, dy, geo: STUGeometry, seed: int, seed_offset, want_uvqk
     n_out = geo.n_out
     st = _stream()
     dy = dy.contiguous()
-    d_uvqk = torch.empty(rows, n_out, dtype=torch.float32, device=dev)
-    d_attn = torch.empty(rows, hv, dtype=torch.float32, device=dev)
-    if geo.concat_ua and _cat_wide(hv, D):
+    if pre_d is not None:
+        d_uvqk, d_attn = pre_d  # this layer's gate_o_bwd ran in the next layer's boundary
+    else:
+        d_uvqk = torch.empty(rows, n_out, dtype=torch.float32, device=dev)
+        d_attn = torch.empty(rows, hv, dtype=torch.float32, device=dev)
+    if pre_d is not None:
+        pass
+    elif geo.concat_ua and _cat_wide(hv, D):
         g_cat = torch.empty(rows, 3 * hv, dtype=torch.float32, device=dev)
         _lib.call("hstu_gate_o_cat_wide_bwd", dy.data_ptr(), D, offsets.data_ptr(), B, rows, hv,
                   D, w_o.data_ptr(), uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
@@ -449,10 +484,24 @@ def _stu_backward(saved, dy, geo: STUGeometry, seed: int, seed_offset, want_uvqk
     else:
         _lib.call("hstu_attn_bwd", *bwd_args, _lib.ptr(ws_a), ws_a_n, st)
     dx = torch.empty(rows, D, dtype=torch.float32, device=dev)
-    _lib.call("hstu_ln_uvqk_bwd" + ("_bf16" if geo.bf16 else ""), d_uvqk.data_ptr(), n_out,
-              offsets.data_ptr(), B, rows, D,
-              n_out, w_uvqk.data_ptr(), x.data_ptr(), x.stride(0), x_stats.data_ptr(),
-              dy.data_ptr(), D, dx.data_ptr(), D, st)
+    pre_d_prev = None
+    if prev is not None:
+        if geo.concat_ua or geo.bf16:
+            raise ValueError("hstu_boundary_bwd: fp32, no concat_ua")
+        (_, _, _, _, p_w_o, _, _, _, p_uvqk, p_h_pre, p_attn, p_attn_stats, _, _), p_seed = prev
+        pre_d_prev = (torch.empty(rows, n_out, dtype=torch.float32, device=dev),
+                      torch.empty(rows, hv, dtype=torch.float32, device=dev))
+        _lib.call("hstu_boundary_bwd", d_uvqk.data_ptr(), n_out, offsets.data_ptr(), B, rows, D,
+                  n_out, w_uvqk.data_ptr(), x.data_ptr(), x.stride(0), x_stats.data_ptr(),
+                  dy.data_ptr(), D, dx.data_ptr(), D, hv, p_w_o.data_ptr(), p_uvqk.data_ptr(),
+                  n_out, p_attn.data_ptr(), hv, p_attn_stats.data_ptr(), _lib.ptr(p_h_pre),
+                  n_out, geo.dropout_p, p_seed, _lib.ptr(seed_offset),
+                  pre_d_prev[0].data_ptr(), n_out, pre_d_prev[1].data_ptr(), hv, st)
+    else:
+        _lib.call("hstu_ln_uvqk_bwd" + ("_bf16" if geo.bf16 else ""), d_uvqk.data_ptr(), n_out,
+                  offsets.data_ptr(), B, rows, D,
+                  n_out, w_uvqk.data_ptr(), x.data_ptr(), x.stride(0), x_stats.data_ptr(),
+                  dy.data_ptr(), D, dx.data_ptr(), D, st)
     # weight gradients (off the critical path): both GEMMs of the layer in one launch
     # and one slab reduce (gr_wgrad2), or deferred to the caller's gr_wgrad_multi
     d_w_uvqk = torch.empty(D, n_out, dtype=torch.float32, device=dev) if want_uvqk else None
@@ -490,7 +539,7 @@ def _stu_backward(saved, dy, geo: STUGeometry, seed: int, seed_offset, want_uvqk
         ws = torch.empty(max(ws_n, 4), dtype=torch.uint8, device=dev)
         _lib.call("gr_wgrad", dy.data_ptr(), D, None, o_in.data_ptr(), ow, offsets.data_ptr(),
                   B, rows, D, ow, d_w_o.data_ptr(), d_b_o.data_ptr(), ws.data_ptr(), ws_n, st)
-    return dx, d_w_uvqk, d_w_o, d_b_o, d_pos_w, d_ts_w, problems
+    return dx, d_w_uvqk, d_w_o, d_b_o, d_pos_w, d_ts_w, problems, pre_d_prev
 
 
 class STULayerFunction(torch.autograd.Function):
@@ -502,8 +551,8 @@ class STULayerFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGeometry, seed: int,
                 seed_offset, grad_on: bool = True):
-        y, saved = _stu_forward(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo, seed,
-                                seed_offset, grad_on, w_o.requires_grad or b_o.requires_grad)
+        y, saved, _ = _stu_forward(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo, seed,
+                                   seed_offset, grad_on, w_o.requires_grad or b_o.requires_grad)
         ctx.save_for_backward(*saved)
         ctx.geo = geo
         ctx.seed = seed
@@ -512,12 +561,20 @@ class STULayerFunction(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        dx, d_w_uvqk, d_w_o, d_b_o, d_pos_w, d_ts_w, _ = _stu_backward(
+        dx, d_w_uvqk, d_w_o, d_b_o, d_pos_w, d_ts_w, _, _ = _stu_backward(
             ctx.saved_tensors, dy, ctx.geo, ctx.seed, ctx.seed_offset, ctx.needs_input_grad[3])
         return (dx, None, None, d_w_uvqk, d_w_o, d_b_o, d_pos_w, d_ts_w, None, None, None, None)
 
 
 _SAVED_PER_LAYER = 14  # entries of _stu_forward's saved tuple
+
+# layer boundaries of the stack as one launch each (hstu_boundary_fwd / _bwd); False =
+# the two launches they replace (A/B switch for tests and measurements)
+FUSE_BOUNDARIES = True
+
+
+def _fuse_boundaries(geo: STUGeometry) -> bool:
+    return FUSE_BOUNDARIES and not geo.bf16 and not geo.concat_ua
 
 
 def launch_wgrad_multi(problems, offsets, rows, bf16: bool):
@@ -553,11 +610,14 @@ class STUStackFunction(torch.autograd.Function):
                 *params):
         n_layers = len(seeds)
         saved_all = []
+        fuse = _fuse_boundaries(geo)
+        pre = None
         for l in range(n_layers):
             w_uvqk, w_o, b_o, pos_w, ts_w = params[5 * l:5 * l + 5]
-            x, saved = _stu_forward(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo,
-                                    seeds[l], seed_offset, grad_on,
-                                    w_o.requires_grad or b_o.requires_grad)
+            nxt = params[5 * (l + 1)] if fuse and l + 1 < n_layers else None
+            x, saved, pre = _stu_forward(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo,
+                                         seeds[l], seed_offset, grad_on,
+                                         w_o.requires_grad or b_o.requires_grad, pre, nxt)
             if grad_on:
                 saved_all.extend(saved)
         if grad_on:
@@ -576,11 +636,17 @@ class STUStackFunction(torch.autograd.Function):
         problems = []
         offsets = saved[1]
         rows = saved[0].shape[0]
+        fuse = _fuse_boundaries(geo)
+        pre_d = None
         for l in reversed(range(n_layers)):
             sl = saved[_SAVED_PER_LAYER * l:_SAVED_PER_LAYER * (l + 1)]
+            prev = None
+            if fuse and l > 0:
+                prev = (saved[_SAVED_PER_LAYER * (l - 1):_SAVED_PER_LAYER * l], ctx.seeds[l - 1])
             want_uvqk = ctx.needs_input_grad[7 + 5 * l]
-            dx, d_w_uvqk, d_w_o, d_b_o, d_pos_w, d_ts_w, probs = _stu_backward(
-                sl, dy, geo, ctx.seeds[l], ctx.seed_offset, want_uvqk, defer_wgrad=True)
+            dx, d_w_uvqk, d_w_o, d_b_o, d_pos_w, d_ts_w, probs, pre_d = _stu_backward(
+                sl, dy, geo, ctx.seeds[l], ctx.seed_offset, want_uvqk, defer_wgrad=True,
+                pre_d=pre_d, prev=prev)
             grads[5 * l:5 * l + 5] = [d_w_uvqk, d_w_o, d_b_o, d_pos_w, d_ts_w]
             problems.extend(probs)
             dy = dx

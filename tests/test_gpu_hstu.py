@@ -370,7 +370,9 @@ def test_hstu_stack_node_matches_per_layer_nodes(bf16, B, N0, D, blocks, freeze)
         L = int(lengths[b])
         ts[b, :L + 1] = 1_000_000_000 + torch.cumsum((torch.rand(L + 1, generator=g) * 2e5).long(), 0)
     dy = torch.randn(B, N, D, generator=g).cuda()
+    from mygenerativerecommenders_amd import ops
     outs = []
+    ops.FUSE_BOUNDARIES = False  # the fused boundaries: test_hstu_stack_boundaries_*
     for use_stack in (True, False):
         enc._hstu._use_stack = use_stack
         enc._hstu._dropout_step.zero_()  # same dropout masks in both runs
@@ -381,6 +383,7 @@ def test_hstu_stack_node_matches_per_layer_nodes(bf16, B, N0, D, blocks, freeze)
         outs.append((y.detach(), xg.grad, {n: (p.grad.clone() if p.grad is not None else None)
                                            for n, p in enc.named_parameters()}))
     enc._hstu._use_stack = True
+    ops.FUSE_BOUNDARIES = True
     (y0, dx0, g0), (y1, dx1, g1) = outs
     assert torch.equal(y0, y1)
     assert torch.equal(dx0, dx1)
@@ -394,3 +397,59 @@ def test_hstu_stack_node_matches_per_layer_nodes(bf16, B, N0, D, blocks, freeze)
         # has fp32 operands, the stack's gr_wgrad_multi bf16 ones (the mode's operand type)
         tol = 5e-3 if (bf16 and freeze) else 1e-5
         assert err <= tol * (1 + g1[n].abs().max().item()), (n, err)
+
+
+@pytest.mark.parametrize("B,N0,D,hdv,blocks,act,dropout", [
+    (8, 200, 50, 50, 4, "silu", 0.2), (4, 100, 16, 16, 3, "silu", 0.0),
+    (4, 120, 32, 64, 2, "none", 0.1), (3, 90, 64, 32, 3, "silu", 0.0),
+    (2, 300, 256, 256, 2, "silu", 0.0)])
+def test_hstu_stack_boundaries_match_unfused(B, N0, D, hdv, blocks, act, dropout):
+    """Layer boundaries as one launch (hstu_boundary_fwd: gate_o(l) + LN/UVQK(l+1);
+    hstu_boundary_bwd: ln_uvqk_bwd(l) + gate_o_bwd(l-1)) against the two launches each
+    replaces, train mode (same dropout masks).  The fused launch runs the UVQK product as
+    a row-wave MFMA chain where the separate launch may take the row panel (n_out > 128),
+    so the two agree to fp32 summation order: 2e-5 relative to each tensor's largest
+    entry.  Shapes outside the fused set (D = 256 here) run the two launches inside the
+    entry point and must be bit-identical."""
+    from mygenerativerecommenders_amd import ops
+    from mygenerativerecommenders_amd.hstu import HSTU
+    torch.manual_seed(1)
+    out_len = 11
+    N = N0 + out_len
+    enc = HSTU(max_sequence_len=N0, max_output_len=out_len, embedding_dim=D,
+               item_embedding_dim=D, num_blocks=blocks, num_heads=1, linear_dim=hdv,
+               attention_dim=hdv, normalization="rel_bias", linear_config="uvqk",
+               linear_activation=act, linear_dropout_rate=dropout,
+               attn_dropout_rate=0.0).cuda().train()
+    g = torch.Generator().manual_seed(7)
+    lengths = torch.randint(N0 // 3, N0 + 1, (B,), generator=g)
+    x = torch.randn(B, N, D, generator=g).cuda()
+    ts = torch.zeros(B, N, dtype=torch.int64)
+    for b in range(B):
+        L = int(lengths[b])
+        ts[b, :L + 1] = 1_000_000_000 + torch.cumsum((torch.rand(L + 1, generator=g) * 2e5).long(), 0)
+    dy = torch.randn(B, N, D, generator=g).cuda()
+    outs = []
+    try:
+        for fuse in (True, False):
+            ops.FUSE_BOUNDARIES = fuse
+            enc._hstu._dropout_step.zero_()
+            enc.zero_grad(set_to_none=True)
+            xg = x.clone().requires_grad_(True)
+            y, _ = enc(lengths.cuda(), xg, None, {"timestamps": ts.cuda()})
+            (y * dy).sum().backward()
+            outs.append((y.detach(), xg.grad, {n: p.grad.clone() for n, p in enc.named_parameters()}))
+    finally:
+        ops.FUSE_BOUNDARIES = True
+    (y0, dx0, g0), (y1, dx1, g1) = outs
+
+    def close(a, b, what):
+        if D > 64 or hdv > 64:
+            assert torch.equal(a, b), what
+            return
+        err = (a - b).abs().max().item()
+        assert err <= 2e-5 * (1 + b.abs().max().item()), (what, err)
+    close(y0, y1, "y")
+    close(dx0, dx1, "dx")
+    for n in g0:
+        close(g0[n], g1[n], n)
