@@ -79,6 +79,11 @@ GR_API int gr_timing_reset(void);
  *   GR_OPT_PANEL_VEC          0|1  bf16 backward projection GEMMs at K % 32 == 0 with
  *                                  16-byte aligned rows and 256-column panels: float4
  *                                  operand staging (default 1) or the scalar-staged row panel
+ *   GR_OPT_ATTN_BWD_WIDE_DS   0|1  f32 attention backward at wide heads (dqk or dv > 128): the
+ *                                  dK/dV pass stores dS tiles and dQ = dS K runs in a second
+ *                                  launch without recomputing S / dP (default 1), or 0 = the
+ *                                  recomputing dQ pass.  Needs the workspace of
+ *                                  hstu_attn_bwd_workspace_size_d (which depends on it).
  */
 enum {
   GR_OPT_MIPS_FILTER_FP32 = 1,
@@ -92,7 +97,8 @@ enum {
   GR_OPT_DETERMINISTIC = 9,
   GR_OPT_WGRAD_ROWS = 10,
   GR_OPT_PANEL_VEC = 11,
-  GR_OPT_COUNT_ = 12
+  GR_OPT_ATTN_BWD_WIDE_DS = 12,
+  GR_OPT_COUNT_ = 13
 };
 GR_API int gr_set_option(int option, int64_t value);
 GR_API int64_t gr_get_option(int option);
@@ -272,6 +278,12 @@ GR_API int hstu_attn_fwd_bf16(const float* q, const float* k, const float* v, in
  * bucket map) holds one partial slab per workgroup, reduced in a fixed order.
  */
 GR_API size_t hstu_attn_bwd_workspace_size(int B, int N, int max_len, int H, int num_buckets);
+/* ABI 13: the same with the head dims, needed with or without a bucket map: at wide heads
+ * (dqk or dv > 128, GR_OPT_ATTN_BWD_WIDE_DS) it also holds the dS tiles of the dQ pass
+ * (B H ceil(N/16) (ceil(N/16) + 1) / 2 tiles of 1 KiB: 275 MB at C3).  A smaller
+ * workspace (the size above) still works: dQ is then recomputed. */
+GR_API size_t hstu_attn_bwd_workspace_size_d(int B, int N, int max_len, int H, int dqk, int dv,
+                                             int num_buckets);
 GR_API int hstu_attn_bwd(const float* q, const float* k, const float* v, int64_t ld_qk,
                   int64_t ld_v, const float* dout, int64_t ld_dout, const int64_t* offsets,
                   int B, int N, int max_len, int H, int dqk, int dv,

@@ -776,7 +776,10 @@ template <int KSTEPS, int VTILES, int TT, bool V2, bool WAIT = false>
 __device__ __forceinline__ bool attn_bwd_dq_ds_body(const AttnBwdArgs& a, const int id) {
   const bool v2 = V2 || a.vec2, v2h = V2 || a.vec2h;
   using C = AttnBwdCfg<KSTEPS, VTILES, TT>;
-  static_assert(TT == 64, "dQ from dS: 64-row tiles");
+  // TT = 64: 64-key K tiles (narrow heads); TT = 16: 16-key K tiles (wide heads, d > 128),
+  // the epilogue's silu'(h) rows then come from global (the K stage holds 16 rows only)
+  static_assert(TT == 64 || TT == 16, "dQ from dS: 64- or 16-row tiles");
+  constexpr bool WIDE = TT == 16;
   constexpr int LDK = C::LDQ;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* Ks = reinterpret_cast<float*>(smem);  // [TT][LDK]
@@ -846,7 +849,7 @@ __device__ __forceinline__ bool attn_bwd_dq_ds_body(const AttnBwdArgs& a, const 
     if (more) {
       if (WAIT && !wait_tile(tile_of(j + 1))) return false;
       load_tile(tile_of(j + 1), dsn);
-    } else if (a.hq) {  // the epilogue's silu'(h) rows of this workgroup's queries
+    } else if (!WIDE && a.hq) {  // the epilogue's silu'(h) rows of this workgroup's queries
       kst.load(seq_rsrc(a.hq, a.ld_h, s0, h * a.dqk, L, a.dqk), a.ld_h, q0, a.dqk, v2h);
     }
 #pragma unroll
@@ -877,6 +880,13 @@ __device__ __forceinline__ bool attn_bwd_dq_ds_body(const AttnBwdArgs& a, const 
       for (int kb = 0; kb < C::TB; ++kb) dsv[kb] = dsn[kb];
       lds_barrier();
     }
+  }
+  if constexpr (WIDE) {
+    if (!w_ok) return true;
+    store_scaled<4, C::KT>([&](int i, int t) { return dQ[t][i]; }, L, a.dqk, s0, a.dq, a.ld_d, a.hq,
+                           a.ld_h, h * a.dqk, [&](int i) { return wq_lo + 4 * lg + i; },
+                           [&](int t) { return 16 * t + lr; });
+    return true;
   }
   if (a.hq) {
     lds_barrier();
@@ -915,7 +925,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
 }
 template <int KSTEPS, int VTILES, int TT>
 __global__ __launch_bounds__(256) void attn_bwd_dq_ds_kernel(AttnBwdArgs a) {
-  if constexpr (TT == 64) {
+  if constexpr (TT == 64 || TT == 16) {
     if (BWD_V2(a)) attn_bwd_dq_ds_body<KSTEPS, VTILES, TT, true>(a, blockIdx.x);
     else attn_bwd_dq_ds_body<KSTEPS, VTILES, TT, false>(a, blockIdx.x);
   }
@@ -1020,6 +1030,14 @@ static size_t bwd_ds_bytes(int B, int N, int H) {
   return N <= DS_MAX_N && option(GR_OPT_ATTN_BWD_DS) != 0
              ? sizeof(float) * 256 * (size_t)ds_tiles_per_seq(N) * B * H : 0;
 }
+// wide heads (d > 128: 16-row tiles): dS tiles for the dQ pass at any N (WIDE_DS option)
+static bool wide_heads(int dqk, int dv) { return (dqk > dv ? dqk : dv) > 128; }
+static size_t bwd_ds_bytes_d(int B, int N, int H, int dqk, int dv) {
+  if (wide_heads(dqk, dv))
+    return option(GR_OPT_ATTN_BWD_WIDE_DS) != 0
+               ? sizeof(float) * 256 * (size_t)ds_tiles_per_seq(N) * B * H : 0;
+  return bwd_ds_bytes(B, N, H);
+}
 // one-launch form (GR_OPT_ATTN_BWD_DS = 2): a flag word per (sequence, head, key tile)
 static size_t bwd_flag_bytes(int B, int max_len, int H) {
   return option(GR_OPT_ATTN_BWD_DS) == 2 ? 256 + sizeof(uint32_t) * (size_t)B * H * ceil_div(max_len, 64) : 0;
@@ -1057,8 +1075,9 @@ static int launch_bwd(const AttnBwdArgs& a, float* dpos_w, float* dts_w, hipStre
     zero_words_async(a.ds_flags, (int64_t)a.B * a.H * a.n_tiles, st);
     GR_TIMED("attn_bwd", st, hipLaunchKernelGGL(kern, dim3(g + grid), dim3(256), lds, st, af, g));
     GR_LAUNCH_CHECK("hstu_attn_bwd(fused dS)");
-  } else if (TT == 64 && a.ds && !split) {
-    // two passes: dK/dV (+ dS tiles), then dQ = dS K with nothing recomputed
+  } else if (a.ds && !split) {
+    // two passes: dK/dV (+ dS tiles), then dQ = dS K with nothing recomputed (narrow heads
+    // with GR_OPT_ATTN_BWD_DS = 1; wide heads by default, GR_OPT_ATTN_BWD_WIDE_DS)
     auto kkv = a.map_kq ? attn_bwd_dkv_kernel<KS, VT, TT, true> : attn_bwd_dkv_kernel<KS, VT, TT, false>;
     AttnBwdArgs akv = a, aq = a;
     const int s_kv = device_cus() * resident_wgs(kkv, lds_kv);
@@ -1067,7 +1086,7 @@ static int launch_bwd(const AttnBwdArgs& a, float* dpos_w, float* dts_w, hipStre
     GR_TIMED("attn_bwd_dkv", st, hipLaunchKernelGGL(kkv, dim3(n_slabs), dim3(256), lds_kv, st, akv));
     GR_LAUNCH_CHECK("hstu_attn_bwd(dkv)");
     aq.paired = 0;
-    const size_t lds_dq = sizeof(float) * TT * C::LDQ;
+    const size_t lds_dq = sizeof(float) * TT * C::LDQ + 16;
     GR_TIMED("attn_bwd_dq", st, hipLaunchKernelGGL((attn_bwd_dq_ds_kernel<KS, VT, TT>), dim3(grid), dim3(256), lds_dq, st, aq));
     GR_LAUNCH_CHECK("hstu_attn_bwd(dq from dS)");
   } else if (!split && C::KT <= 8) {
@@ -1120,6 +1139,15 @@ extern "C" size_t hstu_attn_bwd_workspace_size(int B, int N, int max_len, int H,
             : gr::bwd_slab_bytes(B, N, max_len, H, num_buckets);
 }
 
+extern "C" size_t hstu_attn_bwd_workspace_size_d(int B, int N, int max_len, int H, int dqk,
+                                                 int dv, int num_buckets) {
+  if (B <= 0 || N <= 0 || H <= 0 || max_len <= 0 || dqk <= 0 || dv <= 0) return 0;
+  if (!gr::wide_heads(dqk, dv)) return hstu_attn_bwd_workspace_size(B, N, max_len, H, num_buckets);
+  const size_t ds = gr::bwd_ds_bytes_d(B, N, H, dqk, dv);
+  return ds ? gr::bwd_ds_offset(B, N, max_len, H, num_buckets) + ds
+            : gr::bwd_slab_bytes(B, N, max_len, H, num_buckets);
+}
+
 extern "C" int hstu_attn_bwd(const float* q, const float* k, const float* v, int64_t ld_qk,
                              int64_t ld_v, const float* dout, int64_t ld_dout,
                              const int64_t* offsets, int B, int N, int max_len, int H, int dqk,
@@ -1160,13 +1188,16 @@ extern "C" int hstu_attn_bwd(const float* q, const float* k, const float* v, int
   a.cus = (int64_t)a.n_tiles * B * H <= 2 * device_cus() ? device_cus() : (1 << 30);
   a.vec2 = pair_aligned({q, k, v, dout}, {ld_qk, ld_v, ld_dout, dqk, dv});
   a.vec2h = hq ? pair_aligned({hq, hk, hv}, {ld_h, dqk, dv}) : 0;
-  // short sequences with a workspace large enough for the dS tiles: two-pass backward
-  if (bucket_map && bwd_ds_bytes(B, N, H) && option(GR_OPT_ATTN_BWD_DS) != 0 &&
-      ws_bytes >= bwd_ds_offset(B, N, max_len, H, num_buckets) + bwd_ds_bytes(B, N, H)) {
+  // a workspace large enough for the dS tiles: two-pass backward (short sequences with
+  // GR_OPT_ATTN_BWD_DS and a bucket map; wide heads at any N, GR_OPT_ATTN_BWD_WIDE_DS)
+  const bool wide = wide_heads(dqk, dv);
+  const size_t ds_b = bwd_ds_bytes_d(B, N, H, dqk, dv);
+  if (workspace && ds_b && (bucket_map || wide) &&
+      ws_bytes >= bwd_ds_offset(B, N, max_len, H, num_buckets) + ds_b) {
     a.ds = (float*)((char*)workspace + bwd_ds_offset(B, N, max_len, H, num_buckets));
     a.ds_tps = ds_tiles_per_seq(N);
-    const size_t fo = (bwd_ds_offset(B, N, max_len, H, num_buckets) + bwd_ds_bytes(B, N, H) + 255) & ~(size_t)255;
-    if (option(GR_OPT_ATTN_BWD_DS) == 2 && ws_bytes >= fo + bwd_flag_bytes(B, max_len, H) - 256)
+    const size_t fo = (bwd_ds_offset(B, N, max_len, H, num_buckets) + ds_b + 255) & ~(size_t)255;
+    if (!wide && option(GR_OPT_ATTN_BWD_DS) == 2 && ws_bytes >= fo + bwd_flag_bytes(B, max_len, H) - 256)
       a.ds_flags = (uint32_t*)((char*)workspace + fo);
   }
   const int d = dqk > dv ? dqk : dv;

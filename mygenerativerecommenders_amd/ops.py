@@ -456,11 +456,15 @@ def _stu_backward(saved, dy, geo: STUGeometry, seed: int, seed_offset, want_uvqk
     if bmap is not None:
         d_pos_w = torch.empty(2 * geo.N - 1, dtype=torch.float32, device=dev)
         d_ts_w = torch.empty(NUM_BUCKETS + 1, dtype=torch.float32, device=dev)
-    if bmap is not None or geo.bf16:  # wide bf16 heads use the workspace without a map too
+    # the workspace: bias slabs (with a map), the wide bf16 form's buffers and the wide
+    # f32 form's dS tiles (with or without a map)
+    if geo.bf16:
         ws_fn = (L.hstu_attn_bwd_bf16_workspace_size_copies if copies is not None else
                  L.hstu_attn_bwd_bf16_workspace_size)
-        ws_a_n = (ws_fn(B, geo.N, geo.max_len, H, dqk, dv, NUM_BUCKETS) if geo.bf16 else
-                  L.hstu_attn_bwd_workspace_size(B, geo.N, geo.max_len, H, NUM_BUCKETS))
+        ws_a_n = ws_fn(B, geo.N, geo.max_len, H, dqk, dv, NUM_BUCKETS)
+    else:
+        ws_a_n = L.hstu_attn_bwd_workspace_size_d(B, geo.N, geo.max_len, H, dqk, dv, NUM_BUCKETS)
+    if ws_a_n or bmap is not None:
         ws_a = torch.empty(max(ws_a_n, 4), dtype=torch.uint8, device=dev)
     q = uvqk[:, 2 * hv:2 * hv + hq]
     k = uvqk[:, 2 * hv + hq:]

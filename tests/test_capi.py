@@ -80,6 +80,13 @@ def test_workspace_size_queries_are_host_only():
         assert L.hstu_attn_bwd_workspace_size(128, 211, 200, 1, 128) == (slabs + 255) // 256 * 256 + ds
     slabs3 = 4 * 32 * 32 * (2 * 2059 - 1 + 129)
     assert L.hstu_attn_bwd_workspace_size(32, 2059, 2048, 1, 128) == slabs3  # no dS above 512
+    # head dims given: narrow heads as above; wide heads (d > 128) add the dS tiles at any N
+    assert L.hstu_attn_bwd_workspace_size_d(32, 2059, 2048, 1, 64, 64, 128) == slabs3
+    ds3 = 4 * 256 * 129 * 130 // 2 * 32
+    assert L.hstu_attn_bwd_workspace_size_d(32, 2059, 2048, 1, 256, 256, 128) == \
+        (slabs3 + 255) // 256 * 256 + ds3
+    with _lib.option("ATTN_BWD_WIDE_DS", 0):
+        assert L.hstu_attn_bwd_workspace_size_d(32, 2059, 2048, 1, 256, 256, 128) == slabs3
     assert L.hstu_bucket_map_bytes(128, 211) == 2 * 128 * 10 * 4096
     assert L.mips_packed_items_bytes(3953, 50) == 4 * ((3953 + 15) // 16) * 7 * 128
     # filter-sized catalogs: f32 blocks | bf16 copy (a full 16x16x32 chunk + 3 of the second
@@ -109,8 +116,10 @@ def test_launch_options_are_explicit_not_environment():
     opts = _lib.parse_options()
     assert set(opts) == {"MIPS_FILTER_FP32", "MIPS_FILTER_WGS", "MIPS_FILTER_ROUNDS",
                          "MIPS_FORCE_FALLBACK", "ATTN_BWD_SPLIT", "ROWWAVE", "ATTN_BWD_PAIRS",
-                         "ATTN_BWD_DS", "DETERMINISTIC", "WGRAD_ROWS", "PANEL_VEC"}
-    defaults = {"MIPS_FILTER_WGS": 2, "ROWWAVE": 1, "ATTN_BWD_PAIRS": 1, "PANEL_VEC": 1}
+                         "ATTN_BWD_DS", "DETERMINISTIC", "WGRAD_ROWS", "PANEL_VEC",
+                         "ATTN_BWD_WIDE_DS"}
+    defaults = {"MIPS_FILTER_WGS": 2, "ROWWAVE": 1, "ATTN_BWD_PAIRS": 1, "PANEL_VEC": 1,
+                "ATTN_BWD_WIDE_DS": 1}
     for n in opts:
         assert _lib.get_option(n) == defaults.get(n, 0), n
     with _lib.option("ATTN_BWD_SPLIT", 1):

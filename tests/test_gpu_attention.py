@@ -135,7 +135,7 @@ def _run_gpu_bwd(offsets, uvqk, dout, ts, pos_w, ts_w, B, N, H, dqk, dv, hpre=No
     max_len = int((offsets[1:] - offsets[:-1]).max()) if B else 0
     L = _lib.lib()
     ws_bytes = (L.hstu_attn_bwd_bf16_workspace_size(B, N, max_len, H, dqk, dv, 128) if bf16
-                else L.hstu_attn_bwd_workspace_size(B, N, max_len, H, 128))
+                else L.hstu_attn_bwd_workspace_size_d(B, N, max_len, H, dqk, dv, 128))
     del thr
     ws = torch.empty(max(ws_bytes, 4), dtype=torch.uint8, device=dev)
     hd = hpre.to(dev) if hpre is not None else None
@@ -274,6 +274,29 @@ def test_attn_bwd_launch_modes_bitexact(B, N, d):
             else:  # bias grads across slab layouts; dQ of the in-launch hand-off (its key
                 # tiles are summed in descending order, as they are published)
                 _close(y, x, rel=1e-6)
+
+
+@pytest.mark.parametrize("B,N,dqk,dv,with_ts", [(2, 300, 256, 256, True), (3, 140, 160, 160, True),
+                                                (2, 90, 200, 136, False)])
+def test_attn_bwd_wide_stored_ds_bitexact(B, N, dqk, dv, with_ts):
+    """Wide heads (d > 128): dQ from the dS tiles the dK/dV pass stores
+    (GR_OPT_ATTN_BWD_WIDE_DS, default) against the recomputing dQ pass (option 0) and
+    against a workspace too small for the tiles (the recomputing form runs): every
+    gradient bit-identical (the same dS values, summed in the same key order), with and
+    without a bucket map, silu'(h) epilogue on."""
+    from mygenerativerecommenders_amd import _lib
+    lengths, offsets, uvqk, ts, pos_w, ts_w = _case(41 + N, B, N, 1, dqk, dv, with_ts=with_ts)
+    g = torch.Generator().manual_seed(4)
+    dout = torch.randn(uvqk.shape[0], dv, generator=g)
+    hpre = torch.randn(uvqk.shape, generator=g)
+    a = _run_gpu_bwd(offsets, uvqk, dout, ts, pos_w, ts_w, B, N, 1, dqk, dv, hpre=hpre)
+    with _lib.option("ATTN_BWD_WIDE_DS", 0):
+        b = _run_gpu_bwd(offsets, uvqk, dout, ts, pos_w, ts_w, B, N, 1, dqk, dv, hpre=hpre)
+    for i, (x, y) in enumerate(zip(a, b)):
+        if i >= 3 and not with_ts:
+            break  # no bias gradients without a bucket map
+        assert torch.isfinite(x).all(), i
+        assert torch.equal(x, y), (i, (x - y).abs().max().item())
 
 
 def test_bucket_map_vs_reference_semantics():
