@@ -107,7 +107,7 @@ def call(name: str, *args):
 KERNEL_NAMES = ("bucket_map", "attn_fwd", "attn_bwd", "attn_bwd_dkv", "attn_bwd_dq", "attn_bias_reduce", "attn_bf16_copies",
                 "ln_uvqk_fwd", "gate_o_fwd", "gate_o_bwd", "ln_uvqk_bwd", "boundary_fwd", "boundary_bwd",
                 "wgrad_partial",
-                "wgrad_reduce", "mips_pack", "mips_select", "mips_merge", "mips_sample", "mips_tau",
+                "wgrad_reduce", "mips_pack", "mips_select", "mips_merge", "mips_small", "mips_sample", "mips_tau",
                 "mips_filter", "mips_select_fallback", "mips_merge_fallback", "cumsum",
                 "dense_to_jagged", "jagged_to_padded", "l2_normalize", "current_embeddings",
                 "sampled_softmax_fwd", "sampled_softmax_bwd", "sampled_softmax_csr",

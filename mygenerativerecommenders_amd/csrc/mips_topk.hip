@@ -612,31 +612,68 @@ struct SelLDS {
   uint32_t s_key[256];
   int64_t s_idx[256];
   int s_src[256];
+  uint32_t part[2][4][2];  // ballot counts per wave, two phases
 };
 
-// k-th largest nonzero key of key[0..M) by 8-bit radix passes (256 threads).
-__device__ void block_radix_kth(const uint32_t* key, int M, int kk, SelLDS& L, uint32_t& kstar,
-                                int& k_rem) {
-  const int tid = threadIdx.x;
-  uint32_t prefix = 0, mask = 0;
-  int need = kk;
-  for (int shift = 24; shift >= 0; shift -= 8) {
-    L.hist[tid] = 0;
-    __syncthreads();
-    for (int e = tid; e < M; e += 256) {
-      const uint32_t x = key[e];
-      if (x != 0u && (x & mask) == prefix) atomicAdd(&L.hist[(x >> shift) & 255], 1);
+// k-th largest nonzero key of key[0..M) (256 threads): a threshold search over the keys,
+// 2 bits per step -- three candidate thresholds, each counted by wave ballots (SALU
+// popcounts, no atomics), one barrier per step.  (An 8-bit radix histogram put every key
+// of a query into the few bins its scores share: LDS atomics serialised on them.)
+template <int PER>
+__device__ void ballot_kth(const uint32_t* key, int M, int kk, SelLDS& L, uint32_t& kstar,
+                           int& k_rem) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  uint32_t kr[PER];
+#pragma unroll
+  for (int t = 0; t < PER; ++t) {
+    const int e = tid + 256 * t;
+    kr[t] = e < M ? key[e] : 0u;
+  }
+  int ph = 0;
+  uint32_t T = 0u;
+  for (int b = 30; b >= 0; b -= 2) {
+    const uint32_t c1 = T | (1u << b), c2 = T | (2u << b), c3 = T | (3u << b);
+    uint32_t n1 = 0, n2 = 0, n3 = 0;
+#pragma unroll
+    for (int t = 0; t < PER; ++t) {
+      n1 += __popcll(__ballot(kr[t] >= c1));
+      n2 += __popcll(__ballot(kr[t] >= c2));
+      n3 += __popcll(__ballot(kr[t] >= c3));
+    }
+    if (lane == 0) {
+      L.part[ph][wv][0] = n1 | (n2 << 16);
+      L.part[ph][wv][1] = n3;
     }
     __syncthreads();
-    if (tid < 64) hist_find_digit(L.hist, need, &L.digit, &L.above);
-    __syncthreads();
-    prefix |= (uint32_t)L.digit << shift;
-    mask |= 0xFFu << shift;
-    need -= L.above;
-    __syncthreads();
+    uint32_t t12 = 0, t3 = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      t12 += L.part[ph][w][0];
+      t3 += L.part[ph][w][1];
+    }
+    ph ^= 1;
+    T = (int)t3 >= kk ? c3 : (int)(t12 >> 16) >= kk ? c2 : (int)(t12 & 0xFFFF) >= kk ? c1 : T;
   }
-  kstar = prefix;
-  k_rem = need;
+  uint32_t gt = 0;
+#pragma unroll
+  for (int t = 0; t < PER; ++t) gt += __popcll(__ballot(kr[t] > T));
+  if (lane == 0) L.part[ph][wv][0] = gt;
+  __syncthreads();
+  uint32_t g = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) g += L.part[ph][w][0];
+  __syncthreads();  // L.part is free again for the caller's next selection
+  kstar = T;
+  k_rem = kk - (int)g;
+}
+
+// k-th largest nonzero key of key[0..M), M <= MERGE_MAX (= 32 keys per thread), k <= 8192
+__device__ void block_kth(const uint32_t* key, int M, int kk, SelLDS& L, uint32_t& kstar,
+                                int& k_rem) {
+  if (M <= 1024) ballot_kth<4>(key, M, kk, L, kstar, k_rem);
+  else if (M <= 2048) ballot_kth<8>(key, M, kk, L, kstar, k_rem);
+  else if (M <= 4096) ballot_kth<16>(key, M, kk, L, kstar, k_rem);
+  else ballot_kth<32>(key, M, kk, L, kstar, k_rem);
 }
 
 __device__ __forceinline__ int block_sum(int v, SelLDS& L) {
@@ -657,7 +694,7 @@ __device__ int block_topk_sorted(const uint32_t* key, const int64_t* idx, int M,
   uint32_t kstar = 0u;
   int k_rem = 0;
   const bool all = tot <= kk;
-  if (!all) block_radix_kth(key, M, kk, L, kstar, k_rem);
+  if (!all) block_kth(key, M, kk, L, kstar, k_rem);
   // ties at kstar: count them; if more than k_rem, keep the smallest indices
   int eq = 0;
   if (!all)
@@ -897,6 +934,195 @@ __global__ __launch_bounds__(256) void mips_scoreall_kernel(ScoreAllArgs a) {
   }
 }
 
+// ----------------------------------------------------------------- small-catalog selection
+// The merge of the score-all lists (X <= MERGE_MAX, k <= 256): one workgroup of 1024
+// threads per query, a thread holding 8 consecutive items' keys in registers:
+//   1. the k-th largest key T by a threshold search, 2 bits per step: three candidate
+//      thresholds per step, their counts packed into one 64-bit block sum -- no
+//      histogram atomics (the radix merge's first digit passes put a query's scores into
+//      a few bins and serialised on them: 31 us per batch at ml-1m);
+//   2. winners = keys > T plus the first k - count(> T) keys == T in index order (one
+//      block scan), compacted in index order, then each written at its rank in
+//      (score desc, index asc) order by counting (<= 256 entries, LDS broadcast reads).
+// Same order and outputs as mips_merge_kernel over the one list (bit-identical).
+struct SmallArgs {
+  const float* score;    // [B][X] (score-all output)
+  const int64_t* index;  // [B][X], -1 = excluded
+  int X, k;
+  const int64_t* item_ids;
+  int64_t index_base;
+  float* out_score;
+  int64_t* out_ids;
+  int64_t* out_index;
+};
+constexpr int SM_T = 1024;                // threads
+constexpr int SM_PER = MERGE_MAX / SM_T;  // consecutive items per thread
+static_assert(SM_PER == 8, "two 16-byte score loads per thread");
+
+// Block totals of per-lane predicates by wave ballots (no lane shuffles): each wave's
+// counts land in one LDS slot, one barrier, every thread sums the 16 slots.  Two phase
+// buffers, so a buffer is rewritten only after the barrier that follows every read of it.
+__device__ __forceinline__ int wave_count(bool p) { return __popcll(__ballot(p)); }
+
+__global__ __launch_bounds__(1024) void mips_small_select_kernel(SmallArgs a) {
+  __shared__ float sc[MERGE_MAX];
+  __shared__ __attribute__((aligned(16))) uint32_t part[2][SM_T / 64][2];
+  __shared__ uint32_t wgt[SM_T / 64], weq[SM_T / 64];
+  __shared__ __attribute__((aligned(16))) uint32_t s_key[256];
+  __shared__ __attribute__((aligned(16))) int s_idx[256];
+  const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int X = a.X, i0 = SM_PER * tid;
+  typedef float fv4 __attribute__((ext_vector_type(4)));
+  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  typedef int i4 __attribute__((ext_vector_type(4)));
+  uint32_t kr[SM_PER];
+  {
+    const float* srow = a.score + (int64_t)q * X;
+    const int64_t* irow = a.index + (int64_t)q * X;
+    float v[SM_PER];
+    int64_t ix[SM_PER];
+    if (i0 + SM_PER <= X && (X & 3) == 0) {  // rows 16-byte aligned
+      const fv4 v0 = *reinterpret_cast<const fv4*>(srow + i0);
+      const fv4 v1 = *reinterpret_cast<const fv4*>(srow + i0 + 4);
+      v[0] = v0.x; v[1] = v0.y; v[2] = v0.z; v[3] = v0.w;
+      v[4] = v1.x; v[5] = v1.y; v[6] = v1.z; v[7] = v1.w;
+#pragma unroll
+      for (int e = 0; e < SM_PER; ++e) ix[e] = irow[i0 + e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < SM_PER; ++e) {
+        const bool in = i0 + e < X;
+        v[e] = in ? srow[i0 + e] : 0.f;
+        ix[e] = in ? irow[i0 + e] : -1;
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < SM_PER; ++e) {
+      kr[e] = ix[e] >= 0 ? ord_key(v[e]) : 0u;
+      if (i0 + e < X) sc[i0 + e] = v[e];
+    }
+  }
+  int ph = 0;
+  // block totals of two wave-uniform counts (each <= 8192: 16 bits)
+  auto block_sum2 = [&](uint32_t c0, uint32_t c1, uint32_t& t0, uint32_t& t1) {
+    if (lane == 0) {
+      part[ph][wv][0] = c0;
+      part[ph][wv][1] = c1;
+    }
+    __syncthreads();
+    t0 = t1 = 0u;
+#pragma unroll
+    for (int w = 0; w < SM_T / 64; w += 2) {
+      const u4 x = *reinterpret_cast<const u4*>(&part[ph][w][0]);
+      t0 += x.x + x.z;
+      t1 += x.y + x.w;
+    }
+    ph ^= 1;
+  };
+  uint32_t nz = 0;
+#pragma unroll
+  for (int e = 0; e < SM_PER; ++e) nz += wave_count(kr[e] != 0u);
+  uint32_t tot_u, unused;
+  block_sum2(nz, 0u, tot_u, unused);
+  const int tot = (int)tot_u;
+  const int kk = a.k;
+  uint32_t T = 1u;  // every nonzero key when tot <= k
+  int k_rem = SM_T * SM_PER;
+  if (tot > kk) {
+    T = 0u;
+    for (int b = 30; b >= 0; b -= 2) {
+      const uint32_t c1 = T | (1u << b), c2 = T | (2u << b), c3 = T | (3u << b);
+      uint32_t n1 = 0, n2 = 0, n3 = 0;
+#pragma unroll
+      for (int e = 0; e < SM_PER; ++e) {
+        n1 += wave_count(kr[e] >= c1);
+        n2 += wave_count(kr[e] >= c2);
+        n3 += wave_count(kr[e] >= c3);
+      }
+      uint32_t t12, t3;
+      block_sum2(n1 | (n2 << 16), n3, t12, t3);
+      T = (int)t3 >= kk ? c3 : (int)(t12 >> 16) >= kk ? c2 : (int)(t12 & 0xFFFF) >= kk ? c1 : T;
+    }
+    uint32_t gt = 0;
+#pragma unroll
+    for (int e = 0; e < SM_PER; ++e) gt += wave_count(kr[e] > T);
+    uint32_t gt_tot;
+    block_sum2(gt, 0u, gt_tot, unused);
+    k_rem = kk - (int)gt_tot;
+  }
+  // winners in index order: the (count > T, count == T) of the items before a thread's
+  // own, from the ballots (lanes below in the wave) plus the waves below
+  uint32_t gt_l = 0, eq_l = 0, gt_w = 0, eq_w = 0;
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+#pragma unroll
+  for (int e = 0; e < SM_PER; ++e) {
+    const uint64_t mg = __ballot(kr[e] > T), me = __ballot(kr[e] == T);
+    gt_l += __popcll(mg & below);
+    eq_l += __popcll(me & below);
+    gt_w += __popcll(mg);
+    eq_w += __popcll(me);
+  }
+  if (lane == 0) {
+    wgt[wv] = gt_w;
+    weq[wv] = eq_w;
+  }
+  __syncthreads();
+  for (int w = 0; w < wv; ++w) {
+    gt_l += wgt[w];
+    eq_l += weq[w];
+  }
+  int gt_b = (int)gt_l, eq_b = (int)eq_l;
+#pragma unroll
+  for (int e = 0; e < SM_PER; ++e) {
+    const uint32_t x = kr[e];
+    if (x == 0u) continue;
+    int pos = -1;
+    if (x > T) {
+      pos = gt_b + (eq_b < k_rem ? eq_b : k_rem);
+      ++gt_b;
+    } else if (x == T) {
+      if (eq_b < k_rem) pos = gt_b + eq_b;
+      ++eq_b;
+    }
+    if (pos >= 0) {
+      s_key[pos] = x;
+      s_idx[pos] = i0 + e;
+    }
+  }
+  const int n_sel = tot < kk ? tot : kk;
+  for (int p = n_sel + tid; p < 256; p += SM_T) {  // padding: sorts after every winner
+    s_key[p] = 0u;
+    s_idx[p] = 0x7fffffff;
+  }
+  __syncthreads();
+  // rank of each winner in (key desc, index asc) order: 16-byte broadcast reads
+  if (tid < n_sel) {
+    const uint32_t x = s_key[tid];
+    const int ix = s_idx[tid];
+    int r = 0;
+    const int nq = (n_sel + 3) >> 2;
+#pragma unroll 4
+    for (int f = 0; f < nq; ++f) {
+      const u4 y = *reinterpret_cast<const u4*>(&s_key[4 * f]);
+      const i4 z = *reinterpret_cast<const i4*>(&s_idx[4 * f]);
+      r += (y.x > x) | ((y.x == x) & (z.x < ix));
+      r += (y.y > x) | ((y.y == x) & (z.y < ix));
+      r += (y.z > x) | ((y.z == x) & (z.z < ix));
+      r += (y.w > x) | ((y.w == x) & (z.w < ix));
+    }
+    const int64_t o = (int64_t)q * kk + r;
+    const int64_t gi = a.index_base + ix;
+    a.out_score[o] = sc[ix];
+    if (a.out_index) a.out_index[o] = gi;
+    a.out_ids[o] = a.item_ids ? a.item_ids[ix] : gi;
+  } else if (tid < kk) {
+    const int64_t o = (int64_t)q * kk + tid;
+    a.out_score[o] = -INFINITY;
+    if (a.out_index) a.out_index[o] = -1;
+    a.out_ids[o] = -1;
+  }
+}
+
 // ----------------------------------------------------------------- large catalogs
 // Threshold-filter path (D <= 64, X >= FILTER_MIN_X).  The 16-query-per-workgroup
 // select above re-reads the table once per query group (8x at B = 128) and keeps
@@ -911,7 +1137,7 @@ __global__ __launch_bounds__(256) void mips_scoreall_kernel(ScoreAllArgs a) {
 //      sampled) about M_SAMPLE * SR do.
 //   3. filter:  full pass; scores >= tau_q are appended (global atomics; ~1e-4 of
 //      scores) to a per-query list of FILTER_CAP.
-//   4. merge:   per query, drop invalid ids, exact top-k (radix select + sort).  Every
+//   4. merge:   per query, drop invalid ids, exact top-k (threshold select + sort).  Every
 //      uncollected item scores < tau_q <= every collected one, so the result is exact
 //      whenever the list did not overflow and kept >= k valid items.  Otherwise the
 //      merge raises a device flag and the exact select + merge kernels above (gated on
@@ -1289,7 +1515,7 @@ __global__ __launch_bounds__(256) void mips_tau_kernel(TauArgs a) {
   const int m = a.G < M_SAMPLE ? a.G : M_SAMPLE;
   uint32_t kstar;
   int k_rem;
-  block_radix_kth(key, a.G, m, L, kstar, k_rem);
+  block_kth(key, a.G, m, L, kstar, k_rem);
   if (tid < NSUB) a.cnt[q * NSUB + tid] = 0;
   if (a.q_rows && tid < a.DP) a.q_rows[(int64_t)q * a.DP + tid] = tid < a.D ? a.q[(int64_t)q * a.D + tid] : 0.f;
   // ||q||^2, ||q~||^2, ||q~ - q||^2 by wave 0 (lane-strided partial sums, fixed-order
@@ -1934,10 +2160,9 @@ extern "C" int mips_topk(const float* queries, const float* packed_items, int64_
     }
 #undef GR_SA
     GR_LAUNCH_CHECK("mips_topk(score-all)");
-    MergeArgs m{sc, ix, nullptr, 1, B, (int)X, k, item_ids, index_base,
-                out_scores, out_ids, out_index, nullptr};
-    GR_TIMED("mips_merge", st, hipLaunchKernelGGL(mips_merge_kernel, dim3(B), dim3(256), 0, st, m));
-    GR_LAUNCH_CHECK("mips_topk(merge)");
+    SmallArgs m{sc, ix, (int)X, k, item_ids, index_base, out_scores, out_ids, out_index};
+    GR_TIMED("mips_small", st, hipLaunchKernelGGL(mips_small_select_kernel, dim3(B), dim3(SM_T), 0, st, m));
+    GR_LAUNCH_CHECK("mips_topk(small select)");
     return 0;
   }
   char* ws = (char*)workspace;

@@ -581,6 +581,25 @@ def _fuse_boundaries(geo: STUGeometry) -> bool:
     return FUSE_BOUNDARIES and not geo.bf16 and not geo.concat_ua
 
 
+# weight gradients of layers L-1 .. 1 on a side stream, each launched as soon as its layer's
+# backward is enqueued, so they run beside the later layers' critical-path kernels; layer
+# 0's runs on the main stream, which is the join.  Measured slower at C2 (0.872 vs 0.795 ms
+# per step, r4h: the side-stream GEMMs take the CUs the attention backward's tail would
+# free and the launches no longer batch), so off by default: all layers' weight gradients
+# in one launch at the end.
+OVERLAP_WGRAD = False
+_SIDE_STREAMS: dict = {}
+
+
+def _side_stream(device):
+    key = (device.type, device.index)
+    s = _SIDE_STREAMS.get(key)
+    if s is None:
+        s = torch.cuda.Stream(device=device)
+        _SIDE_STREAMS[key] = s
+    return s
+
+
 def launch_wgrad_multi(problems, offsets, rows, bf16: bool):
     """Launches the deferred weight-gradient problems (``_stu_backward(defer_wgrad=True)``)
     through gr_wgrad_multi, up to 16 per launch."""
@@ -604,9 +623,9 @@ class STUStackFunction(torch.autograd.Function):
     """Every STU layer of an encoder (HSTUJagged.jagged_forward's loop, hstu.py:467-478)
     as ONE autograd node.  Forward: the per-layer launches of ``_stu_forward``.  Backward:
     the per-layer critical path (gate_o_bwd, attention backward, ln_uvqk_bwd) layer by
-    layer, and the weight gradients of ALL layers afterwards in one gr_wgrad_multi (one
-    partial + one reduce launch for the encoder instead of two per layer: at ml-1m each
-    layer's pair is latency-bound, 4 x 32 us).
+    layer; each layer's two weight-gradient GEMMs as one gr_wgrad_multi launch on a side
+    stream beside the later layers (``OVERLAP_WGRAD``), or all layers' in one launch at
+    the end.
     params: per layer (_uvqk, _o.weight, _o.bias, _pos_w or None, _ts_w or None)."""
 
     @staticmethod
@@ -641,6 +660,8 @@ class STUStackFunction(torch.autograd.Function):
         offsets = saved[1]
         rows = saved[0].shape[0]
         fuse = _fuse_boundaries(geo)
+        main = torch.cuda.current_stream(offsets.device)
+        side = _side_stream(offsets.device) if OVERLAP_WGRAD and n_layers > 1 else None
         pre_d = None
         for l in reversed(range(n_layers)):
             sl = saved[_SAVED_PER_LAYER * l:_SAVED_PER_LAYER * (l + 1)]
@@ -652,9 +673,19 @@ class STUStackFunction(torch.autograd.Function):
                 sl, dy, geo, ctx.seeds[l], ctx.seed_offset, want_uvqk, defer_wgrad=True,
                 pre_d=pre_d, prev=prev)
             grads[5 * l:5 * l + 5] = [d_w_uvqk, d_w_o, d_b_o, d_pos_w, d_ts_w]
-            problems.extend(probs)
+            if side is not None and l > 0 and probs:
+                side.wait_stream(main)  # this layer's operands are enqueued on main
+                with torch.cuda.stream(side):
+                    launch_wgrad_multi(probs, offsets, rows, geo.bf16)
+                for _, keep in probs:  # no reuse of their memory before the side stream ran
+                    for t in keep:
+                        t.record_stream(side)
+            else:
+                problems.extend(probs)
             dy = dx
         launch_wgrad_multi(problems, offsets, rows, geo.bf16)
+        if side is not None:
+            main.wait_stream(side)
         return (dy, None, None, None, None, None, None, *grads)
 
 

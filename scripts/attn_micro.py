@@ -77,7 +77,7 @@ def main():
     _lib.set_option("ATTN_BWD_PAIRS", 0 if args.nopairs else args.pairs)
     _lib.set_option("ATTN_BWD_DS", int(args.ds))  # before the workspace size query
     ws_n = (L_.hstu_attn_bwd_bf16_workspace_size(B, N, L, H, d, d, 128) if args.bf16
-            else L_.hstu_attn_bwd_workspace_size(B, N, L, H, 128))
+            else L_.hstu_attn_bwd_workspace_size_d(B, N, L, H, d, d, 128))
     ws = torch.empty(max(ws_n, 4), dtype=torch.uint8, device=dev)
     st = _lib.stream_handle()
 

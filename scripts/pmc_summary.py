@@ -28,6 +28,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 _MAP = [
     (r"bucket_map_kernel", "bucket_map"),
+    (r"rowwave2_kernel<.*RwGateOBwd", "boundary_bwd"),
+    (r"rowwave2_kernel", "boundary_fwd"),
+    (r"mips_small_select_kernel", "mips_small"),
+    (r"current_embeddings_kernel", "current_embeddings"),
     (r"attn_bwd_bf16w_kv_kernel|attn_bwd_bf16_dkv_kernel", "attn_bwd_dkv"),
     (r"attn_bwd_bf16w_dq_kernel|attn_bwd_bf16_dq_kernel", "attn_bwd_dq"),
     (r"attn_fwd_bf16w_kernel|attn_fwd_bf16_kernel", "attn_fwd"),

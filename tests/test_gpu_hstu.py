@@ -453,3 +453,69 @@ def test_hstu_stack_boundaries_match_unfused(B, N0, D, hdv, blocks, act, dropout
     close(dx0, dx1, "dx")
     for n in g0:
         close(g0[n], g1[n], n)
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+def test_hstu_stack_wgrad_overlap(bf16):
+    """Weight gradients on the side stream (ops.OVERLAP_WGRAD: layer l's launched beside
+    the later layers' backward, layer 0's on the main stream) against all layers' in one
+    launch at the end, eager and under HIP-graph capture: output and input gradient
+    bit-identical, weight gradients equal to fp32 split-K order (1e-5 relative)."""
+    from mygenerativerecommenders_amd import ops
+    from mygenerativerecommenders_amd.hstu import HSTU
+    torch.manual_seed(2)
+    B, N0, out_len, D, blocks = 8, 200, 11, 50, 4
+    N = N0 + out_len
+    enc = HSTU(max_sequence_len=N0, max_output_len=out_len, embedding_dim=D,
+               item_embedding_dim=D, num_blocks=blocks, num_heads=1, linear_dim=D,
+               attention_dim=D, normalization="rel_bias", linear_config="uvqk",
+               linear_activation="silu", linear_dropout_rate=0.2, attn_dropout_rate=0.0,
+               autocast_dtype=torch.bfloat16 if bf16 else None).cuda().train()
+    g = torch.Generator().manual_seed(9)
+    lengths = torch.randint(N0 // 3, N0 + 1, (B,), generator=g).cuda()
+    x = torch.randn(B, N, D, generator=g).cuda()
+    ts = (1_000_000_000 + torch.cumsum(torch.randint(0, 200_000, (B, N), generator=g), 1)).cuda()
+    dy = torch.randn(B, N, D, generator=g).cuda()
+
+    def run():
+        enc._hstu._dropout_step.zero_()
+        enc.zero_grad(set_to_none=False)
+        xg = x.clone().requires_grad_(True)
+        y, _ = enc(lengths, xg, None, {"timestamps": ts})
+        (y * dy).sum().backward()
+        return y.detach().clone(), xg.grad.clone(), {n: p.grad.clone() for n, p in enc.named_parameters()}
+
+    outs = []
+    try:
+        for ov in (True, False):
+            ops.OVERLAP_WGRAD = ov
+            outs.append(run())
+        # the overlapped form captured in a graph and replayed
+        ops.OVERLAP_WGRAD = True
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            run()
+        torch.cuda.current_stream().wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        enc._hstu._dropout_step.zero_()
+        xg = x.clone().requires_grad_(True)
+        with torch.cuda.graph(graph):
+            y, _ = enc(lengths, xg, None, {"timestamps": ts})
+            (y * dy).sum().backward()
+        enc._hstu._dropout_step.zero_()
+        for p in enc.parameters():
+            p.grad.zero_()
+        xg.grad.zero_()
+        graph.replay()
+        torch.cuda.synchronize()
+        outs.append((y.detach().clone(), xg.grad.clone(), {n: p.grad.clone() for n, p in enc.named_parameters()}))
+    finally:
+        ops.OVERLAP_WGRAD = False
+    (y0, dx0, g0) = outs[1]
+    for y1, dx1, g1 in (outs[0], outs[2]):
+        assert torch.equal(y0, y1)
+        assert torch.equal(dx0, dx1)
+        for n in g0:
+            err = (g0[n] - g1[n]).abs().max().item()
+            assert err <= 1e-5 * (1 + g0[n].abs().max().item()), (n, err)

@@ -119,6 +119,35 @@ def test_mips_topk_adversarial_orderings():
     _check_exact(Q, E3, np.arange(150, dtype=np.int64), inv3, k)
 
 
+def test_mips_topk_small_path_edges():
+    """The one-kernel small-catalog path (X <= 8192, D <= 64, k <= 256) at its edges:
+    X = 8192 exactly, k = 256, all-equal scores (ties by index), sorted scores, -0.0 vs
+    +0.0 ties, explicit ids with a long sorted invalid list (N0 = 2059), every item
+    invalid, and X < k."""
+    g = np.random.default_rng(17)
+    B, D = 9, 64
+    X = 8192
+    Q = g.standard_normal((B, D), dtype=np.float32)
+    E = g.standard_normal((X, D), dtype=np.float32)
+    _check_exact(Q, E, np.arange(1, X + 1, dtype=np.int64), None, 256)
+    E2 = np.ones((X, D), np.float32)
+    inv = np.zeros((B, 40), np.int64)
+    inv[:, :20] = np.arange(1, 21)[None, :]
+    _check_exact(np.abs(Q), E2, np.arange(1, X + 1, dtype=np.int64), inv, 200)
+    base = np.linspace(-1.0, 1.0, X, dtype=np.float32)[:, None]
+    _check_exact(np.abs(Q), (base * np.ones((1, D), np.float32)).astype(np.float32),
+                 np.arange(X, dtype=np.int64), None, 256)
+    E0 = np.zeros((777, D), np.float32)  # every score +-0: ties resolved by index
+    E0[::3, 0] = -0.0
+    _check_exact(Q, E0, np.arange(777, dtype=np.int64), None, 100)
+    ids = g.permutation(np.arange(7, 7 + 2 * 3953, 2, dtype=np.int64))
+    inv2 = np.stack([g.choice(ids, 2059) for _ in range(B)])
+    _check_exact(Q[:, :50].copy(), E[:3953, :50].copy(), ids, inv2, 200)
+    inv3 = np.tile(np.arange(300, dtype=np.int64)[None, :], (B, 1))  # all invalid
+    _check_exact(Q[:, :16].copy(), E[:300, :16].copy(), np.arange(300, dtype=np.int64), inv3, 50)
+    _check_exact(Q[:, :8].copy(), E[:37, :8].copy(), np.arange(37, dtype=np.int64), None, 200)
+
+
 def test_sharded_merge_equals_full():
     from mygenerativerecommenders_amd.top_k import PackedItems, merge_topk, mips_topk
     g = np.random.default_rng(11)
