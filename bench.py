@@ -563,6 +563,8 @@ def main():
     ap.add_argument("--no-bf16-leg", action="store_true", help="skip the C2 bf16-attention leg")
     ap.add_argument("--c5-steps", type=int, default=3,
                     help="timed steps of the full C5-shaped train step (tables, Muon; 0 = skip)")
+    ap.add_argument("--opt", action="append", default=[],
+                    help="library launch option NAME=VALUE (gr_set_option), for A/B runs")
     ap.add_argument("--cpu-batch", type=int, default=128,
                     help="sequences per iteration of the CPU proxy baseline")
     args = ap.parse_args()
@@ -574,6 +576,9 @@ def main():
                                                           init_from_env, shard_bounds)
     from mygenerativerecommenders_amd.ops import get_current_embeddings
     from mygenerativerecommenders_amd.top_k import MIPSBruteForceTopK
+    for o in args.opt:
+        name, val = o.split("=")
+        _lib.set_option(name, int(val))
 
     # GR_BENCH_SHARED_GPU=1: rehearsal of the N > 1 path on a one-GPU box (every rank on
     # cuda:0, gloo instead of RCCL); numbers from such a run are not scaling results

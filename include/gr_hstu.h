@@ -84,6 +84,13 @@ GR_API int gr_timing_reset(void);
  *                                  launch without recomputing S / dP (default 1), or 0 = the
  *                                  recomputing dQ pass.  Needs the workspace of
  *                                  hstu_attn_bwd_workspace_size_d (which depends on it).
+ *   GR_OPT_ATTN_BWD_WIDE_SPLIT 0|1|2 f32 attention backward at wide heads with stored dS:
+ *                                  dV and dK in separate workgroups of one launch (1, default),
+ *                                  as two launches (2), or both in one workgroup (0)
+ *   GR_OPT_MIPS_FILTER_PAIRED 0|1  filter pass with several query chunks (D > 64 at B = 128):
+ *                                  the chunks of one item range run on one XCD back to back
+ *                                  (default 1: the range streams from HBM once) or as the
+ *                                  2-D grid (0: every chunk streams the table)
  */
 enum {
   GR_OPT_MIPS_FILTER_FP32 = 1,
@@ -98,7 +105,9 @@ enum {
   GR_OPT_WGRAD_ROWS = 10,
   GR_OPT_PANEL_VEC = 11,
   GR_OPT_ATTN_BWD_WIDE_DS = 12,
-  GR_OPT_COUNT_ = 13
+  GR_OPT_ATTN_BWD_WIDE_SPLIT = 13,
+  GR_OPT_MIPS_FILTER_PAIRED = 14,
+  GR_OPT_COUNT_ = 15
 };
 GR_API int gr_set_option(int option, int64_t value);
 GR_API int64_t gr_get_option(int option);

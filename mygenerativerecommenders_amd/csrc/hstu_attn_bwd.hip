@@ -127,10 +127,21 @@ struct AttnBwdCfg {
 // mod 32.
 __host__ __device__ constexpr int dts_stride(int nb1) { return ((nb1 + 30) / 32) * 32 + 1; }
 
-template <int KSTEPS, int VTILES, int TT, bool HB, bool V2>
+// KIND: 0 = dK, dV and the bias gradients in one pass; 1 = dV only (S, P, dV += P^T dO);
+// 2 = dK only (S, dP, dS, dK += dS^T Q, the bias gradients, the stored dS).  The wide
+// heads (d > 128) run kinds 1 and 2 as separate workgroups: one pass holding the K and V
+// fragments, both accumulators and the block's operands needed ~460 registers (one wave
+// per SIMD and ~370 AGPR copies per block); a kind holds about half (two waves per SIMD)
+// for 25 % more MFMA work (S is formed by both kinds).
+template <int KSTEPS, int VTILES, int TT, bool HB, bool V2, int KIND = 0>
 __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const int id) {
   // V2: 8-byte pair staging known at compile time (see BWD_V2 below)
   const bool v2 = V2 || a.vec2, v2h = V2 || a.vec2h;
+  constexpr bool DO_V = KIND != 2, DO_K = KIND != 1;
+  // A-operand (Q / dO rows) reads of a block: all before the first MFMA, or for the wide
+  // heads a window of PW k-steps read ahead of the MFMAs (64 + 64 operands in registers
+  // at d = 256 otherwise)
+  constexpr int PW = KSTEPS > 16 ? 8 : KSTEPS;
   using C = AttnBwdCfg<KSTEPS, VTILES, TT>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* Qs = reinterpret_cast<float*>(smem);  // [TT][LDQ]
@@ -164,8 +175,9 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
   const int b = bh / a.H, h = bh % a.H;
   const int64_t s0 = a.offsets[b];
   const int L = (int)(a.offsets[b + 1] - s0);
-  constexpr bool has_bias = HB;  // compile-time: the 4 bias gathers of a lane issue together
-  float* slab = a.slabs ? a.slabs + (int64_t)id * nbins : nullptr;
+  constexpr bool has_bias = HB && DO_K;  // compile-time: the 4 bias gathers of a lane issue together
+  constexpr bool bias_in_s = HB;          // S includes the bias in both kinds
+  float* slab = a.slabs && DO_K ? a.slabs + (int64_t)id * nbins : nullptr;
   const int tid = threadIdx.x, w = wave_id(), lane = tid & 63;
   const int lr = lane & 15, lg = lane >> 4;
 
@@ -174,11 +186,12 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
       for (int i = tid; i < nbins; i += 256) slab[i] = 0.f;
     return;
   }
-  if (has_bias) {
+  if (bias_in_s) {
     for (int i = tid; i <= a.nb; i += 256) tsw[i] = a.ts_w[i];
     for (int i = tid; i < npos; i += 256) posw[i] = a.pos_w[i];
-    for (int i = tid; i < 4 * wbins; i += 256) hist[i] = 0.f;
   }
+  if (has_bias)
+    for (int i = tid; i < 4 * wbins; i += 256) hist[i] = 0.f;
   float* whist = hist + w * wbins;
   float* wts = whist + npos + (lr % GR_DTS_COPIES) * tss;
   float carry = 0.f;   // dpos: diagonal partial sums handed to the next block
@@ -221,8 +234,10 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
       const int d = 4 * st + lg;
       const float x = krow[d < a.dqk ? d : a.dqk - 1];
       kreg[st] = d < a.dqk ? x : 0.f;
-      const float y = vrow[d < a.dv ? d : a.dv - 1];
-      vreg[st] = d < a.dv ? y : 0.f;
+      if (DO_K) {
+        const float y = vrow[d < a.dv ? d : a.dv - 1];
+        vreg[st] = d < a.dv ? y : 0.f;
+      }
     }
   }
   f4 dV[VTILES], dK[C::KT];
@@ -296,15 +311,15 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
         f4 s = f4_zero(), dp = f4_zero();
         const float* qrow = Qs + (qb * 16 + lr) * C::LDQ + lg;
         const float* drow = Ds + (qb * 16 + lr) * C::LDV + lg;
-        // every LDS operand of the block is requested before the first MFMA (the
-        // chain then waits on in-order completions instead of one round trip per
-        // k-step); the bias terms are gathered in the same burst
-        float qa[KSTEPS], da[KSTEPS], bias[4];
+        // the block's LDS operands are requested before the first MFMA (the chain then
+        // waits on in-order completions instead of one round trip per k-step), PW
+        // k-steps ahead; the bias terms are gathered in the same burst
+        float qa[PW], da[PW], bias[4];
         int bk[4];
 #pragma unroll
-        for (int st = 0; st < KSTEPS; ++st) {
+        for (int st = 0; st < PW; ++st) {
           qa[st] = qrow[4 * st];
-          da[st] = drow[4 * st];
+          if (DO_K) da[st] = drow[4 * st];
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -312,13 +327,19 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
           int pi = a.N - 1 + kj - qi;
           pi = pi < 0 ? 0 : (pi > npos - 1 ? npos - 1 : pi);
           bk[r] = (mw[qb] >> (8 * r)) & 0xFF;
-          bias[r] = has_bias ? posw[pi] + tsw[bk[r]] : 0.f;
+          bias[r] = bias_in_s ? posw[pi] + tsw[bk[r]] : 0.f;
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int st = 0; st < KSTEPS; ++st) {
-          s = mfma16x16x4(qa[st], kreg[st], s);
-          dp = mfma16x16x4(da[st], vreg[st], dp);
+          const float q0v = qa[st % PW];
+          const float d0v = DO_K ? da[st % PW] : 0.f;
+          if (PW < KSTEPS && st + PW < KSTEPS) {
+            qa[st % PW] = qrow[4 * (st + PW)];
+            if (DO_K) da[st % PW] = drow[4 * (st + PW)];
+          }
+          s = mfma16x16x4(q0v, kreg[st], s);
+          if (DO_K) dp = mfma16x16x4(d0v, vreg[st], dp);
         }
         GR_ST(st_mm1, s[0] + dp[0]);
         float p[4], ds[4];
@@ -329,17 +350,15 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
           const bool ok = k_ok && qi < L && kj <= qi;
           okr[r] = ok;
           float x = s[r];
-          int pi = a.N - 1 + kj - qi;
-          pi = pi < 0 ? 0 : (pi > npos - 1 ? npos - 1 : pi);
-          if (has_bias) x = x + bias[r];
+          if (bias_in_s) x = x + bias[r];
           const float sg = sigmoidf_(x);
-          p[r] = ok ? x * sg * a.inv_n : 0.f;
-          ds[r] = ok ? dp[r] * (sg * (1.0f + x * (1.0f - sg))) * a.inv_n : 0.f;
+          p[r] = DO_V && ok ? x * sg * a.inv_n : 0.f;
+          ds[r] = DO_K && ok ? dp[r] * (sg * (1.0f + x * (1.0f - sg))) * a.inv_n : 0.f;
 #ifdef GR_STAMP
           if (r == 3) GR_ST(st_ew, ds[0] + ds[1] + ds[2] + ds[3] + p[0] + p[1] + p[2] + p[3]);
 #endif
         }
-        if (a.ds) {  // dS tile (query block, key block), row-major [query][key]
+        if (DO_K && a.ds) {  // dS tile (query block, key block), row-major [query][key]
           const int qbi = qb0 >> 4, kbi = wk_lo >> 4;
           float* dt = a.ds + ((int64_t)bh * a.ds_tps + qbi * (qbi + 1) / 2 + kbi) * 256;
 #pragma unroll
@@ -403,12 +422,16 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
           for (int stage = 0; stage < 4; ++stage) bias_stage(stage);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
+            if (DO_V) {
 #pragma unroll
-            for (int t = 0; t < VTILES; ++t)
-              dV[t] = mfma16x16x4(p[r], dcol[r * C::LDV + t * 16], dV[t]);
+              for (int t = 0; t < VTILES; ++t)
+                dV[t] = mfma16x16x4(p[r], dcol[r * C::LDV + t * 16], dV[t]);
+            }
+            if (DO_K) {
 #pragma unroll
-            for (int t = 0; t < C::KT; ++t)
-              dK[t] = mfma16x16x4(ds[r], qcol[r * C::LDQ + t * 16], dK[t]);
+              for (int t = 0; t < C::KT; ++t)
+                dK[t] = mfma16x16x4(ds[r], qcol[r * C::LDQ + t * 16], dK[t]);
+            }
           }
         } else {
         // B operands of k-step r+1 are read from LDS while the MFMAs of step r run, and
@@ -490,12 +513,14 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
   }
   // ---- epilogue: rows = keys wk_lo + 4lg + r, cols = lr + 16 t
   if constexpr (!STAGED) {  // silu'(h) from global: every load issued before any store
-    store_scaled<4, VTILES>([&](int i, int t) { return dV[t][i]; }, L, a.dv, s0, a.dvv, a.ld_d, a.hv,
-                            a.ld_h, h * a.dv, [&](int i) { return wk_lo + 4 * lg + i; },
-                            [&](int t) { return 16 * t + lr; });
-    store_scaled<4, C::KT>([&](int i, int t) { return dK[t][i]; }, L, a.dqk, s0, a.dk, a.ld_d, a.hk,
-                           a.ld_h, h * a.dqk, [&](int i) { return wk_lo + 4 * lg + i; },
-                           [&](int t) { return 16 * t + lr; });
+    if (DO_V)
+      store_scaled<4, VTILES>([&](int i, int t) { return dV[t][i]; }, L, a.dv, s0, a.dvv, a.ld_d, a.hv,
+                              a.ld_h, h * a.dv, [&](int i) { return wk_lo + 4 * lg + i; },
+                              [&](int t) { return 16 * t + lr; });
+    if (DO_K)
+      store_scaled<4, C::KT>([&](int i, int t) { return dK[t][i]; }, L, a.dqk, s0, a.dk, a.ld_d, a.hk,
+                             a.ld_h, h * a.dqk, [&](int i) { return wk_lo + 4 * lg + i; },
+                             [&](int t) { return 16 * t + lr; });
   } else
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -923,6 +948,38 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
   else attn_bwd_dkv_body<KSTEPS, VTILES, TT, HB, false>(a, blockIdx.x);
   GR_TL_END(blockIdx.x, 0);
 }
+// wide heads: dV workgroups (even blockIdx) and dK workgroups (odd), key tile j = blockIdx / 2
+template <int KSTEPS, int VTILES, int TT, bool HB>
+__global__ __launch_bounds__(256) void attn_bwd_dkv_split_kernel(AttnBwdArgs a) {
+  const int j = blockIdx.x >> 1;
+  if (blockIdx.x & 1) {
+    if (BWD_V2(a)) attn_bwd_dkv_body<KSTEPS, VTILES, TT, HB, true, 2>(a, j);
+    else attn_bwd_dkv_body<KSTEPS, VTILES, TT, HB, false, 2>(a, j);
+  } else {
+    if (BWD_V2(a)) attn_bwd_dkv_body<KSTEPS, VTILES, TT, HB, true, 1>(a, j);
+    else attn_bwd_dkv_body<KSTEPS, VTILES, TT, HB, false, 1>(a, j);
+  }
+}
+// the same kinds as two launches: dV (235 VGPRs under a two-waves-per-SIMD bound, no
+// histograms: two workgroups per CU) and dK (one wave per SIMD: the dpos histograms of
+// N = 2059 take 76 KB of LDS per workgroup)
+template <int KSTEPS, int VTILES, int TT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void attn_bwd_dv_kernel(AttnBwdArgs a) {
+  if (BWD_V2(a)) attn_bwd_dkv_body<KSTEPS, VTILES, TT, true, true, 1>(a, blockIdx.x);
+  else attn_bwd_dkv_body<KSTEPS, VTILES, TT, true, false, 1>(a, blockIdx.x);
+}
+template <int KSTEPS, int VTILES, int TT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void attn_bwd_dv_nobias_kernel(AttnBwdArgs a) {
+  if (BWD_V2(a)) attn_bwd_dkv_body<KSTEPS, VTILES, TT, false, true, 1>(a, blockIdx.x);
+  else attn_bwd_dkv_body<KSTEPS, VTILES, TT, false, false, 1>(a, blockIdx.x);
+}
+template <int KSTEPS, int VTILES, int TT, bool HB>
+__global__ __launch_bounds__(256) void attn_bwd_dk_kernel(AttnBwdArgs a) {
+  if (BWD_V2(a)) attn_bwd_dkv_body<KSTEPS, VTILES, TT, HB, true, 2>(a, blockIdx.x);
+  else attn_bwd_dkv_body<KSTEPS, VTILES, TT, HB, false, 2>(a, blockIdx.x);
+}
 template <int KSTEPS, int VTILES, int TT>
 __global__ __launch_bounds__(256) void attn_bwd_dq_ds_kernel(AttnBwdArgs a) {
   if constexpr (TT == 64 || TT == 16) {
@@ -1078,12 +1135,29 @@ static int launch_bwd(const AttnBwdArgs& a, float* dpos_w, float* dts_w, hipStre
   } else if (a.ds && !split) {
     // two passes: dK/dV (+ dS tiles), then dQ = dS K with nothing recomputed (narrow heads
     // with GR_OPT_ATTN_BWD_DS = 1; wide heads by default, GR_OPT_ATTN_BWD_WIDE_DS)
-    auto kkv = a.map_kq ? attn_bwd_dkv_kernel<KS, VT, TT, true> : attn_bwd_dkv_kernel<KS, VT, TT, false>;
     AttnBwdArgs akv = a, aq = a;
-    const int s_kv = device_cus() * resident_wgs(kkv, lds_kv);
-    akv.paired = pairs_force || (pairs_on && grid > s_kv && pgrid <= s_kv);
-    n_slabs = akv.paired ? pgrid : grid;
-    GR_TIMED("attn_bwd_dkv", st, hipLaunchKernelGGL(kkv, dim3(n_slabs), dim3(256), lds_kv, st, akv));
+    if (TT == 16 && option(GR_OPT_ATTN_BWD_WIDE_SPLIT) == 2) {
+      // wide heads: a dV launch (no histograms in LDS) then a dK launch
+      auto kv = a.map_kq ? attn_bwd_dv_kernel<KS, VT, TT> : attn_bwd_dv_nobias_kernel<KS, VT, TT>;
+      auto kk = a.map_kq ? attn_bwd_dk_kernel<KS, VT, TT, true> : attn_bwd_dk_kernel<KS, VT, TT, false>;
+      akv.paired = 0;
+      n_slabs = grid;
+      const size_t lds_v = sizeof(float) * (TT * C::LDQ + TT * C::LDV) + tail;
+      GR_TIMED("attn_bwd_dkv", st, hipLaunchKernelGGL(kv, dim3(grid), dim3(256), lds_v, st, akv));
+      GR_TIMED("attn_bwd_dkv", st, hipLaunchKernelGGL(kk, dim3(grid), dim3(256), lds_kv, st, akv));
+    } else if (TT == 16 && option(GR_OPT_ATTN_BWD_WIDE_SPLIT) != 0) {
+      // wide heads: dV and dK workgroups (single tiles, heaviest first)
+      auto ksp = a.map_kq ? attn_bwd_dkv_split_kernel<KS, VT, TT, true> : attn_bwd_dkv_split_kernel<KS, VT, TT, false>;
+      akv.paired = 0;
+      n_slabs = grid;
+      GR_TIMED("attn_bwd_dkv", st, hipLaunchKernelGGL(ksp, dim3(2 * grid), dim3(256), lds_kv, st, akv));
+    } else {
+      auto kkv = a.map_kq ? attn_bwd_dkv_kernel<KS, VT, TT, true> : attn_bwd_dkv_kernel<KS, VT, TT, false>;
+      const int s_kv = device_cus() * resident_wgs(kkv, lds_kv);
+      akv.paired = pairs_force || (pairs_on && grid > s_kv && pgrid <= s_kv);
+      n_slabs = akv.paired ? pgrid : grid;
+      GR_TIMED("attn_bwd_dkv", st, hipLaunchKernelGGL(kkv, dim3(n_slabs), dim3(256), lds_kv, st, akv));
+    }
     GR_LAUNCH_CHECK("hstu_attn_bwd(dkv)");
     aq.paired = 0;
     const size_t lds_dq = sizeof(float) * TT * C::LDQ + 16;

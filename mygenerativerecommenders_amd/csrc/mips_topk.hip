@@ -1174,6 +1174,11 @@ struct FilterArgs {
   const float* rows;    // items, DP floats per row
   const float* q_rows;  // queries, DP floats per row (workspace)
   int DP;
+  // filter pass with several query chunks: a 1-D grid whose workgroups 8 apart (one XCD
+  // under the round-robin placement) take the chunks of one item range in turn, so the
+  // range streams from HBM once and the other chunks read it from that XCD's L2
+  int nch;   // query chunks (0: the 2-D grid, blockIdx.y = chunk)
+  int gx;    // workgroups per chunk
 };
 
 constexpr int WG_CAP = 2048;  // per-workgroup LDS staging of filter hits (~450 expected at 10M)
@@ -1187,8 +1192,15 @@ __global__ __launch_bounds__(256) void mips_filter_kernel(FilterArgs a) {
   constexpr bool BF = KC > 0;
   typedef float fv2 __attribute__((ext_vector_type(2)));
   const int lane = threadIdx.x & 63, lr = lane & 15, lg = lane >> 4;
-  const int64_t wv = (int64_t)blockIdx.x * 4 + wave_id();
-  const int qb = blockIdx.y * (NQG * 16);
+  int bx = blockIdx.x, by = blockIdx.y;
+  if (!SAMPLE && a.nch > 1) {
+    const int xcd = bx & 7, slot = bx >> 3;
+    by = slot % a.nch;
+    bx = (slot / a.nch) * 8 + xcd;
+    if (bx >= a.gx) return;
+  }
+  const int64_t wv = (int64_t)bx * 4 + wave_id();
+  const int qb = by * (NQG * 16);
 
   int64_t b0 = 0, b1 = 0, bstride;
   if (SAMPLE) {
@@ -1451,7 +1463,7 @@ __global__ __launch_bounds__(256) void mips_filter_kernel(FilterArgs a) {
             }
           }
         }
-        const int64_t sub = (int64_t)qq * NSUB + (blockIdx.x & (NSUB - 1));
+        const int64_t sub = (int64_t)qq * NSUB + (bx & (NSUB - 1));
         const int pos = atomicAdd(&a.cnt[sub], 1);
         if (pos < SUBCAP) {
           a.cand_s[sub * SUBCAP + pos] = sc;
@@ -2008,8 +2020,15 @@ static int launch_filter_pair(const FilterArgs& f, const TopkPlan& p, bool sampl
     GR_TIMED("mips_sample", st, hipLaunchKernelGGL((mips_filter_kernel<KS, KC, NQG, true>), g, dim3(256), 0, st, f));
     GR_LAUNCH_CHECK("mips_topk(sample)");
   } else {
-    const dim3 g(ceil_div(p.filter_waves, 4), p.n_chunks);
-    GR_TIMED("mips_filter", st, hipLaunchKernelGGL((mips_filter_kernel<KS, KC, NQG, false>), g, dim3(256), 0, st, f));
+    const int gx = ceil_div(p.filter_waves, 4);
+    FilterArgs fx = f;
+    dim3 g(gx, p.n_chunks);
+    if (p.n_chunks > 1 && option(GR_OPT_MIPS_FILTER_PAIRED) != 0) {
+      fx.nch = p.n_chunks;
+      fx.gx = gx;
+      g = dim3(ceil_div(gx, 8) * 8 * p.n_chunks, 1);
+    }
+    GR_TIMED("mips_filter", st, hipLaunchKernelGGL((mips_filter_kernel<KS, KC, NQG, false>), g, dim3(256), 0, st, fx));
     GR_LAUNCH_CHECK("mips_topk(filter)");
   }
   return 0;

@@ -46,7 +46,11 @@ def main():
                     help="f32 backward dS forms: 1 = two launches, 2 = in-launch hand-off")
     ap.add_argument("--hepi", action="store_true",
                     help="fused silu'(h) epilogue on dQ/dK/dV (as in the training step)")
+    ap.add_argument("--opt", action="append", default=[], help="launch option NAME=VALUE")
     args = ap.parse_args()
+    for o in args.opt:
+        n, v = o.split("=")
+        _lib.set_option(n, int(v))
     B, N, L, d, H = SHAPES[args.shape]
     if args.batch:
         B = args.batch

@@ -117,9 +117,9 @@ def test_launch_options_are_explicit_not_environment():
     assert set(opts) == {"MIPS_FILTER_FP32", "MIPS_FILTER_WGS", "MIPS_FILTER_ROUNDS",
                          "MIPS_FORCE_FALLBACK", "ATTN_BWD_SPLIT", "ROWWAVE", "ATTN_BWD_PAIRS",
                          "ATTN_BWD_DS", "DETERMINISTIC", "WGRAD_ROWS", "PANEL_VEC",
-                         "ATTN_BWD_WIDE_DS"}
+                         "ATTN_BWD_WIDE_DS", "ATTN_BWD_WIDE_SPLIT", "MIPS_FILTER_PAIRED"}
     defaults = {"MIPS_FILTER_WGS": 2, "ROWWAVE": 1, "ATTN_BWD_PAIRS": 1, "PANEL_VEC": 1,
-                "ATTN_BWD_WIDE_DS": 1}
+                "ATTN_BWD_WIDE_DS": 1, "ATTN_BWD_WIDE_SPLIT": 1, "MIPS_FILTER_PAIRED": 1}
     for n in opts:
         assert _lib.get_option(n) == defaults.get(n, 0), n
     with _lib.option("ATTN_BWD_SPLIT", 1):

@@ -280,23 +280,30 @@ def test_attn_bwd_launch_modes_bitexact(B, N, d):
                                                 (2, 90, 200, 136, False)])
 def test_attn_bwd_wide_stored_ds_bitexact(B, N, dqk, dv, with_ts):
     """Wide heads (d > 128): dQ from the dS tiles the dK/dV pass stores
-    (GR_OPT_ATTN_BWD_WIDE_DS, default) against the recomputing dQ pass (option 0) and
-    against a workspace too small for the tiles (the recomputing form runs): every
-    gradient bit-identical (the same dS values, summed in the same key order), with and
-    without a bucket map, silu'(h) epilogue on."""
+    (GR_OPT_ATTN_BWD_WIDE_DS, default) against the recomputing dQ pass (option 0), and
+    the dK/dV forms (GR_OPT_ATTN_BWD_WIDE_SPLIT: dV and dK workgroups in one launch, the
+    default; two launches; one workgroup for both): every gradient bit-identical (the
+    same S, dS values, summed in the same order), with and without a bucket map, silu'(h)
+    epilogue on."""
     from mygenerativerecommenders_amd import _lib
     lengths, offsets, uvqk, ts, pos_w, ts_w = _case(41 + N, B, N, 1, dqk, dv, with_ts=with_ts)
     g = torch.Generator().manual_seed(4)
     dout = torch.randn(uvqk.shape[0], dv, generator=g)
     hpre = torch.randn(uvqk.shape, generator=g)
     a = _run_gpu_bwd(offsets, uvqk, dout, ts, pos_w, ts_w, B, N, 1, dqk, dv, hpre=hpre)
-    with _lib.option("ATTN_BWD_WIDE_DS", 0):
-        b = _run_gpu_bwd(offsets, uvqk, dout, ts, pos_w, ts_w, B, N, 1, dqk, dv, hpre=hpre)
-    for i, (x, y) in enumerate(zip(a, b)):
-        if i >= 3 and not with_ts:
-            break  # no bias gradients without a bucket map
-        assert torch.isfinite(x).all(), i
-        assert torch.equal(x, y), (i, (x - y).abs().max().item())
+    others = []
+    with _lib.option("ATTN_BWD_WIDE_DS", 0):  # recomputing dQ pass (combined dK/dV)
+        others.append(_run_gpu_bwd(offsets, uvqk, dout, ts, pos_w, ts_w, B, N, 1, dqk, dv, hpre=hpre))
+    for sp in (0, 2):  # dK/dV in one workgroup; dV and dK as two launches
+        with _lib.option("ATTN_BWD_WIDE_SPLIT", sp):
+            others.append(_run_gpu_bwd(offsets, uvqk, dout, ts, pos_w, ts_w, B, N, 1, dqk, dv,
+                                       hpre=hpre))
+    for b in others:
+        for i, (x, y) in enumerate(zip(a, b)):
+            if i >= 3 and not with_ts:
+                break  # no bias gradients without a bucket map
+            assert torch.isfinite(x).all(), i
+            assert torch.equal(x, y), (i, (x - y).abs().max().item())
 
 
 def test_bucket_map_vs_reference_semantics():
