@@ -85,8 +85,9 @@ GR_API int gr_timing_reset(void);
  *                                  recomputing dQ pass.  Needs the workspace of
  *                                  hstu_attn_bwd_workspace_size_d (which depends on it).
  *   GR_OPT_ATTN_BWD_WIDE_SPLIT 0|1|2 f32 attention backward at wide heads with stored dS:
- *                                  dV and dK in separate workgroups of one launch (1, default),
- *                                  as two launches (2), or both in one workgroup (0)
+ *                                  dV and dK as two launches (2, default: C3 dK/dV 2.11 ->
+ *                                  1.08 ms per layer), in separate workgroups of one launch
+ *                                  (1), or both in one workgroup (0)
  *   GR_OPT_MIPS_FILTER_PAIRED 0|1  filter pass with several query chunks (D > 64 at B = 128):
  *                                  the chunks of one item range run on one XCD back to back
  *                                  (default 1: the range streams from HBM once) or as the

@@ -215,18 +215,15 @@ inline int resident_wgs(K kernel, size_t lds) {
 // relative-time bucket: max{b : thr[b] <= |dt|}, thr = integer threshold table of the
 // reference bucket fn (hstu.py:579-581, clamped at hstu.py:117-123).
 __device__ __forceinline__ int time_bucket(int64_t dt, const int64_t* thr_lds, int nb) {
-  // max{b <= nb : thr[b] <= |dt|} over the non-decreasing threshold table (thr[0] = 0) by a
-  // fixed 8-step binary search: branch-free, and a thread's calls are independent chains
-  // of LDS reads the compiler interleaves (the log2 estimate + correction loops it replaces
-  // diverged per lane and waited on each LDS read in turn)
-  const uint64_t ad = dt < 0 ? (uint64_t)(-dt) : (uint64_t)dt;
+  uint64_t ad = dt < 0 ? (uint64_t)(-dt) : (uint64_t)dt;
   int b = 0;
-#pragma unroll
-  for (int step = 128; step >= 1; step >>= 1) {
-    const int c = b + step;
-    const int cc = c <= nb ? c : nb;
-    b = (c <= nb && ad >= (uint64_t)thr_lds[cc]) ? c : b;
+  if (ad > 1) {
+    float f = (float)ad;
+    b = (int)(__log2f(f) * 2.30283176f);  // log2(x) * ln(2) / 0.301
+    b = b > nb ? nb : b;
   }
+  while (b < nb && ad >= (uint64_t)thr_lds[b + 1]) ++b;
+  while (b > 0 && ad < (uint64_t)thr_lds[b]) --b;
   return b;
 }
 

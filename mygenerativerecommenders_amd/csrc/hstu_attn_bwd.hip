@@ -263,12 +263,17 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
   // on every workgroup's tail: +16 us per launch at C2).  Wide heads: read in the
   // epilogue (128 prefetched values per lane spilled; their workgroups run for ms)
   if constexpr (STAGED) {
-    // K / V rows k0 .. k0 + 63 (rows past L and columns past dqk / dv read as 0)
-    qst.load(seq_rsrc(a.k, a.ld_qk, s0, h * a.dqk, L, a.dqk), a.ld_qk, k0, a.dqk, v2);
-    dst.load(seq_rsrc(a.v, a.ld_v, s0, h * a.dv, L, a.dv), a.ld_v, k0, a.dv, v2);
-    qst.store(Qs, C::LDQ, v2);
-    dst.store(Ds, C::LDV, v2);
-    load_tile(k0 / TT, mw);  // the first query tile's loads fly while the fragments are read
+    // K / V rows k0 .. k0 + 63 (rows past L and columns past dqk / dv read as 0) in their
+    // own staging registers, issued together with the first query tile's loads: one HBM
+    // round trip for the prologue instead of two (the K / V stores wait only for their
+    // own loads, which were issued first)
+    BufTile<C::KPT, TT> kst0;
+    BufTile<C::VP, TT> vst0;
+    kst0.load(seq_rsrc(a.k, a.ld_qk, s0, h * a.dqk, L, a.dqk), a.ld_qk, k0, a.dqk, v2);
+    vst0.load(seq_rsrc(a.v, a.ld_v, s0, h * a.dv, L, a.dv), a.ld_v, k0, a.dv, v2);
+    load_tile(k0 / TT, mw);
+    kst0.store(Qs, C::LDQ, v2);
+    vst0.store(Ds, C::LDV, v2);
     __syncthreads();
 #pragma unroll
     for (int st = 0; st < KSTEPS; ++st) {
@@ -671,11 +676,14 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& a, const int
       m[kb] = buf_ld_u32(rmap, map_voff, map_soff(q0, kt * TT + kb * 16, true));
   };
   if constexpr (STAGED) {
-    kst.load(seq_rsrc(a.q, a.ld_qk, s0, h * a.dqk, L, a.dqk), a.ld_qk, q0, a.dqk, v2);
-    vst.load(seq_rsrc(a.dout, a.ld_dout, s0, h * a.dv, L, a.dv), a.ld_dout, q0, a.dv, v2);
-    kst.store(Ks, LDK, v2);
-    vst.store(Vs, LDV, v2);
+    // the workgroup's Q / dO rows and the first key tile in one round trip (see dK/dV)
+    BufTile<C::KPT, TT> qst0;
+    BufTile<C::VP, TT> dst0;
+    qst0.load(seq_rsrc(a.q, a.ld_qk, s0, h * a.dqk, L, a.dqk), a.ld_qk, q0, a.dqk, v2);
+    dst0.load(seq_rsrc(a.dout, a.ld_dout, s0, h * a.dv, L, a.dv), a.ld_dout, q0, a.dv, v2);
     load_tile(0, mw);
+    qst0.store(Ks, LDK, v2);
+    dst0.store(Vs, LDV, v2);
     __syncthreads();
 #pragma unroll
     for (int st = 0; st < KSTEPS; ++st) {

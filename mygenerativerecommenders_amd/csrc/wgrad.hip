@@ -84,7 +84,10 @@ struct WgCfg {
   static constexpr int BRPP = WG_THREADS / NP2;                   // B rows per pass
   static constexpr int BPER = WG_CH / BRPP;                       // B loads per thread
   static constexpr int APER = WG_CH * WG_KA / WG_THREADS;         // A loads per thread
-  static constexpr int SUPER = NT <= 8 ? WG_SUPER : 2;             // register budget at NT 13/16
+  // chunks in flight: 4 at every panel width (NT 13: 211 VGPRs, NT 16: 230, no spills; the
+  // workgroup is one per CU either way, 8 waves x > 128 VGPRs).  Two at NT 13/16 left one
+  // chunk of MFMA work (~1.4 us) to cover each chunk's HBM round trip (~4.6 us at C2)
+  static constexpr int SUPER = WG_SUPER;
   static constexpr size_t LDS = sizeof(float) * 2 * WG_CH * (WG_LDA + LDB + 2);
   static_assert(LDS >= sizeof(float) * (4 * NT * 4 * 64 + 4 * 16), "exchange area");
 };
@@ -766,6 +769,13 @@ static WgPlan wgrad_plan(int64_t max_rows, const int* Ka, const int* Nb, int np)
   int target = 2 * device_cus() / (total_panels > 0 ? total_panels : 1);
   if (target < 1) target = 1;
   int64_t rps = (max_rows + target - 1) / target;
+  // many problems over few rows (the encoder's layers in one gr_wgrad_multi launch at C2:
+  // 8 problems x 27 K rows): shorter splits while the grid stays within 8 workgroups per
+  // CU -- every split is a latency chain of chunks (C2, 8 problems, rows per split
+  // 448 (the rule above) -> 111 us partial + reduce, 256 -> 102, 192 -> 95, 128 -> 98)
+  constexpr int64_t RPS_SHORT = 192;
+  if (rps > RPS_SHORT && (max_rows + RPS_SHORT - 1) / RPS_SHORT * total_panels <= 8 * device_cus())
+    rps = RPS_SHORT;
   if (option(GR_OPT_WGRAD_ROWS) > 0) rps = option(GR_OPT_WGRAD_ROWS);
   rps = ((rps + WGB_CH - 1) / WGB_CH) * WGB_CH;  // whole chunks of either panel kind
   if (rps < 4 * WG_CH) rps = 4 * WG_CH;

@@ -11,8 +11,10 @@
   loss    = sum(loss_t * w) / sum(w)
 
 so the (M, R, D) negatives tensor and the (M, R) logits are never materialised.  The
-fused path covers ``LocalNegativesSampler`` + ``DotProductSimilarity`` (the ml-1m / ml-20m
-configs, configs/model/hstu.yaml); other samplers / similarities raise.
+fused path covers ``LocalNegativesSampler`` (the ml-1m / ml-20m configs,
+configs/model/hstu.yaml) and ``InBatchNegativesSampler`` (table = the batch cache of
+negative_sampler.py:153-188, sampled by the reference's draw over it), each with
+``DotProductSimilarity``; other similarities (MoL) raise.
 """
 from __future__ import annotations
 
@@ -21,7 +23,7 @@ import abc
 import torch
 
 from . import ops
-from .negatives_sampler import LocalNegativesSampler, NegativesSampler
+from .negatives_sampler import InBatchNegativesSampler, LocalNegativesSampler, NegativesSampler
 
 
 class AutoregressiveLoss(torch.nn.Module):
@@ -52,14 +54,14 @@ class SampledSoftmaxLoss(AutoregressiveLoss):
         assert output_embeddings.size() == supervision_embeddings.size()
         assert supervision_ids.size() == supervision_embeddings.size()[:-1]
         assert supervision_ids.size() == supervision_weights.size()
-        if not isinstance(negatives_sampler, LocalNegativesSampler):
+        if not isinstance(negatives_sampler, (LocalNegativesSampler, InBatchNegativesSampler)):
             raise NotImplementedError("SampledSoftmaxLoss: the fused path takes a "
-                                      "LocalNegativesSampler")
+                                      "LocalNegativesSampler or an InBatchNegativesSampler")
         if not _is_dot_product(similarity):
             raise NotImplementedError("SampledSoftmaxLoss: the fused path takes "
                                       "DotProductSimilarity")
         offsets = negatives_sampler.sample_offsets(supervision_ids, self._num_to_sample)
-        table = negatives_sampler.normalize_embeddings(negatives_sampler.item_table())
+        table = negatives_sampler.normalized_table()
         positive_embeddings = negatives_sampler.normalize_embeddings(supervision_embeddings)
         jagged_loss = ops.sampled_softmax_loss(
             output_embeddings, positive_embeddings, table, supervision_ids, offsets,

@@ -18,7 +18,11 @@ ap.add_argument("--batch", type=int, default=128)
 ap.add_argument("--k", type=int, default=200)
 ap.add_argument("--n0", type=int, default=211)
 ap.add_argument("--iters", type=int, default=20)
+ap.add_argument("--opt", action="append", default=[], help="launch option NAME=VALUE")
 a = ap.parse_args()
+for o in a.opt:
+    _n, _v = o.split("=")
+    _lib.set_option(_n, int(_v))
 dev = torch.device("cuda")
 g = torch.Generator(device=dev).manual_seed(0)
 E = torch.randn(a.items, a.dim, device=dev, generator=g)

@@ -119,7 +119,7 @@ def test_launch_options_are_explicit_not_environment():
                          "ATTN_BWD_DS", "DETERMINISTIC", "WGRAD_ROWS", "PANEL_VEC",
                          "ATTN_BWD_WIDE_DS", "ATTN_BWD_WIDE_SPLIT", "MIPS_FILTER_PAIRED"}
     defaults = {"MIPS_FILTER_WGS": 2, "ROWWAVE": 1, "ATTN_BWD_PAIRS": 1, "PANEL_VEC": 1,
-                "ATTN_BWD_WIDE_DS": 1, "ATTN_BWD_WIDE_SPLIT": 1, "MIPS_FILTER_PAIRED": 1}
+                "ATTN_BWD_WIDE_DS": 1, "ATTN_BWD_WIDE_SPLIT": 2, "MIPS_FILTER_PAIRED": 1}
     for n in opts:
         assert _lib.get_option(n) == defaults.get(n, 0), n
     with _lib.option("ATTN_BWD_SPLIT", 1):

@@ -281,8 +281,8 @@ def test_attn_bwd_launch_modes_bitexact(B, N, d):
 def test_attn_bwd_wide_stored_ds_bitexact(B, N, dqk, dv, with_ts):
     """Wide heads (d > 128): dQ from the dS tiles the dK/dV pass stores
     (GR_OPT_ATTN_BWD_WIDE_DS, default) against the recomputing dQ pass (option 0), and
-    the dK/dV forms (GR_OPT_ATTN_BWD_WIDE_SPLIT: dV and dK workgroups in one launch, the
-    default; two launches; one workgroup for both): every gradient bit-identical (the
+    the dK/dV forms (GR_OPT_ATTN_BWD_WIDE_SPLIT: dV and dK as two launches, the default;
+    as workgroups of one launch; one workgroup for both): every gradient bit-identical (the
     same S, dS values, summed in the same order), with and without a bucket map, silu'(h)
     epilogue on."""
     from mygenerativerecommenders_amd import _lib
@@ -294,7 +294,7 @@ def test_attn_bwd_wide_stored_ds_bitexact(B, N, dqk, dv, with_ts):
     others = []
     with _lib.option("ATTN_BWD_WIDE_DS", 0):  # recomputing dQ pass (combined dK/dV)
         others.append(_run_gpu_bwd(offsets, uvqk, dout, ts, pos_w, ts_w, B, N, 1, dqk, dv, hpre=hpre))
-    for sp in (0, 2):  # dK/dV in one workgroup; dV and dK as two launches
+    for sp in (0, 1):  # dK/dV in one workgroup; dV and dK workgroups in one launch
         with _lib.option("ATTN_BWD_WIDE_SPLIT", sp):
             others.append(_run_gpu_bwd(offsets, uvqk, dout, ts, pos_w, ts_w, B, N, 1, dqk, dv,
                                        hpre=hpre))

@@ -296,3 +296,50 @@ def test_loss_graph_replays_match_eager():
         # the counting sort's bound checks dropped nothing
         from mygenerativerecommenders_amd.ops import last_sampled_softmax_status
         assert last_sampled_softmax_status() == 0
+
+
+@pytest.mark.parametrize("dedup", [False, True])
+def test_in_batch_negatives_vs_oracle(dedup):
+    """InBatchNegativesSampler (negative_sampler.py:135-211) under the fused loss: the
+    batch's present rows (de-duplicated by id with the reference's own torch.unique call)
+    are the table, offsets are the reference's draw over it (same generator state), and
+    loss, d_out and the embedding-weight gradient (through the cache, the positives and
+    the normalisation) match the float64 oracle run on that table."""
+    from mygenerativerecommenders_amd.losses import SampledSoftmaxLoss
+    from mygenerativerecommenders_amd.negatives_sampler import InBatchNegativesSampler
+    from mygenerativerecommenders_amd.similarity import DotProductSimilarity
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(31 + int(dedup))
+    B, N, D, V, R, T = 6, 40, 48, 90, 64, 0.05
+    weight = torch.randn(V, D, generator=g)
+    ids = torch.randint(1, V, (B, N), generator=g)
+    presences = torch.rand(B, N, generator=g) > 0.25
+    out = torch.randn(int(presences.sum()), D, generator=g)
+    w_p = weight.clone().to(dev).requires_grad_(True)
+    out_p = out.clone().to(dev).requires_grad_(True)
+    ids_d, pres_d = ids.to(dev), presences.to(dev)
+    emb = w_p[ids_d]                                  # (B, N, D): a function of the id
+    sampler = InBatchNegativesSampler(True, 1e-6, dedup)
+    sampler.process_batch(ids_d, pres_d, emb)
+    sup_ids = ids_d[pres_d]
+    sup_emb = emb[pres_d]
+    weights = torch.ones(sup_ids.shape, device=dev)
+    torch.manual_seed(123)
+    loss = SampledSoftmaxLoss(R, T).jagged_forward(out_p, sup_ids, sup_emb, weights, sampler,
+                                                   DotProductSimilarity())
+    loss.backward()
+    torch.manual_seed(123)
+    offsets = sampler.sample_offsets(sup_ids, R)
+    cache_ids = sampler.get_all_ids_and_embeddings()[0].cpu().numpy()
+    table = weight.numpy()[cache_ids]               # the cache rows before normalisation
+    r = loss_oracle.sampled_softmax(out.numpy(), sup_ids.cpu().numpy(), sup_emb.detach().cpu().numpy(),
+                                    weights.cpu().numpy(), table, cache_ids,
+                                    offsets.cpu().numpy(), T, True, 1e-6)
+    assert abs(loss.item() - float(r["loss"])) <= 1e-5 * max(1.0, abs(float(r["loss"])))
+    d_weight = np.zeros((V, D), dtype=np.float64)
+    np.add.at(d_weight, sup_ids.cpu().numpy(), r["d_sup_emb"])
+    np.add.at(d_weight, cache_ids, r["d_table"])
+    _close(out_p.grad.cpu().double().numpy(), r["d_out"], 2e-4, "d_out")
+    _close(w_p.grad.cpu().double().numpy(), d_weight, 2e-4, "d_weight")
+    if dedup:
+        assert len(set(cache_ids.tolist())) == len(cache_ids)
