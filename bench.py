@@ -972,12 +972,15 @@ def main():
         c3_bf16 = c3_leg(True)
     if not args.no_bf16_leg:
         r = encoder_leg(B, N0, out_len, D, blocks, 1, args.steps, 3, device, world, 2500 + rank,
-                        bf16=True)
+                        bf16=True, instrument=True)
+        kps = r["kernel_per_step_ms"]
         c2_bf16 = {"metric": "HSTU seq/s (fwd+bwd)", "value": r["value"], "unit": "seq/s",
                    "ms_per_step": r["ms_per_step"], "dtype": "bf16 operands / fp32 accumulation",
                    "config": {"workload": "C2 encoder train step (fwd+bwd+AdamW), "
                                           "autocast_dtype=bfloat16 (bf16 MFMA operands)",
-                              "global_batch": B * world, "seq_len": N0, "execution": r["execution"]}}
+                              "global_batch": B * world, "seq_len": N0, "execution": r["execution"]},
+                   "per_step_device_ms": {k: round(v, 4) for k, v in sorted(kps.items(),
+                                                                            key=lambda kv: -kv[1])}}
 
     # the reference yaml's 2 blocks (configs/model/hstu.yaml:23) beside BASELINE's 4
     r2b = encoder_leg(B, N0, out_len, D, 2, 1, args.steps, 3, device, world, 2600 + rank)

@@ -68,9 +68,10 @@ GR_API int gr_timing_reset(void);
  *   GR_OPT_ATTN_BWD_DS      0|1|2  f32 attention backward at N <= 512: the dK/dV pass stores dS
  *                                  tiles and dQ = dS K runs without recompute, 1 = in a second
  *                                  launch, 2 = in the same launch (the dQ workgroups take each
- *                                  key tile's dS once its producer publishes it); default 0 =
- *                                  the recomputing one-launch form.  The workspace size
- *                                  (hstu_attn_bwd_workspace_size) depends on this option.
+ *                                  key tile's dS once its producer publishes it), 0 = the
+ *                                  recomputing one-launch form.  Default 1 (C2: 37.8 + 13.0 us
+ *                                  against 57.1 us for the recomputing launch).  The workspace
+ *                                  size (hstu_attn_bwd_workspace_size) depends on this option.
  *   GR_OPT_DETERMINISTIC      0|1  reductions that default to fp32 atomics run in a fixed
  *                                  order instead (gr_item_embedding_bwd: owner-computes)
  *   GR_OPT_WGRAD_ROWS         >=0  f32 / bf16 weight gradients (64-wide panels): rows per
@@ -85,13 +86,16 @@ GR_API int gr_timing_reset(void);
  *                                  recomputing dQ pass.  Needs the workspace of
  *                                  hstu_attn_bwd_workspace_size_d (which depends on it).
  *   GR_OPT_ATTN_BWD_WIDE_SPLIT 0|1|2 f32 attention backward at wide heads with stored dS:
- *                                  dV and dK as two launches (2, default: C3 dK/dV 2.11 ->
- *                                  1.08 ms per layer), in separate workgroups of one launch
- *                                  (1), or both in one workgroup (0)
+ *                                  dV and dK in one workgroup (0, default: C3 dK/dV 1.88 ms
+ *                                  per layer), as separate workgroups of one launch (1:
+ *                                  2.62 ms), or as two launches (2: 2 x 1.08 ms)
  *   GR_OPT_MIPS_FILTER_PAIRED 0|1  filter pass with several query chunks (D > 64 at B = 128):
  *                                  the chunks of one item range run on one XCD back to back
  *                                  (default 1: the range streams from HBM once) or as the
  *                                  2-D grid (0: every chunk streams the table)
+ *   GR_OPT_MIPS_SAMPLE_STRIDE >=0  filter path: item blocks between the blocks the sample
+ *                                  pass scores (0 = 16); the threshold is the (1024 /
+ *                                  stride)-th largest group maximum (~1024 candidates)
  */
 enum {
   GR_OPT_MIPS_FILTER_FP32 = 1,
@@ -108,7 +112,8 @@ enum {
   GR_OPT_ATTN_BWD_WIDE_DS = 12,
   GR_OPT_ATTN_BWD_WIDE_SPLIT = 13,
   GR_OPT_MIPS_FILTER_PAIRED = 14,
-  GR_OPT_COUNT_ = 15
+  GR_OPT_MIPS_SAMPLE_STRIDE = 15,
+  GR_OPT_COUNT_ = 16
 };
 GR_API int gr_set_option(int option, int64_t value);
 GR_API int64_t gr_get_option(int option);

@@ -516,6 +516,27 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
     dst.store(Ds, C::LDV, v2h);
     lds_barrier();
   }
+  if (has_bias && lg == 0) {  // the last block's wrapped diagonals
+    const int bin = a.N - 1 + last_db - 16 + lr;
+    if (bin >= 0 && bin < npos) whist[bin] += carry;
+  }
+  carry = 0.f;
+  // the workgroup's bias slab is written before its dK / dV rows: its barrier then waits
+  // for no stores of this workgroup (a barrier after them drained every one)
+  if (pass == 1 || !(TT == 64 && kt_b >= 0 && kt_b * 64 < L)) {
+    if (has_bias && run_b >= 0) atomicAdd(&wts[run_b], run_s);  // the open dts run
+    if (has_bias && slab) {
+      __syncthreads();
+      for (int i = tid; i < npos; i += 256)
+        slab[i] = ((hist[i] + hist[wbins + i]) + hist[2 * wbins + i]) + hist[3 * wbins + i];
+      for (int i = tid; i <= a.nb; i += 256) {
+        float acc = 0.f;
+        for (int ww = 0; ww < 4; ++ww)
+          for (int c = 0; c < GR_DTS_COPIES; ++c) acc += hist[ww * wbins + npos + c * tss + i];
+        slab[npos + i] = acc;
+      }
+    }
+  }
   // ---- epilogue: rows = keys wk_lo + 4lg + r, cols = lr + 16 t
   if constexpr (!STAGED) {  // silu'(h) from global: every load issued before any store
     if (DO_V)
@@ -557,24 +578,7 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
       if (ok) a.dk[row * a.ld_d + h * a.dqk + c] = g;
     }
   }
-  if (has_bias && lg == 0) {  // the last block's wrapped diagonals
-    const int bin = a.N - 1 + last_db - 16 + lr;
-    if (bin >= 0 && bin < npos) whist[bin] += carry;
-  }
-  carry = 0.f;
   }  // pass
-  if (has_bias && run_b >= 0) atomicAdd(&wts[run_b], run_s);  // the open dts run
-  if (has_bias && slab) {
-    __syncthreads();
-    for (int i = tid; i < npos; i += 256)
-      slab[i] = ((hist[i] + hist[wbins + i]) + hist[2 * wbins + i]) + hist[3 * wbins + i];
-    for (int i = tid; i <= a.nb; i += 256) {
-      float acc = 0.f;
-      for (int ww = 0; ww < 4; ++ww)
-        for (int c = 0; c < GR_DTS_COPIES; ++c) acc += hist[ww * wbins + npos + c * tss + i];
-      slab[npos + i] = acc;
-    }
-  }
 #ifdef GR_STAMP
   if (lane == 0) {
     const int slot = (id * 4 + w) * 12;
@@ -988,8 +992,18 @@ __global__ __launch_bounds__(256) void attn_bwd_dk_kernel(AttnBwdArgs a) {
   if (BWD_V2(a)) attn_bwd_dkv_body<KSTEPS, VTILES, TT, HB, true, 2>(a, blockIdx.x);
   else attn_bwd_dkv_body<KSTEPS, VTILES, TT, HB, false, 2>(a, blockIdx.x);
 }
+__device__ __forceinline__ void bias_grad_reduce_body(const float* slabs, int n_slabs, int n_pos,
+                                                      int n_ts, float* dpos_w, float* dts_w, int blk);
+// dQ = dS K; workgroups past grid_dq reduce the bias slabs the dK/dV launch wrote (no
+// launch of its own: they fill the CUs the light query tiles free)
 template <int KSTEPS, int VTILES, int TT>
-__global__ __launch_bounds__(256) void attn_bwd_dq_ds_kernel(AttnBwdArgs a) {
+__global__ __launch_bounds__(256) void attn_bwd_dq_ds_kernel(AttnBwdArgs a, int grid_dq, int n_slabs,
+                                                             float* dpos_w, float* dts_w) {
+  if ((int)blockIdx.x >= grid_dq) {
+    bias_grad_reduce_body(a.slabs, n_slabs, 2 * a.N - 1, a.nb + 1, dpos_w, dts_w,
+                          (int)blockIdx.x - grid_dq);
+    return;
+  }
   if constexpr (TT == 64 || TT == 16) {
     if (BWD_V2(a)) attn_bwd_dq_ds_body<KSTEPS, VTILES, TT, true>(a, blockIdx.x);
     else attn_bwd_dq_ds_body<KSTEPS, VTILES, TT, false>(a, blockIdx.x);
@@ -1048,13 +1062,13 @@ __global__ __launch_bounds__(256) void attn_bwd_fused_kernel(AttnBwdArgs a, int 
 // ------------------------------------------------------------------ slab reduce
 // Deterministic: a workgroup owns 16 bins; thread (bin, g) sums slabs g, g+16, ... in
 // order (loads 8-deep), then the 16 partials are added in g order.
-__global__ __launch_bounds__(256) void bias_grad_reduce_kernel(const float* slabs, int n_slabs,
-                                                               int n_pos, int n_ts,
-                                                               float* dpos_w, float* dts_w) {
+__device__ __forceinline__ void bias_grad_reduce_body(const float* slabs, int n_slabs, int n_pos,
+                                                      int n_ts, float* dpos_w, float* dts_w,
+                                                      int blk) {
   __shared__ float part[16][17];
   const int nbins = n_pos + n_ts;
   const int bl = threadIdx.x & 15, g = threadIdx.x >> 4;
-  const int i = blockIdx.x * 16 + bl;
+  const int i = blk * 16 + bl;
   const int ic = i < nbins ? i : nbins - 1;
   gptr<float> src = as_global(slabs);
   float acc = 0.f;
@@ -1076,6 +1090,11 @@ __global__ __launch_bounds__(256) void bias_grad_reduce_kernel(const float* slab
     if (i < n_pos) dpos_w[i] = s;
     else dts_w[i - n_pos] = s;
   }
+}
+__global__ __launch_bounds__(256) void bias_grad_reduce_kernel(const float* slabs, int n_slabs,
+                                                               int n_pos, int n_ts,
+                                                               float* dpos_w, float* dts_w) {
+  bias_grad_reduce_body(slabs, n_slabs, n_pos, n_ts, dpos_w, dts_w, blockIdx.x);
 }
 
 static size_t bwd_slab_bytes(int B, int N, int max_len, int H, int nb) {
@@ -1169,8 +1188,11 @@ static int launch_bwd(const AttnBwdArgs& a, float* dpos_w, float* dts_w, hipStre
     GR_LAUNCH_CHECK("hstu_attn_bwd(dkv)");
     aq.paired = 0;
     const size_t lds_dq = sizeof(float) * TT * C::LDQ + 16;
-    GR_TIMED("attn_bwd_dq", st, hipLaunchKernelGGL((attn_bwd_dq_ds_kernel<KS, VT, TT>), dim3(grid), dim3(256), lds_dq, st, aq));
+    const int nbias = a.map_kq ? ceil_div(nbins, 16) : 0;  // the slab reduce rides along
+    GR_TIMED("attn_bwd_dq", st, hipLaunchKernelGGL((attn_bwd_dq_ds_kernel<KS, VT, TT>), dim3(grid + nbias), dim3(256),
+                                                   lds_dq, st, aq, grid, n_slabs, dpos_w, dts_w));
     GR_LAUNCH_CHECK("hstu_attn_bwd(dq from dS)");
+    return 0;
   } else if (!split && C::KT <= 8) {
     const size_t lds = lds_kv > lds_q ? lds_kv : lds_q;
     auto kern = a.map_kq ? attn_bwd_fused_kernel<KS, VT, TT, true> : attn_bwd_fused_kernel<KS, VT, TT, false>;

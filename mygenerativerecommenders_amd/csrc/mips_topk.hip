@@ -1130,11 +1130,12 @@ __global__ __launch_bounds__(1024) void mips_small_select_kernel(SmallArgs a) {
 // chunk (up to 128, fragments held in VGPRs) against each item block it loads, so the
 // table streams from HBM once and the MFMA pipe is the bound.  The per-query selection
 // state becomes one threshold tau_q, fixed before the pass:
-//   1. sample:  score every SR-th item block; each wave reduces its group of sample
-//      blocks to one max per query -> smax[q][g] (G groups).
-//   2. tau:     tau_q = the M_SAMPLE-th largest of the G group maxima.  Those maxima
-//      are real catalog items, so >= M_SAMPLE items score >= tau_q, and (1/SR
-//      sampled) about M_SAMPLE * SR do.
+//   1. sample:  score every SR-th item block; each workgroup reduces its group of
+//      sample blocks (a few per wave) to one max per query -> smax[q][g] (G groups =
+//      the sample workgroups; a group per wave made the tau kernel's selection 4x wider).
+//   2. tau:     tau_q = the M-th largest of the G group maxima (M = 1024 / SR).  Those
+//      maxima are real catalog items, so >= M items score >= tau_q, and (1/SR
+//      sampled) about M * SR = 1024 do.
 //   3. filter:  full pass; scores >= tau_q are appended (global atomics; ~1e-4 of
 //      scores) to a per-query list of FILTER_CAP.
 //   4. merge:   per query, drop invalid ids, exact top-k (threshold select + sort).  Every
@@ -1143,8 +1144,9 @@ __global__ __launch_bounds__(1024) void mips_small_select_kernel(SmallArgs a) {
 //      merge raises a device flag and the exact select + merge kernels above (gated on
 //      that flag, no host sync) recompute every query.
 constexpr int SAMPLE_STRIDE = 16;       // sample every 16th item block
-constexpr int SAMPLE_GROUPS = 4096;     // target number of group maxima per query
-constexpr int M_SAMPLE = 64;            // tau = 64th largest group max -> ~1024 candidates
+constexpr int SAMPLE_WAVES = 4096;      // target number of sample waves (4 per group)
+constexpr int M_SAMPLE = 64;            // M at the default stride (~1024 candidates)
+constexpr int SAMPLE_GB = 10;           // sample blocks per wave (when G stays >= 4 M)
 constexpr int FILTER_CAP = 4096;        // candidate list per query
 constexpr int NSUB = 16;                // ... split into sub-lists by workgroup (blockIdx % 16)
 constexpr int SUBCAP = FILTER_CAP / NSUB;  // so each counter sees 1/16 of the atomics
@@ -1159,7 +1161,7 @@ struct FilterArgs {
   int D, B;
   int64_t n_blocks;
   // sample pass
-  int GB, G;          // sample blocks per group, groups
+  int GB, G;          // sample blocks per wave, groups (= sample workgroups)
   int sr;             // sample stride (item blocks)
   float* smax;        // [B][G]
   // filter pass
@@ -1206,7 +1208,7 @@ __global__ __launch_bounds__(256) void mips_filter_kernel(FilterArgs a) {
   if (SAMPLE) {
     const int64_t n_sb = (a.n_blocks + a.sr - 1) / a.sr;
     const int64_t s0 = wv * a.GB, s1 = min(n_sb, s0 + a.GB);
-    if (wv < a.G) {
+    if (s0 < n_sb) {
       b0 = s0 * a.sr;
       b1 = s1 * a.sr;
     }
@@ -1472,14 +1474,20 @@ __global__ __launch_bounds__(256) void mips_filter_kernel(FilterArgs a) {
       }
     }
   }
-  if (SAMPLE && b0 < b1) {
+  if constexpr (SAMPLE) {  // the group max of each query: its 4 waves' maxima
+    __shared__ float smx[4][NQG * 16];
 #pragma unroll
     for (int g = 0; g < NQG; ++g) {
-      float m = thr[g];
+      float m = thr[g];  // -inf for a wave without sample blocks
       m = fmaxf(m, __shfl_xor(m, 16, 64));
       m = fmaxf(m, __shfl_xor(m, 32, 64));
-      const int qq = qb + 16 * g + lr;
-      if (lg == 0 && qq < a.B) a.smax[(int64_t)qq * a.G + wv] = m;
+      if (lg == 0) smx[wave_id()][16 * g + lr] = m;
+    }
+    __syncthreads();
+    for (int r = threadIdx.x; r < NQG * 16; r += 256) {
+      const int qq = qb + r;
+      if (qq < a.B)
+        a.smax[(int64_t)qq * a.G + bx] = fmaxf(fmaxf(smx[0][r], smx[1][r]), fmaxf(smx[2][r], smx[3][r]));
     }
   }
 }
@@ -1509,9 +1517,10 @@ struct TauArgs {
   int* flag;
   float* q_rows;           // bf16 filter: the queries padded to DP floats (for the rescoring)
   int DP;
+  int m;                   // tau~ = the m-th largest group maximum
 };
 
-// tau~ = M_SAMPLE-th largest group max (one workgroup per query).  f32 filter:
+// tau~ = m-th largest group max (one workgroup per query).  f32 filter:
 // tau = tau_e = tau~.  bf16 filter, with d = delta_q (1 + 2^-10):
 //   tau = tau~ - 2 d  (collect s~ >= tau),   tau_e = tau + d.
 // Any item with exact s >= tau_e has s~ >= s - delta_q >= tau, so it was collected;
@@ -1519,12 +1528,12 @@ struct TauArgs {
 // (The 2^-10 inflation covers the fp32 rounding of tau + d.)  Also resets the query's
 // candidate counters and (query 0) the fallback flag.
 __global__ __launch_bounds__(256) void mips_tau_kernel(TauArgs a) {
-  __shared__ uint32_t key[SAMPLE_GROUPS];
+  __shared__ uint32_t key[SAMPLE_WAVES / 4];
   __shared__ SelLDS L;
   const int q = blockIdx.x, tid = threadIdx.x;
   for (int e = tid; e < a.G; e += 256) key[e] = ord_key(a.smax[(int64_t)q * a.G + e]);
   __syncthreads();
-  const int m = a.G < M_SAMPLE ? a.G : M_SAMPLE;
+  const int m = a.G < a.m ? a.G : a.m;
   uint32_t kstar;
   int k_rem;
   block_kth(key, a.G, m, L, kstar, k_rem);
@@ -1592,6 +1601,10 @@ __global__ __launch_bounds__(256) void mips_filter_merge_kernel(FilterMergeArgs 
   __shared__ float cs[FILTER_CAP];
   __shared__ int ci[FILTER_CAP];
   const int q = blockIdx.x, tid = threadIdx.x;
+  // the invalid row's loads go out first, beside the counter loads (independent of them)
+  const int n0p = inv_pad(a.N0);
+  for (int j = tid; j < n0p; j += 256)
+    inv[j] = j < a.N0 ? a.invalid[(int64_t)q * a.N0 + j] : INT64_MAX;
   if (tid == 0) {
     int o = 0;
     bool over = false;
@@ -1641,9 +1654,6 @@ __global__ __launch_bounds__(256) void mips_filter_merge_kernel(FilterMergeArgs 
       }
     }
   }
-  const int n0p = inv_pad(a.N0);
-  for (int j = tid; j < n0p; j += 256)
-    inv[j] = j < a.N0 ? a.invalid[(int64_t)q * a.N0 + j] : INT64_MAX;
   __syncthreads();
   if (n0p > 256) block_bitonic_i64(inv, n0p);
   else if (n0p > 0) block_sort_i64_asc(inv, n0p);
@@ -1887,7 +1897,7 @@ struct TopkPlan {
   size_t part_bytes;   // legacy select partial lists (also the filter path's fallback)
   // filter path
   int64_t n_blocks, RB;
-  int GB, G, NQG, n_chunks, filter_waves, sr;
+  int GB, G, NQG, n_chunks, filter_waves, sr, m;
   int KC;              // > 0: the filter scores the bf16 copy (KC k-chunks of 32 dims)
   size_t off_tau, off_tau_e, off_qrows, off_cnt, off_smax, off_cs, off_ci, off_part, total_bytes;
   int n0p;             // inv_pad(N0)
@@ -1961,12 +1971,17 @@ static TopkPlan plan_topk(int B, int64_t X, int D, int k, int N0) {
   p.off_part = 0;
   if (p.filter) {
     p.n_blocks = (X + 15) / 16;
-    // (a 32-block stride at 10M items: sample 112 -> 84 us, but merge +9 us and filter
-    // +34 us from twice the candidates; no net gain, so one stride)
-    p.sr = SAMPLE_STRIDE;
+    // sample stride sr and rank m = 1024 / sr keep ~1024 candidates per query at any stride
+    // (a 32-block stride with m fixed at 64 doubled them: merge +9 us, filter +34 us)
+    p.sr = option(GR_OPT_MIPS_SAMPLE_STRIDE) > 0 ? (int)option(GR_OPT_MIPS_SAMPLE_STRIDE) : SAMPLE_STRIDE;
+    p.m = std::max(8, M_SAMPLE * SAMPLE_STRIDE / p.sr);
     const int64_t n_sb = (p.n_blocks + p.sr - 1) / p.sr;
-    p.GB = (int)((n_sb + SAMPLE_GROUPS - 1) / SAMPLE_GROUPS);
-    p.G = (int)((n_sb + p.GB - 1) / p.GB);
+    // ~SAMPLE_GB blocks per wave while the groups (4 waves each) stay >= 4 m, and at most
+    // SAMPLE_WAVES waves: fewer workgroups each staging the queries
+    int64_t gb = std::min<int64_t>(SAMPLE_GB, n_sb / (16 * (int64_t)p.m));
+    gb = std::max<int64_t>({gb, 1, (n_sb + SAMPLE_WAVES - 1) / SAMPLE_WAVES});
+    p.GB = (int)gb;
+    p.G = ceil_div((int)((n_sb + p.GB - 1) / p.GB), 4);  // sample workgroups
     p.NQG = B <= 32 ? 2 : (kc_bf > 2 ? 4 : 8);
     p.n_chunks = ceil_div(B, p.NQG * 16);
     // whole rounds of 2 four-wave workgroups per CU, >= ~48 blocks per wave
@@ -2016,7 +2031,7 @@ static TopkPlan plan_topk(int B, int64_t X, int D, int k, int N0) {
 template <int KS, int KC, int NQG>
 static int launch_filter_pair(const FilterArgs& f, const TopkPlan& p, bool sample, hipStream_t st) {
   if (sample) {
-    const dim3 g(ceil_div(p.G, 4), p.n_chunks);
+    const dim3 g(p.G, p.n_chunks);
     GR_TIMED("mips_sample", st, hipLaunchKernelGGL((mips_filter_kernel<KS, KC, NQG, true>), g, dim3(256), 0, st, f));
     GR_LAUNCH_CHECK("mips_topk(sample)");
   } else {
@@ -2203,7 +2218,7 @@ extern "C" int mips_topk(const float* queries, const float* packed_items, int64_
     int rc = launch_filter(f, p, true, st);
     if (rc) return rc;
     TauArgs ta{f.smax, p.G, queries, D, p.KC ? (const uint32_t*)(pbase + L.off_norm) : nullptr,
-               tau, tau_e, cnt, flag, p.KC ? (float*)(ws + p.off_qrows) : nullptr, L.DP};
+               tau, tau_e, cnt, flag, p.KC ? (float*)(ws + p.off_qrows) : nullptr, L.DP, p.m};
     GR_TIMED("mips_tau", st, hipLaunchKernelGGL(mips_tau_kernel, dim3(B), dim3(256), 0, st, ta));
     GR_LAUNCH_CHECK("mips_topk(tau)");
     rc = launch_filter(f, p, false, st);

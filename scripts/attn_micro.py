@@ -42,8 +42,9 @@ def main():
     ap.add_argument("--split", action="store_true", help="f32 backward as separate dK/dV, dQ launches")
     ap.add_argument("--nopairs", action="store_true", help="f32 backward: one tile per workgroup")
     ap.add_argument("--pairs", type=int, default=1, help="GR_OPT_ATTN_BWD_PAIRS (0/1/2)")
-    ap.add_argument("--ds", type=int, default=0, nargs="?", const=1,
-                    help="f32 backward dS forms: 1 = two launches, 2 = in-launch hand-off")
+    ap.add_argument("--ds", type=int, default=None, nargs="?", const=1,
+                    help="f32 backward dS forms: 0 = recompute, 1 = two launches (library "
+                         "default), 2 = in-launch hand-off")
     ap.add_argument("--hepi", action="store_true",
                     help="fused silu'(h) epilogue on dQ/dK/dV (as in the training step)")
     ap.add_argument("--opt", action="append", default=[], help="launch option NAME=VALUE")
@@ -79,7 +80,8 @@ def main():
     L_ = _lib.lib()
     _lib.set_option("ATTN_BWD_SPLIT", int(args.split))
     _lib.set_option("ATTN_BWD_PAIRS", 0 if args.nopairs else args.pairs)
-    _lib.set_option("ATTN_BWD_DS", int(args.ds))  # before the workspace size query
+    if args.ds is not None:
+        _lib.set_option("ATTN_BWD_DS", int(args.ds))  # before the workspace size query
     ws_n = (L_.hstu_attn_bwd_bf16_workspace_size(B, N, L, H, d, d, 128) if args.bf16
             else L_.hstu_attn_bwd_workspace_size_d(B, N, L, H, d, d, 128))
     ws = torch.empty(max(ws_n, 4), dtype=torch.uint8, device=dev)
@@ -131,9 +133,11 @@ def main():
     for name, (tot, n) in kt.items():
         if not n:
             continue
-        avg = tot / n
-        res[name] = {"avg_us": round(avg * 1e3, 2),
-                     "tflops": round(fl.get(name, 0) / (avg * 1e-3) / 1e12, 2) if name in fl else None}
+        # per call of the op (a form may issue several launches under one name: the
+        # wide-head dV / dK launches are both "attn_bwd_dkv")
+        per_call = tot / args.iters
+        res[name] = {"us_per_call": round(per_call * 1e3, 2), "launches_per_call": n / args.iters,
+                     "tflops": round(fl.get(name, 0) / (per_call * 1e-3) / 1e12, 2) if name in fl else None}
     print(json.dumps({"shape": args.shape, "bf16": args.bf16, "B": B, "N": N, "L": L, "d": d, "H": H,
                       "kernels": res}))
 

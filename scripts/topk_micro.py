@@ -52,7 +52,7 @@ print(f"X={a.items} D={a.dim} B={a.batch}: {dt*1e3:.3f} ms/batch  {a.batch*a.ite
       f"  fallback={int(ws[:4].view(torch.int32).item())}")
 if a.items >= 262144 and a.dim <= 64:  # filter path: candidate counts (workspace layout)
     al = lambda v: (v + 255) // 256 * 256  # noqa: E731  (flag | tau | tau_e | q rows | cnt)
-    off_cnt = al(al(al(256 + 4 * a.batch) + 4 * a.batch) + 256 * a.batch)
+    off_cnt = al(al(al(256 + 4 * a.batch) + 4 * a.batch) + 16 * a.batch * ((a.dim + 3) // 4))
     cnt = ws[off_cnt:off_cnt + 4 * 16 * a.batch].view(torch.int32).view(a.batch, 16).sum(1).float()
     print(f"  candidates/query: mean {cnt.mean().item():.0f} min {cnt.min().item():.0f} "
           f"max {cnt.max().item():.0f}")

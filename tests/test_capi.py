@@ -74,10 +74,10 @@ def test_call_rejects_wrong_argument_count():
 def test_workspace_size_queries_are_host_only():
     L = _lib.lib()
     slabs = 4 * 128 * 4 * (2 * 211 - 1 + 129)
-    assert L.hstu_attn_bwd_workspace_size(128, 211, 200, 1, 128) == slabs
-    ds = 4 * 256 * 14 * 15 // 2 * 128  # dS tiles of the two-pass backward (N <= 512)
-    with _lib.option("ATTN_BWD_DS", 1):
-        assert L.hstu_attn_bwd_workspace_size(128, 211, 200, 1, 128) == (slabs + 255) // 256 * 256 + ds
+    ds = 4 * 256 * 14 * 15 // 2 * 128  # dS tiles of the two-pass backward (N <= 512, default)
+    assert L.hstu_attn_bwd_workspace_size(128, 211, 200, 1, 128) == (slabs + 255) // 256 * 256 + ds
+    with _lib.option("ATTN_BWD_DS", 0):
+        assert L.hstu_attn_bwd_workspace_size(128, 211, 200, 1, 128) == slabs
     slabs3 = 4 * 32 * 32 * (2 * 2059 - 1 + 129)
     assert L.hstu_attn_bwd_workspace_size(32, 2059, 2048, 1, 128) == slabs3  # no dS above 512
     # head dims given: narrow heads as above; wide heads (d > 128) add the dS tiles at any N
@@ -117,9 +117,10 @@ def test_launch_options_are_explicit_not_environment():
     assert set(opts) == {"MIPS_FILTER_FP32", "MIPS_FILTER_WGS", "MIPS_FILTER_ROUNDS",
                          "MIPS_FORCE_FALLBACK", "ATTN_BWD_SPLIT", "ROWWAVE", "ATTN_BWD_PAIRS",
                          "ATTN_BWD_DS", "DETERMINISTIC", "WGRAD_ROWS", "PANEL_VEC",
-                         "ATTN_BWD_WIDE_DS", "ATTN_BWD_WIDE_SPLIT", "MIPS_FILTER_PAIRED"}
-    defaults = {"MIPS_FILTER_WGS": 2, "ROWWAVE": 1, "ATTN_BWD_PAIRS": 1, "PANEL_VEC": 1,
-                "ATTN_BWD_WIDE_DS": 1, "ATTN_BWD_WIDE_SPLIT": 2, "MIPS_FILTER_PAIRED": 1}
+                         "ATTN_BWD_WIDE_DS", "ATTN_BWD_WIDE_SPLIT", "MIPS_FILTER_PAIRED",
+                         "MIPS_SAMPLE_STRIDE"}
+    defaults = {"MIPS_FILTER_WGS": 2, "ROWWAVE": 1, "ATTN_BWD_PAIRS": 1, "PANEL_VEC": 1, "ATTN_BWD_DS": 1,
+                "ATTN_BWD_WIDE_DS": 1, "ATTN_BWD_WIDE_SPLIT": 0, "MIPS_FILTER_PAIRED": 1}
     for n in opts:
         assert _lib.get_option(n) == defaults.get(n, 0), n
     with _lib.option("ATTN_BWD_SPLIT", 1):

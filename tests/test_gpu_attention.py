@@ -254,8 +254,9 @@ def test_attn_bwd_launch_modes_bitexact(B, N, d):
     g = torch.Generator().manual_seed(3)
     dout = torch.randn(uvqk.shape[0], d, generator=g)
     hpre = torch.randn(uvqk.shape, generator=g)
-    modes = [{}, {"ATTN_BWD_PAIRS": 2}, {"ATTN_BWD_PAIRS": 0}, {"ATTN_BWD_SPLIT": 1},
-             {"ATTN_BWD_DS": 1}, {"ATTN_BWD_DS": 1, "ATTN_BWD_PAIRS": 2},
+    modes = [{}, {"ATTN_BWD_DS": 0}, {"ATTN_BWD_DS": 0, "ATTN_BWD_PAIRS": 2},
+             {"ATTN_BWD_DS": 0, "ATTN_BWD_PAIRS": 0}, {"ATTN_BWD_DS": 0, "ATTN_BWD_SPLIT": 1},
+             {"ATTN_BWD_DS": 1, "ATTN_BWD_PAIRS": 2},
              {"ATTN_BWD_DS": 2}, {"ATTN_BWD_DS": 2, "ATTN_BWD_PAIRS": 2}]
     outs = []
     for m in modes:
@@ -281,8 +282,8 @@ def test_attn_bwd_launch_modes_bitexact(B, N, d):
 def test_attn_bwd_wide_stored_ds_bitexact(B, N, dqk, dv, with_ts):
     """Wide heads (d > 128): dQ from the dS tiles the dK/dV pass stores
     (GR_OPT_ATTN_BWD_WIDE_DS, default) against the recomputing dQ pass (option 0), and
-    the dK/dV forms (GR_OPT_ATTN_BWD_WIDE_SPLIT: dV and dK as two launches, the default;
-    as workgroups of one launch; one workgroup for both): every gradient bit-identical (the
+    the dK/dV forms (GR_OPT_ATTN_BWD_WIDE_SPLIT: one workgroup for both, the default; dV
+    and dK as workgroups of one launch; as two launches): every gradient bit-identical (the
     same S, dS values, summed in the same order), with and without a bucket map, silu'(h)
     epilogue on."""
     from mygenerativerecommenders_amd import _lib
@@ -294,7 +295,7 @@ def test_attn_bwd_wide_stored_ds_bitexact(B, N, dqk, dv, with_ts):
     others = []
     with _lib.option("ATTN_BWD_WIDE_DS", 0):  # recomputing dQ pass (combined dK/dV)
         others.append(_run_gpu_bwd(offsets, uvqk, dout, ts, pos_w, ts_w, B, N, 1, dqk, dv, hpre=hpre))
-    for sp in (0, 1):  # dK/dV in one workgroup; dV and dK workgroups in one launch
+    for sp in (1, 2):  # dV and dK workgroups in one launch; dV and dK launches
         with _lib.option("ATTN_BWD_WIDE_SPLIT", sp):
             others.append(_run_gpu_bwd(offsets, uvqk, dout, ts, pos_w, ts_w, B, N, 1, dqk, dv,
                                        hpre=hpre))
