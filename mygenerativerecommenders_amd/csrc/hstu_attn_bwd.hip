@@ -521,12 +521,12 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const AttnBwdArgs& a, const in
     if (bin >= 0 && bin < npos) whist[bin] += carry;
   }
   carry = 0.f;
-  // the workgroup's bias slab is written before its dK / dV rows: its barrier then waits
-  // for no stores of this workgroup (a barrier after them drained every one)
+  // the workgroup's bias slab is written before its dK / dV rows, behind an LDS-only
+  // barrier (a __syncthreads() also drained the dS tile stores still in flight)
   if (pass == 1 || !(TT == 64 && kt_b >= 0 && kt_b * 64 < L)) {
     if (has_bias && run_b >= 0) atomicAdd(&wts[run_b], run_s);  // the open dts run
     if (has_bias && slab) {
-      __syncthreads();
+      lds_barrier();
       for (int i = tid; i < npos; i += 256)
         slab[i] = ((hist[i] + hist[wbins + i]) + hist[2 * wbins + i]) + hist[3 * wbins + i];
       for (int i = tid; i <= a.nb; i += 256) {
@@ -994,19 +994,84 @@ __global__ __launch_bounds__(256) void attn_bwd_dk_kernel(AttnBwdArgs a) {
 }
 __device__ __forceinline__ void bias_grad_reduce_body(const float* slabs, int n_slabs, int n_pos,
                                                       int n_ts, float* dpos_w, float* dts_w, int blk);
-// dQ = dS K; workgroups past grid_dq reduce the bias slabs the dK/dV launch wrote (no
-// launch of its own: they fill the CUs the light query tiles free)
+// dQ = dS K at narrow heads, one wave per 16-query block (no LDS tile, no workgroup
+// barrier): the lane's K elements (key row 4g + r of a block, column 16 t + lr) come from
+// L2 through the range-checked sequence descriptor, PD key blocks in flight.  Blocks past
+// the last one of the walk re-read it with a zero A operand (+0 to every sum), so the
+// loads stay unconditional.  The MFMA sequence (key blocks ascending, k-step r = keys
+// 4g + r) is the recomputing pass's: dQ is bit-identical to it.
+template <int KSTEPS, int VTILES>
+__device__ __forceinline__ void attn_bwd_dq_wave_body(const AttnBwdArgs& a, const int item) {
+  using C = AttnBwdCfg<KSTEPS, VTILES, 64>;
+  constexpr int KT = C::KT, PD = 4;
+  const int BH = a.B * a.H;
+  const int qb = a.n_tiles * 4 - 1 - item / BH;  // heaviest blocks first
+  const int bh = item % BH;
+  if (qb < 0) return;
+  const int b = bh / a.H, h = bh % a.H;
+  const int64_t s0 = a.offsets[b];
+  const int L = (int)(a.offsets[b + 1] - s0);
+  const int q0 = qb * 16;
+  if (q0 >= L) return;
+  const int lane = threadIdx.x & 63, lr = lane & 15, lg = lane >> 4;
+  const __amdgpu_buffer_rsrc_t rk = seq_rsrc(a.k, a.ld_qk, s0, h * a.dqk, L, a.dqk);
+  const float* dsq = a.ds + ((int64_t)bh * a.ds_tps + qb * (qb + 1) / 2) * 256 + lr * 16 + 4 * lg;
+  const int rowb = (int)a.ld_qk * 4;  // bytes per K row
+  int voff[KT];
+#pragma unroll
+  for (int t = 0; t < KT; ++t) {
+    const int c = 16 * t + lr;
+    voff[t] = c < a.dqk ? (4 * lg * (int)a.ld_qk + c) * 4 : 0x40000000;
+  }
+  f4 dQ[KT];
+#pragma unroll
+  for (int t = 0; t < KT; ++t) dQ[t] = f4_zero();
+  f4 dsr[PD];
+  float kr[PD][4][KT];
+  auto load = [&](int u, int kb) {
+    const int kc = kb < qb ? kb : qb;
+    dsr[u] = *as_global(reinterpret_cast<const f4*>(dsq + kc * 256));
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int t = 0; t < KT; ++t) kr[u][r][t] = buf_ld(rk, voff[t], (kc * 16 + r) * rowb);
+  };
+#pragma unroll
+  for (int u = 0; u < PD; ++u) load(u, u);
+  for (int kb0 = 0; kb0 <= qb; kb0 += PD) {
+#pragma unroll
+    for (int u = 0; u < PD; ++u) {
+      const bool live = kb0 + u <= qb;  // wave-uniform; a re-read block adds +0
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float av = live ? dsr[u][r] : 0.f;
+#pragma unroll
+        for (int t = 0; t < KT; ++t) dQ[t] = mfma16x16x4(av, kr[u][r][t], dQ[t]);
+      }
+      load(u, kb0 + PD + u);
+    }
+  }
+  store_scaled<4, KT>([&](int i, int t) { return dQ[t][i]; }, L, a.dqk, s0, a.dq, a.ld_d, a.hq,
+                      a.ld_h, h * a.dqk, [&](int i) { return q0 + 4 * lg + i; },
+                      [&](int t) { return 16 * t + lr; });
+}
+
+// dQ = dS K; the first n_bias workgroups reduce the bias slabs the dK/dV launch wrote (no
+// launch of their own: they run beside the dQ workgroups).  TT = 64: four query blocks
+// per workgroup, one per wave (attn_bwd_dq_wave_body).
 template <int KSTEPS, int VTILES, int TT>
-__global__ __launch_bounds__(256) void attn_bwd_dq_ds_kernel(AttnBwdArgs a, int grid_dq, int n_slabs,
+__global__ __launch_bounds__(256) void attn_bwd_dq_ds_kernel(AttnBwdArgs a, int n_bias, int n_slabs,
                                                              float* dpos_w, float* dts_w) {
-  if ((int)blockIdx.x >= grid_dq) {
-    bias_grad_reduce_body(a.slabs, n_slabs, 2 * a.N - 1, a.nb + 1, dpos_w, dts_w,
-                          (int)blockIdx.x - grid_dq);
+  const int id = (int)blockIdx.x - n_bias;
+  if (id < 0) {
+    bias_grad_reduce_body(a.slabs, n_slabs, 2 * a.N - 1, a.nb + 1, dpos_w, dts_w, (int)blockIdx.x);
     return;
   }
-  if constexpr (TT == 64 || TT == 16) {
-    if (BWD_V2(a)) attn_bwd_dq_ds_body<KSTEPS, VTILES, TT, true>(a, blockIdx.x);
-    else attn_bwd_dq_ds_body<KSTEPS, VTILES, TT, false>(a, blockIdx.x);
+  if constexpr (TT == 64) {
+    attn_bwd_dq_wave_body<KSTEPS, VTILES>(a, id * 4 + wave_id());
+  } else if constexpr (TT == 16) {
+    if (BWD_V2(a)) attn_bwd_dq_ds_body<KSTEPS, VTILES, TT, true>(a, id);
+    else attn_bwd_dq_ds_body<KSTEPS, VTILES, TT, false>(a, id);
   }
 }
 // One launch, dS handed over inside it: workgroups [0, grid_kv) are the key-major pass
@@ -1187,10 +1252,12 @@ static int launch_bwd(const AttnBwdArgs& a, float* dpos_w, float* dts_w, hipStre
     }
     GR_LAUNCH_CHECK("hstu_attn_bwd(dkv)");
     aq.paired = 0;
-    const size_t lds_dq = sizeof(float) * TT * C::LDQ + 16;
+    // narrow heads: one wave per 16-query block, no LDS
+    const size_t lds_dq = TT == 64 ? 0 : sizeof(float) * TT * C::LDQ + 16;
+    const int grid_dq = grid;  // TT = 64: 4 query blocks per workgroup (one 64-row tile)
     const int nbias = a.map_kq ? ceil_div(nbins, 16) : 0;  // the slab reduce rides along
-    GR_TIMED("attn_bwd_dq", st, hipLaunchKernelGGL((attn_bwd_dq_ds_kernel<KS, VT, TT>), dim3(grid + nbias), dim3(256),
-                                                   lds_dq, st, aq, grid, n_slabs, dpos_w, dts_w));
+    GR_TIMED("attn_bwd_dq", st, hipLaunchKernelGGL((attn_bwd_dq_ds_kernel<KS, VT, TT>), dim3(grid_dq + nbias), dim3(256),
+                                                   lds_dq, st, aq, nbias, n_slabs, dpos_w, dts_w));
     GR_LAUNCH_CHECK("hstu_attn_bwd(dq from dS)");
     return 0;
   } else if (!split && C::KT <= 8) {

@@ -1143,14 +1143,15 @@ __global__ __launch_bounds__(1024) void mips_small_select_kernel(SmallArgs a) {
 //      whenever the list did not overflow and kept >= k valid items.  Otherwise the
 //      merge raises a device flag and the exact select + merge kernels above (gated on
 //      that flag, no host sync) recompute every query.
-constexpr int SAMPLE_STRIDE = 16;       // sample every 16th item block
+constexpr int SAMPLE_STRIDE = 32;       // sample every 32nd item block (10M items: sample
+                                        // 26.0 us at 16, 14.0 at 32, 10.7 at 64 but merge +4.5)
 constexpr int SAMPLE_WAVES = 4096;      // target number of sample waves (4 per group)
-constexpr int M_SAMPLE = 64;            // M at the default stride (~1024 candidates)
+constexpr int SAMPLE_CAND = 1024;       // M = SAMPLE_CAND / stride: ~1024 candidates per query
 constexpr int SAMPLE_GB = 10;           // sample blocks per wave (when G stays >= 4 M)
 constexpr int FILTER_CAP = 4096;        // candidate list per query
 constexpr int NSUB = 16;                // ... split into sub-lists by workgroup (blockIdx % 16)
 constexpr int SUBCAP = FILTER_CAP / NSUB;  // so each counter sees 1/16 of the atomics
-constexpr int64_t FILTER_MIN_X = (int64_t)SAMPLE_STRIDE * 16 * 1024;  // >= 1024 sample blocks
+constexpr int64_t FILTER_MIN_X = (int64_t)16 * 16 * 1024;  // >= 1024 blocks at a 16-block stride
 
 struct FilterArgs {
   const float* q;
@@ -1230,24 +1231,44 @@ __global__ __launch_bounds__(256) void mips_filter_kernel(FilterArgs a) {
   // so each wave's reads are conflict-free: frag[(g KS + st) 64 + lr + 16 lg] =
   // Q[qb + 16 g + lr][4 st + lg].
   // (bf16: frag16[(g KC + c) 64 + lr + 16 lg] = bf16(Q[qb + 16 g + lr][32 c + 8 lg + 0..7]))
+  // Wide bf16 rows (KC > 2) with 8 query groups: groups 0..3 live in VGPRs, 4..7 are read
+  // from LDS per block (all 128 queries of a batch in one pass over the table; 8 groups in
+  // VGPRs would not fit beside the block prefetch)
+  constexpr int NQR = (BF && NQG == 8 && KC > 2) ? (SAMPLE ? 2 : 3) : NQG;  // query groups in VGPRs
+  constexpr int NQL = NQG - NQR;                             // query groups read from LDS
+  constexpr int NQS = NQR > NQL ? NQR : NQL;                 // groups staged at a time
   __shared__ float q_lds[BF ? 1 : NQG * KS * 64];
-  __shared__ u32x4 q16_lds[BF ? NQG * KC * 64 : 1];
+  __shared__ u32x4 q16_lds[BF ? NQS * KC * 64 : 1];
   __shared__ float tau_lds[NQG * 16];
+  u32x4 qreg16[NQR][BF ? KC : 1];
+  float qreg[NQG][BF ? 1 : KS];
   {
     const int rows = NQG * 16;
     if constexpr (BF) {
-      for (int e = threadIdx.x; e < rows * KC * 4; e += 256) {
-        const int r = e / (KC * 4), u = e - r * (KC * 4);
-        const int qq = qb + r, d0 = 32 * (u >> 2) + 8 * (u & 3);
-        uint32_t w[4];
+      auto stage = [&](int g0, int ng) {
+        for (int e = threadIdx.x; e < ng * 16 * KC * 4; e += 256) {
+          const int r = e / (KC * 4), u = e - r * (KC * 4);
+          const int qq = qb + 16 * g0 + r, d0 = 32 * (u >> 2) + 8 * (u & 3);
+          uint32_t w[4];
 #pragma unroll
-        for (int h = 0; h < 4; ++h) {
-          const int d = d0 + 2 * h;
-          const float v0 = (qq < a.B && d < a.D) ? a.q[(int64_t)qq * a.D + d] : 0.f;
-          const float v1 = (qq < a.B && d + 1 < a.D) ? a.q[(int64_t)qq * a.D + d + 1] : 0.f;
-          w[h] = bf16_bits(v0) | (bf16_bits(v1) << 16);
+          for (int h = 0; h < 4; ++h) {
+            const int d = d0 + 2 * h;
+            const float v0 = (qq < a.B && d < a.D) ? a.q[(int64_t)qq * a.D + d] : 0.f;
+            const float v1 = (qq < a.B && d + 1 < a.D) ? a.q[(int64_t)qq * a.D + d + 1] : 0.f;
+            w[h] = bf16_bits(v0) | (bf16_bits(v1) << 16);
+          }
+          q16_lds[((r >> 4) * KC + (u >> 2)) * 64 + (r & 15) + 16 * (u & 3)] = u32x4{w[0], w[1], w[2], w[3]};
         }
-        q16_lds[((r >> 4) * KC + (u >> 2)) * 64 + (r & 15) + 16 * (u & 3)] = u32x4{w[0], w[1], w[2], w[3]};
+      };
+      stage(0, NQR);
+      __syncthreads();
+#pragma unroll
+      for (int g = 0; g < NQR; ++g)
+#pragma unroll
+        for (int c = 0; c < KC; ++c) qreg16[g][c] = q16_lds[(g * KC + c) * 64 + lane];
+      if constexpr (NQL > 0) {
+        __syncthreads();
+        stage(NQR, NQL);
       }
     } else {
       const int cols = 4 * KS;
@@ -1264,17 +1285,11 @@ __global__ __launch_bounds__(256) void mips_filter_kernel(FilterArgs a) {
     }
     __syncthreads();
   }
-  float qreg[NQG][BF ? 1 : KS];
-  u32x4 qreg16[NQG][BF ? KC : 1];
+  if constexpr (!BF) {
 #pragma unroll
-  for (int g = 0; g < NQG; ++g) {
-    if constexpr (BF) {
-#pragma unroll
-      for (int c = 0; c < KC; ++c) qreg16[g][c] = q16_lds[(g * KC + c) * 64 + lane];
-    } else {
+    for (int g = 0; g < NQG; ++g)
 #pragma unroll
       for (int st = 0; st < KS; ++st) qreg[g][st] = q_lds[(g * KS + st) * 64 + lane];
-    }
   }
   float thr[NQG];  // filter: tau of query 16 g + lr (+inf for padded queries); sample: running max
 #pragma unroll
@@ -1315,11 +1330,29 @@ __global__ __launch_bounds__(256) void mips_filter_kernel(FilterArgs a) {
     f4 s[NQG];
 #pragma unroll
     for (int g = 0; g < NQG; ++g) s[g] = f4_zero();
-    if constexpr (BF) {
+    if constexpr (BF && NQL == 0) {
 #pragma unroll
       for (int c = 0; c < KC; ++c)
 #pragma unroll
         for (int g = 0; g < NQG; ++g) s[g] = mfma16x16x32bf16(f.h[c], qreg16[g][c], s[g]);
+    } else if constexpr (BF) {
+      // the LDS groups' fragments of chunk c + 1 are read while chunk c's MFMAs run (a
+      // barrier per chunk keeps hipcc from hoisting every chunk's reads: 4x the registers)
+      u32x4 ql[2][NQL > 0 ? NQL : 1];
+#pragma unroll
+      for (int g = 0; g < NQL; ++g) ql[0][g] = q16_lds[(g * KC) * 64 + lane];
+#pragma unroll
+      for (int c = 0; c < KC; ++c) {
+        if (c + 1 < KC) {
+#pragma unroll
+          for (int g = 0; g < NQL; ++g) ql[(c + 1) & 1][g] = q16_lds[(g * KC + c + 1) * 64 + lane];
+        }
+#pragma unroll
+        for (int g = 0; g < NQR; ++g) s[g] = mfma16x16x32bf16(f.h[c], qreg16[g][c], s[g]);
+#pragma unroll
+        for (int g = 0; g < NQL; ++g) s[NQR + g] = mfma16x16x32bf16(f.h[c], ql[c & 1][g], s[NQR + g]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
     } else {
 #pragma unroll
       for (int st = 0; st < KS; ++st) {
@@ -1524,7 +1557,7 @@ struct TauArgs {
 // tau = tau_e = tau~.  bf16 filter, with d = delta_q (1 + 2^-10):
 //   tau = tau~ - 2 d  (collect s~ >= tau),   tau_e = tau + d.
 // Any item with exact s >= tau_e has s~ >= s - delta_q >= tau, so it was collected;
-// the M_SAMPLE sampled maxima (s~ >= tau~) all have s >= tau~ - delta_q >= tau_e.
+// the m sampled maxima (s~ >= tau~) all have s >= tau~ - delta_q >= tau_e.
 // (The 2^-10 inflation covers the fp32 rounding of tau + d.)  Also resets the query's
 // candidate counters and (query 0) the fallback flag.
 __global__ __launch_bounds__(256) void mips_tau_kernel(TauArgs a) {
@@ -1974,7 +2007,7 @@ static TopkPlan plan_topk(int B, int64_t X, int D, int k, int N0) {
     // sample stride sr and rank m = 1024 / sr keep ~1024 candidates per query at any stride
     // (a 32-block stride with m fixed at 64 doubled them: merge +9 us, filter +34 us)
     p.sr = option(GR_OPT_MIPS_SAMPLE_STRIDE) > 0 ? (int)option(GR_OPT_MIPS_SAMPLE_STRIDE) : SAMPLE_STRIDE;
-    p.m = std::max(8, M_SAMPLE * SAMPLE_STRIDE / p.sr);
+    p.m = std::max(8, SAMPLE_CAND / p.sr);
     const int64_t n_sb = (p.n_blocks + p.sr - 1) / p.sr;
     // ~SAMPLE_GB blocks per wave while the groups (4 waves each) stay >= 4 m, and at most
     // SAMPLE_WAVES waves: fewer workgroups each staging the queries
@@ -1982,7 +2015,7 @@ static TopkPlan plan_topk(int B, int64_t X, int D, int k, int N0) {
     gb = std::max<int64_t>({gb, 1, (n_sb + SAMPLE_WAVES - 1) / SAMPLE_WAVES});
     p.GB = (int)gb;
     p.G = ceil_div((int)((n_sb + p.GB - 1) / p.GB), 4);  // sample workgroups
-    p.NQG = B <= 32 ? 2 : (kc_bf > 2 ? 4 : 8);
+    p.NQG = B <= 32 ? 2 : 8;  // KC > 2: 4 groups in VGPRs, 4 read from LDS
     p.n_chunks = ceil_div(B, p.NQG * 16);
     // whole rounds of 2 four-wave workgroups per CU, >= ~48 blocks per wave
     const int64_t per_round = (int64_t)device_cus() * 4 * option(GR_OPT_MIPS_FILTER_WGS);
@@ -2051,12 +2084,8 @@ static int launch_filter_pair(const FilterArgs& f, const TopkPlan& p, bool sampl
 
 template <int KS, int KC>
 static int launch_filter_ks(const FilterArgs& f, const TopkPlan& p, bool sample, hipStream_t st) {
-  if constexpr (KC > 2)  // D > 64: 2 or 4 query tiles per workgroup (register budget)
-    return p.NQG == 2 ? launch_filter_pair<KS, KC, 2>(f, p, sample, st)
-                      : launch_filter_pair<KS, KC, 4>(f, p, sample, st);
-  else
-    return p.NQG == 2 ? launch_filter_pair<KS, KC, 2>(f, p, sample, st)
-                      : launch_filter_pair<KS, KC, 8>(f, p, sample, st);
+  return p.NQG == 2 ? launch_filter_pair<KS, KC, 2>(f, p, sample, st)
+                    : launch_filter_pair<KS, KC, 8>(f, p, sample, st);
 }
 
 static int launch_filter(const FilterArgs& f, const TopkPlan& p, bool sample, hipStream_t st) {
