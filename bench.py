@@ -823,9 +823,15 @@ def main():
                        and not _lib.get_option("MIPS_FILTER_FP32"))
         if bf16_filter:
             # bound used: HBM, on the bf16 payload of the table (X x D x 2 B) that the
-            # filter streams once; the stored copy pads D to 32-dim chunks (padded_bytes)
+            # filter streams once; padded_bytes = the stored copy (mips_topk.hip
+            # bf16_block_bytes: 32-dim chunks, the last one trimmed to whole 8-dim lane
+            # groups, or to a 1-2 dim tail: 1,600 B per 16 items at D = 50)
+            kc = (D + 31) // 32
+            rem = D - 32 * (kc - 1)
+            tail = kc <= 2 and rem > 8 and rem % 8 in (1, 2)
+            blk = 1024 * (kc - 1) + 256 * (rem // 8 if tail else (rem + 7) // 8) + (64 if tail else 0)
             alg_bytes = float(xs * D * 2)
-            pad_bytes = float((xs + 15) // 16 * ((D + 31) // 32) * 1024)
+            pad_bytes = float((xs + 15) // 16 * blk)
             ach_r = alg_bytes / (ktop * 1e-3) / 1e9 if ktop else 0.0
             # SURVEY §8d's bound for this workload (fp32 compute, 2BXD flop at 157.3 TF/s
             # vs 4XD bytes at 8 TB/s): the ms per batch it allows, beside ours

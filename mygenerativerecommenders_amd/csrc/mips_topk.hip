@@ -123,29 +123,52 @@ __device__ __forceinline__ f4 mfma16x16x32bf16(u32x4 a, u32x4 b, f4 c) {
 // lane groups (dims past D would be zero): a block is BB = 1024 (KC-1) + 256 LG bytes
 // (D = 50: 1,792 B instead of 2,048), word (ib, c, l) at byte ib BB + 1024 c + 16 l.  The
 // filter's lanes of the unstored groups re-read group 0's word (same address: no extra
-// bytes) against zero query dims.  The largest item L2 norm (fp32 bits, for the filter's
-// error bound) follows the copy.
-__host__ __device__ inline int bf16_last_groups(int D, int KC) { return (D - 32 * (KC - 1) + 7) / 8; }
+// bytes) against zero query dims.  When the last chunk ends 1 or 2 dims past a whole lane
+// group (D = 50: dims 48, 49), that group is a 64-byte tail after the chunks instead (one
+// u32 of <= 2 bf16 per item): its lanes build their A operand {tail, 0, 0, 0} -- the same
+// operand the full word held, so the scores are unchanged -- and D = 50 stores 1,600 B
+// per block instead of 1,792.  The largest item L2 norm (fp32 bits, for
+// the filter's error bound) follows the copy.
+__host__ __device__ inline int bf16_tail_dims(int D, int KC) {  // (KC <= 2 only)
+  const int rem = D - 32 * (KC - 1), t = rem % 8;
+  return KC <= 2 && rem > 8 && (t == 1 || t == 2) ? t : 0;
+}
+__host__ __device__ inline int bf16_last_groups(int D, int KC) {
+  return bf16_tail_dims(D, KC) ? (D - 32 * (KC - 1)) / 8 : (D - 32 * (KC - 1) + 7) / 8;
+}
 __host__ __device__ inline int bf16_block_bytes(int D, int KC) {
-  return 1024 * (KC - 1) + 256 * bf16_last_groups(D, KC);
+  return 1024 * (KC - 1) + 256 * bf16_last_groups(D, KC) + (bf16_tail_dims(D, KC) ? 64 : 0);
 }
 __global__ void pack_bf16_kernel(const float* items, int64_t X, int D, int KC, u32x4* packed16) {
   const int words = bf16_block_bytes(D, KC) / 16;  // 16-byte words per block
+  const int chunk_words = 64 * (KC - 1) + 16 * bf16_last_groups(D, KC);
+  const int dt = D - bf16_tail_dims(D, KC);  // first tail dim (D without a tail)
+  // (tail word j: items 4j .. 4j + 3)
   const int64_t total = (X + 15) / 16 * words;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * blockDim.x) {
     const int64_t ib = e / words;
     const int u = (int)(e - ib * words);
-    const int c = u >> 6, l = u & 63;
-    const int64_t i = ib * 16 + (l & 15);
-    const int d0 = 32 * c + 8 * (l >> 4);
     uint32_t w[4];
+    if (u < chunk_words) {
+      const int c = u >> 6, l = u & 63;
+      const int64_t i = ib * 16 + (l & 15);
+      const int d0 = 32 * c + 8 * (l >> 4);
 #pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      const int d = d0 + 2 * h;
-      const float v0 = (i < X && d < D) ? items[i * D + d] : 0.f;
-      const float v1 = (i < X && d + 1 < D) ? items[i * D + d + 1] : 0.f;
-      w[h] = bf16_bits(v0) | (bf16_bits(v1) << 16);
+      for (int h = 0; h < 4; ++h) {
+        const int d = d0 + 2 * h;
+        const float v0 = (i < X && d < dt) ? items[i * D + d] : 0.f;
+        const float v1 = (i < X && d + 1 < dt) ? items[i * D + d + 1] : 0.f;
+        w[h] = bf16_bits(v0) | (bf16_bits(v1) << 16);
+      }
+    } else {  // tail word j = u - chunk_words: items 4j .. 4j + 3, dims dt, dt + 1
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        const int64_t i = ib * 16 + 4 * (u - chunk_words) + h;
+        const float v0 = (i < X && dt < D) ? items[i * D + dt] : 0.f;
+        const float v1 = (i < X && dt + 1 < D) ? items[i * D + dt + 1] : 0.f;
+        w[h] = bf16_bits(v0) | (bf16_bits(v1) << 16);
+      }
     }
     packed16[e] = u32x4{w[0], w[1], w[2], w[3]};
   }
@@ -1158,6 +1181,7 @@ struct FilterArgs {
   const float* packed;
   const u32x4* packed16;  // bf16 copy (KC > 0 instantiations)
   int BB, LG;             // its block bytes and stored lane groups of the last chunk
+  int TD;                 // tail dims (0, 1, 2): lane group LG of the last chunk reads the tail
   int64_t X;
   int D, B;
   int64_t n_blocks;
@@ -1190,7 +1214,8 @@ constexpr int WV_CAP = WG_CAP / 4;  // per-wave segment
 // KC == 0: f32 table (KS k-steps of 16x16x4); KC > 0: the bf16 copy (KC k-chunks of
 // 16x16x32), scores approximate to within the bound the tau kernel folds into tau.
 template <int KS, int KC, int NQG, bool SAMPLE>
-__global__ __launch_bounds__(256) void mips_filter_kernel(FilterArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KC >= 1 && KC <= 2 ? 3 : 1)))
+void mips_filter_kernel(FilterArgs a) {
   constexpr int KS2 = (KS + 1) / 2;
   constexpr bool BF = KC > 0;
   typedef float fv2 __attribute__((ext_vector_type(2)));
@@ -1307,7 +1332,11 @@ __global__ __launch_bounds__(256) void mips_filter_kernel(FilterArgs a) {
     fv2 p[NP > 0 ? NP : 1];
     float t;
     u32x4 h[BF ? KC : 1];
+    uint32_t tw;  // bf16 tail: item lr's last dims (lane group LG of the last chunk)
   };
+  // byte offset of item lr's tail u32 in a block (word 0 of the block without a tail)
+  const int tail_off = a.TD ? (64 * (KC - 1) + 16 * a.LG) * 16 + 4 * lr : 0;
+  const bool tail_lane = a.TD && lg == a.LG;
   Frag fa, fb;
   auto load = [&](Frag& f, int64_t ib) {
     ib = ib < b1 ? ib : b1 - bstride;  // clamped: loads stay unconditional
@@ -1319,6 +1348,8 @@ __global__ __launch_bounds__(256) void mips_filter_kernel(FilterArgs a) {
 #pragma unroll
       for (int c = 0; c < KC; ++c)
         f.h[c] = __builtin_nontemporal_load(&src[c * 64 + (c == KC - 1 ? last_lane : lane)]);
+      f.tw = __builtin_nontemporal_load(as_global(reinterpret_cast<const uint32_t*>(
+          reinterpret_cast<const char*>(a.packed16) + ib * a.BB + tail_off)));
     } else {
       gptr<fv2> src = pk + ib * KS2 * 64 + lane;
 #pragma unroll
@@ -1330,12 +1361,17 @@ __global__ __launch_bounds__(256) void mips_filter_kernel(FilterArgs a) {
     f4 s[NQG];
 #pragma unroll
     for (int g = 0; g < NQG; ++g) s[g] = f4_zero();
-    if constexpr (BF && NQL == 0) {
+    // the last chunk's tail lanes: {tail, 0, 0, 0} (built here, at the use, so the select
+    // does not wait on the prefetch)
+    u32x4 hlast = f.h[KC > 0 ? KC - 1 : 0];
+    if constexpr (BF) hlast = tail_lane ? u32x4{f.tw, 0u, 0u, 0u} : hlast;
+    if constexpr (!BF) {
+    } else if constexpr (NQL == 0) {
 #pragma unroll
       for (int c = 0; c < KC; ++c)
 #pragma unroll
-        for (int g = 0; g < NQG; ++g) s[g] = mfma16x16x32bf16(f.h[c], qreg16[g][c], s[g]);
-    } else if constexpr (BF) {
+        for (int g = 0; g < NQG; ++g) s[g] = mfma16x16x32bf16(c == KC - 1 ? hlast : f.h[c], qreg16[g][c], s[g]);
+    } else {
       // the LDS groups' fragments of chunk c + 1 are read while chunk c's MFMAs run (a
       // barrier per chunk keeps hipcc from hoisting every chunk's reads: 4x the registers)
       u32x4 ql[2][NQL > 0 ? NQL : 1];
@@ -1348,12 +1384,14 @@ __global__ __launch_bounds__(256) void mips_filter_kernel(FilterArgs a) {
           for (int g = 0; g < NQL; ++g) ql[(c + 1) & 1][g] = q16_lds[(g * KC + c + 1) * 64 + lane];
         }
 #pragma unroll
-        for (int g = 0; g < NQR; ++g) s[g] = mfma16x16x32bf16(f.h[c], qreg16[g][c], s[g]);
+        for (int g = 0; g < NQR; ++g) s[g] = mfma16x16x32bf16(c == KC - 1 ? hlast : f.h[c], qreg16[g][c], s[g]);
 #pragma unroll
-        for (int g = 0; g < NQL; ++g) s[NQR + g] = mfma16x16x32bf16(f.h[c], ql[c & 1][g], s[NQR + g]);
+        for (int g = 0; g < NQL; ++g)
+          s[NQR + g] = mfma16x16x32bf16(c == KC - 1 ? hlast : f.h[c], ql[c & 1][g], s[NQR + g]);
         __builtin_amdgcn_sched_barrier(0);
       }
-    } else {
+    }
+    if constexpr (!BF) {
 #pragma unroll
       for (int st = 0; st < KS; ++st) {
         const float av = (st >> 1) < NP ? ((st & 1) ? f.p[st >> 1].y : f.p[st >> 1].x) : f.t;
@@ -2238,7 +2276,8 @@ extern "C" int mips_topk(const float* queries, const float* packed_items, int64_
     const PackLayout L = pack_layout(X, D);
     const char* pbase = (const char*)packed_items;
     FilterArgs f{queries, packed_items, p.KC ? (const u32x4*)(pbase + L.off16) : nullptr,
-                 p.KC ? bf16_block_bytes(D, p.KC) : 0, p.KC ? bf16_last_groups(D, p.KC) : 0, X, D, B,
+                 p.KC ? bf16_block_bytes(D, p.KC) : 0, p.KC ? bf16_last_groups(D, p.KC) : 0,
+                 p.KC ? bf16_tail_dims(D, p.KC) : 0, X, D, B,
                  p.n_blocks, p.GB, p.G, p.sr, (float*)(ws + p.off_smax),
                  p.RB, tau, cnt, (float*)(ws + p.off_cs), (int*)(ws + p.off_ci), (int*)ws,
                  option(GR_OPT_MIPS_FORCE_FALLBACK) != 0,

@@ -41,7 +41,7 @@ _MAP = [
     (r"attn_fwd_kernel", "attn_fwd"),
     (r"attn_bwd_fused_kernel", "attn_bwd"),
     (r"attn_bwd_dkv_kernel", "attn_bwd_dkv"),
-    (r"attn_bwd_dq_kernel", "attn_bwd_dq"),
+    (r"attn_bwd_dq_kernel|attn_bwd_dq_ds_kernel", "attn_bwd_dq"),
     (r"bias_grad_reduce_kernel", "attn_bias_reduce"),
     (r"(Op|Rw)LnUvqkBwd", "ln_uvqk_bwd"),
     (r"(Op|Rw)LnUvqk", "ln_uvqk_fwd"),
