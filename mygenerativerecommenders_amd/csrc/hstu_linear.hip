@@ -1187,6 +1187,12 @@ static int hstu_ln_uvqk_fwd_impl(bool bf16, const float* x, int64_t ld_x, const 
   return bf16 ? launch_rowpanel_bf16(op, max_rows, false, "hstu_ln_uvqk_fwd", (hipStream_t)stream)
               : launch_rowpanel(op, max_rows, false, "hstu_ln_uvqk_fwd", (hipStream_t)stream);
 }
+#ifdef GR_STAMP
+extern "C" __attribute__((visibility("default"))) int gr_rw_stamp_read(unsigned long long* host, int n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(gr::gr_rw_buf), sizeof(unsigned long long) * n) == hipSuccess ? 0 : 1;
+}
+#endif
+
 extern "C" int hstu_ln_uvqk_fwd(const float* x, int64_t ld_x, const int64_t* offsets, int B,
                                 int64_t max_rows, int D, const float* w_uvqk, int n_out,
                                 float eps, int activation, float* x_stats, float* h_pre,

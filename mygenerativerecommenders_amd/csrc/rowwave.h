@@ -172,8 +172,26 @@ __device__ __forceinline__ void rw_mma(const float* Wl, const float (&a)[KG][4],
 // boundary is gate_o(l) -> ln_uvqk(l + 1) (y = x + o W_o^T + b, then silu(LN(y) W_uvqk)),
 // the backward one ln_uvqk_bwd(l) -> gate_o_bwd(l - 1) (dx_l is the dy of layer l - 1):
 // one launch and no re-read of the boundary rows instead of two launches.
+#ifdef GR_STAMP
+// Diagnostic build only (-DGR_STAMP): per-wave s_memrealtime stamps of rowwave2_kernel
+// (entry, panels staged, product 1, epilogue 1, product 2, epilogue 2), gr_rw_stamp_read.
+static __device__ unsigned long long gr_rw_buf[1 << 15];
+#define GR_RW_T(i)                                                                  \
+  do {                                                                              \
+    __builtin_amdgcn_sched_barrier(0);                                              \
+    rw_t[i] = __builtin_amdgcn_s_memrealtime();                                     \
+    __builtin_amdgcn_sched_barrier(0);                                              \
+  } while (0)
+#else
+#define GR_RW_T(i) do { } while (0)
+#endif
+
 template <int KG1, int NT1, int NT2, class Op1, class Op2>
 __global__ __launch_bounds__(256) void rowwave2_kernel(Op1 op1, Op2 op2) {
+#ifdef GR_STAMP
+  unsigned long long rw_t[8] = {};
+#endif
+  GR_RW_T(0);
   using C1 = RowWaveCfg<KG1, NT1>;
   constexpr int VEC = Op1::VEC;
   static_assert(Op2::VEC == VEC, "one quad layout");
@@ -194,6 +212,7 @@ __global__ __launch_bounds__(256) void rowwave2_kernel(Op1 op1, Op2 op2) {
   rw_stage_w<KG1, NT1>(op1, W1);
   rw_stage_w<NT1, NT2>(op2, W2);
   __syncthreads();
+  GR_RW_T(1);
   for (; u < n_units; u += ustep) {
     const int64_t m = u * 16 + lr;
     const bool ok = m < total;
@@ -205,15 +224,33 @@ __global__ __launch_bounds__(256) void rowwave2_kernel(Op1 op1, Op2 op2) {
     op2.epi_load(es2, m, ok, lg);
     f4 acc1[NT1];
     rw_mma<KG1, NT1, VEC>(W1, a1, acc1, lr, lg);
+#ifdef GR_STAMP
+    asm volatile("" ::"v"(acc1[0][0]));
+#endif
+    GR_RW_T(2);
     typename Op2::Src s2;
     op1.epi(acc1, es1, m, ok, lg, s2.v);
     if (u + ustep < n_units) op1.load(cur, m + ustep * 16, lg);  // the next unit's rows
     float a2[NT1][4];
     op2.prep(s2, a2, m, ok, lg);
+#ifdef GR_STAMP
+    asm volatile("" ::"v"(a2[0][0]));
+#endif
+    GR_RW_T(3);
     f4 acc2[NT2];
     rw_mma<NT1, NT2, VEC>(W2, a2, acc2, lr, lg);
+#ifdef GR_STAMP
+    asm volatile("" ::"v"(acc2[0][0]));
+#endif
+    GR_RW_T(4);
     op2.epi(acc2, es2, m, ok, lg);
+    GR_RW_T(5);
   }
+#ifdef GR_STAMP
+  const int slot = ((int)blockIdx.x * 4 + w) * 8;
+  if (lane == 0 && slot + 8 <= (1 << 15))
+    for (int i = 0; i < 8; ++i) gr_rw_buf[slot + i] = rw_t[i];
+#endif
 }
 
 template <int KG, int NT, class Op>

@@ -89,14 +89,17 @@ def test_workspace_size_queries_are_host_only():
         assert L.hstu_attn_bwd_workspace_size_d(32, 2059, 2048, 1, 256, 256, 128) == slabs3
     assert L.hstu_bucket_map_bytes(128, 211) == 2 * 128 * 10 * 4096
     assert L.mips_packed_items_bytes(3953, 50) == 4 * ((3953 + 15) // 16) * 7 * 128
-    # filter-sized catalogs: f32 blocks | bf16 copy (a full 16x16x32 chunk + 3 of the second
-    # chunk's 4 lane groups = 1,792 B per 16 items) | max norm |
-    # row-major f32 rows padded to 52 floats
+    # filter-sized catalogs: f32 blocks | bf16 copy (a full 16x16x32 chunk + 2 of the second
+    # chunk's 4 lane groups + a 64-byte tail for dims 48, 49 = 1,600 B per 16 items) |
+    # max norm | row-major f32 rows padded to 52 floats
     X = 1_000_003
     nblk = (X + 15) // 16
     f32 = 4 * nblk * 7 * 128
     al = lambda v: (v + 255) // 256 * 256  # noqa: E731
-    assert L.mips_packed_items_bytes(X, 50) == (al(f32) + al(nblk * 1792) + 256
+    assert L.mips_packed_items_bytes(X, 50) == (al(f32) + al(nblk * 1600) + 256
+                                                + al(4 * X * 52))
+    # D = 52: the last group holds 4 dims (no tail; 1,792 B)
+    assert L.mips_packed_items_bytes(X, 52) == (al(f32) + al(nblk * 1792) + 256
                                                 + al(4 * X * 52))
     assert L.mips_packed_items_bytes(X, 64) == (al(4 * nblk * 8 * 128) + al(nblk * 2048) + 256
                                                 + al(4 * X * 64))

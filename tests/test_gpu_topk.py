@@ -232,7 +232,7 @@ def test_mips_filter_path_bitexact(B, X, D, k, N0):
     _check_filter(Q, E, np.arange(1, X + 1, dtype=np.int64), inv, k, expect_flag=0)
 
 
-@pytest.mark.parametrize("D", [5, 8, 20, 40, 47, 58])
+@pytest.mark.parametrize("D", [5, 8, 17, 20, 40, 47, 49, 58])
 def test_mips_filter_bf16_layouts_bitexact(D):
     """Every bf16 block layout of the filter copy (16x16x32 chunks, a 16x16x16 chunk and a
     tail of 1-3 stored k-groups; dims padded to 4, not 32) is bit-exact end to end."""
