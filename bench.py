@@ -20,6 +20,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import sys
 import time
 
 import torch
@@ -40,6 +41,16 @@ def _max_over_ranks(x: float, world: int) -> float:
     t = torch.tensor([x], dtype=torch.float64, device="cuda")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+_T0 = time.perf_counter()
+
+
+def progress(msg: str) -> None:
+    """A line on stderr per finished leg (rank 0): the run's progress, and output that a
+    supervisor watching for silence sees while the long legs run."""
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(f"[bench {time.perf_counter() - _T0:7.1f} s] {msg}", file=sys.stderr, flush=True)
 
 
 def make_batch(B, N0, out_len, D, seed, device, fixed_len=True):
@@ -568,6 +579,7 @@ def main():
     ap.add_argument("--cpu-batch", type=int, default=128,
                     help="sequences per iteration of the CPU proxy baseline")
     args = ap.parse_args()
+    progress("start")
 
     from mygenerativerecommenders_amd import _lib
     from mygenerativerecommenders_amd.candidate_index import CandidateIndex
@@ -693,6 +705,7 @@ def main():
     kern = {n: (t / c if c else 0.0) for n, (t, c) in ktimes.items()}
     kern_total = {n: t / args.steps for n, (t, c) in ktimes.items() if c}
 
+    progress("C2 headline timed and instrumented")
     # ---- roofline of the dominant kernel (largest device time per step)
     peaks = peak_table()
     fwd_f, dkv_f, dq_f = attn_flops(lengths.cpu(), 1, D, D, blocks)
@@ -868,6 +881,7 @@ def main():
                              merge_avg_launch_ms=round(kmerge, 4), flops_per_launch=fl),
         }
 
+    progress("C4 retrieval leg done")
     # ---- C4 variant D = 256: the bf16 filter path beyond D = 64
     retrieval_d256 = None
     if not args.no_retrieval_leg and args.retrieval_d256_items > 0:
@@ -923,6 +937,7 @@ def main():
         }
         del sidx2
 
+    progress("C4 D=256 leg done")
     # ---- C2 batch sweep (encoder step alone) and the C3 leg
     sweep = None
     if args.sweep:
@@ -975,7 +990,9 @@ def main():
     c3 = c3_bf16 = c2_bf16 = None
     if args.c3_steps > 0:
         c3 = c3_leg(False)
+        progress("C3 fp32 leg done")
         c3_bf16 = c3_leg(True)
+        progress("C3 bf16 leg done")
     if not args.no_bf16_leg:
         r = encoder_leg(B, N0, out_len, D, blocks, 1, args.steps, 3, device, world, 2500 + rank,
                         bf16=True, instrument=True)
@@ -989,6 +1006,7 @@ def main():
                                                                             key=lambda kv: -kv[1])}}
 
     # the reference yaml's 2 blocks (configs/model/hstu.yaml:23) beside BASELINE's 4
+    progress("C2 sweep / bf16 legs done")
     r2b = encoder_leg(B, N0, out_len, D, 2, 1, args.steps, 3, device, world, 2600 + rank)
     c2_two_blocks = {"metric": "HSTU seq/s (fwd+bwd)", "value": r2b["value"], "unit": "seq/s",
                      "ms_per_step": r2b["ms_per_step"], "dtype": "fp32",
@@ -997,6 +1015,7 @@ def main():
                                 "execution": r2b["execution"]}}
 
     e2e = None
+    progress("C2 two-block leg done")
     if args.e2e_steps > 0:
         try:
             e2e = e2e_train_leg(args, device, world, lengths, ts, past_ids)
@@ -1004,6 +1023,7 @@ def main():
             e2e = {"error": f"{type(e).__name__}: {e}"}
 
     c5_full = None
+    progress("e2e leg done")
     if args.c5_steps > 0:
         try:
             B5, N5, D5, L5, V5 = 32, 2048, 256, 8, 131_262
@@ -1027,6 +1047,7 @@ def main():
         for nth in sorted({share, host}):
             torch.set_num_threads(nth)
             trials[nth] = cpu_baseline_hstu(args.cpu_batch, N0, out_len, D, blocks, budget_s=10.0)
+            progress(f"CPU baseline at {nth} threads done")
         threads = max(trials, key=lambda n: trials[n][0])
         torch.set_num_threads(threads)
         sps, n_it, dt_it = trials[threads]
