@@ -1040,11 +1040,26 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # BASELINE.md step 3 asks for torch.set_num_threads(os.cpu_count()); on the GPU box
         # os.cpu_count() is the whole host while the job's CPU share is OMP_NUM_THREADS
-        # (torch's default), so both are timed and the faster one is the baseline
+        # (torch's default, 16).  The host count is timed beside the share when the job can
+        # use that many CPUs (affinity and cgroup quota); when it exceeds twice the share
+        # it only oversubscribes the share (one iteration at 256 threads on 16 CPUs ran for
+        # minutes), so the share is the baseline and the line says why.
         share = torch.get_num_threads()
         host = os.cpu_count() or share
+        usable = min(host, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else host)
+        try:
+            q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+            if q != "max":
+                usable = min(usable, max(1, int(q) // int(per)))
+        except (OSError, ValueError):
+            pass
+        host_note = None
+        if usable > 2 * share:
+            host_note = (f"{host} host CPUs not timed: the job's CPU share is {share} "
+                         f"(OMP_NUM_THREADS); more threads only oversubscribe it")
+            usable = share
         trials = {}
-        for nth in sorted({share, host}):
+        for nth in sorted({share, usable}):
             torch.set_num_threads(nth)
             trials[nth] = cpu_baseline_hstu(args.cpu_batch, N0, out_len, D, blocks, budget_s=10.0)
             progress(f"CPU baseline at {nth} threads done")
@@ -1057,6 +1072,7 @@ def main():
         cpu = {"value": round(sps, 2), "unit": "seq/s", "cores": threads, "kind": "port",
                "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
                "threads_tried": {str(n): round(t[0], 2) for n, t in trials.items()},
+               **({"host_threads_note": host_note} if host_note else {}),
                "sample": f"oracle reference-order fp32 HSTU fwd+bwd (train, dropout 0.2), "
                          f"{args.cpu_batch} seqs x {N0} tokens, {blocks} blocks, median of "
                          f"{n_it} iters ({dt_it * 1e3:.0f} ms/iter); proxy within 5 % of the "
