@@ -1053,7 +1053,8 @@ def main():
                 usable = min(usable, max(1, int(q) // int(per)))
         except (OSError, ValueError):
             pass
-        host_note = None
+        host_note = (f"{host} host CPUs, {usable} usable by this job (affinity / cgroup quota)"
+                     if usable < host else None)
         if usable > 2 * share:
             host_note = (f"{host} host CPUs not timed: the job's CPU share is {share} "
                          f"(OMP_NUM_THREADS); more threads only oversubscribe it")
