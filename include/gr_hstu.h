@@ -89,7 +89,8 @@ GR_API int gr_timing_reset(void);
  *                                  dV and dK in one workgroup (0, default: C3 dK/dV 1.88 ms
  *                                  per layer), as separate workgroups of one launch (1:
  *                                  2.62 ms), or as two launches (2: 2 x 1.08 ms)
- *   GR_OPT_MIPS_FILTER_PAIRED 0|1  filter pass with several query chunks (D > 64 at B = 128):
+ *   GR_OPT_MIPS_FILTER_PAIRED 0|1  filter pass with several 128-query chunks (B > 128; a
+ *                                  workgroup holds 128 queries at every D <= 256):
  *                                  the chunks of one item range run on one XCD back to back
  *                                  (default 1: the range streams from HBM once) or as the
  *                                  2-D grid (0: every chunk streams the table)
