@@ -55,7 +55,9 @@ GR_API int gr_timing_reset(void);
  * captured.  gr_get_option returns the current value (or -1 for an unknown option).
  *   GR_OPT_MIPS_FILTER_FP32   0|1  bf16 items table off: the filter pass scores on the
  *                                  f32 table (slower, exact scores; results identical)
- *   GR_OPT_MIPS_FILTER_WGS    >=1  filter workgroups per CU per round (default 2)
+ *   GR_OPT_MIPS_FILTER_WGS    >=0  filter workgroups per CU per round (0 = default: 3 at
+ *                                  D <= 64, whose kernels fit 3 per CU: 10M x 50 filter
+ *                                  221 -> 202 us; 2 above)
  *   GR_OPT_MIPS_FILTER_ROUNDS >=0  filter rounds (0 = chosen from the catalog size)
  *   GR_OPT_MIPS_FORCE_FALLBACK 0|1 thresholds forced to +inf: every query takes the
  *                                  exact fallback scan (tests / profiling)

@@ -23,7 +23,7 @@ void set_error(const char* fmt, ...) {
 const char* last_error() { return g_err.c_str(); }
 
 // ---------------------------------------------------------------- launch options
-static std::atomic<int64_t> g_opt[GR_OPT_COUNT_] = {0, 0, 2, 0, 0, 0, 1, 1, 1, 0, 0, 1, 1, 0, 1, 0};
+static std::atomic<int64_t> g_opt[GR_OPT_COUNT_] = {0, 0, 0, 0, 0, 0, 1, 1, 1, 0, 0, 1, 1, 0, 1, 0};
 
 int64_t option(int which) { return g_opt[which].load(std::memory_order_relaxed); }
 
@@ -58,8 +58,8 @@ int gr_version(void) { return GR_HSTU_ABI_VERSION; }
 
 int gr_set_option(int option, int64_t value) {
   GR_REQUIRE(option > 0 && option < GR_OPT_COUNT_, "gr_set_option: unknown option %d", option);
-  GR_REQUIRE(option != GR_OPT_MIPS_FILTER_WGS || (value >= 1 && value <= 16),
-             "gr_set_option: filter WGs per CU %lld not in [1, 16]", (long long)value);
+  GR_REQUIRE(option != GR_OPT_MIPS_FILTER_WGS || (value >= 0 && value <= 16),
+             "gr_set_option: filter WGs per CU %lld not in [0, 16]", (long long)value);
   GR_REQUIRE(value >= 0, "gr_set_option: negative value %lld", (long long)value);
   gr::g_opt[option].store(value, std::memory_order_relaxed);
   return 0;

@@ -2056,7 +2056,10 @@ static TopkPlan plan_topk(int B, int64_t X, int D, int k, int N0) {
     p.NQG = B <= 32 ? 2 : 8;  // KC > 2: 4 groups in VGPRs, 4 read from LDS
     p.n_chunks = ceil_div(B, p.NQG * 16);
     // whole rounds of 2 four-wave workgroups per CU, >= ~48 blocks per wave
-    const int64_t per_round = (int64_t)device_cus() * 4 * option(GR_OPT_MIPS_FILTER_WGS);
+    // (GR_OPT_MIPS_FILTER_WGS = 0: 3 per CU at KC <= 2, whose kernels hold 168 VGPRs)
+    const int64_t wgs = option(GR_OPT_MIPS_FILTER_WGS) > 0 ? option(GR_OPT_MIPS_FILTER_WGS)
+                                                           : (kc_bf > 0 && kc_bf <= 2 ? 3 : 2);
+    const int64_t per_round = (int64_t)device_cus() * 4 * wgs;
     // GR_OPT_MIPS_FILTER_FP32: filter on the f32 table (exact scores, 16x fewer flop/s)
     p.KC = kc_bf;
     // f32: >= ~48 blocks per wave.  bf16 (streaming-bound): one round (10M items: 7

@@ -122,7 +122,7 @@ def test_launch_options_are_explicit_not_environment():
                          "ATTN_BWD_DS", "DETERMINISTIC", "WGRAD_ROWS", "PANEL_VEC",
                          "ATTN_BWD_WIDE_DS", "ATTN_BWD_WIDE_SPLIT", "MIPS_FILTER_PAIRED",
                          "MIPS_SAMPLE_STRIDE"}
-    defaults = {"MIPS_FILTER_WGS": 2, "ROWWAVE": 1, "ATTN_BWD_PAIRS": 1, "PANEL_VEC": 1, "ATTN_BWD_DS": 1,
+    defaults = {"ROWWAVE": 1, "ATTN_BWD_PAIRS": 1, "PANEL_VEC": 1, "ATTN_BWD_DS": 1,
                 "ATTN_BWD_WIDE_DS": 1, "ATTN_BWD_WIDE_SPLIT": 0, "MIPS_FILTER_PAIRED": 1}
     for n in opts:
         assert _lib.get_option(n) == defaults.get(n, 0), n
@@ -133,7 +133,7 @@ def test_launch_options_are_explicit_not_environment():
     assert L.gr_get_option(0) == -1 and L.gr_get_option(99) == -1
     assert L.gr_set_option(99, 1) != 0 and "unknown option" in L.gr_last_error().decode()
     with pytest.raises(_lib.GrError):
-        _lib.set_option("MIPS_FILTER_WGS", 0)
+        _lib.set_option("MIPS_FILTER_WGS", 17)
     with pytest.raises(_lib.GrError):
         _lib.set_option("ROWWAVE", -1)
     # none of the library's own sources reads the environment (rocPRIM, linked for the
