@@ -53,7 +53,13 @@ GR_API int gr_timing_reset(void);
 /* Process-wide launch options (the library reads no environment variables).  Set
  * before the launches they should affect; not while a graph that used them is being
  * captured.  gr_get_option returns the current value (or -1 for an unknown option).
- *   GR_OPT_MIPS_FILTER_FP32   0|1  bf16 items table off: the filter pass scores on the
+ * Workspace sizes: a *_workspace_size query answers for the options in force when it
+ * is called, and every launch re-derives its need under the options in force at launch.
+ * A workspace sized under other options is therefore never overrun: the launch returns
+ * non-zero with "workspace N B < M B" (gr_wgrad*, mips_topk, sampled softmax, rel bias),
+ * or, for hstu_attn_bwd's optional dS tiles, runs the recomputing form that needs only
+ * the bias slabs (tests/test_capi.py::test_option_changed_between_sizing_and_launch...).
+ *   GR_OPT_MIPS_FILTER_FP32  0|1  bf16 items table off: the filter pass scores on the
  *                                  f32 table (slower, exact scores; results identical)
  *   GR_OPT_MIPS_FILTER_WGS    >=0  filter workgroups per CU per round (0 = default: 3 at
  *                                  D <= 64, whose kernels fit 3 per CU: 10M x 50 filter
@@ -97,7 +103,7 @@ GR_API int gr_timing_reset(void);
  *                                  (default 1: the range streams from HBM once) or as the
  *                                  2-D grid (0: every chunk streams the table)
  *   GR_OPT_MIPS_SAMPLE_STRIDE >=0  filter path: item blocks between the blocks the sample
- *                                  pass scores (0 = 16); the threshold is the (1024 /
+ *                                  pass scores (0 = 32); the threshold is the (1024 /
  *                                  stride)-th largest group maximum (~1024 candidates)
  */
 enum {
@@ -461,9 +467,10 @@ GR_API int hstu_ln_uvqk_bwd_bf16(const float* dh, int64_t ld_dh, const int64_t* 
  *   bwd: hstu_ln_uvqk_bwd of layer l (dx = dy_res + LN_bwd(dh W_uvqk^T)) then
  *        hstu_gate_o_bwd of layer l - 1 with dy = dx (du, d_attn of layer l - 1).
  * Arguments: those of the two calls it replaces (the second call's row input is the
- * first one's output, y / dx, which is still stored).  Results are identical to the two
- * calls; shapes the fused form does not cover (D or h dv > 64, n_out > 256, unaligned
- * rows) run exactly those two calls.  fp32 only. */
+ * first one's output, y / dx, which is still stored).  Results agree with the two calls to
+ * fp32 summation order (the fused UVQK product is a row-wave MFMA chain where the separate
+ * launch may take the row panel); shapes the fused form does not cover (D or h dv > 64,
+ * n_out > 256, unaligned rows) run exactly those two calls, bit-identical.  fp32 only. */
 GR_API int hstu_boundary_fwd(const float* u, int64_t ld_u, const float* attn, int64_t ld_attn,
                     const int64_t* offsets, int B, int64_t max_rows, int hdv, int D,
                     const float* w_o, const float* b_o, const float* x_res, int64_t ld_x,

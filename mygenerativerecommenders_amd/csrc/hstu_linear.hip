@@ -1598,7 +1598,8 @@ extern "C" int hstu_gate_o_cat_wide_bwd(const float* dy, int64_t ld_dy, const in
 // unit per wave and ~1.6 units per SIMD), so the boundary's two launches cost about twice
 // one, and the boundary rows (y, dx) are handed over in registers.  Shapes outside the
 // instantiated set (D, h dv <= 64, n_out <= 256) fall back to the two separate launches,
-// with identical results either way (same per-unit arithmetic).
+// results agreeing to fp32 summation order (the fused UVQK product is a row-wave chain
+// where the separate launch may take the row panel; bit-identical on the fallback shapes).
 namespace gr {
 
 static int rw2_bucket_small(int x) {  // the boundary's shared width (D and h dv) in 16-col groups

@@ -2053,7 +2053,7 @@ static TopkPlan plan_topk(int B, int64_t X, int D, int k, int N0) {
     gb = std::max<int64_t>({gb, 1, (n_sb + SAMPLE_WAVES - 1) / SAMPLE_WAVES});
     p.GB = (int)gb;
     p.G = ceil_div((int)((n_sb + p.GB - 1) / p.GB), 4);  // sample workgroups
-    p.NQG = B <= 32 ? 2 : 8;  // KC > 2: 4 groups in VGPRs, 4 read from LDS
+    p.NQG = B <= 32 ? 2 : 8;  // KC > 2: 3 groups in VGPRs and 5 read from LDS (filter), 2 and 6 (sample)
     p.n_chunks = ceil_div(B, p.NQG * 16);
     // whole rounds of 2 four-wave workgroups per CU, >= ~48 blocks per wave
     // (GR_OPT_MIPS_FILTER_WGS = 0: 3 per CU at KC <= 2, whose kernels hold 168 VGPRs)

@@ -27,7 +27,7 @@ import torch
 import torch.nn.functional as F  # noqa: F401  (kept for API parity of the module)
 
 from . import ops
-from .bucket_table import NUM_BUCKETS
+from .bucket_table import BUCKET_THRESHOLDS, NUM_BUCKETS
 
 TIMESTAMPS_KEY = "timestamps"
 
@@ -38,6 +38,42 @@ def _default_bucketization_fn(x: torch.Tensor) -> torch.Tensor:
     """hstu.py:579-581.  The fused kernel evaluates this function exactly through the
     integer threshold table in ``bucket_table.py``; it is kept for API parity."""
     return (torch.log(torch.abs(x).clamp(min=1)) / 0.301).long()
+
+
+def _bucket_probe_deltas() -> torch.Tensor:
+    """int64 time deltas probing every edge of the threshold table: each threshold, its
+    two neighbours, the midpoint to the next threshold, and their negations."""
+    thr = BUCKET_THRESHOLDS
+    vals = set()
+    for b, t in enumerate(thr):
+        vals.update((t - 1, t, t + 1))
+        if b + 1 < len(thr):
+            vals.add((t + thr[b + 1]) // 2)
+    vals = sorted(v for v in vals if v >= 0)
+    return torch.tensor(vals + [-v for v in vals], dtype=torch.int64)
+
+
+def _check_bucketization_fn(fn: Callable[[torch.Tensor], torch.Tensor]) -> None:
+    """The attention kernels bucket relative times through the integer threshold table
+    of the reference's default function (hstu.py:579-581, clamped to [0, num_buckets] at
+    hstu.py:117-123).  A caller-supplied function is accepted only if it agrees with
+    that table on every probe delta (the reference builds it as a lambda, so an identity
+    test would reject valid models); anything else raises instead of silently using
+    the default buckets."""
+    d = _bucket_probe_deltas()
+    thr = torch.tensor(BUCKET_THRESHOLDS, dtype=torch.int64)
+    want = torch.searchsorted(thr, d.abs(), right=True) - 1
+    try:
+        got = torch.clamp(fn(d).long(), min=0, max=NUM_BUCKETS)
+    except Exception as e:  # noqa: BLE001 — any failure means "not the default function"
+        raise ValueError(f"bucketization_fn could not be evaluated on int64 deltas: {e}") from e
+    if got.shape != want.shape or not torch.equal(got, want):
+        bad = int((got != want).nonzero()[0, 0]) if got.shape == want.shape else 0
+        raise ValueError(
+            "bucketization_fn differs from the reference default "
+            "(log(|dt|.clamp(min=1)) / 0.301).long() (hstu.py:579-581), which is the only "
+            f"bucketization the fused attention kernels implement (first mismatch at "
+            f"dt = {int(d[bad])})")
 
 
 class RelativeAttentionBiasModule(torch.nn.Module):
@@ -57,10 +93,11 @@ class RelativeBucketedTimeAndPositionBasedBias(RelativeAttentionBiasModule):
     def __init__(self, max_seq_len: int, num_buckets: int,
                  bucketization_fn: Callable[[torch.Tensor], torch.Tensor]) -> None:
         super().__init__()
-        if num_buckets != NUM_BUCKETS or bucketization_fn is not _default_bucketization_fn:
-            # the threshold table encodes the reference's default function only
-            if num_buckets != NUM_BUCKETS:
-                raise ValueError(f"num_buckets must be {NUM_BUCKETS} (got {num_buckets})")
+        # the kernels' threshold table encodes the reference's default function only
+        if num_buckets != NUM_BUCKETS:
+            raise ValueError(f"num_buckets must be {NUM_BUCKETS} (got {num_buckets})")
+        if bucketization_fn is not _default_bucketization_fn:
+            _check_bucketization_fn(bucketization_fn)
         self._max_seq_len: int = max_seq_len
         self._ts_w = torch.nn.Parameter(torch.empty(num_buckets + 1).normal_(mean=0, std=0.02))
         self._pos_w = torch.nn.Parameter(
@@ -215,6 +252,8 @@ class HSTUJagged(torch.nn.Module):
     def jagged_forward(self, x, x_offsets, all_timestamps, invalid_attn_mask,
                        delta_x_offsets=None, cache=None, return_cache_states=False,
                        max_len: Optional[int] = None):
+        if delta_x_offsets is not None or cache is not None:
+            raise NotImplementedError("incremental (cached) HSTU decoding is not supported")
         cache_states: List[HSTUCacheState] = []
         n = invalid_attn_mask.size(-1)
         # one bucket map per batch, shared by every layer's forward and backward

@@ -462,7 +462,8 @@ def _stu_backward(saved, dy, geo: STUGeometry, seed: int, seed_offset, want_uvqk
         ws_fn = (L.hstu_attn_bwd_bf16_workspace_size_copies if copies is not None else
                  L.hstu_attn_bwd_bf16_workspace_size)
         ws_a_n = ws_fn(B, geo.N, geo.max_len, H, dqk, dv, NUM_BUCKETS)
-    else:
+    elif bmap is not None or max(dqk, dv) > 128:
+        # narrow f32 heads use the workspace (slabs, dS tiles) only with a bucket map
         ws_a_n = L.hstu_attn_bwd_workspace_size_d(B, geo.N, geo.max_len, H, dqk, dv, NUM_BUCKETS)
     if ws_a_n or bmap is not None:
         ws_a = torch.empty(max(ws_a_n, 4), dtype=torch.uint8, device=dev)

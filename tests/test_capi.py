@@ -114,6 +114,41 @@ def test_workspace_size_queries_are_host_only():
     assert L.hstu_attn_bwd_workspace_size(0, 211, 200, 1, 128) == 0
 
 
+def test_option_changed_between_sizing_and_launch_is_rejected():
+    """A launch re-derives its workspace need under the options in force at launch time
+    and returns non-zero when the caller's workspace (sized under other options) is
+    smaller — never an overflow.  The check runs before any device work, so fake
+    non-null pointers are safe here (no GPU needed)."""
+    L = _lib.lib()
+    fake = 1 << 20  # never dereferenced: the launch returns at the workspace check
+    # Ka = 300 (> 256: the narrow plan only, whose split size the option sets)
+    with _lib.option("WGRAD_ROWS", 4096):
+        ws = L.gr_wgrad_workspace_size(200000, 300, 200)
+    with _lib.option("WGRAD_ROWS", 256):
+        assert L.gr_wgrad_workspace_size(200000, 300, 200) > ws  # more splits, more slabs
+        with pytest.raises(_lib.GrError, match="workspace"):
+            _lib.call("gr_wgrad", fake, 300, None, fake, 200, fake, 128, 200000, 300, 200, fake,
+                      None, fake, ws, None)
+        desc = (ctypes.c_int64 * 18)(fake, 300, 0, fake, 200, 300, 200, fake, 0,
+                                     fake, 300, 0, fake, 50, 300, 50, fake, fake)
+        with pytest.raises(_lib.GrError, match="workspace"):
+            _lib.call("gr_wgrad_multi", ctypes.addressof(desc), 2, fake, 128, 200000, 0, fake, ws,
+                      None)
+    with _lib.option("MIPS_SAMPLE_STRIDE", 64):
+        ws_t = L.mips_topk_workspace_size(128, 10_000_000, 50, 200, 211)
+    with _lib.option("MIPS_SAMPLE_STRIDE", 8):
+        assert L.mips_topk_workspace_size(128, 10_000_000, 50, 200, 211) > ws_t
+        with pytest.raises(_lib.GrError, match="workspace"):
+            _lib.call("mips_topk", fake, fake, 10_000_000, 50, fake, 0, fake, 211, 128, 200, fake,
+                      fake, fake, fake, ws_t, None)
+    # the attention backward's dS tiles are optional: sized without them (ATTN_BWD_DS=0)
+    # and launched with them on, it runs the recomputing form, which needs only the slabs
+    # (tests/test_gpu_attention.py checks that form's results)
+    with _lib.option("ATTN_BWD_DS", 0):
+        slabs_only = L.hstu_attn_bwd_workspace_size(128, 211, 200, 1, 128)
+    assert slabs_only < L.hstu_attn_bwd_workspace_size(128, 211, 200, 1, 128)
+
+
 def test_launch_options_are_explicit_not_environment():
     """Launch options go through gr_set_option; the library reads no environment."""
     opts = _lib.parse_options()

@@ -81,6 +81,41 @@ def test_bias_module_materialises_on_gpu_only():
         RelativeBucketedTimeAndPositionBasedBias(10, 64, _default_bucketization_fn)
 
 
+def test_custom_bucketization_fn_checked_against_the_kernel_table():
+    """hstu.py:71-95 honours any bucketization_fn; the kernels implement the default
+    one only, so a different function must raise instead of being silently replaced."""
+    from mygenerativerecommenders_amd.hstu import RelativeBucketedTimeAndPositionBasedBias
+    # the reference builds its default as a lambda (hstu.py:579-581): accepted
+    ref_fn = lambda x: (torch.log(torch.abs(x).clamp(min=1)) / 0.301).long()  # noqa: E731
+    m = RelativeBucketedTimeAndPositionBasedBias(10, 128, ref_fn)
+    assert m._bucketization_fn is ref_fn
+    for bad in (lambda x: (torch.log(torch.abs(x).clamp(min=1)) / 0.302).long(),
+                lambda x: torch.log2(torch.abs(x).clamp(min=1)).long(),
+                lambda x: torch.zeros_like(x),
+                lambda x: (torch.log(torch.abs(x).clamp(min=1)) / 0.301).long() + (x > 10**6)):
+        with pytest.raises(ValueError, match="bucketization_fn"):
+            RelativeBucketedTimeAndPositionBasedBias(10, 128, bad)
+    with pytest.raises(ValueError, match="bucketization_fn"):
+        RelativeBucketedTimeAndPositionBasedBias(10, 128, lambda x: x.nonexistent())
+
+
+def test_incremental_decoding_raises_on_every_path():
+    """delta_x_offsets / cache (hstu.py:293-298, 415-418) are not supported: both the
+    per-layer path and the one-node stack must raise, never run a full forward."""
+    enc = _hstu(max_sequence_len=8, max_output_len=0, embedding_dim=8, item_embedding_dim=8,
+                linear_dim=8, attention_dim=8)
+    x = torch.randn(16, 8)
+    off = torch.tensor([0, 8, 16])
+    mask = enc._attn_mask
+    delta = (torch.tensor([0, 1]), torch.tensor([7, 15]))
+    for rcs in (False, True):
+        with pytest.raises(NotImplementedError):
+            enc._hstu.jagged_forward(x, off, None, mask, delta_x_offsets=delta,
+                                     return_cache_states=rcs)
+    with pytest.raises(NotImplementedError):
+        enc._hstu.jagged_forward(x, off, None, mask, cache=[None, None])
+
+
 def test_candidate_index_contract():
     from mygenerativerecommenders_amd.candidate_index import CandidateIndex
     from mygenerativerecommenders_amd.top_k import MIPSBruteForceTopK
