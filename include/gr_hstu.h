@@ -105,6 +105,11 @@ GR_API int gr_timing_reset(void);
  *   GR_OPT_MIPS_SAMPLE_STRIDE >=0  filter path: item blocks between the blocks the sample
  *                                  pass scores (0 = 32); the threshold is the (1024 /
  *                                  stride)-th largest group maximum (~1024 candidates)
+ *   GR_OPT_WGRAD_STREAM       0|1  f32 weight gradients at Ka <= 64, Nb <= 256: the streaming
+ *                                  form (default 1: operands loaded straight into MFMA
+ *                                  fragments, one workgroup per (problem, row split), splits
+ *                                  per problem by MFMA work) or the LDS-staged panels (0).
+ *                                  Workspace queries cover both forms.
  */
 enum {
   GR_OPT_MIPS_FILTER_FP32 = 1,
@@ -122,7 +127,8 @@ enum {
   GR_OPT_ATTN_BWD_WIDE_SPLIT = 13,
   GR_OPT_MIPS_FILTER_PAIRED = 14,
   GR_OPT_MIPS_SAMPLE_STRIDE = 15,
-  GR_OPT_COUNT_ = 16
+  GR_OPT_WGRAD_STREAM = 16,
+  GR_OPT_COUNT_ = 17
 };
 GR_API int gr_set_option(int option, int64_t value);
 GR_API int64_t gr_get_option(int option);

@@ -856,6 +856,10 @@ static WgPlan wgrad_plan_wide(int64_t max_rows, const int* Ka, const int* Nb, in
   return pl;
 }
 
+static bool ws_fits(const int* Ka, const int* Nb, int np);
+static int wgrad_run_stream(const WgradProb* in, int np, const int64_t* offsets, int B,
+                            int64_t max_rows, void* workspace, size_t ws_bytes, hipStream_t st);
+
 static int wgrad_run(const WgradProb* in, int np, const int64_t* offsets, int B, int64_t max_rows,
                      void* workspace, size_t ws_bytes, hipStream_t st, bool bf16 = false) {
   GR_REQUIRE(np >= 1 && np <= WG_MAXP, "gr_wgrad: %d problems (1..%d)", np, WG_MAXP);
@@ -872,6 +876,9 @@ static int wgrad_run(const WgradProb* in, int np, const int64_t* offsets, int B,
     }
     return 0;
   }
+  // f32 at Ka <= 64, Nb <= 256: the streaming form (GR_OPT_WGRAD_STREAM, default on)
+  if (!bf16 && option(GR_OPT_WGRAD_STREAM) != 0 && ws_fits(Ka, Nb, np))
+    return wgrad_run_stream(in, np, offsets, B, max_rows, workspace, ws_bytes, st);
   const bool wide = wgrad_wide_ok(in, np);
   const WgPlan pl = wide ? wgrad_plan_wide(max_rows, Ka, Nb, np) : wgrad_plan(max_rows, Ka, Nb, np);
   GR_REQUIRE(pl.ok, "gr_wgrad: the problems need more than two panel widths");
@@ -941,12 +948,282 @@ static int wgrad_run(const WgradProb* in, int np, const int64_t* offsets, int B,
   return 0;
 }
 
-// workspace of a problem list: the larger of the narrow and (when it may be taken) wide plans
+// ---------------------------------------------------------------- narrow streaming form
+// Ka <= 64, Nb <= 256, f32 (ml-1m: per layer _uvqk 50 x 200 over LN(x) rows and _o 50 x 50
+// over dy rows, 8 problems per encoder backward).  No LDS staging: a lane loads its MFMA
+// operands straight from the row-major operands (A fragment: row 4s + lane/16, column
+// 16c + lane%16; B fragment: the same row, column 16t + lane%16 — four 64-byte row
+// segments per wave instruction), WS_DEPTH k-steps (4 rows each) in flight per wave.
+// Workgroup = one (problem, row split), 8 waves: wave w owns ka-tile c = w & 3 against
+// every nb-tile of the problem, over the k-steps of parity h = w >> 2.  The two parities
+// meet in LDS (h0 + h1) and the workgroup writes one slab; ws_reduce sums each problem's
+// slabs in split order.  Splits per problem are proportional to its nb-tiles (its MFMA
+// time per row), ~one workgroup per CU over the launch, so every workgroup streams about
+// the same MFMA work and the grid is one round.  Deterministic: k-ordered MFMA chains, a
+// fixed parity order, a fixed split order.
+constexpr int WS_THREADS = 512;
+constexpr int WS_DEPTH = 4;
+constexpr int WS_MAXTNB = 16;
+
+struct WsProb {
+  const float* a;
+  int64_t lda;
+  const float2* a_stats;
+  const float* bm;
+  int64_t ldb;
+  int Ka, Nb, NC;  // NC = Nb + 1: slab column Nb holds the column sum of A'
+  int tnb;         // nb-tile class (4, 8, 13, 16) >= ceil(Nb / 16)
+  int splits;      // row splits = workgroups of this problem
+  int wg0;         // first workgroup of this problem
+  float* slabs;    // [splits][Ka][NC]
+  float* c;
+  float* colsum;
+};
+struct WsArgs {
+  WsProb p[WG_MAXP];
+  int np;
+  int wg0[WG_MAXP + 1];   // prefix of workgroups (main launch)
+  int blk0[WG_MAXP + 1];  // prefix of reduce blocks
+  const int64_t* offsets;
+  int B;
+};
+
+template <int TNB>
+__device__ __forceinline__ void ws_body(const WsProb& g, int64_t total, int split, char* smem) {
+  const int w = wave_id(), lane = threadIdx.x & 63;
+  const int c = w & 3, h = w >> 2;
+  const int lr = lane & 15, lg = lane >> 4;
+  // this split's rows: [r0, r1), r0 a multiple of 8 (k-steps of the two parities align)
+  const int64_t rps = ((total + g.splits - 1) / g.splits + 7) & ~(int64_t)7;
+  const int64_t r0 = (int64_t)split * rps;
+  const int64_t r1 = min(total, r0 + rps);
+  const int nks = __builtin_amdgcn_readfirstlane(r1 > r0 ? (int)((r1 - r0 + 3) >> 2) : 0);
+  const int mine = nks > h ? (nks - h + 1) >> 1 : 0;  // k-steps h, h + 2, ... of this split
+  const bool active = 16 * c < g.Ka;
+  // rows >= total read as 0 through the descriptors' range (A and its stats 0: A' = 0)
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)g.a, 0, total > 0 ? (int)(((total - 1) * g.lda + g.Ka) * 4) : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)g.bm, 0, total > 0 ? (int)(((total - 1) * g.ldb + g.Nb) * 4) : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(g.a_stats ? (const void*)g.a_stats : (const void*)g.a), 0,
+      g.a_stats ? (int)(total * 8) : 0, 0x00020000);
+  const int acol = 16 * c + lr;
+  const bool a_ok = acol < g.Ka;
+  int bcol_ok = 0;  // bit t: column 16 t + lr < Nb
+#pragma unroll
+  for (int t = 0; t < TNB; ++t) bcol_ok |= (16 * t + lr < g.Nb) ? (1 << t) : 0;
+  constexpr int OOBW = 0x40000000;
+
+  float av[WS_DEPTH], bv[WS_DEPTH][TNB];
+  float2 sv[WS_DEPTH];
+  // issue the loads of this wave's k-step j into slot u (j >= mine: all out of range)
+  auto issue = [&](int u, int j) {
+    const bool in = j < mine;
+    const int row = (int)(r0 + 4 * (2 * j + h)) + lg;
+    const int ro_a = row * (int)g.lda, ro_b = row * (int)g.ldb;
+    av[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+        ra, in && a_ok ? (ro_a + acol) * 4 : OOBW, 0, 0));
+    if (g.a_stats) {
+      const u32x2_t s = __builtin_amdgcn_raw_buffer_load_b64(rs, in ? row * 8 : OOBW, 0, 0);
+      sv[u] = make_float2(__uint_as_float(s.x), __uint_as_float(s.y));
+    } else {
+      sv[u] = make_float2(0.f, 1.f);
+    }
+#pragma unroll
+    for (int t = 0; t < TNB; ++t)
+      bv[u][t] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+          rb, in && ((bcol_ok >> t) & 1) ? (ro_b + 16 * t + lr) * 4 : OOBW, 0, 0));
+  };
+
+  f4 acc[TNB];
+#pragma unroll
+  for (int t = 0; t < TNB; ++t) acc[t] = f4_zero();
+  float csum = 0.f;  // sum over this wave's rows of A'[row][16c + lr] (the _o bias gradient)
+  if (active && mine > 0) {
+#pragma unroll
+    for (int u = 0; u < WS_DEPTH; ++u) issue(u, u);
+    const int iters = (mine + WS_DEPTH - 1) / WS_DEPTH * WS_DEPTH;
+    for (int j0 = 0; j0 < iters; j0 += WS_DEPTH) {
+#pragma unroll
+      for (int u = 0; u < WS_DEPTH; ++u) {
+        // A'[row 4 s + lg][ka 16 c + lr] (LN applied; rows out of range: 0 * 0)
+        const float a = g.a_stats ? (av[u] - sv[u].x) * sv[u].y : av[u];
+        csum += a;
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int t = 0; t < TNB; ++t) acc[t] = mfma16x16x4(a, bv[u][t], acc[t]);
+        __builtin_amdgcn_sched_barrier(0);
+        issue(u, j0 + u + WS_DEPTH);
+      }
+    }
+  }
+  // parity 1 hands its partial sums to parity 0 through LDS (fixed order h0 + h1)
+  float* xch = reinterpret_cast<float*>(smem);  // [4][TNB][4][64], then [4][16] column sums
+  csum = wg_colsum_lanes(csum);
+  if (h == 1) {
+#pragma unroll
+    for (int t = 0; t < TNB; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) xch[((c * TNB + t) * 4 + r) * 64 + lane] = acc[t][r];
+    if (lg == 0) xch[4 * TNB * 4 * 64 + 16 * c + lr] = csum;
+  }
+  __syncthreads();
+  if (h == 1) return;
+  float* slab = g.slabs + (int64_t)split * g.Ka * g.NC;
+  if (g.colsum && lg == 0 && a_ok)
+    slab[(int64_t)acol * g.NC + g.Nb] = csum + xch[4 * TNB * 4 * 64 + 16 * c + lr];
+  // acc[t][r] = C[ka 16 c + 4 lg + r][nb 16 t + lr]
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int ka = 16 * c + 4 * lg + r;
+    if (ka >= g.Ka) continue;
+#pragma unroll
+    for (int t = 0; t < TNB; ++t) {
+      const int nb = 16 * t + lr;
+      if (nb < g.Nb) slab[(int64_t)ka * g.NC + nb] = acc[t][r] + xch[((c * TNB + t) * 4 + r) * 64 + lane];
+    }
+  }
+}
+
+__global__ __launch_bounds__(WS_THREADS) void wgrad_stream_kernel(WsArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int i = wg_find(g.wg0, g.np, blockIdx.x);
+  const WsProb& p = g.p[i];
+  const int split = blockIdx.x - g.wg0[i];
+  const int64_t total = g.offsets[g.B];
+  switch (p.tnb) {
+    case 4: ws_body<4>(p, total, split, smem); break;
+    case 8: ws_body<8>(p, total, split, smem); break;
+    case 13: ws_body<13>(p, total, split, smem); break;
+    default: ws_body<16>(p, total, split, smem); break;
+  }
+}
+
+// out = sum over a problem's splits in split order: thread (o, grp) of a 256-thread block
+// sums splits grp, grp + 16, ... of output o, then the 16 partials are added in grp order
+__global__ __launch_bounds__(256) void ws_reduce_kernel(WsArgs g) {
+  __shared__ float part[16][17];
+  const int pi = wg_find(g.blk0, g.np, blockIdx.x);
+  const WsProb& p = g.p[pi];
+  const int blk = blockIdx.x - g.blk0[pi];
+  const int64_t ne = (int64_t)p.Ka * p.NC;
+  const int o = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const int64_t i = (int64_t)blk * 16 + o;
+  const int64_t ic = i < ne ? i : ne - 1;
+  gptr<float> src = as_global(p.slabs);
+  float acc = 0.f;
+  int j = grp;
+  for (; j + 112 < p.splits; j += 128) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = src[(int64_t)(j + 16 * u) * ne + ic];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc += v[u];
+  }
+  for (; j < p.splits; j += 16) acc += src[(int64_t)j * ne + ic];
+  part[grp][o] = acc;
+  __syncthreads();
+  if (grp == 0 && i < ne) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += part[k][o];
+    const int ka = (int)(i / p.NC), nb = (int)(i - (int64_t)ka * p.NC);
+    if (nb < p.Nb) p.c[(int64_t)ka * p.Nb + nb] = s;
+    else if (p.colsum) p.colsum[ka] = s;
+  }
+}
+
+static int ws_tnb(int nb) {
+  const int t = ceil_div(nb, 16);
+  return t <= 4 ? 4 : t <= 8 ? 8 : t <= 13 ? 13 : 16;
+}
+static bool ws_fits(const int* Ka, const int* Nb, int np) {
+  for (int i = 0; i < np; ++i)
+    if (Ka[i] > 0 && (Ka[i] > 64 || Nb[i] > 16 * WS_MAXTNB)) return false;
+  return true;
+}
+static size_t ws_lds(int tnb) { return sizeof(float) * (4 * (size_t)tnb * 4 * 64 + 4 * 16); }
+
+struct WsPlan {
+  int splits[WG_MAXP];
+  size_t slab_bytes[WG_MAXP];
+  size_t need;
+};
+// splits per problem proportional to its nb-tiles, ~one workgroup per CU in total, each
+// split >= 64 rows
+static WsPlan ws_plan(int64_t max_rows, const int* Ka, const int* Nb, int np) {
+  WsPlan pl{};
+  int tsum = 0;
+  for (int i = 0; i < np; ++i)
+    if (Ka[i] > 0) tsum += ws_tnb(Nb[i]);
+  const int G = device_cus();
+  const int64_t cap = std::max<int64_t>(1, (max_rows + 63) / 64);
+  for (int i = 0; i < np; ++i) {
+    if (Ka[i] <= 0) continue;
+    int64_t s = ((int64_t)G * ws_tnb(Nb[i]) + tsum / 2) / std::max(tsum, 1);
+    s = std::max<int64_t>(1, std::min(s, cap));
+    pl.splits[i] = (int)s;
+    pl.slab_bytes[i] = sizeof(float) * (size_t)s * Ka[i] * (Nb[i] + 1);
+    pl.need += (pl.slab_bytes[i] + 255) & ~(size_t)255;
+  }
+  return pl;
+}
+
+static int wgrad_run_stream(const WgradProb* in, int np, const int64_t* offsets, int B,
+                            int64_t max_rows, void* workspace, size_t ws_bytes, hipStream_t st) {
+  int Ka[WG_MAXP], Nb[WG_MAXP];
+  for (int i = 0; i < np; ++i) {
+    Ka[i] = in[i].a ? in[i].Ka : 0;
+    Nb[i] = in[i].a ? in[i].Nb : 0;
+  }
+  const WsPlan pl = ws_plan(max_rows, Ka, Nb, np);
+  GR_REQUIRE(workspace && ws_bytes >= pl.need, "gr_wgrad: workspace %zu B < %zu B", ws_bytes, pl.need);
+  WsArgs g{};
+  g.offsets = offsets;
+  g.B = B;
+  g.np = 0;
+  char* ws = (char*)workspace;
+  size_t off = 0, lds = 0;
+  g.wg0[0] = g.blk0[0] = 0;
+  for (int i = 0; i < np; ++i) {
+    if (Ka[i] <= 0) continue;
+    WsProb& p = g.p[g.np];
+    p.a = in[i].a;
+    p.lda = in[i].lda;
+    p.a_stats = in[i].a_stats;
+    p.bm = in[i].bm;
+    p.ldb = in[i].ldb;
+    p.Ka = Ka[i];
+    p.Nb = Nb[i];
+    p.NC = Nb[i] + 1;
+    p.tnb = ws_tnb(Nb[i]);
+    p.splits = pl.splits[i];
+    p.slabs = (float*)(ws + off);
+    off += (pl.slab_bytes[i] + 255) & ~(size_t)255;
+    p.c = in[i].c;
+    p.colsum = in[i].colsum;
+    lds = std::max(lds, ws_lds(p.tnb));
+    g.wg0[g.np + 1] = g.wg0[g.np] + p.splits;
+    g.blk0[g.np + 1] = g.blk0[g.np] + (int)(((int64_t)p.Ka * p.NC + 15) / 16);
+    ++g.np;
+  }
+  if (g.np == 0) return 0;
+  GR_TIMED("wgrad_partial", st, hipLaunchKernelGGL(wgrad_stream_kernel, dim3(g.wg0[g.np]), dim3(WS_THREADS), lds, st, g));
+  GR_LAUNCH_CHECK("gr_wgrad(stream)");
+  GR_TIMED("wgrad_reduce", st, hipLaunchKernelGGL(ws_reduce_kernel, dim3(g.blk0[g.np]), dim3(256), 0, st, g));
+  GR_LAUNCH_CHECK("gr_wgrad(stream reduce)");
+  return 0;
+}
+
+// workspace of a problem list: the largest of the narrow, streaming and (when it may be
+// taken) wide plans
 static size_t wgrad_ws_need(const int* Ka, const int* Nb, int np, int64_t max_rows) {
   size_t need = wgrad_plan(max_rows, Ka, Nb, np).need;
   int kmax = 0;
   for (int i = 0; i < np; ++i) kmax = std::max(kmax, Ka[i]);
   if (kmax <= WGW_T) need = std::max(need, wgrad_plan_wide(max_rows, Ka, Nb, np).need);
+  if (ws_fits(Ka, Nb, np)) need = std::max(need, ws_plan(max_rows, Ka, Nb, np).need);
   return need;
 }
 

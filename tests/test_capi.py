@@ -156,9 +156,10 @@ def test_launch_options_are_explicit_not_environment():
                          "MIPS_FORCE_FALLBACK", "ATTN_BWD_SPLIT", "ROWWAVE", "ATTN_BWD_PAIRS",
                          "ATTN_BWD_DS", "DETERMINISTIC", "WGRAD_ROWS", "PANEL_VEC",
                          "ATTN_BWD_WIDE_DS", "ATTN_BWD_WIDE_SPLIT", "MIPS_FILTER_PAIRED",
-                         "MIPS_SAMPLE_STRIDE"}
+                         "MIPS_SAMPLE_STRIDE", "WGRAD_STREAM"}
     defaults = {"ROWWAVE": 1, "ATTN_BWD_PAIRS": 1, "PANEL_VEC": 1, "ATTN_BWD_DS": 1,
-                "ATTN_BWD_WIDE_DS": 1, "ATTN_BWD_WIDE_SPLIT": 0, "MIPS_FILTER_PAIRED": 1}
+                "ATTN_BWD_WIDE_DS": 1, "ATTN_BWD_WIDE_SPLIT": 0, "MIPS_FILTER_PAIRED": 1,
+                "WGRAD_STREAM": 1}
     for n in opts:
         assert _lib.get_option(n) == defaults.get(n, 0), n
     with _lib.option("ATTN_BWD_SPLIT", 1):

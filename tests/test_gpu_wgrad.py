@@ -56,10 +56,20 @@ def _check(got, ref, what):
     assert err <= 1e-5 * scale, (what, err, scale)
 
 
+@pytest.mark.parametrize("stream", [1, 0])
 @pytest.mark.parametrize("Ka,Nb", [(50, 200), (256, 1024), (256, 256), (64, 64), (33, 17),
-                                   (256, 257), (128, 128)])
-def test_wgrad_single_with_colsum(Ka, Nb):
+                                   (256, 257), (128, 128), (16, 250), (64, 256), (50, 1)])
+def test_wgrad_single_with_colsum(Ka, Nb, stream):
+    """stream = GR_OPT_WGRAD_STREAM (Ka <= 64, Nb <= 256: the streaming form or the
+    LDS-staged panels; other shapes ignore it)."""
     L = _lib()
+    if stream == 0 and (Ka > 64 or Nb > 256):
+        pytest.skip("the option only selects among the narrow forms")
+    with L.option("WGRAD_STREAM", stream):
+        _single_with_colsum(L, Ka, Nb)
+
+
+def _single_with_colsum(L, Ka, Nb):
     offs, total, cap, a, b, st = _case([700, 1, 333, 64, 1000], Ka, Nb, Ka + Nb)
     lib = L.lib()
     ws_n = lib.gr_wgrad_workspace_size(cap, Ka, Nb)
