@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GR_HSTU_ABI_VERSION 13
+#define GR_HSTU_ABI_VERSION 14
 
 #ifndef GR_API
 #define GR_API __attribute__((visibility("default")))
@@ -110,6 +110,9 @@ GR_API int gr_timing_reset(void);
  *                                  fragments, one workgroup per (problem, row split), splits
  *                                  per problem by MFMA work) or the LDS-staged panels (0).
  *                                  Workspace queries cover both forms.
+ *   GR_OPT_BOUNDARY_FUSE      0|1  hstu_attn_bwd_bnd: the layer boundary as the epilogue of
+ *                                  the dQ launch where the shapes allow (default 1), or the
+ *                                  attention backward and the boundary as separate calls (0)
  */
 enum {
   GR_OPT_MIPS_FILTER_FP32 = 1,
@@ -128,7 +131,8 @@ enum {
   GR_OPT_MIPS_FILTER_PAIRED = 14,
   GR_OPT_MIPS_SAMPLE_STRIDE = 15,
   GR_OPT_WGRAD_STREAM = 16,
-  GR_OPT_COUNT_ = 17
+  GR_OPT_BOUNDARY_FUSE = 17,
+  GR_OPT_COUNT_ = 18
 };
 GR_API int gr_set_option(int option, int64_t value);
 GR_API int64_t gr_get_option(int option);
@@ -492,6 +496,58 @@ GR_API int hstu_boundary_bwd(const float* dh, int64_t ld_dh, const int64_t* offs
                     const float* h_u, int64_t ld_h, float dropout_p, uint64_t seed,
                     const int64_t* seed_offset, float* du, int64_t ld_du, float* d_attn,
                     int64_t ld_da, void* stream);
+
+/* ABI 14: the attention backward of layer l followed by its layer boundary, i.e.
+ * hstu_attn_bwd(...) then hstu_boundary_bwd(bnd...) (or, with bnd->hdv == 0 for the first
+ * layer, hstu_ln_uvqk_bwd(bnd...)) in one call.  At narrow single-head shapes (H == 1,
+ * dqk, dv <= 64, N <= 512 with a bucket map and the dS workspace; D, h dv <= 64,
+ * n_out <= 256) the boundary runs as the epilogue of the dQ launch: each 16-query block's
+ * wave, once its dq rows are stored, runs the row-wave boundary unit of those 16 rows
+ * (d_uvqk of the rows is then complete: du from the previous boundary, dk / dv from the
+ * dK/dV launch, dq just stored) -- one launch and one re-read of the rows fewer.
+ * Otherwise the two calls run as they are.  `bnd` holds the boundary call's arguments
+ * (dh = the d_uvqk the attention writes into, stride ld_dh = n_out); results equal the
+ * two calls' (the fused epilogue is the row-wave unit of hstu_boundary_bwd; the first
+ * layer's hstu_ln_uvqk_bwd alone may take the row panel: fp32 summation order). */
+typedef struct GrBoundaryBwd {
+  const float* dh;
+  int64_t ld_dh;
+  int64_t max_rows;
+  int D;
+  int n_out;
+  const float* w_uvqk;
+  const float* x;
+  int64_t ld_x;
+  const float* x_stats;
+  const float* dy_res;
+  int64_t ld_dy;
+  float* dx;
+  int64_t ld_dx;
+  int hdv;              /* 0: no gate_o backward of a previous layer (the first layer) */
+  const float* w_o;
+  const float* u;
+  int64_t ld_u;
+  const float* attn;
+  int64_t ld_attn;
+  const float* attn_stats;
+  const float* h_u;
+  int64_t ld_h;
+  float dropout_p;
+  uint64_t seed;
+  const int64_t* seed_offset;
+  float* du;
+  int64_t ld_du;
+  float* d_attn;
+  int64_t ld_da;
+} GrBoundaryBwd;
+GR_API int hstu_attn_bwd_bnd(const float* q, const float* k, const float* v, int64_t ld_qk,
+                    int64_t ld_v, const float* dout, int64_t ld_dout, const int64_t* offsets,
+                    int B, int N, int max_len, int H, int dqk, int dv,
+                    const uint8_t* bucket_map, const float* pos_w, const float* ts_w,
+                    int num_buckets, const float* hq, const float* hk, const float* hv,
+                    int64_t ld_h, float* dq, float* dk, float* dv_out, int64_t ld_d,
+                    float* dpos_w, float* dts_w, void* workspace, size_t ws_bytes,
+                    const GrBoundaryBwd* bnd, void* stream);
 
 /* gr_wgrad: weight gradient C = A'^T B over all jagged rows (replaces the mm-backward
  * of hstu.py:303 and of the _o Linear at hstu.py:404-411):

@@ -23,7 +23,7 @@ void set_error(const char* fmt, ...) {
 const char* last_error() { return g_err.c_str(); }
 
 // ---------------------------------------------------------------- launch options
-static std::atomic<int64_t> g_opt[GR_OPT_COUNT_] = {0, 0, 0, 0, 0, 0, 1, 1, 1, 0, 0, 1, 1, 0, 1, 0, 1};
+static std::atomic<int64_t> g_opt[GR_OPT_COUNT_] = {0, 0, 0, 0, 0, 0, 1, 1, 1, 0, 0, 1, 1, 0, 1, 0, 1, 1};
 
 int64_t option(int which) { return g_opt[which].load(std::memory_order_relaxed); }
 

@@ -18,6 +18,7 @@
 // multiplied by silu'(h) of the UVQK pre-activation (hstu.py:303-305), so the caller
 // gets d(pre-activation) directly.
 #include "attn_common.h"
+#include "rowwave.h"
 
 #include "../../include/gr_hstu.h"
 
@@ -1000,19 +1001,28 @@ __device__ __forceinline__ void bias_grad_reduce_body(const float* slabs, int n_
 // the last one of the walk re-read it with a zero A operand (+0 to every sum), so the
 // loads stay unconditional.  The MFMA sequence (key blocks ascending, k-step r = keys
 // 4g + r) is the recomputing pass's: dQ is bit-identical to it.
+// Returns false for an item past the sequence; otherwise the block's first query q0, the
+// sequence's first row s0 and length L (the layer-boundary epilogue, hstu_attn_bwd_bnd).
 template <int KSTEPS, int VTILES>
-__device__ __forceinline__ void attn_bwd_dq_wave_body(const AttnBwdArgs& a, const int item) {
+__device__ __forceinline__ bool attn_bwd_dq_wave_body(const AttnBwdArgs& a, const int item,
+                                                      int* q0_out = nullptr, int* L_out = nullptr,
+                                                      int64_t* s0_out = nullptr) {
   using C = AttnBwdCfg<KSTEPS, VTILES, 64>;
   constexpr int KT = C::KT, PD = 4;
   const int BH = a.B * a.H;
   const int qb = a.n_tiles * 4 - 1 - item / BH;  // heaviest blocks first
   const int bh = item % BH;
-  if (qb < 0) return;
+  if (qb < 0) return false;
   const int b = bh / a.H, h = bh % a.H;
   const int64_t s0 = a.offsets[b];
   const int L = (int)(a.offsets[b + 1] - s0);
   const int q0 = qb * 16;
-  if (q0 >= L) return;
+  if (q0 >= L) return false;
+  if (q0_out) {
+    *q0_out = q0;
+    *L_out = L;
+    *s0_out = s0;
+  }
   const int lane = threadIdx.x & 63, lr = lane & 15, lg = lane >> 4;
   const __amdgpu_buffer_rsrc_t rk = seq_rsrc(a.k, a.ld_qk, s0, h * a.dqk, L, a.dqk);
   const float* dsq = a.ds + ((int64_t)bh * a.ds_tps + qb * (qb + 1) / 2) * 256 + lr * 16 + 4 * lg;
@@ -1054,6 +1064,7 @@ __device__ __forceinline__ void attn_bwd_dq_wave_body(const AttnBwdArgs& a, cons
   store_scaled<4, KT>([&](int i, int t) { return dQ[t][i]; }, L, a.dqk, s0, a.dq, a.ld_d, a.hq,
                       a.ld_h, h * a.dqk, [&](int i) { return q0 + 4 * lg + i; },
                       [&](int t) { return 16 * t + lr; });
+  return true;
 }
 
 // dQ = dS K; the first n_bias workgroups reduce the bias slabs the dK/dV launch wrote (no
@@ -1074,6 +1085,80 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_ds_kernel(AttnBwdArgs a, int 
     else attn_bwd_dq_ds_body<KSTEPS, VTILES, TT, false>(a, id);
   }
 }
+// dQ = dS K with the layer boundary as its epilogue (hstu_attn_bwd_bnd, H == 1): the
+// workgroup stages the boundary's weight panels (ln_uvqk_bwd's W_uvqk^T, gate_o_bwd's W_o)
+// in LDS, each wave computes and stores the dq rows of its 16-query block, then -- the
+// rows' d_uvqk now complete -- runs the row-wave boundary unit of those 16 rows (rows past
+// the sequence fall outside the ops' descriptors).  OP2 = false: the first layer, whose
+// boundary is ln_uvqk_bwd alone.  The first n_bias workgroups reduce the bias slabs.
+template <int KSTEPS, int VTILES, int KG1, int W, bool OP2>
+__global__ __launch_bounds__(256) void attn_bwd_dq_bnd_kernel(AttnBwdArgs a, int n_bias, int n_slabs,
+                                                              float* dpos_w, float* dts_w,
+                                                              RwLnUvqkBwd<KG1, W, 2> op1,
+                                                              RwGateOBwd<W, W, 2> op2) {
+  using C1 = RowWaveCfg<KG1, W>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* W1 = reinterpret_cast<float*>(smem);
+  float* W2 = W1 + C1::KP * C1::LDW;
+  const int id = (int)blockIdx.x - n_bias;
+  if (id < 0) {
+    bias_grad_reduce_body(a.slabs, n_slabs, 2 * a.N - 1, a.nb + 1, dpos_w, dts_w, (int)blockIdx.x);
+    return;
+  }
+  rw_stage_w<KG1, W>(op1, W1);
+  if constexpr (OP2) rw_stage_w<W, W>(op2, W2);
+  int q0 = 0, L = 0;
+  int64_t s0 = 0;
+  const bool live = attn_bwd_dq_wave_body<KSTEPS, VTILES>(a, id * 4 + wave_id(), &q0, &L, &s0);
+  __syncthreads();  // the panels are staged (every wave reaches this, live or not)
+  if (!live) return;
+  // this wave's dq stores have landed before its unit reads the rows back (the rows' other
+  // columns were written by earlier launches; no other wave writes these rows)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  op1.setup(s0 + L);
+  if constexpr (OP2) op2.setup(s0 + L);
+  const int lane = threadIdx.x & 63, lr = lane & 15, lg = lane >> 4;
+  const int64_t m = s0 + q0 + lr;
+  const bool ok = q0 + lr < L;
+  if constexpr (OP2) rw2_unit<KG1, W, W>(op1, op2, W1, W2, m, ok, lr, lg);
+  else rw1_unit<KG1, W>(op1, W1, m, ok, lr, lg);
+}
+
+// the boundary of hstu_attn_bwd_bnd as the dQ launch's epilogue (see attn_bwd_dq_bnd_kernel)
+struct BndCtx {
+  RwArgsLnUvqkBwd a1;
+  RwArgsGateOBwd a2;
+  bool op2;
+  int kg1;      // 13 | 16 (n_out in 16-column groups)
+  bool fused;   // set by the launch that ran it
+};
+
+template <int KS, int VT, int KG1, bool OP2>
+static int launch_dq_bnd_k(const AttnBwdArgs& aq, BndCtx& bc, int grid, int nbias, int n_slabs,
+                           float* dpos_w, float* dts_w, hipStream_t st) {
+  RwLnUvqkBwd<KG1, 4, 2> o1{};
+  RwGateOBwd<4, 4, 2> o2{};
+  bc.a1.fill(o1);
+  if (OP2) bc.a2.fill(o2);
+  const size_t lds = RowWaveCfg<KG1, 4>::LDS_BYTES + (OP2 ? RowWaveCfg<4, 4>::LDS_BYTES : 0);
+  GR_TIMED("attn_bwd_dq", st, hipLaunchKernelGGL((attn_bwd_dq_bnd_kernel<KS, VT, KG1, 4, OP2>),
+                                                 dim3(grid + nbias), dim3(256), lds, st, aq, nbias,
+                                                 n_slabs, dpos_w, dts_w, o1, o2));
+  GR_LAUNCH_CHECK("hstu_attn_bwd_bnd(dq + boundary)");
+  bc.fused = true;
+  return 0;
+}
+template <int KS, int VT>
+static int launch_dq_bnd(const AttnBwdArgs& aq, BndCtx& bc, int grid, int nbias, int n_slabs,
+                         float* dpos_w, float* dts_w, hipStream_t st) {
+  if (bc.kg1 == 13) {
+    return bc.op2 ? launch_dq_bnd_k<KS, VT, 13, true>(aq, bc, grid, nbias, n_slabs, dpos_w, dts_w, st)
+                  : launch_dq_bnd_k<KS, VT, 13, false>(aq, bc, grid, nbias, n_slabs, dpos_w, dts_w, st);
+  }
+  return bc.op2 ? launch_dq_bnd_k<KS, VT, 16, true>(aq, bc, grid, nbias, n_slabs, dpos_w, dts_w, st)
+                : launch_dq_bnd_k<KS, VT, 16, false>(aq, bc, grid, nbias, n_slabs, dpos_w, dts_w, st);
+}
+
 // One launch, dS handed over inside it: workgroups [0, grid_kv) are the key-major pass
 // (publishing each key tile's dS), the rest compute dQ = dS K as the tiles appear (a
 // workgroup that times out waiting recomputes its tile, attn_bwd_dq_body).  All key-major
@@ -1193,7 +1278,8 @@ static size_t bwd_flag_bytes(int B, int max_len, int H) {
 }
 
 template <int KS, int VT, int TT = 64>
-static int launch_bwd(const AttnBwdArgs& a, float* dpos_w, float* dts_w, hipStream_t st) {
+static int launch_bwd(const AttnBwdArgs& a, float* dpos_w, float* dts_w, hipStream_t st,
+                      BndCtx* bnd = nullptr) {
   using C = AttnBwdCfg<KS, VT, TT>;
   const int grid = a.n_tiles * a.B * a.H;
   const int nbins = 2 * a.N - 1 + a.nb + 1;
@@ -1256,6 +1342,10 @@ static int launch_bwd(const AttnBwdArgs& a, float* dpos_w, float* dts_w, hipStre
     const size_t lds_dq = TT == 64 ? 0 : sizeof(float) * TT * C::LDQ + 16;
     const int grid_dq = grid;  // TT = 64: 4 query blocks per workgroup (one 64-row tile)
     const int nbias = a.map_kq ? ceil_div(nbins, 16) : 0;  // the slab reduce rides along
+    if constexpr (TT == 64 && VT == 4 && (KS == 13 || KS == 16)) {
+      if (bnd && a.H == 1)
+        return launch_dq_bnd<KS, VT>(aq, *bnd, grid_dq, nbias, n_slabs, dpos_w, dts_w, st);
+    }
     GR_TIMED("attn_bwd_dq", st, hipLaunchKernelGGL((attn_bwd_dq_ds_kernel<KS, VT, TT>), dim3(grid_dq + nbias), dim3(256),
                                                    lds_dq, st, aq, nbias, n_slabs, dpos_w, dts_w));
     GR_LAUNCH_CHECK("hstu_attn_bwd(dq from dS)");
@@ -1319,15 +1409,15 @@ extern "C" size_t hstu_attn_bwd_workspace_size_d(int B, int N, int max_len, int 
             : gr::bwd_slab_bytes(B, N, max_len, H, num_buckets);
 }
 
-extern "C" int hstu_attn_bwd(const float* q, const float* k, const float* v, int64_t ld_qk,
-                             int64_t ld_v, const float* dout, int64_t ld_dout,
-                             const int64_t* offsets, int B, int N, int max_len, int H, int dqk,
-                             int dv, const uint8_t* bucket_map, const float* pos_w,
-                             const float* ts_w, int num_buckets, const float* hq,
-                             const float* hk, const float* hv, int64_t ld_h, float* dq,
-                             float* dk, float* dvv, int64_t ld_d, float* dpos_w, float* dts_w,
-                             void* workspace, size_t ws_bytes, void* stream) {
-  using namespace gr;
+namespace gr {
+static int attn_bwd_impl(const float* q, const float* k, const float* v, int64_t ld_qk,
+                         int64_t ld_v, const float* dout, int64_t ld_dout,
+                         const int64_t* offsets, int B, int N, int max_len, int H, int dqk,
+                         int dv, const uint8_t* bucket_map, const float* pos_w,
+                         const float* ts_w, int num_buckets, const float* hq,
+                         const float* hk, const float* hv, int64_t ld_h, float* dq,
+                         float* dk, float* dvv, int64_t ld_d, float* dpos_w, float* dts_w,
+                         void* workspace, size_t ws_bytes, void* stream, BndCtx* bnd) {
   GR_REQUIRE(q && k && v && dout && offsets && dq && dk && dvv, "hstu_attn_bwd: null pointer");
   GR_REQUIRE(B >= 0 && N > 0 && H > 0 && dqk > 0 && dv > 0, "hstu_attn_bwd: bad sizes");
   GR_REQUIRE(max_len >= 0 && max_len <= N, "hstu_attn_bwd: max_len %d not in [0, N=%d]", max_len, N);
@@ -1372,11 +1462,73 @@ extern "C" int hstu_attn_bwd(const float* q, const float* k, const float* v, int
       a.ds_flags = (uint32_t*)((char*)workspace + fo);
   }
   const int d = dqk > dv ? dqk : dv;
-  if (d <= 8) return launch_bwd<2, 1>(a, dpos_w, dts_w, st);
-  if (d <= 16) return launch_bwd<4, 1>(a, dpos_w, dts_w, st);
-  if (d <= 32) return launch_bwd<8, 2>(a, dpos_w, dts_w, st);
-  if (d <= 52) return launch_bwd<13, 4>(a, dpos_w, dts_w, st);
-  if (d <= 64) return launch_bwd<16, 4>(a, dpos_w, dts_w, st);
-  if (d <= 128) return launch_bwd<32, 8>(a, dpos_w, dts_w, st);
-  return launch_bwd<64, 16, 16>(a, dpos_w, dts_w, st);
+  if (d <= 8) return launch_bwd<2, 1>(a, dpos_w, dts_w, st, bnd);
+  if (d <= 16) return launch_bwd<4, 1>(a, dpos_w, dts_w, st, bnd);
+  if (d <= 32) return launch_bwd<8, 2>(a, dpos_w, dts_w, st, bnd);
+  if (d <= 52) return launch_bwd<13, 4>(a, dpos_w, dts_w, st, bnd);
+  if (d <= 64) return launch_bwd<16, 4>(a, dpos_w, dts_w, st, bnd);
+  if (d <= 128) return launch_bwd<32, 8>(a, dpos_w, dts_w, st, bnd);
+  return launch_bwd<64, 16, 16>(a, dpos_w, dts_w, st, bnd);
+}
+}  // namespace gr
+
+extern "C" int hstu_attn_bwd(const float* q, const float* k, const float* v, int64_t ld_qk,
+                             int64_t ld_v, const float* dout, int64_t ld_dout,
+                             const int64_t* offsets, int B, int N, int max_len, int H, int dqk,
+                             int dv, const uint8_t* bucket_map, const float* pos_w,
+                             const float* ts_w, int num_buckets, const float* hq,
+                             const float* hk, const float* hv, int64_t ld_h, float* dq,
+                             float* dk, float* dvv, int64_t ld_d, float* dpos_w, float* dts_w,
+                             void* workspace, size_t ws_bytes, void* stream) {
+  return gr::attn_bwd_impl(q, k, v, ld_qk, ld_v, dout, ld_dout, offsets, B, N, max_len, H, dqk, dv,
+                           bucket_map, pos_w, ts_w, num_buckets, hq, hk, hv, ld_h, dq, dk, dvv, ld_d,
+                           dpos_w, dts_w, workspace, ws_bytes, stream, nullptr);
+}
+
+extern "C" int hstu_attn_bwd_bnd(const float* q, const float* k, const float* v, int64_t ld_qk,
+                                 int64_t ld_v, const float* dout, int64_t ld_dout,
+                                 const int64_t* offsets, int B, int N, int max_len, int H, int dqk,
+                                 int dv, const uint8_t* bucket_map, const float* pos_w,
+                                 const float* ts_w, int num_buckets, const float* hq,
+                                 const float* hk, const float* hv, int64_t ld_h, float* dq,
+                                 float* dk, float* dvv, int64_t ld_d, float* dpos_w, float* dts_w,
+                                 void* workspace, size_t ws_bytes, const GrBoundaryBwd* bnd,
+                                 void* stream) {
+  using namespace gr;
+  GR_REQUIRE(bnd, "hstu_attn_bwd_bnd: null boundary");
+  const GrBoundaryBwd& g = *bnd;
+  GR_REQUIRE(g.dh && g.w_uvqk && g.x && g.x_stats && g.dx && g.D > 0 && g.n_out > 0,
+             "hstu_attn_bwd_bnd: boundary null pointer or bad sizes");
+  GR_REQUIRE(g.hdv == 0 || (g.w_o && g.u && g.attn && g.attn_stats && g.du && g.d_attn),
+             "hstu_attn_bwd_bnd: gate_o backward null pointer");
+  // the epilogue form: narrow single-head boundary shapes the row-wave ops instantiate
+  BndCtx bc{};
+  bc.a1 = RwArgsLnUvqkBwd{offsets, B, g.n_out, g.D, g.dh, g.ld_dh, g.w_uvqk, g.x, g.ld_x,
+                          (const float2*)g.x_stats, g.dy_res, g.ld_dy, g.dx, g.ld_dx};
+  bc.op2 = g.hdv > 0;
+  if (bc.op2)
+    bc.a2 = RwArgsGateOBwd{offsets, B, g.D, g.hdv, g.dx, g.ld_dx, g.w_o, g.u, g.ld_u, g.attn,
+                           g.ld_attn, (const float2*)g.attn_stats, g.h_u, g.ld_h, g.dropout_p,
+                           g.seed, g.seed_offset, g.du, g.ld_du, g.d_attn, g.ld_da};
+  const int ng = ceil_div(g.n_out, 16);
+  bc.kg1 = ng > 8 && ng <= 13 ? 13 : ng > 13 && ng <= 16 ? 16 : -1;
+  auto in_w4 = [](int x) { return x > 32 && x <= 64; };  // the W = 4 (64-column) instantiation
+  const bool aligned = pair_aligned({g.dh, g.x, g.dy_res, g.dx, g.u, g.attn, g.h_u, g.du, g.d_attn},
+                                    {g.ld_dh, g.ld_x, g.ld_dy, g.ld_dx, g.ld_u, g.ld_attn, g.ld_h,
+                                     g.ld_du, g.ld_da, g.n_out, g.D, g.hdv});
+  const bool fuse = option(GR_OPT_BOUNDARY_FUSE) != 0 && option(GR_OPT_ROWWAVE) != 0 && H == 1 &&
+                    bc.kg1 > 0 && in_w4(g.D) && (!bc.op2 || in_w4(g.hdv)) && aligned &&
+                    g.max_rows * 4 * 1024 <= 0x7fffffffLL;
+  if (int rc = attn_bwd_impl(q, k, v, ld_qk, ld_v, dout, ld_dout, offsets, B, N, max_len, H, dqk, dv,
+                             bucket_map, pos_w, ts_w, num_buckets, hq, hk, hv, ld_h, dq, dk, dvv,
+                             ld_d, dpos_w, dts_w, workspace, ws_bytes, stream, fuse ? &bc : nullptr))
+    return rc;
+  if (bc.fused) return 0;
+  if (g.hdv > 0)
+    return hstu_boundary_bwd(g.dh, g.ld_dh, offsets, B, g.max_rows, g.D, g.n_out, g.w_uvqk, g.x,
+                             g.ld_x, g.x_stats, g.dy_res, g.ld_dy, g.dx, g.ld_dx, g.hdv, g.w_o, g.u,
+                             g.ld_u, g.attn, g.ld_attn, g.attn_stats, g.h_u, g.ld_h, g.dropout_p,
+                             g.seed, g.seed_offset, g.du, g.ld_du, g.d_attn, g.ld_da, stream);
+  return hstu_ln_uvqk_bwd(g.dh, g.ld_dh, offsets, B, g.max_rows, g.D, g.n_out, g.w_uvqk, g.x, g.ld_x,
+                          g.x_stats, g.dy_res, g.ld_dy, g.dx, g.ld_dx, stream);
 }

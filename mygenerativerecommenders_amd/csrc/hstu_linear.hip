@@ -1062,43 +1062,6 @@ static int rw_dispatch(const Args& a, int K, int N, int vec, int64_t max_rows, c
   return rw_kg<2, OpT>(a, kg, nt, max_rows, tname, st);
 }
 
-struct RwArgsLnUvqk {
-  const int64_t* offsets; int B, K, N; const float* x; int64_t ldx; const float* w; float eps;
-  int act; float2* x_stats; float* h_pre; float* out; int64_t ld_out;
-  template <class Op> void fill(Op& o) const {
-    o.offsets = offsets; o.B = B; o.K = K; o.N = N; o.x = x; o.ldx = ldx; o.w = w; o.eps = eps;
-    o.act = act; o.x_stats = x_stats; o.h_pre = h_pre; o.out = out; o.ld_out = ld_out;
-  }
-};
-struct RwArgsGateO {
-  const int64_t* offsets; int B, K, N; const float* u; int64_t ldu; const float* attn; int64_t lda;
-  const float* w; const float* bias; const float* xres; int64_t ldx; float eps, p; uint64_t seed;
-  const int64_t* seed_off; float2* a_stats; float* o_in; float* y; int64_t ldy;
-  template <class Op> void fill(Op& o) const {
-    o.offsets = offsets; o.B = B; o.K = K; o.N = N; o.u = u; o.ldu = ldu; o.attn = attn; o.lda = lda;
-    o.w = w; o.bias = bias; o.xres = xres; o.ldx = ldx; o.eps = eps; o.p = p; o.seed = seed;
-    o.seed_off = seed_off; o.a_stats = a_stats; o.o_in = o_in; o.y = y; o.ldy = ldy;
-  }
-};
-struct RwArgsGateOBwd {
-  const int64_t* offsets; int B, K, N; const float* dy; int64_t lddy; const float* w; const float* u;
-  int64_t ldu; const float* attn; int64_t lda; const float2* a_stats; const float* h_u; int64_t ldh;
-  float p; uint64_t seed; const int64_t* seed_off; float* du; int64_t lddu; float* da; int64_t ldda;
-  template <class Op> void fill(Op& o) const {
-    o.offsets = offsets; o.B = B; o.K = K; o.N = N; o.dy = dy; o.lddy = lddy; o.w = w; o.u = u;
-    o.ldu = ldu; o.attn = attn; o.lda = lda; o.a_stats = a_stats; o.h_u = h_u; o.ldh = ldh; o.p = p;
-    o.seed = seed; o.seed_off = seed_off; o.du = du; o.lddu = lddu; o.da = da; o.ldda = ldda;
-  }
-};
-struct RwArgsLnUvqkBwd {
-  const int64_t* offsets; int B, K, N; const float* dh; int64_t lddh; const float* w; const float* x;
-  int64_t ldx; const float2* x_stats; const float* dy; int64_t lddy; float* dx; int64_t lddx;
-  template <class Op> void fill(Op& o) const {
-    o.offsets = offsets; o.B = B; o.K = K; o.N = N; o.dh = dh; o.lddh = lddh; o.w = w; o.x = x;
-    o.ldx = ldx; o.x_stats = x_stats; o.dy = dy; o.lddy = lddy; o.dx = dx; o.lddx = lddx;
-  }
-};
-
 // concat_ua row-wave launches (KG / NT = 3 segments of KGH 16-column groups)
 template <class Op, int KG, int NT>
 static int rw_launch_op(const Op& op, int64_t max_rows, const char* tname, hipStream_t st) {

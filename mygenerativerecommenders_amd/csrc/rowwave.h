@@ -931,4 +931,86 @@ struct RwLnUvqkBwd {
   }
 };
 
+// ------------------------------------------------------------------ one unit, callable
+// One 16-row unit of rowwave2_kernel's loop (rows m = the lane's row, ok = its validity)
+// for kernels that run a layer boundary as the epilogue of other work (the attention
+// backward's dQ pass, hstu_attn_bwd_bnd): the panels W1 / W2 are staged (rw_stage_w) and
+// the ops set up (setup(row_end): rows >= row_end read 0, their stores are dropped).  Same
+// arithmetic as the rowwave2_kernel unit, so results are bit-identical to it.
+template <int KG1, int NT1, int NT2, class Op1, class Op2>
+__device__ __forceinline__ void rw2_unit(const Op1& op1, const Op2& op2, const float* W1,
+                                         const float* W2, int64_t m, bool ok, int lr, int lg) {
+  constexpr int VEC = Op1::VEC;
+  typename Op1::Src cur;
+  op1.load(cur, m, lg);
+  float a1[KG1][4];
+  op1.prep(cur, a1, m, ok, lg);
+  typename Op1::Epi es1;
+  op1.epi_load(es1, m, ok, lg);
+  typename Op2::Epi es2;
+  op2.epi_load(es2, m, ok, lg);
+  f4 acc1[NT1];
+  rw_mma<KG1, NT1, VEC>(W1, a1, acc1, lr, lg);
+  typename Op2::Src s2;
+  op1.epi(acc1, es1, m, ok, lg, s2.v);
+  float a2[NT1][4];
+  op2.prep(s2, a2, m, ok, lg);
+  f4 acc2[NT2];
+  rw_mma<NT1, NT2, VEC>(W2, a2, acc2, lr, lg);
+  op2.epi(acc2, es2, m, ok, lg);
+}
+// the same for one op (rowwave_kernel's unit)
+template <int KG, int NT, class Op>
+__device__ __forceinline__ void rw1_unit(const Op& op, const float* Wl, int64_t m, bool ok, int lr,
+                                         int lg) {
+  constexpr int VEC = Op::VEC;
+  typename Op::Src cur;
+  op.load(cur, m, lg);
+  float a[KG][4];
+  op.prep(cur, a, m, ok, lg);
+  typename Op::Epi es;
+  op.epi_load(es, m, ok, lg);
+  f4 acc[NT];
+  rw_mma<KG, NT, VEC>(Wl, a, acc, lr, lg);
+  op.epi(acc, es, m, ok, lg);
+}
+
+// ------------------------------------------------------------------ host-side op arguments
+struct RwArgsLnUvqk {
+  const int64_t* offsets; int B, K, N; const float* x; int64_t ldx; const float* w; float eps;
+  int act; float2* x_stats; float* h_pre; float* out; int64_t ld_out;
+  template <class Op> void fill(Op& o) const {
+    o.offsets = offsets; o.B = B; o.K = K; o.N = N; o.x = x; o.ldx = ldx; o.w = w; o.eps = eps;
+    o.act = act; o.x_stats = x_stats; o.h_pre = h_pre; o.out = out; o.ld_out = ld_out;
+  }
+};
+struct RwArgsGateO {
+  const int64_t* offsets; int B, K, N; const float* u; int64_t ldu; const float* attn; int64_t lda;
+  const float* w; const float* bias; const float* xres; int64_t ldx; float eps, p; uint64_t seed;
+  const int64_t* seed_off; float2* a_stats; float* o_in; float* y; int64_t ldy;
+  template <class Op> void fill(Op& o) const {
+    o.offsets = offsets; o.B = B; o.K = K; o.N = N; o.u = u; o.ldu = ldu; o.attn = attn; o.lda = lda;
+    o.w = w; o.bias = bias; o.xres = xres; o.ldx = ldx; o.eps = eps; o.p = p; o.seed = seed;
+    o.seed_off = seed_off; o.a_stats = a_stats; o.o_in = o_in; o.y = y; o.ldy = ldy;
+  }
+};
+struct RwArgsGateOBwd {
+  const int64_t* offsets; int B, K, N; const float* dy; int64_t lddy; const float* w; const float* u;
+  int64_t ldu; const float* attn; int64_t lda; const float2* a_stats; const float* h_u; int64_t ldh;
+  float p; uint64_t seed; const int64_t* seed_off; float* du; int64_t lddu; float* da; int64_t ldda;
+  template <class Op> void fill(Op& o) const {
+    o.offsets = offsets; o.B = B; o.K = K; o.N = N; o.dy = dy; o.lddy = lddy; o.w = w; o.u = u;
+    o.ldu = ldu; o.attn = attn; o.lda = lda; o.a_stats = a_stats; o.h_u = h_u; o.ldh = ldh; o.p = p;
+    o.seed = seed; o.seed_off = seed_off; o.du = du; o.lddu = lddu; o.da = da; o.ldda = ldda;
+  }
+};
+struct RwArgsLnUvqkBwd {
+  const int64_t* offsets; int B, K, N; const float* dh; int64_t lddh; const float* w; const float* x;
+  int64_t ldx; const float2* x_stats; const float* dy; int64_t lddy; float* dx; int64_t lddx;
+  template <class Op> void fill(Op& o) const {
+    o.offsets = offsets; o.B = B; o.K = K; o.N = N; o.dh = dh; o.lddh = lddh; o.w = w; o.x = x;
+    o.ldx = ldx; o.x_stats = x_stats; o.dy = dy; o.lddy = lddy; o.dx = dx; o.lddx = lddx;
+  }
+};
+
 }  // namespace gr

@@ -856,7 +856,7 @@ static WgPlan wgrad_plan_wide(int64_t max_rows, const int* Ka, const int* Nb, in
   return pl;
 }
 
-static bool ws_fits(const int* Ka, const int* Nb, int np);
+static bool ws_fits(const WgradProb* in, int np);
 static int wgrad_run_stream(const WgradProb* in, int np, const int64_t* offsets, int B,
                             int64_t max_rows, void* workspace, size_t ws_bytes, hipStream_t st);
 
@@ -877,7 +877,7 @@ static int wgrad_run(const WgradProb* in, int np, const int64_t* offsets, int B,
     return 0;
   }
   // f32 at Ka <= 64, Nb <= 256: the streaming form (GR_OPT_WGRAD_STREAM, default on)
-  if (!bf16 && option(GR_OPT_WGRAD_STREAM) != 0 && ws_fits(Ka, Nb, np))
+  if (!bf16 && option(GR_OPT_WGRAD_STREAM) != 0 && ws_fits(in, np))
     return wgrad_run_stream(in, np, offsets, B, max_rows, workspace, ws_bytes, st);
   const bool wide = wgrad_wide_ok(in, np);
   const WgPlan pl = wide ? wgrad_plan_wide(max_rows, Ka, Nb, np) : wgrad_plan(max_rows, Ka, Nb, np);
@@ -949,21 +949,29 @@ static int wgrad_run(const WgradProb* in, int np, const int64_t* offsets, int B,
 }
 
 // ---------------------------------------------------------------- narrow streaming form
-// Ka <= 64, Nb <= 256, f32 (ml-1m: per layer _uvqk 50 x 200 over LN(x) rows and _o 50 x 50
-// over dy rows, 8 problems per encoder backward).  No LDS staging: a lane loads its MFMA
-// operands straight from the row-major operands (A fragment: row 4s + lane/16, column
-// 16c + lane%16; B fragment: the same row, column 16t + lane%16 — four 64-byte row
-// segments per wave instruction), WS_DEPTH k-steps (4 rows each) in flight per wave.
-// Workgroup = one (problem, row split), 8 waves: wave w owns ka-tile c = w & 3 against
-// every nb-tile of the problem, over the k-steps of parity h = w >> 2.  The two parities
-// meet in LDS (h0 + h1) and the workgroup writes one slab; ws_reduce sums each problem's
-// slabs in split order.  Splits per problem are proportional to its nb-tiles (its MFMA
-// time per row), ~one workgroup per CU over the launch, so every workgroup streams about
-// the same MFMA work and the grid is one round.  Deterministic: k-ordered MFMA chains, a
-// fixed parity order, a fixed split order.
+// Ka <= 64, Nb <= 256, Ka + Nb <= 264, even widths, contiguous 16-byte aligned rows, f32
+// (ml-1m: per layer _uvqk 50 x 200 over LN(x) rows and _o 50 x 50 over dy rows; the 8
+// problems of an encoder backward in one launch).
+// Workgroup = one (problem, row split), 8 waves, one per CU.  The split's rows stream
+// through a 4-deep LDS ring of 32-row chunks by LDS-DMA (buffer_load_dwordx4 ... lds: each
+// wave instruction moves 1 KB of contiguous rows, no VGPRs; rows >= offsets[B] land as
+// exact zeros from the descriptor's per-dword range check), one barrier per chunk.  The
+// MFMA fragments are read from the chunk with the columns PERMUTED so that one 8-byte LDS
+// read feeds several MFMAs:
+//   A fragment of ka-tile ct:  lane (lr, lg) = A'[row 4 s + lg][ka 4 lr + ct]
+//   B fragment of nb-tile t of 64-column group gi:  B[row 4 s + lg][64 gi + 4 lr + t]
+// Wave (gi, th, ph) runs the 8 MFMAs (ct 0..3) x (t = 2 th, 2 th + 1) of the k-steps
+// ph, ph + P, ... of each chunk (NG = ceil(Nb / 64) column groups, P = 4 / NG phases);
+// accumulator (ct, t) holds C[ka 16 lg + 4 r + ct][nb 64 gi + 4 lr + t].  The phases
+// meet in LDS by a fixed pairwise tree and the workgroup writes one slab; ws_reduce sums
+// each problem's slabs in split order.  Splits per problem are proportional to its column
+// groups (MFMA work per row), ~one workgroup per CU in total.  Deterministic: k-ordered
+// MFMA chains, a fixed tree, a fixed split order.  (Operands loaded per lane straight into
+// MFMA fragments instead -- 64-byte row segments, or 8/16-byte pieces: 2.4-2.8 TB/s.)
 constexpr int WS_THREADS = 512;
-constexpr int WS_DEPTH = 4;
-constexpr int WS_MAXTNB = 16;
+constexpr int WS_NBUF = 4;       // chunks in the ring
+constexpr int WS_KD = 5;         // DMA instructions per wave per chunk (<= 40 KB chunks)
+constexpr int WS_CHUNK_MAX = 35 * 1024;
 
 struct WsProb {
   const float* a;
@@ -972,9 +980,10 @@ struct WsProb {
   const float* bm;
   int64_t ldb;
   int Ka, Nb, NC;  // NC = Nb + 1: slab column Nb holds the column sum of A'
-  int tnb;         // nb-tile class (4, 8, 13, 16) >= ceil(Nb / 16)
+  int ng;          // 64-column groups of Nb (1, 2, 4)
   int splits;      // row splits = workgroups of this problem
-  int wg0;         // first workgroup of this problem
+  int ia, ib, is;  // 1 KB DMA pieces per chunk: A rows, B rows, stats
+  int cb;          // chunk bytes in LDS ((ia + ib + is) KB)
   float* slabs;    // [splits][Ka][NC]
   float* c;
   float* colsum;
@@ -988,102 +997,155 @@ struct WsArgs {
   int B;
 };
 
-template <int TNB>
+constexpr int WS_XCH = 36;  // floats per lane in the phase exchange: 32 accumulators + 4 column sums
+
+// One LDS-DMA instruction: each lane's 16 bytes at byte goff of r land at LDS byte
+// lds + 16 lane.  Inline asm (M0 saved and restored in the same statement): hipcc does not
+// count it, so it cannot add the vmcnt(0) it otherwise puts before every LDS read that the
+// DMA might alias (that drained the whole ring once per chunk); the kernel waits for the
+// ring with its own counted vmcnt + barrier.
+__device__ __forceinline__ void ws_dma(__amdgpu_buffer_rsrc_t r, const char* lds, int goff) {
+  const uint32_t la = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)lds);
+  uint32_t keep;
+  asm volatile(
+      "s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(goff), "s"(la), "s"(r)
+      : "memory");
+}
+
+template <int P>
 __device__ __forceinline__ void ws_body(const WsProb& g, int64_t total, int split, char* smem) {
+  constexpr int NG = 4 / P;
+  constexpr int NW = 2 * NG;  // waves per phase
   const int w = wave_id(), lane = threadIdx.x & 63;
-  const int c = w & 3, h = w >> 2;
+  const int gi = (w >> 1) % NG, th = w & 1, ph = w / NW;
   const int lr = lane & 15, lg = lane >> 4;
-  // this split's rows: [r0, r1), r0 a multiple of 8 (k-steps of the two parities align)
-  const int64_t rps = ((total + g.splits - 1) / g.splits + 7) & ~(int64_t)7;
+  const int64_t rps = ((total + g.splits - 1) / g.splits + 31) & ~(int64_t)31;
   const int64_t r0 = (int64_t)split * rps;
   const int64_t r1 = min(total, r0 + rps);
-  const int nks = __builtin_amdgcn_readfirstlane(r1 > r0 ? (int)((r1 - r0 + 3) >> 2) : 0);
-  const int mine = nks > h ? (nks - h + 1) >> 1 : 0;  // k-steps h, h + 2, ... of this split
-  const bool active = 16 * c < g.Ka;
-  // rows >= total read as 0 through the descriptors' range (A and its stats 0: A' = 0)
+  const int nch = __builtin_amdgcn_readfirstlane(r1 > r0 ? (int)((r1 - r0 + 31) >> 5) : 0);
+  // rows >= total read as 0 (per-dword range check), so A' = (0 - 0) * 0 and B = 0 there
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)g.a, 0, total > 0 ? (int)(((total - 1) * g.lda + g.Ka) * 4) : 0, 0x00020000);
+      (void*)g.a, 0, (int)(total * g.Ka * 4), 0x00020000);
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)g.bm, 0, total > 0 ? (int)(((total - 1) * g.ldb + g.Nb) * 4) : 0, 0x00020000);
+      (void*)g.bm, 0, (int)(total * g.Nb * 4), 0x00020000);
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(g.a_stats ? (const void*)g.a_stats : (const void*)g.a), 0,
       g.a_stats ? (int)(total * 8) : 0, 0x00020000);
-  const int acol = 16 * c + lr;
-  const bool a_ok = acol < g.Ka;
-  int bcol_ok = 0;  // bit t: column 16 t + lr < Nb
+  char* dummy = smem + WS_NBUF * WS_CHUNK_MAX;  // 1 KB sink of the padding instructions
+  const int npiece = g.ia + g.ib + g.is;
+  // chunk c into ring slot c % NBUF: piece i (1 KB) by wave i % 8; every wave issues
+  // exactly WS_KD instructions per chunk (out-of-range ones into the sink) so one
+  // constant vmcnt covers the ring
+  auto dma = [&](int c) {
+    char* buf = smem + (c & (WS_NBUF - 1)) * WS_CHUNK_MAX;
+    const bool live = c < nch;
+    const int row0 = (int)r0 + 32 * c;
 #pragma unroll
-  for (int t = 0; t < TNB; ++t) bcol_ok |= (16 * t + lr < g.Nb) ? (1 << t) : 0;
-  constexpr int OOBW = 0x40000000;
-
-  float av[WS_DEPTH], bv[WS_DEPTH][TNB];
-  float2 sv[WS_DEPTH];
-  // issue the loads of this wave's k-step j into slot u (j >= mine: all out of range)
-  auto issue = [&](int u, int j) {
-    const bool in = j < mine;
-    const int row = (int)(r0 + 4 * (2 * j + h)) + lg;
-    const int ro_a = row * (int)g.lda, ro_b = row * (int)g.ldb;
-    av[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-        ra, in && a_ok ? (ro_a + acol) * 4 : OOBW, 0, 0));
-    if (g.a_stats) {
-      const u32x2_t s = __builtin_amdgcn_raw_buffer_load_b64(rs, in ? row * 8 : OOBW, 0, 0);
-      sv[u] = make_float2(__uint_as_float(s.x), __uint_as_float(s.y));
-    } else {
-      sv[u] = make_float2(0.f, 1.f);
+    for (int k = 0; k < WS_KD; ++k) {
+      const int i = w + 8 * k;
+      if (live && i < g.ia) {
+        ws_dma(ra, buf + 1024 * i, row0 * g.Ka * 4 + 1024 * i + 16 * lane);
+      } else if (live && i < g.ia + g.ib) {
+        const int j = i - g.ia;
+        ws_dma(rb, buf + 1024 * i, row0 * g.Nb * 4 + 1024 * j + 16 * lane);
+      } else if (live && i < npiece) {
+        ws_dma(rs, buf + 1024 * i, row0 * 8 + 16 * lane);
+      } else {
+        ws_dma(ra, dummy, 0x40000000);
+      }
     }
-#pragma unroll
-    for (int t = 0; t < TNB; ++t)
-      bv[u][t] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-          rb, in && ((bcol_ok >> t) & 1) ? (ro_b + 16 * t + lr) * 4 : OOBW, 0, 0));
   };
-
-  f4 acc[TNB];
+  const int offB = 1024 * g.ia, offS = 1024 * (g.ia + g.ib);
+  const int acol = 4 * lr, bcol = 64 * gi + 4 * lr + 2 * th;
+  f4 acc[4][2];  // [ct][t - 2 th]
 #pragma unroll
-  for (int t = 0; t < TNB; ++t) acc[t] = f4_zero();
-  float csum = 0.f;  // sum over this wave's rows of A'[row][16c + lr] (the _o bias gradient)
-  if (active && mine > 0) {
+  for (int ct = 0; ct < 4; ++ct) acc[ct][0] = acc[ct][1] = f4_zero();
+  f4 csum = f4_zero();  // A'[row][4 lr + ct] over this wave's rows (the _o bias gradient)
+  const bool ln = g.a_stats != nullptr;
 #pragma unroll
-    for (int u = 0; u < WS_DEPTH; ++u) issue(u, u);
-    const int iters = (mine + WS_DEPTH - 1) / WS_DEPTH * WS_DEPTH;
-    for (int j0 = 0; j0 < iters; j0 += WS_DEPTH) {
+  for (int c = 0; c < WS_NBUF - 1; ++c) dma(c);
+  for (int c = 0; c < nch; ++c) {
+    // chunk c landed (the two newer chunks' 2 x WS_KD instructions may still fly), and
+    // every wave is past chunk c - 1, whose slot the next DMA refills
+    asm volatile("s_waitcnt vmcnt(10)\n\ts_barrier" ::: "memory");
+    dma(c + WS_NBUF - 1);
+    const char* buf = smem + (c & (WS_NBUF - 1)) * WS_CHUNK_MAX;
 #pragma unroll
-      for (int u = 0; u < WS_DEPTH; ++u) {
-        // A'[row 4 s + lg][ka 16 c + lr] (LN applied; rows out of range: 0 * 0)
-        const float a = g.a_stats ? (av[u] - sv[u].x) * sv[u].y : av[u];
-        csum += a;
-        __builtin_amdgcn_sched_barrier(0);
+    for (int s = ph; s < 8; s += P) {
+      const int row = 4 * s + lg;
+      const float* arow = reinterpret_cast<const float*>(buf) + row * g.Ka + acol;
+      const float2 a01 = *reinterpret_cast<const float2*>(arow);
+      const float2 a23 = *reinterpret_cast<const float2*>(arow + 2);
+      const float2 b = *reinterpret_cast<const float2*>(buf + offB + 4 * (row * g.Nb + bcol));
+      f4 a = f4{a01.x, a01.y, a23.x, a23.y};
+      if (ln) {
+        const float2 st = *reinterpret_cast<const float2*>(buf + offS + 8 * row);
 #pragma unroll
-        for (int t = 0; t < TNB; ++t) acc[t] = mfma16x16x4(a, bv[u][t], acc[t]);
-        __builtin_amdgcn_sched_barrier(0);
-        issue(u, j0 + u + WS_DEPTH);
+        for (int e = 0; e < 4; ++e) a[e] = (a[e] - st.x) * st.y;
+      }
+      csum += a;
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) {
+        acc[ct][0] = mfma16x16x4(a[ct], b.x, acc[ct][0]);
+        acc[ct][1] = mfma16x16x4(a[ct], b.y, acc[ct][1]);
       }
     }
   }
-  // parity 1 hands its partial sums to parity 0 through LDS (fixed order h0 + h1)
-  float* xch = reinterpret_cast<float*>(smem);  // [4][TNB][4][64], then [4][16] column sums
-  csum = wg_colsum_lanes(csum);
-  if (h == 1) {
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");  // the ring is free for the exchange
+  // column sums over the k-step rows (lanes lr, lr + 16, lr + 32, lr + 48), fixed order
 #pragma unroll
-    for (int t = 0; t < TNB; ++t)
+  for (int e = 0; e < 4; ++e) csum[e] = wg_colsum_lanes(csum[e]);
+  // phases meet pairwise in LDS: round s, phases s .. 2s - 1 hand their sums to phase - s
+  float* xch = reinterpret_cast<float*>(smem);  // [P / 2 slots][NW][WS_XCH][64]
+  const int wi = w % NW;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) xch[((c * TNB + t) * 4 + r) * 64 + lane] = acc[t][r];
-    if (lg == 0) xch[4 * TNB * 4 * 64 + 16 * c + lr] = csum;
-  }
-  __syncthreads();
-  if (h == 1) return;
-  float* slab = g.slabs + (int64_t)split * g.Ka * g.NC;
-  if (g.colsum && lg == 0 && a_ok)
-    slab[(int64_t)acol * g.NC + g.Nb] = csum + xch[4 * TNB * 4 * 64 + 16 * c + lr];
-  // acc[t][r] = C[ka 16 c + 4 lg + r][nb 16 t + lr]
+  for (int s = P / 2; s >= 1; s >>= 1) {
+    if (ph >= s && ph < 2 * s) {
+      float* x = xch + ((ph - s) * NW + wi) * WS_XCH * 64 + lane;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int ka = 16 * c + 4 * lg + r;
-    if (ka >= g.Ka) continue;
+      for (int ct = 0; ct < 4; ++ct)
 #pragma unroll
-    for (int t = 0; t < TNB; ++t) {
-      const int nb = 16 * t + lr;
-      if (nb < g.Nb) slab[(int64_t)ka * g.NC + nb] = acc[t][r] + xch[((c * TNB + t) * 4 + r) * 64 + lane];
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) x[((ct * 2 + t) * 4 + r) * 64] = acc[ct][t][r];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[(32 + e) * 64] = csum[e];
     }
+    __syncthreads();
+    if (ph < s) {
+      const float* x = xch + (ph * NW + wi) * WS_XCH * 64 + lane;
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[ct][t][r] += x[((ct * 2 + t) * 4 + r) * 64];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) csum[e] += x[(32 + e) * 64];
+    }
+    __syncthreads();
   }
+  if (ph != 0 || bcol >= g.Nb) return;
+  float* slab = g.slabs + (int64_t)split * g.Ka * g.NC;
+  if (g.colsum && gi == 0 && th == 0 && lg == 0) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (acol + e < g.Ka) slab[(int64_t)(acol + e) * g.NC + g.Nb] = csum[e];
+  }
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int ka = 16 * lg + 4 * r + ct;
+      if (ka >= g.Ka) continue;
+      // columns bcol, bcol + 1 (Nb even: both in range; NC = Nb + 1 is odd, so two dwords)
+      slab[(int64_t)ka * g.NC + bcol] = acc[ct][0][r];
+      slab[(int64_t)ka * g.NC + bcol + 1] = acc[ct][1][r];
+    }
 }
 
 __global__ __launch_bounds__(WS_THREADS) void wgrad_stream_kernel(WsArgs g) {
@@ -1092,12 +1154,9 @@ __global__ __launch_bounds__(WS_THREADS) void wgrad_stream_kernel(WsArgs g) {
   const WsProb& p = g.p[i];
   const int split = blockIdx.x - g.wg0[i];
   const int64_t total = g.offsets[g.B];
-  switch (p.tnb) {
-    case 4: ws_body<4>(p, total, split, smem); break;
-    case 8: ws_body<8>(p, total, split, smem); break;
-    case 13: ws_body<13>(p, total, split, smem); break;
-    default: ws_body<16>(p, total, split, smem); break;
-  }
+  if (p.ng == 1) ws_body<4>(p, total, split, smem);
+  else if (p.ng == 2) ws_body<2>(p, total, split, smem);
+  else ws_body<1>(p, total, split, smem);
 }
 
 // out = sum over a problem's splits in split order: thread (o, grp) of a 256-thread block
@@ -1134,34 +1193,49 @@ __global__ __launch_bounds__(256) void ws_reduce_kernel(WsArgs g) {
   }
 }
 
-static int ws_tnb(int nb) {
-  const int t = ceil_div(nb, 16);
-  return t <= 4 ? 4 : t <= 8 ? 8 : t <= 13 ? 13 : 16;
-}
-static bool ws_fits(const int* Ka, const int* Nb, int np) {
+static int ws_ng(int nb) { return nb <= 64 ? 1 : nb <= 128 ? 2 : 4; }
+static int ws_pieces(int w) { return (128 * w + 1023) / 1024; }  // 1 KB DMA pieces of 32 rows
+// the streaming form: every problem Ka <= 64, Nb <= 256, even widths, rows contiguous
+// (ld == width) and 16-byte aligned bases, and a 32-row chunk within WS_CHUNK_MAX
+static bool ws_fits_shapes(const int* Ka, const int* Nb, int np) {
   for (int i = 0; i < np; ++i)
-    if (Ka[i] > 0 && (Ka[i] > 64 || Nb[i] > 16 * WS_MAXTNB)) return false;
+    if (Ka[i] > 0 && (Ka[i] > 64 || Nb[i] > 256 || (Ka[i] | Nb[i]) & 1 ||
+                      1024 * (ws_pieces(Ka[i]) + ws_pieces(Nb[i]) + 1) > WS_CHUNK_MAX))
+      return false;
   return true;
 }
-static size_t ws_lds(int tnb) { return sizeof(float) * (4 * (size_t)tnb * 4 * 64 + 4 * 16); }
+static bool ws_fits(const WgradProb* in, int np) {
+  int Ka[WG_MAXP], Nb[WG_MAXP];
+  for (int i = 0; i < np; ++i) {
+    const WgradProb& p = in[i];
+    Ka[i] = p.a ? p.Ka : 0;
+    Nb[i] = p.a ? p.Nb : 0;
+    if (!p.a) continue;
+    if (p.lda != p.Ka || p.ldb != p.Nb || (uintptr_t)p.a % 16 || (uintptr_t)p.bm % 16 ||
+        (p.a_stats && (uintptr_t)p.a_stats % 16))
+      return false;
+  }
+  return ws_fits_shapes(Ka, Nb, np);
+}
+static size_t ws_lds() { return (size_t)WS_NBUF * WS_CHUNK_MAX + 1024; }
 
 struct WsPlan {
   int splits[WG_MAXP];
   size_t slab_bytes[WG_MAXP];
   size_t need;
 };
-// splits per problem proportional to its nb-tiles, ~one workgroup per CU in total, each
-// split >= 64 rows
+// splits per problem proportional to its column groups, ~one workgroup per CU in total,
+// each split >= 64 rows
 static WsPlan ws_plan(int64_t max_rows, const int* Ka, const int* Nb, int np) {
   WsPlan pl{};
-  int tsum = 0;
+  int csum = 0;
   for (int i = 0; i < np; ++i)
-    if (Ka[i] > 0) tsum += ws_tnb(Nb[i]);
+    if (Ka[i] > 0) csum += ws_ng(Nb[i]);
   const int G = device_cus();
   const int64_t cap = std::max<int64_t>(1, (max_rows + 63) / 64);
   for (int i = 0; i < np; ++i) {
     if (Ka[i] <= 0) continue;
-    int64_t s = ((int64_t)G * ws_tnb(Nb[i]) + tsum / 2) / std::max(tsum, 1);
+    int64_t s = ((int64_t)G * ws_ng(Nb[i]) + csum / 2) / std::max(csum, 1);
     s = std::max<int64_t>(1, std::min(s, cap));
     pl.splits[i] = (int)s;
     pl.slab_bytes[i] = sizeof(float) * (size_t)s * Ka[i] * (Nb[i] + 1);
@@ -1197,13 +1271,17 @@ static int wgrad_run_stream(const WgradProb* in, int np, const int64_t* offsets,
     p.Ka = Ka[i];
     p.Nb = Nb[i];
     p.NC = Nb[i] + 1;
-    p.tnb = ws_tnb(Nb[i]);
+    p.ng = ws_ng(Nb[i]);
+    p.ia = ws_pieces(Ka[i]);
+    p.ib = ws_pieces(Nb[i]);
+    p.is = p.a_stats ? 1 : 0;
+    p.cb = 1024 * (p.ia + p.ib + p.is);
     p.splits = pl.splits[i];
     p.slabs = (float*)(ws + off);
     off += (pl.slab_bytes[i] + 255) & ~(size_t)255;
     p.c = in[i].c;
     p.colsum = in[i].colsum;
-    lds = std::max(lds, ws_lds(p.tnb));
+    lds = ws_lds();
     g.wg0[g.np + 1] = g.wg0[g.np] + p.splits;
     g.blk0[g.np + 1] = g.blk0[g.np] + (int)(((int64_t)p.Ka * p.NC + 15) / 16);
     ++g.np;
@@ -1223,7 +1301,7 @@ static size_t wgrad_ws_need(const int* Ka, const int* Nb, int np, int64_t max_ro
   int kmax = 0;
   for (int i = 0; i < np; ++i) kmax = std::max(kmax, Ka[i]);
   if (kmax <= WGW_T) need = std::max(need, wgrad_plan_wide(max_rows, Ka, Nb, np).need);
-  if (ws_fits(Ka, Nb, np)) need = std::max(need, ws_plan(max_rows, Ka, Nb, np).need);
+  if (ws_fits_shapes(Ka, Nb, np)) need = std::max(need, ws_plan(max_rows, Ka, Nb, np).need);
   return need;
 }
 

@@ -16,6 +16,7 @@ Reference map (``src/generative_recommenders_pl/models/``):
 from __future__ import annotations
 
 
+import ctypes
 from dataclasses import dataclass
 from typing import Optional
 
@@ -254,6 +255,22 @@ def rel_bias(timestamps: torch.Tensor, N: int, pos_w: torch.Tensor,
 
 # ------------------------------------------------------------------ fused STU layer
 
+class GrBoundaryBwd(ctypes.Structure):
+    """include/gr_hstu.h GrBoundaryBwd: the layer-boundary arguments of hstu_attn_bwd_bnd
+    (those of hstu_boundary_bwd; hdv = 0 for the first layer: ln_uvqk_bwd alone)."""
+    _fields_ = [("dh", ctypes.c_void_p), ("ld_dh", ctypes.c_int64), ("max_rows", ctypes.c_int64),
+                ("D", ctypes.c_int), ("n_out", ctypes.c_int), ("w_uvqk", ctypes.c_void_p),
+                ("x", ctypes.c_void_p), ("ld_x", ctypes.c_int64), ("x_stats", ctypes.c_void_p),
+                ("dy_res", ctypes.c_void_p), ("ld_dy", ctypes.c_int64), ("dx", ctypes.c_void_p),
+                ("ld_dx", ctypes.c_int64), ("hdv", ctypes.c_int), ("w_o", ctypes.c_void_p),
+                ("u", ctypes.c_void_p), ("ld_u", ctypes.c_int64), ("attn", ctypes.c_void_p),
+                ("ld_attn", ctypes.c_int64), ("attn_stats", ctypes.c_void_p),
+                ("h_u", ctypes.c_void_p), ("ld_h", ctypes.c_int64), ("dropout_p", ctypes.c_float),
+                ("seed", ctypes.c_uint64), ("seed_offset", ctypes.c_void_p),
+                ("du", ctypes.c_void_p), ("ld_du", ctypes.c_int64), ("d_attn", ctypes.c_void_p),
+                ("ld_da", ctypes.c_int64)]
+
+
 @dataclass
 class STUGeometry:
     N: int              # padded max length (attention normaliser and bias extent)
@@ -484,29 +501,44 @@ def _stu_backward(saved, dy, geo: STUGeometry, seed: int, seed_offset, want_uvqk
                 _lib.ptr(bmap), _lib.ptr(pos_w), _lib.ptr(ts_w), NUM_BUCKETS,
                 hq_p, hk_p, hv_p, n_out, dq.data_ptr(), dk.data_ptr(), dvv.data_ptr(), n_out,
                 _lib.ptr(d_pos_w), _lib.ptr(d_ts_w))
-    if geo.bf16:
-        _lib.call("hstu_attn_bwd_bf16", *bwd_args, _lib.ptr(copies), _lib.ptr(ws_a), ws_a_n, st)
-    else:
-        _lib.call("hstu_attn_bwd", *bwd_args, _lib.ptr(ws_a), ws_a_n, st)
     dx = torch.empty(rows, D, dtype=torch.float32, device=dev)
     pre_d_prev = None
-    if prev is not None:
-        if geo.concat_ua or geo.bf16:
-            raise ValueError("hstu_boundary_bwd: fp32, no concat_ua")
-        (_, _, _, _, p_w_o, _, _, _, p_uvqk, p_h_pre, p_attn, p_attn_stats, _, _), p_seed = prev
-        pre_d_prev = (torch.empty(rows, n_out, dtype=torch.float32, device=dev),
-                      torch.empty(rows, hv, dtype=torch.float32, device=dev))
-        _lib.call("hstu_boundary_bwd", d_uvqk.data_ptr(), n_out, offsets.data_ptr(), B, rows, D,
-                  n_out, w_uvqk.data_ptr(), x.data_ptr(), x.stride(0), x_stats.data_ptr(),
-                  dy.data_ptr(), D, dx.data_ptr(), D, hv, p_w_o.data_ptr(), p_uvqk.data_ptr(),
-                  n_out, p_attn.data_ptr(), hv, p_attn_stats.data_ptr(), _lib.ptr(p_h_pre),
-                  n_out, geo.dropout_p, p_seed, _lib.ptr(seed_offset),
-                  pre_d_prev[0].data_ptr(), n_out, pre_d_prev[1].data_ptr(), hv, st)
-    else:
-        _lib.call("hstu_ln_uvqk_bwd" + ("_bf16" if geo.bf16 else ""), d_uvqk.data_ptr(), n_out,
-                  offsets.data_ptr(), B, rows, D,
-                  n_out, w_uvqk.data_ptr(), x.data_ptr(), x.stride(0), x_stats.data_ptr(),
+    if prev is not None and (geo.concat_ua or geo.bf16):
+        raise ValueError("hstu_boundary_bwd: fp32, no concat_ua")
+    if geo.bf16:
+        _lib.call("hstu_attn_bwd_bf16", *bwd_args, _lib.ptr(copies), _lib.ptr(ws_a), ws_a_n, st)
+        _lib.call("hstu_ln_uvqk_bwd_bf16", d_uvqk.data_ptr(), n_out, offsets.data_ptr(), B, rows,
+                  D, n_out, w_uvqk.data_ptr(), x.data_ptr(), x.stride(0), x_stats.data_ptr(),
                   dy.data_ptr(), D, dx.data_ptr(), D, st)
+    else:
+        # the attention backward and this layer's ln_uvqk_bwd (+ the previous layer's
+        # gate_o_bwd: the layer boundary) in one call; at narrow shapes the boundary runs as
+        # the epilogue of the dQ launch (hstu_attn_bwd_bnd)
+        bnd = GrBoundaryBwd(dh=d_uvqk.data_ptr(), ld_dh=n_out, max_rows=rows, D=D, n_out=n_out,
+                            w_uvqk=w_uvqk.data_ptr(), x=x.data_ptr(), ld_x=x.stride(0),
+                            x_stats=x_stats.data_ptr(), dy_res=dy.data_ptr(), ld_dy=D,
+                            dx=dx.data_ptr(), ld_dx=D)
+        if prev is not None:
+            (_, _, _, _, p_w_o, _, _, _, p_uvqk, p_h_pre, p_attn, p_attn_stats, _, _), p_seed = prev
+            pre_d_prev = (torch.empty(rows, n_out, dtype=torch.float32, device=dev),
+                          torch.empty(rows, hv, dtype=torch.float32, device=dev))
+            bnd.hdv = hv
+            bnd.w_o = p_w_o.data_ptr()
+            bnd.u = p_uvqk.data_ptr()
+            bnd.ld_u = n_out
+            bnd.attn = p_attn.data_ptr()
+            bnd.ld_attn = hv
+            bnd.attn_stats = p_attn_stats.data_ptr()
+            bnd.h_u = _lib.ptr(p_h_pre)
+            bnd.ld_h = n_out
+            bnd.dropout_p = geo.dropout_p
+            bnd.seed = p_seed
+            bnd.seed_offset = _lib.ptr(seed_offset)
+            bnd.du = pre_d_prev[0].data_ptr()
+            bnd.ld_du = n_out
+            bnd.d_attn = pre_d_prev[1].data_ptr()
+            bnd.ld_da = hv
+        _lib.call("hstu_attn_bwd_bnd", *bwd_args, _lib.ptr(ws_a), ws_a_n, ctypes.addressof(bnd), st)
     # weight gradients (off the critical path): both GEMMs of the layer in one launch
     # and one slab reduce (gr_wgrad2), or deferred to the caller's gr_wgrad_multi
     d_w_uvqk = torch.empty(D, n_out, dtype=torch.float32, device=dev) if want_uvqk else None

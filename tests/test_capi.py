@@ -156,10 +156,10 @@ def test_launch_options_are_explicit_not_environment():
                          "MIPS_FORCE_FALLBACK", "ATTN_BWD_SPLIT", "ROWWAVE", "ATTN_BWD_PAIRS",
                          "ATTN_BWD_DS", "DETERMINISTIC", "WGRAD_ROWS", "PANEL_VEC",
                          "ATTN_BWD_WIDE_DS", "ATTN_BWD_WIDE_SPLIT", "MIPS_FILTER_PAIRED",
-                         "MIPS_SAMPLE_STRIDE", "WGRAD_STREAM"}
+                         "MIPS_SAMPLE_STRIDE", "WGRAD_STREAM", "BOUNDARY_FUSE"}
     defaults = {"ROWWAVE": 1, "ATTN_BWD_PAIRS": 1, "PANEL_VEC": 1, "ATTN_BWD_DS": 1,
                 "ATTN_BWD_WIDE_DS": 1, "ATTN_BWD_WIDE_SPLIT": 0, "MIPS_FILTER_PAIRED": 1,
-                "WGRAD_STREAM": 1}
+                "WGRAD_STREAM": 1, "BOUNDARY_FUSE": 1}
     for n in opts:
         assert _lib.get_option(n) == defaults.get(n, 0), n
     with _lib.option("ATTN_BWD_SPLIT", 1):
@@ -187,3 +187,20 @@ def test_library_is_gfx950_code_object():
     for other in (b"gfx942", b"gfx90a", b"sm_"):
         assert b"amdgcn-amd-amdhsa--" + other not in data
     assert ctypes.sizeof(ctypes.c_void_p) == 8
+
+
+def test_boundary_struct_layout_matches_header(tmp_path):
+    """ops.GrBoundaryBwd (ctypes) has the C layout of include/gr_hstu.h's GrBoundaryBwd:
+    same size and field offsets, checked against gcc on the header itself."""
+    from mygenerativerecommenders_amd.ops import GrBoundaryBwd
+    names = [f[0] for f in GrBoundaryBwd._fields_]
+    src = tmp_path / "layout.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "gr_hstu.h"\nint main(void) {\n'
+                   '  printf("%zu\\n", sizeof(GrBoundaryBwd));\n'
+                   + "".join(f'  printf("%zu\\n", offsetof(GrBoundaryBwd, {n}));\n' for n in names)
+                   + "  return 0;\n}\n")
+    exe = tmp_path / "layout"
+    subprocess.check_call(["gcc", "-I", os.path.dirname(_lib.HEADER_PATH), str(src), "-o", str(exe)])
+    got = [int(v) for v in subprocess.check_output([str(exe)], text=True).split()]
+    assert got[0] == ctypes.sizeof(GrBoundaryBwd)
+    assert got[1:] == [getattr(GrBoundaryBwd, n).offset for n in names]

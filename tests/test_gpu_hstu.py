@@ -455,6 +455,64 @@ def test_hstu_stack_boundaries_match_unfused(B, N0, D, hdv, blocks, act, dropout
         close(g0[n], g1[n], n)
 
 
+@pytest.mark.parametrize("B,N0,D,hdv,blocks", [(16, 200, 50, 50, 3), (6, 70, 64, 64, 2),
+                                                (5, 40, 48, 40, 2), (4, 96, 256, 256, 2),
+                                                (8, 64, 50, 20, 2)])
+def test_hstu_boundary_as_dq_epilogue_matches_separate(B, N0, D, hdv, blocks):
+    """hstu_attn_bwd_bnd runs the layer boundary (ln_uvqk_bwd(l) + gate_o_bwd(l - 1), or
+    ln_uvqk_bwd(0) alone) as the epilogue of the attention dQ launch at narrow single-head
+    shapes (GR_OPT_BOUNDARY_FUSE, default on), against the attention backward and the
+    boundary as separate launches (option 0), train mode with dropout and ragged lengths.
+    The epilogue is the row-wave unit of hstu_boundary_bwd, so the boundaries between
+    layers are bit-identical; the first layer's ln_uvqk_bwd alone may take the row panel
+    when separate (n_out > 128), so gradients agree to fp32 summation order: 2e-5 relative.
+    Shapes the epilogue does not cover (D = 256; h dv = 20) run the separate launches
+    inside the call and are bit-identical."""
+    from mygenerativerecommenders_amd import _lib
+    from mygenerativerecommenders_amd.hstu import HSTU
+    torch.manual_seed(3)
+    out_len = 11
+    N = N0 + out_len
+    enc = HSTU(max_sequence_len=N0, max_output_len=out_len, embedding_dim=D,
+               item_embedding_dim=D, num_blocks=blocks, num_heads=1, linear_dim=hdv,
+               attention_dim=hdv, normalization="rel_bias", linear_config="uvqk",
+               linear_activation="silu", linear_dropout_rate=0.2,
+               attn_dropout_rate=0.0).cuda().train()
+    g = torch.Generator().manual_seed(11)
+    lengths = torch.randint(1, N0 + 1, (B,), generator=g)
+    lengths[0] = N0
+    x = torch.randn(B, N, D, generator=g).cuda()
+    ts = torch.zeros(B, N, dtype=torch.int64)
+    for b in range(B):
+        L = int(lengths[b])
+        ts[b, :L + 1] = 1_000_000_000 + torch.cumsum((torch.rand(L + 1, generator=g) * 2e5).long(), 0)
+    dy = torch.randn(B, N, D, generator=g).cuda()
+    outs = []
+    for fuse in (1, 0):
+        with _lib.option("BOUNDARY_FUSE", fuse):
+            enc._hstu._dropout_step.zero_()
+            enc.zero_grad(set_to_none=True)
+            xg = x.clone().requires_grad_(True)
+            y, _ = enc(lengths.cuda(), xg, None, {"timestamps": ts.cuda()})
+            (y * dy).sum().backward()
+            torch.cuda.synchronize()
+            outs.append((y.detach(), xg.grad, {n: p.grad.clone() for n, p in enc.named_parameters()}))
+    (y0, dx0, g0), (y1, dx1, g1) = outs
+    assert torch.equal(y0, y1)
+    exact = D > 64 or hdv <= 32
+
+    def close(a, b, what):
+        if exact:
+            assert torch.equal(a, b), what
+            return
+        assert torch.isfinite(a).all(), what
+        err = (a - b).abs().max().item()
+        assert err <= 2e-5 * (1 + b.abs().max().item()), (what, err)
+    close(dx0, dx1, "dx")
+    for n in g0:
+        close(g0[n], g1[n], n)
+
+
 @pytest.mark.parametrize("bf16", [False, True])
 def test_hstu_stack_wgrad_overlap(bf16):
     """Weight gradients on the side stream (ops.OVERLAP_WGRAD: layer l's launched beside
