@@ -497,6 +497,49 @@ GR_API int hstu_boundary_bwd(const float* dh, int64_t ld_dh, const int64_t* offs
                     const int64_t* seed_offset, float* du, int64_t ld_du, float* d_attn,
                     int64_t ld_da, void* stream);
 
+/* ABI 14: the attention forward of layer l followed by its layer boundary, i.e.
+ * hstu_attn_fwd(... out ...) then hstu_boundary_fwd(bnd..., attn = out) -- or, with
+ * bnd->w_uvqk == NULL for the last layer, hstu_gate_o_fwd(bnd...) -- in one call.  At
+ * narrow single-head shapes (H == 1, dqk, dv <= 64; D, h dv in (32, 64], n_out <= 256)
+ * the boundary runs as the epilogue of the attention launch: a workgroup's 64 query rows
+ * are complete once stored, so its waves re-stage the K / V tile area with the weight
+ * panels and run the row-wave boundary unit of their 16 rows (one launch and one re-read
+ * of u / attn fewer); otherwise the two calls run as they are.  Results agree with the two
+ * calls' to fp32 rounding (the epilogue is hstu_boundary_fwd's row-wave unit, the last
+ * layer's gate_o alone the row-wave form of hstu_gate_o_fwd; hipcc may contract their
+ * multiply-adds differently inside the attention kernel: a few ulp). */
+typedef struct GrBoundaryFwd {
+  const float* u;
+  int64_t ld_u;
+  int64_t max_rows;
+  int hdv;
+  int D;
+  const float* w_o;
+  const float* b_o;
+  const float* x_res;
+  int64_t ld_x;
+  float eps;
+  float dropout_p;
+  uint64_t seed;
+  const int64_t* seed_offset;
+  float* attn_stats;
+  float* o_in;
+  float* y;
+  int64_t ld_y;
+  const float* w_uvqk;  /* NULL: no next layer (the last layer: gate_o alone) */
+  int n_out;
+  int activation;
+  float* x_stats;
+  float* h_pre;
+  float* uvqk;
+  int64_t ld_out;
+} GrBoundaryFwd;
+GR_API int hstu_attn_fwd_bnd(const float* q, const float* k, const float* v, int64_t ld_qk,
+                    int64_t ld_v, const int64_t* offsets, int B, int N, int max_len, int H,
+                    int dqk, int dv, const uint8_t* bucket_map, const float* pos_w,
+                    const float* ts_w, int num_buckets, float* out, int64_t ld_out,
+                    const GrBoundaryFwd* bnd, void* stream);
+
 /* ABI 14: the attention backward of layer l followed by its layer boundary, i.e.
  * hstu_attn_bwd(...) then hstu_boundary_bwd(bnd...) (or, with bnd->hdv == 0 for the first
  * layer, hstu_ln_uvqk_bwd(bnd...)) in one call.  At narrow single-head shapes (H == 1,
@@ -506,9 +549,9 @@ GR_API int hstu_boundary_bwd(const float* dh, int64_t ld_dh, const int64_t* offs
  * (d_uvqk of the rows is then complete: du from the previous boundary, dk / dv from the
  * dK/dV launch, dq just stored) -- one launch and one re-read of the rows fewer.
  * Otherwise the two calls run as they are.  `bnd` holds the boundary call's arguments
- * (dh = the d_uvqk the attention writes into, stride ld_dh = n_out); results equal the
- * two calls' (the fused epilogue is the row-wave unit of hstu_boundary_bwd; the first
- * layer's hstu_ln_uvqk_bwd alone may take the row panel: fp32 summation order). */
+ * (dh = the d_uvqk the attention writes into, stride ld_dh = n_out); results agree with
+ * the two calls' to fp32 summation order (the fused epilogue is the row-wave unit of
+ * hstu_boundary_bwd; the first layer's hstu_ln_uvqk_bwd alone may take the row panel). */
 typedef struct GrBoundaryBwd {
   const float* dh;
   int64_t ld_dh;

@@ -1105,17 +1105,23 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_bnd_kernel(AttnBwdArgs a, int
     bias_grad_reduce_body(a.slabs, n_slabs, 2 * a.N - 1, a.nb + 1, dpos_w, dts_w, (int)blockIdx.x);
     return;
   }
-  rw_stage_w<KG1, W>(op1, W1);
-  if constexpr (OP2) rw_stage_w<W, W>(op2, W2);
+  // the panels' loads land while dQ is computed; written to LDS after it
+  RwStage<KG1, W, RwLnUvqkBwd<KG1, W, 2>> st1;
+  RwStage<W, W, RwGateOBwd<W, W, 2>> st2;
+  st1.load(op1);
+  if constexpr (OP2) st2.load(op2);
   int q0 = 0, L = 0;
   int64_t s0 = 0;
   const bool live = attn_bwd_dq_wave_body<KSTEPS, VTILES>(a, id * 4 + wave_id(), &q0, &L, &s0);
+  st1.store(W1);
+  if constexpr (OP2) st2.store(W2);
   __syncthreads();  // the panels are staged (every wave reaches this, live or not)
   if (!live) return;
   // this wave's dq stores have landed before its unit reads the rows back (the rows' other
   // columns were written by earlier launches; no other wave writes these rows)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   op1.setup(s0 + L);
+  op1.rd_aux = 16;  // d_uvqk rows: L2 (the dq columns were just stored by this wave)
   if constexpr (OP2) op2.setup(s0 + L);
   const int lane = threadIdx.x & 63, lr = lane & 15, lg = lane >> 4;
   const int64_t m = s0 + q0 + lr;

@@ -16,6 +16,7 @@
 // (k-step r uses keys 4g + r, g = lane>>4) — no LDS round trip for P.
 // Blocks are issued heaviest-first (largest query tile first) for causal balance.
 #include "attn_common.h"
+#include "rowwave.h"
 
 #include "../../include/gr_hstu.h"
 
@@ -52,8 +53,11 @@ struct AttnFwdCfg {
 };
 
 // V2: pair staging fixed at compile time (see BWD_V2 in hstu_attn_bwd.hip)
+// Returns false when the workgroup's query tile is past its sequence (the whole workgroup
+// returns), else the tile's first query q0, the sequence's first row s0 and length L.
 template <int KSTEPS, int VTILES, int TK, bool HB, bool V2>
-__device__ __forceinline__ void hstu_attn_fwd_body(const AttnFwdArgs& a) {
+__device__ __forceinline__ bool hstu_attn_fwd_body(const AttnFwdArgs& a, int* q0_out = nullptr,
+                                                   int* L_out = nullptr, int64_t* s0_out = nullptr) {
   using C = AttnFwdCfg<KSTEPS, VTILES, TK>;
   const bool v2 = V2 || a.vec2;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -71,7 +75,12 @@ __device__ __forceinline__ void hstu_attn_fwd_body(const AttnFwdArgs& a) {
   const int64_t s0 = a.offsets[b];
   const int L = (int)(a.offsets[b + 1] - s0);
   const int q0 = qt * 64;
-  if (q0 >= L) return;
+  if (q0 >= L) return false;
+  if (q0_out) {
+    *q0_out = q0;
+    *L_out = L;
+    *s0_out = s0;
+  }
 
   const int tid = threadIdx.x, w = wave_id(), lane = tid & 63;
   const int lr = lane & 15, lg = lane >> 4;
@@ -203,6 +212,7 @@ __device__ __forceinline__ void hstu_attn_fwd_body(const AttnFwdArgs& a) {
       if (c < a.dv) orow[c] = acc[ct][r];
     }
   }
+  return true;
 }
 
 template <int KSTEPS, int VTILES, int TK, bool HB>
@@ -211,8 +221,85 @@ __global__ __launch_bounds__(256) void hstu_attn_fwd_kernel(AttnFwdArgs a) {
   else hstu_attn_fwd_body<KSTEPS, VTILES, TK, HB, false>(a);
 }
 
+// Attention forward with the layer boundary as its epilogue (hstu_attn_fwd_bnd, H == 1):
+// once a workgroup's 64 query rows of attention output are stored, the K / V tile area is
+// re-staged with the boundary's weight panels (gate_o's W_o, the next layer's W_uvqk) and
+// each wave runs the row-wave boundary unit of its 16 rows -- y = x + gate(u, LN(attn))
+// W_o^T + b, then LN(y) W_uvqk of the next layer -- or, OP2 = false (the last layer),
+// gate_o alone.  Rows past the sequence fall outside the ops' descriptors.
+template <int KSTEPS, int VTILES, bool HB, int NT2, bool OP2>
+__global__ __launch_bounds__(256) void hstu_attn_fwd_bnd_kernel(AttnFwdArgs a, RwGateO<4, 4, 2> op1,
+                                                                RwLnUvqk<4, NT2, 2> op2) {
+  // the weight panels' loads are issued first and land while the attention runs; they
+  // reach LDS once the K / V tiles they overwrite are done with
+  RwStage<4, 4, RwGateO<4, 4, 2>> st1;
+  RwStage<4, NT2, RwLnUvqk<4, NT2, 2>> st2;
+  st1.load(op1);
+  if constexpr (OP2) st2.load(op2);
+  int q0 = 0, L = 0;
+  int64_t s0 = 0;
+  const bool live = a.vec2 ? hstu_attn_fwd_body<KSTEPS, VTILES, 64, HB, true>(a, &q0, &L, &s0)
+                           : hstu_attn_fwd_body<KSTEPS, VTILES, 64, HB, false>(a, &q0, &L, &s0);
+  if (!live) return;  // uniform over the workgroup
+  using C1 = RowWaveCfg<4, 4>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* W1 = reinterpret_cast<float*>(smem);
+  float* W2 = W1 + C1::KP * C1::LDW;
+  __syncthreads();  // every wave is done with the K / V tiles the panels overwrite
+  st1.store(W1);
+  if constexpr (OP2) st2.store(W2);
+  __syncthreads();
+  // this wave's attention rows have landed before its unit reads them back
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int w = wave_id(), lane = threadIdx.x & 63, lr = lane & 15, lg = lane >> 4;
+  op1.setup(s0 + L);
+  op1.rd_aux = 16;  // attn rows: L2, not an L1 line a neighbouring wave filled before our store
+  if constexpr (OP2) op2.setup(s0 + L);
+  const int r = q0 + 16 * w + lr;
+  if (q0 + 16 * w >= L) return;  // wave-uniform: no rows of this wave
+  if constexpr (OP2) rw2_unit<4, 4, NT2>(op1, op2, W1, W2, s0 + r, r < L, lr, lg);
+  else rw1_unit<4, 4>(op1, W1, s0 + r, r < L, lr, lg);
+}
+
+struct BndFwdCtx {
+  RwArgsGateO a1;
+  RwArgsLnUvqk a2;
+  bool op2;
+  int nt2;     // 13 | 16
+  bool fused;
+};
+
+template <int KS, int VT, bool HB, int NT2, bool OP2>
+static int launch_fwd_bnd_k(const AttnFwdArgs& a, int grid, BndFwdCtx& bc, hipStream_t st) {
+  using C = AttnFwdCfg<KS, VT, 64>;
+  RwGateO<4, 4, 2> o1{};
+  RwLnUvqk<4, NT2, 2> o2{};
+  bc.a1.fill(o1);
+  if (OP2) bc.a2.fill(o2);
+  const size_t lds_attn = sizeof(float) * (C::LDS_FLOATS + a.nb + 1 + 2 * a.N - 1);
+  const size_t lds_w = RowWaveCfg<4, 4>::LDS_BYTES + (OP2 ? RowWaveCfg<4, NT2>::LDS_BYTES : 0);
+  const size_t lds = lds_attn > lds_w ? lds_attn : lds_w;
+  GR_REQUIRE(lds <= 160 * 1024, "hstu_attn_fwd_bnd: LDS %zu B exceeds 160 KiB (N=%d)", lds, a.N);
+  GR_TIMED("attn_fwd", st, hipLaunchKernelGGL((hstu_attn_fwd_bnd_kernel<KS, VT, HB, NT2, OP2>), dim3(grid),
+                                              dim3(256), lds, st, a, o1, o2));
+  GR_LAUNCH_CHECK("hstu_attn_fwd_bnd");
+  bc.fused = true;
+  return 0;
+}
+template <int KS, int VT, bool HB>
+static int launch_fwd_bnd_h(const AttnFwdArgs& a, int grid, BndFwdCtx& bc, hipStream_t st) {
+  if (!bc.op2) return launch_fwd_bnd_k<KS, VT, HB, 13, false>(a, grid, bc, st);
+  return bc.nt2 == 13 ? launch_fwd_bnd_k<KS, VT, HB, 13, true>(a, grid, bc, st)
+                      : launch_fwd_bnd_k<KS, VT, HB, 16, true>(a, grid, bc, st);
+}
+
 template <int KS, int VT, int TK = 64>
-static int launch_fwd(const AttnFwdArgs& a, int grid, hipStream_t st) {
+static int launch_fwd(const AttnFwdArgs& a, int grid, hipStream_t st, BndFwdCtx* bnd = nullptr) {
+  if constexpr (TK == 64 && VT == 4 && (KS == 13 || KS == 16)) {
+    if (bnd && a.H == 1)
+      return a.map_qk ? launch_fwd_bnd_h<KS, VT, true>(a, grid, *bnd, st)
+                      : launch_fwd_bnd_h<KS, VT, false>(a, grid, *bnd, st);
+  }
   using C = AttnFwdCfg<KS, VT, TK>;
   size_t lds = sizeof(float) * (C::LDS_FLOATS + a.nb + 1 + 2 * a.N - 1);
   GR_REQUIRE(lds <= 160 * 1024, "hstu_attn_fwd: LDS %zu B exceeds 160 KiB (N=%d)", lds, a.N);
@@ -227,12 +314,12 @@ static int launch_fwd(const AttnFwdArgs& a, int grid, hipStream_t st) {
 
 }  // namespace gr
 
-extern "C" int hstu_attn_fwd(const float* q, const float* k, const float* v, int64_t ld_qk,
-                             int64_t ld_v, const int64_t* offsets, int B, int N, int max_len,
-                             int H, int dqk, int dv, const uint8_t* bucket_map,
-                             const float* pos_w, const float* ts_w, int num_buckets, float* out,
-                             int64_t ld_out, void* stream) {
-  using namespace gr;
+namespace gr {
+static int attn_fwd_impl(const float* q, const float* k, const float* v, int64_t ld_qk,
+                         int64_t ld_v, const int64_t* offsets, int B, int N, int max_len,
+                         int H, int dqk, int dv, const uint8_t* bucket_map,
+                         const float* pos_w, const float* ts_w, int num_buckets, float* out,
+                         int64_t ld_out, void* stream, BndFwdCtx* bnd) {
   GR_REQUIRE(q && k && v && offsets && out, "hstu_attn_fwd: null pointer");
   GR_REQUIRE(B >= 0 && N > 0 && H > 0 && dqk > 0 && dv > 0, "hstu_attn_fwd: bad sizes");
   GR_REQUIRE(max_len >= 0 && max_len <= N, "hstu_attn_fwd: max_len %d not in [0, N=%d]", max_len, N);
@@ -250,11 +337,64 @@ extern "C" int hstu_attn_fwd(const float* q, const float* k, const float* v, int
   const int grid = a.n_qtiles * B * H;
   hipStream_t st = (hipStream_t)stream;
   const int d = dqk > dv ? dqk : dv;
-  if (d <= 8) return launch_fwd<2, 1>(a, grid, st);
-  if (d <= 16) return launch_fwd<4, 1>(a, grid, st);
-  if (d <= 32) return launch_fwd<8, 2>(a, grid, st);
-  if (d <= 52) return launch_fwd<13, 4>(a, grid, st);
-  if (d <= 64) return launch_fwd<16, 4>(a, grid, st);
-  if (d <= 128) return launch_fwd<32, 8>(a, grid, st);
-  return launch_fwd<64, 16, 16>(a, grid, st);
+  if (d <= 8) return launch_fwd<2, 1>(a, grid, st, bnd);
+  if (d <= 16) return launch_fwd<4, 1>(a, grid, st, bnd);
+  if (d <= 32) return launch_fwd<8, 2>(a, grid, st, bnd);
+  if (d <= 52) return launch_fwd<13, 4>(a, grid, st, bnd);
+  if (d <= 64) return launch_fwd<16, 4>(a, grid, st, bnd);
+  if (d <= 128) return launch_fwd<32, 8>(a, grid, st, bnd);
+  return launch_fwd<64, 16, 16>(a, grid, st, bnd);
+}
+}  // namespace gr
+
+extern "C" int hstu_attn_fwd(const float* q, const float* k, const float* v, int64_t ld_qk,
+                             int64_t ld_v, const int64_t* offsets, int B, int N, int max_len,
+                             int H, int dqk, int dv, const uint8_t* bucket_map,
+                             const float* pos_w, const float* ts_w, int num_buckets, float* out,
+                             int64_t ld_out, void* stream) {
+  return gr::attn_fwd_impl(q, k, v, ld_qk, ld_v, offsets, B, N, max_len, H, dqk, dv, bucket_map,
+                           pos_w, ts_w, num_buckets, out, ld_out, stream, nullptr);
+}
+
+extern "C" int hstu_attn_fwd_bnd(const float* q, const float* k, const float* v, int64_t ld_qk,
+                                 int64_t ld_v, const int64_t* offsets, int B, int N, int max_len,
+                                 int H, int dqk, int dv, const uint8_t* bucket_map,
+                                 const float* pos_w, const float* ts_w, int num_buckets, float* out,
+                                 int64_t ld_out, const GrBoundaryFwd* bnd, void* stream) {
+  using namespace gr;
+  GR_REQUIRE(bnd, "hstu_attn_fwd_bnd: null boundary");
+  const GrBoundaryFwd& g = *bnd;
+  GR_REQUIRE(g.u && g.w_o && g.y && g.attn_stats && g.hdv > 0 && g.D > 0,
+             "hstu_attn_fwd_bnd: boundary null pointer or bad sizes");
+  GR_REQUIRE(!g.w_uvqk || (g.uvqk && g.x_stats && g.n_out > 0),
+             "hstu_attn_fwd_bnd: next-layer LN / UVQK null pointer");
+  BndFwdCtx bc{};
+  bc.a1 = RwArgsGateO{offsets, B, g.hdv, g.D, g.u, g.ld_u, out, ld_out, g.w_o, g.b_o, g.x_res,
+                      g.ld_x, g.eps, g.dropout_p, g.seed, g.seed_offset, (float2*)g.attn_stats,
+                      g.o_in, g.y, g.ld_y};
+  bc.op2 = g.w_uvqk != nullptr;
+  if (bc.op2)
+    bc.a2 = RwArgsLnUvqk{offsets, B, g.D, g.n_out, g.y, g.ld_y, g.w_uvqk, g.eps, g.activation,
+                         (float2*)g.x_stats, g.h_pre, g.uvqk, g.ld_out};
+  const int ng = bc.op2 ? ceil_div(g.n_out, 16) : 13;
+  bc.nt2 = ng > 8 && ng <= 13 ? 13 : ng > 13 && ng <= 16 ? 16 : -1;
+  auto in_w4 = [](int x) { return x > 32 && x <= 64; };  // the W = 4 (64-column) instantiation
+  const bool aligned = pair_aligned({g.u, out, g.x_res, g.o_in, g.y, g.h_pre, g.uvqk},
+                                    {g.ld_u, ld_out, g.ld_x, g.ld_y, g.ld_out, g.hdv, g.D,
+                                     bc.op2 ? g.n_out : 2});
+  const bool fuse = option(GR_OPT_BOUNDARY_FUSE) != 0 && option(GR_OPT_ROWWAVE) != 0 && H == 1 &&
+                    bc.nt2 > 0 && in_w4(g.D) && in_w4(g.hdv) && g.hdv == H * dv && aligned &&
+                    g.max_rows * 4 * 1024 <= 0x7fffffffLL;
+  if (int rc = attn_fwd_impl(q, k, v, ld_qk, ld_v, offsets, B, N, max_len, H, dqk, dv, bucket_map,
+                             pos_w, ts_w, num_buckets, out, ld_out, stream, fuse ? &bc : nullptr))
+    return rc;
+  if (bc.fused) return 0;
+  if (bc.op2)
+    return hstu_boundary_fwd(g.u, g.ld_u, out, ld_out, offsets, B, g.max_rows, g.hdv, g.D, g.w_o,
+                             g.b_o, g.x_res, g.ld_x, g.eps, g.dropout_p, g.seed, g.seed_offset,
+                             g.attn_stats, g.o_in, g.y, g.ld_y, g.w_uvqk, g.n_out, g.activation,
+                             g.x_stats, g.h_pre, g.uvqk, g.ld_out, stream);
+  return hstu_gate_o_fwd(g.u, g.ld_u, out, ld_out, offsets, B, g.max_rows, g.hdv, g.D, g.w_o, g.b_o,
+                         g.x_res, g.ld_x, g.eps, g.dropout_p, g.seed, g.seed_offset, g.attn_stats,
+                         g.o_in, g.y, g.ld_y, stream);
 }

@@ -42,17 +42,21 @@ template <int VEC>
 __device__ __forceinline__ int qcol(int tb, int lg, int e) {
   return VEC == 4 ? tb + 4 * lg + e : tb + 2 * lg + (e & 1) + 8 * (e >> 1);
 }
+// aux: cache policy of the loads (16 = sc1: served by L2, not the CU's vector L1 -- rows
+// this wave stored in the same launch, whose L1 lines another wave may have filled first)
 template <int VEC>
 __device__ __forceinline__ f4 ldq(__amdgpu_buffer_rsrc_t r, int64_t row_off, int tb, int lg,
-                                  int N = 1 << 30) {
+                                  int N = 1 << 30, int aux = 0) {
   if constexpr (VEC == 4) {
     const int c = qcol<4>(tb, lg, 0);
-    const u4v v = __builtin_amdgcn_raw_buffer_load_b128(r, c < N ? (int)((row_off + c) * 4) : OOB, 0, 0);
+    const u4v v = aux ? __builtin_amdgcn_raw_buffer_load_b128(r, c < N ? (int)((row_off + c) * 4) : OOB, 0, 16)
+                      : __builtin_amdgcn_raw_buffer_load_b128(r, c < N ? (int)((row_off + c) * 4) : OOB, 0, 0);
     return f4{__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w)};
   } else {
     const int c0 = qcol<2>(tb, lg, 0), c2 = qcol<2>(tb, lg, 2);
-    const u2v a = __builtin_amdgcn_raw_buffer_load_b64(r, c0 < N ? (int)((row_off + c0) * 4) : OOB, 0, 0);
-    const u2v b = __builtin_amdgcn_raw_buffer_load_b64(r, c2 < N ? (int)((row_off + c2) * 4) : OOB, 0, 0);
+    const int o0 = c0 < N ? (int)((row_off + c0) * 4) : OOB, o2 = c2 < N ? (int)((row_off + c2) * 4) : OOB;
+    const u2v a = aux ? __builtin_amdgcn_raw_buffer_load_b64(r, o0, 0, 16) : __builtin_amdgcn_raw_buffer_load_b64(r, o0, 0, 0);
+    const u2v b = aux ? __builtin_amdgcn_raw_buffer_load_b64(r, o2, 0, 16) : __builtin_amdgcn_raw_buffer_load_b64(r, o2, 0, 0);
     return f4{__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(b.x), __uint_as_float(b.y)};
   }
 }
@@ -136,6 +140,50 @@ __device__ __forceinline__ void rw_stage_w(const Op& op, float* Wl) {
     }
   }
 }
+
+// rw_stage_w split in two: load() issues the panel's loads into registers (e.g. before other
+// work of the kernel, so they land meanwhile), store() writes them to LDS later (the same
+// layout and values as rw_stage_w).  ITER <= 64 loads per thread.
+template <int KG, int NT, class Op>
+struct RwStage {
+  using C = RowWaveCfg<KG, NT>;
+  static constexpr int VEC = Op::VEC;
+  static constexpr int FP = Op::K_CONTIG ? C::KP : C::NP;
+  static constexpr int SP = Op::K_CONTIG ? C::NP : C::KP;
+  static constexpr int FP2 = FP <= 16 ? 16 : FP <= 32 ? 32 : FP <= 64 ? 64 : FP <= 128 ? 128 : 256;
+  static constexpr int SSTEP = 256 / FP2;
+  static constexpr int ITER = SP / SSTEP;
+  static_assert(ITER <= 64, "one batch of loads");
+  float v[ITER];
+  __device__ __forceinline__ void load(const Op& op) {
+    const int tid = threadIdx.x;
+    const int f = tid % FP2, s0 = tid / FP2;
+    const int64_t wlast = (int64_t)(op.K - 1) * op.bks() + (int64_t)(op.N - 1) * op.bns() + 1;
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)op.w, 0, (int)(wlast * 4 < 0x7fffffff ? wlast * 4 : 0x7fffffff), 0x00020000);
+#pragma unroll
+    for (int i = 0; i < ITER; ++i) {
+      const int sl = s0 + i * SSTEP;
+      const int k = Op::K_CONTIG ? f : sl;
+      const int p = Op::K_CONTIG ? sl : f;
+      const int n = (p & ~15) + qcol<VEC>(0, (p & 15) >> 2, p & 3);
+      const bool ok = f < FP && k < op.K && n < op.N;
+      v[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+          rw, ok ? (int)(((int64_t)k * op.bks() + (int64_t)n * op.bns()) * 4) : OOB, 0, 0));
+    }
+  }
+  __device__ __forceinline__ void store(float* Wl) const {
+    const int tid = threadIdx.x;
+    const int f = tid % FP2, s0 = tid / FP2;
+    if (f < FP) {
+#pragma unroll
+      for (int i = 0; i < ITER; ++i) {
+        const int sl = s0 + i * SSTEP;
+        Wl[(Op::K_CONTIG ? f : sl) * C::LDW + (Op::K_CONTIG ? sl : f)] = v[i];
+      }
+    }
+  }
+};
 
 // acc[t] = sum_k W'(k, 16 t + .) a(k): the row-wave k-step loop of rowwave_kernel
 template <int KG, int NT, int VEC>
@@ -465,6 +513,7 @@ struct RwGateO {
   float* o_in;
   float* y;
   int64_t ldy;
+  int rd_aux = 0;  // cache policy of the attn loads (16: rows stored earlier in the launch)
   __amdgpu_buffer_rsrc_t ru, ra, rx, ro, ry, rb;
   uint64_t seed_eff;
   struct Src { f4 v[KG]; f4 uu[KG]; };
@@ -482,7 +531,7 @@ struct RwGateO {
   __device__ void load(Src& s, int64_t m, int lg) const {
 #pragma unroll
     for (int g = 0; g < KG; ++g) {
-      s.v[g] = ldq<VEC>(ra, m * lda, 16 * g, lg, K);
+      s.v[g] = ldq<VEC>(ra, m * lda, 16 * g, lg, K, rd_aux);
       s.uu[g] = ldq<VEC>(ru, m * ldu, 16 * g, lg, K);
     }
   }
@@ -865,6 +914,7 @@ struct RwLnUvqkBwd {
   int64_t lddy;
   float* dx;
   int64_t lddx;
+  int rd_aux = 0;  // cache policy of the dh loads (16: rows stored earlier in the launch)
   __amdgpu_buffer_rsrc_t rdh, rx, rdy, rdx;
   struct Src { f4 v[KG]; };
   __device__ int bks() const { return 1; }
@@ -877,7 +927,7 @@ struct RwLnUvqkBwd {
   }
   __device__ void load(Src& s, int64_t m, int lg) const {
 #pragma unroll
-    for (int g = 0; g < KG; ++g) s.v[g] = ldq<VEC>(rdh, m * lddh, 16 * g, lg, K);
+    for (int g = 0; g < KG; ++g) s.v[g] = ldq<VEC>(rdh, m * lddh, 16 * g, lg, K, rd_aux);
   }
   __device__ void prep(const Src& s, float (&a)[KG][4], int64_t, bool, int) const {
 #pragma unroll

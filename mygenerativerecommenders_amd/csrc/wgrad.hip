@@ -949,29 +949,27 @@ static int wgrad_run(const WgradProb* in, int np, const int64_t* offsets, int B,
 }
 
 // ---------------------------------------------------------------- narrow streaming form
-// Ka <= 64, Nb <= 256, Ka + Nb <= 264, even widths, contiguous 16-byte aligned rows, f32
-// (ml-1m: per layer _uvqk 50 x 200 over LN(x) rows and _o 50 x 50 over dy rows; the 8
-// problems of an encoder backward in one launch).
-// Workgroup = one (problem, row split), 8 waves, one per CU.  The split's rows stream
-// through a 4-deep LDS ring of 32-row chunks by LDS-DMA (buffer_load_dwordx4 ... lds: each
-// wave instruction moves 1 KB of contiguous rows, no VGPRs; rows >= offsets[B] land as
-// exact zeros from the descriptor's per-dword range check), one barrier per chunk.  The
-// MFMA fragments are read from the chunk with the columns PERMUTED so that one 8-byte LDS
-// read feeds several MFMAs:
+// Ka <= 64, Nb <= 256, even widths and strides, f32 (ml-1m: per layer _uvqk 50 x 200 over
+// LN(x) rows and _o 50 x 50 over dy rows; the 8 problems of an encoder backward in one
+// launch).  No LDS staging: a lane loads its MFMA operands straight from the row-major
+// operands as 8- / 16-byte pieces, with the columns PERMUTED so that one piece feeds four
+// MFMAs:
 //   A fragment of ka-tile ct:  lane (lr, lg) = A'[row 4 s + lg][ka 4 lr + ct]
 //   B fragment of nb-tile t of 64-column group gi:  B[row 4 s + lg][64 gi + 4 lr + t]
-// Wave (gi, th, ph) runs the 8 MFMAs (ct 0..3) x (t = 2 th, 2 th + 1) of the k-steps
-// ph, ph + P, ... of each chunk (NG = ceil(Nb / 64) column groups, P = 4 / NG phases);
-// accumulator (ct, t) holds C[ka 16 lg + 4 r + ct][nb 64 gi + 4 lr + t].  The phases
-// meet in LDS by a fixed pairwise tree and the workgroup writes one slab; ws_reduce sums
-// each problem's slabs in split order.  Splits per problem are proportional to its column
-// groups (MFMA work per row), ~one workgroup per CU in total.  Deterministic: k-ordered
-// MFMA chains, a fixed tree, a fixed split order.  (Operands loaded per lane straight into
-// MFMA fragments instead -- 64-byte row segments, or 8/16-byte pieces: 2.4-2.8 TB/s.)
+// so a lane's float4 of A (two 8-byte loads) and of B (one 16-byte load, or two 8-byte)
+// are the operands of the 16 MFMAs (ct, t) of the k-step, and accumulator (ct, t) holds
+// C[ka 16 lg + 4 r + ct][nb 64 gi + 4 lr + t].  Workgroup = one (problem, row split), 8
+// waves = NG column groups x P row phases (NG = ceil(Nb / 64), P = 8 / NG); wave (gi, ph)
+// takes k-steps ph, ph + P, ..., WS_DEPTH of them in flight.  The phases meet in LDS by a
+// fixed pairwise tree and the workgroup writes one slab; ws_reduce sums each problem's
+// slabs in split order.  Splits per problem are proportional to its column groups (MFMA
+// work per row), ~one workgroup per CU in total.  Deterministic: k-ordered MFMA chains, a
+// fixed tree, a fixed split order.  Measured at C2 (scripts/wgrad_micro.py, 8 problems):
+// 52 us against 79 us for the LDS-staged panels; a dword-per-lane mapping (four 64-byte
+// row segments per instruction, B re-read per ka-tile) 61 us, 16 waves with 8 MFMAs each
+// 57 us, a 4-deep LDS-DMA ring of 32-row chunks 85 us.
 constexpr int WS_THREADS = 512;
-constexpr int WS_NBUF = 4;       // chunks in the ring
-constexpr int WS_KD = 5;         // DMA instructions per wave per chunk (<= 40 KB chunks)
-constexpr int WS_CHUNK_MAX = 35 * 1024;
+constexpr int WS_DEPTH = 4;
 
 struct WsProb {
   const float* a;
@@ -981,9 +979,8 @@ struct WsProb {
   int64_t ldb;
   int Ka, Nb, NC;  // NC = Nb + 1: slab column Nb holds the column sum of A'
   int ng;          // 64-column groups of Nb (1, 2, 4)
+  int vb;          // B piece: 4 = one 16-byte load (Nb, ldb % 4 == 0, 16-byte base), 2 = two 8-byte
   int splits;      // row splits = workgroups of this problem
-  int ia, ib, is;  // 1 KB DMA pieces per chunk: A rows, B rows, stats
-  int cb;          // chunk bytes in LDS ((ia + ib + is) KB)
   float* slabs;    // [splits][Ka][NC]
   float* c;
   float* colsum;
@@ -997,141 +994,125 @@ struct WsArgs {
   int B;
 };
 
-constexpr int WS_XCH = 36;  // floats per lane in the phase exchange: 32 accumulators + 4 column sums
+constexpr int WS_XCH = 68;  // floats per lane in the phase exchange: 64 accumulators + 4 column sums
 
-// One LDS-DMA instruction: each lane's 16 bytes at byte goff of r land at LDS byte
-// lds + 16 lane.  Inline asm (M0 saved and restored in the same statement): hipcc does not
-// count it, so it cannot add the vmcnt(0) it otherwise puts before every LDS read that the
-// DMA might alias (that drained the whole ring once per chunk); the kernel waits for the
-// ring with its own counted vmcnt + barrier.
-__device__ __forceinline__ void ws_dma(__amdgpu_buffer_rsrc_t r, const char* lds, int goff) {
-  const uint32_t la = __builtin_amdgcn_readfirstlane(
-      (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)lds);
-  uint32_t keep;
-  asm volatile(
-      "s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-      "buffer_load_dwordx4 %1, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(goff), "s"(la), "s"(r)
-      : "memory");
-}
-
-template <int P>
+template <int P, int VB, int DEPTH>
 __device__ __forceinline__ void ws_body(const WsProb& g, int64_t total, int split, char* smem) {
-  constexpr int NG = 4 / P;
-  constexpr int NW = 2 * NG;  // waves per phase
+  constexpr int NG = 8 / P;
   const int w = wave_id(), lane = threadIdx.x & 63;
-  const int gi = (w >> 1) % NG, th = w & 1, ph = w / NW;
+  const int gi = w % NG, ph = w / NG;
   const int lr = lane & 15, lg = lane >> 4;
-  const int64_t rps = ((total + g.splits - 1) / g.splits + 31) & ~(int64_t)31;
+  // this split's rows [r0, r1); r0 a multiple of 4 P (the phases' k-steps align)
+  const int64_t step = 4 * P;
+  const int64_t rps = ((total + g.splits - 1) / g.splits + step - 1) / step * step;
   const int64_t r0 = (int64_t)split * rps;
   const int64_t r1 = min(total, r0 + rps);
-  const int nch = __builtin_amdgcn_readfirstlane(r1 > r0 ? (int)((r1 - r0 + 31) >> 5) : 0);
-  // rows >= total read as 0 (per-dword range check), so A' = (0 - 0) * 0 and B = 0 there
+  const int nks = __builtin_amdgcn_readfirstlane(r1 > r0 ? (int)((r1 - r0 + 3) >> 2) : 0);
+  const int mine = nks > ph ? (nks - ph + P - 1) / P : 0;
+  // rows >= total read 0 (per-dword range check): A, its stats and B, so A' = 0 there
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)g.a, 0, (int)(total * g.Ka * 4), 0x00020000);
+      (void*)g.a, 0, (int)(total * g.lda * 4), 0x00020000);
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)g.bm, 0, (int)(total * g.Nb * 4), 0x00020000);
+      (void*)g.bm, 0, (int)(total * g.ldb * 4), 0x00020000);
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(g.a_stats ? (const void*)g.a_stats : (const void*)g.a), 0,
       g.a_stats ? (int)(total * 8) : 0, 0x00020000);
-  char* dummy = smem + WS_NBUF * WS_CHUNK_MAX;  // 1 KB sink of the padding instructions
-  const int npiece = g.ia + g.ib + g.is;
-  // chunk c into ring slot c % NBUF: piece i (1 KB) by wave i % 8; every wave issues
-  // exactly WS_KD instructions per chunk (out-of-range ones into the sink) so one
-  // constant vmcnt covers the ring
-  auto dma = [&](int c) {
-    char* buf = smem + (c & (WS_NBUF - 1)) * WS_CHUNK_MAX;
-    const bool live = c < nch;
-    const int row0 = (int)r0 + 32 * c;
-#pragma unroll
-    for (int k = 0; k < WS_KD; ++k) {
-      const int i = w + 8 * k;
-      if (live && i < g.ia) {
-        ws_dma(ra, buf + 1024 * i, row0 * g.Ka * 4 + 1024 * i + 16 * lane);
-      } else if (live && i < g.ia + g.ib) {
-        const int j = i - g.ia;
-        ws_dma(rb, buf + 1024 * i, row0 * g.Nb * 4 + 1024 * j + 16 * lane);
-      } else if (live && i < npiece) {
-        ws_dma(rs, buf + 1024 * i, row0 * 8 + 16 * lane);
-      } else {
-        ws_dma(ra, dummy, 0x40000000);
-      }
+  constexpr int OOBW = 0x40000000;
+  const int acol = 4 * lr, bcol = 64 * gi + 4 * lr;
+  const bool a_lo = acol < g.Ka, a_hi = acol + 2 < g.Ka;  // Ka even: 8-byte pieces in or out
+  const bool b_lo = bcol < g.Nb, b_hi = bcol + 2 < g.Nb;
+
+  f4 av[DEPTH], bv[DEPTH];
+  float2 sv[DEPTH];
+  auto issue = [&](int u, int j) {
+    const bool in = j < mine;
+    const int row = (int)(r0 + 4 * (ph + P * j)) + lg;
+    const int ao = row * (int)g.lda + acol, bo = row * (int)g.ldb + bcol;
+    const u32x2_t a0 = __builtin_amdgcn_raw_buffer_load_b64(ra, in && a_lo ? ao * 4 : OOBW, 0, 0);
+    const u32x2_t a1 = __builtin_amdgcn_raw_buffer_load_b64(ra, in && a_hi ? ao * 4 + 8 : OOBW, 0, 0);
+    av[u] = f4{__uint_as_float(a0.x), __uint_as_float(a0.y), __uint_as_float(a1.x), __uint_as_float(a1.y)};
+    if (g.a_stats) {
+      const u32x2_t st = __builtin_amdgcn_raw_buffer_load_b64(rs, in ? row * 8 : OOBW, 0, 0);
+      sv[u] = make_float2(__uint_as_float(st.x), __uint_as_float(st.y));
+    } else {
+      sv[u] = make_float2(0.f, 1.f);
+    }
+    if constexpr (VB == 4) {
+      const u32x4_t b = __builtin_amdgcn_raw_buffer_load_b128(rb, in && b_lo ? bo * 4 : OOBW, 0, 0);
+      bv[u] = f4{__uint_as_float(b.x), __uint_as_float(b.y), __uint_as_float(b.z), __uint_as_float(b.w)};
+    } else {
+      const u32x2_t b0 = __builtin_amdgcn_raw_buffer_load_b64(rb, in && b_lo ? bo * 4 : OOBW, 0, 0);
+      const u32x2_t b1 = __builtin_amdgcn_raw_buffer_load_b64(rb, in && b_hi ? bo * 4 + 8 : OOBW, 0, 0);
+      bv[u] = f4{__uint_as_float(b0.x), __uint_as_float(b0.y), __uint_as_float(b1.x), __uint_as_float(b1.y)};
     }
   };
-  const int offB = 1024 * g.ia, offS = 1024 * (g.ia + g.ib);
-  const int acol = 4 * lr, bcol = 64 * gi + 4 * lr + 2 * th;
-  f4 acc[4][2];  // [ct][t - 2 th]
+
+  f4 acc[4][4];  // [ct][t]
 #pragma unroll
-  for (int ct = 0; ct < 4; ++ct) acc[ct][0] = acc[ct][1] = f4_zero();
-  f4 csum = f4_zero();  // A'[row][4 lr + ct] over this wave's rows (the _o bias gradient)
-  const bool ln = g.a_stats != nullptr;
+  for (int ct = 0; ct < 4; ++ct)
 #pragma unroll
-  for (int c = 0; c < WS_NBUF - 1; ++c) dma(c);
-  for (int c = 0; c < nch; ++c) {
-    // chunk c landed (the two newer chunks' 2 x WS_KD instructions may still fly), and
-    // every wave is past chunk c - 1, whose slot the next DMA refills
-    asm volatile("s_waitcnt vmcnt(10)\n\ts_barrier" ::: "memory");
-    dma(c + WS_NBUF - 1);
-    const char* buf = smem + (c & (WS_NBUF - 1)) * WS_CHUNK_MAX;
+    for (int t = 0; t < 4; ++t) acc[ct][t] = f4_zero();
+  f4 csum = f4_zero();  // A'[row][4 lr + ct] summed over this wave's rows (the _o bias gradient)
+  if (mine > 0) {
 #pragma unroll
-    for (int s = ph; s < 8; s += P) {
-      const int row = 4 * s + lg;
-      const float* arow = reinterpret_cast<const float*>(buf) + row * g.Ka + acol;
-      const float2 a01 = *reinterpret_cast<const float2*>(arow);
-      const float2 a23 = *reinterpret_cast<const float2*>(arow + 2);
-      const float2 b = *reinterpret_cast<const float2*>(buf + offB + 4 * (row * g.Nb + bcol));
-      f4 a = f4{a01.x, a01.y, a23.x, a23.y};
-      if (ln) {
-        const float2 st = *reinterpret_cast<const float2*>(buf + offS + 8 * row);
+    for (int u = 0; u < DEPTH; ++u) issue(u, u);
+    const int iters = (mine + DEPTH - 1) / DEPTH * DEPTH;
+    for (int j0 = 0; j0 < iters; j0 += DEPTH) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) a[e] = (a[e] - st.x) * st.y;
-      }
-      csum += a;
+      for (int u = 0; u < DEPTH; ++u) {
+        f4 a = av[u];
+        if (g.a_stats) {
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct) {
-        acc[ct][0] = mfma16x16x4(a[ct], b.x, acc[ct][0]);
-        acc[ct][1] = mfma16x16x4(a[ct], b.y, acc[ct][1]);
+          for (int e = 0; e < 4; ++e) a[e] = (a[e] - sv[u].x) * sv[u].y;  // rows out of range: 0 * 0
+        }
+        csum += a;
+        const f4 b = bv[u];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) acc[ct][t] = mfma16x16x4(a[ct], b[t], acc[ct][t]);
+        __builtin_amdgcn_sched_barrier(0);
+        issue(u, j0 + u + DEPTH);
       }
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");  // the ring is free for the exchange
   // column sums over the k-step rows (lanes lr, lr + 16, lr + 32, lr + 48), fixed order
 #pragma unroll
   for (int e = 0; e < 4; ++e) csum[e] = wg_colsum_lanes(csum[e]);
   // phases meet pairwise in LDS: round s, phases s .. 2s - 1 hand their sums to phase - s
-  float* xch = reinterpret_cast<float*>(smem);  // [P / 2 slots][NW][WS_XCH][64]
-  const int wi = w % NW;
+  float* xch = reinterpret_cast<float*>(smem);  // [P / 2 slots][NG][WS_XCH][64]
 #pragma unroll
   for (int s = P / 2; s >= 1; s >>= 1) {
     if (ph >= s && ph < 2 * s) {
-      float* x = xch + ((ph - s) * NW + wi) * WS_XCH * 64 + lane;
+      float* x = xch + ((ph - s) * NG + gi) * WS_XCH * 64 + lane;
 #pragma unroll
       for (int ct = 0; ct < 4; ++ct)
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
+        for (int t = 0; t < 4; ++t)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) x[((ct * 2 + t) * 4 + r) * 64] = acc[ct][t][r];
+          for (int r = 0; r < 4; ++r) x[((ct * 4 + t) * 4 + r) * 64] = acc[ct][t][r];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) x[(32 + e) * 64] = csum[e];
+      for (int e = 0; e < 4; ++e) x[(64 + e) * 64] = csum[e];
     }
     __syncthreads();
     if (ph < s) {
-      const float* x = xch + (ph * NW + wi) * WS_XCH * 64 + lane;
+      const float* x = xch + (ph * NG + gi) * WS_XCH * 64 + lane;
 #pragma unroll
       for (int ct = 0; ct < 4; ++ct)
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
+        for (int t = 0; t < 4; ++t)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) acc[ct][t][r] += x[((ct * 2 + t) * 4 + r) * 64];
+          for (int r = 0; r < 4; ++r) acc[ct][t][r] += x[((ct * 4 + t) * 4 + r) * 64];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) csum[e] += x[(32 + e) * 64];
+      for (int e = 0; e < 4; ++e) csum[e] += x[(64 + e) * 64];
     }
     __syncthreads();
   }
-  if (ph != 0 || bcol >= g.Nb) return;
+  if (ph != 0) return;
   float* slab = g.slabs + (int64_t)split * g.Ka * g.NC;
-  if (g.colsum && gi == 0 && th == 0 && lg == 0) {
+  // column sums of ka 4 lr .. 4 lr + 3 (a lane whose B columns lie past Nb still owns them)
+  if (g.colsum && gi == 0 && lg == 0) {
 #pragma unroll
     for (int e = 0; e < 4; ++e)
       if (acol + e < g.Ka) slab[(int64_t)(acol + e) * g.NC + g.Nb] = csum[e];
@@ -1142,9 +1123,9 @@ __device__ __forceinline__ void ws_body(const WsProb& g, int64_t total, int spli
     for (int r = 0; r < 4; ++r) {
       const int ka = 16 * lg + 4 * r + ct;
       if (ka >= g.Ka) continue;
-      // columns bcol, bcol + 1 (Nb even: both in range; NC = Nb + 1 is odd, so two dwords)
-      slab[(int64_t)ka * g.NC + bcol] = acc[ct][0][r];
-      slab[(int64_t)ka * g.NC + bcol + 1] = acc[ct][1][r];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        if (bcol + t < g.Nb) slab[(int64_t)ka * g.NC + bcol + t] = acc[ct][t][r];
     }
 }
 
@@ -1154,9 +1135,16 @@ __global__ __launch_bounds__(WS_THREADS) void wgrad_stream_kernel(WsArgs g) {
   const WsProb& p = g.p[i];
   const int split = blockIdx.x - g.wg0[i];
   const int64_t total = g.offsets[g.B];
-  if (p.ng == 1) ws_body<4>(p, total, split, smem);
-  else if (p.ng == 2) ws_body<2>(p, total, split, smem);
-  else ws_body<1>(p, total, split, smem);
+  const int P = 8 / p.ng;
+  if (p.vb == 4) {
+    if (P == 8) ws_body<8, 4, WS_DEPTH>(p, total, split, smem);
+    else if (P == 4) ws_body<4, 4, WS_DEPTH>(p, total, split, smem);
+    else ws_body<2, 4, WS_DEPTH>(p, total, split, smem);
+  } else {
+    if (P == 8) ws_body<8, 2, WS_DEPTH>(p, total, split, smem);
+    else if (P == 4) ws_body<4, 2, WS_DEPTH>(p, total, split, smem);
+    else ws_body<2, 2, WS_DEPTH>(p, total, split, smem);
+  }
 }
 
 // out = sum over a problem's splits in split order: thread (o, grp) of a 256-thread block
@@ -1194,14 +1182,11 @@ __global__ __launch_bounds__(256) void ws_reduce_kernel(WsArgs g) {
 }
 
 static int ws_ng(int nb) { return nb <= 64 ? 1 : nb <= 128 ? 2 : 4; }
-static int ws_pieces(int w) { return (128 * w + 1023) / 1024; }  // 1 KB DMA pieces of 32 rows
-// the streaming form: every problem Ka <= 64, Nb <= 256, even widths, rows contiguous
-// (ld == width) and 16-byte aligned bases, and a 32-row chunk within WS_CHUNK_MAX
+// the streaming form: every problem Ka <= 64, Nb <= 256, even widths and strides, 8-byte
+// aligned bases
 static bool ws_fits_shapes(const int* Ka, const int* Nb, int np) {
   for (int i = 0; i < np; ++i)
-    if (Ka[i] > 0 && (Ka[i] > 64 || Nb[i] > 256 || (Ka[i] | Nb[i]) & 1 ||
-                      1024 * (ws_pieces(Ka[i]) + ws_pieces(Nb[i]) + 1) > WS_CHUNK_MAX))
-      return false;
+    if (Ka[i] > 0 && (Ka[i] > 64 || Nb[i] > 256 || (Ka[i] | Nb[i]) & 1)) return false;
   return true;
 }
 static bool ws_fits(const WgradProb* in, int np) {
@@ -1211,13 +1196,13 @@ static bool ws_fits(const WgradProb* in, int np) {
     Ka[i] = p.a ? p.Ka : 0;
     Nb[i] = p.a ? p.Nb : 0;
     if (!p.a) continue;
-    if (p.lda != p.Ka || p.ldb != p.Nb || (uintptr_t)p.a % 16 || (uintptr_t)p.bm % 16 ||
-        (p.a_stats && (uintptr_t)p.a_stats % 16))
+    if ((p.lda | p.ldb) & 1 || (uintptr_t)p.a % 8 || (uintptr_t)p.bm % 8 ||
+        (p.a_stats && (uintptr_t)p.a_stats % 8))
       return false;
   }
   return ws_fits_shapes(Ka, Nb, np);
 }
-static size_t ws_lds() { return (size_t)WS_NBUF * WS_CHUNK_MAX + 1024; }
+static size_t ws_lds(int ng) { return sizeof(float) * (size_t)(8 / ng / 2) * ng * WS_XCH * 64; }
 
 struct WsPlan {
   int splits[WG_MAXP];
@@ -1272,16 +1257,13 @@ static int wgrad_run_stream(const WgradProb* in, int np, const int64_t* offsets,
     p.Nb = Nb[i];
     p.NC = Nb[i] + 1;
     p.ng = ws_ng(Nb[i]);
-    p.ia = ws_pieces(Ka[i]);
-    p.ib = ws_pieces(Nb[i]);
-    p.is = p.a_stats ? 1 : 0;
-    p.cb = 1024 * (p.ia + p.ib + p.is);
+    p.vb = (Nb[i] % 4 == 0 && p.ldb % 4 == 0 && (uintptr_t)p.bm % 16 == 0) ? 4 : 2;
     p.splits = pl.splits[i];
     p.slabs = (float*)(ws + off);
     off += (pl.slab_bytes[i] + 255) & ~(size_t)255;
     p.c = in[i].c;
     p.colsum = in[i].colsum;
-    lds = ws_lds();
+    lds = std::max(lds, ws_lds(p.ng));
     g.wg0[g.np + 1] = g.wg0[g.np] + p.splits;
     g.blk0[g.np + 1] = g.blk0[g.np] + (int)(((int64_t)p.Ka * p.NC + 15) / 16);
     ++g.np;

@@ -255,6 +255,20 @@ def rel_bias(timestamps: torch.Tensor, N: int, pos_w: torch.Tensor,
 
 # ------------------------------------------------------------------ fused STU layer
 
+class GrBoundaryFwd(ctypes.Structure):
+    """include/gr_hstu.h GrBoundaryFwd: the layer-boundary arguments of hstu_attn_fwd_bnd
+    (those of hstu_boundary_fwd; w_uvqk = NULL for the last layer: gate_o alone)."""
+    _fields_ = [("u", ctypes.c_void_p), ("ld_u", ctypes.c_int64), ("max_rows", ctypes.c_int64),
+                ("hdv", ctypes.c_int), ("D", ctypes.c_int), ("w_o", ctypes.c_void_p),
+                ("b_o", ctypes.c_void_p), ("x_res", ctypes.c_void_p), ("ld_x", ctypes.c_int64),
+                ("eps", ctypes.c_float), ("dropout_p", ctypes.c_float), ("seed", ctypes.c_uint64),
+                ("seed_offset", ctypes.c_void_p), ("attn_stats", ctypes.c_void_p),
+                ("o_in", ctypes.c_void_p), ("y", ctypes.c_void_p), ("ld_y", ctypes.c_int64),
+                ("w_uvqk", ctypes.c_void_p), ("n_out", ctypes.c_int), ("activation", ctypes.c_int),
+                ("x_stats", ctypes.c_void_p), ("h_pre", ctypes.c_void_p), ("uvqk", ctypes.c_void_p),
+                ("ld_out", ctypes.c_int64)]
+
+
 class GrBoundaryBwd(ctypes.Structure):
     """include/gr_hstu.h GrBoundaryBwd: the layer-boundary arguments of hstu_attn_bwd_bnd
     (those of hstu_boundary_bwd; hdv = 0 for the first layer: ln_uvqk_bwd alone)."""
@@ -351,15 +365,13 @@ def _stu_forward(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGeomet
             copies = torch.empty(cb, dtype=torch.uint8, device=dev)
             _lib.call("hstu_attn_bf16_copies", q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out,
                       n_out, offsets.data_ptr(), B, geo.N, H, dqk, dv, copies.data_ptr(), st)
+    attn_args = (q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out, n_out, offsets.data_ptr(), B,
+                 geo.N, geo.max_len, H, dqk, dv, _lib.ptr(bmap), _lib.ptr(pos_w_c),
+                 _lib.ptr(ts_w_c), NUM_BUCKETS, attn.data_ptr(), hv)
     if geo.bf16:
-        _lib.call("hstu_attn_fwd_bf16", q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out, n_out,
-                  offsets.data_ptr(), B, geo.N, geo.max_len, H, dqk, dv, _lib.ptr(bmap),
-                  _lib.ptr(pos_w_c), _lib.ptr(ts_w_c), NUM_BUCKETS, attn.data_ptr(), hv,
-                  _lib.ptr(copies), st)
-    else:
-        _lib.call("hstu_attn_fwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), n_out, n_out,
-                  offsets.data_ptr(), B, geo.N, geo.max_len, H, dqk, dv, _lib.ptr(bmap),
-                  _lib.ptr(pos_w_c), _lib.ptr(ts_w_c), NUM_BUCKETS, attn.data_ptr(), hv, st)
+        _lib.call("hstu_attn_fwd_bf16", *attn_args, _lib.ptr(copies), st)
+    elif geo.concat_ua:
+        _lib.call("hstu_attn_fwd", *attn_args, st)
     attn_stats = torch.empty(rows, 2, dtype=torch.float32, device=dev)
     needs_w_grad = grad_on and needs_w_grad
     ow = 3 * hv if geo.concat_ua else hv  # o_in width
@@ -372,18 +384,29 @@ def _stu_forward(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGeomet
     y = torch.empty(rows, D, dtype=torch.float32, device=dev)
     b_o_c = b_o.contiguous()
     pre_next = None
-    if next_w_uvqk is not None:
-        if geo.concat_ua or geo.bf16:
-            raise ValueError("hstu_boundary_fwd: fp32, no concat_ua")
-        w_next = next_w_uvqk.contiguous()
-        pre_next = _ln_uvqk_outputs(rows, n_out, geo, grad_on, dev)
-        nx_stats, nx_uvqk, nx_h_pre = pre_next
-        _lib.call("hstu_boundary_fwd", uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
-                  offsets.data_ptr(), B, rows, hv, D, w_o.data_ptr(), b_o_c.data_ptr(),
-                  x.data_ptr(), x.stride(0), geo.eps, geo.dropout_p, seed,
-                  _lib.ptr(seed_offset), attn_stats.data_ptr(), _lib.ptr(o_in), y.data_ptr(),
-                  D, w_next.data_ptr(), n_out, geo.activation, nx_stats.data_ptr(),
-                  _lib.ptr(nx_h_pre), nx_uvqk.data_ptr(), n_out, st)
+    if next_w_uvqk is not None and (geo.concat_ua or geo.bf16):
+        raise ValueError("hstu_boundary_fwd: fp32, no concat_ua")
+    if not geo.bf16 and not geo.concat_ua:
+        # the attention and this layer's gate_o (+ the next layer's LN + UVQK: the layer
+        # boundary) in one call; at narrow shapes the boundary runs as the attention
+        # launch's epilogue (hstu_attn_fwd_bnd)
+        bnd = GrBoundaryFwd(u=uvqk.data_ptr(), ld_u=n_out, max_rows=rows, hdv=hv, D=D,
+                            w_o=w_o.data_ptr(), b_o=b_o_c.data_ptr(), x_res=x.data_ptr(),
+                            ld_x=x.stride(0), eps=geo.eps, dropout_p=geo.dropout_p, seed=seed,
+                            seed_offset=_lib.ptr(seed_offset), attn_stats=attn_stats.data_ptr(),
+                            o_in=_lib.ptr(o_in), y=y.data_ptr(), ld_y=D)
+        if next_w_uvqk is not None:
+            w_next = next_w_uvqk.contiguous()
+            pre_next = _ln_uvqk_outputs(rows, n_out, geo, grad_on, dev)
+            nx_stats, nx_uvqk, nx_h_pre = pre_next
+            bnd.w_uvqk = w_next.data_ptr()
+            bnd.n_out = n_out
+            bnd.activation = geo.activation
+            bnd.x_stats = nx_stats.data_ptr()
+            bnd.h_pre = _lib.ptr(nx_h_pre)
+            bnd.uvqk = nx_uvqk.data_ptr()
+            bnd.ld_out = n_out
+        _lib.call("hstu_attn_fwd_bnd", *attn_args, ctypes.addressof(bnd), st)
     elif cat_wide:
         _lib.call("hstu_gate_o_cat_wide_fwd", uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
                   offsets.data_ptr(), B, rows, hv, D, w_o.data_ptr(), b_o_c.data_ptr(),
@@ -398,7 +421,7 @@ def _stu_forward(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGeomet
                   x.data_ptr(), x.stride(0), geo.eps, geo.dropout_p, seed,
                   _lib.ptr(seed_offset), attn_stats.data_ptr(), _lib.ptr(o_in), y.data_ptr(),
                   D, st)
-    else:
+    else:  # bf16 mode
         _lib.call("hstu_gate_o_fwd" + sfx, uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
                   offsets.data_ptr(), B, rows, hv, D, w_o.data_ptr(), b_o_c.data_ptr(),
                   x.data_ptr(), x.stride(0), geo.eps, geo.dropout_p, seed,

@@ -189,15 +189,17 @@ def test_library_is_gfx950_code_object():
     assert ctypes.sizeof(ctypes.c_void_p) == 8
 
 
-def test_boundary_struct_layout_matches_header(tmp_path):
-    """ops.GrBoundaryBwd (ctypes) has the C layout of include/gr_hstu.h's GrBoundaryBwd:
-    same size and field offsets, checked against gcc on the header itself."""
-    from mygenerativerecommenders_amd.ops import GrBoundaryBwd
+@pytest.mark.parametrize("struct", ["GrBoundaryBwd", "GrBoundaryFwd"])
+def test_boundary_struct_layout_matches_header(tmp_path, struct):
+    """ops.GrBoundaryBwd / GrBoundaryFwd (ctypes) have the C layout of include/gr_hstu.h's
+    structs: same size and field offsets, checked against gcc on the header itself."""
+    from mygenerativerecommenders_amd import ops
+    GrBoundaryBwd = getattr(ops, struct)
     names = [f[0] for f in GrBoundaryBwd._fields_]
     src = tmp_path / "layout.c"
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "gr_hstu.h"\nint main(void) {\n'
-                   '  printf("%zu\\n", sizeof(GrBoundaryBwd));\n'
-                   + "".join(f'  printf("%zu\\n", offsetof(GrBoundaryBwd, {n}));\n' for n in names)
+                   '  printf("%zu\\n", sizeof(' + struct + '));\n'
+                   + "".join(f'  printf("%zu\\n", offsetof({struct}, {n}));\n' for n in names)
                    + "  return 0;\n}\n")
     exe = tmp_path / "layout"
     subprocess.check_call(["gcc", "-I", os.path.dirname(_lib.HEADER_PATH), str(src), "-o", str(exe)])

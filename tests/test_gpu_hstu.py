@@ -463,9 +463,11 @@ def test_hstu_boundary_as_dq_epilogue_matches_separate(B, N0, D, hdv, blocks):
     ln_uvqk_bwd(0) alone) as the epilogue of the attention dQ launch at narrow single-head
     shapes (GR_OPT_BOUNDARY_FUSE, default on), against the attention backward and the
     boundary as separate launches (option 0), train mode with dropout and ragged lengths.
-    The epilogue is the row-wave unit of hstu_boundary_bwd, so the boundaries between
-    layers are bit-identical; the first layer's ln_uvqk_bwd alone may take the row panel
-    when separate (n_out > 128), so gradients agree to fp32 summation order: 2e-5 relative.
+    The epilogues are the row-wave units of hstu_boundary_fwd / _bwd (same operation
+    order; hipcc may contract multiply-adds differently inside another kernel: the forward
+    agrees to 1e-6 relative), and the first layer's ln_uvqk_bwd alone may take the row
+    panel when separate (n_out > 128), so gradients agree to fp32 summation order: 2e-5
+    relative.  Also the forward epilogue (hstu_attn_fwd_bnd) is exercised here.
     Shapes the epilogue does not cover (D = 256; h dv = 20) run the separate launches
     inside the call and are bit-identical."""
     from mygenerativerecommenders_amd import _lib
@@ -498,16 +500,18 @@ def test_hstu_boundary_as_dq_epilogue_matches_separate(B, N0, D, hdv, blocks):
             torch.cuda.synchronize()
             outs.append((y.detach(), xg.grad, {n: p.grad.clone() for n, p in enc.named_parameters()}))
     (y0, dx0, g0), (y1, dx1, g1) = outs
-    assert torch.equal(y0, y1)
     exact = D > 64 or hdv <= 32
 
-    def close(a, b, what):
+    def close(a, b, what, rel=2e-5):
         if exact:
             assert torch.equal(a, b), what
             return
         assert torch.isfinite(a).all(), what
         err = (a - b).abs().max().item()
-        assert err <= 2e-5 * (1 + b.abs().max().item()), (what, err)
+        assert err <= rel * (1 + b.abs().max().item()), (what, err)
+    # the epilogue is the same row-wave unit, but hipcc may contract its multiply-adds
+    # differently inside another kernel: the forward agrees to a few ulp
+    close(y0, y1, "y", 1e-6)
     close(dx0, dx1, "dx")
     for n in g0:
         close(g0[n], g1[n], n)

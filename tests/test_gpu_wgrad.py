@@ -58,7 +58,8 @@ def _check(got, ref, what):
 
 @pytest.mark.parametrize("stream", [1, 0])
 @pytest.mark.parametrize("Ka,Nb", [(50, 200), (256, 1024), (256, 256), (64, 64), (33, 17),
-                                   (256, 257), (128, 128), (16, 250), (64, 256), (50, 1)])
+                                   (256, 257), (128, 128), (16, 250), (64, 256), (50, 1),
+                                   (64, 32), (62, 30), (40, 100), (64, 130)])
 def test_wgrad_single_with_colsum(Ka, Nb, stream):
     """stream = GR_OPT_WGRAD_STREAM (Ka <= 64, Nb <= 256: the streaming form or the
     LDS-staged panels; other shapes ignore it)."""
@@ -95,7 +96,7 @@ def _single_with_colsum(L, Ka, Nb):
 
 @pytest.mark.parametrize("bf16", [False, True])
 @pytest.mark.parametrize("D,n_out,hv", [(50, 200, 50), (256, 1024, 256), (128, 512, 128),
-                                        (64, 256, 64)])
+                                        (64, 256, 64), (64, 128, 32), (48, 160, 40)])
 def test_wgrad2_layer_shapes(bf16, D, n_out, hv):
     """The layer's pair: (_uvqk: LN(x)^T d_uvqk, no colsum) + (_o: dy^T o_in, colsum)."""
     L = _lib()
