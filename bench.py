@@ -719,6 +719,11 @@ def main():
         "boundary_fwd": 2.0 * rows * D * D + 2.0 * rows * D * nout,
         "boundary_bwd": 2.0 * rows * D * D + 2.0 * rows * nout * D,
     }
+    # the attention launches that carry a layer boundary as their epilogue (ABI 14)
+    flops_per_launch["attn_fwd_bnd"] = fwd_f + flops_per_launch["boundary_fwd"]
+    flops_per_launch["attn_fwd_bnd1"] = fwd_f + flops_per_launch["gate_o_fwd"]
+    flops_per_launch["attn_bwd_dq_bnd"] = dq_f + flops_per_launch["boundary_bwd"]
+    flops_per_launch["attn_bwd_dq_bnd1"] = dq_f + flops_per_launch["ln_uvqk_bwd"]
     dominant = max(kern_total, key=kern_total.get)
     ach = flops_per_launch.get(dominant, 0.0) / (kern[dominant] * 1e-3) / 1e12 if kern[dominant] else 0.0
     traffic, traffic_src = None, None

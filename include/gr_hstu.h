@@ -40,7 +40,9 @@ GR_API int gr_version(void);
 /* Live per-kernel timing (measurement only; off by default).  When enabled, every
  * launch records a HIP event pair on its stream; gr_timing_query(kernel, ...) waits
  * for and drains that kernel's pairs, returning the summed device time and launch
- * count.  Kernel names: bucket_map, attn_fwd, attn_bwd_dkv, attn_bwd_dq,
+ * count.  Kernel names: bucket_map, attn_fwd, attn_bwd_dkv, attn_bwd_dq, attn_fwd_bnd
+ * (attention + layer boundary), attn_fwd_bnd1 (+ gate_o of the last layer), attn_bwd_dq_bnd
+ * (dQ + layer boundary), attn_bwd_dq_bnd1 (+ ln_uvqk_bwd of the first layer),
  * attn_bias_reduce, ln_uvqk_fwd, gate_o_fwd, gate_o_bwd, ln_uvqk_bwd, wgrad_partial,
  * wgrad_reduce, mips_pack, mips_select, mips_merge, cumsum, dense_to_jagged,
  * jagged_to_padded, l2_normalize, current_embeddings, sampled_softmax_fwd,

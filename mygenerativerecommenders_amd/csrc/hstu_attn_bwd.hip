@@ -1147,7 +1147,7 @@ static int launch_dq_bnd_k(const AttnBwdArgs& aq, BndCtx& bc, int grid, int nbia
   bc.a1.fill(o1);
   if (OP2) bc.a2.fill(o2);
   const size_t lds = RowWaveCfg<KG1, 4>::LDS_BYTES + (OP2 ? RowWaveCfg<4, 4>::LDS_BYTES : 0);
-  GR_TIMED("attn_bwd_dq", st, hipLaunchKernelGGL((attn_bwd_dq_bnd_kernel<KS, VT, KG1, 4, OP2>),
+  GR_TIMED(OP2 ? "attn_bwd_dq_bnd" : "attn_bwd_dq_bnd1", st, hipLaunchKernelGGL((attn_bwd_dq_bnd_kernel<KS, VT, KG1, 4, OP2>),
                                                  dim3(grid + nbias), dim3(256), lds, st, aq, nbias,
                                                  n_slabs, dpos_w, dts_w, o1, o2));
   GR_LAUNCH_CHECK("hstu_attn_bwd_bnd(dq + boundary)");

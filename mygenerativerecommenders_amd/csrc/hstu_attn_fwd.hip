@@ -280,7 +280,7 @@ static int launch_fwd_bnd_k(const AttnFwdArgs& a, int grid, BndFwdCtx& bc, hipSt
   const size_t lds_w = RowWaveCfg<4, 4>::LDS_BYTES + (OP2 ? RowWaveCfg<4, NT2>::LDS_BYTES : 0);
   const size_t lds = lds_attn > lds_w ? lds_attn : lds_w;
   GR_REQUIRE(lds <= 160 * 1024, "hstu_attn_fwd_bnd: LDS %zu B exceeds 160 KiB (N=%d)", lds, a.N);
-  GR_TIMED("attn_fwd", st, hipLaunchKernelGGL((hstu_attn_fwd_bnd_kernel<KS, VT, HB, NT2, OP2>), dim3(grid),
+  GR_TIMED(OP2 ? "attn_fwd_bnd" : "attn_fwd_bnd1", st, hipLaunchKernelGGL((hstu_attn_fwd_bnd_kernel<KS, VT, HB, NT2, OP2>), dim3(grid),
                                               dim3(256), lds, st, a, o1, o2));
   GR_LAUNCH_CHECK("hstu_attn_fwd_bnd");
   bc.fused = true;

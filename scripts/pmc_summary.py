@@ -28,6 +28,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 _MAP = [
     (r"bucket_map_kernel", "bucket_map"),
+    # attention launches carrying a layer boundary (ABI 14): the last template flag = OP2
+    (r"attn_fwd_bnd_kernel<[^(]*true>", "attn_fwd_bnd"),
+    (r"attn_fwd_bnd_kernel<[^(]*false>", "attn_fwd_bnd1"),
+    (r"attn_bwd_dq_bnd_kernel<[^(]*true>", "attn_bwd_dq_bnd"),
+    (r"attn_bwd_dq_bnd_kernel<[^(]*false>", "attn_bwd_dq_bnd1"),
+    (r"wgrad_stream_kernel", "wgrad_partial"),
+    (r"ws_reduce_kernel", "wgrad_reduce"),
     (r"rowwave2_kernel<.*RwGateOBwd", "boundary_bwd"),
     (r"rowwave2_kernel", "boundary_fwd"),
     (r"mips_small_select_kernel", "mips_small"),
