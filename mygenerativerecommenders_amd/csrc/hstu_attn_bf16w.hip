@@ -25,16 +25,38 @@
 // the DMA's lane-linear image is the tile and both the A-fragment reads (ds_read_b128,
 // lanes = consecutive rows) and the transposed B reads need no per-lane address math.
 // Relative-bias gradients stay fp32 and deterministic: dpos_w per wave as plain stores of
-// each diagonal bin (a chunk's wrapped diagonals are carried into the next chunk, whose
-// main diagonals are the same bins), dts_w per lane as running (bucket, sum) flushed to
-// per-wave LDS histograms; one slab per wave, reduced in a fixed order.
+// each diagonal bin, summed through a per-wave LDS skew image (element (row R, key c) at
+// row 31 - c + R: a lane sums one diagonal with no shuffles; a chunk's wrapped diagonals
+// are carried into the next chunk, whose main diagonals are the same bins), dts_w per
+// lane as running (bucket, sum) flushed to per-wave LDS histograms (a chunk that extends
+// every lane's open run skips the per-element loop); one slab per wave, reduced in a
+// fixed order.
 #include "attn_common.h"
+#include <type_traits>
 #include "mfma32.h"
 
 
 #include "../../include/gr_hstu.h"
 
 namespace gr {
+
+#ifdef GR_STAMP
+// Diagnostic build only (-DGR_STAMP): per-wave phase cycle sums of the key-major kernel,
+// [workgroup][wave][12]: prologue, S/dP, elementwise, dV/dK, dS store + dts, barrier, dpos,
+// total, kind
+__device__ unsigned long long gr_stamp_bw_buf[1 << 16];
+#define BW_ST(i, dep)                                            \
+  do {                                                           \
+    asm volatile("" ::"v"(dep));                                 \
+    __builtin_amdgcn_sched_barrier(0);                           \
+    const unsigned long long t1_ = __builtin_amdgcn_s_memtime(); \
+    __builtin_amdgcn_sched_barrier(0);                           \
+    st_[i] += t1_ - st_t0;                                       \
+    st_t0 = t1_;                                                 \
+  } while (0)
+#else
+#define BW_ST(i, dep) do { } while (0)
+#endif
 
 // Chunk-major tiles: element (row r, column c) at byte ((c >> 3) * 32 + r) * 16 + (c & 7) * 2.
 // trB_acc / trB_nat on such a tile (rows = k): k-step s, columns 32 t .. 32 t + 31.
@@ -114,6 +136,7 @@ struct AttnBwdArgsW {
 
 constexpr int WK = 128;  // keys (queries) per workgroup: 4 waves x 32
 constexpr int kDtsCopies = 4;  // dts histogram copies per wave (lane % copies)
+constexpr int kSkew = 33;      // dpos skew image row stride (floats; odd: no bank conflicts)
 __host__ __device__ constexpr int w_dts_stride(int nb1) { return ((nb1 + 30) / 32) * 32 + 1; }
 
 // fp32 -> bf16 copies [row][head][32 D32] (blockIdx.y = tensor of the set), zero padding
@@ -370,6 +393,9 @@ __device__ __forceinline__ void kv_body(const AttnBwdArgsW& a, char* smem, int k
   float* posw = tsw + (a.nb + 1);
   const int tss = w_dts_stride(a.nb + 1);
   float* hts = posw + npos;  // [4 waves][kDtsCopies][tss]
+  // dpos skew image per wave: element (query row R, key lane lr) at row e = 31 - lr + R,
+  // column R ([64 rows][kSkew]); cells no element maps to stay 0
+  float* skw = hts + 4 * kDtsCopies * tss + wave_id() * 64 * kSkew;
 
   const int BH = a.B * a.H;
   const int rank = kt * BH + bh;  // slab index
@@ -381,6 +407,11 @@ __device__ __forceinline__ void kv_body(const AttnBwdArgsW& a, char* smem, int k
   const int lr = lane & 31, lh = lane >> 5;
   const int nbins = npos + a.nb + 1;
   float* slab = BIAS ? a.slabs + ((int64_t)rank * 4 + w) * nbins : nullptr;
+#ifdef GR_STAMP
+  unsigned long long st_[12] = {0, 0, 0, 0, 0, 0, 0, 0, KIND_K ? 1ull : 0ull, 0, 0, 0};
+  const unsigned long long st_start = __builtin_amdgcn_s_memtime();
+  unsigned long long st_t0 = st_start;
+#endif
   if (k0 >= L) {
     if (BIAS)
       for (int i = lane; i < nbins; i += 64) slab[i] = 0.f;
@@ -391,7 +422,7 @@ __device__ __forceinline__ void kv_body(const AttnBwdArgsW& a, char* smem, int k
     for (int i = tid; i < npos; i += 256) posw[i] = a.pos_w[i];
   }
   if (BIAS)
-    for (int i = tid; i < 4 * kDtsCopies * tss; i += 256) hts[i] = 0.f;
+    for (int i = tid; i < 4 * kDtsCopies * tss + 4 * 64 * kSkew; i += 256) hts[i] = 0.f;
   const int k0w = k0 + 32 * w;   // this wave's first key
   const int kj = k0w + lr;       // this lane's key (column of S / dP)
   const bool k_ok = kj < L;
@@ -424,6 +455,8 @@ __device__ __forceinline__ void kv_body(const AttnBwdArgsW& a, char* smem, int k
   // dpos: each bin of the wave's slab is written once: main diagonals of a chunk plus the
   // wrapped diagonals of the previous chunk (carry), see the file header
   float carry = 0.f;
+  int pend_bin = -1;  // dpos bin held back one chunk
+  float pend_v = 0.f;
 
   const int n_chunks = (L - k0 + 31) / 32;  // the workgroup's chunks: queries k0, k0 + 32, ...
   const bool w_on = k0w < L;
@@ -446,6 +479,7 @@ __device__ __forceinline__ void kv_body(const AttnBwdArgsW& a, char* smem, int k
   };
   dma(0, k0);
   __syncthreads();
+  BW_ST(0, kf[0].x);
   for (int ci = 0; ci < n_chunks; ++ci) {
     const int qc0 = k0 + 32 * ci;
     const char* Qs = tiles + (ci & 1) * 2 * TB;
@@ -471,6 +505,7 @@ __device__ __forceinline__ void kv_body(const AttnBwdArgsW& a, char* smem, int k
         }
       }
       __builtin_amdgcn_sched_barrier(0);
+      BW_ST(9, HB ? bias_t[15] + bias_p[15] : 0.f);
       // S (and dP) with the A fragments read PF k-steps ahead; two independent chains per
       // kind (S, dP or the even / odd k-steps of S)
       constexpr int PF = 4;
@@ -508,29 +543,39 @@ __device__ __forceinline__ void kv_body(const AttnBwdArgsW& a, char* smem, int k
         __builtin_amdgcn_sched_group_barrier(0x008, GR, 0);
         if (ks + PF < KS) __builtin_amdgcn_sched_group_barrier(0x100, GR, 0);
       }
+      BW_ST(1, S[0]);
+      BW_ST(1, dP[0]);
       if (!KIND_K) S += dP;
       float x16[16];
+      // interior chunks (every query after every key of the wave, all rows in range) need
+      // no causal / length mask: a mask-free instance of the elementwise pass
+      const bool full = qc0 >= k0w + 32 && qc0 + 32 <= L && k0w + 32 <= L;
+      auto elementwise = [&](auto full_tag) {
+        constexpr bool FULL = decltype(full_tag)::value;
 #pragma unroll
-      for (int rr = 0; rr < 16; ++rr) {
-        const int qi = qc0 + (rr & 3) + 8 * (rr >> 2) + 4 * lh;
-        const bool ok = k_ok && qi < L && kj <= qi;
-        float x = S[rr];
-        if (HB) {
-          float bp = bias_p[rr], bt = bias_t[rr];
-          asm volatile("" : "+v"(bp), "+v"(bt));  // keep the add here, after the products
-          x = x + (bp + bt);
+        for (int rr = 0; rr < 16; ++rr) {
+          float x = S[rr];
+          if (HB) {
+            float bp = bias_p[rr], bt = bias_t[rr];
+            asm volatile("" : "+v"(bp), "+v"(bt));  // keep the add here, after the products
+            x = x + (bp + bt);
+          }
+          const float sg = sigmoidf_(x);
+          const float v = KIND_K ? dP[rr] * (sg * (1.0f + x * (1.0f - sg))) * a.inv_n
+                                 : x * sg * a.inv_n;
+          if constexpr (FULL) {
+            x16[rr] = v;
+          } else {
+            const int qi = qc0 + (rr & 3) + 8 * (rr >> 2) + 4 * lh;
+            const bool ok = k_ok && qi < L && kj <= qi;
+            x16[rr] = __uint_as_float(__float_as_uint(v) & (ok ? 0xffffffffu : 0u));
+          }
         }
-        const float sg = sigmoidf_(x);
-        const uint32_t msk = ok ? 0xffffffffu : 0u;
-        if (!KIND_K) {
-          x16[rr] = __uint_as_float(__float_as_uint(x * sg * a.inv_n) & msk);
-        } else {
-          const float dsv = __uint_as_float(
-              __float_as_uint(dP[rr] * (sg * (1.0f + x * (1.0f - sg))) * a.inv_n) & msk);
-          x16[rr] = dsv;
-        }
-      }
+      };
+      if (full) elementwise(std::true_type{});
+      else elementwise(std::false_type{});
       const u32x4_t f0 = acc_frag(x16, 0), f1 = acc_frag(x16, 1);
+      BW_ST(2, f1.x);
       __builtin_amdgcn_sched_barrier(0);
       // acc += X^T B, B = dO (dV) or Q (dK) rows of the chunk, transposed reads
       const char* Bt = KIND_K ? Qs : Ds;
@@ -553,56 +598,81 @@ __device__ __forceinline__ void kv_body(const AttnBwdArgsW& a, char* smem, int k
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
         if (u + PB < NU) __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
       }
+      BW_ST(3, acc[D32 - 1][0]);
       if (KIND_K) {
         // dS block for the query-major pass: [key][query] image, registers 4g .. 4g+3 =
-        // queries 8g + 4lh + 0..3 (8-byte stores)
+        // queries 8g + 4lh + 0..3 (8-byte stores of the A fragments' packed pairs)
         const int qb = qc0 >> 5, kb = k0w >> 5;
         __bf16* blk = a.ds + ((int64_t)bh * a.nbt + qb * (qb + 1) / 2 + kb) * 1024;
+        const u32x4_t fr[2] = {f0, f1};
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const u32x2_t v2 = u32x2_t{pack_bf16(x16[4 * g], x16[4 * g + 1]),
-                                     pack_bf16(x16[4 * g + 2], x16[4 * g + 3])};
-          *reinterpret_cast<u32x2_t*>(blk + lr * 32 + 8 * g + 4 * lh) = v2;
-        }
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<u32x2_t*>(blk + lr * 32 + 8 * g + 4 * lh) =
+              u32x2_t{fr[g >> 1][2 * (g & 1)], fr[g >> 1][2 * (g & 1) + 1]};
       }
       if (BIAS) {
         // dts run (a lane's queries ascend with rr), after the math so that the branches
-        // do not split its schedule; the accumulator MFMAs above run meanwhile
+        // do not split its schedule; the accumulator MFMAs above run meanwhile.  A chunk
+        // whose 16 buckets equal every lane's open run (the common case: the lanes' time
+        // gaps share their log bucket across 32 queries) only extends the runs, in the
+        // same order as the general loop.
+        const uint32_t rb4 = (uint32_t)run_b * 0x01010101u;
+        const bool same = full && run_b >= 0 && mw[0] == rb4 && mw[1] == rb4 && mw[2] == rb4 &&
+                          mw[3] == rb4;
+        if (__builtin_amdgcn_ballot_w64(!same) == 0) {
 #pragma unroll
-        for (int rr = 0; rr < 16; ++rr) {
-          const int qi = qc0 + (rr & 3) + 8 * (rr >> 2) + 4 * lh;
-          const bool ok = k_ok && qi < L && kj <= qi;
-          const int bk = (mw[rr >> 2] >> (8 * (rr & 3))) & 0xFF;
-          if (ok && bk != run_b) {
-            if (run_b >= 0) atomicAdd(&wts[run_b], run_s);
-            run_b = bk;
-            run_s = 0.f;
+          for (int rr = 0; rr < 16; ++rr) run_s += x16[rr];
+        } else {
+#pragma unroll
+          for (int rr = 0; rr < 16; ++rr) {
+            const int qi = qc0 + (rr & 3) + 8 * (rr >> 2) + 4 * lh;
+            const bool ok = full || (k_ok && qi < L && kj <= qi);
+            const int bk = (mw[rr >> 2] >> (8 * (rr & 3))) & 0xFF;
+            if (ok && bk != run_b) {
+              if (run_b >= 0) atomicAdd(&wts[run_b], run_s);
+              run_b = bk;
+              run_s = 0.f;
+            }
+            run_s += x16[rr];  // 0 where !ok
           }
-          run_s += x16[rr];  // 0 where !ok
         }
       }
+      BW_ST(4, run_s);
       if (BIAS) {
-        // dpos: rotate register rr (row R = (rr & 3) + 8 (rr >> 2) + 4 lh) left by R in
-        // the 32-lane half: lane c then holds diagonal c (main) or c - 32 (wrapped)
-        float dmain = 0.f, dwrap = 0.f;
+        // dpos: element rr (row R = (rr & 3) + 8 (rr >> 2) + 4 lh, key lane lr) lies on the
+        // diagonal c = lr - R of the chunk.  Written to the wave's skew image at row
+        // e = 31 - c, column R (immediate offsets per rr), lane e then sums its row: lane
+        // 31 - c holds diagonal c >= 0 (main), lane 63 - c diagonal c - 32 (wrapped, the
+        // same bins as the next chunk's main diagonals: carried).  The wave's LDS
+        // operations complete in order, so the reads see the writes.
+        float* wr = skw + (31 - lr) * kSkew + (kSkew + 1) * 4 * lh;
 #pragma unroll
-        for (int rr = 0; rr < 16; ++rr) {
-          const int R = (rr & 3) + 8 * (rr >> 2) + 4 * lh;
-          const float v = __shfl(x16[rr], (lh << 5) | ((lr + R) & 31), 64);
-          const bool mn = lr + R < 32;
-          dmain += mn ? v : 0.f;
-          dwrap += mn ? 0.f : v;
-        }
-        auto sm = __builtin_amdgcn_permlane32_swap(__float_as_uint(dmain), __float_as_uint(dmain), false, false);
-        auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(dwrap), __float_as_uint(dwrap), false, false);
-        dmain = __uint_as_float(sm[0]) + __uint_as_float(sm[1]);
-        dwrap = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
-        const int bin = a.N - 1 + (k0w - qc0) + lr;  // diagonal kj - qi = k0w - qc0 + c - R
-        if (lh == 0 && bin >= 0 && bin < npos) slab[bin] = dmain + carry;
-        carry = dwrap;
+        for (int rr = 0; rr < 16; ++rr) wr[(kSkew + 1) * ((rr & 3) + 8 * (rr >> 2))] = x16[rr];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const float* rd = skw + lane * kSkew;
+        float rv[32];
+#pragma unroll
+        for (int R = 0; R < 32; ++R) rv[R] = rd[R];
+        float ps[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int R = 0; R < 32; ++R) ps[R & 3] += rv[R];
+        const float dsum = (ps[0] + ps[1]) + (ps[2] + ps[3]);
+        auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(dsum), __float_as_uint(dsum), false, false);
+        // lanes < 32: sw[0] = own (main, c = 31 - lane), sw[1] = lane + 32 (wrapped)
+        // the bin is stored at the next chunk (or the epilogue): a store issued here would
+        // hold the chunk's barrier until it completes
+        if (pend_bin >= 0) slab[pend_bin] = pend_v;
+        const int bin = a.N - 1 + (k0w - qc0) + (31 - lane);
+        pend_bin = lh == 0 && bin >= 0 && bin < npos ? bin : -1;
+        pend_v = __uint_as_float(sw[0]) + carry;
+        carry = __uint_as_float(sw[1]);
       }
+      BW_ST(6, carry);
     }
     if (more) __syncthreads();
+    BW_ST(5, lane);
   }
   // ---- epilogue: acc[t][rr] = (dV or dK)[key k0w + (rr & 3) + 8 (rr >> 2) + 4 lh][32 t + lr]
   float* outp = KIND_K ? a.dk : a.dvv;
@@ -616,10 +686,11 @@ __device__ __forceinline__ void kv_body(const AttnBwdArgsW& a, char* smem, int k
   if (BIAS) {
     // the last chunk's wrapped diagonals; zero every bin this wave never wrote: written
     // bins N-1 + d0 + [-32, 31] over d0 = k0w - qc0, qc0 = k0w .. last chunk
+    if (pend_bin >= 0) slab[pend_bin] = pend_v;
     int lo = npos, hi = -1;
     if (w_on) {
       const int d0_last = k0w - (k0 + 32 * (n_chunks - 1));
-      const int bin = a.N - 1 + d0_last - 32 + lr;
+      const int bin = a.N - 1 + d0_last - 32 + (31 - lr);
       if (lh == 0 && bin >= 0 && bin < npos) slab[bin] = carry;
       lo = a.N - 1 + d0_last - 32;
       hi = a.N - 1 + 31;
@@ -635,6 +706,15 @@ __device__ __forceinline__ void kv_body(const AttnBwdArgsW& a, char* smem, int k
       slab[npos + i] = s;
     }
   }
+#ifdef GR_STAMP
+  st_[7] = __builtin_amdgcn_s_memtime() - st_start;
+  if (lane < 12 && blockIdx.x * 48 + 48 <= (1 << 16)) {
+    unsigned long long v = 0;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) v = lane == i ? st_[i] : v;
+    gr_stamp_bw_buf[(blockIdx.x * 4 + w) * 12 + lane] = v;
+  }
+#endif
 }
 
 // workgroup i -> (sequence-head bh, slot j of per_seq): XCD x = i % 8 takes the
@@ -812,7 +892,7 @@ static int launch_bwd_bf16w(AttnBwdArgsW a, float* dpos_w, float* dts_w, hipStre
   constexpr int DP = 32 * D32, TB = 64 * DP;
   const size_t npos = 2 * a.N - 1;
   const int tss = w_dts_stride(a.nb + 1);
-  const size_t lds_kv = 4 * TB + sizeof(float) * ((a.nb + 1) + npos + 4 * kDtsCopies * tss);
+  const size_t lds_kv = 4 * TB + sizeof(float) * ((a.nb + 1) + npos + 4 * kDtsCopies * tss + 4 * 64 * kSkew);
   const size_t lds_q = 2 * TB + 4 * 2 * 2048;
   GR_REQUIRE(lds_kv <= 160 * 1024, "hstu_attn_bwd_bf16: LDS %zu B exceeds 160 KiB (N=%d)", lds_kv, a.N);
   const int grid = a.n_kt * a.B * a.H;
@@ -928,3 +1008,9 @@ int gr_attn_bwd_bf16w(const float* q, const float* k, const float* v, int64_t ld
   if (D32 == 7) return launch_bwd_bf16w<7>(a, dpos_w, dts_w, st);
   return launch_bwd_bf16w<8>(a, dpos_w, dts_w, st);
 }
+
+#ifdef GR_STAMP
+extern "C" __attribute__((visibility("default"))) int gr_stamp_bw_read(unsigned long long* host, int n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(gr::gr_stamp_bw_buf), sizeof(unsigned long long) * n) == hipSuccess ? 0 : 1;
+}
+#endif

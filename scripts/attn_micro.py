@@ -48,6 +48,8 @@ def main():
     ap.add_argument("--hepi", action="store_true",
                     help="fused silu'(h) epilogue on dQ/dK/dV (as in the training step)")
     ap.add_argument("--opt", action="append", default=[], help="launch option NAME=VALUE")
+    ap.add_argument("--stamp", action="store_true",
+                    help="print the wide bf16 key-major kernel's phase cycles (-DGR_STAMP library)")
     args = ap.parse_args()
     for o in args.opt:
         n, v = o.split("=")
@@ -140,6 +142,33 @@ def main():
                      "tflops": round(fl.get(name, 0) / (per_call * 1e-3) / 1e12, 2) if name in fl else None}
     print(json.dumps({"shape": args.shape, "bf16": args.bf16, "B": B, "N": N, "L": L, "d": d, "H": H,
                       "kernels": res}))
+    if args.stamp:
+        stamp_report(B * H, (L + 127) // 128)
+
+
+def stamp_report(BH, n_kt):
+    """Phase cycles per wave of the wide bf16 key-major launch (last call), by kind and key
+    tile: the workgroup -> (bh, key tile, kind) map is xcd_slot's (hstu_attn_bf16w.hip)."""
+    import ctypes
+    import numpy as np
+    raw = ctypes.CDLL(_lib.LIB_PATH)
+    per_seq = 2 * n_kt
+    grid = ((BH + 7) // 8) * 8 * per_seq
+    buf = (ctypes.c_ulonglong * (grid * 48))()
+    assert raw.gr_stamp_bw_read(buf, grid * 48) == 0
+    st = np.frombuffer(buf, dtype=np.uint64).reshape(grid, 4, 12).astype(np.float64)
+    names = ["prologue", "S_dP", "elementwise", "dV_dK", "dS_dts", "barrier", "dpos", "total", "kind", "lookups"]
+    rows = {}
+    for i in range(grid):
+        x, sl = i & 7, i >> 3
+        bh, j = (sl // per_seq) * 8 + x, sl % per_seq
+        if bh >= BH:
+            continue
+        rows.setdefault(("K" if j % 2 == 0 else "V", j >> 1), []).append(st[i])
+    for key in sorted(rows):
+        a = np.stack(rows[key])  # [wgs, 4 waves, 8]
+        print(f"{key[0]} kt={key[1]:2d} " + " ".join(
+            f"{n}={a[:, :, c].mean():8.0f}" for c, n in enumerate(names) if n != "kind"))
 
 
 if __name__ == "__main__":
