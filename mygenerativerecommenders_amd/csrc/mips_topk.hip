@@ -312,8 +312,9 @@ struct SelectArgs {
   const int64_t* inv_sorted;  // N0 > INV_MAX: [B][n0p] sorted lists (mips_sort_invalid_kernel)
 };
 
+// One (item range, query group) unit of the select kernel.
 template <int KS, int BLOCKS>
-__global__ __launch_bounds__(ST) void mips_select_kernel(SelectArgs a) {
+__device__ __forceinline__ void mips_select_unit(const SelectArgs& a, const int bid) {
   constexpr int KS2 = (KS + 1) / 2;
   constexpr int STEP = BLOCKS * 16;  // items per wave per step
   __shared__ float cs[QG * CAP];
@@ -323,13 +324,11 @@ __global__ __launch_bounds__(ST) void mips_select_kernel(SelectArgs a) {
   __shared__ int cnt[QG];
   __shared__ float tau_s[QG];
   __shared__ int need_compact;
-  if (a.gate && *a.gate == 0) return;
 
   const int tid = threadIdx.x, w = wave_id(), lane = tid & 63;
   const int lr = lane & 15, lg = lane >> 4;
   // XCD-aware decode: the query groups of one item range share blockIdx % 8
   const int n_qg = (a.B + QG - 1) / QG;
-  const int bid = blockIdx.x;
   const int xcd = bid & 7, rest = bid >> 3;
   const int g = rest % n_qg;
   const int range = (rest / n_qg) * 8 + xcd;
@@ -576,6 +575,19 @@ __global__ __launch_bounds__(ST) void mips_select_kernel(SelectArgs a) {
       a.part_score[o] = -INFINITY;
       a.part_index[o] = -1;
     }
+  }
+}
+
+// Units blockIdx.x, + gridDim.x, ... (gridDim.x a multiple of 8: a workgroup's units stay
+// on its XCD).  The gated fallback launches at most two workgroups per CU, so the common
+// case (flag clear) costs one small grid that exits at once instead of every unit's
+// workgroup being dispatched to read the flag.
+template <int KS, int BLOCKS>
+__global__ __launch_bounds__(ST) void mips_select_kernel(SelectArgs a, int n_units) {
+  if (a.gate && *a.gate == 0) return;
+  for (int bid = blockIdx.x; bid < n_units; bid += gridDim.x) {
+    mips_select_unit<KS, BLOCKS>(a, bid);
+    __syncthreads();  // the next unit rewrites the LDS lists
   }
 }
 
@@ -2155,8 +2167,10 @@ static int launch_select(const SelectArgs& a, hipStream_t st) {
   constexpr int BLOCKS = KS <= 16 ? 2 : 1;  // SW * 16 * BLOCKS <= CAP - 256
   const int n_qg = ceil_div(a.B, QG);
   const int n_r8 = ceil_div(a.n_ranges, 8) * 8;
-  const int grid = n_r8 * n_qg;
-  GR_TIMED(a.gate ? "mips_select_fallback" : "mips_select", st, hipLaunchKernelGGL((mips_select_kernel<KS, BLOCKS>), dim3(grid), dim3(ST), 0, st, a));
+  const int units = n_r8 * n_qg;
+  const int cap = 2 * ceil_div(device_cus(), 8) * 8;
+  const int grid = a.gate && units > cap ? cap : units;
+  GR_TIMED(a.gate ? "mips_select_fallback" : "mips_select", st, hipLaunchKernelGGL((mips_select_kernel<KS, BLOCKS>), dim3(grid), dim3(ST), 0, st, a, units));
   GR_LAUNCH_CHECK("mips_topk(select)");
   return 0;
 }
