@@ -67,11 +67,20 @@ __device__ __forceinline__ u32x4_t trB_acc_cm(const char* tile, int s, int t, in
                 hi = tr16(reinterpret_cast<const __bf16*>(base + 8 * 16));
   return u32x4_t{lo.x, lo.y, hi.x, hi.y};
 }
-__device__ __forceinline__ u32x4_t trB_nat_cm(const char* tile, int s, int t, int lane) {
+// The query-major pass's K tile is swizzled: row r of chunk k sits in slot r ^ 4 (k & 3).
+// A chunk is 512 B, so unswizzled the same row of chunks k .. k + 3 shares its LDS banks
+// and each transposed read below (lanes over 4 chunks x 4 rows) was a 4-way bank
+// conflict; swizzled, those 16 (chunk, row) pairs cover the 64 banks once (dQ 125 -> 118
+// us per C3 layer).  The key-major and forward tiles stay unswizzled: their readers'
+// extra address VALU cost more than their conflicts did (measured).
+__device__ __forceinline__ int swz_row(int r, int k) { return r ^ ((k & 3) << 2); }
+__device__ __forceinline__ u32x4_t trB_nat_cm_swz(const char* tile, int s, int t, int lane) {
   const int g = lane >> 4, h = lane >> 5, q = (lane & 15) >> 2, p = lane & 3;
-  const char* base = tile + ((4 * t + 2 * (g & 1) + (p >> 1)) * 32 + 16 * s + 8 * h + q) * 16 + 8 * (p & 1);
+  const int k = 2 * (g & 1) + (p >> 1);  // chunk 4 t + k
+  const char* base = tile + ((4 * t + k) * 32 + 16 * s + swz_row(8 * h + q, k)) * 16 + 8 * (p & 1);
+  const int d2 = (p >> 1) ? -4 : 4;      // rows + 4 flip bit 2, which the XOR sets for p >> 1
   const u32x2_t lo = tr16(reinterpret_cast<const __bf16*>(base)),
-                hi = tr16(reinterpret_cast<const __bf16*>(base + 4 * 16));
+                hi = tr16(reinterpret_cast<const __bf16*>(base + d2 * 16));
   return u32x4_t{lo.x, lo.y, hi.x, hi.y};
 }
 // A fragment (row lane % 32, k-step ks) of a chunk-major tile: 16 bytes
@@ -79,12 +88,13 @@ __device__ __forceinline__ u32x4_t frag_cm(const char* tile, int ks, int lane) {
   return *reinterpret_cast<const u32x4_t*>(tile + ((2 * ks + (lane >> 5)) * 32 + (lane & 31)) * 16);
 }
 // One 32-row tile of a bf16 copy into chunk-major LDS by LDS-DMA: DMA instruction i moves
-// chunks 2i, 2i + 1 (lane l: row l % 32, chunk 2i + l / 32, LDS byte 1024 i + 16 l); the
-// workgroup's 4 waves take i = w, w + 4, ...; rows >= L read the zero row.
-template <int D32>
+// chunks 2i, 2i + 1 (lane l: LDS byte 1024 i + 16 l = chunk 2i + l / 32, slot l % 32); the
+// workgroup's 4 waves take i = w, w + 4, ...; rows >= L read the zero row.  SWZ: slot l % 32
+// holds row swz_row(l % 32, chunk) (i has the parity of w: one source row per lane).
+template <int D32, bool SWZ = false>
 __device__ __forceinline__ void dma_tile(char* tile, const __bf16* rows, int64_t rsb, int r0, int L,
                                          const __bf16* zrow, int w, int lane) {
-  const int r = r0 + (lane & 31);
+  const int r = r0 + (SWZ ? swz_row(lane & 31, 2 * (w & 1) + (lane >> 5)) : (lane & 31));
   const __bf16* src = (r < L ? rows + (int64_t)r * rsb : zrow) + 8 * (lane >> 5);
 #pragma unroll
   for (int i = 0; i < 2 * D32; i += 4)
@@ -774,7 +784,7 @@ void attn_bwd_bf16w_dq_kernel(AttnBwdArgsW a) {
   const bool w_on = q0w < L;
   const __bf16* dsrow = a.ds + ((int64_t)bh * a.nbt + qb * (qb + 1) / 2) * 1024;
   auto dma = [&](int kb, int buf) {
-    dma_tile<D32>(kt_l + buf * TB, krows, rsb, 32 * kb, L, a.zrow, w, lane);
+    dma_tile<D32, true>(kt_l + buf * TB, krows, rsb, 32 * kb, L, a.zrow, w, lane);
     // the wave's 2 KB dS block (qb, kb): two 1 KB pieces, lane-linear
     const bool ok = w_on && kb <= qb;
 #pragma unroll
@@ -797,11 +807,11 @@ void attn_bwd_bf16w_dq_kernel(AttnBwdArgsW a) {
       constexpr int NU = 2 * D32, PB = 4;
       u32x4_t bq[PB];
 #pragma unroll
-      for (int u = 0; u < PB; ++u) bq[u] = trB_nat_cm(Kl, u / D32, u % D32, lane);
+      for (int u = 0; u < PB; ++u) bq[u] = trB_nat_cm_swz(Kl, u / D32, u % D32, lane);
 #pragma unroll
       for (int u = 0; u < NU; ++u) {
         const u32x4_t b0 = bq[u % PB];
-        if (u + PB < NU) bq[u % PB] = trB_nat_cm(Kl, (u + PB) / D32, (u + PB) % D32, lane);
+        if (u + PB < NU) bq[u % PB] = trB_nat_cm_swz(Kl, (u + PB) / D32, (u + PB) % D32, lane);
         acc[u % D32] = mfma32(u < D32 ? a0 : a1, b0, acc[u % D32]);
       }
 #pragma unroll
