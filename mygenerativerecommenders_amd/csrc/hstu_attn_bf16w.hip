@@ -8,10 +8,12 @@
 //
 // Layout of the work (one wave per SIMD, 512 registers: the 32 x d f32 accumulators of a
 // wave's 32 keys sit beside the keys' K / V fragments):
-//   * key-major pass, two workgroup kinds in one launch, 4 waves x 32 keys each:
-//       kind V: S (A = Q rows from LDS, B = K^T fragments in registers), P, dV += P^T dO;
-//       kind K: S, dP, dS, dK += dS^T Q, the relative-bias gradients, and the bf16 dS
-//               blocks for the query-major pass.
+//   * key-major dK pass, 4 waves x 32 keys each: S (A = Q rows from LDS, B = K^T
+//     fragments in registers), dP, dS, dK += dS^T Q, the relative-bias gradients, the bf16
+//     dS blocks for the query-major pass and the bf16 P blocks for the dV pass;
+//   * key-major dV pass: dV += P^T dO with P read back as the dK wave's A-fragment image
+//     (S and the sigmoid run once per element; a dV workgroup beside each dK workgroup
+//     used to recompute them);
 //     S / dP are 32 x 32 f32 tiles with the key on the lane and the queries in registers,
 //     so P and dS convert in place to the A operand of the next product (X^T B: no LDS
 //     round trip); its B operand (dO / Q rows, k = queries) comes from the row-major LDS
@@ -132,6 +134,8 @@ struct AttnBwdArgsW {
   int64_t ld_d;
   float* slabs;    // [grid_k][4 waves][2N-1 + nb+1]
   __bf16* ds;      // dS blocks: [bh][tri(qb, kb)][32 keys][32 queries]
+  __bf16* pb;      // P blocks, same index: the key-major dK wave's A-fragment image of P
+                   // (lane l: bytes 16 l and 1024 + 16 l), read back by the dV pass
   __bf16* qb;      // bf16 copies [row][head][32 D32] of Q, K, V, dO
   __bf16* kb;
   __bf16* vb;
@@ -241,11 +245,13 @@ void attn_fwd_bf16w_kernel(AttnFwdArgsW a) {
   float* tsw = reinterpret_cast<float*>(smem + 4 * TB);
   const int npos = 2 * a.N - 1;
   float* posw = tsw + (a.nb + 1);
-  // XCD-aware order: the query tiles of one (sequence, head) on one XCD, heaviest first
+  // XCD-aware order (x = i % 8 takes the sequence-heads x, x + 8, ...), query-tile-major:
+  // every XCD dispatches its heaviest query tiles (the last: most keys) first
   const int x = blockIdx.x & 7, sl = blockIdx.x >> 3;
-  const int bh = (sl / a.n_qt) * 8 + x;
+  const int nbh8 = (a.B * a.H + 7) >> 3;
+  const int bh = (sl % nbh8) * 8 + x;
   if (bh >= a.B * a.H) return;
-  const int qt = a.n_qt - 1 - sl % a.n_qt;
+  const int qt = a.n_qt - 1 - sl / nbh8;
   const int b = bh / a.H, h = bh % a.H;
   const int64_t s0 = a.offsets[b];
   const int L = (int)(a.offsets[b + 1] - s0);
@@ -391,7 +397,7 @@ void attn_fwd_bf16w_kernel(AttnFwdArgsW a) {
 
 // ------------------------------------------------------------------ key-major pass
 // KIND_K = false: dV += P^T dO;  true: dK += dS^T Q, bias gradients, dS blocks.
-template <int D32, bool HB, bool KIND_K>
+template <int D32, bool HB, bool KIND_K, bool PST = false>
 __device__ __forceinline__ void kv_body(const AttnBwdArgsW& a, char* smem, int kt, int bh) {
   constexpr int DP = 32 * D32;   // padded head dim
   constexpr int KS = DP / 16;    // k-steps of the S / dP products
@@ -560,6 +566,7 @@ __device__ __forceinline__ void kv_body(const AttnBwdArgsW& a, char* smem, int k
       // interior chunks (every query after every key of the wave, all rows in range) need
       // no causal / length mask: a mask-free instance of the elementwise pass
       const bool full = qc0 >= k0w + 32 && qc0 + 32 <= L && k0w + 32 <= L;
+      float p16[PST ? 16 : 1];
       auto elementwise = [&](auto full_tag) {
         constexpr bool FULL = decltype(full_tag)::value;
 #pragma unroll
@@ -575,10 +582,13 @@ __device__ __forceinline__ void kv_body(const AttnBwdArgsW& a, char* smem, int k
                                  : x * sg * a.inv_n;
           if constexpr (FULL) {
             x16[rr] = v;
+            if constexpr (PST) p16[rr] = x * sg * a.inv_n;
           } else {
             const int qi = qc0 + (rr & 3) + 8 * (rr >> 2) + 4 * lh;
             const bool ok = k_ok && qi < L && kj <= qi;
-            x16[rr] = __uint_as_float(__float_as_uint(v) & (ok ? 0xffffffffu : 0u));
+            const uint32_t msk = ok ? 0xffffffffu : 0u;
+            x16[rr] = __uint_as_float(__float_as_uint(v) & msk);
+            if constexpr (PST) p16[rr] = __uint_as_float(__float_as_uint(x * sg * a.inv_n) & msk);
           }
         }
       };
@@ -619,6 +629,12 @@ __device__ __forceinline__ void kv_body(const AttnBwdArgsW& a, char* smem, int k
         for (int g = 0; g < 4; ++g)
           *reinterpret_cast<u32x2_t*>(blk + lr * 32 + 8 * g + 4 * lh) =
               u32x2_t{fr[g >> 1][2 * (g & 1)], fr[g >> 1][2 * (g & 1) + 1]};
+        if constexpr (PST) {
+          // P of the same block as the dV pass's A fragments, 1 KB per store
+          char* pblk = reinterpret_cast<char*>(a.pb + ((int64_t)bh * a.nbt + qb * (qb + 1) / 2 + kb) * 1024);
+          *reinterpret_cast<u32x4_t*>(pblk + 16 * lane) = acc_frag(p16, 0);
+          *reinterpret_cast<u32x4_t*>(pblk + 1024 + 16 * lane) = acc_frag(p16, 1);
+        }
       }
       if (BIAS) {
         // dts run (a lane's queries ascend with rr), after the math so that the branches
@@ -727,26 +743,110 @@ __device__ __forceinline__ void kv_body(const AttnBwdArgsW& a, char* smem, int k
 #endif
 }
 
-// workgroup i -> (sequence-head bh, slot j of per_seq): XCD x = i % 8 takes the
-// sequence-heads x, x + 8, ... in turn (the grid is padded to a multiple of 8 of them)
-__device__ __forceinline__ void xcd_slot(const AttnBwdArgsW& a, int per_seq, int& bh, int& j) {
-  const int x = blockIdx.x & 7, sl = blockIdx.x >> 3;
-  bh = (sl / per_seq) * 8 + x;
-  j = sl % per_seq;
+// ------------------------------------------------------------------ dV from the stored P
+// dV[key][:] = sum over query chunks of P^T dO: the key-major dK pass stored each 32 x 32
+// P block as its wave's A-fragment image, so a wave here loads its two fragments (2 x 16
+// B per lane) and streams the dO tiles through LDS: no S product, no bias lookups, no
+// sigmoid (it ran once, in the dK pass).  Same block order and MFMA order as the dV
+// workgroups of the one-launch form; P comes from the dK wave's S chain (that form summed
+// S in two interleaved chains), so dV differs from it at fp32 rounding.
+template <int D32>
+__device__ __forceinline__ void v_from_p_body(const AttnBwdArgsW& a, char* smem, int kt, int bh) {
+  constexpr int DP = 32 * D32;
+  constexpr int TB = 64 * DP;
+  char* tiles = smem;  // [2 buffers][dO][TB]
+  const int b = bh / a.H, h = bh % a.H;
+  const int64_t s0 = a.offsets[b];
+  const int L = (int)(a.offsets[b + 1] - s0);
+  const int k0 = kt * WK;
+  if (k0 >= L) return;
+  const int tid = threadIdx.x, w = wave_id(), lane = tid & 63;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int k0w = k0 + 32 * w;
+  const bool w_on = k0w < L;
+  const int64_t rsb = (int64_t)a.H * DP;
+  const int64_t hoff = s0 * rsb + (int64_t)h * DP;
+  f32x16 acc[D32];
+#pragma unroll
+  for (int t = 0; t < D32; ++t) acc[t] = f16_zero();
+  const int n_chunks = (L - k0 + 31) / 32;
+  const int kb = k0w >> 5;
+  auto pfrag = [&](int qc, u32x4_t& f0, u32x4_t& f1) {
+    const int qb = qc >> 5;
+    const char* pblk = reinterpret_cast<const char*>(a.pb + ((int64_t)bh * a.nbt + qb * (qb + 1) / 2 + kb) * 1024);
+    f0 = *reinterpret_cast<const u32x4_t*>(pblk + 16 * lane);
+    f1 = *reinterpret_cast<const u32x4_t*>(pblk + 1024 + 16 * lane);
+  };
+  u32x4_t n0 = {0u, 0u, 0u, 0u}, n1 = n0;  // the wave's next P block, one chunk ahead
+  if (w_on) pfrag(k0w, n0, n1);
+  dma_tile<D32>(tiles, a.ob + hoff, rsb, k0, L, a.zrow, w, lane);
+  __syncthreads();
+  for (int ci = 0; ci < n_chunks; ++ci) {
+    const int qc0 = k0 + 32 * ci;
+    const char* Ds = tiles + (ci & 1) * TB;
+    const bool more = ci + 1 < n_chunks;
+    if (more) dma_tile<D32>(tiles + ((ci + 1) & 1) * TB, a.ob + hoff, rsb, qc0 + 32, L, a.zrow, w, lane);
+    if (w_on && qc0 >= k0w) {
+      const u32x4_t f0 = n0, f1 = n1;
+      if (more) pfrag(qc0 + 32, n0, n1);
+      constexpr int NU = 2 * D32, PB = 4;
+      u32x4_t bq[PB];
+#pragma unroll
+      for (int u = 0; u < PB; ++u) bq[u] = trB_acc_cm(Ds, u / D32, u % D32, lane);
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        const u32x4_t b0 = bq[u % PB];
+        if (u + PB < NU) bq[u % PB] = trB_acc_cm(Ds, (u + PB) / D32, (u + PB) % D32, lane);
+        acc[u % D32] = mfma32(u < D32 ? f0 : f1, b0, acc[u % D32]);
+      }
+#pragma unroll
+      for (int u = 0; u < PB; ++u) __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+        if (u + PB < NU) __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
+      }
+    }
+    if (more) __syncthreads();
+  }
+  if (!w_on) return;
+#pragma unroll
+  for (int g = 0; g < 16; g += 8)
+    store_scaled<8, D32>([&](int i, int t) { return acc[t][g + i]; }, L, a.d, s0, a.dvv, a.ld_d,
+                         a.hv, a.ld_h, h * a.d,
+                         [&](int i) { return k0w + ((g + i) & 3) + 8 * ((g + i) >> 2) + 4 * lh; },
+                         [&](int t) { return 32 * t + lr; });
 }
 
+// Workgroup i -> (bh, key tile kt), key-tile-major within an XCD (x = i % 8 takes the
+// sequence-heads x, x + 8, ...): every XCD dispatches its kt = 0 workgroups first, then
+// kt = 1, ..., so the heaviest causal tiles start first and a CU freed early takes the
+// next-heaviest (with the sequence-head-major order one CU could draw two heavy tiles)
+__device__ __forceinline__ void xcd_slot_kt(const AttnBwdArgsW& a, int& bh, int& kt) {
+  const int x = blockIdx.x & 7, sl = blockIdx.x >> 3;
+  const int nbh8 = (a.B * a.H + 7) >> 3;
+  kt = sl / nbh8;
+  bh = (sl % nbh8) * 8 + x;
+}
+
+// Two-launch form: dK (+ dS, bias gradients and the P blocks), then dV from P.
 template <int D32, bool HB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
-void attn_bwd_bf16w_kv_kernel(AttnBwdArgsW a) {
+void attn_bwd_bf16w_k_kernel(AttnBwdArgsW a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  // XCD-aware order (workgroup i runs on XCD i % 8): every workgroup of one (sequence,
-  // head) lands on one XCD, so its Q / dO rows, re-read by each key tile and by both
-  // kinds, come from that XCD's L2; within it dK / dV pairs, heaviest key tiles first
-  int bh, j;
-  xcd_slot(a, 2 * a.n_kt, bh, j);
+  int bh, kt;
+  xcd_slot_kt(a, bh, kt);
   if (bh >= a.B * a.H) return;
-  if ((j & 1) == 0) kv_body<D32, HB, true>(a, smem, j >> 1, bh);
-  else kv_body<D32, HB, false>(a, smem, j >> 1, bh);
+  kv_body<D32, HB, true, true>(a, smem, kt, bh);
+}
+template <int D32>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2)))
+void attn_bwd_bf16w_vp_kernel(AttnBwdArgsW a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int bh, kt;
+  xcd_slot_kt(a, bh, kt);
+  if (bh >= a.B * a.H) return;
+  v_from_p_body<D32>(a, smem, kt, bh);
 }
 
 // ------------------------------------------------------------------ query-major pass
@@ -762,9 +862,9 @@ void attn_bwd_bf16w_dq_kernel(AttnBwdArgsW a) {
   char* kt_l = smem;             // [2][TB]
   char* dsl = smem + 2 * TB;     // [4 waves][2][2048 B]
   int bh, j;
-  xcd_slot(a, a.n_qt, bh, j);  // one (sequence, head) per XCD at a time: K rows from L2
+  xcd_slot_kt(a, bh, j);  // tile-major: the heaviest query tiles (the last) first
   if (bh >= a.B * a.H) return;
-  const int qt = a.n_qt - 1 - j;  // heaviest tiles first
+  const int qt = a.n_qt - 1 - j;
   const int b = bh / a.H, h = bh % a.H;
   const int64_t s0 = a.offsets[b];
   const int L = (int)(a.offsets[b + 1] - s0);
@@ -906,10 +1006,15 @@ static int launch_bwd_bf16w(AttnBwdArgsW a, float* dpos_w, float* dts_w, hipStre
   const size_t lds_q = 2 * TB + 4 * 2 * 2048;
   GR_REQUIRE(lds_kv <= 160 * 1024, "hstu_attn_bwd_bf16: LDS %zu B exceeds 160 KiB (N=%d)", lds_kv, a.N);
   const int grid = a.n_kt * a.B * a.H;
-  auto kkv = a.map_kq ? attn_bwd_bf16w_kv_kernel<D32, true> : attn_bwd_bf16w_kv_kernel<D32, false>;
-  const int bh8 = ceil_div(a.B * a.H, 8) * 8;  // XCD-aware order: see xcd_slot
-  GR_TIMED("attn_bwd_dkv", st, hipLaunchKernelGGL(kkv, dim3(2 * a.n_kt * bh8), dim3(256), lds_kv, st, a));
-  GR_LAUNCH_CHECK("hstu_attn_bwd_bf16(wide dkv)");
+  const int bh8 = ceil_div(a.B * a.H, 8) * 8;  // XCD-aware order: see xcd_slot_kt
+  // dK (+ dS, the bias gradients and the P blocks), then dV from P: S and the sigmoid are
+  // computed once per element (a dV workgroup beside each dK workgroup recomputed them)
+  auto kk = a.map_kq ? attn_bwd_bf16w_k_kernel<D32, true> : attn_bwd_bf16w_k_kernel<D32, false>;
+  GR_TIMED("attn_bwd_dkv", st, hipLaunchKernelGGL(kk, dim3(a.n_kt * bh8), dim3(256), lds_kv, st, a));
+  GR_LAUNCH_CHECK("hstu_attn_bwd_bf16(wide dk)");
+  GR_TIMED("attn_bwd_dkv", st, hipLaunchKernelGGL(attn_bwd_bf16w_vp_kernel<D32>, dim3(a.n_kt * bh8), dim3(256),
+                                                  2 * TB, st, a));
+  GR_LAUNCH_CHECK("hstu_attn_bwd_bf16(wide dv)");
   GR_TIMED("attn_bwd_dq", st, hipLaunchKernelGGL(attn_bwd_bf16w_dq_kernel<D32>, dim3(a.n_qt * bh8), dim3(256), lds_q, st, a));
   GR_LAUNCH_CHECK("hstu_attn_bwd_bf16(wide dq)");
   if (a.map_kq) {
@@ -958,13 +1063,13 @@ int gr_attn_fwd_bf16w(const void* copies, const int64_t* offsets, int B, int N, 
   return launch_fwd_bf16w<8>(a, st, max_len);
 }
 
-// workspace: slabs | dS blocks | dO copy + zero row | Q, K, V copies (used when the caller
-// passes none)
+// workspace: slabs | dS blocks | P blocks | dO copy + zero row | Q, K, V copies (used when
+// the caller passes none)
 // own Q/K/V copies sit at the end: a caller passing the forward's copies needs none
 size_t gr_attn_bwd_bf16w_workspace(int B, int N, int max_len, int H, int d, int num_buckets,
                                    bool with_copies) {
   using namespace gr;
-  return al256(bf16w_slab_bytes(B, N, max_len, H, num_buckets)) + al256(bf16w_ds_bytes(B, N, H)) +
+  return al256(bf16w_slab_bytes(B, N, max_len, H, num_buckets)) + 2 * al256(bf16w_ds_bytes(B, N, H)) +
          bf16w_copy_bytes(B, N, H, d) + al256(ceil_div(d, 32) * 64) +
          (with_copies ? 0 : bf16w_copies_bytes(B, N, H, d));
 }
@@ -988,7 +1093,8 @@ int gr_attn_bwd_bf16w(const float* q, const float* k, const float* v, int64_t ld
   a.dq = dq; a.dk = dk; a.dvv = dvv; a.ld_d = ld_d;
   a.slabs = (float*)workspace;
   a.ds = (__bf16*)((char*)workspace + slab_b);
-  char* cp = (char*)workspace + slab_b + ds_b;
+  a.pb = (__bf16*)((char*)workspace + slab_b + ds_b);
+  char* cp = (char*)workspace + slab_b + 2 * ds_b;
   a.ob = (__bf16*)cp;
   __bf16* ozrow = (__bf16*)(cp + cp_b);
   char* own = cp + cp_b + al256(nch * 16);
