@@ -822,8 +822,9 @@ __device__ __forceinline__ void v_from_p_body(const AttnBwdArgsW& a, char* smem,
 // sequence-heads x, x + 8, ...): every XCD dispatches its kt = 0 workgroups first, then
 // kt = 1, ..., so the heaviest causal tiles start first and a CU freed early takes the
 // next-heaviest (with the sequence-head-major order one CU could draw two heavy tiles)
-__device__ __forceinline__ void xcd_slot_kt(const AttnBwdArgsW& a, int& bh, int& kt) {
-  const int x = blockIdx.x & 7, sl = blockIdx.x >> 3;
+__device__ __forceinline__ void xcd_slot_kt(const AttnBwdArgsW& a, int& bh, int& kt,
+                                            int id = (int)blockIdx.x) {
+  const int x = id & 7, sl = id >> 3;
   const int nbh8 = (a.B * a.H + 7) >> 3;
   kt = sl / nbh8;
   bh = (sl % nbh8) * 8 + x;
@@ -839,12 +840,54 @@ void attn_bwd_bf16w_k_kernel(AttnBwdArgsW a) {
   if (bh >= a.B * a.H) return;
   kv_body<D32, HB, true, true>(a, smem, kt, bh);
 }
+// The bias-gradient slabs (written by the dK launch) reduced by the first workgroups of
+// the dV launch: workgroup r owns bins 16 r .. 16 r + 15; thread (bin, group g) sums
+// slabs g, g + 16, ... in order (16 loads in flight), then the 16 groups are added in
+// order: a fixed order, no float atomics.
+struct BiasRed {
+  int n_slabs, npos, nts, nbias;
+  float* dpos_w;
+  float* dts_w;
+};
+__device__ __forceinline__ void bias_reduce_wg(const float* slabs, const BiasRed& r, int wg, char* smem) {
+  float* part = reinterpret_cast<float*>(smem);  // [16 groups][16 bins]
+  const int nbins = r.npos + r.nts;
+  const int tid = threadIdx.x, bi = tid & 15, g = tid >> 4;
+  const int bin = 16 * wg + bi;
+  float acc = 0.f;
+  if (bin < nbins) {
+    int j = g;
+    for (; j + 15 * 16 < r.n_slabs; j += 16 * 16) {
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = slabs[(int64_t)(j + 16 * u) * nbins + bin];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) acc += v[u];
+    }
+    for (; j < r.n_slabs; j += 16) acc += slabs[(int64_t)j * nbins + bin];
+  }
+  part[g * 16 + bi] = acc;
+  __syncthreads();
+  if (tid < 16 && bin < nbins) {
+    float s = 0.f;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) s += part[u * 16 + bi];
+    if (bin < r.npos) r.dpos_w[bin] = s;
+    else r.dts_w[bin - r.npos] = s;
+  }
+}
+
 template <int D32>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2)))
-void attn_bwd_bf16w_vp_kernel(AttnBwdArgsW a) {
+void attn_bwd_bf16w_vp_kernel(AttnBwdArgsW a, BiasRed r) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  if ((int)blockIdx.x < r.nbias) {
+    bias_reduce_wg(a.slabs, r, blockIdx.x, smem);
+    return;
+  }
+  // r.nbias is a multiple of 8: blockIdx.x - nbias keeps the workgroup's XCD
   int bh, kt;
-  xcd_slot_kt(a, bh, kt);
+  xcd_slot_kt(a, bh, kt, (int)blockIdx.x - r.nbias);
   if (bh >= a.B * a.H) return;
   v_from_p_body<D32>(a, smem, kt, bh);
 }
@@ -937,27 +980,6 @@ void attn_bwd_bf16w_dq_kernel(AttnBwdArgsW a) {
 // slabs: [n][2N-1 + nb+1]; fixed-order reduce in two coalesced stages: stage 1 sums slabs
 // 64 g .. 64 g + 63 of each bin in order into slab 64 g (each thread reads its own bins
 // before overwriting them); stage 2 adds the groups in g order
-constexpr int kRedGroup = 64;
-__global__ __launch_bounds__(256) void attn_bf16w_bias_reduce1(float* slabs, int n_slabs, int nbins) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= nbins) return;
-  const int j0 = blockIdx.y * kRedGroup, j1 = min(j0 + kRedGroup, n_slabs);
-  float acc = 0.f;
-  for (int j = j0; j < j1; ++j) acc += slabs[(int64_t)j * nbins + i];
-  slabs[(int64_t)j0 * nbins + i] = acc;
-}
-__global__ __launch_bounds__(256) void attn_bf16w_bias_reduce2(const float* slabs, int n_slabs,
-                                                               int n_pos, int n_ts, float* dpos_w,
-                                                               float* dts_w) {
-  const int nbins = n_pos + n_ts;
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= nbins) return;
-  float acc = 0.f;
-  for (int j = 0; j < n_slabs; j += kRedGroup) acc += slabs[(int64_t)j * nbins + i];
-  if (i < n_pos) dpos_w[i] = acc;
-  else dts_w[i - n_pos] = acc;
-}
-
 static size_t bf16w_slab_bytes(int B, int N, int max_len, int H, int nb) {
   return sizeof(float) * 4 * (size_t)ceil_div(max_len, WK) * B * H * (size_t)(2 * N - 1 + nb + 1);
 }
@@ -1012,20 +1034,14 @@ static int launch_bwd_bf16w(AttnBwdArgsW a, float* dpos_w, float* dts_w, hipStre
   auto kk = a.map_kq ? attn_bwd_bf16w_k_kernel<D32, true> : attn_bwd_bf16w_k_kernel<D32, false>;
   GR_TIMED("attn_bwd_dkv", st, hipLaunchKernelGGL(kk, dim3(a.n_kt * bh8), dim3(256), lds_kv, st, a));
   GR_LAUNCH_CHECK("hstu_attn_bwd_bf16(wide dk)");
-  GR_TIMED("attn_bwd_dkv", st, hipLaunchKernelGGL(attn_bwd_bf16w_vp_kernel<D32>, dim3(a.n_kt * bh8), dim3(256),
-                                                  2 * TB, st, a));
+  // the dV launch also reduces the dK launch's bias slabs (its first workgroups)
+  BiasRed red{4 * grid, (int)npos, a.nb + 1, 0, dpos_w, dts_w};
+  if (a.map_kq) red.nbias = ceil_div(ceil_div((int)npos + a.nb + 1, 16), 8) * 8;
+  GR_TIMED("attn_bwd_dkv", st, hipLaunchKernelGGL(attn_bwd_bf16w_vp_kernel<D32>, dim3(red.nbias + a.n_kt * bh8), dim3(256),
+                                                  2 * TB, st, a, red));
   GR_LAUNCH_CHECK("hstu_attn_bwd_bf16(wide dv)");
   GR_TIMED("attn_bwd_dq", st, hipLaunchKernelGGL(attn_bwd_bf16w_dq_kernel<D32>, dim3(a.n_qt * bh8), dim3(256), lds_q, st, a));
   GR_LAUNCH_CHECK("hstu_attn_bwd_bf16(wide dq)");
-  if (a.map_kq) {
-    const int nbins = (int)npos + a.nb + 1;
-    const int n_slabs = 4 * grid;
-    GR_TIMED("attn_bias_reduce", st, hipLaunchKernelGGL(attn_bf16w_bias_reduce1, dim3(ceil_div(nbins, 256), ceil_div(n_slabs, kRedGroup)),
-                                                        dim3(256), 0, st, a.slabs, n_slabs, nbins));
-    GR_TIMED("attn_bias_reduce", st, hipLaunchKernelGGL(attn_bf16w_bias_reduce2, dim3(ceil_div(nbins, 256)), dim3(256), 0, st,
-                                                        a.slabs, n_slabs, (int)npos, a.nb + 1, dpos_w, dts_w));
-    GR_LAUNCH_CHECK("hstu_attn_bwd_bf16(wide bias reduce)");
-  }
   return 0;
 }
 
