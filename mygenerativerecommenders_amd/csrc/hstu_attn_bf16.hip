@@ -332,7 +332,7 @@ extern "C" int hstu_attn_fwd_bf16(const float* q, const float* k, const float* v
 // Relative-bias gradients stay fp32 and deterministic: dts_w in per-wave LDS histograms;
 // dpos_w per chunk as per-wave diagonal sums (47 bins) that one pass per tile adds, in
 // wave order, into the workgroup's histogram; each workgroup writes one slab, reduced in
-// a fixed order by attn_bf16_bias_reduce.
+// a fixed order by the first workgroups of the dQ launch (bias_reduce_block).
 
 namespace gr {
 
@@ -665,11 +665,51 @@ __global__ __launch_bounds__(64 * WAVES) void attn_bwd_bf16_dkv_kernel(AttnBwdAr
   }
 }
 
+// The bias-gradient slabs of the dK/dV launch reduced by the first workgroups of the dQ
+// launch (one launch fewer per layer): workgroup wg owns bins 16 wg .. 16 wg + 15, thread
+// (bin, group g) sums slabs g, g + G, ... in order (8 loads in flight), then the G groups
+// are added in order.  At 256 threads (G = 16) the order is that of the former reduce launch.
+template <int NTH>
+__device__ __forceinline__ void bias_reduce_block(const float* slabs, int n_slabs, int n_pos, int n_ts,
+                                                  float* dpos_w, float* dts_w, int wg, float* part) {
+  constexpr int G = NTH / 16;
+  const int nbins = n_pos + n_ts;
+  const int bl = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int i = wg * 16 + bl;
+  float acc = 0.f;
+  if (i < nbins) {
+    int j = g;
+    for (; j + 7 * G < n_slabs; j += 8 * G) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = slabs[(int64_t)(j + u * G) * nbins + i];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; j < n_slabs; j += G) acc += slabs[(int64_t)j * nbins + i];
+  }
+  part[g * 16 + bl] = acc;
+  __syncthreads();
+  if (g == 0 && i < nbins) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < G; ++k) s += part[k * 16 + bl];
+    if (i < n_pos) dpos_w[i] = s;
+    else dts_w[i - n_pos] = s;
+  }
+}
+
 template <int KC, int VC, int TK, int WAVES, bool HB>
-__global__ __launch_bounds__(64 * WAVES) void attn_bwd_bf16_dq_kernel(AttnBwdArgsBf16 a) {
+__global__ __launch_bounds__(64 * WAVES) void attn_bwd_bf16_dq_kernel(AttnBwdArgsBf16 a, int nbias,
+                                                                     float* dpos_w, float* dts_w) {
   using C = BwdBf16Cfg<KC, VC, TK>;
   constexpr int NTH = 64 * WAVES, QT = 16 * WAVES;
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  if (HB && (int)blockIdx.x < nbias) {
+    bias_reduce_block<NTH>(a.slabs, a.n_kt * a.B * a.H, 2 * a.N - 1, a.nb + 1, dpos_w, dts_w,
+                           blockIdx.x, reinterpret_cast<float*>(smem));
+    return;
+  }
   __bf16* Ks = reinterpret_cast<__bf16*>(smem);  // [TK][LDK]
   __bf16* Kt = Ks + TK * C::LDK;                 // [KP][LDT]
   __bf16* Vs = Kt + C::KP * C::LDT;              // [TK][LDV]
@@ -677,7 +717,7 @@ __global__ __launch_bounds__(64 * WAVES) void attn_bwd_bf16_dq_kernel(AttnBwdArg
   float* posw = tsw + (a.nb + 1);
 
   const int BH = a.B * a.H;
-  const int rank = snake_rank(blockIdx.x, a.cus);
+  const int rank = snake_rank((int)blockIdx.x - nbias, a.cus);
   const int qt = a.n_qt - 1 - rank / BH;  // heaviest tiles first
   const int bh = rank % BH;
   const int b = bh / a.H, h = bh % a.H;
@@ -787,27 +827,6 @@ __global__ __launch_bounds__(64 * WAVES) void attn_bwd_bf16_dq_kernel(AttnBwdArg
 
 // Deterministic slab reduction (fixed order): a workgroup owns 16 bins; thread (bin, g)
 // sums slabs g, g + 16, ..., then the 16 partials are added in g order.
-__global__ __launch_bounds__(256) void attn_bf16_bias_reduce(const float* slabs, int n_slabs,
-                                                             int n_pos, int n_ts, float* dpos_w,
-                                                             float* dts_w) {
-  __shared__ float part[16][17];
-  const int nbins = n_pos + n_ts;
-  const int bl = threadIdx.x & 15, g = threadIdx.x >> 4;
-  const int i = blockIdx.x * 16 + bl;
-  const int ic = i < nbins ? i : nbins - 1;
-  float acc = 0.f;
-  for (int j = g; j < n_slabs; j += 16) acc += slabs[(int64_t)j * nbins + ic];
-  part[g][bl] = acc;
-  __syncthreads();
-  if (g == 0 && i < nbins) {
-    float s = 0.f;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) s += part[k][bl];
-    if (i < n_pos) dpos_w[i] = s;
-    else dts_w[i - n_pos] = s;
-  }
-}
-
 template <int KC, int VC, int TQ, int WAVES>
 static size_t dkv_lds(const AttnBwdArgsBf16& a, bool priv) {
   using C = BwdBf16Cfg<KC, VC, TQ>;
@@ -853,20 +872,18 @@ static int launch_bwd_bf16(AttnBwdArgsBf16 a, float* dpos_w, float* dts_w, hipSt
   GR_REQUIRE(l_kv <= 160 * 1024 && l_q <= 160 * 1024,
              "hstu_attn_bwd_bf16: LDS (%zu, %zu B) exceeds 160 KiB (N=%d)", l_kv, l_q, a.N);
   a.cus = (int64_t)grid <= 2 * device_cus() ? device_cus() : (1 << 30);
+  // the dQ launch's first workgroups reduce the dK/dV launch's bias slabs
   if (a.map_kq) {
+    const int nbias = ceil_div(2 * a.N - 1 + a.nb + 1, 16);
     launch_dkv_bf16<KC, VC, T, WAVES, true>(a, grid, l_kv, st);
-    GR_TIMED("attn_bwd_dq", st, hipLaunchKernelGGL((attn_bwd_bf16_dq_kernel<KC, VC, T, WAVES, true>), dim3(grid), dim3(64 * WAVES), l_q, st, a));
+    GR_TIMED("attn_bwd_dq", st, hipLaunchKernelGGL((attn_bwd_bf16_dq_kernel<KC, VC, T, WAVES, true>), dim3(nbias + grid), dim3(64 * WAVES),
+                                                   std::max(l_q, sizeof(float) * 64 * WAVES), st, a, nbias, dpos_w, dts_w));
   } else {
     launch_dkv_bf16<KC, VC, T, WAVES, false>(a, grid, l_kv, st);
-    GR_TIMED("attn_bwd_dq", st, hipLaunchKernelGGL((attn_bwd_bf16_dq_kernel<KC, VC, T, WAVES, false>), dim3(grid), dim3(64 * WAVES), l_q, st, a));
+    GR_TIMED("attn_bwd_dq", st, hipLaunchKernelGGL((attn_bwd_bf16_dq_kernel<KC, VC, T, WAVES, false>), dim3(grid), dim3(64 * WAVES), l_q, st, a,
+                                                   0, dpos_w, dts_w));
   }
   GR_LAUNCH_CHECK("hstu_attn_bwd_bf16");
-  if (a.map_kq) {
-    const int nbins = 2 * a.N - 1 + a.nb + 1;
-    GR_TIMED("attn_bias_reduce", st, hipLaunchKernelGGL(attn_bf16_bias_reduce, dim3(ceil_div(nbins, 16)), dim3(256), 0, st,
-                                                        a.slabs, grid, 2 * a.N - 1, a.nb + 1, dpos_w, dts_w));
-    GR_LAUNCH_CHECK("hstu_attn_bwd_bf16(bias reduce)");
-  }
   return 0;
 }
 
