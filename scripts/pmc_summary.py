@@ -39,11 +39,10 @@ _MAP = [
     (r"rowwave2_kernel", "boundary_fwd"),
     (r"mips_small_select_kernel", "mips_small"),
     (r"current_embeddings_kernel", "current_embeddings"),
-    (r"attn_bwd_bf16w_kv_kernel|attn_bwd_bf16_dkv_kernel", "attn_bwd_dkv"),
+    (r"attn_bwd_bf16w_k_kernel|attn_bwd_bf16w_vp_kernel|attn_bwd_bf16_dkv_kernel", "attn_bwd_dkv"),
     (r"attn_bwd_bf16w_dq_kernel|attn_bwd_bf16_dq_kernel", "attn_bwd_dq"),
     (r"attn_fwd_bf16w_kernel|attn_fwd_bf16_kernel", "attn_fwd"),
     (r"attn_bf16w_convert", "attn_bf16_copies"),
-    (r"attn_bf16w_bias_reduce", "attn_bias_reduce"),
     (r"wgrad_partial_(wide|bf16)_kernel", "wgrad_partial"),
     (r"attn_fwd_kernel", "attn_fwd"),
     (r"attn_bwd_fused_kernel", "attn_bwd"),
