@@ -743,6 +743,23 @@ __device__ __forceinline__ void kv_body(const AttnBwdArgsW& a, char* smem, int k
 #endif
 }
 
+// LDS-DMA issued from inline asm (global_load_lds_dwordx4: lane l's 16 bytes land at LDS
+// byte lds_off + 16 l).  The builtin makes hipcc wait vmcnt(0) before every later LDS read
+// that might alias the destination, which drains a deeper prefetch ring on each chunk;
+// hipcc does not see these, so the caller waits (vmcnt) and synchronises itself.  m0 is
+// saved and restored around the instruction.
+__device__ __forceinline__ void dma16_asm(const void* gaddr, uint32_t lds_off) {
+  uint32_t tmp;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(tmp)
+               : "s"(lds_off), "v"(gaddr)
+               : "memory");
+}
+__device__ __forceinline__ uint32_t lds_u32(const void* p) {
+  return __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char*)p);
+}
+
 // ------------------------------------------------------------------ dV from the stored P
 // dV[key][:] = sum over query chunks of P^T dO: the key-major dK pass stored each 32 x 32
 // P block as its wave's A-fragment image, so a wave here loads its two fragments (2 x 16
@@ -808,6 +825,97 @@ __device__ __forceinline__ void v_from_p_body(const AttnBwdArgsW& a, char* smem,
       }
     }
     if (more) __syncthreads();
+  }
+  if (!w_on) return;
+#pragma unroll
+  for (int g = 0; g < 16; g += 8)
+    store_scaled<8, D32>([&](int i, int t) { return acc[t][g + i]; }, L, a.d, s0, a.dvv, a.ld_d,
+                         a.hv, a.ld_h, h * a.d,
+                         [&](int i) { return k0w + ((g + i) & 3) + 8 * ((g + i) >> 2) + 4 * lh; },
+                         [&](int t) { return 32 * t + lr; });
+}
+
+// dV from P with a 3-deep ring (even D32: every wave issues D32 / 2 dO pieces + 2 P pieces
+// per chunk, so one vmcnt count fits all waves).  Chunk ci: wait for chunk ci's DMA
+// (vmcnt: chunk ci + 1's 6 or so pieces may stay in flight), barrier (every wave is past
+// chunk ci - 1, whose slot the next DMA overwrites), issue chunk ci + 2, compute chunk ci.
+// The dO tile and the wave's 2 KB P block both arrive by LDS-DMA, so P costs no
+// register-load wait either.
+template <int D32>
+__device__ __forceinline__ void v_from_p_ring_body(const AttnBwdArgsW& a, char* smem, int kt, int bh) {
+  static_assert(D32 % 2 == 0, "uniform DMA pieces per wave");
+  constexpr int DP = 32 * D32;
+  constexpr int TB = 64 * DP;
+  constexpr int NR = 3;             // ring depth
+  constexpr int OPS = D32 / 2 + 2;  // asm DMA instructions per wave per chunk
+  char* dslot = smem;               // [NR][TB] dO tiles
+  char* pslot = smem + NR * TB;     // [NR][4 waves][2 KB] P blocks
+  const int b = bh / a.H, h = bh % a.H;
+  const int64_t s0 = a.offsets[b];
+  const int L = (int)(a.offsets[b + 1] - s0);
+  const int k0 = kt * WK;
+  if (k0 >= L) return;
+  const int tid = threadIdx.x, w = wave_id(), lane = tid & 63;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int k0w = k0 + 32 * w;
+  const bool w_on = k0w < L;
+  const int64_t rsb = (int64_t)a.H * DP;
+  const int64_t hoff = s0 * rsb + (int64_t)h * DP;
+  f32x16 acc[D32];
+#pragma unroll
+  for (int t = 0; t < D32; ++t) acc[t] = f16_zero();
+  const int n_chunks = (L - k0 + 31) / 32;
+  const int kb = k0w >> 5;
+  auto issue = [&](int c) {  // chunk c's dO tile pieces and this wave's P block
+    const int slot = c % NR;
+    const int r = k0 + 32 * c + lr;
+    const __bf16* src = (r < L ? a.ob + hoff + (int64_t)r * rsb : a.zrow) + 8 * lh;
+    const uint32_t dbase = lds_u32(dslot + slot * TB);
+#pragma unroll
+    for (int i = 0; i < 2 * D32; i += 4) dma16_asm(src + 16 * (i + w), dbase + 1024 * (i + w));
+    // the wave's P block (a clamped valid block where the chunk precedes the wave's keys)
+    int qb = (k0 + 32 * c) >> 5;
+    qb = qb < kb ? kb : qb;
+    const int64_t blk = w_on ? (int64_t)qb * (qb + 1) / 2 + kb : 0;  // a wave past L: block 0
+    const char* pblk = reinterpret_cast<const char*>(a.pb + ((int64_t)bh * a.nbt + blk) * 1024);
+    const uint32_t pbase = lds_u32(pslot + (slot * 4 + w) * 2048);
+    dma16_asm(pblk + 16 * lane, pbase);
+    dma16_asm(pblk + 1024 + 16 * lane, pbase + 1024);
+  };
+  issue(0);
+  if (n_chunks > 1) issue(1);
+  for (int ci = 0; ci < n_chunks; ++ci) {
+    const int qc0 = k0 + 32 * ci;
+    if (ci + 1 < n_chunks) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPS) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (ci + 2 < n_chunks) issue(ci + 2);
+    const int slot = ci % NR;
+    const char* Ds = dslot + slot * TB;
+    if (w_on && qc0 >= k0w) {
+      const char* pp = pslot + (slot * 4 + w) * 2048;
+      const u32x4_t f0 = *reinterpret_cast<const u32x4_t*>(pp + 16 * lane);
+      const u32x4_t f1 = *reinterpret_cast<const u32x4_t*>(pp + 1024 + 16 * lane);
+      constexpr int NU = 2 * D32, PB = 4;
+      u32x4_t bq[PB];
+#pragma unroll
+      for (int u = 0; u < PB; ++u) bq[u] = trB_acc_cm(Ds, u / D32, u % D32, lane);
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        const u32x4_t b0 = bq[u % PB];
+        if (u + PB < NU) bq[u % PB] = trB_acc_cm(Ds, (u + PB) / D32, (u + PB) % D32, lane);
+        acc[u % D32] = mfma32(u < D32 ? f0 : f1, b0, acc[u % D32]);
+      }
+#pragma unroll
+      for (int u = 0; u < PB + 2; ++u) __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+        if (u + PB < NU) __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this chunk's LDS reads done
   }
   if (!w_on) return;
 #pragma unroll
@@ -889,7 +997,8 @@ void attn_bwd_bf16w_vp_kernel(AttnBwdArgsW a, BiasRed r) {
   int bh, kt;
   xcd_slot_kt(a, bh, kt, (int)blockIdx.x - r.nbias);
   if (bh >= a.B * a.H) return;
-  v_from_p_body<D32>(a, smem, kt, bh);
+  if constexpr (D32 % 2 == 0) v_from_p_ring_body<D32>(a, smem, kt, bh);
+  else v_from_p_body<D32>(a, smem, kt, bh);
 }
 
 // ------------------------------------------------------------------ query-major pass
@@ -1037,8 +1146,9 @@ static int launch_bwd_bf16w(AttnBwdArgsW a, float* dpos_w, float* dts_w, hipStre
   // the dV launch also reduces the dK launch's bias slabs (its first workgroups)
   BiasRed red{4 * grid, (int)npos, a.nb + 1, 0, dpos_w, dts_w};
   if (a.map_kq) red.nbias = ceil_div(ceil_div((int)npos + a.nb + 1, 16), 8) * 8;
+  const size_t lds_vp = D32 % 2 == 0 ? 3 * TB + 3 * 4 * 2048 : 2 * TB;  // ring / two buffers
   GR_TIMED("attn_bwd_dkv", st, hipLaunchKernelGGL(attn_bwd_bf16w_vp_kernel<D32>, dim3(red.nbias + a.n_kt * bh8), dim3(256),
-                                                  2 * TB, st, a, red));
+                                                  lds_vp, st, a, red));
   GR_LAUNCH_CHECK("hstu_attn_bwd_bf16(wide dv)");
   GR_TIMED("attn_bwd_dq", st, hipLaunchKernelGGL(attn_bwd_bf16w_dq_kernel<D32>, dim3(a.n_qt * bh8), dim3(256), lds_q, st, a));
   GR_LAUNCH_CHECK("hstu_attn_bwd_bf16(wide dq)");
