@@ -1046,6 +1046,60 @@ void attn_bwd_bf16w_dq_kernel(AttnBwdArgsW a) {
                                        (__attribute__((address_space(3))) void*)(mydl + buf * 2048 + 1024 * i), 16, 0, 0);
     }
   };
+  if constexpr (D32 % 2 == 0) {
+    // 3-deep ring by inline-asm LDS-DMA (see v_from_p_ring_body): chunk kb waits for its
+    // own pieces only, the next key block's stay in flight
+    constexpr int NR = 3, OPS = D32 / 2 + 2;
+    char* kring = smem;                // [NR][TB] K tiles (swizzled)
+    char* dring = smem + NR * TB;      // [NR][4 waves][2 KB] dS blocks
+    const int kr_row = swz_row(lr, 2 * (w & 1) + (lane >> 5));
+    auto issue = [&](int kb) {
+      const int slot = kb % NR;
+      const int r = 32 * kb + kr_row;
+      const __bf16* src = (r < L ? krows + (int64_t)r * rsb : a.zrow) + 8 * (lane >> 5);
+      const uint32_t kbase = lds_u32(kring + slot * TB);
+#pragma unroll
+      for (int i = 0; i < 2 * D32; i += 4) dma16_asm(src + 16 * (i + w), kbase + 1024 * (i + w));
+      const bool ok = w_on && kb <= qb;
+      const uint32_t dbase = lds_u32(dring + (slot * 4 + w) * 2048);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        dma16_asm(ok ? dsrow + kb * 1024 + 512 * i + 8 * lane : a.zrow, dbase + 1024 * i);
+    };
+    issue(0);
+    if (n_kb > 1) issue(1);
+    for (int kb = 0; kb < n_kb; ++kb) {
+      if (kb + 1 < n_kb) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPS) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (kb + 2 < n_kb) issue(kb + 2);
+      const int slot = kb % NR;
+      const char* Kl = kring + slot * TB;
+      const __bf16* Dl = reinterpret_cast<const __bf16*>(dring + (slot * 4 + w) * 2048);
+      if (w_on && kb <= qb) {
+        const u32x4_t a0 = trB_nat(Dl, 32, 0, 0, lane), a1 = trB_nat(Dl, 32, 1, 0, lane);
+        constexpr int NU = 2 * D32, PB = 4;
+        u32x4_t bq[PB];
+#pragma unroll
+        for (int u = 0; u < PB; ++u) bq[u] = trB_nat_cm_swz(Kl, u / D32, u % D32, lane);
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+          const u32x4_t b0 = bq[u % PB];
+          if (u + PB < NU) bq[u % PB] = trB_nat_cm_swz(Kl, (u + PB) / D32, (u + PB) % D32, lane);
+          acc[u % D32] = mfma32(u < D32 ? a0 : a1, b0, acc[u % D32]);
+        }
+#pragma unroll
+        for (int u = 0; u < PB + 2; ++u) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          if (u + PB < NU) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this block's LDS reads done
+    }
+  } else {
   dma(0, 0);
   __syncthreads();
   for (int kb = 0; kb < n_kb; ++kb) {
@@ -1075,6 +1129,7 @@ void attn_bwd_bf16w_dq_kernel(AttnBwdArgsW a) {
       }
     }
     if (more) __syncthreads();
+  }
   }
   if (!w_on) return;
   const int lh = lane >> 5;
@@ -1134,7 +1189,7 @@ static int launch_bwd_bf16w(AttnBwdArgsW a, float* dpos_w, float* dts_w, hipStre
   const size_t npos = 2 * a.N - 1;
   const int tss = w_dts_stride(a.nb + 1);
   const size_t lds_kv = 4 * TB + sizeof(float) * ((a.nb + 1) + npos + 4 * kDtsCopies * tss + 4 * 64 * kSkew);
-  const size_t lds_q = 2 * TB + 4 * 2 * 2048;
+  const size_t lds_q = D32 % 2 == 0 ? 3 * TB + 3 * 4 * 2048 : 2 * TB + 4 * 2 * 2048;  // ring / two buffers
   GR_REQUIRE(lds_kv <= 160 * 1024, "hstu_attn_bwd_bf16: LDS %zu B exceeds 160 KiB (N=%d)", lds_kv, a.N);
   const int grid = a.n_kt * a.B * a.H;
   const int bh8 = ceil_div(a.B * a.H, 8) * 8;  // XCD-aware order: see xcd_slot_kt
