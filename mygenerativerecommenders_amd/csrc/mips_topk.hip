@@ -1682,7 +1682,6 @@ __global__ __launch_bounds__(256) void mips_filter_merge_kernel(FilterMergeArgs 
   __shared__ SelLDS L;
   __shared__ int sub_off[NSUB + 1];
   __shared__ float cs[FILTER_CAP];
-  __shared__ int ci[FILTER_CAP];
   const int q = blockIdx.x, tid = threadIdx.x;
   // the invalid row's loads go out first, beside the counter loads (independent of them)
   const int n0p = inv_pad(a.N0);
@@ -1705,17 +1704,23 @@ __global__ __launch_bounds__(256) void mips_filter_merge_kernel(FilterMergeArgs 
     if (tid == 0) atomicExch(a.flag, 1);
     return;
   }
-  {  // compact the sub-lists into LDS: every load issued before any store (a loop per
-     // sub-list waited for each one's loads in turn: 16 serial round trips)
-    constexpr int PER = FILTER_CAP / 256;
+  // Compaction and the validity test run on registers: thread t holds list positions
+  // t + 256 j.  Every score / index load is issued before any use, then every id gather
+  // (a loop over the positions gathered each id in turn: a dependent round trip per
+  // element), and the ids are tested after the invalid row is sorted.
+  constexpr int PER = FILTER_CAP / 256;
+  float vs[PER];
+  int vi[PER];
+  int64_t vid[PER];
+  {
     int off[NSUB];
 #pragma unroll
     for (int u = 0; u < NSUB; ++u) off[u] = __builtin_amdgcn_readfirstlane(sub_off[u]);
-    float vs[PER];
-    int vi[PER];
 #pragma unroll
     for (int t = 0; t < PER; ++t) {
       const int p = tid + 256 * t;
+      vs[t] = -INFINITY;
+      vi[t] = 0;
       if (p < n_raw) {
         int u = 0;
 #pragma unroll
@@ -1731,26 +1736,30 @@ __global__ __launch_bounds__(256) void mips_filter_merge_kernel(FilterMergeArgs 
 #pragma unroll
     for (int t = 0; t < PER; ++t) {
       const int p = tid + 256 * t;
-      if (p < n_raw) {
-        cs[p] = vs[t];
-        ci[p] = vi[t];
-      }
+      vid[t] = a.index_base + vi[t];
+      if (a.item_ids && p < n_raw) vid[t] = a.item_ids[vi[t]];
+    }
+#pragma unroll
+    for (int t = 0; t < PER; ++t) {
+      const int p = tid + 256 * t;
+      if (p < n_raw) cs[p] = vs[t];
     }
   }
-  __syncthreads();
   if (n0p > 256) block_bitonic_i64(inv, n0p);
   else if (n0p > 0) block_sort_i64_asc(inv, n0p);
   // bf16 filter: cs holds the exact scores (rescored at the filter's flush); only candidates at
   // or above tau_e are provably complete
   const float te = a.rescore ? a.tau_e[q] : -INFINITY;
   int nvalid = 0;
-  for (int e = tid; e < n_raw; e += 256) {
-    const int64_t li = ci[e];
-    const int64_t id = a.item_ids ? a.item_ids[li] : a.index_base + li;
-    const bool ok = !(n0p > 0 && sorted_contains(inv, n0p, id)) && cs[e] >= te;
-    key[e] = ok ? ord_key(cs[e]) : 0u;
-    idx[e] = a.index_base + li;
-    nvalid += ok;
+#pragma unroll
+  for (int t = 0; t < PER; ++t) {
+    const int p = tid + 256 * t;
+    if (p < n_raw) {
+      const bool ok = !(n0p > 0 && sorted_contains(inv, n0p, vid[t])) && vs[t] >= te;
+      key[p] = ok ? ord_key(vs[t]) : 0u;
+      idx[p] = a.index_base + vi[t];
+      nvalid += ok;
+    }
   }
   const int tot = block_sum(nvalid, L);
   if (tot < a.k) {  // fewer than k valid items at or above tau: not provably exact
