@@ -1750,12 +1750,38 @@ __global__ __launch_bounds__(256) void mips_filter_merge_kernel(FilterMergeArgs 
   // bf16 filter: cs holds the exact scores (rescored at the filter's flush); only candidates at
   // or above tau_e are provably complete
   const float te = a.rescore ? a.tau_e[q] : -INFINITY;
+  // invalid-id tests: branch-free binary searches over the sorted row (n0p a power of
+  // two; pos = the last entry <= the id), the searches of 4 candidates interleaved (one
+  // search per candidate in turn waited log2(n0p) dependent LDS reads each)
+  bool bad[PER];
+#pragma unroll
+  for (int t = 0; t < PER; ++t) bad[t] = false;
+  if (n0p > 0) {
+#pragma unroll
+    for (int c = 0; c < PER / 4; ++c) {
+      if (1024 * c < n_raw) {
+        const int64_t k0 = vid[4 * c], k1 = vid[4 * c + 1], k2 = vid[4 * c + 2], k3 = vid[4 * c + 3];
+        int p0 = 0, p1 = 0, p2 = 0, p3 = 0;
+        for (int step = n0p >> 1; step > 0; step >>= 1) {
+          const int64_t v0 = inv[p0 + step], v1 = inv[p1 + step], v2 = inv[p2 + step], v3 = inv[p3 + step];
+          p0 += v0 <= k0 ? step : 0;
+          p1 += v1 <= k1 ? step : 0;
+          p2 += v2 <= k2 ? step : 0;
+          p3 += v3 <= k3 ? step : 0;
+        }
+        bad[4 * c] = inv[p0] == k0;
+        bad[4 * c + 1] = inv[p1] == k1;
+        bad[4 * c + 2] = inv[p2] == k2;
+        bad[4 * c + 3] = inv[p3] == k3;
+      }
+    }
+  }
   int nvalid = 0;
 #pragma unroll
   for (int t = 0; t < PER; ++t) {
     const int p = tid + 256 * t;
     if (p < n_raw) {
-      const bool ok = !(n0p > 0 && sorted_contains(inv, n0p, vid[t])) && vs[t] >= te;
+      const bool ok = !bad[t] && vs[t] >= te;
       key[p] = ok ? ord_key(vs[t]) : 0u;
       idx[p] = a.index_base + vi[t];
       nvalid += ok;
