@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GR_HSTU_ABI_VERSION 14
+#define GR_HSTU_ABI_VERSION 15
 
 #ifndef GR_API
 #define GR_API __attribute__((visibility("default")))
@@ -52,9 +52,14 @@ GR_API int gr_timing_enable(int on);
 GR_API int gr_timing_query(const char* kernel, double* total_ms, int* launches);
 GR_API int gr_timing_reset(void);
 
-/* Process-wide launch options (the library reads no environment variables).  Set
- * before the launches they should affect; not while a graph that used them is being
- * captured.  gr_get_option returns the current value (or -1 for an unknown option).
+/* Launch options (the library reads no environment variables).  gr_set_option sets the
+ * process-wide value; gr_set_thread_option overrides it for the calling thread only
+ * (gr_clear_thread_option(opt) drops one override, opt = 0 all of them), so threads or
+ * streams driven from different threads can use different options without racing
+ * (ABI 15; tests/test_capi.py::test_thread_options_are_per_thread).  Every launch and
+ * workspace query reads the calling thread's value.  Set options before the launches they
+ * should affect; not while a graph that used them is being captured.  gr_get_option
+ * returns the calling thread's current value (or -1 for an unknown option).
  * Workspace sizes: a *_workspace_size query answers for the options in force when it
  * is called, and every launch re-derives its need under the options in force at launch.
  * A workspace sized under other options is therefore never overrun: the launch returns
@@ -137,6 +142,8 @@ enum {
   GR_OPT_COUNT_ = 18
 };
 GR_API int gr_set_option(int option, int64_t value);
+GR_API int gr_set_thread_option(int option, int64_t value);
+GR_API int gr_clear_thread_option(int option);
 GR_API int64_t gr_get_option(int option);
 
 /* ---------------------------------------------------------------- jagged layout
@@ -550,6 +557,10 @@ GR_API int hstu_attn_fwd_bnd(const float* q, const float* k, const float* v, int
  * wave, once its dq rows are stored, runs the row-wave boundary unit of those 16 rows
  * (d_uvqk of the rows is then complete: du from the previous boundary, dk / dv from the
  * dK/dV launch, dq just stored) -- one launch and one re-read of the rows fewer.
+ * The epilogue form needs the two-pass stored-dS backward (option GR_OPT_ATTN_BWD_DS at 1,
+ * the default; at 0 or 2 the attention runs without it and the boundary is the second call)
+ * and dq / dk / dv_out as column slices of bnd->dh (ld_d == ld_dh, each pointer within
+ * dh's first row), since the epilogue reads the rows' d_uvqk back from dh.
  * Otherwise the two calls run as they are.  `bnd` holds the boundary call's arguments
  * (dh = the d_uvqk the attention writes into, stride ld_dh = n_out); results agree with
  * the two calls' to fp32 summation order (the fused epilogue is the row-wave unit of

@@ -118,7 +118,7 @@ KERNEL_NAMES = ("bucket_map", "attn_fwd", "attn_bwd", "attn_bwd_dkv", "attn_bwd_
 
 def parse_options(path: str = HEADER_PATH) -> dict:
     """{"MIPS_FILTER_FP32": 1, ...}: the GR_OPT_* launch options declared in gr_hstu.h."""
-    text = open(path).read()
+    text = re.sub(r"/\*.*?\*/", "", open(path).read(), flags=re.S)  # the enum, not the comments
     return {m.group(1): int(m.group(2))
             for m in re.finditer(r"\bGR_OPT_([A-Z0-9_]*[A-Z0-9])\s*=\s*(\d+)", text)}
 
@@ -144,6 +144,29 @@ def option(name: str, value: int):
         yield
     finally:
         set_option(name, old)
+
+
+def set_thread_option(name: str, value: int) -> None:
+    """Overrides launch option GR_OPT_<name> for the calling thread only (gr_set_thread_option);
+    launches and workspace queries from other threads keep their own values."""
+    call("gr_set_thread_option", parse_options()[name], int(value))
+
+
+def clear_thread_option(name: str | None = None) -> None:
+    """Drops the calling thread's override of GR_OPT_<name> (all overrides for None)."""
+    call("gr_clear_thread_option", 0 if name is None else parse_options()[name])
+
+
+@contextlib.contextmanager
+def thread_option(name: str, value: int):
+    """Scoped per-thread launch option.  Note that torch runs autograd backward functions
+    of GPU tensors on its own device threads: options meant for a backward must be
+    process-wide (``option``) or set inside the backward's thread."""
+    set_thread_option(name, value)
+    try:
+        yield
+    finally:
+        clear_thread_option(name)
 
 
 def timing_enable(on: bool = True):

@@ -64,7 +64,7 @@ struct BufTile {
     const int tid = threadIdx.x;
     if (vec2) {
       const int c = 2 * (tid % CPH), rr = tid / CPH;
-      const int voff = c < ncols ? ((r0 + rr) * (int)ld + c) * 4 : 0x40000000;
+      const int voff = c < ncols ? ((r0 + rr) * (int)ld + c) * 4 : OOB_OFF;
       const int step = RPP2 * (int)ld * 4;
 #pragma unroll
       for (int i = 0; i < PER2; ++i) {
@@ -77,7 +77,7 @@ struct BufTile {
       // columns past ncols read out of range (0 from the range check): no select after
       // the load, so all PER loads stay in flight
       const int c = tid % CPR, rr = tid / CPR;
-      const int voff = c < ncols ? ((r0 + rr) * (int)ld + c) * 4 : 0x40000000;
+      const int voff = c < ncols ? ((r0 + rr) * (int)ld + c) * 4 : OOB_OFF;
       const int step = RPP * (int)ld * 4;
 #pragma unroll
       for (int i = 0; i < PER; ++i) v[i] = buf_ld(r, voff, i * step);

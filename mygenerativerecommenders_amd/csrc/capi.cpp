@@ -24,8 +24,25 @@ const char* last_error() { return g_err.c_str(); }
 
 // ---------------------------------------------------------------- launch options
 static std::atomic<int64_t> g_opt[GR_OPT_COUNT_] = {0, 0, 0, 0, 0, 0, 1, 1, 1, 0, 0, 1, 1, 0, 1, 0, 1, 1};
+// Per-thread overrides (gr_set_thread_option): bit i of t_set = option i overridden on this
+// thread.  A launch and the workspace query before it read the same thread's values, so
+// threads that use different options never see each other's.
+static thread_local int64_t t_opt[GR_OPT_COUNT_];
+static thread_local uint32_t t_set = 0u;
+static_assert(GR_OPT_COUNT_ <= 32, "t_set holds one bit per option");
 
-int64_t option(int which) { return g_opt[which].load(std::memory_order_relaxed); }
+int64_t option(int which) {
+  if ((t_set >> which) & 1u) return t_opt[which];
+  return g_opt[which].load(std::memory_order_relaxed);
+}
+
+static int check_option(int option, int64_t value) {
+  GR_REQUIRE(option > 0 && option < GR_OPT_COUNT_, "gr_set_option: unknown option %d", option);
+  GR_REQUIRE(option != GR_OPT_MIPS_FILTER_WGS || (value >= 0 && value <= 16),
+             "gr_set_option: filter WGs per CU %lld not in [0, 16]", (long long)value);
+  GR_REQUIRE(value >= 0, "gr_set_option: negative value %lld", (long long)value);
+  return 0;
+}
 
 // ---------------------------------------------------------------- live kernel timing
 struct TimedPair {
@@ -57,11 +74,24 @@ const char* gr_last_error(void) { return gr::last_error(); }
 int gr_version(void) { return GR_HSTU_ABI_VERSION; }
 
 int gr_set_option(int option, int64_t value) {
-  GR_REQUIRE(option > 0 && option < GR_OPT_COUNT_, "gr_set_option: unknown option %d", option);
-  GR_REQUIRE(option != GR_OPT_MIPS_FILTER_WGS || (value >= 0 && value <= 16),
-             "gr_set_option: filter WGs per CU %lld not in [0, 16]", (long long)value);
-  GR_REQUIRE(value >= 0, "gr_set_option: negative value %lld", (long long)value);
+  if (gr::check_option(option, value)) return 1;
   gr::g_opt[option].store(value, std::memory_order_relaxed);
+  return 0;
+}
+
+int gr_set_thread_option(int option, int64_t value) {
+  if (gr::check_option(option, value)) return 1;
+  gr::t_opt[option] = value;
+  gr::t_set |= 1u << option;
+  return 0;
+}
+
+int gr_clear_thread_option(int option) {
+  GR_REQUIRE(option >= 0 && option < GR_OPT_COUNT_, "gr_clear_thread_option: unknown option %d", option);
+  if (option == 0)
+    gr::t_set = 0u;
+  else
+    gr::t_set &= ~(1u << option);
   return 0;
 }
 

@@ -147,6 +147,13 @@ __device__ __forceinline__ float sum16(float v) {
   return v;
 }
 
+// Buffer voffset of a masked lane: loads through it return 0 and stores are dropped.
+// A descriptor's num_records is an int (< 2^31 bytes) and voffsets are unsigned, so 2^31
+// — plus any row step below 2^31 — fails the range check for every buffer this library
+// builds.  (Rounds 1-5 used 2^30, which a buffer over 1 GiB would have served from real
+// data; tests/test_gpu_wgrad.py::test_wgrad_stream_operand_over_1gib covers that case.)
+constexpr int OOB_OFF = (int)0x80000000u;
+
 // Global-address-space view of a pointer: keeps hipcc on global_load (counted by
 // vmcnt alone) where address-space inference fails (pointers through structs /
 // lambdas), instead of flat_load (which forces vmcnt(0) + lgkmcnt(0) waits).

@@ -63,8 +63,8 @@ struct Bf16Stage {
 #pragma unroll
       for (int u = 0; u < RU; ++u) {
         const int base = ((r0 + row + u) * (int)ld + c) * 4;
-        v[i][2 * u] = buf_ld(r, in && c < ncols ? base : 0x40000000, 0);
-        v[i][2 * u + 1] = buf_ld(r, in && c + 1 < ncols ? base + 4 : 0x40000000, 0);
+        v[i][2 * u] = buf_ld(r, in && c < ncols ? base : OOB_OFF, 0);
+        v[i][2 * u + 1] = buf_ld(r, in && c + 1 < ncols ? base + 4 : OOB_OFF, 0);
       }
     }
   }
@@ -381,8 +381,8 @@ struct DualStage {
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int base = ((r0 + row + u) * (int)ld + c) * 4;
-        v[i][2 * u] = buf_ld(r, in && c < ncols ? base : 0x40000000, 0);
-        v[i][2 * u + 1] = buf_ld(r, in && c + 1 < ncols ? base + 4 : 0x40000000, 0);
+        v[i][2 * u] = buf_ld(r, in && c < ncols ? base : OOB_OFF, 0);
+        v[i][2 * u + 1] = buf_ld(r, in && c + 1 < ncols ? base + 4 : OOB_OFF, 0);
       }
     }
   }

@@ -1031,7 +1031,7 @@ __device__ __forceinline__ bool attn_bwd_dq_wave_body(const AttnBwdArgs& a, cons
 #pragma unroll
   for (int t = 0; t < KT; ++t) {
     const int c = 16 * t + lr;
-    voff[t] = c < a.dqk ? (4 * lg * (int)a.ld_qk + c) * 4 : 0x40000000;
+    voff[t] = c < a.dqk ? (4 * lg * (int)a.ld_qk + c) * 4 : OOB_OFF;
   }
   f4 dQ[KT];
 #pragma unroll
@@ -1522,8 +1522,15 @@ extern "C" int hstu_attn_bwd_bnd(const float* q, const float* k, const float* v,
   const bool aligned = pair_aligned({g.dh, g.x, g.dy_res, g.dx, g.u, g.attn, g.h_u, g.du, g.d_attn},
                                     {g.ld_dh, g.ld_x, g.ld_dy, g.ld_dx, g.ld_u, g.ld_attn, g.ld_h,
                                      g.ld_du, g.ld_da, g.n_out, g.D, g.hdv});
+  // the epilogue reads the rows' d_uvqk from dh right after the dQ stores: only when dq,
+  // dk and dv are column slices of dh (the layout ops.py uses); any other layout runs the
+  // two calls, which are correct for every layout
+  auto in_dh = [&](const float* p) {
+    return p >= g.dh && p < g.dh + g.ld_dh && ld_d == g.ld_dh;
+  };
+  const bool alias_ok = in_dh(dq) && in_dh(dk) && in_dh(dvv);
   const bool fuse = option(GR_OPT_BOUNDARY_FUSE) != 0 && option(GR_OPT_ROWWAVE) != 0 && H == 1 &&
-                    bc.kg1 > 0 && in_w4(g.D) && (!bc.op2 || in_w4(g.hdv)) && aligned &&
+                    bc.kg1 > 0 && in_w4(g.D) && (!bc.op2 || in_w4(g.hdv)) && aligned && alias_ok &&
                     g.max_rows * 4 * 1024 <= 0x7fffffffLL;
   if (int rc = attn_bwd_impl(q, k, v, ld_qk, ld_v, dout, ld_dout, offsets, B, N, max_len, H, dqk, dv,
                              bucket_map, pos_w, ts_w, num_buckets, hq, hk, hv, ld_h, dq, dk, dvv,

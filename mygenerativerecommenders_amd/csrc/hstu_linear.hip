@@ -182,7 +182,7 @@ __global__ __launch_bounds__(256) void rowpanel_kernel(Op op) {
   const int b_c = Op::B_N_CONTIG ? tid % NP2 : tid / BKT;  // B: column n0 + b_c (+CPP i)
   const int b_r = Op::B_N_CONTIG ? tid / NP2 : tid % BKT;  // of k-row b_r (+RPB i)
   const bool b_col = Op::B_N_CONTIG ? (b_c < P::BN && n0 + b_c < op.N) : true;
-  const int vb = b_col ? (b_r * bks + (n0 + b_c) * bns) * 4 : 0x40000000;
+  const int vb = b_col ? (b_r * bks + (n0 + b_c) * bns) * 4 : OOB_OFF;
 
   float ra[NA], ra2[Op::NSRC == 2 ? NA : 1], rb[NB];
   auto load = [&](int k0) {
@@ -328,7 +328,7 @@ __global__ __launch_bounds__(256) void rowpanel_bf16_kernel(Op op) {
   const int b_c = Op::B_N_CONTIG ? tid % NP2 : tid / BKT;
   const int b_r = Op::B_N_CONTIG ? tid / NP2 : tid % BKT;
   const bool b_col = Op::B_N_CONTIG ? (b_c < P::BN && n0 + b_c < op.N) : true;
-  const int vb = b_col ? (b_r * bks + (n0 + b_c) * bns) * 4 : 0x40000000;
+  const int vb = b_col ? (b_r * bks + (n0 + b_c) * bns) * 4 : OOB_OFF;
 
   float ra[NA], ra2[Op::NSRC == 2 ? NA : 1], rb[NB];
   auto load = [&](int k0) {
@@ -457,7 +457,7 @@ __global__ __launch_bounds__(256) void rowpanel_bf16v_kernel(Op op) {
   const int bp = lane & 3, bn = (lane >> 2) + 16 * w;
   int vb;
   if constexpr (Op::B_N_CONTIG)
-    vb = n0 + 4 * bn < op.N ? (2 * bp * bks + n0 + 4 * bn) * 4 : 0x40000000;
+    vb = n0 + 4 * bn < op.N ? (2 * bp * bks + n0 + 4 * bn) * 4 : OOB_OFF;
   else
     vb = (4 * bq + (n0 + bc) * bns) * 4;
 

@@ -31,7 +31,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t mat_rsrc(const float* base, in
 
 // Byte offset that fails the buffer range check: loads through it return 0 and stores
 // are dropped — column / row masking without branches.
-constexpr int OOB = 0x40000000;
+constexpr int OOB = OOB_OFF;
 
 // A lane's "quad": 4 columns of a 16-column tile (base tb) owned by lane group lg.
 //   VEC = 4 (16-byte aligned rows):  tb + 4lg + e                     (one 16-byte access)

@@ -138,13 +138,13 @@ __device__ __forceinline__ void wgrad_panel(const WgradProb& g, const int64_t* o
 #pragma unroll
     for (int i = 0; i < C::APER; ++i) {
       const int rr = rr0 + ar + (WG_THREADS / 64) * i;
-      ra_v[u][i] = buf_ld(ra, a_ok ? (int)((rr * g.lda + aka) * 4) : 0x40000000, 0);
+      ra_v[u][i] = buf_ld(ra, a_ok ? (int)((rr * g.lda + aka) * 4) : OOB_OFF, 0);
     }
     if (g.a_stats && tid < WG_CH) st_v[u] = ld_f2(g.a_stats, min(r0 + rr0 + tid, total - 1));
 #pragma unroll
     for (int i = 0; i < C::BPER; ++i) {
       const int rr = rr0 + br + C::BRPP * i;
-      rb_v[u][i] = buf_ld(rb, b_in ? (int)((rr * g.ldb + bnb) * 4) : 0x40000000, 0);
+      rb_v[u][i] = buf_ld(rb, b_in ? (int)((rr * g.ldb + bnb) * 4) : OOB_OFF, 0);
     }
   };
   auto store = [&](int u, int buf, int ch) {
@@ -317,13 +317,13 @@ __device__ __forceinline__ void wgrad_panel_bf16(const WgradProb& g, const int64
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int rr = rr0 + 8 * ag + i;
-      av_[i] = buf_ld(ra, a_ok ? (int)((rr * g.lda + aka) * 4) : 0x40000000, 0);
+      av_[i] = buf_ld(ra, a_ok ? (int)((rr * g.lda + aka) * 4) : OOB_OFF, 0);
       sv_[i] = g.a_stats ? ld_f2(g.a_stats, min(r0 + rr, total - 1)) : make_float2(0.f, 1.f);
     }
 #pragma unroll
     for (int i = 0; i < C::RB; ++i) {
       const int rr = rr0 + C::RB * bg + i;
-      bv_[i] = buf_ld(rb, b_in ? (int)((rr * g.ldb + bnb) * 4) : 0x40000000, 0);
+      bv_[i] = buf_ld(rb, b_in ? (int)((rr * g.ldb + bnb) * 4) : OOB_OFF, 0);
     }
   };
   auto store = [&](int ch) {
@@ -444,7 +444,7 @@ __device__ __forceinline__ void wgrad_tile_bf16w(const WgradProb& g, const int64
   // staging: thread t owns columns 4 (t % 64) .. +3 of rows t / 64 + 8 i (i < 4)
   const int sc = 4 * (tid & 63), sr = tid >> 6;
   const bool a_ok = sc < g.Ka, b_ok = nb0 + sc < g.Nb;  // Ka, Nb multiples of 4 (host check)
-  const int aoff = a_ok ? sc * 4 : 0x40000000, boff = b_ok ? (nb0 + sc) * 4 : 0x40000000;
+  const int aoff = a_ok ? sc * 4 : OOB_OFF, boff = b_ok ? (nb0 + sc) * 4 : OOB_OFF;
   typedef float f4v __attribute__((ext_vector_type(4)));
   f4v av[4], bv[4];
   float2 stv[4];
@@ -569,7 +569,7 @@ __device__ __forceinline__ void wgrad_tile_f32w(const WgradProb& g, const int64_
   // staging: thread t owns columns 4 (t % 64) .. +3 of rows t / 64 + 8 i (i < 2)
   const int sc = 4 * (tid & 63), sr = tid >> 6;
   const bool a_ok = sc < g.Ka, b_ok = nb0 + sc < g.Nb;
-  const int aoff = a_ok ? sc * 4 : 0x40000000, boff = b_ok ? (nb0 + sc) * 4 : 0x40000000;
+  const int aoff = a_ok ? sc * 4 : OOB_OFF, boff = b_ok ? (nb0 + sc) * 4 : OOB_OFF;
   typedef float f4v __attribute__((ext_vector_type(4)));
   f4v av[2], bv[2];
   float2 stv[2];
@@ -1017,7 +1017,7 @@ __device__ __forceinline__ void ws_body(const WsProb& g, int64_t total, int spli
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(g.a_stats ? (const void*)g.a_stats : (const void*)g.a), 0,
       g.a_stats ? (int)(total * 8) : 0, 0x00020000);
-  constexpr int OOBW = 0x40000000;
+  constexpr int OOBW = OOB_OFF;
   const int acol = 4 * lr, bcol = 64 * gi + 4 * lr;
   const bool a_lo = acol < g.Ka, a_hi = acol + 2 < g.Ka;  // Ka even: 8-byte pieces in or out
   const bool b_lo = bcol < g.Nb, b_hi = bcol + 2 < g.Nb;

@@ -41,14 +41,18 @@ def _default_bucketization_fn(x: torch.Tensor) -> torch.Tensor:
 
 
 def _bucket_probe_deltas() -> torch.Tensor:
-    """int64 time deltas probing every edge of the threshold table: each threshold, its
-    two neighbours, the midpoint to the next threshold, and their negations."""
+    """int64 time deltas probing the threshold table: each threshold, its two neighbours
+    and the midpoint to the next threshold; every delta in [0, 4096]; 8,192 deltas drawn
+    log-uniformly over [1, 2^62] from a fixed seed; and their negations."""
     thr = BUCKET_THRESHOLDS
-    vals = set()
+    vals = set(range(4097))
     for b, t in enumerate(thr):
         vals.update((t - 1, t, t + 1))
         if b + 1 < len(thr):
             vals.add((t + thr[b + 1]) // 2)
+    g = torch.Generator().manual_seed(20240)
+    e = torch.rand(8192, generator=g, dtype=torch.float64) * 62.0
+    vals.update(int(v) for v in torch.exp2(e).to(torch.int64).tolist())
     vals = sorted(v for v in vals if v >= 0)
     return torch.tensor(vals + [-v for v in vals], dtype=torch.int64)
 
@@ -59,7 +63,9 @@ def _check_bucketization_fn(fn: Callable[[torch.Tensor], torch.Tensor]) -> None:
     hstu.py:117-123).  A caller-supplied function is accepted only if it agrees with
     that table on every probe delta (the reference builds it as a lambda, so an identity
     test would reject valid models); anything else raises instead of silently using
-    the default buckets."""
+    the default buckets.  The check is a sampling heuristic, not a proof: ~25 K probes
+    cover every threshold edge, all small deltas and a log-uniform sample of the int64
+    range, so a function that agrees on all of them and differs elsewhere would pass."""
     d = _bucket_probe_deltas()
     thr = torch.tensor(BUCKET_THRESHOLDS, dtype=torch.int64)
     want = torch.searchsorted(thr, d.abs(), right=True) - 1

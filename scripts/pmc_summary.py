@@ -119,6 +119,8 @@ def main():
         per_grid[f"{key[0]}@grid{key[1]}"] = {
             "kernel": key[0], "grid": key[1], "launches_traced": len(d),
             "avg_ms": sum(d) / len(d) if d else None,
+            "median_ms": sorted(d)[len(d) // 2] if d else None,
+            "min_ms": min(d) if d else None,
             "fetch_kb": fa, "write_kb": wa,
             "hbm_bytes_per_launch": (2 * fa + wa) * 1024 if fa is not None and wa is not None else None,
         }
@@ -137,6 +139,7 @@ def main():
     for k, e in sorted(kernels.items()):
         hb = e["hbm_bytes_per_launch"]
         print(f"{k:18s} grid={e['grid']:>9d} avg_ms={e['avg_ms'] or 0:8.4f} "
+              f"median_ms={e['median_ms'] or 0:8.4f} "
               f"hbm_MB={(hb or 0) / 1e6:9.3f}")
 
 

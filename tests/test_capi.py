@@ -206,3 +206,56 @@ def test_boundary_struct_layout_matches_header(tmp_path, struct):
     got = [int(v) for v in subprocess.check_output([str(exe)], text=True).split()]
     assert got[0] == ctypes.sizeof(GrBoundaryBwd)
     assert got[1:] == [getattr(GrBoundaryBwd, n).offset for n in names]
+
+
+def test_thread_options_are_per_thread():
+    """gr_set_thread_option overrides an option for the calling thread only,
+    so two threads that size and launch under different options never see each other's
+    values (ctypes drops the GIL inside each call, so the threads really overlap in the
+    library).  Each thread checks its workspace sizes against the values its options
+    give when run alone, and a launch sized under the other thread's options is rejected
+    (the check runs before any device work: fake pointers are never dereferenced)."""
+    import threading
+    L = _lib.lib()
+    fake = 1 << 20
+    # reference sizes, computed serially with process-wide options
+    want = {}
+    for rows, stride in ((4096, 64), (256, 8)):
+        with _lib.option("WGRAD_ROWS", rows), _lib.option("MIPS_SAMPLE_STRIDE", stride):
+            want[rows] = (L.gr_wgrad_workspace_size(200000, 300, 200),
+                          L.mips_topk_workspace_size(128, 10_000_000, 50, 200, 211))
+    assert want[256][0] > want[4096][0] and want[256][1] > want[4096][1]
+    start = threading.Barrier(2)
+    errors = []
+
+    def worker(rows, stride, other_rows):
+        try:
+            _lib.set_thread_option("WGRAD_ROWS", rows)
+            _lib.set_thread_option("MIPS_SAMPLE_STRIDE", stride)
+            assert _lib.get_option("WGRAD_ROWS") == rows
+            start.wait()
+            for _ in range(2000):
+                got = (L.gr_wgrad_workspace_size(200000, 300, 200),
+                       L.mips_topk_workspace_size(128, 10_000_000, 50, 200, 211))
+                assert got == want[rows], (rows, got, want[rows])
+            if rows == 256:  # the other thread's (smaller) workspace is refused here
+                with pytest.raises(_lib.GrError, match="workspace"):
+                    _lib.call("gr_wgrad", fake, 300, None, fake, 200, fake, 128, 200000, 300, 200,
+                              fake, None, fake, want[other_rows][0], None)
+            _lib.clear_thread_option()
+            assert _lib.get_option("WGRAD_ROWS") == 0  # back to the process-wide default
+        except BaseException as e:  # noqa: BLE001 — reported by the main thread
+            errors.append(e)
+
+    ts = [threading.Thread(target=worker, args=(4096, 64, 256)),
+          threading.Thread(target=worker, args=(256, 8, 4096))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors
+    # the main thread never saw either override
+    assert _lib.get_option("WGRAD_ROWS") == 0 and _lib.get_option("MIPS_SAMPLE_STRIDE") == 0
+    with pytest.raises(_lib.GrError):
+        _lib.set_thread_option("MIPS_FILTER_WGS", 17)
+    assert L.gr_clear_thread_option(99) != 0

@@ -139,3 +139,29 @@ def test_wgrad_single_wide_many_rows(Ka, Nb):
     rc, rcs = _ref(a, b, st, total)
     _check(c, rc, "C")
     _check(cs, rcs, "colsum")
+
+
+def test_wgrad_stream_operand_over_1gib():
+    """the streaming form masks padding k-steps and out-of-range
+    columns with a buffer voffset that must fail the range check at ANY operand size.
+    Rounds 1-5 used 2^30: with an operand over 1 GiB those lanes read real data there and
+    added it into C.  Here A (no row stats, the _o problem's dy) and B are 1.1 GB each;
+    the masked offset is now 2^31 (common.h OOB_OFF), above every num_records."""
+    L = _lib()
+    Ka = Nb = 64
+    rows = [1_100_000, 1_050_001, 1_100_003, 1_050_000]  # 4.3 M rows: 1.1 GB per operand
+    offs, total, cap, a, b, _ = _case(rows, Ka, Nb, 11, stats=False)
+    assert a.numel() * 4 > (1 << 30) and b.numel() * 4 > (1 << 30)
+    lib = L.lib()
+    with L.option("WGRAD_STREAM", 1):
+        ws_n = lib.gr_wgrad_workspace_size(cap, Ka, Nb)
+        ws = torch.empty(max(ws_n, 4), dtype=torch.uint8, device="cuda")
+        c = torch.full((Ka, Nb), float("nan"), device="cuda")
+        cs = torch.full((Ka,), float("nan"), device="cuda")
+        L.call("gr_wgrad", a.data_ptr(), Ka, None, b.data_ptr(), Nb, offs.data_ptr(),
+               offs.numel() - 1, cap, Ka, Nb, c.data_ptr(), cs.data_ptr(), ws.data_ptr(), ws_n,
+               L.stream_handle())
+        torch.cuda.synchronize()
+    rc, rcs = _ref(a, b, None, total)
+    _check(c, rc, "C")
+    _check(cs, rcs, "colsum")
