@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GR_HSTU_ABI_VERSION 15
+#define GR_HSTU_ABI_VERSION 16
 
 #ifndef GR_API
 #define GR_API __attribute__((visibility("default")))
@@ -647,6 +647,69 @@ GR_API int gr_wgrad2_bf16(const float* a0, int64_t lda0, const float* a_stats0, 
 GR_API size_t gr_wgrad_multi_workspace_size(const int64_t* desc, int n_problems, int64_t max_rows);
 GR_API int gr_wgrad_multi(const int64_t* desc, int n_problems, const int64_t* offsets, int B,
                     int64_t max_rows, int bf16, void* workspace, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------- bf16 activations
+ * ABI 16.  HSTU(autocast_dtype=torch.bfloat16) at wide heads (dqk == dv = d, d % 32 == 0,
+ * 128 < d <= 256: the ml-20m width) keeps the layer's activations in HBM as bf16, as the
+ * reference's autocast region does (hstu.py:439-480: the mm outputs h, silu(h) and their
+ * gradients are bf16 there; LayerNorm statistics, accumulation, parameters, the residual
+ * stream x / y and d_attn stay fp32).  bf16 buffers are uint16_t* (raw bf16 bits).
+ * Every entry runs the same kernels as its *_bf16 counterpart on the same bf16 operands,
+ * so results equal that entry's on the bf16-rounded inputs, rounded to bf16 where the
+ * output is bf16 (tests/test_gpu_a16.py).  What the layout removes: the Q/K/V conversion
+ * pass (the attention DMAs its tiles straight from the bf16 uvqk rows), half of every
+ * projection's activation bytes, and the weight gradients' fp32 operand reads.
+ *
+ * hstu_ln_uvqk_fwd_a16: hstu_ln_uvqk_fwd with bf16 h_pre (optional) and uvqk (n_out,
+ *   ld_out even), plus optional xn (rows, D) = bf16 LN(x), the weight gradient's A operand
+ *   (replaces hstu.py:258-305 under autocast).
+ * hstu_attn_fwd_a16: hstu_attn_fwd_bf16 on bf16 q / k / v rows (16-byte aligned, ld_qkv a
+ *   multiple of 8); zrow = d zero bf16 values (caller-owned, 16-byte aligned).
+ * hstu_gate_o_fwd_a16 / _bwd_a16: u, h_u, o_in and du in bf16 (hstu.py:393-413).
+ * hstu_attn_bwd_a16: dq / dk / dv (bf16, written with silu'(h) from bf16 h applied) of
+ *   hstu_attn_bwd_bf16; dout stays fp32 (it is d_attn); workspace from
+ *   hstu_attn_bwd_a16_workspace_size.
+ * hstu_ln_uvqk_bwd_a16: dh (d_uvqk) in bf16.
+ * gr_wgrad_multi_a16: gr_wgrad_multi with bf16 MFMA operands and a 10th descriptor word of
+ *   flags per problem (bit 0: A rows bf16, bit 1: B rows bf16); Ka <= 256, Ka, Nb, lda,
+ *   ldb multiples of 4, bf16 rows 8-byte aligned, a bf16 A takes no row stats. */
+GR_API int hstu_ln_uvqk_fwd_a16(const float* x, int64_t ld_x, const int64_t* offsets, int B,
+                    int64_t max_rows, int D, const float* w_uvqk, int n_out, float eps,
+                    int activation, float* x_stats, uint16_t* h_pre, uint16_t* uvqk,
+                    int64_t ld_out, uint16_t* xn, void* stream);
+GR_API int hstu_attn_fwd_a16(const uint16_t* q, const uint16_t* k, const uint16_t* v,
+                    int64_t ld_qkv, const int64_t* offsets, int B, int N, int max_len, int H,
+                    int d, const uint8_t* bucket_map, const float* pos_w, const float* ts_w,
+                    int num_buckets, const uint16_t* zrow, float* out, int64_t ld_out,
+                    void* stream);
+GR_API int hstu_gate_o_fwd_a16(const uint16_t* u, int64_t ld_u, const float* attn, int64_t ld_attn,
+                    const int64_t* offsets, int B, int64_t max_rows, int hdv, int D,
+                    const float* w_o, const float* b_o, const float* x_res, int64_t ld_x,
+                    float eps, float dropout_p, uint64_t seed, const int64_t* seed_offset,
+                    float* attn_stats, uint16_t* o_in, float* y, int64_t ld_y, void* stream);
+GR_API int hstu_gate_o_bwd_a16(const float* dy, int64_t ld_dy, const int64_t* offsets, int B,
+                    int64_t max_rows, int hdv, int D, const float* w_o, const uint16_t* u,
+                    int64_t ld_u, const float* attn, int64_t ld_attn, const float* attn_stats,
+                    const uint16_t* h_u, int64_t ld_h, float dropout_p, uint64_t seed,
+                    const int64_t* seed_offset, uint16_t* du, int64_t ld_du, float* d_attn,
+                    int64_t ld_da, void* stream);
+GR_API size_t hstu_attn_bwd_a16_workspace_size(int B, int N, int max_len, int H, int d,
+                    int num_buckets);
+GR_API int hstu_attn_bwd_a16(const uint16_t* q, const uint16_t* k, const uint16_t* v,
+                    int64_t ld_qkv, const float* dout, int64_t ld_dout, const int64_t* offsets,
+                    int B, int N, int max_len, int H, int d, const uint8_t* bucket_map,
+                    const float* pos_w, const float* ts_w, int num_buckets, const uint16_t* hq,
+                    const uint16_t* hk, const uint16_t* hv, int64_t ld_h, uint16_t* dq,
+                    uint16_t* dk, uint16_t* dv_out, int64_t ld_d, float* dpos_w, float* dts_w,
+                    void* workspace, size_t ws_bytes, void* stream);
+GR_API int hstu_ln_uvqk_bwd_a16(const uint16_t* dh, int64_t ld_dh, const int64_t* offsets, int B,
+                    int64_t max_rows, int D, int n_out, const float* w_uvqk, const float* x,
+                    int64_t ld_x, const float* x_stats, const float* dy_res, int64_t ld_dy,
+                    float* dx, int64_t ld_dx, void* stream);
+GR_API size_t gr_wgrad_multi_a16_workspace_size(const int64_t* desc, int n_problems,
+                    int64_t max_rows);
+GR_API int gr_wgrad_multi_a16(const int64_t* desc, int n_problems, const int64_t* offsets, int B,
+                    int64_t max_rows, void* workspace, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------- MIPS retrieval
  * Replaces indexing/top_k.py:44-70 (MIPSBruteForceTopK: mm + torch.topk) and

@@ -144,9 +144,10 @@ __device__ __forceinline__ int map_soff(int q, int k, bool query_major) {
 // compiler waited for each load in turn (vmcnt(0) per element: ~50 us of serial latency
 // per workgroup at d = 256).
 //   row_of(i): the element row (sequence-relative), col_of(t): the column
-template <int NR, int NT, typename V, typename RowF, typename ColF>
+//   OutT / HT: float, or __bf16 for the bf16-activation layout (hstu_attn_bwd_a16)
+template <int NR, int NT, typename V, typename RowF, typename ColF, typename OutT, typename HT>
 __device__ __forceinline__ void store_scaled(const V& val, int L, int width, int64_t s0,
-                                             float* out, int64_t ld_out, const float* hp,
+                                             OutT* out, int64_t ld_out, const HT* hp,
                                              int64_t ld_h, int c0, RowF row_of, ColF col_of) {
   float hv[NR][NT];
   if (hp) {
@@ -157,7 +158,7 @@ __device__ __forceinline__ void store_scaled(const V& val, int L, int width, int
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         const int c = col_of(t);
-        hv[i][t] = as_global(hp)[row * ld_h + c0 + (c < width ? c : 0)];
+        hv[i][t] = (float)as_global(hp)[row * ld_h + c0 + (c < width ? c : 0)];
       }
     }
   }
@@ -169,7 +170,7 @@ __device__ __forceinline__ void store_scaled(const V& val, int L, int width, int
       const int c = col_of(t);
       float g = val(i, t);
       if (hp) g *= silu_grad_(hv[i][t]);
-      if (r < L && c < width) out[(s0 + r) * ld_out + c0 + c] = g;
+      if (r < L && c < width) out[(s0 + r) * ld_out + c0 + c] = (OutT)g;
     }
   }
 }

@@ -146,7 +146,23 @@ struct AttnBwdArgsW {
   float inv_n;
   int n_kt;        // 128-key tiles
   int n_qt;        // 128-query tiles
+  int64_t rsb_qkv; // bf16 elements between rows of qb / kb / vb (H 32 D32 for the copies,
+                   // n_out for the bf16 uvqk of hstu_attn_bwd_a16); ob keeps H 32 D32
+  int a16;         // 1: hq / hk / hv are bf16 h_pre and dq / dk / dvv bf16 d_uvqk (the
+                   // pointers above reinterpreted), 0: fp32
 };
+
+// Epilogue store of 8 accumulator rows: d = acc * silu'(h) in the fp32 or the bf16 layout
+template <int D32, typename V, typename RowF, typename ColF>
+__device__ __forceinline__ void store_dh(const AttnBwdArgsW& a, const V& val, int L, int64_t s0,
+                                         float* out, const float* hp, int h, RowF row_of,
+                                         ColF col_of) {
+  if (a.a16)
+    store_scaled<8, D32>(val, L, a.d, s0, reinterpret_cast<__bf16*>(out), a.ld_d,
+                         reinterpret_cast<const __bf16*>(hp), a.ld_h, h * a.d, row_of, col_of);
+  else
+    store_scaled<8, D32>(val, L, a.d, s0, out, a.ld_d, hp, a.ld_h, h * a.d, row_of, col_of);
+}
 
 constexpr int WK = 128;  // keys (queries) per workgroup: 4 waves x 32
 constexpr int kDtsCopies = 4;  // dts histogram copies per wave (lane % copies)
@@ -234,6 +250,8 @@ struct AttnFwdArgsW {
   int64_t ld_out;
   float inv_n;
   int n_qt;
+  int64_t rsb_qkv;  // bf16 elements between rows of qb / kb / vb: H 32 D32 for the copies,
+                    // n_out for the bf16 uvqk itself (hstu_attn_fwd_a16)
 };
 
 template <int D32, bool HB>
@@ -266,7 +284,7 @@ void attn_fwd_bf16w_kernel(AttnFwdArgsW a) {
   const int q0w = q0 + 32 * w;
   const int qi = q0w + lr;  // this lane's query (column of S^T)
   const bool q_ok = qi < L;
-  const int64_t rsb = (int64_t)a.H * DP;
+  const int64_t rsb = a.rsb_qkv;
   const int64_t hoff = s0 * rsb + (int64_t)h * DP;
   // Q^T fragments of the wave's queries: element j of k-step ks = dim 16 ks + 8 lh + j
   u32x4_t qf[KS];
@@ -442,9 +460,11 @@ __device__ __forceinline__ void kv_body(const AttnBwdArgsW& a, char* smem, int k
   const int k0w = k0 + 32 * w;   // this wave's first key
   const int kj = k0w + lr;       // this lane's key (column of S / dP)
   const bool k_ok = kj < L;
-  // bf16 copies of this (sequence, head): row r at rows + r * rsb
-  const int64_t rsb = (int64_t)a.H * DP;
+  // bf16 Q / K / V of this (sequence, head): row r at rows + r * rsb; dO copy: rsb_o
+  const int64_t rsb = a.rsb_qkv;
   const int64_t hoff = s0 * rsb + (int64_t)h * DP;
+  const int64_t rsb_o = (int64_t)a.H * DP;
+  const int64_t hoff_o = s0 * rsb_o + (int64_t)h * DP;
   // K^T / V^T fragments of the wave's keys: element j of k-step ks = dim 16 ks + 8 lh + j
   u32x4_t kf[KS], vf[KS];
   {
@@ -491,7 +511,7 @@ __device__ __forceinline__ void kv_body(const AttnBwdArgsW& a, char* smem, int k
   // the chunk's Q and dO rows by LDS-DMA, one chunk ahead (drained by the chunk's barrier)
   auto dma = [&](int buf, int r0) {
     dma_tile<D32>(tiles + buf * 2 * TB, a.qb + hoff, rsb, r0, L, a.zrow, w, lane);
-    dma_tile<D32>(tiles + buf * 2 * TB + TB, a.ob + hoff, rsb, r0, L, a.zrow, w, lane);
+    dma_tile<D32>(tiles + buf * 2 * TB + TB, a.ob + hoff_o, rsb_o, r0, L, a.zrow, w, lane);
   };
   dma(0, k0);
   __syncthreads();
@@ -705,8 +725,7 @@ __device__ __forceinline__ void kv_body(const AttnBwdArgsW& a, char* smem, int k
   const float* hp = KIND_K ? a.hk : a.hv;
 #pragma unroll
   for (int g = 0; g < 16; g += 8)  // 8 rows (8 D32 silu'(h) loads) in flight at a time
-    store_scaled<8, D32>([&](int i, int t) { return acc[t][g + i]; }, L, a.d, s0, outp, a.ld_d,
-                         hp, a.ld_h, h * a.d,
+    store_dh<D32>(a, [&](int i, int t) { return acc[t][g + i]; }, L, s0, outp, hp, h,
                          [&](int i) { return k0w + ((g + i) & 3) + 8 * ((g + i) >> 2) + 4 * lh; },
                          [&](int t) { return 32 * t + lr; });
   if (BIAS) {
@@ -829,8 +848,7 @@ __device__ __forceinline__ void v_from_p_body(const AttnBwdArgsW& a, char* smem,
   if (!w_on) return;
 #pragma unroll
   for (int g = 0; g < 16; g += 8)
-    store_scaled<8, D32>([&](int i, int t) { return acc[t][g + i]; }, L, a.d, s0, a.dvv, a.ld_d,
-                         a.hv, a.ld_h, h * a.d,
+    store_dh<D32>(a, [&](int i, int t) { return acc[t][g + i]; }, L, s0, a.dvv, a.hv, h,
                          [&](int i) { return k0w + ((g + i) & 3) + 8 * ((g + i) >> 2) + 4 * lh; },
                          [&](int t) { return 32 * t + lr; });
 }
@@ -920,8 +938,7 @@ __device__ __forceinline__ void v_from_p_ring_body(const AttnBwdArgsW& a, char* 
   if (!w_on) return;
 #pragma unroll
   for (int g = 0; g < 16; g += 8)
-    store_scaled<8, D32>([&](int i, int t) { return acc[t][g + i]; }, L, a.d, s0, a.dvv, a.ld_d,
-                         a.hv, a.ld_h, h * a.d,
+    store_dh<D32>(a, [&](int i, int t) { return acc[t][g + i]; }, L, s0, a.dvv, a.hv, h,
                          [&](int i) { return k0w + ((g + i) & 3) + 8 * ((g + i) >> 2) + 4 * lh; },
                          [&](int t) { return 32 * t + lr; });
 }
@@ -1029,7 +1046,7 @@ void attn_bwd_bf16w_dq_kernel(AttnBwdArgsW a) {
   f32x16 acc[D32];
 #pragma unroll
   for (int t = 0; t < D32; ++t) acc[t] = f16_zero();
-  const int64_t rsb = (int64_t)a.H * DP;
+  const int64_t rsb = a.rsb_qkv;
   const __bf16* krows = a.kb + s0 * rsb + (int64_t)h * DP;
   const int n_kb = (min(q0 + WK, L) + 31) / 32;  // key blocks the workgroup needs
   char* mydl = dsl + w * 2 * 2048;
@@ -1135,8 +1152,7 @@ void attn_bwd_bf16w_dq_kernel(AttnBwdArgsW a) {
   const int lh = lane >> 5;
 #pragma unroll
   for (int g = 0; g < 16; g += 8)
-    store_scaled<8, D32>([&](int i, int t) { return acc[t][g + i]; }, L, a.d, s0, a.dq, a.ld_d,
-                         a.hq, a.ld_h, h * a.d,
+    store_dh<D32>(a, [&](int i, int t) { return acc[t][g + i]; }, L, s0, a.dq, a.hq, h,
                          [&](int i) { return q0w + ((g + i) & 3) + 8 * ((g + i) >> 2) + 4 * lh; },
                          [&](int t) { return 32 * t + lr; });
 }
@@ -1234,6 +1250,7 @@ int gr_attn_fwd_bf16w(const void* copies, const int64_t* offsets, int B, int N, 
   const CopyPtrs c = copy_ptrs(copies, B, N, H, d);
   AttnFwdArgsW a{};
   a.qb = c.q; a.kb = c.k; a.vb = c.v; a.zrow = c.zrow;
+  a.rsb_qkv = (int64_t)H * 32 * ceil_div(d, 32);
   a.offsets = offsets; a.B = B; a.N = N; a.H = H; a.d = d;
   a.map_qk = map_qk; a.pos_w = pos_w; a.ts_w = ts_w; a.nb = map_qk ? num_buckets : 0;
   a.out = out; a.ld_out = ld_out; a.inv_n = 1.0f / (float)N;
@@ -1292,6 +1309,8 @@ int gr_attn_bwd_bf16w(const float* q, const float* k, const float* v, int64_t ld
     n = 4;
   }
   a.zrow = ozrow;
+  a.rsb_qkv = (int64_t)H * 32 * ceil_div(d, 32);
+  a.a16 = 0;
   a.total_rows = (int64_t)B * N;
   if (launch_convert(cs, n, a.total_rows, st)) return -1;
   const int nb32 = ceil_div(N, 32);
@@ -1301,6 +1320,122 @@ int gr_attn_bwd_bf16w(const float* q, const float* k, const float* v, int64_t ld
   a.n_qt = ceil_div(max_len, WK);
   const int D32 = ceil_div(d, 32);
   if (D32 <= 5) return launch_bwd_bf16w<5>(a, dpos_w, dts_w, st);
+  if (D32 == 6) return launch_bwd_bf16w<6>(a, dpos_w, dts_w, st);
+  if (D32 == 7) return launch_bwd_bf16w<7>(a, dpos_w, dts_w, st);
+  return launch_bwd_bf16w<8>(a, dpos_w, dts_w, st);
+}
+
+// ------------------------------------------------------------------ bf16 activations (ABI 16)
+// autocast_dtype = bfloat16 at wide heads with d % 32 == 0: the projection writes uvqk and
+// h_pre as bf16 (hstu_ln_uvqk_fwd_a16), so the attention DMAs its Q / K / V tiles straight
+// from the uvqk rows (row stride n_out, no conversion pass), reads silu'(h) from bf16 h_pre
+// and writes dQ / dK / dV as bf16 into d_uvqk.  Same kernels, same operands: results are
+// the fp32-activation entries' on the bf16-rounded inputs, rounded to bf16 on store.
+static bool a16_shape(int d) { return d > 128 && d <= 256 && d % 32 == 0; }
+static bool a16_aligned(std::initializer_list<const void*> ptrs, int64_t ld) {
+  for (const void* p : ptrs)
+    if ((uintptr_t)p % 16 != 0) return false;
+  return ld % 8 == 0;
+}
+
+extern "C" int hstu_attn_fwd_a16(const uint16_t* q, const uint16_t* k, const uint16_t* v,
+                                 int64_t ld_qkv, const int64_t* offsets, int B, int N, int max_len,
+                                 int H, int d, const uint8_t* bucket_map, const float* pos_w,
+                                 const float* ts_w, int num_buckets, const uint16_t* zrow,
+                                 float* out, int64_t ld_out, void* stream) {
+  using namespace gr;
+  GR_REQUIRE(q && k && v && offsets && out && zrow, "hstu_attn_fwd_a16: null pointer");
+  GR_REQUIRE(B >= 0 && N > 0 && H > 0, "hstu_attn_fwd_a16: bad sizes");
+  GR_REQUIRE(max_len >= 0 && max_len <= N, "hstu_attn_fwd_a16: max_len %d not in [0, N=%d]", max_len, N);
+  GR_REQUIRE(a16_shape(d) && a16_aligned({q, k, v, zrow}, ld_qkv) && ld_qkv >= (int64_t)H * d,
+             "hstu_attn_fwd_a16: needs d %% 32 == 0 in (128, 256] and 16-byte aligned rows (d %d)", d);
+  GR_REQUIRE(!bucket_map || (pos_w && ts_w && num_buckets > 0 && num_buckets < 256),
+             "hstu_attn_fwd_a16: bucket_map given without pos_w/ts_w");
+  if (B == 0 || max_len == 0) return 0;
+  AttnFwdArgsW a{};
+  a.qb = (const __bf16*)q; a.kb = (const __bf16*)k; a.vb = (const __bf16*)v;
+  a.zrow = (const __bf16*)zrow;
+  a.rsb_qkv = ld_qkv;
+  a.offsets = offsets; a.B = B; a.N = N; a.H = H; a.d = d;
+  a.map_qk = bucket_map; a.pos_w = pos_w; a.ts_w = ts_w; a.nb = bucket_map ? num_buckets : 0;
+  a.out = out; a.ld_out = ld_out; a.inv_n = 1.0f / (float)N;
+  hipStream_t st = (hipStream_t)stream;
+  const int D32 = d / 32;
+  if (D32 == 5) return launch_fwd_bf16w<5>(a, st, max_len);
+  if (D32 == 6) return launch_fwd_bf16w<6>(a, st, max_len);
+  if (D32 == 7) return launch_fwd_bf16w<7>(a, st, max_len);
+  return launch_fwd_bf16w<8>(a, st, max_len);
+}
+
+extern "C" size_t hstu_attn_bwd_a16_workspace_size(int B, int N, int max_len, int H, int d,
+                                                   int num_buckets) {
+  if (B <= 0 || N <= 0 || H <= 0 || max_len <= 0 || !a16_shape(d)) return 0;
+  return gr_attn_bwd_bf16w_workspace(B, N, max_len, H, d, num_buckets, true);
+}
+
+extern "C" int hstu_attn_bwd_a16(const uint16_t* q, const uint16_t* k, const uint16_t* v,
+                                 int64_t ld_qkv, const float* dout, int64_t ld_dout,
+                                 const int64_t* offsets, int B, int N, int max_len, int H, int d,
+                                 const uint8_t* bucket_map, const float* pos_w, const float* ts_w,
+                                 int num_buckets, const uint16_t* hq, const uint16_t* hk,
+                                 const uint16_t* hv, int64_t ld_h, uint16_t* dq, uint16_t* dk,
+                                 uint16_t* dvv, int64_t ld_d, float* dpos_w, float* dts_w,
+                                 void* workspace, size_t ws_bytes, void* stream) {
+  using namespace gr;
+  GR_REQUIRE(q && k && v && dout && offsets && dq && dk && dvv, "hstu_attn_bwd_a16: null pointer");
+  GR_REQUIRE(B >= 0 && N > 0 && H > 0, "hstu_attn_bwd_a16: bad sizes");
+  GR_REQUIRE(max_len >= 0 && max_len <= N, "hstu_attn_bwd_a16: max_len %d not in [0, N=%d]", max_len, N);
+  GR_REQUIRE(a16_shape(d) && a16_aligned({q, k, v}, ld_qkv) && ld_qkv >= (int64_t)H * d &&
+                 pair_aligned({dout}, {ld_dout}),
+             "hstu_attn_bwd_a16: needs d %% 32 == 0 in (128, 256] and 16-byte aligned rows (d %d)", d);
+  GR_REQUIRE((hq == nullptr) == (hk == nullptr) && (hk == nullptr) == (hv == nullptr),
+             "hstu_attn_bwd_a16: hq/hk/hv must be all given or all NULL");
+  if (bucket_map)
+    GR_REQUIRE(pos_w && ts_w && dpos_w && dts_w && num_buckets > 0 && num_buckets < 256,
+               "hstu_attn_bwd_a16: bucket_map given without pos_w/ts_w/dpos_w/dts_w");
+  hipStream_t st = (hipStream_t)stream;
+  if (B == 0 || max_len == 0) {
+    if (bucket_map) {
+      zero_words_async(dpos_w, 2 * N - 1, st);
+      zero_words_async(dts_w, num_buckets + 1, st);
+    }
+    return 0;
+  }
+  const size_t need = gr_attn_bwd_bf16w_workspace(B, N, max_len, H, d, num_buckets, true);
+  GR_REQUIRE(workspace && ws_bytes >= need, "hstu_attn_bwd_a16: workspace %zu B < %zu B", ws_bytes, need);
+  const size_t slab_b = al256(bf16w_slab_bytes(B, N, max_len, H, num_buckets));
+  const size_t ds_b = al256(bf16w_ds_bytes(B, N, H));
+  const size_t cp_b = bf16w_copy_bytes(B, N, H, d);
+  const int nch = 4 * (d / 32);
+  AttnBwdArgsW a{};
+  a.dout = dout; a.ld_dout = ld_dout;
+  a.offsets = offsets; a.B = B; a.N = N; a.H = H; a.d = d;
+  a.map_kq = bucket_map ? bucket_map + (size_t)B * attn_tiles_per_seq(N) * 4096 : nullptr;
+  a.pos_w = pos_w; a.ts_w = ts_w; a.nb = bucket_map ? num_buckets : 0;
+  // bf16 h / d through the fp32 pointer fields (a16 = 1, see store_dh)
+  a.hq = (const float*)hq; a.hk = (const float*)hk; a.hv = (const float*)hv; a.ld_h = ld_h;
+  a.dq = (float*)dq; a.dk = (float*)dk; a.dvv = (float*)dvv; a.ld_d = ld_d;
+  a.a16 = 1;
+  a.slabs = (float*)workspace;
+  a.ds = (__bf16*)((char*)workspace + slab_b);
+  a.pb = (__bf16*)((char*)workspace + slab_b + ds_b);
+  char* cp = (char*)workspace + slab_b + 2 * ds_b;
+  a.ob = (__bf16*)cp;
+  __bf16* ozrow = (__bf16*)(cp + cp_b);
+  a.qb = (__bf16*)q; a.kb = (__bf16*)k; a.vb = (__bf16*)v;  // read only
+  a.rsb_qkv = ld_qkv;
+  a.zrow = ozrow;
+  a.total_rows = (int64_t)B * N;
+  ConvSet cs{{dout, nullptr, nullptr, nullptr}, {ld_dout, 0, 0, 0}, {a.ob, nullptr, nullptr, nullptr},
+             ozrow, offsets, B, H, d, nch};
+  if (launch_convert(cs, 1, a.total_rows, st)) return -1;
+  const int nb32 = ceil_div(N, 32);
+  a.nbt = nb32 * (nb32 + 1) / 2;
+  a.inv_n = 1.0f / (float)N;
+  a.n_kt = ceil_div(max_len, WK);
+  a.n_qt = ceil_div(max_len, WK);
+  const int D32 = d / 32;
+  if (D32 == 5) return launch_bwd_bf16w<5>(a, dpos_w, dts_w, st);
   if (D32 == 6) return launch_bwd_bf16w<6>(a, dpos_w, dts_w, st);
   if (D32 == 7) return launch_bwd_bf16w<7>(a, dpos_w, dts_w, st);
   return launch_bwd_bf16w<8>(a, dpos_w, dts_w, st);

@@ -17,6 +17,8 @@
 // and a panel of up to 256 output columns; K is streamed in chunks of 16 through LDS.
 // A operand layout (row stride 18 == 18 mod 32) and B layout (stride == 16 mod 32) make
 // the per-k-step ds_read_b32 of both operands bank-conflict-free.
+#include <type_traits>
+
 #include "common.h"
 #include "attn_common.h"
 #include "rowwave.h"
@@ -133,6 +135,15 @@ __device__ __forceinline__ void panel_row_stats(const float* base, int64_t ld, i
       if (st_glob && m < total) st_glob[m] = make_float2(mean, rstd);
     }
   }
+}
+
+// One A element of EB bytes (4: fp32, 2: bf16 -- the bf16-activation ops, Op::A0_BYTES)
+template <int EB>
+__device__ __forceinline__ float buf_ld_e(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  if constexpr (EB == 2)
+    return __uint_as_float((uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, voff, soff, 0) << 16);
+  else
+    return buf_ld(r, voff, soff);
 }
 
 // Generic row-panel GEMM: C[m, n] = sum_k A'(m, k) * W'(k, n), epilogue by Op.
@@ -321,7 +332,8 @@ __global__ __launch_bounds__(256) void rowpanel_bf16_kernel(Op op) {
   const __amdgpu_buffer_rsrc_t ra1 = op.a_rsrc1(m0, total);
   const int ld0 = (int)op.a_ld0(), ld1 = (int)op.a_ld1();
   const int a_c = tid % BKT, a_r = tid / BKT;
-  const int va0 = (a_r * ld0 + a_c) * 4, va1 = (a_r * ld1 + a_c) * 4;
+  constexpr int E0 = Op::A0_BYTES;  // bytes per element of the first A source
+  const int va0 = (a_r * ld0 + a_c) * E0, va1 = (a_r * ld1 + a_c) * 4;
   const __amdgpu_buffer_rsrc_t rw =
       __builtin_amdgcn_make_buffer_rsrc((void*)op.w, 0, op.K * op.N * 4, 0x00020000);
   const int bks = op.bks(), bns = op.bns();
@@ -334,7 +346,7 @@ __global__ __launch_bounds__(256) void rowpanel_bf16_kernel(Op op) {
   auto load = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
-      ra[i] = buf_ld(ra0, va0 + k0 * 4, i * RPA * ld0 * 4);
+      ra[i] = buf_ld_e<E0>(ra0, va0 + k0 * E0, i * RPA * ld0 * E0);
       if constexpr (Op::NSRC == 2) ra2[i] = buf_ld(ra1, va1 + k0 * 4, i * RPA * ld1 * 4);
     }
 #pragma unroll
@@ -448,7 +460,10 @@ __global__ __launch_bounds__(256) void rowpanel_bf16v_kernel(Op op) {
   const __amdgpu_buffer_rsrc_t ra1 = op.a_rsrc1(m0, total);
   const int ld0 = (int)op.a_ld0(), ld1 = (int)op.a_ld1();
   const int aq = tid & 7, ar = tid >> 3;
-  const int va0 = (ar * ld0 + 4 * aq) * 4, va1 = (ar * ld1 + 4 * aq) * 4;
+  // A0 in bf16 (Op::A0_BYTES == 2, an identity a_xform): the 4 k-values are one 8-byte load
+  // whose bits go to LDS unchanged
+  constexpr bool A0H = Op::A0_BYTES == 2;
+  const int va0 = (ar * ld0 + 4 * aq) * Op::A0_BYTES, va1 = (ar * ld1 + 4 * aq) * 4;
   const __amdgpu_buffer_rsrc_t rw =
       __builtin_amdgcn_make_buffer_rsrc((void*)op.w, 0, op.K * op.N * 4, 0x00020000);
   const int bks = op.bks(), bns = op.bns();
@@ -462,13 +477,17 @@ __global__ __launch_bounds__(256) void rowpanel_bf16v_kernel(Op op) {
     vb = (4 * bq + (n0 + bc) * bns) * 4;
 
   f4 ra[2], ra2[Op::NSRC == 2 ? 2 : 1], rb[8];
+  u32x2_t rh[A0H ? 2 : 1];
   auto ld4 = [](__amdgpu_buffer_rsrc_t r, int v, int s) {
     return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, v, s, 0));
   };
   auto load = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      ra[i] = ld4(ra0, va0 + k0 * 4, i * 32 * ld0 * 4);
+      if constexpr (A0H)
+        rh[A0H ? i : 0] = __builtin_amdgcn_raw_buffer_load_b64(ra0, va0 + k0 * 2, i * 32 * ld0 * 2, 0);
+      else
+        ra[i] = ld4(ra0, va0 + k0 * 4, i * 32 * ld0 * 4);
       if constexpr (Op::NSRC == 2) ra2[Op::NSRC == 2 ? i : 0] = ld4(ra1, va1 + k0 * 4, i * 32 * ld1 * 4);
     }
 #pragma unroll
@@ -486,6 +505,10 @@ __global__ __launch_bounds__(256) void rowpanel_bf16v_kernel(Op op) {
     for (int i = 0; i < 2; ++i) {
       const int r = ar + 32 * i;
       const bool rok = m0 + r < total;
+      if constexpr (A0H) {  // rows >= total read 0 (descriptor range)
+        *reinterpret_cast<u32x2_t*>(As + r * LDK + 4 * aq) = rh[A0H ? i : 0];
+        continue;
+      }
       float v[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -555,6 +578,20 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const float* base, i
   return __builtin_amdgcn_make_buffer_rsrc((void*)(base + m0 * ld), 0, (int)bytes, 0x00020000);
 }
 
+// the same over bf16 rows (the bf16-activation ops)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const __bf16* base, int64_t ld,
+                                                           int64_t m0, int64_t total) {
+  int64_t bytes = (total - m0) * ld * 2;
+  if (bytes > 0x7fffffff) bytes = 0x7fffffff;
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(base + m0 * ld), 0, (int)bytes, 0x00020000);
+}
+
+// Op templates: A16 = the bf16-activation layout (autocast_dtype = bfloat16 at wide heads,
+// hstu_*_a16): uvqk, h_pre, o_in and d_uvqk live in HBM as bf16, read with 2-byte loads
+// and written rounded from the fp32 epilogue values; everything else is unchanged.
+template <bool A16>
+using act_t = typename std::conditional<A16, __bf16, float>::type;
+
 // ------------------------------------------------------------------ ops
 struct NoStats {
   __device__ void prologue(int64_t, int64_t, float2* st) const {
@@ -567,8 +604,10 @@ __device__ __forceinline__ int64_t clamp_row(int64_t m, int64_t total) {
 }
 
 // F1: uvqk = act(LN(x) @ W), W row-major (D, n_out)
-struct OpLnUvqk {
+template <bool A16>
+struct OpLnUvqkT {
   static constexpr bool B_N_CONTIG = true;
+  static constexpr int A0_BYTES = 4;
   const int64_t* offsets;
   int B, K, N;
   const float* x;
@@ -577,9 +616,10 @@ struct OpLnUvqk {
   float eps;
   int act;
   float2* x_stats;
-  float* h_pre;
-  float* out;
+  act_t<A16>* h_pre;
+  act_t<A16>* out;
   int64_t ld_out;
+  __bf16* xn;  // A16: optional bf16 LN(x) rows (ld K), the weight gradient's A operand
   __device__ void prologue(int64_t m0, int64_t total, float2* st) const {
     panel_row_stats(x, ldx, m0, total, K, eps, st, blockIdx.y == 0 ? x_stats : nullptr);
   }
@@ -588,8 +628,11 @@ struct OpLnUvqk {
   __device__ __amdgpu_buffer_rsrc_t a_rsrc1(int64_t m0, int64_t t) const { return rows_rsrc(x, ldx, m0, t); }
   __device__ int64_t a_ld0() const { return ldx; }
   __device__ int64_t a_ld1() const { return ldx; }
-  __device__ float a_xform(float v, float, int64_t, int, float2 st, bool) const {
-    return (v - st.x) * st.y;
+  __device__ float a_xform(float v, float, int64_t m, int k, float2 st, bool valid) const {
+    const float y = (v - st.x) * st.y;
+    if constexpr (A16)
+      if (xn && valid && blockIdx.y == 0) xn[m * K + k] = (__bf16)y;
+    return y;
   }
   __device__ int bks() const { return N; }
   __device__ int bns() const { return 1; }
@@ -599,6 +642,30 @@ struct OpLnUvqk {
   __device__ void epi_load(Epi<NT>&, int64_t, int, int64_t) const {}
   template <int NT>
   __device__ void epilogue(f4 (&acc)[NT], const Epi<NT>&, int64_t mrow, int ncol, int64_t total) const {
+    if constexpr (A16) {
+      // bf16 pairs: lanes lr, lr ^ 1 hold adjacent columns; the even lane stores rows 0, 1
+      // and the odd lane rows 2, 3 of both columns as packed 4-byte stores (N, ld_out even)
+      const bool odd = (threadIdx.x & 1) != 0;
+      const int cb = ncol - (odd ? 1 : 0);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const float sx = odd ? acc[t][0] : acc[t][2], sy = odd ? acc[t][1] : acc[t][3];
+        const float rx = dpp_mov<0xB1>(sx), ry = dpp_mov<0xB1>(sy);
+        const int n = cb + 16 * t;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int64_t m = mrow + (odd ? 2 : 0) + j;
+          const float lo = odd ? (j ? ry : rx) : acc[t][j];
+          const float hi = odd ? acc[t][2 + j] : (j ? ry : rx);
+          if (m < total && n < N) {
+            if (h_pre) *reinterpret_cast<uint32_t*>(h_pre + m * ld_out + n) = pack_bf16(lo, hi);
+            *reinterpret_cast<uint32_t*>(out + m * ld_out + n) =
+                act ? pack_bf16(siluf_(lo), siluf_(hi)) : pack_bf16(lo, hi);
+          }
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int64_t m = mrow + r;
@@ -614,6 +681,7 @@ struct OpLnUvqk {
     }
   }
 };
+using OpLnUvqk = OpLnUvqkT<false>;
 
 __device__ __forceinline__ float dropout_keep(uint64_t seed, int64_t m, int k, int K, float p) {
   if (p <= 0.f) return 1.f;
@@ -623,11 +691,13 @@ __device__ __forceinline__ float dropout_keep(uint64_t seed, int64_t m, int k, i
 }
 
 // F3: y = dropout(u * LN(attn)) @ W_o^T + b_o + x,  W_o row-major (D, hdv)
-struct OpGateO {
+template <bool A16>
+struct OpGateOT {
   static constexpr bool B_N_CONTIG = false;
+  static constexpr int A0_BYTES = A16 ? 2 : 4;  // u
   const int64_t* offsets;
   int B, K, N;  // K = hdv, N = D
-  const float* u;
+  const act_t<A16>* u;
   int64_t ldu;
   const float* attn;
   int64_t lda;
@@ -639,7 +709,7 @@ struct OpGateO {
   uint64_t seed;
   const int64_t* seed_off;
   float2* a_stats;
-  float* o_in;
+  act_t<A16>* o_in;
   float* y;
   int64_t ldy;
   __device__ void prologue(int64_t m0, int64_t total, float2* st) const {
@@ -653,7 +723,7 @@ struct OpGateO {
   __device__ float a_xform(float uv, float av, int64_t m, int k, float2 st, bool valid) const {
     float v = uv * ((av - st.x) * st.y);
     if (p > 0.f) v *= dropout_keep(seed + (seed_off ? (uint64_t)*seed_off : 0ull), m, k, K, p);
-    if (valid && o_in && blockIdx.y == 0) o_in[m * K + k] = v;
+    if (valid && o_in && blockIdx.y == 0) o_in[m * K + k] = (act_t<A16>)v;
     return v;
   }
   __device__ int bks() const { return 1; }
@@ -694,27 +764,30 @@ struct OpGateO {
     }
   }
 };
+using OpGateO = OpGateOT<false>;
 
 // B1: g = dy @ W_o (rows, hdv); epilogue: dropout bwd, du = g*LN(a) (*silu'(h_u)),
 //     d_attn = LayerNorm_bwd(g * u).  Needs the whole hdv row in one panel.
-struct OpGateOBwd : NoStats {
+template <bool A16>
+struct OpGateOBwdT : NoStats {
   static constexpr bool B_N_CONTIG = true;
+  static constexpr int A0_BYTES = 4;  // dy
   const int64_t* offsets;
   int B, K, N;  // K = D, N = hdv
   const float* dy;
   int64_t lddy;
   const float* w;
-  const float* u;
+  const act_t<A16>* u;
   int64_t ldu;
   const float* attn;
   int64_t lda;
   const float2* a_stats;
-  const float* h_u;
+  const act_t<A16>* h_u;
   int64_t ldh;
   float p;
   uint64_t seed;
   const int64_t* seed_off;
-  float* du;
+  act_t<A16>* du;
   int64_t lddu;
   float* da;
   int64_t ldda;
@@ -744,8 +817,8 @@ struct OpGateOBwd : NoStats {
         const int n = ncol + 16 * t;
         const int nc = n < N ? n : N - 1;
         av[t] = as_global(attn)[mc * lda + nc];
-        uv[t] = as_global(u)[mc * ldu + nc];
-        hv[t] = h_u ? as_global(h_u)[mc * ldh + nc] : 0.f;
+        uv[t] = (float)as_global(u)[mc * ldu + nc];
+        hv[t] = h_u ? (float)as_global(h_u)[mc * ldh + nc] : 0.f;
       }
       float s1 = 0.f, s2 = 0.f;
       float lnv[NT], dln[NT];
@@ -757,7 +830,7 @@ struct OpGateOBwd : NoStats {
         const float ln = (av[t] - st.x) * st.y;
         float dd = g * ln;
         if (h_u) dd *= silu_grad_(hv[t]);
-        if (ok) du[m * lddu + n] = dd;
+        if (ok) du[m * lddu + n] = (act_t<A16>)dd;
         lnv[t] = ok ? ln : 0.f;
         dln[t] = ok ? g * uv[t] : 0.f;
         s1 += dln[t];
@@ -776,13 +849,16 @@ struct OpGateOBwd : NoStats {
     }
   }
 };
+using OpGateOBwd = OpGateOBwdT<false>;
 
 // B3: dn = dh @ W_uvqk^T (rows, D); epilogue: dx = dy + LayerNorm_bwd(x; dn).
-struct OpLnUvqkBwd : NoStats {
+template <bool A16>
+struct OpLnUvqkBwdT : NoStats {
   static constexpr bool B_N_CONTIG = false;
+  static constexpr int A0_BYTES = A16 ? 2 : 4;  // dh
   const int64_t* offsets;
   int B, K, N;  // K = n_out (4hd), N = D
-  const float* dh;
+  const act_t<A16>* dh;
   int64_t lddh;
   const float* w;  // (D, n_out) row-major -> b(k, n) = w[n][k]
   const float* x;
@@ -878,6 +954,7 @@ struct OpLnUvqkBwd : NoStats {
     }
   }
 };
+using OpLnUvqkBwd = OpLnUvqkBwdT<false>;
 
 template <class Op>
 static int launch_rowpanel(const Op& op, int64_t max_rows, bool full_row, const char* name,
@@ -1288,6 +1365,74 @@ extern "C" int hstu_ln_uvqk_bwd_bf16(const float* dh, int64_t ld_dh, const int64
                                 const float* dy_res, int64_t ld_dy, float* dx, int64_t ld_dx,
                                 void* stream) {
   return hstu_ln_uvqk_bwd_impl(true, dh, ld_dh, offsets, B, max_rows, D, n_out, w_uvqk, x, ld_x, x_stats, dy_res, ld_dy, dx, ld_dx, stream);
+}
+
+// ---------------------------------------------------------------- bf16 activations (ABI 16)
+// autocast_dtype = bfloat16 at wide heads: uvqk / h_pre / o_in / d_uvqk in bf16 (see the
+// Op templates).  Same bf16 row panels; results equal the *_bf16 entries' on the same
+// (bf16-rounded) inputs, rounded to bf16 where the output is bf16.
+extern "C" int hstu_ln_uvqk_fwd_a16(const float* x, int64_t ld_x, const int64_t* offsets, int B,
+                                    int64_t max_rows, int D, const float* w_uvqk, int n_out,
+                                    float eps, int activation, float* x_stats, uint16_t* h_pre,
+                                    uint16_t* uvqk, int64_t ld_out, uint16_t* xn, void* stream) {
+  GR_REQUIRE(x && offsets && w_uvqk && uvqk && x_stats, "hstu_ln_uvqk_fwd_a16: null pointer");
+  GR_REQUIRE(D > 0 && n_out > 0 && B >= 0 && max_rows >= 0, "hstu_ln_uvqk_fwd_a16: bad sizes");
+  GR_REQUIRE(activation == 0 || activation == 1, "hstu_ln_uvqk_fwd_a16: activation must be 0|1");
+  GR_REQUIRE(n_out % 2 == 0 && ld_out % 2 == 0 && (uintptr_t)uvqk % 4 == 0 && (uintptr_t)h_pre % 4 == 0,
+             "hstu_ln_uvqk_fwd_a16: n_out and ld_out must be even, outputs 4-byte aligned");
+  OpLnUvqkT<true> op{offsets, B, D, n_out, x, ld_x, w_uvqk, eps, activation, (float2*)x_stats,
+                     (__bf16*)h_pre, (__bf16*)uvqk, ld_out, (__bf16*)xn};
+  return launch_rowpanel_bf16(op, max_rows, false, "hstu_ln_uvqk_fwd", (hipStream_t)stream);
+}
+
+extern "C" int hstu_gate_o_fwd_a16(const uint16_t* u, int64_t ld_u, const float* attn, int64_t ld_attn,
+                                   const int64_t* offsets, int B, int64_t max_rows, int hdv, int D,
+                                   const float* w_o, const float* b_o, const float* x_res,
+                                   int64_t ld_x, float eps, float dropout_p, uint64_t seed,
+                                   const int64_t* seed_offset, float* attn_stats, uint16_t* o_in,
+                                   float* y, int64_t ld_y, void* stream) {
+  GR_REQUIRE(u && attn && offsets && w_o && y && attn_stats, "hstu_gate_o_fwd_a16: null pointer");
+  GR_REQUIRE(hdv > 0 && D > 0 && B >= 0, "hstu_gate_o_fwd_a16: bad sizes");
+  GR_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f, "hstu_gate_o_fwd_a16: dropout_p %f", dropout_p);
+  OpGateOT<true> op{offsets, B, hdv, D, (const __bf16*)u, ld_u, attn, ld_attn, w_o, b_o, x_res, ld_x,
+                    eps, dropout_p, seed, seed_offset, (float2*)attn_stats, (__bf16*)o_in, y, ld_y};
+  return launch_rowpanel_bf16(op, max_rows, false, "hstu_gate_o_fwd", (hipStream_t)stream);
+}
+
+extern "C" int hstu_gate_o_bwd_a16(const float* dy, int64_t ld_dy, const int64_t* offsets, int B,
+                                   int64_t max_rows, int hdv, int D, const float* w_o,
+                                   const uint16_t* u, int64_t ld_u, const float* attn, int64_t ld_attn,
+                                   const float* attn_stats, const uint16_t* h_u, int64_t ld_h,
+                                   float dropout_p, uint64_t seed, const int64_t* seed_offset,
+                                   uint16_t* du, int64_t ld_du, float* d_attn, int64_t ld_da,
+                                   void* stream) {
+  GR_REQUIRE(dy && offsets && w_o && u && attn && attn_stats && du && d_attn,
+             "hstu_gate_o_bwd_a16: null pointer");
+  GR_REQUIRE(hdv > 0 && D > 0 && B >= 0, "hstu_gate_o_bwd_a16: bad sizes");
+  OpGateOBwdT<true> op;
+  op.offsets = offsets; op.B = B; op.K = D; op.N = hdv; op.dy = dy; op.lddy = ld_dy;
+  op.w = w_o; op.u = (const __bf16*)u; op.ldu = ld_u; op.attn = attn; op.lda = ld_attn;
+  op.a_stats = (const float2*)attn_stats; op.h_u = (const __bf16*)h_u; op.ldh = ld_h;
+  op.p = dropout_p; op.seed = seed; op.seed_off = seed_offset; op.du = (__bf16*)du; op.lddu = ld_du;
+  op.da = d_attn; op.ldda = ld_da;
+  return launch_rowpanel_bf16(op, max_rows, true, "hstu_gate_o_bwd", (hipStream_t)stream,
+                              rw_vec({dy, w_o}, {ld_dy, hdv}) == 4);
+}
+
+extern "C" int hstu_ln_uvqk_bwd_a16(const uint16_t* dh, int64_t ld_dh, const int64_t* offsets, int B,
+                                    int64_t max_rows, int D, int n_out, const float* w_uvqk,
+                                    const float* x, int64_t ld_x, const float* x_stats,
+                                    const float* dy_res, int64_t ld_dy, float* dx, int64_t ld_dx,
+                                    void* stream) {
+  GR_REQUIRE(dh && offsets && w_uvqk && x && x_stats && dx, "hstu_ln_uvqk_bwd_a16: null pointer");
+  GR_REQUIRE(D > 0 && n_out > 0 && B >= 0, "hstu_ln_uvqk_bwd_a16: bad sizes");
+  OpLnUvqkBwdT<true> op;
+  op.offsets = offsets; op.B = B; op.K = n_out; op.N = D; op.dh = (const __bf16*)dh; op.lddh = ld_dh;
+  op.w = w_uvqk; op.x = x; op.ldx = ld_x; op.x_stats = (const float2*)x_stats;
+  op.dy = dy_res; op.lddy = ld_dy; op.dx = dx; op.lddx = ld_dx;
+  // the float4 panel takes dh as 8-byte pieces of 4 bf16
+  const bool vec = (uintptr_t)dh % 8 == 0 && ld_dh % 4 == 0 && rw_vec({w_uvqk}, {D}) == 4;
+  return launch_rowpanel_bf16(op, max_rows, true, "hstu_ln_uvqk_bwd", (hipStream_t)stream, vec);
 }
 
 extern "C" int hstu_gate_o_cat_fwd(const float* u, int64_t ld_u, const float* attn, int64_t ld_attn,

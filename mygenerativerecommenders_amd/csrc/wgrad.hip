@@ -43,6 +43,7 @@ struct WgradProb {
   float* slabs;       // [split][Ka][NC]
   float* c;           // reduce outputs
   float* colsum;
+  int a16, b16;       // gr_wgrad_multi_a16: A / B rows are bf16 (the wide bf16 tile only)
 };
 
 // Up to WG_MAXP problems per launch (a layer's two, or every layer's of an encoder at
@@ -426,6 +427,9 @@ constexpr int WGW_T = 256;            // tile edge
 constexpr int WGW_RS = WGW_T + 8;     // LDS row stride (bf16)
 constexpr size_t WGW_LDS = 2 * 2 * 32 * WGW_RS * 2;
 
+// A16 / B16: that operand's rows are bf16 in HBM (gr_wgrad_multi_a16): a thread loads its 4
+// columns as one 8-byte piece and writes the bits to LDS unchanged (A16 has no row stats)
+template <bool A16, bool B16>
 __device__ __forceinline__ void wgrad_tile_bf16w(const WgradProb& g, const int64_t* offsets, int B,
                                                  int64_t rows_per_split, int split, int tile,
                                                  char* smem) {
@@ -437,24 +441,34 @@ __device__ __forceinline__ void wgrad_tile_bf16w(const WgradProb& g, const int64
   const int tid = threadIdx.x, wv = wave_id(), lane = tid & 63;
   const int n_ch = __builtin_amdgcn_readfirstlane(r1 > r0 ? (int)((r1 - r0 + 31) / 32) : 0);
   const int64_t nrows = r1 > r0 ? r1 - r0 : 0;
+  constexpr int EA = A16 ? 2 : 4, EB = B16 ? 2 : 4;  // bytes per element
+  const char* abase = (const char*)g.a + r0 * g.lda * EA;
+  const char* bbase = (const char*)g.bm + r0 * g.ldb * EB;
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(g.a + r0 * g.lda), 0, nrows ? (int)(((nrows - 1) * g.lda + g.Ka) * 4) : 0, 0x00020000);
+      (void*)abase, 0, nrows ? (int)(((nrows - 1) * g.lda + g.Ka) * EA) : 0, 0x00020000);
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(g.bm + r0 * g.ldb), 0, nrows ? (int)(((nrows - 1) * g.ldb + g.Nb) * 4) : 0, 0x00020000);
+      (void*)bbase, 0, nrows ? (int)(((nrows - 1) * g.ldb + g.Nb) * EB) : 0, 0x00020000);
   // staging: thread t owns columns 4 (t % 64) .. +3 of rows t / 64 + 8 i (i < 4)
   const int sc = 4 * (tid & 63), sr = tid >> 6;
   const bool a_ok = sc < g.Ka, b_ok = nb0 + sc < g.Nb;  // Ka, Nb multiples of 4 (host check)
-  const int aoff = a_ok ? sc * 4 : OOB_OFF, boff = b_ok ? (nb0 + sc) * 4 : OOB_OFF;
+  const int aoff = a_ok ? sc * EA : OOB_OFF, boff = b_ok ? (nb0 + sc) * EB : OOB_OFF;
   typedef float f4v __attribute__((ext_vector_type(4)));
-  f4v av[4], bv[4];
+  f4v av[A16 ? 1 : 4], bv[B16 ? 1 : 4];
+  u32x2_t ah[A16 ? 4 : 1], bh[B16 ? 4 : 1];
   float2 stv[4];
   auto load = [&](int ch) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int rr = 32 * ch + sr + 8 * i;
-      av[i] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(ra, aoff + rr * (int)g.lda * 4, 0, 0));
-      bv[i] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rb, boff + rr * (int)g.ldb * 4, 0, 0));
-      stv[i] = g.a_stats ? ld_f2(g.a_stats, min(r0 + rr, total - 1)) : make_float2(0.f, 1.f);
+      if constexpr (A16)
+        ah[i] = __builtin_amdgcn_raw_buffer_load_b64(ra, aoff + rr * (int)g.lda * 2, 0, 0);
+      else
+        av[i] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(ra, aoff + rr * (int)g.lda * 4, 0, 0));
+      if constexpr (B16)
+        bh[i] = __builtin_amdgcn_raw_buffer_load_b64(rb, boff + rr * (int)g.ldb * 2, 0, 0);
+      else
+        bv[i] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rb, boff + rr * (int)g.ldb * 4, 0, 0));
+      if constexpr (!A16) stv[i] = g.a_stats ? ld_f2(g.a_stats, min(r0 + rr, total - 1)) : make_float2(0.f, 1.f);
     }
   };
   const bool do_cs = g.NC > g.Nb && tile == 0;
@@ -466,10 +480,17 @@ __device__ __forceinline__ void wgrad_tile_bf16w(const WgradProb& g, const int64
     for (int i = 0; i < 4; ++i) {
       const int rr = sr + 8 * i;
       const bool ok = r0 + 32 * ch + rr < r1;
-      float x[4];
+      uint32_t p0, p1;
+      if constexpr (A16) {  // rows >= r1 read 0 (descriptor range)
+        p0 = ah[i].x;
+        p1 = ah[i].y;
+      } else {
+        float x[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) x[e] = ok ? (av[i][e] - stv[i].x) * stv[i].y : 0.f;
-      const uint32_t p0 = pack_bf16(x[0], x[1]), p1 = pack_bf16(x[2], x[3]);
+        for (int e = 0; e < 4; ++e) x[e] = ok ? (av[A16 ? 0 : i][e] - stv[i].x) * stv[i].y : 0.f;
+        p0 = pack_bf16(x[0], x[1]);
+        p1 = pack_bf16(x[2], x[3]);
+      }
       if (do_cs) {
         cs[0] += __uint_as_float(p0 << 16);
         cs[1] += __uint_as_float(p0 & 0xffff0000u);
@@ -477,8 +498,12 @@ __device__ __forceinline__ void wgrad_tile_bf16w(const WgradProb& g, const int64
         cs[3] += __uint_as_float(p1 & 0xffff0000u);
       }
       *reinterpret_cast<u32x2_t*>(At + rr * WGW_RS + sc) = u32x2_t{p0, p1};
-      *reinterpret_cast<u32x2_t*>(Bt + rr * WGW_RS + sc) =
-          u32x2_t{pack_bf16(bv[i][0], bv[i][1]), pack_bf16(bv[i][2], bv[i][3])};  // rows past r1 meet a zero A
+      if constexpr (B16)
+        *reinterpret_cast<u32x2_t*>(Bt + rr * WGW_RS + sc) = bh[i];
+      else  // rows past r1 meet a zero A
+        *reinterpret_cast<u32x2_t*>(Bt + rr * WGW_RS + sc) =
+            u32x2_t{pack_bf16(bv[B16 ? 0 : i][0], bv[B16 ? 0 : i][1]),
+                    pack_bf16(bv[B16 ? 0 : i][2], bv[B16 ? 0 : i][3])};
     }
   };
   const int wka = 64 * (wv & 3), wnb = 128 * (wv >> 2);
@@ -670,8 +695,17 @@ __global__ __launch_bounds__(WG_THREADS) void wgrad_partial_wide_kernel(WgradArg
   const int i = wg_find(g.pan0, g.np, tile);
   const WgradProb& p = g.p[i];
   const int t = tile - g.pan0[i];
-  if (BF16) wgrad_tile_bf16w(p, g.offsets, g.B, g.rows_per_split, split, t, smem);
-  else wgrad_tile_f32w(p, g.offsets, g.B, g.rows_per_split, split, t, smem);
+  if (BF16) {
+    if (p.a16) {
+      if (p.b16) wgrad_tile_bf16w<true, true>(p, g.offsets, g.B, g.rows_per_split, split, t, smem);
+      else wgrad_tile_bf16w<true, false>(p, g.offsets, g.B, g.rows_per_split, split, t, smem);
+    } else {
+      if (p.b16) wgrad_tile_bf16w<false, true>(p, g.offsets, g.B, g.rows_per_split, split, t, smem);
+      else wgrad_tile_bf16w<false, false>(p, g.offsets, g.B, g.rows_per_split, split, t, smem);
+    }
+  } else {
+    wgrad_tile_f32w(p, g.offsets, g.B, g.rows_per_split, split, t, smem);
+  }
 }
 
 // out = sum over splits (fixed order): a workgroup owns 16 outputs of one problem; thread
@@ -831,11 +865,16 @@ static bool wgrad_wide_ok(const WgradProb* in, int np) {
     if (!in[i].a) continue;
     const WgradProb& p = in[i];
     if (p.Ka > WGW_T || p.Ka % 4 || p.Nb % 4 || p.lda % 4 || p.ldb % 4 ||
-        (uintptr_t)p.a % 16 || (uintptr_t)p.bm % 16)
+        (uintptr_t)p.a % (p.a16 ? 8 : 16) || (uintptr_t)p.bm % (p.b16 ? 8 : 16))
       return false;
     kmax = std::max(kmax, p.Ka);
   }
   return kmax > 128;
+}
+static bool wgrad_any16(const WgradProb* in, int np) {
+  for (int i = 0; i < np; ++i)
+    if (in[i].a && (in[i].a16 || in[i].b16)) return true;
+  return false;
 }
 static WgPlan wgrad_plan_wide(int64_t max_rows, const int* Ka, const int* Nb, int np) {
   WgPlan pl{};
@@ -879,7 +918,9 @@ static int wgrad_run(const WgradProb* in, int np, const int64_t* offsets, int B,
   // f32 at Ka <= 64, Nb <= 256: the streaming form (GR_OPT_WGRAD_STREAM, default on)
   if (!bf16 && option(GR_OPT_WGRAD_STREAM) != 0 && ws_fits(in, np))
     return wgrad_run_stream(in, np, offsets, B, max_rows, workspace, ws_bytes, st);
-  const bool wide = wgrad_wide_ok(in, np);
+  const bool any16 = wgrad_any16(in, np);
+  // bf16 operands: only the wide bf16 tile reads them (the caller checked its shape rules)
+  const bool wide = any16 || wgrad_wide_ok(in, np);
   const WgPlan pl = wide ? wgrad_plan_wide(max_rows, Ka, Nb, np) : wgrad_plan(max_rows, Ka, Nb, np);
   GR_REQUIRE(pl.ok, "gr_wgrad: the problems need more than two panel widths");
   GR_REQUIRE(workspace && ws_bytes >= pl.need, "gr_wgrad: workspace %zu B < %zu B", ws_bytes, pl.need);
@@ -1377,6 +1418,46 @@ extern "C" size_t gr_wgrad_multi_workspace_size(const int64_t* desc, int n_probl
     Nb[i] = (int)desc[9 * i + 6];
   }
   return wgrad_ws_need(Ka, Nb, n_problems, max_rows);
+}
+
+// desc: 10 int64 per problem, gr_wgrad_multi's 9 plus flags (bit 0: A rows bf16, bit 1: B
+// rows bf16); bf16 MFMA operands, the wide tile (Ka <= 256, 4-aligned widths and strides,
+// bf16 operands 8-byte aligned; A in bf16 takes no row stats).
+extern "C" size_t gr_wgrad_multi_a16_workspace_size(const int64_t* desc, int n_problems, int64_t max_rows) {
+  if (!desc || n_problems < 1 || n_problems > WG_MAXP || max_rows <= 0) return 0;
+  int Ka[WG_MAXP], Nb[WG_MAXP];
+  for (int i = 0; i < n_problems; ++i) {
+    Ka[i] = (int)desc[10 * i + 5];
+    Nb[i] = (int)desc[10 * i + 6];
+    if (Ka[i] > WGW_T) return 0;
+  }
+  return wgrad_plan_wide(max_rows, Ka, Nb, n_problems).need;
+}
+
+extern "C" int gr_wgrad_multi_a16(const int64_t* desc, int n_problems, const int64_t* offsets, int B,
+                                  int64_t max_rows, void* workspace, size_t ws_bytes, void* stream) {
+  GR_REQUIRE(desc && n_problems >= 1 && n_problems <= WG_MAXP, "gr_wgrad_multi_a16: %d problems (1..%d)",
+             n_problems, WG_MAXP);
+  WgradProb p[WG_MAXP] = {};
+  int64_t ld = 0;
+  for (int i = 0; i < n_problems; ++i) {
+    const int64_t* d = desc + 10 * i;
+    p[i] = WgradProb{(const float*)d[0], d[1], (const float2*)d[2], (const float*)d[3], d[4],
+                     (int)d[5], (int)d[6], 0, 0, 0, nullptr, (float*)d[7], (float*)d[8],
+                     (int)(d[9] & 1), (int)((d[9] >> 1) & 1)};
+    const WgradProb& q = p[i];
+    GR_REQUIRE(q.a && q.bm && q.c && q.Ka > 0 && q.Nb > 0,
+               "gr_wgrad_multi_a16: problem %d has a null pointer or an empty shape", i);
+    GR_REQUIRE(!(q.a16 && q.a_stats), "gr_wgrad_multi_a16: problem %d: bf16 A takes no row stats", i);
+    GR_REQUIRE(q.Ka <= WGW_T && q.Ka % 4 == 0 && q.Nb % 4 == 0 && q.lda % 4 == 0 && q.ldb % 4 == 0 &&
+                   (uintptr_t)q.a % (q.a16 ? 8 : 16) == 0 && (uintptr_t)q.bm % (q.b16 ? 8 : 16) == 0,
+               "gr_wgrad_multi_a16: problem %d needs Ka <= 256, 4-aligned widths / strides and aligned rows", i);
+    ld = std::max(ld, std::max(d[1], d[4]));
+  }
+  GR_REQUIRE(offsets && B >= 0 && max_rows >= 0, "gr_wgrad_multi_a16: bad sizes");
+  GR_REQUIRE(max_rows * ld * 4 < 0x7fffffffLL,
+             "gr_wgrad_multi_a16: %lld rows exceed the 32-bit buffer range", (long long)max_rows);
+  return wgrad_run(p, n_problems, offsets, B, max_rows, workspace, ws_bytes, (hipStream_t)stream, true);
 }
 
 extern "C" int gr_wgrad_multi(const int64_t* desc, int n_problems, const int64_t* offsets, int B,

@@ -303,6 +303,31 @@ class STUGeometry:
     def n_out(self):
         return 2 * self.H * self.dv + 2 * self.H * self.dqk
 
+    @property
+    def a16(self) -> bool:
+        """bf16 activations in HBM (ABI 16, the ``*_a16`` entries): bf16 mode at wide
+        heads, dqk == dv = d with d % 32 == 0 in (128, 256] (the ml-20m width)."""
+        d = self.dqk
+        return (A16 and self.bf16 and not self.concat_ua and self.dqk == self.dv
+                and 128 < d <= 256 and d % 32 == 0)
+
+
+# bf16 mode keeps the wide-head layer's activations (uvqk, h_pre, o_in, d_uvqk) in bf16
+# (STUGeometry.a16); False = the fp32-activation bf16 path (A/B switch for tests and
+# measurements)
+A16 = True
+_ZROWS: dict = {}
+
+
+def _zero_row(device) -> torch.Tensor:
+    """256 zero bf16 values (hstu_attn_fwd_a16's row for keys past a sequence)."""
+    key = (device.type, device.index)
+    z = _ZROWS.get(key)
+    if z is None:
+        z = torch.zeros(256, dtype=torch.bfloat16, device=device)
+        _ZROWS[key] = z
+    return z
+
 
 def _cat_wide(hv: int, D: int) -> bool:
     """concat_ua beyond the LDS-resident row-wave form (hdv <= 64, D <= 128): o_in
@@ -343,6 +368,9 @@ def _stu_forward(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGeomet
     w_uvqk = w_uvqk.contiguous()
     w_o = w_o.contiguous()
     sfx = "_bf16" if geo.bf16 else ""  # bf16 MFMA operands in the projections too
+    if geo.a16:
+        return _stu_forward_a16(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo, seed,
+                                seed_offset, grad_on, needs_w_grad)
     if pre is not None:
         x_stats, uvqk, h_pre = pre
     else:
@@ -432,6 +460,108 @@ def _stu_forward(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGeomet
     return y, saved, pre_next
 
 
+def _stu_forward_a16(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGeometry, seed: int,
+                     seed_offset, grad_on: bool, needs_w_grad: bool):
+    """One STU layer forward with bf16 activations (ABI 16): LN + UVQK writes bf16 uvqk /
+    h_pre (and the weight gradient's bf16 LN(x)), the attention DMAs Q / K / V from the
+    bf16 uvqk rows, gate_o reads bf16 u and writes bf16 o_in.  The saved tuple's last
+    slot holds xn (the fp32 path keeps its bf16 copies there)."""
+    dev = x.device
+    rows, D = x.shape
+    B = offsets.numel() - 1
+    H, d = geo.H, geo.dqk
+    hv = H * d
+    n_out = geo.n_out
+    st = _stream()
+    x = x.contiguous()
+    w_uvqk = w_uvqk.contiguous()
+    w_o = w_o.contiguous()
+    needs_w_grad = grad_on and needs_w_grad
+    x_stats = torch.empty(rows, 2, dtype=torch.float32, device=dev)
+    uvqk = torch.empty(rows, n_out, dtype=torch.bfloat16, device=dev)
+    h_pre = torch.empty_like(uvqk) if geo.activation and grad_on else None
+    xn = torch.empty(rows, D, dtype=torch.bfloat16, device=dev) if grad_on else None
+    _lib.call("hstu_ln_uvqk_fwd_a16", x.data_ptr(), x.stride(0), offsets.data_ptr(), B, rows, D,
+              w_uvqk.data_ptr(), n_out, geo.eps, geo.activation, x_stats.data_ptr(),
+              _lib.ptr(h_pre), uvqk.data_ptr(), n_out, _lib.ptr(xn), st)
+    attn = torch.empty(rows, hv, dtype=torch.float32, device=dev)
+    pos_w_c = pos_w.contiguous() if bmap is not None else None
+    ts_w_c = ts_w.contiguous() if bmap is not None else None
+    _lib.call("hstu_attn_fwd_a16", uvqk[:, 2 * hv:].data_ptr(), uvqk[:, 3 * hv:].data_ptr(),
+              uvqk[:, hv:].data_ptr(), n_out, offsets.data_ptr(), B, geo.N, geo.max_len, H, d,
+              _lib.ptr(bmap), _lib.ptr(pos_w_c), _lib.ptr(ts_w_c), NUM_BUCKETS,
+              _zero_row(dev).data_ptr(), attn.data_ptr(), hv, st)
+    attn_stats = torch.empty(rows, 2, dtype=torch.float32, device=dev)
+    o_in = torch.empty(rows, hv, dtype=torch.bfloat16, device=dev) if needs_w_grad else None
+    y = torch.empty(rows, D, dtype=torch.float32, device=dev)
+    b_o_c = b_o.contiguous()
+    _lib.call("hstu_gate_o_fwd_a16", uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
+              offsets.data_ptr(), B, rows, hv, D, w_o.data_ptr(), b_o_c.data_ptr(), x.data_ptr(),
+              x.stride(0), geo.eps, geo.dropout_p, seed, _lib.ptr(seed_offset),
+              attn_stats.data_ptr(), _lib.ptr(o_in), y.data_ptr(), D, st)
+    saved = (x, offsets, bmap, w_uvqk, w_o, pos_w_c, ts_w_c, x_stats, uvqk, h_pre, attn,
+             attn_stats, o_in, xn)
+    return y, saved, None
+
+
+def _stu_backward_a16(saved, dy, geo: STUGeometry, seed: int, seed_offset, want_uvqk: bool,
+                      defer_wgrad: bool):
+    """The backward of ``_stu_forward_a16``: gate_o_bwd writes bf16 du into a bf16 d_uvqk,
+    the attention backward its bf16 dq / dk / dv, ln_uvqk_bwd reads it, and the weight
+    gradients take bf16 LN(x), d_uvqk and o_in (gr_wgrad_multi_a16)."""
+    (x, offsets, bmap, w_uvqk, w_o, pos_w, ts_w, x_stats, uvqk, h_pre, attn, attn_stats,
+     o_in, xn) = saved
+    dev = x.device
+    rows, D = x.shape
+    B = offsets.numel() - 1
+    H, d = geo.H, geo.dqk
+    hv = H * d
+    n_out = geo.n_out
+    st = _stream()
+    dy = dy.contiguous()
+    d_uvqk = torch.empty(rows, n_out, dtype=torch.bfloat16, device=dev)
+    d_attn = torch.empty(rows, hv, dtype=torch.float32, device=dev)
+    _lib.call("hstu_gate_o_bwd_a16", dy.data_ptr(), D, offsets.data_ptr(), B, rows, hv, D,
+              w_o.data_ptr(), uvqk.data_ptr(), n_out, attn.data_ptr(), hv, attn_stats.data_ptr(),
+              _lib.ptr(h_pre), n_out, geo.dropout_p, seed, _lib.ptr(seed_offset),
+              d_uvqk.data_ptr(), n_out, d_attn.data_ptr(), hv, st)
+    L = _lib.lib()
+    d_pos_w = d_ts_w = None
+    if bmap is not None:
+        d_pos_w = torch.empty(2 * geo.N - 1, dtype=torch.float32, device=dev)
+        d_ts_w = torch.empty(NUM_BUCKETS + 1, dtype=torch.float32, device=dev)
+    ws_n = L.hstu_attn_bwd_a16_workspace_size(B, geo.N, geo.max_len, H, d, NUM_BUCKETS)
+    ws = torch.empty(max(ws_n, 4), dtype=torch.uint8, device=dev)
+    hp = (lambda c: h_pre[:, c:].data_ptr()) if h_pre is not None else (lambda c: None)
+    _lib.call("hstu_attn_bwd_a16", uvqk[:, 2 * hv:].data_ptr(), uvqk[:, 3 * hv:].data_ptr(),
+              uvqk[:, hv:].data_ptr(), n_out, d_attn.data_ptr(), hv, offsets.data_ptr(), B, geo.N,
+              geo.max_len, H, d, _lib.ptr(bmap), _lib.ptr(pos_w), _lib.ptr(ts_w), NUM_BUCKETS,
+              hp(2 * hv), hp(3 * hv), hp(hv), n_out, d_uvqk[:, 2 * hv:].data_ptr(),
+              d_uvqk[:, 3 * hv:].data_ptr(), d_uvqk[:, hv:].data_ptr(), n_out,
+              _lib.ptr(d_pos_w), _lib.ptr(d_ts_w), ws.data_ptr(), ws_n, st)
+    dx = torch.empty(rows, D, dtype=torch.float32, device=dev)
+    _lib.call("hstu_ln_uvqk_bwd_a16", d_uvqk.data_ptr(), n_out, offsets.data_ptr(), B, rows, D,
+              n_out, w_uvqk.data_ptr(), x.data_ptr(), x.stride(0), x_stats.data_ptr(),
+              dy.data_ptr(), D, dx.data_ptr(), D, st)
+    d_w_uvqk = torch.empty(D, n_out, dtype=torch.float32, device=dev) if want_uvqk else None
+    d_w_o = d_b_o = None
+    if o_in is not None:
+        d_w_o = torch.empty(D, hv, dtype=torch.float32, device=dev)
+        d_b_o = torch.empty(D, dtype=torch.float32, device=dev)
+    # gr_wgrad_multi_a16 rows {a, lda, a_stats, b, ldb, Ka, Nb, c, colsum, flags}
+    problems = []
+    if want_uvqk:
+        problems.append(((xn.data_ptr(), D, 0, d_uvqk.data_ptr(), n_out, D, n_out,
+                          d_w_uvqk.data_ptr(), 0, 3), (xn, d_uvqk)))
+    if o_in is not None:
+        problems.append(((dy.data_ptr(), D, 0, o_in.data_ptr(), hv, D, hv, d_w_o.data_ptr(),
+                          d_b_o.data_ptr(), 2), (dy, o_in)))
+    if not defer_wgrad:
+        launch_wgrad_multi(problems, offsets, rows, True, a16=True)
+        problems = []
+    return dx, d_w_uvqk, d_w_o, d_b_o, d_pos_w, d_ts_w, problems, None
+
+
 def _ln_uvqk_outputs(rows, n_out, geo: STUGeometry, grad_on: bool, dev):
     """(x_stats, uvqk, h_pre) of one layer's LN + UVQK.  h_pre (pre-activation, for
     silu') exists only for the backward: inference / no_grad forwards skip its write."""
@@ -451,6 +581,8 @@ def _stu_backward(saved, dy, geo: STUGeometry, seed: int, seed_offset, want_uvqk
     layer: this layer's ln_uvqk_bwd and the previous layer's gate_o_bwd run as one
     hstu_boundary_bwd launch, whose (d_uvqk, d_attn) are returned as ``pre_d_prev``.
     Returns (dx, d_w_uvqk, d_w_o, d_b_o, d_pos_w, d_ts_w, problems, pre_d_prev)."""
+    if geo.a16:
+        return _stu_backward_a16(saved, dy, geo, seed, seed_offset, want_uvqk, defer_wgrad)
     (x, offsets, bmap, w_uvqk, w_o, pos_w, ts_w, x_stats, uvqk, h_pre, attn, attn_stats,
      o_in, copies) = saved
     dev = x.device
@@ -656,9 +788,10 @@ def _side_stream(device):
     return s
 
 
-def launch_wgrad_multi(problems, offsets, rows, bf16: bool):
+def launch_wgrad_multi(problems, offsets, rows, bf16: bool, a16: bool = False):
     """Launches the deferred weight-gradient problems (``_stu_backward(defer_wgrad=True)``)
-    through gr_wgrad_multi, up to 16 per launch."""
+    through gr_wgrad_multi (gr_wgrad_multi_a16 for the bf16-activation layout's 10-word
+    rows), up to 16 per launch."""
     import numpy as np
     if not problems:
         return
@@ -669,6 +802,12 @@ def launch_wgrad_multi(problems, offsets, rows, bf16: bool):
         chunk = problems[c0:c0 + 16]
         desc = np.ascontiguousarray(np.array([p[0] for p in chunk], dtype=np.int64))
         n = len(chunk)
+        if a16:
+            ws_n = int(L.gr_wgrad_multi_a16_workspace_size(desc.ctypes.data, n, rows))
+            ws = torch.empty(max(ws_n, 4), dtype=torch.uint8, device=dev)
+            _lib.call("gr_wgrad_multi_a16", desc.ctypes.data, n, offsets.data_ptr(), B, rows,
+                      ws.data_ptr(), ws_n, _stream())
+            continue
         ws_n = int(L.gr_wgrad_multi_workspace_size(desc.ctypes.data, n, rows))
         ws = torch.empty(max(ws_n, 4), dtype=torch.uint8, device=dev)
         _lib.call("gr_wgrad_multi", desc.ctypes.data, n, offsets.data_ptr(), B, rows,
@@ -732,14 +871,14 @@ class STUStackFunction(torch.autograd.Function):
             if side is not None and l > 0 and probs:
                 side.wait_stream(main)  # this layer's operands are enqueued on main
                 with torch.cuda.stream(side):
-                    launch_wgrad_multi(probs, offsets, rows, geo.bf16)
+                    launch_wgrad_multi(probs, offsets, rows, geo.bf16, geo.a16)
                 for _, keep in probs:  # no reuse of their memory before the side stream ran
                     for t in keep:
                         t.record_stream(side)
             else:
                 problems.extend(probs)
             dy = dx
-        launch_wgrad_multi(problems, offsets, rows, geo.bf16)
+        launch_wgrad_multi(problems, offsets, rows, geo.bf16, geo.a16)
         if side is not None:
             main.wait_stream(side)
         return (dy, None, None, None, None, None, None, *grads)

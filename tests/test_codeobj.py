@@ -71,7 +71,7 @@ SCRATCH_OK = {
     # row-wave gate_o at D = 256 with hdv = 64 (C3 widths take the row panel)
     "rowwave_kernelILi16ELi4ENS_7RwGateOILi16ELi4ELi2EEEEEvT1_": 108,
     # f32 ln_uvqk backward row panel at 8 column groups (a local array indexed per row)
-    "rowpanel_kernelILi8ELi64ENS_11OpLnUvqkBwdEEEvT1_": 20,
+    "rowpanel_kernelILi8ELi64ENS_*OpLnUvqkBwd": 20,
     # top-k merges: a small per-lane array indexed dynamically
     "_ZN2gr17mips_merge_kernelENS_9MergeArgsE": 16,
     "_ZN2gr24mips_filter_merge_kernelENS_15FilterMergeArgsE": 16,
@@ -83,7 +83,7 @@ SCRATCH_OK = {
 
 def _allowed(name):
     for k, v in SCRATCH_OK.items():
-        if k in name:
+        if all(part in name for part in k.split("*")):
             return v
     return 0
 
