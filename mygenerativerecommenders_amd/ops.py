@@ -309,7 +309,7 @@ class STUGeometry:
         heads, dqk == dv = d with d % 32 == 0 in (128, 256] (the ml-20m width)."""
         d = self.dqk
         return (A16 and self.bf16 and not self.concat_ua and self.dqk == self.dv
-                and 128 < d <= 256 and d % 32 == 0)
+                and 128 < d <= 256 and d % 32 == 0 and self.H * d <= 256)
 
 
 # bf16 mode keeps the wide-head layer's activations (uvqk, h_pre, o_in, d_uvqk) in bf16

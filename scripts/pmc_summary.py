@@ -61,7 +61,8 @@ _MAP = [
     (r"mips_filter_kernel<[^>]*true>", "mips_sample"),
     (r"mips_filter_kernel<[^>]*false>", "mips_filter"),
     (r"mips_tau_kernel", "mips_tau"),
-    (r"mips_merge_kernel", "mips_merge"),
+    # the exact path's merge: gated on the filter path's flag (C4), timed as mips_merge_fallback
+    (r"mips_merge_kernel", "mips_merge_fallback"),
     (r"cumsum_kernel", "cumsum"),
     (r"dense_to_jagged_kernel", "dense_to_jagged"),
     (r"jagged_to_padded_kernel", "jagged_to_padded"),

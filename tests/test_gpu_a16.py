@@ -145,7 +145,7 @@ def test_attn_a16_bitexact(d, H, lengths, N):
     _eq(dt, dt32, "d ts_w")
 
 
-@pytest.mark.parametrize("D,hv", [(256, 256), (192, 384)])
+@pytest.mark.parametrize("D,hv", [(256, 256), (192, 192), (256, 160)])
 def test_gate_o_a16_bitexact(D, hv):
     offs, total = _offsets([700, 1, 333, 2048])
     cap = total + 9
@@ -261,7 +261,7 @@ def test_wgrad_multi_a16_bitexact():
     assert err <= 1e-5 * (1 + ref.abs().max().item())
 
 
-@pytest.mark.parametrize("shape", ["c3", "d192h2"])
+@pytest.mark.parametrize("shape", ["c3", "d192"])
 def test_hstu_a16_vs_fp32_activation_bf16_mode(shape):
     """The whole encoder in bf16 mode with bf16 activations against the fp32-activation bf16
     path (ops.A16 = False): both round the MFMA operands to bf16; a16 also rounds uvqk,
@@ -272,7 +272,7 @@ def test_hstu_a16_vs_fp32_activation_bf16_mode(shape):
     if shape == "c3":
         D, H, d, blocks, lengths = 256, 1, 256, 2, [300, 1, 517, 64]
     else:
-        D, H, d, blocks, lengths = 192, 2, 192, 2, [129, 250, 7]
+        D, H, d, blocks, lengths = 192, 1, 192, 2, [129, 250, 7]
     N0, out_len = max(lengths) + 3, 0
     N = N0 + out_len
     B = len(lengths)
