@@ -804,7 +804,11 @@ struct OpGateOBwdT : NoStats {
   template <int NT>
   __device__ void epi_load(Epi<NT>&, int64_t, int, int64_t) const {}
   template <int NT>
-  __device__ void epilogue(f4 (&acc)[NT], const Epi<NT>&, int64_t mrow, int ncol, int64_t total) const {
+  __device__ void epilogue(f4 (&acc)[NT], const Epi<NT>& es, int64_t mrow, int ncol, int64_t total) const {
+    if constexpr (A16) {
+      epilogue16(acc, mrow, ncol, total);
+      return;
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int64_t m = mrow + r;
@@ -835,6 +839,81 @@ struct OpGateOBwdT : NoStats {
         dln[t] = ok ? g * uv[t] : 0.f;
         s1 += dln[t];
         s2 += dln[t] * lnv[t];
+      }
+      s1 = sum16(s1);
+      s2 = sum16(s2);
+      const float inv = 1.f / (float)N;
+      const float mean1 = s1 * inv, mean2 = s2 * inv;
+      if (!row_ok) continue;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int n = ncol + 16 * t;
+        if (n < N) da[m * ldda + n] = st.y * (dln[t] - mean1 - lnv[t] * mean2);
+      }
+    }
+  }
+  // bf16 layout: u / h_u read as the 4-byte bf16 pair holding the lane's column (a lane
+  // pair reads the same word), du written as packed pairs: rows r - 1, r (r odd) are
+  // stored together, the even lane taking row r - 1 and the odd lane row r (one DPP swap
+  // per column tile).  Same values as the fp32 layout, rounded to bf16.
+  template <int NT>
+  __device__ void epilogue16(f4 (&acc)[NT], int64_t mrow, int ncol, int64_t total) const {
+    const bool odd = (threadIdx.x & 1) != 0;
+    const int cb = ncol - (odd ? 1 : 0);
+    const uint32_t* u32 = reinterpret_cast<const uint32_t*>(u);
+    const uint32_t* h32 = reinterpret_cast<const uint32_t*>(h_u);
+    float keep[NT];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t m = mrow + r;
+      const bool row_ok = m < total;
+      const int64_t mc = clamp_row(m, total);
+      const float2 st = ld_f2(a_stats, mc);
+      float av[NT], uv[NT], hv[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int n = ncol + 16 * t;
+        const int nc = n < N ? n : N - 1;
+        const int pc = (n < N ? cb + 16 * t : N - 2) >> 1;  // the pair's word (N even)
+        av[t] = as_global(attn)[mc * lda + nc];
+        const uint32_t wu = as_global(u32)[(mc * ldu >> 1) + pc];
+        uv[t] = __uint_as_float(odd ? wu & 0xffff0000u : wu << 16);
+        if (h_u) {
+          const uint32_t wh = as_global(h32)[(mc * ldh >> 1) + pc];
+          hv[t] = __uint_as_float(odd ? wh & 0xffff0000u : wh << 16);
+        } else {
+          hv[t] = 0.f;
+        }
+      }
+      float s1 = 0.f, s2 = 0.f;
+      float lnv[NT], dln[NT], ddv[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int n = ncol + 16 * t;
+        const bool ok = row_ok && n < N;
+        const float g = p > 0.f ? acc[t][r] * dropout_keep(seed + (seed_off ? (uint64_t)*seed_off : 0ull), m, n, N, p) : acc[t][r];
+        const float ln = (av[t] - st.x) * st.y;
+        float dd = g * ln;
+        if (h_u) dd *= silu_grad_(hv[t]);
+        ddv[t] = dd;
+        lnv[t] = ok ? ln : 0.f;
+        dln[t] = ok ? g * uv[t] : 0.f;
+        s1 += dln[t];
+        s2 += dln[t] * lnv[t];
+      }
+      if (r & 1) {  // rows r - 1 (even lane) and r (odd lane) as packed pairs
+        const int64_t ms = odd ? m : m - 1;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const float rx = dpp_mov<0xB1>(odd ? keep[t] : ddv[t]);
+          const float lo = odd ? rx : keep[t], hi = odd ? ddv[t] : rx;
+          const int n = cb + 16 * t;
+          if (ms < total && n < N)
+            *reinterpret_cast<uint32_t*>(du + ms * lddu + n) = pack_bf16(lo, hi);
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) keep[t] = ddv[t];
       }
       s1 = sum16(s1);
       s2 = sum16(s2);
@@ -1202,6 +1281,7 @@ static bool rw_enabled() { return option(GR_OPT_ROWWAVE) != 0; }
 
 }  // namespace gr
 
+#ifndef GR_LINEAR_LIB_ONLY  // hstu_linear_a16.hip takes the kernels above, not the entries
 // ====================================================================== C-ABI
 using namespace gr;
 
@@ -1365,74 +1445,6 @@ extern "C" int hstu_ln_uvqk_bwd_bf16(const float* dh, int64_t ld_dh, const int64
                                 const float* dy_res, int64_t ld_dy, float* dx, int64_t ld_dx,
                                 void* stream) {
   return hstu_ln_uvqk_bwd_impl(true, dh, ld_dh, offsets, B, max_rows, D, n_out, w_uvqk, x, ld_x, x_stats, dy_res, ld_dy, dx, ld_dx, stream);
-}
-
-// ---------------------------------------------------------------- bf16 activations (ABI 16)
-// autocast_dtype = bfloat16 at wide heads: uvqk / h_pre / o_in / d_uvqk in bf16 (see the
-// Op templates).  Same bf16 row panels; results equal the *_bf16 entries' on the same
-// (bf16-rounded) inputs, rounded to bf16 where the output is bf16.
-extern "C" int hstu_ln_uvqk_fwd_a16(const float* x, int64_t ld_x, const int64_t* offsets, int B,
-                                    int64_t max_rows, int D, const float* w_uvqk, int n_out,
-                                    float eps, int activation, float* x_stats, uint16_t* h_pre,
-                                    uint16_t* uvqk, int64_t ld_out, uint16_t* xn, void* stream) {
-  GR_REQUIRE(x && offsets && w_uvqk && uvqk && x_stats, "hstu_ln_uvqk_fwd_a16: null pointer");
-  GR_REQUIRE(D > 0 && n_out > 0 && B >= 0 && max_rows >= 0, "hstu_ln_uvqk_fwd_a16: bad sizes");
-  GR_REQUIRE(activation == 0 || activation == 1, "hstu_ln_uvqk_fwd_a16: activation must be 0|1");
-  GR_REQUIRE(n_out % 2 == 0 && ld_out % 2 == 0 && (uintptr_t)uvqk % 4 == 0 && (uintptr_t)h_pre % 4 == 0,
-             "hstu_ln_uvqk_fwd_a16: n_out and ld_out must be even, outputs 4-byte aligned");
-  OpLnUvqkT<true> op{offsets, B, D, n_out, x, ld_x, w_uvqk, eps, activation, (float2*)x_stats,
-                     (__bf16*)h_pre, (__bf16*)uvqk, ld_out, (__bf16*)xn};
-  return launch_rowpanel_bf16(op, max_rows, false, "hstu_ln_uvqk_fwd", (hipStream_t)stream);
-}
-
-extern "C" int hstu_gate_o_fwd_a16(const uint16_t* u, int64_t ld_u, const float* attn, int64_t ld_attn,
-                                   const int64_t* offsets, int B, int64_t max_rows, int hdv, int D,
-                                   const float* w_o, const float* b_o, const float* x_res,
-                                   int64_t ld_x, float eps, float dropout_p, uint64_t seed,
-                                   const int64_t* seed_offset, float* attn_stats, uint16_t* o_in,
-                                   float* y, int64_t ld_y, void* stream) {
-  GR_REQUIRE(u && attn && offsets && w_o && y && attn_stats, "hstu_gate_o_fwd_a16: null pointer");
-  GR_REQUIRE(hdv > 0 && D > 0 && B >= 0, "hstu_gate_o_fwd_a16: bad sizes");
-  GR_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f, "hstu_gate_o_fwd_a16: dropout_p %f", dropout_p);
-  OpGateOT<true> op{offsets, B, hdv, D, (const __bf16*)u, ld_u, attn, ld_attn, w_o, b_o, x_res, ld_x,
-                    eps, dropout_p, seed, seed_offset, (float2*)attn_stats, (__bf16*)o_in, y, ld_y};
-  return launch_rowpanel_bf16(op, max_rows, false, "hstu_gate_o_fwd", (hipStream_t)stream);
-}
-
-extern "C" int hstu_gate_o_bwd_a16(const float* dy, int64_t ld_dy, const int64_t* offsets, int B,
-                                   int64_t max_rows, int hdv, int D, const float* w_o,
-                                   const uint16_t* u, int64_t ld_u, const float* attn, int64_t ld_attn,
-                                   const float* attn_stats, const uint16_t* h_u, int64_t ld_h,
-                                   float dropout_p, uint64_t seed, const int64_t* seed_offset,
-                                   uint16_t* du, int64_t ld_du, float* d_attn, int64_t ld_da,
-                                   void* stream) {
-  GR_REQUIRE(dy && offsets && w_o && u && attn && attn_stats && du && d_attn,
-             "hstu_gate_o_bwd_a16: null pointer");
-  GR_REQUIRE(hdv > 0 && D > 0 && B >= 0, "hstu_gate_o_bwd_a16: bad sizes");
-  OpGateOBwdT<true> op;
-  op.offsets = offsets; op.B = B; op.K = D; op.N = hdv; op.dy = dy; op.lddy = ld_dy;
-  op.w = w_o; op.u = (const __bf16*)u; op.ldu = ld_u; op.attn = attn; op.lda = ld_attn;
-  op.a_stats = (const float2*)attn_stats; op.h_u = (const __bf16*)h_u; op.ldh = ld_h;
-  op.p = dropout_p; op.seed = seed; op.seed_off = seed_offset; op.du = (__bf16*)du; op.lddu = ld_du;
-  op.da = d_attn; op.ldda = ld_da;
-  return launch_rowpanel_bf16(op, max_rows, true, "hstu_gate_o_bwd", (hipStream_t)stream,
-                              rw_vec({dy, w_o}, {ld_dy, hdv}) == 4);
-}
-
-extern "C" int hstu_ln_uvqk_bwd_a16(const uint16_t* dh, int64_t ld_dh, const int64_t* offsets, int B,
-                                    int64_t max_rows, int D, int n_out, const float* w_uvqk,
-                                    const float* x, int64_t ld_x, const float* x_stats,
-                                    const float* dy_res, int64_t ld_dy, float* dx, int64_t ld_dx,
-                                    void* stream) {
-  GR_REQUIRE(dh && offsets && w_uvqk && x && x_stats && dx, "hstu_ln_uvqk_bwd_a16: null pointer");
-  GR_REQUIRE(D > 0 && n_out > 0 && B >= 0, "hstu_ln_uvqk_bwd_a16: bad sizes");
-  OpLnUvqkBwdT<true> op;
-  op.offsets = offsets; op.B = B; op.K = n_out; op.N = D; op.dh = (const __bf16*)dh; op.lddh = ld_dh;
-  op.w = w_uvqk; op.x = x; op.ldx = ld_x; op.x_stats = (const float2*)x_stats;
-  op.dy = dy_res; op.lddy = ld_dy; op.dx = dx; op.lddx = ld_dx;
-  // the float4 panel takes dh as 8-byte pieces of 4 bf16
-  const bool vec = (uintptr_t)dh % 8 == 0 && ld_dh % 4 == 0 && rw_vec({w_uvqk}, {D}) == 4;
-  return launch_rowpanel_bf16(op, max_rows, true, "hstu_ln_uvqk_bwd", (hipStream_t)stream, vec);
 }
 
 extern "C" int hstu_gate_o_cat_fwd(const float* u, int64_t ld_u, const float* attn, int64_t ld_attn,
@@ -1859,3 +1871,5 @@ extern "C" int hstu_boundary_bwd(const float* dh, int64_t ld_dh, const int64_t* 
                          attn_stats, h_u, ld_h, dropout_p, seed, seed_offset, du, ld_du, d_attn,
                          ld_da, stream);
 }
+
+#endif  // GR_LINEAR_LIB_ONLY
