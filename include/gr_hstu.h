@@ -662,7 +662,11 @@ GR_API int gr_wgrad_multi(const int64_t* desc, int n_problems, const int64_t* of
  *
  * hstu_ln_uvqk_fwd_a16: hstu_ln_uvqk_fwd with bf16 h_pre (optional) and uvqk (n_out,
  *   ld_out even), plus optional xn (rows, D) = bf16 LN(x), the weight gradient's A operand
- *   (replaces hstu.py:258-305 under autocast).
+ *   (replaces hstu.py:258-305 under autocast).  stats_given = 1: x_stats already holds the
+ *   rows' LayerNorm (mean, rstd) -- the previous layer's hstu_gate_o_fwd_a16 y_stats --
+ *   and the statistics pass over x is skipped (the same values: same sums, same order).
+ * hstu_gate_o_fwd_a16: y_stats (optional, 240 < D <= 256): the LayerNorm statistics of
+ *   each y row with `eps`, i.e. the next layer's x_stats.
  * hstu_attn_fwd_a16: hstu_attn_fwd_bf16 on bf16 q / k / v rows (16-byte aligned, ld_qkv a
  *   multiple of 8); zrow = d zero bf16 values (caller-owned, 16-byte aligned).
  * hstu_gate_o_fwd_a16 / _bwd_a16: u, h_u, o_in and du in bf16 (hstu.py:393-413).
@@ -675,8 +679,8 @@ GR_API int gr_wgrad_multi(const int64_t* desc, int n_problems, const int64_t* of
  *   ldb multiples of 4, bf16 rows 8-byte aligned, a bf16 A takes no row stats. */
 GR_API int hstu_ln_uvqk_fwd_a16(const float* x, int64_t ld_x, const int64_t* offsets, int B,
                     int64_t max_rows, int D, const float* w_uvqk, int n_out, float eps,
-                    int activation, float* x_stats, uint16_t* h_pre, uint16_t* uvqk,
-                    int64_t ld_out, uint16_t* xn, void* stream);
+                    int activation, float* x_stats, int stats_given, uint16_t* h_pre,
+                    uint16_t* uvqk, int64_t ld_out, uint16_t* xn, void* stream);
 GR_API int hstu_attn_fwd_a16(const uint16_t* q, const uint16_t* k, const uint16_t* v,
                     int64_t ld_qkv, const int64_t* offsets, int B, int N, int max_len, int H,
                     int d, const uint8_t* bucket_map, const float* pos_w, const float* ts_w,
@@ -686,7 +690,8 @@ GR_API int hstu_gate_o_fwd_a16(const uint16_t* u, int64_t ld_u, const float* att
                     const int64_t* offsets, int B, int64_t max_rows, int hdv, int D,
                     const float* w_o, const float* b_o, const float* x_res, int64_t ld_x,
                     float eps, float dropout_p, uint64_t seed, const int64_t* seed_offset,
-                    float* attn_stats, uint16_t* o_in, float* y, int64_t ld_y, void* stream);
+                    float* attn_stats, uint16_t* o_in, float* y, int64_t ld_y, float* y_stats,
+                    void* stream);
 GR_API int hstu_gate_o_bwd_a16(const float* dy, int64_t ld_dy, const int64_t* offsets, int B,
                     int64_t max_rows, int hdv, int D, const float* w_o, const uint16_t* u,
                     int64_t ld_u, const float* attn, int64_t ld_attn, const float* attn_stats,

@@ -620,7 +620,13 @@ struct OpLnUvqkT {
   act_t<A16>* out;
   int64_t ld_out;
   __bf16* xn;  // A16: optional bf16 LN(x) rows (ld K), the weight gradient's A operand
+  int stats_given;  // A16: x_stats already holds the rows' (mean, rstd) (the previous
+                    // layer's gate_o epilogue computed them): no statistics pass
   __device__ void prologue(int64_t m0, int64_t total, float2* st) const {
+    if (A16 && stats_given) {
+      if (threadIdx.x < BM) st[threadIdx.x] = ld_f2(x_stats, clamp_row(m0 + threadIdx.x, total));
+      return;
+    }
     panel_row_stats(x, ldx, m0, total, K, eps, st, blockIdx.y == 0 ? x_stats : nullptr);
   }
   static constexpr int NSRC = 1;
@@ -712,6 +718,8 @@ struct OpGateOT {
   act_t<A16>* o_in;
   float* y;
   int64_t ldy;
+  float2* y_stats;  // A16, N <= 256 (one panel): the LayerNorm (mean, rstd) of each y row
+                    // with eps -- the next layer's x_stats, in panel_row_stats's order
   __device__ void prologue(int64_t m0, int64_t total, float2* st) const {
     panel_row_stats(attn, lda, m0, total, K, eps, st, blockIdx.y == 0 ? a_stats : nullptr);
   }
@@ -740,6 +748,12 @@ struct OpGateOT {
       const int n = ncol + 16 * t;
       bv[t] = bias ? as_global(bias)[n < N ? n : N - 1] : 0.f;
     }
+    if constexpr (A16 && NT == 16) {  // y_stats: the host requires the one-panel width
+      if (y_stats) {
+        epilogue_stats(acc, mrow, ncol, total);
+        return;
+      }
+    }
     // every residual load issued before the first store (y may alias xres for hipcc,
     // which otherwise waits for each row's loads after the previous row's stores)
     float xv[4][NT];
@@ -760,6 +774,63 @@ struct OpGateOT {
       for (int t = 0; t < NT; ++t) {
         const int n = ncol + 16 * t;
         if (n < N) y[m * ldy + n] = (acc[t][r] + bv[t]) + xv[r][t];
+      }
+    }
+  }
+  // y rows plus their LayerNorm statistics: a lane holds column 16 t + lr of its rows, the
+  // layout panel_row_stats reduces (value j = column 16 j + sub), so the same sums in the
+  // same order give the statistics the next layer's LN + UVQK would compute from y
+  template <int NT>
+  __device__ void epilogue_stats(f4 (&acc)[NT], int64_t mrow, int ncol, int64_t total) const {
+    float bv[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int n = ncol + 16 * t;
+      bv[t] = bias ? as_global(bias)[n < N ? n : N - 1] : 0.f;
+    }
+    float xv[4][NT];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t mc = clamp_row(mrow + r, total);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int n = ncol + 16 * t;
+        xv[r][t] = xres ? as_global(xres)[mc * ldx + (n < N ? n : N - 1)] : 0.f;
+      }
+    }
+    const float invk = 1.f / (float)N;
+    const int sub = ncol & 15;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t m = mrow + r;
+      float v[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) v[t] = 16 * t + sub < N ? (acc[t][r] + bv[t]) + xv[r][t] : 0.f;
+      float s = 0.f;
+#pragma unroll
+      for (int it = 0; it < 4; ++it) s += (v[4 * it] + v[4 * it + 1]) + (v[4 * it + 2] + v[4 * it + 3]);
+      s = sum16(s);
+      const float mean = s * invk;
+      float q = 0.f;
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        float d[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int j = 4 * it + u;
+          d[u] = 16 * j + sub < N ? v[j] - mean : 0.f;
+        }
+        q += (d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]);
+      }
+      q = sum16(q);
+      const float rstd = rsqrtf(q * invk + eps);
+      if (m < total) {
+        if (sub == 0) y_stats[m] = make_float2(mean, rstd);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const int n = ncol + 16 * t;
+          if (n < N) y[m * ldy + n] = v[t];
+        }
       }
     }
   }
@@ -860,8 +931,14 @@ struct OpGateOBwdT : NoStats {
   __device__ void epilogue16(f4 (&acc)[NT], int64_t mrow, int ncol, int64_t total) const {
     const bool odd = (threadIdx.x & 1) != 0;
     const int cb = ncol - (odd ? 1 : 0);
-    const uint32_t* u32 = reinterpret_cast<const uint32_t*>(u);
-    const uint32_t* h32 = reinterpret_cast<const uint32_t*>(h_u);
+    // restrict-qualified views: the du / d_attn stores of one row do not order the next
+    // row's loads (same-typed stores otherwise made hipcc wait vmcnt(0) between rows)
+    const uint32_t* __restrict__ u32 = reinterpret_cast<const uint32_t*>(u);
+    const uint32_t* __restrict__ h32 = reinterpret_cast<const uint32_t*>(h_u);
+    const float* __restrict__ ap = attn;
+    uint32_t* __restrict__ du32 = reinterpret_cast<uint32_t*>(du);
+    float* __restrict__ dap = da;
+    const uint64_t sd = seed + (seed_off ? (uint64_t)*seed_off : 0ull);
     float keep[NT];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -875,7 +952,7 @@ struct OpGateOBwdT : NoStats {
         const int n = ncol + 16 * t;
         const int nc = n < N ? n : N - 1;
         const int pc = (n < N ? cb + 16 * t : N - 2) >> 1;  // the pair's word (N even)
-        av[t] = as_global(attn)[mc * lda + nc];
+        av[t] = as_global(ap)[mc * lda + nc];
         const uint32_t wu = as_global(u32)[(mc * ldu >> 1) + pc];
         uv[t] = __uint_as_float(odd ? wu & 0xffff0000u : wu << 16);
         if (h_u) {
@@ -891,7 +968,7 @@ struct OpGateOBwdT : NoStats {
       for (int t = 0; t < NT; ++t) {
         const int n = ncol + 16 * t;
         const bool ok = row_ok && n < N;
-        const float g = p > 0.f ? acc[t][r] * dropout_keep(seed + (seed_off ? (uint64_t)*seed_off : 0ull), m, n, N, p) : acc[t][r];
+        const float g = p > 0.f ? acc[t][r] * dropout_keep(sd, m, n, N, p) : acc[t][r];
         const float ln = (av[t] - st.x) * st.y;
         float dd = g * ln;
         if (h_u) dd *= silu_grad_(hv[t]);
@@ -908,8 +985,7 @@ struct OpGateOBwdT : NoStats {
           const float rx = dpp_mov<0xB1>(odd ? keep[t] : ddv[t]);
           const float lo = odd ? rx : keep[t], hi = odd ? ddv[t] : rx;
           const int n = cb + 16 * t;
-          if (ms < total && n < N)
-            *reinterpret_cast<uint32_t*>(du + ms * lddu + n) = pack_bf16(lo, hi);
+          if (ms < total && n < N) du32[(ms * lddu + n) >> 1] = pack_bf16(lo, hi);
         }
       } else {
 #pragma unroll
@@ -923,7 +999,7 @@ struct OpGateOBwdT : NoStats {
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         const int n = ncol + 16 * t;
-        if (n < N) da[m * ldda + n] = st.y * (dln[t] - mean1 - lnv[t] * mean2);
+        if (n < N) dap[m * ldda + n] = st.y * (dln[t] - mean1 - lnv[t] * mean2);
       }
     }
   }

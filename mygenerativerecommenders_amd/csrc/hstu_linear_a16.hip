@@ -12,15 +12,16 @@ using namespace gr;
 // (bf16-rounded) inputs, rounded to bf16 where the output is bf16.
 extern "C" int hstu_ln_uvqk_fwd_a16(const float* x, int64_t ld_x, const int64_t* offsets, int B,
                                     int64_t max_rows, int D, const float* w_uvqk, int n_out,
-                                    float eps, int activation, float* x_stats, uint16_t* h_pre,
-                                    uint16_t* uvqk, int64_t ld_out, uint16_t* xn, void* stream) {
+                                    float eps, int activation, float* x_stats, int stats_given,
+                                    uint16_t* h_pre, uint16_t* uvqk, int64_t ld_out, uint16_t* xn,
+                                    void* stream) {
   GR_REQUIRE(x && offsets && w_uvqk && uvqk && x_stats, "hstu_ln_uvqk_fwd_a16: null pointer");
   GR_REQUIRE(D > 0 && n_out > 0 && B >= 0 && max_rows >= 0, "hstu_ln_uvqk_fwd_a16: bad sizes");
   GR_REQUIRE(activation == 0 || activation == 1, "hstu_ln_uvqk_fwd_a16: activation must be 0|1");
   GR_REQUIRE(n_out % 2 == 0 && ld_out % 2 == 0 && (uintptr_t)uvqk % 4 == 0 && (uintptr_t)h_pre % 4 == 0,
              "hstu_ln_uvqk_fwd_a16: n_out and ld_out must be even, outputs 4-byte aligned");
   OpLnUvqkT<true> op{offsets, B, D, n_out, x, ld_x, w_uvqk, eps, activation, (float2*)x_stats,
-                     (__bf16*)h_pre, (__bf16*)uvqk, ld_out, (__bf16*)xn};
+                     (__bf16*)h_pre, (__bf16*)uvqk, ld_out, (__bf16*)xn, stats_given != 0};
   return launch_rowpanel_bf16(op, max_rows, false, "hstu_ln_uvqk_fwd", (hipStream_t)stream);
 }
 
@@ -29,12 +30,17 @@ extern "C" int hstu_gate_o_fwd_a16(const uint16_t* u, int64_t ld_u, const float*
                                    const float* w_o, const float* b_o, const float* x_res,
                                    int64_t ld_x, float eps, float dropout_p, uint64_t seed,
                                    const int64_t* seed_offset, float* attn_stats, uint16_t* o_in,
-                                   float* y, int64_t ld_y, void* stream) {
+                                   float* y, int64_t ld_y, float* y_stats, void* stream) {
   GR_REQUIRE(u && attn && offsets && w_o && y && attn_stats, "hstu_gate_o_fwd_a16: null pointer");
+  GR_REQUIRE(!y_stats || D <= 256, "hstu_gate_o_fwd_a16: y_stats needs D <= 256 (one panel), D %d", D);
   GR_REQUIRE(hdv > 0 && D > 0 && B >= 0, "hstu_gate_o_fwd_a16: bad sizes");
   GR_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f, "hstu_gate_o_fwd_a16: dropout_p %f", dropout_p);
   OpGateOT<true> op{offsets, B, hdv, D, (const __bf16*)u, ld_u, attn, ld_attn, w_o, b_o, x_res, ld_x,
-                    eps, dropout_p, seed, seed_offset, (float2*)attn_stats, (__bf16*)o_in, y, ld_y};
+                    eps, dropout_p, seed, seed_offset, (float2*)attn_stats, (__bf16*)o_in, y, ld_y,
+                    (float2*)y_stats};
+  // y_stats: the whole row in one 256-column panel (launch_rowpanel_bf16 picks NT = 16 only
+  // when D > 240; narrower D takes the general epilogue, which cannot reduce a row)
+  GR_REQUIRE(!y_stats || D > 240, "hstu_gate_o_fwd_a16: y_stats needs 240 < D <= 256, D %d", D);
   return launch_rowpanel_bf16(op, max_rows, false, "hstu_gate_o_fwd", (hipStream_t)stream);
 }
 

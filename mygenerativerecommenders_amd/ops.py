@@ -316,6 +316,9 @@ class STUGeometry:
 # (STUGeometry.a16); False = the fp32-activation bf16 path (A/B switch for tests and
 # measurements)
 A16 = True
+# a16: each layer's gate_o epilogue computes the next layer's LayerNorm statistics
+# (identical values), so LN + UVQK skips its statistics pass over x (A/B switch)
+STATS_IN_EPILOGUE = True
 _ZROWS: dict = {}
 
 
@@ -370,7 +373,7 @@ def _stu_forward(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGeomet
     sfx = "_bf16" if geo.bf16 else ""  # bf16 MFMA operands in the projections too
     if geo.a16:
         return _stu_forward_a16(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo, seed,
-                                seed_offset, grad_on, needs_w_grad)
+                                seed_offset, grad_on, needs_w_grad, pre, next_w_uvqk is not None)
     if pre is not None:
         x_stats, uvqk, h_pre = pre
     else:
@@ -461,11 +464,14 @@ def _stu_forward(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGeomet
 
 
 def _stu_forward_a16(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGeometry, seed: int,
-                     seed_offset, grad_on: bool, needs_w_grad: bool):
+                     seed_offset, grad_on: bool, needs_w_grad: bool, pre=None, has_next=False):
     """One STU layer forward with bf16 activations (ABI 16): LN + UVQK writes bf16 uvqk /
     h_pre (and the weight gradient's bf16 LN(x)), the attention DMAs Q / K / V from the
     bf16 uvqk rows, gate_o reads bf16 u and writes bf16 o_in.  The saved tuple's last
-    slot holds xn (the fp32 path keeps its bf16 copies there)."""
+    slot holds xn (the fp32 path keeps its bf16 copies there).
+    ``pre``: this layer's x_stats, computed by the previous layer's gate_o epilogue (the
+    LN statistics pass is skipped); ``has_next``: compute the next layer's x_stats in this
+    layer's gate_o epilogue (returned as the third value)."""
     dev = x.device
     rows, D = x.shape
     B = offsets.numel() - 1
@@ -477,13 +483,14 @@ def _stu_forward_a16(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGe
     w_uvqk = w_uvqk.contiguous()
     w_o = w_o.contiguous()
     needs_w_grad = grad_on and needs_w_grad
-    x_stats = torch.empty(rows, 2, dtype=torch.float32, device=dev)
+    stats_given = pre is not None
+    x_stats = pre if stats_given else torch.empty(rows, 2, dtype=torch.float32, device=dev)
     uvqk = torch.empty(rows, n_out, dtype=torch.bfloat16, device=dev)
     h_pre = torch.empty_like(uvqk) if geo.activation and grad_on else None
     xn = torch.empty(rows, D, dtype=torch.bfloat16, device=dev) if grad_on else None
     _lib.call("hstu_ln_uvqk_fwd_a16", x.data_ptr(), x.stride(0), offsets.data_ptr(), B, rows, D,
               w_uvqk.data_ptr(), n_out, geo.eps, geo.activation, x_stats.data_ptr(),
-              _lib.ptr(h_pre), uvqk.data_ptr(), n_out, _lib.ptr(xn), st)
+              1 if stats_given else 0, _lib.ptr(h_pre), uvqk.data_ptr(), n_out, _lib.ptr(xn), st)
     attn = torch.empty(rows, hv, dtype=torch.float32, device=dev)
     pos_w_c = pos_w.contiguous() if bmap is not None else None
     ts_w_c = ts_w.contiguous() if bmap is not None else None
@@ -495,13 +502,16 @@ def _stu_forward_a16(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGe
     o_in = torch.empty(rows, hv, dtype=torch.bfloat16, device=dev) if needs_w_grad else None
     y = torch.empty(rows, D, dtype=torch.float32, device=dev)
     b_o_c = b_o.contiguous()
+    # the next layer's LN statistics from this gate_o's epilogue (one 256-column panel)
+    y_stats = (torch.empty(rows, 2, dtype=torch.float32, device=dev)
+               if has_next and STATS_IN_EPILOGUE and 240 < D <= 256 else None)
     _lib.call("hstu_gate_o_fwd_a16", uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
               offsets.data_ptr(), B, rows, hv, D, w_o.data_ptr(), b_o_c.data_ptr(), x.data_ptr(),
               x.stride(0), geo.eps, geo.dropout_p, seed, _lib.ptr(seed_offset),
-              attn_stats.data_ptr(), _lib.ptr(o_in), y.data_ptr(), D, st)
+              attn_stats.data_ptr(), _lib.ptr(o_in), y.data_ptr(), D, _lib.ptr(y_stats), st)
     saved = (x, offsets, bmap, w_uvqk, w_o, pos_w_c, ts_w_c, x_stats, uvqk, h_pre, attn,
              attn_stats, o_in, xn)
-    return y, saved, None
+    return y, saved, y_stats
 
 
 def _stu_backward_a16(saved, dy, geo: STUGeometry, seed: int, seed_offset, want_uvqk: bool,
@@ -832,7 +842,9 @@ class STUStackFunction(torch.autograd.Function):
         pre = None
         for l in range(n_layers):
             w_uvqk, w_o, b_o, pos_w, ts_w = params[5 * l:5 * l + 5]
-            nxt = params[5 * (l + 1)] if fuse and l + 1 < n_layers else None
+            # the next layer's _uvqk: the fp32 layer boundary (fuse) or, in the bf16
+            # activation layout, "compute the next layer's LN statistics" (a16)
+            nxt = params[5 * (l + 1)] if (fuse or geo.a16) and l + 1 < n_layers else None
             x, saved, pre = _stu_forward(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo,
                                          seeds[l], seed_offset, grad_on,
                                          w_o.requires_grad or b_o.requires_grad, pre, nxt)

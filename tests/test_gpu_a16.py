@@ -60,14 +60,23 @@ def test_ln_uvqk_fwd_a16_bitexact(D, n_out):
     u16 = torch.empty(cap, n_out, dtype=torch.bfloat16, device=DEV)
     xn = torch.empty(cap, D, dtype=torch.bfloat16, device=DEV)
     _lib.call("hstu_ln_uvqk_fwd_a16", x.data_ptr(), D, offs.data_ptr(), B, cap, D, w.data_ptr(),
-              n_out, 1e-6, 1, xs.data_ptr(), h16.data_ptr(), u16.data_ptr(), n_out, xn.data_ptr(),
-              st)
+              n_out, 1e-6, 1, xs.data_ptr(), 0, h16.data_ptr(), u16.data_ptr(), n_out,
+              xn.data_ptr(), st)
     torch.cuda.synchronize()
     _eq(xs[:total], xs32[:total], "x_stats")
     _eq(h16[:total], _bf(h32[:total]), "h_pre")
     _eq(u16[:total], _bf(u32[:total]), "uvqk")
     ln = (x[:total] - xs[:total, 0:1]) * xs[:total, 1:2]
     _eq(xn[:total], _bf(ln), "xn = bf16(LN(x))")
+    # statistics given (the previous layer's gate_o epilogue): the same outputs
+    h2, u2, xn2 = torch.empty_like(h16), torch.empty_like(u16), torch.empty_like(xn)
+    _lib.call("hstu_ln_uvqk_fwd_a16", x.data_ptr(), D, offs.data_ptr(), B, cap, D, w.data_ptr(),
+              n_out, 1e-6, 1, xs.data_ptr(), 1, h2.data_ptr(), u2.data_ptr(), n_out,
+              xn2.data_ptr(), st)
+    torch.cuda.synchronize()
+    _eq(h2[:total], h16[:total], "h_pre (stats given)")
+    _eq(u2[:total], u16[:total], "uvqk (stats given)")
+    _eq(xn2[:total], xn[:total], "xn (stats given)")
 
 
 def _attn_case(seed, lengths, N, d, H=1):
@@ -167,10 +176,20 @@ def test_gate_o_a16_bitexact(D, hv):
         o_in = torch.empty(cap, hv, dtype=torch.bfloat16 if a16 else torch.float32, device=DEV)
         y = torch.empty(cap, D, device=DEV)
         u = uvqk16 if a16 else uvqk32
+        ys = torch.full((cap, 2), float("nan"), device=DEV) if a16 and D == 256 else None
         _lib.call("hstu_gate_o_fwd_a16" if a16 else "hstu_gate_o_fwd_bf16", u.data_ptr(), n_out,
                   attn.data_ptr(), hv, offs.data_ptr(), B, cap, hv, D, w_o.data_ptr(), b_o.data_ptr(),
                   x.data_ptr(), D, 1e-6, 0.2, 1234, seed_off.data_ptr(), ast.data_ptr(),
-                  o_in.data_ptr(), y.data_ptr(), D, st)
+                  o_in.data_ptr(), y.data_ptr(), D, *((_lib.ptr(ys),) if a16 else ()), st)
+        if ys is not None:  # y's LN statistics = what the next LN + UVQK computes from y
+            xs = torch.empty(cap, 2, device=DEV)
+            w = torch.randn(D, 1024, device=DEV) * 0.05
+            hh = torch.empty(cap, 1024, dtype=torch.bfloat16, device=DEV)
+            _lib.call("hstu_ln_uvqk_fwd_a16", y.data_ptr(), D, offs.data_ptr(), B, cap, D,
+                      w.data_ptr(), 1024, 1e-6, 1, xs.data_ptr(), 0, None, hh.data_ptr(), 1024,
+                      None, st)
+            torch.cuda.synchronize()
+            _eq(ys[:total], xs[:total], "y_stats = LN statistics of y")
         dy = torch.randn(cap, D, device=DEV, generator=torch.Generator(device="cuda").manual_seed(3))
         du = torch.empty(cap, n_out, dtype=torch.bfloat16 if a16 else torch.float32, device=DEV)
         da = torch.empty(cap, hv, device=DEV)
