@@ -660,6 +660,12 @@ GR_API int gr_wgrad_multi(const int64_t* desc, int n_problems, const int64_t* of
  * pass (the attention DMAs its tiles straight from the bf16 uvqk rows), half of every
  * projection's activation bytes, and the weight gradients' fp32 operand reads.
  *
+ * Weights enter the a16 projections as bf16 [N][K] images (autocast casts each mm's
+ * weight to bf16 the same way), made once per step by gr_weight_images_bf16: desc = n
+ * (<= 32) x 5 int64 {src (fp32, rows x cols row-major), rows, cols, transpose, dst (bf16:
+ * rows x cols, or cols x rows when transpose = 1)}.  Images: wt_uvqk = W_uvqk^T (n_out, D),
+ * w_o16 = W_o (D, hdv), wt_o16 = W_o^T (hdv, D), w_uvqk16 = W_uvqk (D, n_out); K (the
+ * image's row length) % 8 == 0, 16-byte aligned.
  * hstu_ln_uvqk_fwd_a16: hstu_ln_uvqk_fwd with bf16 h_pre (optional) and uvqk (n_out,
  *   ld_out even), plus optional xn (rows, D) = bf16 LN(x), the weight gradient's A operand
  *   (replaces hstu.py:258-305 under autocast).  stats_given = 1: x_stats already holds the
@@ -677,8 +683,9 @@ GR_API int gr_wgrad_multi(const int64_t* desc, int n_problems, const int64_t* of
  * gr_wgrad_multi_a16: gr_wgrad_multi with bf16 MFMA operands and a 10th descriptor word of
  *   flags per problem (bit 0: A rows bf16, bit 1: B rows bf16); Ka <= 256, Ka, Nb, lda,
  *   ldb multiples of 4, bf16 rows 8-byte aligned, a bf16 A takes no row stats. */
+GR_API int gr_weight_images_bf16(const int64_t* desc, int n, void* stream);
 GR_API int hstu_ln_uvqk_fwd_a16(const float* x, int64_t ld_x, const int64_t* offsets, int B,
-                    int64_t max_rows, int D, const float* w_uvqk, int n_out, float eps,
+                    int64_t max_rows, int D, const uint16_t* wt_uvqk, int n_out, float eps,
                     int activation, float* x_stats, int stats_given, uint16_t* h_pre,
                     uint16_t* uvqk, int64_t ld_out, uint16_t* xn, void* stream);
 GR_API int hstu_attn_fwd_a16(const uint16_t* q, const uint16_t* k, const uint16_t* v,
@@ -688,12 +695,12 @@ GR_API int hstu_attn_fwd_a16(const uint16_t* q, const uint16_t* k, const uint16_
                     void* stream);
 GR_API int hstu_gate_o_fwd_a16(const uint16_t* u, int64_t ld_u, const float* attn, int64_t ld_attn,
                     const int64_t* offsets, int B, int64_t max_rows, int hdv, int D,
-                    const float* w_o, const float* b_o, const float* x_res, int64_t ld_x,
+                    const uint16_t* w_o16, const float* b_o, const float* x_res, int64_t ld_x,
                     float eps, float dropout_p, uint64_t seed, const int64_t* seed_offset,
                     float* attn_stats, uint16_t* o_in, float* y, int64_t ld_y, float* y_stats,
                     void* stream);
 GR_API int hstu_gate_o_bwd_a16(const float* dy, int64_t ld_dy, const int64_t* offsets, int B,
-                    int64_t max_rows, int hdv, int D, const float* w_o, const uint16_t* u,
+                    int64_t max_rows, int hdv, int D, const uint16_t* wt_o16, const uint16_t* u,
                     int64_t ld_u, const float* attn, int64_t ld_attn, const float* attn_stats,
                     const uint16_t* h_u, int64_t ld_h, float dropout_p, uint64_t seed,
                     const int64_t* seed_offset, uint16_t* du, int64_t ld_du, float* d_attn,
@@ -708,7 +715,7 @@ GR_API int hstu_attn_bwd_a16(const uint16_t* q, const uint16_t* k, const uint16_
                     uint16_t* dk, uint16_t* dv_out, int64_t ld_d, float* dpos_w, float* dts_w,
                     void* workspace, size_t ws_bytes, void* stream);
 GR_API int hstu_ln_uvqk_bwd_a16(const uint16_t* dh, int64_t ld_dh, const int64_t* offsets, int B,
-                    int64_t max_rows, int D, int n_out, const float* w_uvqk, const float* x,
+                    int64_t max_rows, int D, int n_out, const uint16_t* w_uvqk16, const float* x,
                     int64_t ld_x, const float* x_stats, const float* dy_res, int64_t ld_dy,
                     float* dx, int64_t ld_dx, void* stream);
 GR_API size_t gr_wgrad_multi_a16_workspace_size(const int64_t* desc, int n_problems,

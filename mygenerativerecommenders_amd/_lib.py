@@ -105,6 +105,7 @@ def call(name: str, *args):
 
 
 KERNEL_NAMES = ("bucket_map", "attn_fwd", "attn_bwd", "attn_bwd_dkv", "attn_bwd_dq", "attn_bias_reduce", "attn_bf16_copies",
+                "weight_images",
                 "attn_fwd_bnd", "attn_fwd_bnd1", "attn_bwd_dq_bnd", "attn_bwd_dq_bnd1",
                 "ln_uvqk_fwd", "gate_o_fwd", "gate_o_bwd", "ln_uvqk_bwd", "boundary_fwd", "boundary_bwd",
                 "wgrad_partial",

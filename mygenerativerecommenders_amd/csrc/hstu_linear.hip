@@ -41,6 +41,32 @@ struct PanelCfg {
 // value masked afterwards): a guarded load makes hipcc branch around it and wait
 // vmcnt(0) per element, serialising dozens of L2 round trips per tile.
 
+// LayerNorm statistics of one row whose 16 lanes hold 16 values each (value j = column
+// 16 j + sub, zero past K): a fixed summation order with fp contraction off, so the
+// statistics pass below and gate_o's a16 epilogue (y_stats) give identical values.
+__device__ __forceinline__ float2 ln_stats16(const float (&v)[16], int sub, int K, float eps) {
+#pragma clang fp contract(off)
+  const float invk = 1.f / (float)K;
+  float s = 0.f;
+#pragma unroll
+  for (int it = 0; it < 4; ++it) s += (v[4 * it] + v[4 * it + 1]) + (v[4 * it + 2] + v[4 * it + 3]);
+  s = sum16(s);
+  const float mean = s * invk;
+  float q = 0.f;
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    float d[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = 4 * it + u;
+      d[u] = 16 * j + sub < K ? v[j] - mean : 0.f;
+    }
+    q += (d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]);
+  }
+  q = sum16(q);
+  return make_float2(mean, rsqrtf(q * invk + eps));
+}
+
 // Row statistics (mean, rstd) of rows [m0, m0+64) over K columns: wave w owns 16 rows,
 // 4 at a time with 16 lanes per row; loads issued 4-deep before the reductions.
 __device__ __forceinline__ void panel_row_stats(const float* base, int64_t ld, int64_t m0,
@@ -72,28 +98,10 @@ __device__ __forceinline__ void panel_row_stats(const float* base, int64_t ld, i
       const int64_t m = m0 + r;
 #pragma unroll
       for (int j = 0; j < 16; ++j) v[pass][j] = 16 * j + sub < K ? v[pass][j] : 0.f;
-      float s = 0.f;
-#pragma unroll
-      for (int it = 0; it < 4; ++it)
-        s += (v[pass][4 * it] + v[pass][4 * it + 1]) + (v[pass][4 * it + 2] + v[pass][4 * it + 3]);
-      s = sum16(s);
-      const float mean = s * invk;
-      float q = 0.f;
-#pragma unroll
-      for (int it = 0; it < 4; ++it) {
-        float d[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int j = 4 * it + u;
-          d[u] = 16 * j + sub < K ? v[pass][j] - mean : 0.f;
-        }
-        q += (d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]);
-      }
-      q = sum16(q);
-      const float rstd = rsqrtf(q * invk + eps);
+      const float2 mr = ln_stats16(v[pass], sub, K, eps);
       if (sub == 0) {
-        st_lds[r] = make_float2(mean, rstd);
-        if (st_glob && m < total) st_glob[m] = make_float2(mean, rstd);
+        st_lds[r] = mr;
+        if (st_glob && m < total) st_glob[m] = mr;
       }
     }
     return;
@@ -341,20 +349,37 @@ __global__ __launch_bounds__(256) void rowpanel_bf16_kernel(Op op) {
   const int b_r = Op::B_N_CONTIG ? tid / NP2 : tid % BKT;
   const bool b_col = Op::B_N_CONTIG ? (b_c < P::BN && n0 + b_c < op.N) : true;
   const int vb = b_col ? (b_r * bks + (n0 + b_c) * bns) * 4 : OOB_OFF;
+  // B16 (the a16 ops): the weight as a bf16 [N][K] image (op.w16, K % 8 == 0); thread t
+  // moves the 16-byte pieces p = t + 256 i (column p / 4, k-octet p % 4) of a chunk, which
+  // land in the [column][k] LDS image unchanged
+  constexpr bool B16 = Op::B16;
+  constexpr int NB16 = B16 ? (P::BN * 4 + 255) / 256 : 1;
+  const __amdgpu_buffer_rsrc_t rw16 = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)op.w16, 0, B16 ? op.K * op.N * 2 : 0, 0x00020000);
 
-  float ra[NA], ra2[Op::NSRC == 2 ? NA : 1], rb[NB];
+  float ra[NA], ra2[Op::NSRC == 2 ? NA : 1], rb[B16 ? 1 : NB];
+  u32x4_t rb16[NB16];
   auto load = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       ra[i] = buf_ld_e<E0>(ra0, va0 + k0 * E0, i * RPA * ld0 * E0);
       if constexpr (Op::NSRC == 2) ra2[i] = buf_ld(ra1, va1 + k0 * 4, i * RPA * ld1 * 4);
     }
+    if constexpr (B16) {
+#pragma unroll
+      for (int i = 0; i < NB16; ++i) {
+        const int p = tid + 256 * i, c = p >> 2, o = p & 3;
+        const bool ok = p < P::BN * 4 && n0 + c < op.N && k0 + 8 * o < op.K;
+        rb16[i] = __builtin_amdgcn_raw_buffer_load_b128(rw16, ok ? ((n0 + c) * op.K + k0 + 8 * o) * 2 : OOB_OFF, 0, 0);
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       if constexpr (Op::B_N_CONTIG)
-        rb[i] = buf_ld(rw, vb, (k0 + RPB * i) * bks * 4);
+        rb[B16 ? 0 : i] = buf_ld(rw, vb, (k0 + RPB * i) * bks * 4);
       else
-        rb[i] = buf_ld(rw, vb, (k0 * bks + CPP * i * bns) * 4);
+        rb[B16 ? 0 : i] = buf_ld(rw, vb, (k0 * bks + CPP * i * bns) * 4);
     }
   };
   auto store = [&](int k0, int buf) {
@@ -368,7 +393,14 @@ __global__ __launch_bounds__(256) void rowpanel_bf16_kernel(Op op) {
                                  stats[r], ok);
       As[r * LDK + a_c] = (__bf16)(ok ? v : 0.f);
     }
-    if constexpr (Op::B_N_CONTIG && RPB == 1) {
+    if constexpr (B16) {
+#pragma unroll
+      for (int i = 0; i < NB16; ++i) {
+        const int p = tid + 256 * i;
+        if ((P::BN * 4) % 256 == 0 || p < P::BN * 4)
+          *reinterpret_cast<u32x4_t*>(Bs + (p >> 2) * LDK + 8 * (p & 3)) = rb16[i];
+      }
+    } else if constexpr (Op::B_N_CONTIG && RPB == 1) {
       // a thread owns one weight column's 32 k-values: 16 packed pair stores
       if (b_c < P::BN) {
 #pragma unroll
@@ -476,8 +508,13 @@ __global__ __launch_bounds__(256) void rowpanel_bf16v_kernel(Op op) {
   else
     vb = (4 * bq + (n0 + bc) * bns) * 4;
 
-  f4 ra[2], ra2[Op::NSRC == 2 ? 2 : 1], rb[8];
+  // B16: the bf16 [N][K] weight image, 16-byte pieces as in rowpanel_bf16_kernel
+  constexpr bool B16 = Op::B16;
+  const __amdgpu_buffer_rsrc_t rw16 = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)op.w16, 0, B16 ? op.K * op.N * 2 : 0, 0x00020000);
+  f4 ra[2], ra2[Op::NSRC == 2 ? 2 : 1], rb[B16 ? 1 : 8];
   u32x2_t rh[A0H ? 2 : 1];
+  u32x4_t rb16[B16 ? 4 : 1];
   auto ld4 = [](__amdgpu_buffer_rsrc_t r, int v, int s) {
     return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, v, s, 0));
   };
@@ -490,12 +527,21 @@ __global__ __launch_bounds__(256) void rowpanel_bf16v_kernel(Op op) {
         ra[i] = ld4(ra0, va0 + k0 * 4, i * 32 * ld0 * 4);
       if constexpr (Op::NSRC == 2) ra2[Op::NSRC == 2 ? i : 0] = ld4(ra1, va1 + k0 * 4, i * 32 * ld1 * 4);
     }
+    if constexpr (B16) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int p = tid + 256 * i, c = p >> 2, o = p & 3;
+        const bool ok = n0 + c < op.N && k0 + 8 * o < op.K;
+        rb16[B16 ? i : 0] = __builtin_amdgcn_raw_buffer_load_b128(rw16, ok ? ((n0 + c) * op.K + k0 + 8 * o) * 2 : OOB_OFF, 0, 0);
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       if constexpr (Op::B_N_CONTIG)
-        rb[i] = ld4(rw, vb, (k0 + 8 * (i >> 1) + (i & 1)) * bks * 4);
+        rb[B16 ? 0 : i] = ld4(rw, vb, (k0 + 8 * (i >> 1) + (i & 1)) * bks * 4);
       else
-        rb[i] = ld4(rw, vb, (k0 + 32 * i * bns) * 4);  // columns >= N: past the range, 0
+        rb[B16 ? 0 : i] = ld4(rw, vb, (k0 + 32 * i * bns) * 4);  // columns >= N: past the range, 0
     }
   };
   auto store = [&](int k0, int buf) {
@@ -520,7 +566,13 @@ __global__ __launch_bounds__(256) void rowpanel_bf16v_kernel(Op op) {
       *reinterpret_cast<u32x2_t*>(As + r * LDK + 4 * aq) =
           u32x2_t{pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3])};
     }
-    if constexpr (Op::B_N_CONTIG) {
+    if constexpr (B16) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int p = tid + 256 * i;
+        *reinterpret_cast<u32x4_t*>(Bs + (p >> 2) * LDK + 8 * (p & 3)) = rb16[B16 ? i : 0];
+      }
+    } else if constexpr (Op::B_N_CONTIG) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -608,6 +660,7 @@ template <bool A16>
 struct OpLnUvqkT {
   static constexpr bool B_N_CONTIG = true;
   static constexpr int A0_BYTES = 4;
+  static constexpr bool B16 = A16;  // the weight as a bf16 [N][K] image (w16)
   const int64_t* offsets;
   int B, K, N;
   const float* x;
@@ -620,7 +673,8 @@ struct OpLnUvqkT {
   act_t<A16>* out;
   int64_t ld_out;
   __bf16* xn;  // A16: optional bf16 LN(x) rows (ld K), the weight gradient's A operand
-  int stats_given;  // A16: x_stats already holds the rows' (mean, rstd) (the previous
+  int stats_given;
+  const __bf16* w16;  // A16: W_uvqk^T as bf16, (n_out, D)  // A16: x_stats already holds the rows' (mean, rstd) (the previous
                     // layer's gate_o epilogue computed them): no statistics pass
   __device__ void prologue(int64_t m0, int64_t total, float2* st) const {
     if (A16 && stats_given) {
@@ -701,6 +755,7 @@ template <bool A16>
 struct OpGateOT {
   static constexpr bool B_N_CONTIG = false;
   static constexpr int A0_BYTES = A16 ? 2 : 4;  // u
+  static constexpr bool B16 = A16;  // the weight as a bf16 [N][K] image (w16)
   const int64_t* offsets;
   int B, K, N;  // K = hdv, N = D
   const act_t<A16>* u;
@@ -720,6 +775,7 @@ struct OpGateOT {
   int64_t ldy;
   float2* y_stats;  // A16, N <= 256 (one panel): the LayerNorm (mean, rstd) of each y row
                     // with eps -- the next layer's x_stats, in panel_row_stats's order
+  const __bf16* w16;  // A16: W_o as bf16, (D, hdv)
   __device__ void prologue(int64_t m0, int64_t total, float2* st) const {
     panel_row_stats(attn, lda, m0, total, K, eps, st, blockIdx.y == 0 ? a_stats : nullptr);
   }
@@ -798,7 +854,6 @@ struct OpGateOT {
         xv[r][t] = xres ? as_global(xres)[mc * ldx + (n < N ? n : N - 1)] : 0.f;
       }
     }
-    const float invk = 1.f / (float)N;
     const int sub = ncol & 15;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -806,26 +861,9 @@ struct OpGateOT {
       float v[NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t) v[t] = 16 * t + sub < N ? (acc[t][r] + bv[t]) + xv[r][t] : 0.f;
-      float s = 0.f;
-#pragma unroll
-      for (int it = 0; it < 4; ++it) s += (v[4 * it] + v[4 * it + 1]) + (v[4 * it + 2] + v[4 * it + 3]);
-      s = sum16(s);
-      const float mean = s * invk;
-      float q = 0.f;
-#pragma unroll
-      for (int it = 0; it < 4; ++it) {
-        float d[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int j = 4 * it + u;
-          d[u] = 16 * j + sub < N ? v[j] - mean : 0.f;
-        }
-        q += (d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]);
-      }
-      q = sum16(q);
-      const float rstd = rsqrtf(q * invk + eps);
+      const float2 mr = ln_stats16(v, sub, N, eps);
       if (m < total) {
-        if (sub == 0) y_stats[m] = make_float2(mean, rstd);
+        if (sub == 0) y_stats[m] = mr;
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
           const int n = ncol + 16 * t;
@@ -843,6 +881,7 @@ template <bool A16>
 struct OpGateOBwdT : NoStats {
   static constexpr bool B_N_CONTIG = true;
   static constexpr int A0_BYTES = 4;  // dy
+  static constexpr bool B16 = A16;  // the weight as a bf16 [N][K] image (w16)
   const int64_t* offsets;
   int B, K, N;  // K = D, N = hdv
   const float* dy;
@@ -862,6 +901,7 @@ struct OpGateOBwdT : NoStats {
   int64_t lddu;
   float* da;
   int64_t ldda;
+  const __bf16* w16 = nullptr;  // A16: W_o^T as bf16, (hdv, D)
   static constexpr int NSRC = 1;
   __device__ __amdgpu_buffer_rsrc_t a_rsrc0(int64_t m0, int64_t t) const { return rows_rsrc(dy, lddy, m0, t); }
   __device__ __amdgpu_buffer_rsrc_t a_rsrc1(int64_t m0, int64_t t) const { return rows_rsrc(dy, lddy, m0, t); }
@@ -1011,6 +1051,7 @@ template <bool A16>
 struct OpLnUvqkBwdT : NoStats {
   static constexpr bool B_N_CONTIG = false;
   static constexpr int A0_BYTES = A16 ? 2 : 4;  // dh
+  static constexpr bool B16 = A16;  // the weight as a bf16 [N][K] image (w16)
   const int64_t* offsets;
   int B, K, N;  // K = n_out (4hd), N = D
   const act_t<A16>* dh;
@@ -1023,6 +1064,7 @@ struct OpLnUvqkBwdT : NoStats {
   int64_t lddy;
   float* dx;
   int64_t lddx;
+  const __bf16* w16 = nullptr;  // A16: W_uvqk as bf16, (D, n_out)
   static constexpr int NSRC = 1;
   __device__ __amdgpu_buffer_rsrc_t a_rsrc0(int64_t m0, int64_t t) const { return rows_rsrc(dh, lddh, m0, t); }
   __device__ __amdgpu_buffer_rsrc_t a_rsrc1(int64_t m0, int64_t t) const { return rows_rsrc(dh, lddh, m0, t); }

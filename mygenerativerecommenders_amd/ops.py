@@ -463,6 +463,24 @@ def _stu_forward(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGeomet
     return y, saved, pre_next
 
 
+def weight_images_bf16(specs):
+    """bf16 [N][K] weight images for the a16 projections (gr_weight_images_bf16, one launch):
+    specs = [(fp32 2-D tensor, transpose)], returns the images."""
+    import numpy as np
+    outs, rows = [], []
+    for w, tr in specs:
+        w = w.detach()
+        if not w.is_contiguous():
+            w = w.contiguous()
+        R, C = w.shape
+        o = torch.empty((C, R) if tr else (R, C), dtype=torch.bfloat16, device=w.device)
+        outs.append(o)
+        rows.append((w.data_ptr(), R, C, 1 if tr else 0, o.data_ptr()))
+    desc = np.ascontiguousarray(np.array(rows, dtype=np.int64))
+    _lib.call("gr_weight_images_bf16", desc.ctypes.data, len(rows), _stream())
+    return outs
+
+
 def _stu_forward_a16(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGeometry, seed: int,
                      seed_offset, grad_on: bool, needs_w_grad: bool, pre=None, has_next=False):
     """One STU layer forward with bf16 activations (ABI 16): LN + UVQK writes bf16 uvqk /
@@ -483,13 +501,14 @@ def _stu_forward_a16(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGe
     w_uvqk = w_uvqk.contiguous()
     w_o = w_o.contiguous()
     needs_w_grad = grad_on and needs_w_grad
+    wt_uvqk, w_o16 = weight_images_bf16([(w_uvqk, True), (w_o, False)])
     stats_given = pre is not None
     x_stats = pre if stats_given else torch.empty(rows, 2, dtype=torch.float32, device=dev)
     uvqk = torch.empty(rows, n_out, dtype=torch.bfloat16, device=dev)
     h_pre = torch.empty_like(uvqk) if geo.activation and grad_on else None
     xn = torch.empty(rows, D, dtype=torch.bfloat16, device=dev) if grad_on else None
     _lib.call("hstu_ln_uvqk_fwd_a16", x.data_ptr(), x.stride(0), offsets.data_ptr(), B, rows, D,
-              w_uvqk.data_ptr(), n_out, geo.eps, geo.activation, x_stats.data_ptr(),
+              wt_uvqk.data_ptr(), n_out, geo.eps, geo.activation, x_stats.data_ptr(),
               1 if stats_given else 0, _lib.ptr(h_pre), uvqk.data_ptr(), n_out, _lib.ptr(xn), st)
     attn = torch.empty(rows, hv, dtype=torch.float32, device=dev)
     pos_w_c = pos_w.contiguous() if bmap is not None else None
@@ -506,7 +525,7 @@ def _stu_forward_a16(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGe
     y_stats = (torch.empty(rows, 2, dtype=torch.float32, device=dev)
                if has_next and STATS_IN_EPILOGUE and 240 < D <= 256 else None)
     _lib.call("hstu_gate_o_fwd_a16", uvqk.data_ptr(), n_out, attn.data_ptr(), hv,
-              offsets.data_ptr(), B, rows, hv, D, w_o.data_ptr(), b_o_c.data_ptr(), x.data_ptr(),
+              offsets.data_ptr(), B, rows, hv, D, w_o16.data_ptr(), b_o_c.data_ptr(), x.data_ptr(),
               x.stride(0), geo.eps, geo.dropout_p, seed, _lib.ptr(seed_offset),
               attn_stats.data_ptr(), _lib.ptr(o_in), y.data_ptr(), D, _lib.ptr(y_stats), st)
     saved = (x, offsets, bmap, w_uvqk, w_o, pos_w_c, ts_w_c, x_stats, uvqk, h_pre, attn,
@@ -529,10 +548,11 @@ def _stu_backward_a16(saved, dy, geo: STUGeometry, seed: int, seed_offset, want_
     n_out = geo.n_out
     st = _stream()
     dy = dy.contiguous()
+    wt_o16, w_uvqk16 = weight_images_bf16([(w_o, True), (w_uvqk, False)])
     d_uvqk = torch.empty(rows, n_out, dtype=torch.bfloat16, device=dev)
     d_attn = torch.empty(rows, hv, dtype=torch.float32, device=dev)
     _lib.call("hstu_gate_o_bwd_a16", dy.data_ptr(), D, offsets.data_ptr(), B, rows, hv, D,
-              w_o.data_ptr(), uvqk.data_ptr(), n_out, attn.data_ptr(), hv, attn_stats.data_ptr(),
+              wt_o16.data_ptr(), uvqk.data_ptr(), n_out, attn.data_ptr(), hv, attn_stats.data_ptr(),
               _lib.ptr(h_pre), n_out, geo.dropout_p, seed, _lib.ptr(seed_offset),
               d_uvqk.data_ptr(), n_out, d_attn.data_ptr(), hv, st)
     L = _lib.lib()
@@ -551,7 +571,7 @@ def _stu_backward_a16(saved, dy, geo: STUGeometry, seed: int, seed_offset, want_
               _lib.ptr(d_pos_w), _lib.ptr(d_ts_w), ws.data_ptr(), ws_n, st)
     dx = torch.empty(rows, D, dtype=torch.float32, device=dev)
     _lib.call("hstu_ln_uvqk_bwd_a16", d_uvqk.data_ptr(), n_out, offsets.data_ptr(), B, rows, D,
-              n_out, w_uvqk.data_ptr(), x.data_ptr(), x.stride(0), x_stats.data_ptr(),
+              n_out, w_uvqk16.data_ptr(), x.data_ptr(), x.stride(0), x_stats.data_ptr(),
               dy.data_ptr(), D, dx.data_ptr(), D, st)
     d_w_uvqk = torch.empty(D, n_out, dtype=torch.float32, device=dev) if want_uvqk else None
     d_w_o = d_b_o = None

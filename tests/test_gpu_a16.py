@@ -41,6 +41,19 @@ def _bf(t):
     return t.to(torch.bfloat16)
 
 
+def _img(w, transpose):
+    """bf16 [N][K] weight image through gr_weight_images_bf16, checked against torch's
+    round-to-nearest-even cast of the same matrix."""
+    src = w.contiguous()
+    R, C = src.shape
+    out = torch.empty((C, R) if transpose else (R, C), dtype=torch.bfloat16, device=DEV)
+    desc = np.array([[src.data_ptr(), R, C, 1 if transpose else 0, out.data_ptr()]], dtype=np.int64)
+    _lib.call("gr_weight_images_bf16", desc.ctypes.data, 1, _lib.stream_handle())
+    torch.cuda.synchronize()
+    _eq(out, _bf(src.t().contiguous() if transpose else src), "weight image")
+    return out
+
+
 @pytest.mark.parametrize("D,n_out", [(256, 1024), (192, 768)])
 def test_ln_uvqk_fwd_a16_bitexact(D, n_out):
     offs, total = _offsets([700, 1, 333, 2048, 64])
@@ -59,7 +72,8 @@ def test_ln_uvqk_fwd_a16_bitexact(D, n_out):
     h16 = torch.empty(cap, n_out, dtype=torch.bfloat16, device=DEV)
     u16 = torch.empty(cap, n_out, dtype=torch.bfloat16, device=DEV)
     xn = torch.empty(cap, D, dtype=torch.bfloat16, device=DEV)
-    _lib.call("hstu_ln_uvqk_fwd_a16", x.data_ptr(), D, offs.data_ptr(), B, cap, D, w.data_ptr(),
+    wt = _img(w, True)
+    _lib.call("hstu_ln_uvqk_fwd_a16", x.data_ptr(), D, offs.data_ptr(), B, cap, D, wt.data_ptr(),
               n_out, 1e-6, 1, xs.data_ptr(), 0, h16.data_ptr(), u16.data_ptr(), n_out,
               xn.data_ptr(), st)
     torch.cuda.synchronize()
@@ -70,7 +84,7 @@ def test_ln_uvqk_fwd_a16_bitexact(D, n_out):
     _eq(xn[:total], _bf(ln), "xn = bf16(LN(x))")
     # statistics given (the previous layer's gate_o epilogue): the same outputs
     h2, u2, xn2 = torch.empty_like(h16), torch.empty_like(u16), torch.empty_like(xn)
-    _lib.call("hstu_ln_uvqk_fwd_a16", x.data_ptr(), D, offs.data_ptr(), B, cap, D, w.data_ptr(),
+    _lib.call("hstu_ln_uvqk_fwd_a16", x.data_ptr(), D, offs.data_ptr(), B, cap, D, wt.data_ptr(),
               n_out, 1e-6, 1, xs.data_ptr(), 1, h2.data_ptr(), u2.data_ptr(), n_out,
               xn2.data_ptr(), st)
     torch.cuda.synchronize()
@@ -170,6 +184,7 @@ def test_gate_o_a16_bitexact(D, hv):
     st = _lib.stream_handle()
     uvqk32, h32 = uvqk16.float(), h16.float()
     seed_off = torch.zeros(1, dtype=torch.int64, device=DEV)
+    w_o16, wt_o16 = _img(w_o, False), _img(w_o, True)
     outs = {}
     for a16 in (False, True):
         ast = torch.empty(cap, 2, device=DEV)
@@ -178,15 +193,16 @@ def test_gate_o_a16_bitexact(D, hv):
         u = uvqk16 if a16 else uvqk32
         ys = torch.full((cap, 2), float("nan"), device=DEV) if a16 and D == 256 else None
         _lib.call("hstu_gate_o_fwd_a16" if a16 else "hstu_gate_o_fwd_bf16", u.data_ptr(), n_out,
-                  attn.data_ptr(), hv, offs.data_ptr(), B, cap, hv, D, w_o.data_ptr(), b_o.data_ptr(),
+                  attn.data_ptr(), hv, offs.data_ptr(), B, cap, hv, D,
+                  (w_o16 if a16 else w_o).data_ptr(), b_o.data_ptr(),
                   x.data_ptr(), D, 1e-6, 0.2, 1234, seed_off.data_ptr(), ast.data_ptr(),
                   o_in.data_ptr(), y.data_ptr(), D, *((_lib.ptr(ys),) if a16 else ()), st)
         if ys is not None:  # y's LN statistics = what the next LN + UVQK computes from y
             xs = torch.empty(cap, 2, device=DEV)
-            w = torch.randn(D, 1024, device=DEV) * 0.05
+            wt = _img(torch.randn(D, 1024, device=DEV) * 0.05, True)
             hh = torch.empty(cap, 1024, dtype=torch.bfloat16, device=DEV)
             _lib.call("hstu_ln_uvqk_fwd_a16", y.data_ptr(), D, offs.data_ptr(), B, cap, D,
-                      w.data_ptr(), 1024, 1e-6, 1, xs.data_ptr(), 0, None, hh.data_ptr(), 1024,
+                      wt.data_ptr(), 1024, 1e-6, 1, xs.data_ptr(), 0, None, hh.data_ptr(), 1024,
                       None, st)
             torch.cuda.synchronize()
             _eq(ys[:total], xs[:total], "y_stats = LN statistics of y")
@@ -195,7 +211,7 @@ def test_gate_o_a16_bitexact(D, hv):
         da = torch.empty(cap, hv, device=DEV)
         h = h16 if a16 else h32
         _lib.call("hstu_gate_o_bwd_a16" if a16 else "hstu_gate_o_bwd_bf16", dy.data_ptr(), D,
-                  offs.data_ptr(), B, cap, hv, D, w_o.data_ptr(), u.data_ptr(), n_out,
+                  offs.data_ptr(), B, cap, hv, D, (wt_o16 if a16 else w_o).data_ptr(), u.data_ptr(), n_out,
                   attn.data_ptr(), hv, ast.data_ptr(), h.data_ptr(), n_out, 0.2, 1234,
                   seed_off.data_ptr(), du.data_ptr(), n_out, da.data_ptr(), hv, st)
         outs[a16] = (ast, o_in, y, du, da)
@@ -227,7 +243,7 @@ def test_ln_uvqk_bwd_a16_bitexact(D, n_out):
     _lib.call("hstu_ln_uvqk_bwd_bf16", dh32.data_ptr(), n_out, offs.data_ptr(), B, cap, D, n_out,
               w.data_ptr(), x.data_ptr(), D, xs.data_ptr(), dy.data_ptr(), D, dx32.data_ptr(), D, st)
     _lib.call("hstu_ln_uvqk_bwd_a16", dh16.data_ptr(), n_out, offs.data_ptr(), B, cap, D, n_out,
-              w.data_ptr(), x.data_ptr(), D, xs.data_ptr(), dy.data_ptr(), D, dx16.data_ptr(), D, st)
+              _img(w, False).data_ptr(), x.data_ptr(), D, xs.data_ptr(), dy.data_ptr(), D, dx16.data_ptr(), D, st)
     torch.cuda.synchronize()
     _eq(dx16[:total], dx32[:total], "dx")
 
