@@ -675,9 +675,10 @@ GR_API int gr_wgrad_multi(const int64_t* desc, int n_problems, const int64_t* of
  *   each y row with `eps`, i.e. the next layer's x_stats.
  * hstu_attn_fwd_a16: hstu_attn_fwd_bf16 on bf16 q / k / v rows (16-byte aligned, ld_qkv a
  *   multiple of 8); zrow = d zero bf16 values (caller-owned, 16-byte aligned).
- * hstu_gate_o_fwd_a16 / _bwd_a16: u, h_u, o_in and du in bf16 (hstu.py:393-413).
+ * hstu_gate_o_fwd_a16 / _bwd_a16: u, h_u, o_in, du and d_attn in bf16 (hstu.py:393-413).
  * hstu_attn_bwd_a16: dq / dk / dv (bf16, written with silu'(h) from bf16 h applied) of
- *   hstu_attn_bwd_bf16; dout stays fp32 (it is d_attn); workspace from
+ *   hstu_attn_bwd_bf16; dout = gate_o_bwd_a16's bf16 d_attn (ld_dout = H d), staged by
+ *   DMA as is (no conversion pass); zrow as in the forward; workspace from
  *   hstu_attn_bwd_a16_workspace_size.
  * hstu_ln_uvqk_bwd_a16: dh (d_uvqk) in bf16.
  * gr_wgrad_multi_a16: gr_wgrad_multi with bf16 MFMA operands and a 10th descriptor word of
@@ -703,17 +704,17 @@ GR_API int hstu_gate_o_bwd_a16(const float* dy, int64_t ld_dy, const int64_t* of
                     int64_t max_rows, int hdv, int D, const uint16_t* wt_o16, const uint16_t* u,
                     int64_t ld_u, const float* attn, int64_t ld_attn, const float* attn_stats,
                     const uint16_t* h_u, int64_t ld_h, float dropout_p, uint64_t seed,
-                    const int64_t* seed_offset, uint16_t* du, int64_t ld_du, float* d_attn,
+                    const int64_t* seed_offset, uint16_t* du, int64_t ld_du, uint16_t* d_attn,
                     int64_t ld_da, void* stream);
 GR_API size_t hstu_attn_bwd_a16_workspace_size(int B, int N, int max_len, int H, int d,
                     int num_buckets);
 GR_API int hstu_attn_bwd_a16(const uint16_t* q, const uint16_t* k, const uint16_t* v,
-                    int64_t ld_qkv, const float* dout, int64_t ld_dout, const int64_t* offsets,
+                    int64_t ld_qkv, const uint16_t* dout, int64_t ld_dout, const int64_t* offsets,
                     int B, int N, int max_len, int H, int d, const uint8_t* bucket_map,
                     const float* pos_w, const float* ts_w, int num_buckets, const uint16_t* hq,
                     const uint16_t* hk, const uint16_t* hv, int64_t ld_h, uint16_t* dq,
                     uint16_t* dk, uint16_t* dv_out, int64_t ld_d, float* dpos_w, float* dts_w,
-                    void* workspace, size_t ws_bytes, void* stream);
+                    const uint16_t* zrow, void* workspace, size_t ws_bytes, void* stream);
 GR_API int hstu_ln_uvqk_bwd_a16(const uint16_t* dh, int64_t ld_dh, const int64_t* offsets, int B,
                     int64_t max_rows, int D, int n_out, const uint16_t* w_uvqk16, const float* x,
                     int64_t ld_x, const float* x_stats, const float* dy_res, int64_t ld_dy,

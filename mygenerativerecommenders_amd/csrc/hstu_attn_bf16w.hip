@@ -1370,24 +1370,27 @@ extern "C" int hstu_attn_fwd_a16(const uint16_t* q, const uint16_t* k, const uin
 extern "C" size_t hstu_attn_bwd_a16_workspace_size(int B, int N, int max_len, int H, int d,
                                                    int num_buckets) {
   if (B <= 0 || N <= 0 || H <= 0 || max_len <= 0 || !a16_shape(d)) return 0;
-  return gr_attn_bwd_bf16w_workspace(B, N, max_len, H, d, num_buckets, true);
+  // bias slabs | dS blocks | P blocks (dO arrives in bf16: no copy, no zero row)
+  return gr::al256(gr::bf16w_slab_bytes(B, N, max_len, H, num_buckets)) + 2 * gr::al256(gr::bf16w_ds_bytes(B, N, H));
 }
 
 extern "C" int hstu_attn_bwd_a16(const uint16_t* q, const uint16_t* k, const uint16_t* v,
-                                 int64_t ld_qkv, const float* dout, int64_t ld_dout,
+                                 int64_t ld_qkv, const uint16_t* dout, int64_t ld_dout,
                                  const int64_t* offsets, int B, int N, int max_len, int H, int d,
                                  const uint8_t* bucket_map, const float* pos_w, const float* ts_w,
                                  int num_buckets, const uint16_t* hq, const uint16_t* hk,
                                  const uint16_t* hv, int64_t ld_h, uint16_t* dq, uint16_t* dk,
                                  uint16_t* dvv, int64_t ld_d, float* dpos_w, float* dts_w,
-                                 void* workspace, size_t ws_bytes, void* stream) {
+                                 const uint16_t* zrow, void* workspace, size_t ws_bytes,
+                                 void* stream) {
   using namespace gr;
-  GR_REQUIRE(q && k && v && dout && offsets && dq && dk && dvv, "hstu_attn_bwd_a16: null pointer");
+  GR_REQUIRE(q && k && v && dout && offsets && dq && dk && dvv && zrow, "hstu_attn_bwd_a16: null pointer");
   GR_REQUIRE(B >= 0 && N > 0 && H > 0, "hstu_attn_bwd_a16: bad sizes");
   GR_REQUIRE(max_len >= 0 && max_len <= N, "hstu_attn_bwd_a16: max_len %d not in [0, N=%d]", max_len, N);
-  GR_REQUIRE(a16_shape(d) && a16_aligned({q, k, v}, ld_qkv) && ld_qkv >= (int64_t)H * d &&
-                 pair_aligned({dout}, {ld_dout}),
-             "hstu_attn_bwd_a16: needs d %% 32 == 0 in (128, 256] and 16-byte aligned rows (d %d)", d);
+  GR_REQUIRE(a16_shape(d) && a16_aligned({q, k, v, zrow}, ld_qkv) && ld_qkv >= (int64_t)H * d &&
+                 a16_aligned({dout}, ld_dout) && ld_dout == (int64_t)H * d,
+             "hstu_attn_bwd_a16: needs d %% 32 == 0 in (128, 256], 16-byte aligned rows and dout "
+             "(bf16) with ld_dout = H d (d %d)", d);
   GR_REQUIRE((hq == nullptr) == (hk == nullptr) && (hk == nullptr) == (hv == nullptr),
              "hstu_attn_bwd_a16: hq/hk/hv must be all given or all NULL");
   if (bucket_map)
@@ -1401,14 +1404,12 @@ extern "C" int hstu_attn_bwd_a16(const uint16_t* q, const uint16_t* k, const uin
     }
     return 0;
   }
-  const size_t need = gr_attn_bwd_bf16w_workspace(B, N, max_len, H, d, num_buckets, true);
+  const size_t need = hstu_attn_bwd_a16_workspace_size(B, N, max_len, H, d, num_buckets);
   GR_REQUIRE(workspace && ws_bytes >= need, "hstu_attn_bwd_a16: workspace %zu B < %zu B", ws_bytes, need);
   const size_t slab_b = al256(bf16w_slab_bytes(B, N, max_len, H, num_buckets));
   const size_t ds_b = al256(bf16w_ds_bytes(B, N, H));
-  const size_t cp_b = bf16w_copy_bytes(B, N, H, d);
-  const int nch = 4 * (d / 32);
   AttnBwdArgsW a{};
-  a.dout = dout; a.ld_dout = ld_dout;
+  a.dout = nullptr; a.ld_dout = ld_dout;
   a.offsets = offsets; a.B = B; a.N = N; a.H = H; a.d = d;
   a.map_kq = bucket_map ? bucket_map + (size_t)B * attn_tiles_per_seq(N) * 4096 : nullptr;
   a.pos_w = pos_w; a.ts_w = ts_w; a.nb = bucket_map ? num_buckets : 0;
@@ -1419,16 +1420,11 @@ extern "C" int hstu_attn_bwd_a16(const uint16_t* q, const uint16_t* k, const uin
   a.slabs = (float*)workspace;
   a.ds = (__bf16*)((char*)workspace + slab_b);
   a.pb = (__bf16*)((char*)workspace + slab_b + ds_b);
-  char* cp = (char*)workspace + slab_b + 2 * ds_b;
-  a.ob = (__bf16*)cp;
-  __bf16* ozrow = (__bf16*)(cp + cp_b);
+  a.ob = (__bf16*)dout;  // d_attn already in bf16, [row][head][d] (gate_o_bwd_a16): no copy
   a.qb = (__bf16*)q; a.kb = (__bf16*)k; a.vb = (__bf16*)v;  // read only
   a.rsb_qkv = ld_qkv;
-  a.zrow = ozrow;
+  a.zrow = (__bf16*)zrow;
   a.total_rows = (int64_t)B * N;
-  ConvSet cs{{dout, nullptr, nullptr, nullptr}, {ld_dout, 0, 0, 0}, {a.ob, nullptr, nullptr, nullptr},
-             ozrow, offsets, B, H, d, nch};
-  if (launch_convert(cs, 1, a.total_rows, st)) return -1;
   const int nb32 = ceil_div(N, 32);
   a.nbt = nb32 * (nb32 + 1) / 2;
   a.inv_n = 1.0f / (float)N;

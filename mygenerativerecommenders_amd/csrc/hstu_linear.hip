@@ -899,7 +899,7 @@ struct OpGateOBwdT : NoStats {
   const int64_t* seed_off;
   act_t<A16>* du;
   int64_t lddu;
-  float* da;
+  act_t<A16>* da;  // A16: d_attn in bf16 -- the attention backward's dO, DMA-staged as is
   int64_t ldda;
   const __bf16* w16 = nullptr;  // A16: W_o^T as bf16, (hdv, D)
   static constexpr int NSRC = 1;
@@ -964,9 +964,9 @@ struct OpGateOBwdT : NoStats {
     }
   }
   // bf16 layout: u / h_u read as the 4-byte bf16 pair holding the lane's column (a lane
-  // pair reads the same word), du written as packed pairs: rows r - 1, r (r odd) are
-  // stored together, the even lane taking row r - 1 and the odd lane row r (one DPP swap
-  // per column tile).  Same values as the fp32 layout, rounded to bf16.
+  // pair reads the same word), du and d_attn written as packed pairs: rows r - 1, r (r odd)
+  // are stored together, the even lane taking row r - 1 and the odd lane row r (one DPP
+  // swap per column tile).  Same values as the fp32 layout, rounded to bf16.
   template <int NT>
   __device__ void epilogue16(f4 (&acc)[NT], int64_t mrow, int ncol, int64_t total) const {
     const bool odd = (threadIdx.x & 1) != 0;
@@ -977,9 +977,9 @@ struct OpGateOBwdT : NoStats {
     const uint32_t* __restrict__ h32 = reinterpret_cast<const uint32_t*>(h_u);
     const float* __restrict__ ap = attn;
     uint32_t* __restrict__ du32 = reinterpret_cast<uint32_t*>(du);
-    float* __restrict__ dap = da;
+    uint32_t* __restrict__ da32 = reinterpret_cast<uint32_t*>(da);
     const uint64_t sd = seed + (seed_off ? (uint64_t)*seed_off : 0ull);
-    float keep[NT];
+    float keep[NT], keepa[NT];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int64_t m = mrow + r;
@@ -1035,11 +1035,21 @@ struct OpGateOBwdT : NoStats {
       s2 = sum16(s2);
       const float inv = 1.f / (float)N;
       const float mean1 = s1 * inv, mean2 = s2 * inv;
-      if (!row_ok) continue;
+      float dav[NT];
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        const int n = ncol + 16 * t;
-        if (n < N) dap[m * ldda + n] = st.y * (dln[t] - mean1 - lnv[t] * mean2);
+      for (int t = 0; t < NT; ++t) dav[t] = st.y * (dln[t] - mean1 - lnv[t] * mean2);
+      if (r & 1) {
+        const int64_t ms = odd ? m : m - 1;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const float rx = dpp_mov<0xB1>(odd ? keepa[t] : dav[t]);
+          const float lo = odd ? rx : keepa[t], hi = odd ? dav[t] : rx;
+          const int n = cb + 16 * t;
+          if (ms < total && n < N) da32[(ms * ldda + n) >> 1] = pack_bf16(lo, hi);
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) keepa[t] = dav[t];
       }
     }
   }

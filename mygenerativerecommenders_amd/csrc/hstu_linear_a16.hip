@@ -127,13 +127,14 @@ extern "C" int hstu_gate_o_bwd_a16(const float* dy, int64_t ld_dy, const int64_t
                                    const uint16_t* u, int64_t ld_u, const float* attn, int64_t ld_attn,
                                    const float* attn_stats, const uint16_t* h_u, int64_t ld_h,
                                    float dropout_p, uint64_t seed, const int64_t* seed_offset,
-                                   uint16_t* du, int64_t ld_du, float* d_attn, int64_t ld_da,
+                                   uint16_t* du, int64_t ld_du, uint16_t* d_attn, int64_t ld_da,
                                    void* stream) {
   GR_REQUIRE(dy && offsets && u && attn && attn_stats && du && d_attn,
              "hstu_gate_o_bwd_a16: null pointer");
   GR_REQUIRE(hdv > 0 && D > 0 && B >= 0, "hstu_gate_o_bwd_a16: bad sizes");
-  GR_REQUIRE(hdv % 2 == 0 && ld_u % 2 == 0 && ld_h % 2 == 0 && ld_du % 2 == 0 &&
-                 (uintptr_t)u % 4 == 0 && (uintptr_t)h_u % 4 == 0 && (uintptr_t)du % 4 == 0,
+  GR_REQUIRE(hdv % 2 == 0 && ld_u % 2 == 0 && ld_h % 2 == 0 && ld_du % 2 == 0 && ld_da % 2 == 0 &&
+                 (uintptr_t)u % 4 == 0 && (uintptr_t)h_u % 4 == 0 && (uintptr_t)du % 4 == 0 &&
+                 (uintptr_t)d_attn % 4 == 0,
              "hstu_gate_o_bwd_a16: bf16 rows must be 4-byte aligned with even widths and strides");
   GR_REQUIRE(img_ok(wt_o16, hdv, D),
              "hstu_gate_o_bwd_a16: wt_o16 must be the 16-byte aligned (hdv, D) bf16 image, D %% 8 == 0");
@@ -143,7 +144,7 @@ extern "C" int hstu_gate_o_bwd_a16(const float* dy, int64_t ld_dy, const int64_t
   op.u = (const __bf16*)u; op.ldu = ld_u; op.attn = attn; op.lda = ld_attn;
   op.a_stats = (const float2*)attn_stats; op.h_u = (const __bf16*)h_u; op.ldh = ld_h;
   op.p = dropout_p; op.seed = seed; op.seed_off = seed_offset; op.du = (__bf16*)du; op.lddu = ld_du;
-  op.da = d_attn; op.ldda = ld_da;
+  op.da = (__bf16*)d_attn; op.ldda = ld_da;
   const bool vec = (uintptr_t)dy % 16 == 0 && ld_dy % 4 == 0;
   return launch_rowpanel_bf16(op, max_rows, true, "hstu_gate_o_bwd", (hipStream_t)stream, vec);
 }

@@ -352,7 +352,8 @@ def _pad_cat_weight(w_o: torch.Tensor, hv: int):
 
 
 def _stu_forward(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGeometry, seed: int,
-                 seed_offset, grad_on: bool, needs_w_grad: bool, pre=None, next_w_uvqk=None):
+                 seed_offset, grad_on: bool, needs_w_grad: bool, pre=None, next_w_uvqk=None,
+                 images=None):
     """One STU layer forward (hstu.py:266-413): 3 launches.  Returns (y, saved, pre_next)
     with the tensors its backward needs (``_stu_backward``).
     Layer boundaries (``_fuse_boundaries``): ``pre`` = (x_stats, uvqk, h_pre) of this layer
@@ -373,7 +374,8 @@ def _stu_forward(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGeomet
     sfx = "_bf16" if geo.bf16 else ""  # bf16 MFMA operands in the projections too
     if geo.a16:
         return _stu_forward_a16(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo, seed,
-                                seed_offset, grad_on, needs_w_grad, pre, next_w_uvqk is not None)
+                                seed_offset, grad_on, needs_w_grad, pre, next_w_uvqk is not None,
+                                images)
     if pre is not None:
         x_stats, uvqk, h_pre = pre
     else:
@@ -476,20 +478,33 @@ def weight_images_bf16(specs):
         o = torch.empty((C, R) if tr else (R, C), dtype=torch.bfloat16, device=w.device)
         outs.append(o)
         rows.append((w.data_ptr(), R, C, 1 if tr else 0, o.data_ptr()))
-    desc = np.ascontiguousarray(np.array(rows, dtype=np.int64))
-    _lib.call("gr_weight_images_bf16", desc.ctypes.data, len(rows), _stream())
+    for c0 in range(0, len(rows), 32):  # up to 32 images per launch
+        desc = np.ascontiguousarray(np.array(rows[c0:c0 + 32], dtype=np.int64))
+        _lib.call("gr_weight_images_bf16", desc.ctypes.data, len(desc), _stream())
     return outs
 
 
+def _a16_images(w_uvqk, w_o, grad_on: bool):
+    """A layer's weight images: forward (W_uvqk^T, W_o) and, for the backward, (W_o^T,
+    W_uvqk) -- the specs of weight_images_bf16."""
+    specs = [(w_uvqk, True), (w_o, False)]
+    if grad_on:
+        specs += [(w_o, True), (w_uvqk, False)]
+    return specs
+
+
 def _stu_forward_a16(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGeometry, seed: int,
-                     seed_offset, grad_on: bool, needs_w_grad: bool, pre=None, has_next=False):
+                     seed_offset, grad_on: bool, needs_w_grad: bool, pre=None, has_next=False,
+                     images=None):
     """One STU layer forward with bf16 activations (ABI 16): LN + UVQK writes bf16 uvqk /
     h_pre (and the weight gradient's bf16 LN(x)), the attention DMAs Q / K / V from the
     bf16 uvqk rows, gate_o reads bf16 u and writes bf16 o_in.  The saved tuple's last
     slot holds xn (the fp32 path keeps its bf16 copies there).
     ``pre``: this layer's x_stats, computed by the previous layer's gate_o epilogue (the
     LN statistics pass is skipped); ``has_next``: compute the next layer's x_stats in this
-    layer's gate_o epilogue (returned as the third value)."""
+    layer's gate_o epilogue (returned as the third value).  ``images``: the layer's bf16
+    weight images (``_a16_images``; made here when None); the backward's two are saved in
+    the tuple's weight slots."""
     dev = x.device
     rows, D = x.shape
     B = offsets.numel() - 1
@@ -501,7 +516,10 @@ def _stu_forward_a16(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGe
     w_uvqk = w_uvqk.contiguous()
     w_o = w_o.contiguous()
     needs_w_grad = grad_on and needs_w_grad
-    wt_uvqk, w_o16 = weight_images_bf16([(w_uvqk, True), (w_o, False)])
+    if images is None:
+        images = weight_images_bf16(_a16_images(w_uvqk, w_o, grad_on))
+    wt_uvqk, w_o16 = images[0], images[1]
+    wt_o16, w_uvqk16 = (images[2], images[3]) if grad_on else (None, None)
     stats_given = pre is not None
     x_stats = pre if stats_given else torch.empty(rows, 2, dtype=torch.float32, device=dev)
     uvqk = torch.empty(rows, n_out, dtype=torch.bfloat16, device=dev)
@@ -528,7 +546,7 @@ def _stu_forward_a16(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGe
               offsets.data_ptr(), B, rows, hv, D, w_o16.data_ptr(), b_o_c.data_ptr(), x.data_ptr(),
               x.stride(0), geo.eps, geo.dropout_p, seed, _lib.ptr(seed_offset),
               attn_stats.data_ptr(), _lib.ptr(o_in), y.data_ptr(), D, _lib.ptr(y_stats), st)
-    saved = (x, offsets, bmap, w_uvqk, w_o, pos_w_c, ts_w_c, x_stats, uvqk, h_pre, attn,
+    saved = (x, offsets, bmap, w_uvqk16, wt_o16, pos_w_c, ts_w_c, x_stats, uvqk, h_pre, attn,
              attn_stats, o_in, xn)
     return y, saved, y_stats
 
@@ -538,8 +556,8 @@ def _stu_backward_a16(saved, dy, geo: STUGeometry, seed: int, seed_offset, want_
     """The backward of ``_stu_forward_a16``: gate_o_bwd writes bf16 du into a bf16 d_uvqk,
     the attention backward its bf16 dq / dk / dv, ln_uvqk_bwd reads it, and the weight
     gradients take bf16 LN(x), d_uvqk and o_in (gr_wgrad_multi_a16)."""
-    (x, offsets, bmap, w_uvqk, w_o, pos_w, ts_w, x_stats, uvqk, h_pre, attn, attn_stats,
-     o_in, xn) = saved
+    (x, offsets, bmap, w_uvqk16, wt_o16, pos_w, ts_w, x_stats, uvqk, h_pre, attn, attn_stats,
+     o_in, xn) = saved  # the weight slots hold the backward's bf16 images
     dev = x.device
     rows, D = x.shape
     B = offsets.numel() - 1
@@ -548,9 +566,8 @@ def _stu_backward_a16(saved, dy, geo: STUGeometry, seed: int, seed_offset, want_
     n_out = geo.n_out
     st = _stream()
     dy = dy.contiguous()
-    wt_o16, w_uvqk16 = weight_images_bf16([(w_o, True), (w_uvqk, False)])
     d_uvqk = torch.empty(rows, n_out, dtype=torch.bfloat16, device=dev)
-    d_attn = torch.empty(rows, hv, dtype=torch.float32, device=dev)
+    d_attn = torch.empty(rows, hv, dtype=torch.bfloat16, device=dev)
     _lib.call("hstu_gate_o_bwd_a16", dy.data_ptr(), D, offsets.data_ptr(), B, rows, hv, D,
               wt_o16.data_ptr(), uvqk.data_ptr(), n_out, attn.data_ptr(), hv, attn_stats.data_ptr(),
               _lib.ptr(h_pre), n_out, geo.dropout_p, seed, _lib.ptr(seed_offset),
@@ -568,7 +585,7 @@ def _stu_backward_a16(saved, dy, geo: STUGeometry, seed: int, seed_offset, want_
               geo.max_len, H, d, _lib.ptr(bmap), _lib.ptr(pos_w), _lib.ptr(ts_w), NUM_BUCKETS,
               hp(2 * hv), hp(3 * hv), hp(hv), n_out, d_uvqk[:, 2 * hv:].data_ptr(),
               d_uvqk[:, 3 * hv:].data_ptr(), d_uvqk[:, hv:].data_ptr(), n_out,
-              _lib.ptr(d_pos_w), _lib.ptr(d_ts_w), ws.data_ptr(), ws_n, st)
+              _lib.ptr(d_pos_w), _lib.ptr(d_ts_w), _zero_row(dev).data_ptr(), ws.data_ptr(), ws_n, st)
     dx = torch.empty(rows, D, dtype=torch.float32, device=dev)
     _lib.call("hstu_ln_uvqk_bwd_a16", d_uvqk.data_ptr(), n_out, offsets.data_ptr(), B, rows, D,
               n_out, w_uvqk16.data_ptr(), x.data_ptr(), x.stride(0), x_stats.data_ptr(),
@@ -860,6 +877,13 @@ class STUStackFunction(torch.autograd.Function):
         saved_all = []
         fuse = _fuse_boundaries(geo)
         pre = None
+        images = [None] * n_layers
+        if geo.a16:  # every layer's bf16 weight images in one launch per 8 layers
+            specs = [sp for l in range(n_layers)
+                     for sp in _a16_images(params[5 * l], params[5 * l + 1], grad_on)]
+            flat = weight_images_bf16(specs)
+            per = len(specs) // n_layers
+            images = [flat[per * l:per * (l + 1)] for l in range(n_layers)]
         for l in range(n_layers):
             w_uvqk, w_o, b_o, pos_w, ts_w = params[5 * l:5 * l + 5]
             # the next layer's _uvqk: the fp32 layer boundary (fuse) or, in the bf16
@@ -867,7 +891,8 @@ class STUStackFunction(torch.autograd.Function):
             nxt = params[5 * (l + 1)] if (fuse or geo.a16) and l + 1 < n_layers else None
             x, saved, pre = _stu_forward(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo,
                                          seeds[l], seed_offset, grad_on,
-                                         w_o.requires_grad or b_o.requires_grad, pre, nxt)
+                                         w_o.requires_grad or b_o.requires_grad, pre, nxt,
+                                         images[l])
             if grad_on:
                 saved_all.extend(saved)
         if grad_on:

@@ -138,7 +138,8 @@ def test_attn_a16_bitexact(d, H, lengths, N):
     _eq(o16, o32, "attn out")
     # backward
     g = torch.Generator(device="cuda").manual_seed(7)
-    dout = torch.randn(total, hv, device=DEV, generator=g)
+    dout16 = _bf(torch.randn(total, hv, device=DEV, generator=g))
+    dout = dout16.float()
     ws_n = L.hstu_attn_bwd_bf16_workspace_size_copies(B, N, max_len, H, d, d, 128)
     ws = torch.empty(ws_n, dtype=torch.uint8, device=DEV)
     d32 = torch.full((total + 5, n_out), float("nan"), device=DEV)
@@ -151,17 +152,17 @@ def test_attn_a16_bitexact(d, H, lengths, N):
               d32[:, 2 * hv:].data_ptr(), d32[:, 3 * hv:].data_ptr(), d32[:, hv:].data_ptr(), n_out,
               dp32.data_ptr(), dt32.data_ptr(), cp.data_ptr(), ws.data_ptr(), ws_n, st)
     ws_a = L.hstu_attn_bwd_a16_workspace_size(B, N, max_len, H, d, 128)
-    assert ws_a == ws_n
+    assert 0 < ws_a < ws_n
     wsa = torch.empty(ws_a, dtype=torch.uint8, device=DEV)
     d16 = torch.zeros(total + 5, n_out, dtype=torch.bfloat16, device=DEV)
     dp = torch.empty(2 * N - 1, device=DEV)
     dt = torch.empty(129, device=DEV)
     _lib.call("hstu_attn_bwd_a16", u16[:, 2 * hv:].data_ptr(), u16[:, 3 * hv:].data_ptr(),
-              u16[:, hv:].data_ptr(), n_out, dout.data_ptr(), hv, offs.data_ptr(), B, N, max_len,
+              u16[:, hv:].data_ptr(), n_out, dout16.data_ptr(), hv, offs.data_ptr(), B, N, max_len,
               H, d, bmap.data_ptr(), pos_w.data_ptr(), ts_w.data_ptr(), 128,
               h16[:, 2 * hv:].data_ptr(), h16[:, 3 * hv:].data_ptr(), h16[:, hv:].data_ptr(), n_out,
               d16[:, 2 * hv:].data_ptr(), d16[:, 3 * hv:].data_ptr(), d16[:, hv:].data_ptr(), n_out,
-              dp.data_ptr(), dt.data_ptr(), wsa.data_ptr(), ws_a, st)
+              dp.data_ptr(), dt.data_ptr(), ops._zero_row(DEV).data_ptr(), wsa.data_ptr(), ws_a, st)
     torch.cuda.synchronize()
     _eq(d16[:total, hv:], _bf(d32[:total, hv:]), "dq / dk / dv")
     _eq(dp, dp32, "d pos_w")
@@ -208,7 +209,7 @@ def test_gate_o_a16_bitexact(D, hv):
             _eq(ys[:total], xs[:total], "y_stats = LN statistics of y")
         dy = torch.randn(cap, D, device=DEV, generator=torch.Generator(device="cuda").manual_seed(3))
         du = torch.empty(cap, n_out, dtype=torch.bfloat16 if a16 else torch.float32, device=DEV)
-        da = torch.empty(cap, hv, device=DEV)
+        da = torch.empty(cap, hv, dtype=torch.bfloat16 if a16 else torch.float32, device=DEV)
         h = h16 if a16 else h32
         _lib.call("hstu_gate_o_bwd_a16" if a16 else "hstu_gate_o_bwd_bf16", dy.data_ptr(), D,
                   offs.data_ptr(), B, cap, hv, D, (wt_o16 if a16 else w_o).data_ptr(), u.data_ptr(), n_out,
@@ -222,7 +223,7 @@ def test_gate_o_a16_bitexact(D, hv):
     _eq(y[:n], y32[:n], "y")
     _eq(oin[:n], _bf(oin32[:n]), "o_in")
     _eq(du[:n, :hv], _bf(du32[:n, :hv]), "du")
-    _eq(da[:n], da32[:n], "d_attn")
+    _eq(da[:n], _bf(da32[:n]), "d_attn")
 
 
 @pytest.mark.parametrize("D,n_out", [(256, 1024), (192, 768)])
