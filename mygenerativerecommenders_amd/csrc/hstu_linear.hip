@@ -875,6 +875,12 @@ struct OpGateOT {
 };
 using OpGateO = OpGateOT<false>;
 
+// LayerNorm backward of one element: rstd * (dln - mean(dln) - ln * mean(dln * ln)), with
+// the contraction spelled out so every epilogue rounds it the same way
+__device__ __forceinline__ float ln_bwd_val(float rstd, float dln, float mean1, float ln, float mean2) {
+  return rstd * __builtin_fmaf(-ln, mean2, dln - mean1);
+}
+
 // B1: g = dy @ W_o (rows, hdv); epilogue: dropout bwd, du = g*LN(a) (*silu'(h_u)),
 //     d_attn = LayerNorm_bwd(g * u).  Needs the whole hdv row in one panel.
 template <bool A16>
@@ -959,14 +965,15 @@ struct OpGateOBwdT : NoStats {
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         const int n = ncol + 16 * t;
-        if (n < N) da[m * ldda + n] = st.y * (dln[t] - mean1 - lnv[t] * mean2);
+        if (n < N) da[m * ldda + n] = ln_bwd_val(st.y, dln[t], mean1, lnv[t], mean2);
       }
     }
   }
   // bf16 layout: u / h_u read as the 4-byte bf16 pair holding the lane's column (a lane
-  // pair reads the same word), du and d_attn written as packed pairs: rows r - 1, r (r odd)
-  // are stored together, the even lane taking row r - 1 and the odd lane row r (one DPP
-  // swap per column tile).  Same values as the fp32 layout, rounded to bf16.
+  // pair reads the same word); du and d_attn written as packed pairs per row: the even
+  // lane of a pair takes its partner's value by one DPP swap and stores both columns (no
+  // values held across rows: two waves per SIMD).  Same values as the fp32 layout,
+  // rounded to bf16 (d_attn through ln_bwd_val, the fp32 epilogue's formula).
   template <int NT>
   __device__ void epilogue16(f4 (&acc)[NT], int64_t mrow, int ncol, int64_t total) const {
     const bool odd = (threadIdx.x & 1) != 0;
@@ -979,7 +986,6 @@ struct OpGateOBwdT : NoStats {
     uint32_t* __restrict__ du32 = reinterpret_cast<uint32_t*>(du);
     uint32_t* __restrict__ da32 = reinterpret_cast<uint32_t*>(da);
     const uint64_t sd = seed + (seed_off ? (uint64_t)*seed_off : 0ull);
-    float keep[NT], keepa[NT];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int64_t m = mrow + r;
@@ -1003,7 +1009,7 @@ struct OpGateOBwdT : NoStats {
         }
       }
       float s1 = 0.f, s2 = 0.f;
-      float lnv[NT], dln[NT], ddv[NT];
+      float lnv[NT], dln[NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         const int n = ncol + 16 * t;
@@ -1012,44 +1018,22 @@ struct OpGateOBwdT : NoStats {
         const float ln = (av[t] - st.x) * st.y;
         float dd = g * ln;
         if (h_u) dd *= silu_grad_(hv[t]);
-        ddv[t] = dd;
+        const float other = dpp_mov<0xB1>(dd);  // the partner's column
+        if (!odd && ok) du32[(m * lddu + cb + 16 * t) >> 1] = pack_bf16(dd, other);
         lnv[t] = ok ? ln : 0.f;
         dln[t] = ok ? g * uv[t] : 0.f;
         s1 += dln[t];
         s2 += dln[t] * lnv[t];
       }
-      if (r & 1) {  // rows r - 1 (even lane) and r (odd lane) as packed pairs
-        const int64_t ms = odd ? m : m - 1;
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-          const float rx = dpp_mov<0xB1>(odd ? keep[t] : ddv[t]);
-          const float lo = odd ? rx : keep[t], hi = odd ? ddv[t] : rx;
-          const int n = cb + 16 * t;
-          if (ms < total && n < N) du32[(ms * lddu + n) >> 1] = pack_bf16(lo, hi);
-        }
-      } else {
-#pragma unroll
-        for (int t = 0; t < NT; ++t) keep[t] = ddv[t];
-      }
       s1 = sum16(s1);
       s2 = sum16(s2);
       const float inv = 1.f / (float)N;
       const float mean1 = s1 * inv, mean2 = s2 * inv;
-      float dav[NT];
 #pragma unroll
-      for (int t = 0; t < NT; ++t) dav[t] = st.y * (dln[t] - mean1 - lnv[t] * mean2);
-      if (r & 1) {
-        const int64_t ms = odd ? m : m - 1;
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-          const float rx = dpp_mov<0xB1>(odd ? keepa[t] : dav[t]);
-          const float lo = odd ? rx : keepa[t], hi = odd ? dav[t] : rx;
-          const int n = cb + 16 * t;
-          if (ms < total && n < N) da32[(ms * ldda + n) >> 1] = pack_bf16(lo, hi);
-        }
-      } else {
-#pragma unroll
-        for (int t = 0; t < NT; ++t) keepa[t] = dav[t];
+      for (int t = 0; t < NT; ++t) {
+        const float dav = ln_bwd_val(st.y, dln[t], mean1, lnv[t], mean2);
+        const float other = dpp_mov<0xB1>(dav);
+        if (!odd && row_ok && cb + 16 * t < N) da32[(m * ldda + cb + 16 * t) >> 1] = pack_bf16(dav, other);
       }
     }
   }
