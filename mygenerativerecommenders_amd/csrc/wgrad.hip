@@ -60,6 +60,7 @@ struct WgradArgs {
   int B;
   int64_t rows_per_split;
   int n_splits;
+  int blkf0[WG_MAXP + 1];  // prefix of 256-output blocks (wgrad_reduce_few_kernel)
 };
 
 // problem owning item x of a prefix table (scalar: kernel arguments are wave-uniform)
@@ -744,6 +745,29 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(WgradArgs g) {
   }
 }
 
+// n_splits <= 16 (the wide plans): one thread per output, the splits summed in order --
+// the same additions in the same order as wgrad_reduce_kernel (whose 16 groups then hold
+// one split each, added in group order), without its 16-output workgroups (C3: 2.6 M
+// outputs x 8 splits took 154 us per step as 164 K workgroups).
+__global__ __launch_bounds__(256) void wgrad_reduce_few_kernel(WgradArgs g) {
+  const int pi = wg_find(g.blkf0, g.np, blockIdx.x);
+  const WgradProb& p = g.p[pi];
+  const int64_t ne = (int64_t)p.Ka * p.NC;
+  const int64_t i = (int64_t)(blockIdx.x - g.blkf0[pi]) * 256 + threadIdx.x;
+  if (i >= ne) return;
+  gptr<float> src = as_global(p.slabs);
+  const int n = g.n_splits;
+  float v[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) v[j] = src[(int64_t)(j < n ? j : 0) * ne + i];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) s += j < n ? v[j] : 0.f;
+  const int ka = (int)(i / p.NC), nb = (int)(i - (int64_t)ka * p.NC);
+  if (nb < p.Nb) p.c[(int64_t)ka * p.Nb + nb] = s;
+  else if (p.colsum) p.colsum[ka] = s;
+}
+
 static int wgrad_nt(int nc) {
   const int nt = ceil_div(nc, 16);
   if (nt <= 4) return 4;
@@ -984,7 +1008,14 @@ static int wgrad_run(const WgradProb* in, int np, const int64_t* offsets, int B,
     }
     GR_LAUNCH_CHECK("gr_wgrad(partial)");
   }
-  GR_TIMED("wgrad_reduce", st, hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(g.blk0[np]), dim3(256), 0, st, g));
+  if (g.n_splits <= 16) {
+    g.blkf0[0] = 0;
+    for (int i = 0; i < np; ++i)
+      g.blkf0[i + 1] = g.blkf0[i] + (g.p[i].panels ? (int)(((int64_t)Ka[i] * g.p[i].NC + 255) / 256) : 0);
+    GR_TIMED("wgrad_reduce", st, hipLaunchKernelGGL(wgrad_reduce_few_kernel, dim3(g.blkf0[np]), dim3(256), 0, st, g));
+  } else {
+    GR_TIMED("wgrad_reduce", st, hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(g.blk0[np]), dim3(256), 0, st, g));
+  }
   GR_LAUNCH_CHECK("gr_wgrad(reduce)");
   return 0;
 }
