@@ -495,6 +495,7 @@ __global__ __launch_bounds__(256) void rowpanel_bf16v_kernel(Op op) {
   // A0 in bf16 (Op::A0_BYTES == 2, an identity a_xform): the 4 k-values are one 8-byte load
   // whose bits go to LDS unchanged
   constexpr bool A0H = Op::A0_BYTES == 2;
+  static_assert(!A0H || Op::A0_RAW, "bf16 A0 rows go to LDS untransformed");
   const int va0 = (ar * ld0 + 4 * aq) * Op::A0_BYTES, va1 = (ar * ld1 + 4 * aq) * 4;
   const __amdgpu_buffer_rsrc_t rw =
       __builtin_amdgcn_make_buffer_rsrc((void*)op.w, 0, op.K * op.N * 4, 0x00020000);
@@ -661,6 +662,7 @@ struct OpLnUvqkT {
   static constexpr bool B_N_CONTIG = true;
   static constexpr int A0_BYTES = 4;
   static constexpr bool B16 = A16;  // the weight as a bf16 [N][K] image (w16)
+  static constexpr bool A0_RAW = false;  // a_xform is the identity on A0 (bf16v's raw bf16 path)
   const int64_t* offsets;
   int B, K, N;
   const float* x;
@@ -756,6 +758,7 @@ struct OpGateOT {
   static constexpr bool B_N_CONTIG = false;
   static constexpr int A0_BYTES = A16 ? 2 : 4;  // u
   static constexpr bool B16 = A16;  // the weight as a bf16 [N][K] image (w16)
+  static constexpr bool A0_RAW = false;  // a_xform is the identity on A0 (bf16v's raw bf16 path)
   const int64_t* offsets;
   int B, K, N;  // K = hdv, N = D
   const act_t<A16>* u;
@@ -888,6 +891,7 @@ struct OpGateOBwdT : NoStats {
   static constexpr bool B_N_CONTIG = true;
   static constexpr int A0_BYTES = 4;  // dy
   static constexpr bool B16 = A16;  // the weight as a bf16 [N][K] image (w16)
+  static constexpr bool A0_RAW = false;  // a_xform is the identity on A0 (bf16v's raw bf16 path)
   const int64_t* offsets;
   int B, K, N;  // K = D, N = hdv
   const float* dy;
@@ -1046,6 +1050,7 @@ struct OpLnUvqkBwdT : NoStats {
   static constexpr bool B_N_CONTIG = false;
   static constexpr int A0_BYTES = A16 ? 2 : 4;  // dh
   static constexpr bool B16 = A16;  // the weight as a bf16 [N][K] image (w16)
+  static constexpr bool A0_RAW = A16;  // a_xform is the identity on A0 (bf16v's raw bf16 path)
   const int64_t* offsets;
   int B, K, N;  // K = n_out (4hd), N = D
   const act_t<A16>* dh;
@@ -1204,6 +1209,7 @@ static int launch_rowpanel_bf16(const Op& op, int64_t max_rows, bool full_row, c
   dim3 grid((unsigned)((max_rows + BM - 1) / BM), (unsigned)panels);
   if (grid.x == 0) return 0;
   const char* tname = name + 5;
+  if constexpr (Op::A0_BYTES == 2 && !Op::A0_RAW) vec = false;  // bf16 A0 with a transform
   if (vec && option(GR_OPT_PANEL_VEC) != 0 && nt == 16 && op.K % 32 == 0 &&
       (!Op::B_N_CONTIG || op.N % 4 == 0) && (int64_t)op.K * op.N * 4 <= 0x7fffffffLL) {
     GR_TIMED(tname, st, hipLaunchKernelGGL((rowpanel_bf16v_kernel<Op>), grid, dim3(256), 0, st, op));

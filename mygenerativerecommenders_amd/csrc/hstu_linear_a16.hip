@@ -99,7 +99,9 @@ extern "C" int hstu_ln_uvqk_fwd_a16(const float* x, int64_t ld_x, const int64_t*
   OpLnUvqkT<true> op{offsets, B, D, n_out, x, ld_x, nullptr, eps, activation, (float2*)x_stats,
                      (__bf16*)h_pre, (__bf16*)uvqk, ld_out, (__bf16*)xn, stats_given != 0,
                      (const __bf16*)wt_uvqk};
-  return launch_rowpanel_bf16(op, max_rows, false, "hstu_ln_uvqk_fwd", (hipStream_t)stream);
+  // GR_OPT_PANEL_VEC = 2: the float4-staged panel for this forward too (A/B)
+  return launch_rowpanel_bf16(op, max_rows, false, "hstu_ln_uvqk_fwd", (hipStream_t)stream,
+                              option(GR_OPT_PANEL_VEC) == 2 && (uintptr_t)x % 16 == 0 && ld_x % 4 == 0);
 }
 
 extern "C" int hstu_gate_o_fwd_a16(const uint16_t* u, int64_t ld_u, const float* attn, int64_t ld_attn,

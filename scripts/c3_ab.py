@@ -20,11 +20,13 @@ def main():
     ap.add_argument("--only", default="")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
-    modes = [("a16", True), ("f32act", False)]
-    for name, a16 in modes:
+    from mygenerativerecommenders_amd import _lib
+    modes = [("a16", True, 1), ("a16_vec2", True, 2), ("f32act", False, 1)]
+    for name, a16, pv in modes:
         if args.only and args.only != name:
             continue
         ops.A16 = a16
+        _lib.set_option("PANEL_VEC", pv)
         r = bench.encoder_leg(32, 2048, 11, 256, 8, 1, args.steps, 2, dev, 1, 3000,
                               instrument=True, muon=True, bf16=True)
         kps = {k: round(v, 4) for k, v in sorted(r["kernel_per_step_ms"].items(), key=lambda kv: -kv[1])}
