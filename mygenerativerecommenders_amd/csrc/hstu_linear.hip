@@ -1209,12 +1209,13 @@ static int launch_rowpanel_bf16(const Op& op, int64_t max_rows, bool full_row, c
   dim3 grid((unsigned)((max_rows + BM - 1) / BM), (unsigned)panels);
   if (grid.x == 0) return 0;
   const char* tname = name + 5;
-  if constexpr (Op::A0_BYTES == 2 && !Op::A0_RAW) vec = false;  // bf16 A0 with a transform
-  if (vec && option(GR_OPT_PANEL_VEC) != 0 && nt == 16 && op.K % 32 == 0 &&
-      (!Op::B_N_CONTIG || op.N % 4 == 0) && (int64_t)op.K * op.N * 4 <= 0x7fffffffLL) {
-    GR_TIMED(tname, st, hipLaunchKernelGGL((rowpanel_bf16v_kernel<Op>), grid, dim3(256), 0, st, op));
-    GR_LAUNCH_CHECK(name);
-    return 0;
+  if constexpr (Op::A0_BYTES == 4 || Op::A0_RAW) {  // bf16 A0 rows with a transform: scalar panel
+    if (vec && option(GR_OPT_PANEL_VEC) != 0 && nt == 16 && op.K % 32 == 0 &&
+        (!Op::B_N_CONTIG || op.N % 4 == 0) && (int64_t)op.K * op.N * 4 <= 0x7fffffffLL) {
+      GR_TIMED(tname, st, hipLaunchKernelGGL((rowpanel_bf16v_kernel<Op>), grid, dim3(256), 0, st, op));
+      GR_LAUNCH_CHECK(name);
+      return 0;
+    }
   }
 #define GR_NT_CASE(NT_)                                                                      \
   case NT_:                                                                                  \
