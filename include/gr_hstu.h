@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GR_HSTU_ABI_VERSION 16
+#define GR_HSTU_ABI_VERSION 17
 
 #ifndef GR_API
 #define GR_API __attribute__((visibility("default")))
@@ -44,7 +44,7 @@ GR_API int gr_version(void);
  * (attention + layer boundary), attn_fwd_bnd1 (+ gate_o of the last layer), attn_bwd_dq_bnd
  * (dQ + layer boundary), attn_bwd_dq_bnd1 (+ ln_uvqk_bwd of the first layer),
  * attn_bias_reduce, ln_uvqk_fwd, gate_o_fwd, gate_o_bwd, ln_uvqk_bwd, wgrad_partial,
- * wgrad_reduce, mips_pack, mips_select, mips_merge, cumsum, dense_to_jagged,
+ * wgrad_reduce, mips_pack, mips_select, mips_merge, cumsum, dense_to_jagged, encoder_prologue,
  * jagged_to_padded, l2_normalize, current_embeddings, sampled_softmax_fwd,
  * sampled_softmax_bwd, sampled_softmax_csr, sampled_softmax_table_grad, preproc.  Not for use inside a captured graph.
  */
@@ -92,9 +92,11 @@ GR_API int gr_timing_reset(void);
  *   GR_OPT_WGRAD_ROWS         >=0  f32 / bf16 weight gradients (64-wide panels): rows per
  *                                  split (0 = chosen from the row count; rounded up to 64).
  *                                  The workspace size (gr_wgrad*_workspace_size) depends on it.
- *   GR_OPT_PANEL_VEC          0|1  bf16 backward projection GEMMs at K % 32 == 0 with
+ *   GR_OPT_PANEL_VEC        0|1|2  bf16 backward projection GEMMs at K % 32 == 0 with
  *                                  16-byte aligned rows and 256-column panels: float4
- *                                  operand staging (default 1) or the scalar-staged row panel
+ *                                  operand staging (default 1) or the scalar-staged row panel;
+ *                                  2 also routes hstu_ln_uvqk_fwd_a16 to the float4-staged
+ *                                  panel (A/B only: C3 1.090 vs 1.093 ms per step)
  *   GR_OPT_ATTN_BWD_WIDE_DS   0|1  f32 attention backward at wide heads (dqk or dv > 128): the
  *                                  dK/dV pass stores dS tiles and dQ = dS K runs in a second
  *                                  launch without recomputing S / dP (default 1), or 0 = the
@@ -259,6 +261,21 @@ GR_API int gr_sampled_softmax_bwd(const float* out, int64_t ld_out, const float*
 GR_API size_t hstu_bucket_map_bytes(int B, int N);
 GR_API int hstu_bucket_map(const int64_t* ts, const int64_t* offsets, int B, int N,
                     const int64_t* bucket_thr, int num_buckets, uint8_t* map, void* stream);
+
+/* hstu_encoder_prologue (ABI 17): the batch setup of an encoder forward in one launch
+ * (HSTU.forward, hstu.py:502 + utils/ops.py:18-64, and the bucket map above):
+ *   offsets = gr_complete_cumsum(lengths)                       (B + 1 entries)
+ *   x_jagged = gr_dense_to_jagged(x, offsets, B, N, D, max_rows, zero_fill = 0)
+ *   map = hstu_bucket_map(ts, offsets, B, N, ...)               (skipped when map is NULL)
+ *   *step += 1                                                  (skipped when step is NULL)
+ * with results identical to those calls (tests/test_gpu_jagged.py).  x (B, N, D) f32,
+ * ts (B, N) int64; lengths are not bounded by N (rows past N are not copied, as
+ * gr_dense_to_jagged).  No workgroup waits on another: each copy workgroup sums the
+ * lengths before its sequence itself. */
+GR_API int hstu_encoder_prologue(const int64_t* lengths, int B, int N, const float* x, int D,
+                                 int64_t max_rows, const int64_t* ts, const int64_t* bucket_thr,
+                                 int num_buckets, int64_t* offsets, float* x_jagged,
+                                 uint8_t* map, int64_t* step, void* stream);
 
 /* hstu_rel_bias_fwd / _bwd (ABI 13) — replaces RelativeBucketedTimeAndPositionBasedBias
  * .forward (sequential_encoders/hstu.py:96-128) for callers that materialise the bias

@@ -219,6 +219,33 @@ inline int resident_wgs(K kernel, size_t lds) {
   return n;
 }
 
+// One workgroup (256 threads): offsets[0] = 0, offsets[b + 1] = sum_{j <= b} lengths[j]
+// (utils/ops.py:18-38).  Thread t owns lengths[t * per, (t + 1) * per); a 64-lane shuffle
+// scan per wave, then the four wave totals meet in LDS (one barrier).
+__device__ __forceinline__ void offsets_scan(const int64_t* lengths, int B, int64_t* offsets) {
+  __shared__ int64_t wave_tot[4];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int per = (B + 255) / 256;
+  const int lo = t * per, hi = min(B, lo + per);
+  int64_t s = 0;
+  for (int i = lo; i < hi; ++i) s += lengths[i];
+  int64_t inc = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t v = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += v;
+  }
+  if (lane == 63) wave_tot[wv] = inc;
+  __syncthreads();
+  int64_t run = inc - s;
+  for (int w = 0; w < wv; ++w) run += wave_tot[w];
+  if (t == 0) offsets[0] = 0;
+  for (int i = lo; i < hi; ++i) {
+    run += lengths[i];
+    offsets[i + 1] = run;
+  }
+}
+
 // relative-time bucket: max{b : thr[b] <= |dt|}, thr = integer threshold table of the
 // reference bucket fn (hstu.py:579-581, clamped at hstu.py:117-123).
 __device__ __forceinline__ int time_bucket(int64_t dt, const int64_t* thr_lds, int nb) {
@@ -229,6 +256,11 @@ __device__ __forceinline__ int time_bucket(int64_t dt, const int64_t* thr_lds, i
     b = (int)(__log2f(f) * 2.30283176f);  // log2(x) * ln(2) / 0.301
     b = b > nb ? nb : b;
   }
+  // the estimate is the bucket or one off (every table threshold and 2e5 random |dt| up
+  // to 2^40 checked on the host): both bracketing thresholds are read together, and the
+  // walks below run only when it missed
+  const uint64_t lo = (uint64_t)thr_lds[b], hi = (uint64_t)thr_lds[b < nb ? b + 1 : nb];
+  if (ad >= lo && (b == nb || ad < hi)) return b;
   while (b < nb && ad >= (uint64_t)thr_lds[b + 1]) ++b;
   while (b > 0 && ad < (uint64_t)thr_lds[b]) --b;
   return b;

@@ -21,22 +21,18 @@ __host__ __device__ inline int tiles_per_seq(int N) {
   return T * (T + 1) / 2;
 }
 
-__global__ __launch_bounds__(256) void bucket_map_kernel(const int64_t* ts, const int64_t* offsets,
-                                                         int B, int N, const int64_t* thr_g,
-                                                         int nb, uint8_t* map_qk,
-                                                         uint8_t* map_kq) {
+// Tile t (causal order) of sequence b, L = its length: both orientations of the tile.
+__device__ __forceinline__ void bucket_tile(const int64_t* ts, int b, int t, int L, int N, int tpb,
+                                            const int64_t* thr_g, int nb, uint8_t* map_qk,
+                                            uint8_t* map_kq) {
   __shared__ int64_t thr[256];
   __shared__ int64_t tsq[64], tsk[64];
-  __shared__ uint32_t tile[64][17];  // [q][k/4] packed bytes, padded row
-  const int tpb = tiles_per_seq(N);
-  const int b = blockIdx.x / tpb;
-  const int t = blockIdx.x % tpb;
-  int qt = 0;
+  __shared__ uint32_t tile_kq[64][17];  // [k][q/4] packed bytes, padded row
+  int qt = (int)((sqrtf(8.f * (float)t + 1.f) - 1.f) * 0.5f);  // t = qt (qt + 1) / 2 + kt
+  while (qt > 0 && qt * (qt + 1) / 2 > t) --qt;
   while ((qt + 1) * (qt + 2) / 2 <= t) ++qt;
   const int kt = t - qt * (qt + 1) / 2;
   const int tid = threadIdx.x;
-  const int64_t s0 = offsets[b];
-  const int L = (int)(offsets[b + 1] - s0);
   for (int i = tid; i <= nb; i += 256) thr[i] = thr_g[i];
   if (tid < 64) {
     const int q = qt * 64 + tid;
@@ -48,40 +44,122 @@ __global__ __launch_bounds__(256) void bucket_map_kernel(const int64_t* ts, cons
     tsk[tid - 64] = ts[(int64_t)b * N + (k < N ? k : N - 1)];
   }
   __syncthreads();
-  // thread -> (q = tid / 4, 16 keys = 4 dwords)
-  const int ql = tid >> 2, part = tid & 3;
-  const int q = qt * 64 + ql;
+  // thread -> a 4 x 4 block: queries 4 qb .. 4 qb + 3, keys 4 kb .. 4 kb + 3.  Its four
+  // query-major words (4 keys each) are stored as they are; the four key-major words
+  // (4 queries each) are the same 16 bytes transposed in registers, staged through LDS
+  // for a coalesced store (conflict-free: row stride 17 dwords)
+  const int kb = tid & 15, qb = tid >> 4;
+  uint32_t bk[4][4];
 #pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    uint32_t word = 0;
+  for (int i = 0; i < 4; ++i) {
+    const int ql = 4 * qb + i, q = qt * 64 + ql;
+    const int64_t tq = tsq[ql];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int kl = part * 16 + d * 4 + e;
-      const int k = kt * 64 + kl;
-      uint32_t bk = 0;
-      if (q < L && k <= q) bk = (uint32_t)time_bucket(tsq[ql] - tsk[kl], thr, nb);
-      word |= bk << (8 * e);
+      const int kl = 4 * kb + e, k = kt * 64 + kl;
+      bk[i][e] = (q < L && k <= q) ? (uint32_t)time_bucket(tq - tsk[kl], thr, nb) : 0u;
     }
-    tile[ql][part * 4 + d] = word;
   }
-  __syncthreads();
   const int64_t base = ((int64_t)b * tpb + t) * 4096;
-  // map_qk: row q = 16 dwords
-  uint32_t* dst_qk = reinterpret_cast<uint32_t*>(map_qk + base);
-  for (int i = tid; i < 64 * 16; i += 256) dst_qk[i] = tile[i >> 4][i & 15];
+  uint32_t* dst_qk = reinterpret_cast<uint32_t*>(map_qk + base);  // row q = 16 dwords
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    dst_qk[(4 * qb + i) * 16 + kb] = bk[i][0] | (bk[i][1] << 8) | (bk[i][2] << 16) | (bk[i][3] << 24);
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    tile_kq[4 * kb + e][qb] = bk[0][e] | (bk[1][e] << 8) | (bk[2][e] << 16) | (bk[3][e] << 24);
+  __syncthreads();
   // map_kq: row k holds the 64 queries' bytes
   uint32_t* dst_kq = reinterpret_cast<uint32_t*>(map_kq + base);
-  for (int i = tid; i < 64 * 16; i += 256) {
-    const int kl = i >> 4, qd = i & 15;
-    uint32_t word = 0;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int ql2 = qd * 4 + e;
-      const uint32_t w = tile[ql2][kl >> 2];
-      word |= ((w >> (8 * (kl & 3))) & 0xFFu) << (8 * e);
-    }
-    dst_kq[i] = word;
+  for (int j = 0; j < 4; ++j) {
+    const int i = tid + 256 * j;
+    dst_kq[i] = tile_kq[i >> 4][i & 15];
   }
+}
+
+__global__ __launch_bounds__(256) void bucket_map_kernel(const int64_t* ts, const int64_t* offsets,
+                                                         int B, int N, const int64_t* thr_g,
+                                                         int nb, uint8_t* map_qk,
+                                                         uint8_t* map_kq) {
+  const int tpb = tiles_per_seq(N);
+  const int b = blockIdx.x / tpb;
+  bucket_tile(ts, b, blockIdx.x % tpb, (int)(offsets[b + 1] - offsets[b]), N, tpb, thr_g, nb,
+              map_qk, map_kq);
+}
+
+// ------------------------------------------------------------------ encoder prologue
+// The batch setup of an encoder forward as one launch (hstu.py:502, utils/ops.py:18-64,
+// and the bucket map above): x_offsets = complete_cumsum(lengths), the padded input rows
+// -> jagged rows, the bucket map, and one step of the dropout counter.  Three kinds of
+// workgroup, none waiting for another:
+//   [0, n_bucket)               bucket tiles (L = lengths[b]),
+//   [n_bucket, + n_copy)        copy chunks: each wave sums lengths[0 .. b) itself for the
+//                               destination row s0; the chunk's padded rows are loaded
+//                               before that sum is known (they are always in range),
+//   last                        the offsets scan, then step += 1.
+// Copies as gr_dense_to_jagged with zero_fill = 0: min(L, N) rows of sequence b, none at
+// or past max_rows.
+struct PrologueArgs {
+  const int64_t* lengths;
+  int B, N;
+  const void* x;      // [B][N][row_units] units of V
+  int64_t row_units;
+  int64_t max_rows;
+  int chunks;         // copy workgroups per sequence
+  const int64_t* ts;  // [B][N] (bucket map) or null
+  const int64_t* thr;
+  int nb, tpb;
+  int n_bucket, n_copy;
+  int64_t* offsets;
+  void* xj;           // [max_rows][row_units]
+  uint8_t* map_qk;
+  uint8_t* map_kq;
+  int64_t* step;      // dropout step counter or null
+};
+
+constexpr int PRO_PER = 4;
+constexpr int PRO_CHUNK = 256 * PRO_PER;
+
+template <typename V>
+__global__ __launch_bounds__(256) void encoder_prologue_kernel(PrologueArgs a) {
+  const int id = blockIdx.x;
+  if (id < a.n_bucket) {
+    const int b = id / a.tpb;
+    bucket_tile(a.ts, b, id % a.tpb, (int)a.lengths[b], a.N, a.tpb, a.thr, a.nb, a.map_qk, a.map_kq);
+    return;
+  }
+  const int j = id - a.n_bucket;
+  if (j < a.n_copy) {
+    const int b = j / a.chunks;
+    const int64_t nd = (int64_t)a.N * a.row_units;
+    const V* src = reinterpret_cast<const V*>(a.x) + (int64_t)b * nd;
+    const int64_t base = (int64_t)(j % a.chunks) * PRO_CHUNK;
+    V v[PRO_PER];
+#pragma unroll
+    for (int k = 0; k < PRO_PER; ++k) {
+      const int64_t i = base + threadIdx.x + 256 * k;
+      v[k] = i < nd ? src[i] : V{};
+    }
+    const int lane = threadIdx.x & 63;
+    int64_t s0 = 0;
+    for (int i = lane; i < b; i += 64) s0 += a.lengths[i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s0 += __shfl_xor(s0, o, 64);
+    const int64_t len = a.lengths[b];
+    if (s0 < 0 || s0 >= a.max_rows || len <= 0) return;
+    const int64_t L = min(min(len, (int64_t)a.N), a.max_rows - s0);
+    const int64_t n_copy = L * a.row_units;
+    V* dst = reinterpret_cast<V*>(a.xj) + s0 * a.row_units;
+#pragma unroll
+    for (int k = 0; k < PRO_PER; ++k) {
+      const int64_t i = base + threadIdx.x + 256 * k;
+      if (i < n_copy) dst[i] = v[k];
+    }
+    return;
+  }
+  offsets_scan(a.lengths, a.B, a.offsets);
+  if (threadIdx.x == 0 && a.step) a.step[0] = a.step[0] + 1;
 }
 
 }  // namespace gr
@@ -103,6 +181,48 @@ extern "C" int hstu_bucket_map(const int64_t* ts, const int64_t* offsets, int B,
   GR_TIMED("bucket_map", (hipStream_t)stream, hipLaunchKernelGGL(gr::bucket_map_kernel, dim3(B * tpb), dim3(256), 0, (hipStream_t)stream, ts,
                      offsets, B, N, bucket_thr, num_buckets, map, map_kq));
   GR_LAUNCH_CHECK("hstu_bucket_map");
+  return 0;
+}
+
+extern "C" int hstu_encoder_prologue(const int64_t* lengths, int B, int N, const float* x, int D,
+                                     int64_t max_rows, const int64_t* ts, const int64_t* bucket_thr,
+                                     int num_buckets, int64_t* offsets, float* x_jagged,
+                                     uint8_t* map, int64_t* step, void* stream) {
+  GR_REQUIRE(offsets && B >= 0 && N >= 0 && D > 0 && max_rows >= 0,
+             "hstu_encoder_prologue: bad args");
+  GR_REQUIRE(B == 0 || (lengths && x && x_jagged), "hstu_encoder_prologue: null pointer");
+  GR_REQUIRE(!map || (ts && bucket_thr && N > 0 && num_buckets > 0 && num_buckets < 256),
+             "hstu_encoder_prologue: bucket map needs ts, the threshold table, N > 0 and "
+             "0 < num_buckets < 256");
+  gr::PrologueArgs a{};
+  a.lengths = lengths;
+  a.B = B;
+  a.N = N;
+  a.x = x;
+  a.max_rows = max_rows;
+  a.ts = ts;
+  a.thr = bucket_thr;
+  a.nb = num_buckets;
+  a.offsets = offsets;
+  a.xj = x_jagged;
+  a.step = step;
+  const bool v2 = D % 2 == 0 && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(x_jagged)) & 7) == 0;
+  a.row_units = v2 ? D / 2 : D;
+  a.chunks = (int)((int64_t)N * a.row_units + gr::PRO_CHUNK - 1) / gr::PRO_CHUNK;
+  a.tpb = N > 0 ? gr::tiles_per_seq(N) : 0;
+  a.n_bucket = map && B > 0 ? B * a.tpb : 0;
+  a.n_copy = max_rows > 0 ? B * a.chunks : 0;
+  if (map) {
+    a.map_qk = map;
+    a.map_kq = map + (size_t)B * a.tpb * 4096;
+  }
+  const dim3 grid((unsigned)(a.n_bucket + a.n_copy + 1));
+  const hipStream_t st = (hipStream_t)stream;
+  if (v2)
+    GR_TIMED("encoder_prologue", st, hipLaunchKernelGGL(gr::encoder_prologue_kernel<float2>, grid, dim3(256), 0, st, a));
+  else
+    GR_TIMED("encoder_prologue", st, hipLaunchKernelGGL(gr::encoder_prologue_kernel<float>, grid, dim3(256), 0, st, a));
+  GR_LAUNCH_CHECK("hstu_encoder_prologue");
   return 0;
 }
 

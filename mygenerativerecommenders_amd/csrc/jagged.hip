@@ -12,29 +12,7 @@ namespace gr {
 // single workgroup exclusive scan: offsets[0] = 0, offsets[b+1] = sum_{<=b} lengths
 __global__ __launch_bounds__(256) void cumsum_kernel(const int64_t* lengths, int B,
                                                     int64_t* offsets) {
-  // thread t owns lengths[t*per, (t+1)*per); 64-lane shuffle scan per wave, then the
-  // four wave totals meet in LDS (one barrier)
-  __shared__ int64_t wave_tot[4];
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const int per = (B + 255) / 256;
-  const int lo = t * per, hi = min(B, lo + per);
-  int64_t s = 0;
-  for (int i = lo; i < hi; ++i) s += lengths[i];
-  int64_t inc = s;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int64_t v = __shfl_up(inc, o, 64);
-    if (lane >= o) inc += v;
-  }
-  if (lane == 63) wave_tot[wv] = inc;
-  __syncthreads();
-  int64_t run = inc - s;
-  for (int w = 0; w < wv; ++w) run += wave_tot[w];
-  if (t == 0) offsets[0] = 0;
-  for (int i = lo; i < hi; ++i) {
-    run += lengths[i];
-    offsets[i + 1] = run;
-  }
+  offsets_scan(lengths, B, offsets);
 }
 
 // Sequence b's valid rows are one contiguous span of L_b * D floats on both sides
@@ -56,6 +34,17 @@ __global__ __launch_bounds__(256) void dense_to_jagged_kernel(const V* dense, co
                                                               int64_t max_rows, int zero_fill,
                                                               V* jagged) {
   for (int b = blockIdx.y; b <= B; b += gridDim.y) {
+    // the first chunk's dense loads do not depend on the offsets (the padded rows of b are
+    // always in range): issued before the offsets are read, so the two round trips overlap
+    const int64_t nd = (int64_t)N * row_units;
+    const V* src = dense + (int64_t)min(b, B - 1) * nd;
+    const int64_t base0 = (int64_t)blockIdx.x * JG_CHUNK;
+    V v0[JG_PER];
+#pragma unroll
+    for (int k = 0; k < JG_PER; ++k) {
+      const int64_t i = base0 + threadIdx.x + 256 * k;
+      v0[k] = b < B && i < nd ? src[i] : V{};
+    }
     const int64_t s0 = offsets[b];
     const int64_t s1 = b < B ? offsets[b + 1] : max_rows;
     if (s0 >= max_rows || s0 < 0 || (b == B && !zero_fill)) continue;
@@ -63,14 +52,13 @@ __global__ __launch_bounds__(256) void dense_to_jagged_kernel(const V* dense, co
     const int64_t L = b < B ? min(min(s1 - s0, (int64_t)N), end - s0) : 0;  // rows copied
     const int64_t n_copy = L * row_units;
     const int64_t n = (zero_fill ? end - s0 : L) * row_units;
-    const V* src = dense + (int64_t)min(b, B - 1) * N * row_units;
     V* dst = jagged + s0 * row_units;
-    for (int64_t base = (int64_t)blockIdx.x * JG_CHUNK; base < n; base += (int64_t)gridDim.x * JG_CHUNK) {
+    for (int64_t base = base0; base < n; base += (int64_t)gridDim.x * JG_CHUNK) {
       V v[JG_PER];
 #pragma unroll
       for (int k = 0; k < JG_PER; ++k) {
         const int64_t i = base + threadIdx.x + 256 * k;
-        v[k] = i < n_copy ? src[i] : V{};
+        v[k] = i < n_copy ? (base == base0 ? v0[k] : src[i]) : V{};
       }
 #pragma unroll
       for (int k = 0; k < JG_PER; ++k) {

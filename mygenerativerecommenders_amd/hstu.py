@@ -255,22 +255,31 @@ class HSTUJagged(torch.nn.Module):
         self.register_buffer("_dropout_step", torch.zeros(1, dtype=torch.int64),
                              persistent=False)
 
+    def _needs_map(self, all_timestamps) -> bool:
+        return all_timestamps is not None and any(
+            layer._rel_attn_bias is not None for layer in self._attention_layers)
+
+    def _needs_step(self) -> bool:
+        return self.training and any(layer._dropout_ratio > 0 for layer in self._attention_layers)
+
     def jagged_forward(self, x, x_offsets, all_timestamps, invalid_attn_mask,
                        delta_x_offsets=None, cache=None, return_cache_states=False,
-                       max_len: Optional[int] = None):
+                       max_len: Optional[int] = None, _prepared=None):
+        """``_prepared`` (internal): (bucket map, advanced dropout step) already produced by
+        ops.encoder_prologue."""
         if delta_x_offsets is not None or cache is not None:
             raise NotImplementedError("incremental (cached) HSTU decoding is not supported")
         cache_states: List[HSTUCacheState] = []
         n = invalid_attn_mask.size(-1)
-        # one bucket map per batch, shared by every layer's forward and backward
-        bmap = None
-        if all_timestamps is not None and any(
-                layer._rel_attn_bias is not None for layer in self._attention_layers):
-            bmap = ops.bucket_map(all_timestamps, x_offsets, n)
-        step = None
-        if self.training and any(layer._dropout_ratio > 0 for layer in self._attention_layers):
-            self._dropout_step.add_(1)
-            step = self._dropout_step
+        if _prepared is not None:
+            bmap, step = _prepared
+        else:
+            # one bucket map per batch, shared by every layer's forward and backward
+            bmap = ops.bucket_map(all_timestamps, x_offsets, n) if self._needs_map(all_timestamps) else None
+            step = None
+            if self._needs_step():
+                self._dropout_step.add_(1)
+                step = self._dropout_step
         stack = self._stack_params(n, max_len, bmap, return_cache_states)
         if stack is not None:
             geo, params, seeds = stack
@@ -315,6 +324,23 @@ class HSTUJagged(torch.nn.Module):
         jagged_x, cache_states = self.jagged_forward(
             x, x_offsets, all_timestamps, invalid_attn_mask, delta_x_offsets, cache,
             return_cache_states, max_len=max_len)
+        y = ops.jagged_to_padded_dense(jagged_x, x_offsets, n, 0.0)
+        return y, cache_states
+
+    def forward_from_lengths(self, lengths, x, all_timestamps, invalid_attn_mask,
+                             return_cache_states=False, max_len: Optional[int] = None):
+        """HSTU.forward on padded fp32 input (B, N, D) with N = the mask size: the offsets,
+        the jagged rows, the bucket map and the dropout step come from one launch
+        (ops.encoder_prologue) instead of four (cumsum, dense_to_jagged, bucket map,
+        counter add); results are identical."""
+        n = invalid_attn_mask.size(1)
+        need_map = self._needs_map(all_timestamps)
+        step = self._dropout_step if self._needs_step() else None
+        xj, x_offsets, bmap = ops.encoder_prologue(
+            lengths, x, all_timestamps if need_map else None, step)
+        jagged_x, cache_states = self.jagged_forward(
+            xj, x_offsets, all_timestamps, invalid_attn_mask, None, None, return_cache_states,
+            max_len=max_len, _prepared=(bmap, step))
         y = ops.jagged_to_padded_dense(jagged_x, x_offsets, n, 0.0)
         return y, cache_states
 
@@ -385,6 +411,9 @@ class HSTU(torch.nn.Module):
             torch.triu(torch.ones((self._max_sequence_length + max_output_len,
                                    self._max_sequence_length + max_output_len),
                                   dtype=torch.bool), diagonal=1))
+        # forward on padded input: offsets, jagged rows, bucket map and dropout step in one
+        # launch (ops.encoder_prologue); False = the reference's separate steps
+        self.use_prologue = True
         self.reset_params()
 
     def reset_params(self):
@@ -422,6 +451,15 @@ class HSTU(torch.nn.Module):
         float_dtype = user_embeddings.dtype
         if float_dtype != torch.float32:
             user_embeddings = user_embeddings.float()
+        ts = past_payloads[TIMESTAMPS_KEY] if TIMESTAMPS_KEY in past_payloads else None
+        n = self._attn_mask.size(1)
+        if (self.use_prologue and delta_x_offsets is None and cache is None
+                and user_embeddings.dim() == 3 and user_embeddings.size(1) == n
+                and (ts is None or tuple(ts.shape) == (user_embeddings.size(0), n))):
+            y, cached_states = self._hstu.forward_from_lengths(
+                past_lengths, user_embeddings, ts, self._attn_mask,
+                return_cache_states=return_cache_states, max_len=max_len)
+            return y.to(float_dtype), cached_states
         y, cached_states = self._hstu(
             x=user_embeddings,
             x_offsets=ops.asynchronous_complete_cumsum(past_lengths),

@@ -205,6 +205,65 @@ def bucket_map(timestamps: torch.Tensor, offsets: torch.Tensor, N: int) -> torch
     return out
 
 
+class _EncoderPrologue(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, dense, lengths, ts, step):
+        B, N, D = dense.shape
+        dev = dense.device
+        offsets = torch.empty(B + 1, dtype=torch.int64, device=dev)
+        out = torch.empty(B * N, D, dtype=dense.dtype, device=dev)
+        bmap = None
+        if ts is not None:
+            bmap = torch.empty(max(_lib.lib().hstu_bucket_map_bytes(B, N), 1), dtype=torch.uint8,
+                               device=dev)
+        thr = bucket_thresholds(dev) if ts is not None else None
+        _lib.call("hstu_encoder_prologue", lengths.data_ptr(), B, N, dense.data_ptr(), D, B * N,
+                  ts.data_ptr() if ts is not None else None, thr.data_ptr() if thr is not None else None,
+                  NUM_BUCKETS, offsets.data_ptr(), out.data_ptr(),
+                  bmap.data_ptr() if bmap is not None else None,
+                  step.data_ptr() if step is not None else None, _stream())
+        ctx.save_for_backward(offsets)
+        ctx.shape = (B, N, D)
+        if bmap is None:
+            ctx.mark_non_differentiable(offsets)
+            return out, offsets
+        ctx.mark_non_differentiable(offsets, bmap)
+        return out, offsets, bmap
+
+    @staticmethod
+    def backward(ctx, g, *_):
+        (offsets,) = ctx.saved_tensors
+        B, N, D = ctx.shape
+        g = g.contiguous()
+        dx = torch.empty(B, N, D, dtype=g.dtype, device=g.device)
+        _lib.call("gr_jagged_to_padded", g.data_ptr(), offsets.data_ptr(), B, N, D, dx.data_ptr(),
+                  _stream())
+        return dx, None, None, None
+
+
+def encoder_prologue(lengths: torch.Tensor, dense: torch.Tensor, timestamps: Optional[torch.Tensor],
+                     step: Optional[torch.Tensor] = None):
+    """The batch setup of an encoder forward as one launch (``hstu_encoder_prologue``):
+    returns (x jagged with B*N capacity rows, offsets, bucket map or None), identical to
+    ``dense_to_jagged(dense, asynchronous_complete_cumsum(lengths), zero_fill=False)`` and
+    ``bucket_map(timestamps, offsets, N)``; ``step`` (an int64 device counter) is advanced by
+    one.  Differentiable in ``dense`` (backward: jagged_to_padded_dense)."""
+    _lib.require_gpu(lengths, dense)
+    if dense.dtype != torch.float32 or dense.dim() != 3:
+        raise TypeError("encoder_prologue: (B, N, D) float32 input expected")
+    B, N, _ = dense.shape
+    lengths = lengths.to(torch.int64).contiguous()
+    if lengths.numel() != B:
+        raise ValueError(f"encoder_prologue: {lengths.numel()} lengths for a batch of {B}")
+    ts = None
+    if timestamps is not None:
+        ts = timestamps.to(torch.int64).contiguous()
+        if ts.shape != (B, N):
+            raise ValueError(f"timestamps must be (B, N) = ({B}, {N}), got {tuple(ts.shape)}")
+    outs = _EncoderPrologue.apply(dense.contiguous(), lengths, ts, step)
+    return (outs[0], outs[1], outs[2] if ts is not None else None)
+
+
 class _RelBias(torch.autograd.Function):
     @staticmethod
     def forward(ctx, ts, N, pos_w, ts_w):

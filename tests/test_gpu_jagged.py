@@ -152,3 +152,103 @@ def test_jagged_to_padded_grad_truncated_rows_are_zero():
         s0, L = int(o[b]), min(int(lengths[b]), N)
         ref[s0:s0 + L] = g[b, :L].cpu()
     assert torch.equal(grad, ref)
+
+
+# ------------------------------------------------------------------ encoder prologue
+def _prologue_vs_separate(B, N, D, lengths, with_ts=True, with_step=True, dense=None):
+    """hstu_encoder_prologue against the separate calls it replaces (cumsum, dense_to_jagged
+    with zero_fill = 0, hstu_bucket_map, step += 1): offsets, the copied rows and the whole
+    bucket map bit-identical, the counter advanced by one."""
+    from mygenerativerecommenders_amd import ops
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(B * 7 + N + D)
+    if dense is None:
+        dense = torch.randn(B, N, D, generator=g).to(dev)
+    ts = None
+    if with_ts:
+        inc = (-torch.log(torch.rand(B, N, generator=g).clamp_min(1e-12)) * 1e5).long()
+        ts = (torch.randint(0, 10**9, (B, 1), generator=g) + torch.cumsum(inc, 1)).to(dev)
+    step = torch.full((1,), 41, dtype=torch.int64, device=dev) if with_step else None
+    lengths_d = lengths.to(dev)
+    xj, offs, bmap = ops.encoder_prologue(lengths_d, dense, ts, step)
+    offs_ref = ops.asynchronous_complete_cumsum(lengths_d)
+    assert torch.equal(offs.cpu(), offs_ref.cpu())
+    ref = ops.dense_to_jagged(dense, offs_ref, zero_fill=False)
+    o = offs_ref.cpu()
+    for b in range(B):
+        s0, L = int(o[b]), min(int(lengths[b]), N)
+        if s0 < B * N:
+            L = min(L, B * N - s0)
+            assert torch.equal(xj[s0:s0 + L].cpu(), ref[s0:s0 + L].cpu()), b
+    if with_ts:
+        assert torch.equal(bmap.cpu(), ops.bucket_map(ts, offs_ref, N).cpu())
+    else:
+        assert bmap is None
+    if with_step:
+        assert int(step.item()) == 42
+    return dense, xj, offs
+
+
+@pytest.mark.parametrize("B,N,D", [(128, 201, 50), (5, 17, 7), (3, 1, 1), (9, 300, 256),
+                                   (2, 2059, 256), (70, 130, 64)])
+def test_encoder_prologue_matches_separate_calls(B, N, D):
+    g = torch.Generator().manual_seed(B + N)
+    lengths = torch.randint(0, N + 1, (B,), generator=g)
+    lengths[0] = 0
+    lengths[-1] = N
+    _prologue_vs_separate(B, N, D, lengths)
+
+
+def test_encoder_prologue_edges():
+    # no bucket map / no counter; lengths above N (truncated copies, offsets keep them)
+    _prologue_vs_separate(6, 40, 50, torch.tensor([40, 0, 55, 3, 40, 1]), with_ts=False)
+    _prologue_vs_separate(4, 64, 50, torch.tensor([64, 64, 64, 64]), with_step=False)
+    # an unaligned view takes the 4-byte stream
+    storage = torch.randn(6 * 40 * 50 + 1).cuda()
+    _prologue_vs_separate(6, 40, 50, torch.tensor([0, 40, 3, 17, 39, 1]),
+                          dense=storage[1:].view(6, 40, 50))
+    # B = 0: offsets = [0] only
+    from mygenerativerecommenders_amd import ops
+    xj, offs, bmap = ops.encoder_prologue(torch.zeros(0, dtype=torch.int64, device="cuda"),
+                                          torch.zeros(0, 5, 8, device="cuda"), None)
+    assert offs.cpu().tolist() == [0] and xj.shape == (0, 8)
+
+
+def test_encoder_prologue_autograd_and_hstu_forward():
+    """dense gradient = jagged_to_padded of the jagged gradient; HSTU.forward through the
+    prologue equals the separate-call path (same output, same input gradient)."""
+    from mygenerativerecommenders_amd import ops
+    from mygenerativerecommenders_amd.hstu import HSTU
+    B, N, D = 4, 23, 50
+    lengths = torch.tensor([23, 0, 11, 5])
+    dense = torch.randn(B, N, D).cuda().requires_grad_(True)
+    xj, offs, _ = ops.encoder_prologue(lengths.cuda(), dense, None)
+    w = torch.randn(xj.shape).cuda()
+    (xj[:39] * w[:39]).sum().backward()
+    offs_np = np.concatenate([[0], np.cumsum(lengths.numpy())]).astype(np.int64)
+    wz = w.cpu().numpy().copy()
+    wz[39:] = 0
+    assert np.array_equal(dense.grad.cpu().numpy(), _np_jagged_to_padded(wz, offs_np, N))
+
+    torch.manual_seed(0)
+    enc = HSTU(max_sequence_len=20, max_output_len=3, embedding_dim=D, item_embedding_dim=D,
+               num_blocks=2, num_heads=1, linear_dim=D, attention_dim=D,
+               normalization="rel_bias", linear_config="uvqk", linear_activation="silu",
+               linear_dropout_rate=0.2, attn_dropout_rate=0.0).cuda()
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(B, N, D, generator=g).cuda()
+    inc = (-torch.log(torch.rand(B, N, generator=g).clamp_min(1e-12)) * 1e5).long()
+    ts = (10**9 + torch.cumsum(inc, 1)).cuda()
+    dy = torch.randn(B, N, D, generator=g).cuda()
+    outs = []
+    for use in (True, False):
+        enc.use_prologue = use
+        enc._hstu._dropout_step.zero_()
+        xr = x.clone().requires_grad_(True)
+        y, _ = enc(past_lengths=lengths.cuda(), user_embeddings=xr, valid_mask=None,
+                   past_payloads={"timestamps": ts})
+        y.backward(dy)
+        outs.append((y.detach().cpu(), xr.grad.cpu(), int(enc._hstu._dropout_step.item())))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+    assert outs[0][2] == outs[1][2] == 1
