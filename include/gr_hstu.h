@@ -44,7 +44,7 @@ GR_API int gr_version(void);
  * (attention + layer boundary), attn_fwd_bnd1 (+ gate_o of the last layer), attn_bwd_dq_bnd
  * (dQ + layer boundary), attn_bwd_dq_bnd1 (+ ln_uvqk_bwd of the first layer),
  * attn_bias_reduce, ln_uvqk_fwd, gate_o_fwd, gate_o_bwd, ln_uvqk_bwd, wgrad_partial,
- * wgrad_reduce, mips_pack, mips_select, mips_merge, cumsum, dense_to_jagged, encoder_prologue,
+ * wgrad_reduce, mips_pack, mips_select, mips_merge, cumsum, dense_to_jagged, encoder_prologue, bf16_scale_add,
  * jagged_to_padded, l2_normalize, current_embeddings, sampled_softmax_fwd,
  * sampled_softmax_bwd, sampled_softmax_csr, sampled_softmax_table_grad, preproc.  Not for use inside a captured graph.
  */
@@ -247,6 +247,13 @@ GR_API int gr_sampled_softmax_bwd(const float* out, int64_t ld_out, const float*
                                   const float* dloss, float* d_out, int64_t ld_dout, float* d_pos,
                                   int64_t ld_dpos, float* d_table, int64_t ld_dtable,
                                   void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------- Muon step (ABI 17)
+ * out[i] = bf16(bf16(s * x[i]) + y[i]) over n bf16 values (bit patterns): the two
+ * combines of the Newton-Schulz chain of optimizers/muon.py:3-29 (B = b*A + (c*A)@A,
+ * X = a*X + B@X) with the reference's two roundings, in one launch.  out may alias x or y. */
+GR_API int gr_bf16_scale_add(const uint16_t* x, float s, const uint16_t* y, uint16_t* out,
+                             int64_t n, void* stream);
 
 /* ---------------------------------------------------------------- HSTU attention
  * hstu_bucket_map: the relative-time bucket of every causal (query i, key j) pair of

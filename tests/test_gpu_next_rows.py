@@ -111,3 +111,27 @@ def test_fused_adamw_graph_replay_matches_unfused():
     torch.cuda.synchronize()
     for a, b in zip(pa, pb):
         assert torch.allclose(a, b, rtol=1e-5, atol=1e-7), (a - b).abs().max().item()
+
+
+@pytest.mark.parametrize("shape", [(8, 256, 1024), (8, 256, 256), (3, 300, 50), (2, 7, 13)])
+def test_muon_ns_combine_kernel_is_bit_identical(shape):
+    """The GPU chain (gr_bf16_scale_add combines) against the reference's torch ops on the
+    same device: the GEMMs are the same calls, the combines keep both bf16 roundings, so
+    the orthogonalised result is bit-identical (any other rounding moves it by ~5 %)."""
+    from mygenerativerecommenders_amd.muon import _NS_COEFFS, zeropower_via_newtonschulz5
+    a, b, c = _NS_COEFFS
+    g = torch.Generator(device="cuda")
+    g.manual_seed(sum(shape))
+    G = torch.randn(shape, device="cuda", generator=g)
+    X = G.bfloat16()
+    if G.size(-2) > G.size(-1):
+        X = X.mT
+    X = X / (X.norm(dim=(-2, -1), keepdim=True) + 1e-7)
+    for _ in range(5):
+        A = X @ X.mT
+        B = b * A + c * A @ A
+        X = a * X + B @ X
+    if G.size(-2) > G.size(-1):
+        X = X.mT
+    got = zeropower_via_newtonschulz5(G, 5)
+    assert torch.equal(got, X)
