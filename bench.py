@@ -73,6 +73,22 @@ def make_batch(B, N0, out_len, D, seed, device, fixed_len=True):
     return (lengths.to(device), x.to(device), ts.to(device), past_ids.to(device), dy.to(device))
 
 
+# AdamW implementation of the training legs (--adamw): "flat" = optim.FlatAdamW (the
+# reference's AdamW update in one launch per step, counter advanced on the device),
+# "torch" = torch.optim.AdamW(fused=True, capturable=True) (two launches per step)
+ADAMW = "flat"
+
+
+def make_adamw(params, **kw):
+    if ADAMW == "flat":
+        from mygenerativerecommenders_amd.optim import FlatAdamW
+        return FlatAdamW(params, **kw)
+    try:  # one fused multi-tensor kernel per step (same AdamW math), graph-capturable
+        return torch.optim.AdamW(params, fused=True, capturable=True, **kw)
+    except (RuntimeError, TypeError, ValueError):
+        return torch.optim.AdamW(params, capturable=True, **kw)
+
+
 def build_model(N0, out_len, D, blocks, device):
     from mygenerativerecommenders_amd.hstu import HSTU
     torch.manual_seed(0)
@@ -266,16 +282,12 @@ def e2e_train_leg(args, device, world, lengths, ts, past_ids, N0=None, D=None, b
         reducer = BucketedGradReducer(params, bucket_bytes=25 << 20, overlap=world > 1,
                                       row_support=support)
         eager = eager or world > 1
-        opts = muon_adamw_split(named, **({} if eager else {"fused": True, "capturable": True}))
+        opts = muon_adamw_split(named, flat_adam=ADAMW == "flat",
+                                **({} if eager else {"fused": True, "capturable": True}))
         xbytes = reducer.exchange_bytes
     else:
         reducer = FlatGradAllReducer(params)
-        try:  # one fused multi-tensor kernel per step (same AdamW math), as in the headline leg
-            opts = [torch.optim.AdamW(params, lr=1e-3, betas=(0.9, 0.98), weight_decay=1e-3,
-                                      fused=True, capturable=True)]
-        except (RuntimeError, TypeError, ValueError):
-            opts = [torch.optim.AdamW(params, lr=1e-3, betas=(0.9, 0.98), weight_decay=1e-3,
-                                      capturable=True)]
+        opts = [make_adamw(params, lr=1e-3, betas=(0.9, 0.98), weight_decay=1e-3)]
         xbytes = 4 * sum(p.numel() for p in params)
 
     def opt_step():
@@ -424,12 +436,11 @@ def encoder_leg(B, N0, out_len, D, blocks, H, steps, warmup, device, world, seed
         reducer = BucketedGradReducer(list(enc.parameters()), bucket_bytes=4 << 20,
                                       overlap=world > 1)
         eager = eager or world > 1
-        opts = muon_adamw_split(enc.named_parameters(),
+        opts = muon_adamw_split(enc.named_parameters(), flat_adam=ADAMW == "flat",
                                 **({} if eager else {"fused": True, "capturable": True}))
     else:
         reducer = FlatGradAllReducer(list(enc.parameters()))
-        opts = [torch.optim.AdamW(enc.parameters(), lr=1e-3, betas=(0.9, 0.98), weight_decay=1e-3,
-                                  fused=True, capturable=True)]
+        opts = [make_adamw(list(enc.parameters()), lr=1e-3, betas=(0.9, 0.98), weight_decay=1e-3)]
 
     class _Opt:
         def step(self):
@@ -565,6 +576,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-retrieval-leg", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no HIP-graph capture of the step")
+    ap.add_argument("--adamw", choices=("flat", "torch"), default="flat",
+                    help="AdamW of the training legs: optim.FlatAdamW (one launch) or torch's fused AdamW")
     ap.add_argument("--e2e-steps", type=int, default=20,
                     help="timed steps of the full training-step leg (0 = skip)")
     ap.add_argument("--sweep", default="32,128,512,2048",
@@ -579,6 +592,8 @@ def main():
     ap.add_argument("--cpu-batch", type=int, default=128,
                     help="sequences per iteration of the CPU proxy baseline")
     args = ap.parse_args()
+    global ADAMW
+    ADAMW = args.adamw
     progress("start")
 
     from mygenerativerecommenders_amd import _lib
@@ -610,12 +625,7 @@ def main():
     N = N0 + out_len
     enc = build_model(N0, out_len, D, blocks, device)
     reducer = FlatGradAllReducer(list(enc.parameters()))
-    try:  # one fused multi-tensor kernel per step (same AdamW math), graph-capturable
-        opt = torch.optim.AdamW(enc.parameters(), lr=1e-3, betas=(0.9, 0.98), weight_decay=1e-3,
-                                fused=True, capturable=True)
-    except (RuntimeError, TypeError, ValueError):
-        opt = torch.optim.AdamW(enc.parameters(), lr=1e-3, betas=(0.9, 0.98), weight_decay=1e-3,
-                                capturable=True)
+    opt = make_adamw(list(enc.parameters()), lr=1e-3, betas=(0.9, 0.98), weight_decay=1e-3)
     lengths, x, ts, past_ids, dy = make_batch(B, N0, out_len, D, 1000 + rank, device)
     x.requires_grad_(True)
     # ml-1m catalog (ids 1..3953, L2-normalised rows as Retrieval.on_validation_epoch_start)
@@ -1108,6 +1118,8 @@ def main():
             "config": {"workload": "ml-1m-hstu train step: HSTU 4 blocks d=50 h=1 fwd+bwd "
                                    "(+grad all-reduce, AdamW) + top-200 retrieval over 3953 items",
                        "execution": "eager" if args.eager else "hip-graph replay (2 graphs around the all-reduce)",
+                       "optimizer": ("AdamW, one launch (optim.FlatAdamW)" if ADAMW == "flat" else
+                                     "torch.optim.AdamW(fused=True, capturable=True)"),
                        "global_batch": B * world, "seq_len": N0, "padded_len": N,
                        "parallelism": f"dp{world}"},
             "roofline": roofline,

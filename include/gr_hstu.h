@@ -44,7 +44,7 @@ GR_API int gr_version(void);
  * (attention + layer boundary), attn_fwd_bnd1 (+ gate_o of the last layer), attn_bwd_dq_bnd
  * (dQ + layer boundary), attn_bwd_dq_bnd1 (+ ln_uvqk_bwd of the first layer),
  * attn_bias_reduce, ln_uvqk_fwd, gate_o_fwd, gate_o_bwd, ln_uvqk_bwd, wgrad_partial,
- * wgrad_reduce, mips_pack, mips_select, mips_merge, cumsum, dense_to_jagged, encoder_prologue, bf16_scale_add,
+ * wgrad_reduce, mips_pack, mips_select, mips_merge, cumsum, dense_to_jagged, encoder_prologue, bf16_scale_add, adamw,
  * jagged_to_padded, l2_normalize, current_embeddings, sampled_softmax_fwd,
  * sampled_softmax_bwd, sampled_softmax_csr, sampled_softmax_table_grad, preproc.  Not for use inside a captured graph.
  */
@@ -254,6 +254,23 @@ GR_API int gr_sampled_softmax_bwd(const float* out, int64_t ld_out, const float*
  * X = a*X + B@X) with the reference's two roundings, in one launch.  out may alias x or y. */
 GR_API int gr_bf16_scale_add(const uint16_t* x, float s, const uint16_t* y, uint16_t* out,
                              int64_t n, void* stream);
+
+/* gr_adamw_step (ABI 17): torch.optim.AdamW's update (fused=True, capturable=True: the
+ * reference's optimizer) over n_tensors fp32 tensors in ONE launch per 48 tensors, the
+ * step counter advanced inside the last one (torch: the step-count _foreach_add_ launch +
+ * the fused kernel).  params / grads / offs / numel: host arrays; tensor i is
+ * params[i][0 .. numel[i]) with its gradient grads[i] and its moments at exp_avg /
+ * exp_avg_sq + offs[i] (flat fp32 buffers); numel[i] == 0 skips it.  The pointers go into
+ * the kernel arguments, so a captured graph replays the ones it was captured with.  step:
+ * one fp32 counter (read as t - 1, written t); done: one uint32 completion counter, zero
+ * before the first call (the kernel re-arms it).
+ *   p -= lr wd p;  m = b1 m + (1 - b1) g;  v = b2 v + (1 - b2) g g;
+ *   p -= (lr / (1 - b1^t)) m / (sqrt(v) / sqrt(1 - b2^t) + eps)
+ * with ATen's promotion of the double hyper-parameters against the fp32 tensors. */
+GR_API int gr_adamw_step(float* const* params, const float* const* grads, const int64_t* offs,
+                         const int64_t* numel, int n_tensors, float* exp_avg, float* exp_avg_sq,
+                         float* step, uint32_t* done, double lr, double beta1, double beta2,
+                         double eps, double weight_decay, void* stream);
 
 /* ---------------------------------------------------------------- HSTU attention
  * hstu_bucket_map: the relative-time bucket of every causal (query i, key j) pair of

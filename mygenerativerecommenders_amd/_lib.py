@@ -27,6 +27,7 @@ _CTYPES = {
     "uint64_t": ctypes.c_uint64,
     "size_t": ctypes.c_size_t,
     "float": ctypes.c_float,
+    "double": ctypes.c_double,
     "const char*": ctypes.c_char_p,
 }
 
@@ -110,7 +111,7 @@ KERNEL_NAMES = ("bucket_map", "attn_fwd", "attn_bwd", "attn_bwd_dkv", "attn_bwd_
                 "ln_uvqk_fwd", "gate_o_fwd", "gate_o_bwd", "ln_uvqk_bwd", "boundary_fwd", "boundary_bwd",
                 "wgrad_partial",
                 "wgrad_reduce", "mips_pack", "mips_select", "mips_merge", "mips_small", "mips_sample", "mips_tau",
-                "mips_filter", "mips_select_fallback", "mips_merge_fallback", "cumsum", "encoder_prologue", "bf16_scale_add",
+                "mips_filter", "mips_select_fallback", "mips_merge_fallback", "cumsum", "encoder_prologue", "bf16_scale_add", "adamw",
                 "dense_to_jagged", "jagged_to_padded", "l2_normalize", "current_embeddings",
                 "sampled_softmax_fwd", "sampled_softmax_bwd", "sampled_softmax_csr",
                 "sampled_softmax_table_grad", "preproc", "item_embedding", "mips_sort_invalid",

@@ -6,6 +6,9 @@
 // so the chain's result is bit-identical (tests/test_gpu_next_rows.py).  Any other
 // rounding (a GEMM epilogue with beta, a single-rounding axpy) moves the orthogonalised
 // update by ~5 % of its largest entry: the bf16 chain amplifies it.
+#include <algorithm>
+#include <vector>
+
 #include "common.h"
 
 #include "../../include/gr_hstu.h"
@@ -67,5 +70,188 @@ extern "C" int gr_bf16_scale_add(const uint16_t* x, float s, const uint16_t* y, 
     GR_TIMED("bf16_scale_add", st, hipLaunchKernelGGL(gr::bf16_scale_add_tail_kernel, dim3((unsigned)((rest + 255) / 256)),
                                                       dim3(256), 0, st, x, s, y, out, n8 * 8, n));
   GR_LAUNCH_CHECK("gr_bf16_scale_add");
+  return 0;
+}
+
+// ------------------------------------------------------------------ AdamW, one launch
+// torch.optim.AdamW(fused=True, capturable=True)'s update (the reference's optimizer,
+// configs/model/*.yaml) over a parameter list in ONE launch, with the step counter
+// advanced inside it.  torch runs it as two launches per step (the step-count
+// _foreach_add_ and the fused multi-tensor kernel).  The tensors travel in the kernel
+// arguments (so a captured graph replays the pointers it was captured with, as torch's
+// tensor lists do), up to ADAMW_MAX per launch; workgroup w takes chunk w of the
+// concatenated list (ADAMW_CHUNK elements, never crossing a tensor).  Scalar
+// hyper-parameters are doubles and tensors fp32, with the arithmetic promoted as in
+// ATen's FusedAdamMathFunctor (ADAMW mode).  In the launch that advances the counter,
+// the last workgroup to finish (a completion counter the caller zeroes once; the kernel
+// re-arms it) writes step + 1, so every workgroup reads the same step.
+namespace gr {
+constexpr int ADAMW_MAX = 48;
+constexpr int ADAMW_CHUNK = 4096;
+struct AdamWArgs {
+  float* param[ADAMW_MAX];
+  const float* grad[ADAMW_MAX];
+  int64_t off[ADAMW_MAX];   // into exp_avg / exp_avg_sq
+  int64_t n[ADAMW_MAX];
+  int first_chunk[ADAMW_MAX + 1];
+  int n_tensors;
+  int advance;              // this launch writes step + 1
+  float* exp_avg;
+  float* exp_avg_sq;
+  float* step;
+  uint32_t* done;
+  double lr, beta1, beta2, eps, wd;
+};
+
+__device__ __forceinline__ void adamw_elem(const AdamWArgs& a, float step_size, float bc2_sqrt,
+                                           float& p, float g, float& m, float& v) {
+  if (a.wd != 0.0) p = (float)((double)p - a.lr * a.wd * (double)p);
+  m = (float)(a.beta1 * (double)m + (1.0 - a.beta1) * (double)g);
+  v = (float)(a.beta2 * (double)v + (1.0 - a.beta2) * (double)g * (double)g);
+  const float denom = (float)((double)(sqrtf(v) / bc2_sqrt) + a.eps);
+  p = p - step_size * m / denom;
+}
+
+__global__ __launch_bounds__(256) void adamw_kernel(AdamWArgs a) {
+  __shared__ int last;
+  __shared__ float sc[4];  // t, step size, sqrt(1 - b2^t): the double pow()s once per workgroup
+  const int w = blockIdx.x;
+  int t = 0;
+  while (t + 1 < a.n_tensors && a.first_chunk[t + 1] <= w) ++t;  // wave-uniform
+  const int64_t c0 = (int64_t)(w - a.first_chunk[t]) * ADAMW_CHUNK;
+  const int64_t cn = a.n[t] - c0 < ADAMW_CHUNK ? a.n[t] - c0 : ADAMW_CHUNK;
+  float* param = a.param[t] + c0;
+  const float* grad = a.grad[t] + c0;
+  float* ma = a.exp_avg + a.off[t] + c0;
+  float* va = a.exp_avg_sq + a.off[t] + c0;
+  // 16 elements per thread: four float4 per operand where the chunk allows (16-byte
+  // aligned, a multiple of 4 long), scalars otherwise.  Every data load is issued before
+  // the step counter is read, so a workgroup waits one round trip, not two.
+  constexpr int PER = ADAMW_CHUNK / 256;
+  const bool vec = (cn & 3) == 0 && ((reinterpret_cast<uintptr_t>(param) | reinterpret_cast<uintptr_t>(grad) |
+                                      reinterpret_cast<uintptr_t>(ma) | reinterpret_cast<uintptr_t>(va)) & 15) == 0;
+  float p[PER], g[PER], m[PER], v[PER];
+  auto idx = [&](int e) -> int64_t {  // element e of the thread (vec: 4 consecutive per float4)
+    return vec ? 4 * ((int64_t)threadIdx.x + 256 * (e >> 2)) + (e & 3) : (int64_t)threadIdx.x + 256 * e;
+  };
+  if (vec) {
+#pragma unroll
+    for (int q = 0; q < PER / 4; ++q) {
+      const int64_t i4 = (int64_t)threadIdx.x + 256 * q;
+      const bool in = 4 * i4 < cn;
+      const float4 pv = in ? reinterpret_cast<const float4*>(param)[i4] : float4{};
+      const float4 gv = in ? reinterpret_cast<const float4*>(grad)[i4] : float4{};
+      const float4 mv = in ? reinterpret_cast<const float4*>(ma)[i4] : float4{};
+      const float4 vv = in ? reinterpret_cast<const float4*>(va)[i4] : float4{};
+      p[4 * q] = pv.x; p[4 * q + 1] = pv.y; p[4 * q + 2] = pv.z; p[4 * q + 3] = pv.w;
+      g[4 * q] = gv.x; g[4 * q + 1] = gv.y; g[4 * q + 2] = gv.z; g[4 * q + 3] = gv.w;
+      m[4 * q] = mv.x; m[4 * q + 1] = mv.y; m[4 * q + 2] = mv.z; m[4 * q + 3] = mv.w;
+      v[4 * q] = vv.x; v[4 * q + 1] = vv.y; v[4 * q + 2] = vv.z; v[4 * q + 3] = vv.w;
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < PER; ++e) {
+      const int64_t i = idx(e);
+      const bool in = i < cn;
+      p[e] = in ? param[i] : 0.f;
+      g[e] = in ? grad[i] : 0.f;
+      m[e] = in ? ma[i] : 0.f;
+      v[e] = in ? va[i] : 0.f;
+    }
+  }
+  if (threadIdx.x == 0) {
+    const float ts = a.step[0] + 1.f;
+    const float bc1 = (float)(1.0 - pow(a.beta1, (double)ts));
+    const float bc2 = (float)(1.0 - pow(a.beta2, (double)ts));
+    sc[0] = ts;
+    sc[1] = (float)(a.lr / (double)bc1);
+    sc[2] = sqrtf(bc2);
+  }
+  __syncthreads();
+  const float ts = sc[0], step_size = sc[1], bc2_sqrt = sc[2];
+#pragma unroll
+  for (int e = 0; e < PER; ++e) adamw_elem(a, step_size, bc2_sqrt, p[e], g[e], m[e], v[e]);
+  if (vec) {
+#pragma unroll
+    for (int q = 0; q < PER / 4; ++q) {
+      const int64_t i4 = (int64_t)threadIdx.x + 256 * q;
+      if (4 * i4 < cn) {
+        reinterpret_cast<float4*>(param)[i4] = float4{p[4 * q], p[4 * q + 1], p[4 * q + 2], p[4 * q + 3]};
+        reinterpret_cast<float4*>(ma)[i4] = float4{m[4 * q], m[4 * q + 1], m[4 * q + 2], m[4 * q + 3]};
+        reinterpret_cast<float4*>(va)[i4] = float4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+      }
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < PER; ++e) {
+      const int64_t i = idx(e);
+      if (i < cn) {
+        param[i] = p[e];
+        ma[i] = m[e];
+        va[i] = v[e];
+      }
+    }
+  }
+  if (!a.advance) return;
+  // completion: the last workgroup advances the step and re-arms the counter.  Relaxed:
+  // the increment only has to follow this workgroup's read of the step (thread 0 consumed
+  // it before the barrier above); the parameter and moment stores need no ordering inside
+  // the launch (an agent-scope release per workgroup: 0.60 against 0.19 ms for a 33.6 M
+  // element table, scripts/adamw_micro.py)
+  if (threadIdx.x == 0) {
+    last = __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    if (last) {
+      a.step[0] = ts;
+      __hip_atomic_store(a.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+}  // namespace gr
+
+extern "C" int gr_adamw_step(float* const* params, const float* const* grads, const int64_t* offs,
+                             const int64_t* numel, int n_tensors, float* exp_avg, float* exp_avg_sq,
+                             float* step, uint32_t* done, double lr, double beta1, double beta2,
+                             double eps, double weight_decay, void* stream) {
+  GR_REQUIRE(n_tensors >= 0 && (n_tensors == 0 || (params && grads && offs && numel && exp_avg &&
+                                                   exp_avg_sq && step && done)),
+             "gr_adamw_step: bad args");
+  const hipStream_t st = (hipStream_t)stream;
+  // launches of up to ADAMW_MAX tensors; the last one advances the counter
+  std::vector<int> idx;
+  for (int i = 0; i < n_tensors; ++i) {
+    GR_REQUIRE(numel[i] >= 0 && offs[i] >= 0 && (numel[i] == 0 || (params[i] && grads[i])),
+               "gr_adamw_step: tensor %d: bad pointer / size", i);
+    if (numel[i] > 0) idx.push_back(i);
+  }
+  if (idx.empty()) return 0;
+  for (size_t b = 0; b < idx.size(); b += gr::ADAMW_MAX) {
+    gr::AdamWArgs a{};
+    int chunks = 0;
+    a.n_tensors = (int)std::min(idx.size() - b, (size_t)gr::ADAMW_MAX);
+    for (int j = 0; j < a.n_tensors; ++j) {
+      const int i = idx[b + j];
+      a.param[j] = params[i];
+      a.grad[j] = grads[i];
+      a.off[j] = offs[i];
+      a.n[j] = numel[i];
+      a.first_chunk[j] = chunks;
+      const int64_t c = (numel[i] + gr::ADAMW_CHUNK - 1) / gr::ADAMW_CHUNK;
+      GR_REQUIRE(chunks + c < 0x7fffffff, "gr_adamw_step: too many chunks");
+      chunks += (int)c;
+    }
+    a.first_chunk[a.n_tensors] = chunks;
+    a.advance = b + gr::ADAMW_MAX >= idx.size();
+    a.exp_avg = exp_avg;
+    a.exp_avg_sq = exp_avg_sq;
+    a.step = step;
+    a.done = done;
+    a.lr = lr;
+    a.beta1 = beta1;
+    a.beta2 = beta2;
+    a.eps = eps;
+    a.wd = weight_decay;
+    GR_TIMED("adamw", st, hipLaunchKernelGGL(gr::adamw_kernel, dim3((unsigned)chunks), dim3(256), 0, st, a));
+  }
+  GR_LAUNCH_CHECK("gr_adamw_step");
   return 0;
 }

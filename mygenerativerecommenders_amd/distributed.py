@@ -249,19 +249,24 @@ class BucketedGradReducer:
 
 def muon_adamw_split(named_params, muon_lr=5e-3, muon_momentum=0.95, muon_wd=5e-3,
                      adam_lr=5e-4, adam_betas=(0.8, 0.95), adam_eps=1e-10, adam_wd=5e-3,
-                     **adam_kwargs):
+                     flat_adam: bool = False, **adam_kwargs):
     """The reference's two-optimizer split (generative_recommenders.py:297-310,
     configs/experiment/ml-1m-hstu-muon.yaml:23-36): parameters whose name contains
     "emb" and every parameter with ndim < 2 -> AdamW; the remaining matrices -> Muon.
     ``named_params``: iterable of (name, parameter).  Returns [AdamW, Muon] (the
-    reference's optimizer1, optimizer2), skipping an empty group."""
+    reference's optimizer1, optimizer2), skipping an empty group.  ``flat_adam``: the
+    AdamW group as ``optim.FlatAdamW`` (the same update in one launch; ``adam_kwargs``
+    such as fused / capturable are then not used)."""
     from .muon import Muon
     named = [(n, p) for n, p in named_params if p.requires_grad]
     adam = [p for n, p in named if "emb" in n or p.ndim < 2]
     ids = {id(p) for p in adam}
     mats = [p for n, p in named if id(p) not in ids]
     opts = []
-    if adam:
+    if adam and flat_adam:
+        from .optim import FlatAdamW
+        opts.append(FlatAdamW(adam, lr=adam_lr, betas=adam_betas, eps=adam_eps, weight_decay=adam_wd))
+    elif adam:
         opts.append(torch.optim.AdamW(adam, lr=adam_lr, betas=adam_betas, eps=adam_eps,
                                       weight_decay=adam_wd, **adam_kwargs))
     if mats:

@@ -19,6 +19,9 @@ from typing import Dict, List, Tuple
 import torch
 
 _NS_COEFFS = (3.4445, -4.7750, 2.0315)
+# the GPU chain's combines as gr_bf16_scale_add launches (False: the reference's torch ops;
+# the results are bit-identical, tests/test_gpu_next_rows.py)
+FUSED_COMBINE = True
 
 
 def _scale_add(x: torch.Tensor, s: float, y: torch.Tensor) -> torch.Tensor:
@@ -43,7 +46,7 @@ def zeropower_via_newtonschulz5(G: torch.Tensor, steps: int) -> torch.Tensor:
     if tall:
         X = X.mT
     X = X / (X.norm(dim=(-2, -1), keepdim=True) + 1e-7)
-    fused = X.is_cuda
+    fused = X.is_cuda and FUSED_COMBINE
     for _ in range(steps):
         A = X @ X.mT
         if fused:
