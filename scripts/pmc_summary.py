@@ -64,6 +64,10 @@ _MAP = [
     # the exact path's merge: gated on the filter path's flag (C4), timed as mips_merge_fallback
     (r"mips_merge_kernel", "mips_merge_fallback"),
     (r"cumsum_kernel", "cumsum"),
+    (r"encoder_prologue_kernel", "encoder_prologue"),
+    (r"weight_image_kernel", "weight_images"),
+    (r"bf16_scale_add", "bf16_scale_add"),
+    (r"adamw_kernel", "adamw"),
     (r"dense_to_jagged_kernel", "dense_to_jagged"),
     (r"jagged_to_padded_kernel", "jagged_to_padded"),
 ]
