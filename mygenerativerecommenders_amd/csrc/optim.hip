@@ -80,20 +80,22 @@ extern "C" int gr_bf16_scale_add(const uint16_t* x, float s, const uint16_t* y, 
 // _foreach_add_ and the fused multi-tensor kernel).  The tensors travel in the kernel
 // arguments (so a captured graph replays the pointers it was captured with, as torch's
 // tensor lists do), up to ADAMW_MAX per launch; workgroup w takes chunk w of the
-// concatenated list (ADAMW_CHUNK elements, never crossing a tensor).  Scalar
+// concatenated list (`chunk` elements, never crossing a tensor; chosen per call so that
+// small lists get many workgroups and large tables few enough passes).  Scalar
 // hyper-parameters are doubles and tensors fp32, with the arithmetic promoted as in
 // ATen's FusedAdamMathFunctor (ADAMW mode).  In the launch that advances the counter,
 // the last workgroup to finish (a completion counter the caller zeroes once; the kernel
 // re-arms it) writes step + 1, so every workgroup reads the same step.
 namespace gr {
 constexpr int ADAMW_MAX = 48;
-constexpr int ADAMW_CHUNK = 4096;
+constexpr int ADAMW_SUB = 1024;  // elements per workgroup pass (4 per thread)
 struct AdamWArgs {
   float* param[ADAMW_MAX];
   const float* grad[ADAMW_MAX];
   int64_t off[ADAMW_MAX];   // into exp_avg / exp_avg_sq
   int64_t n[ADAMW_MAX];
   int first_chunk[ADAMW_MAX + 1];
+  int64_t chunk;            // elements per workgroup: a multiple of ADAMW_SUB
   int n_tensors;
   int advance;              // this launch writes step + 1
   float* exp_avg;
@@ -118,47 +120,67 @@ __global__ __launch_bounds__(256) void adamw_kernel(AdamWArgs a) {
   const int w = blockIdx.x;
   int t = 0;
   while (t + 1 < a.n_tensors && a.first_chunk[t + 1] <= w) ++t;  // wave-uniform
-  const int64_t c0 = (int64_t)(w - a.first_chunk[t]) * ADAMW_CHUNK;
-  const int64_t cn = a.n[t] - c0 < ADAMW_CHUNK ? a.n[t] - c0 : ADAMW_CHUNK;
-  float* param = a.param[t] + c0;
-  const float* grad = a.grad[t] + c0;
-  float* ma = a.exp_avg + a.off[t] + c0;
-  float* va = a.exp_avg_sq + a.off[t] + c0;
-  // 16 elements per thread: four float4 per operand where the chunk allows (16-byte
-  // aligned, a multiple of 4 long), scalars otherwise.  Every data load is issued before
-  // the step counter is read, so a workgroup waits one round trip, not two.
-  constexpr int PER = ADAMW_CHUNK / 256;
-  const bool vec = (cn & 3) == 0 && ((reinterpret_cast<uintptr_t>(param) | reinterpret_cast<uintptr_t>(grad) |
-                                      reinterpret_cast<uintptr_t>(ma) | reinterpret_cast<uintptr_t>(va)) & 15) == 0;
-  float p[PER], g[PER], m[PER], v[PER];
-  auto idx = [&](int e) -> int64_t {  // element e of the thread (vec: 4 consecutive per float4)
-    return vec ? 4 * ((int64_t)threadIdx.x + 256 * (e >> 2)) + (e & 3) : (int64_t)threadIdx.x + 256 * e;
+  const int64_t c0 = (int64_t)(w - a.first_chunk[t]) * a.chunk;
+  const int64_t cend = a.n[t] < c0 + a.chunk ? a.n[t] : c0 + a.chunk;
+  float* param = a.param[t];
+  const float* grad = a.grad[t];
+  float* ma = a.exp_avg + a.off[t];
+  float* va = a.exp_avg_sq + a.off[t];
+  // sub-chunks of ADAMW_SUB elements, 4 per thread: one float4 per operand where the tensor
+  // allows (16-byte aligned, a multiple of 4 long), scalars otherwise.  The first
+  // sub-chunk's loads are issued before the step counter is read, so a workgroup starts
+  // after one round trip, not two.
+  const bool vec = (a.n[t] & 3) == 0 && ((reinterpret_cast<uintptr_t>(param) | reinterpret_cast<uintptr_t>(grad) |
+                                          reinterpret_cast<uintptr_t>(ma) | reinterpret_cast<uintptr_t>(va)) & 15) == 0;
+  float p[4], g[4], m[4], v[4];
+  auto elem = [&](int64_t s0, int e) -> int64_t {
+    return vec ? s0 + 4 * (int64_t)threadIdx.x + e : s0 + (int64_t)threadIdx.x + 256 * e;
   };
-  if (vec) {
+  auto load = [&](int64_t s0) {
+    if (vec) {
+      const int64_t i = s0 + 4 * (int64_t)threadIdx.x;
+      const bool in = i < cend;
+      const float4 pv = in ? *reinterpret_cast<const float4*>(param + i) : float4{};
+      const float4 gv = in ? *reinterpret_cast<const float4*>(grad + i) : float4{};
+      const float4 mv = in ? *reinterpret_cast<const float4*>(ma + i) : float4{};
+      const float4 vv = in ? *reinterpret_cast<const float4*>(va + i) : float4{};
+      p[0] = pv.x; p[1] = pv.y; p[2] = pv.z; p[3] = pv.w;
+      g[0] = gv.x; g[1] = gv.y; g[2] = gv.z; g[3] = gv.w;
+      m[0] = mv.x; m[1] = mv.y; m[2] = mv.z; m[3] = mv.w;
+      v[0] = vv.x; v[1] = vv.y; v[2] = vv.z; v[3] = vv.w;
+    } else {
 #pragma unroll
-    for (int q = 0; q < PER / 4; ++q) {
-      const int64_t i4 = (int64_t)threadIdx.x + 256 * q;
-      const bool in = 4 * i4 < cn;
-      const float4 pv = in ? reinterpret_cast<const float4*>(param)[i4] : float4{};
-      const float4 gv = in ? reinterpret_cast<const float4*>(grad)[i4] : float4{};
-      const float4 mv = in ? reinterpret_cast<const float4*>(ma)[i4] : float4{};
-      const float4 vv = in ? reinterpret_cast<const float4*>(va)[i4] : float4{};
-      p[4 * q] = pv.x; p[4 * q + 1] = pv.y; p[4 * q + 2] = pv.z; p[4 * q + 3] = pv.w;
-      g[4 * q] = gv.x; g[4 * q + 1] = gv.y; g[4 * q + 2] = gv.z; g[4 * q + 3] = gv.w;
-      m[4 * q] = mv.x; m[4 * q + 1] = mv.y; m[4 * q + 2] = mv.z; m[4 * q + 3] = mv.w;
-      v[4 * q] = vv.x; v[4 * q + 1] = vv.y; v[4 * q + 2] = vv.z; v[4 * q + 3] = vv.w;
+      for (int e = 0; e < 4; ++e) {
+        const int64_t i = elem(s0, e);
+        const bool in = i < cend;
+        p[e] = in ? param[i] : 0.f;
+        g[e] = in ? grad[i] : 0.f;
+        m[e] = in ? ma[i] : 0.f;
+        v[e] = in ? va[i] : 0.f;
+      }
     }
-  } else {
+  };
+  auto store = [&](int64_t s0) {
+    if (vec) {
+      const int64_t i = s0 + 4 * (int64_t)threadIdx.x;
+      if (i < cend) {
+        *reinterpret_cast<float4*>(param + i) = float4{p[0], p[1], p[2], p[3]};
+        *reinterpret_cast<float4*>(ma + i) = float4{m[0], m[1], m[2], m[3]};
+        *reinterpret_cast<float4*>(va + i) = float4{v[0], v[1], v[2], v[3]};
+      }
+    } else {
 #pragma unroll
-    for (int e = 0; e < PER; ++e) {
-      const int64_t i = idx(e);
-      const bool in = i < cn;
-      p[e] = in ? param[i] : 0.f;
-      g[e] = in ? grad[i] : 0.f;
-      m[e] = in ? ma[i] : 0.f;
-      v[e] = in ? va[i] : 0.f;
+      for (int e = 0; e < 4; ++e) {
+        const int64_t i = elem(s0, e);
+        if (i < cend) {
+          param[i] = p[e];
+          ma[i] = m[e];
+          va[i] = v[e];
+        }
+      }
     }
-  }
+  };
+  load(c0);
   if (threadIdx.x == 0) {
     const float ts = a.step[0] + 1.f;
     const float bc1 = (float)(1.0 - pow(a.beta1, (double)ts));
@@ -169,28 +191,11 @@ __global__ __launch_bounds__(256) void adamw_kernel(AdamWArgs a) {
   }
   __syncthreads();
   const float ts = sc[0], step_size = sc[1], bc2_sqrt = sc[2];
+  for (int64_t s0 = c0; s0 < cend; s0 += ADAMW_SUB) {
+    if (s0 != c0) load(s0);
 #pragma unroll
-  for (int e = 0; e < PER; ++e) adamw_elem(a, step_size, bc2_sqrt, p[e], g[e], m[e], v[e]);
-  if (vec) {
-#pragma unroll
-    for (int q = 0; q < PER / 4; ++q) {
-      const int64_t i4 = (int64_t)threadIdx.x + 256 * q;
-      if (4 * i4 < cn) {
-        reinterpret_cast<float4*>(param)[i4] = float4{p[4 * q], p[4 * q + 1], p[4 * q + 2], p[4 * q + 3]};
-        reinterpret_cast<float4*>(ma)[i4] = float4{m[4 * q], m[4 * q + 1], m[4 * q + 2], m[4 * q + 3]};
-        reinterpret_cast<float4*>(va)[i4] = float4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
-      }
-    }
-  } else {
-#pragma unroll
-    for (int e = 0; e < PER; ++e) {
-      const int64_t i = idx(e);
-      if (i < cn) {
-        param[i] = p[e];
-        ma[i] = m[e];
-        va[i] = v[e];
-      }
-    }
+    for (int e = 0; e < 4; ++e) adamw_elem(a, step_size, bc2_sqrt, p[e], g[e], m[e], v[e]);
+    store(s0);
   }
   if (!a.advance) return;
   // completion: the last workgroup advances the step and re-arms the counter.  Relaxed:
@@ -224,8 +229,15 @@ extern "C" int gr_adamw_step(float* const* params, const float* const* grads, co
     if (numel[i] > 0) idx.push_back(i);
   }
   if (idx.empty()) return 0;
+  int64_t total = 0;
+  for (int i : idx) total += numel[i];
+  // >= ~4096 workgroups' worth of passes before a workgroup takes more than one
+  int64_t subs = total / ((int64_t)gr::ADAMW_SUB * 4096) + 1;
+  subs = subs > 8 ? 8 : subs;
+  const int64_t chunk = gr::ADAMW_SUB * subs;
   for (size_t b = 0; b < idx.size(); b += gr::ADAMW_MAX) {
     gr::AdamWArgs a{};
+    a.chunk = chunk;
     int chunks = 0;
     a.n_tensors = (int)std::min(idx.size() - b, (size_t)gr::ADAMW_MAX);
     for (int j = 0; j < a.n_tensors; ++j) {
@@ -235,7 +247,7 @@ extern "C" int gr_adamw_step(float* const* params, const float* const* grads, co
       a.off[j] = offs[i];
       a.n[j] = numel[i];
       a.first_chunk[j] = chunks;
-      const int64_t c = (numel[i] + gr::ADAMW_CHUNK - 1) / gr::ADAMW_CHUNK;
+      const int64_t c = (numel[i] + chunk - 1) / chunk;
       GR_REQUIRE(chunks + c < 0x7fffffff, "gr_adamw_step: too many chunks");
       chunks += (int)c;
     }
