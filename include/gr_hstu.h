@@ -121,7 +121,10 @@ GR_API int gr_timing_reset(void);
  *                                  Workspace queries cover both forms.
  *   GR_OPT_BOUNDARY_FUSE      0|1  hstu_attn_bwd_bnd: the layer boundary as the epilogue of
  *                                  the dQ launch where the shapes allow (default 1), or the
- *                                  attention backward and the boundary as separate calls (0)
+ *                                  attention backward and the boundary as separate calls (0).
+ *                                  The epilogue exists on the two-pass dS path only
+ *                                  (GR_OPT_ATTN_BWD_DS = 1 with a bucket map); other forms
+ *                                  run the separate calls whatever this option says
  */
 enum {
   GR_OPT_MIPS_FILTER_FP32 = 1,

@@ -455,10 +455,11 @@ def test_hstu_stack_boundaries_match_unfused(B, N0, D, hdv, blocks, act, dropout
         close(g0[n], g1[n], n)
 
 
-@pytest.mark.parametrize("B,N0,D,hdv,blocks", [(16, 200, 50, 50, 3), (6, 70, 64, 64, 2),
-                                                (5, 40, 48, 40, 2), (4, 96, 256, 256, 2),
-                                                (8, 64, 50, 20, 2)])
-def test_hstu_boundary_as_dq_epilogue_matches_separate(B, N0, D, hdv, blocks):
+@pytest.mark.parametrize("B,N0,D,hdv,blocks,rab", [(16, 200, 50, 50, 3, True), (6, 70, 64, 64, 2, True),
+                                                    (5, 40, 48, 40, 2, True), (4, 96, 256, 256, 2, True),
+                                                    (8, 64, 50, 20, 2, True), (16, 200, 50, 50, 3, False),
+                                                    (6, 70, 64, 64, 2, False)])
+def test_hstu_boundary_as_dq_epilogue_matches_separate(B, N0, D, hdv, blocks, rab):
     """hstu_attn_bwd_bnd runs the layer boundary (ln_uvqk_bwd(l) + gate_o_bwd(l - 1), or
     ln_uvqk_bwd(0) alone) as the epilogue of the attention dQ launch at narrow single-head
     shapes (GR_OPT_BOUNDARY_FUSE, default on), against the attention backward and the
@@ -467,9 +468,10 @@ def test_hstu_boundary_as_dq_epilogue_matches_separate(B, N0, D, hdv, blocks):
     order; hipcc may contract multiply-adds differently inside another kernel: the forward
     agrees to 1e-6 relative), and the first layer's ln_uvqk_bwd alone may take the row
     panel when separate (n_out > 128), so gradients agree to fp32 summation order: 2e-5
-    relative.  Also the forward epilogue (hstu_attn_fwd_bnd) is exercised here.
-    Shapes the epilogue does not cover (D = 256; h dv = 20) run the separate launches
-    inside the call and are bit-identical."""
+    relative.  Also the forward epilogue (hstu_attn_fwd_bnd) is exercised here, with and
+    without the relative bias (rab = False: the no-bucket-map instantiations), n_out = 4 h dv
+    up to 256 (h dv = 64).  Shapes the epilogue does not cover (D = 256; h dv = 20) run the
+    separate launches inside the call and are bit-identical."""
     from mygenerativerecommenders_amd import _lib
     from mygenerativerecommenders_amd.hstu import HSTU
     torch.manual_seed(3)
@@ -479,7 +481,7 @@ def test_hstu_boundary_as_dq_epilogue_matches_separate(B, N0, D, hdv, blocks):
                item_embedding_dim=D, num_blocks=blocks, num_heads=1, linear_dim=hdv,
                attention_dim=hdv, normalization="rel_bias", linear_config="uvqk",
                linear_activation="silu", linear_dropout_rate=0.2,
-               attn_dropout_rate=0.0).cuda().train()
+               attn_dropout_rate=0.0, enable_relative_attention_bias=rab).cuda().train()
     g = torch.Generator().manual_seed(11)
     lengths = torch.randint(1, N0 + 1, (B,), generator=g)
     lengths[0] = N0
