@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define GR_HSTU_ABI_VERSION 17
+#define GR_HSTU_ABI_VERSION 18
 
 #ifndef GR_API
 #define GR_API __attribute__((visibility("default")))
@@ -46,7 +46,8 @@ GR_API int gr_version(void);
  * attn_bias_reduce, ln_uvqk_fwd, gate_o_fwd, gate_o_bwd, ln_uvqk_bwd, wgrad_partial,
  * wgrad_reduce, mips_pack, mips_select, mips_merge, cumsum, dense_to_jagged, encoder_prologue, bf16_scale_add, adamw,
  * jagged_to_padded, l2_normalize, current_embeddings, sampled_softmax_fwd,
- * sampled_softmax_bwd, sampled_softmax_csr, sampled_softmax_table_grad, preproc.  Not for use inside a captured graph.
+ * sampled_softmax_bwd, sampled_softmax_csr, sampled_softmax_table_grad, preproc, rows_copy,
+ * decode_attn.  Not for use inside a captured graph.
  */
 GR_API int gr_timing_enable(int on);
 GR_API int gr_timing_query(const char* kernel, double* total_ms, int* launches);
@@ -303,6 +304,40 @@ GR_API int hstu_encoder_prologue(const int64_t* lengths, int B, int N, const flo
                                  int64_t max_rows, const int64_t* ts, const int64_t* bucket_thr,
                                  int num_buckets, int64_t* offsets, float* x_jagged,
                                  uint8_t* map, int64_t* step, void* stream);
+
+/* ---------------------------------------------------------------- cached decoding (ABI 18)
+ * The delta_x_offsets / cache branch of SequentialTransductionUnitJagged.forward
+ * (sequential_encoders/hstu.py:151-177, 293-298, 321-322, 393-423): a step re-encodes one
+ * jagged row per sequence against per-layer caches (v jagged, q / k padded (B, n, .),
+ * outputs jagged) that a full pass with return_cache_states produced.
+ *
+ * gr_rows_copy (replaces the index_select / index_copy_ row moves of that branch):
+ *   dst[row_d(e)][0:width] = src[row_s(e)][0:width] for e < n,
+ *   row_s(e) = src_index ? src_index[e] + e * src_step : e   (row_d likewise),
+ * rows outside [0, src_rows) / [0, dst_rows) are skipped.  src_step = n gives the
+ * reference's flattened padded index delta[1][e] + e * n (hstu.py:153-159).
+ */
+GR_API int gr_rows_copy(const float* src, int64_t ld_src, const int64_t* src_index,
+                        int64_t src_step, int64_t src_rows, float* dst, int64_t ld_dst,
+                        const int64_t* dst_index, int64_t dst_step, int64_t dst_rows, int n,
+                        int width, void* stream);
+/* hstu_decode_attn (replaces hstu.py:186-205 + 393-397 of the cached branch: the full
+ * (B, h, n, n) attention over the caches of which only the delta rows are kept): for
+ * e < n_rows, h < H, with r = rows[e] in sequence b (offsets[b] <= r < offsets[b + 1])
+ * at position p = r - offsets[b]:
+ *   out[e][h dv + c] = sum_{j <= p} silu(q_cache[b][p] . k_cache[b][j] + bias(b, p, j)) / N
+ *                      * v_cache[offsets[b] + j][h dv + c]
+ * (head h's columns h dqk .. of q / k; bias as hstu_rel_bias_fwd, none when ts is NULL).
+ * q_cache / k_cache (B, N, ld_qk) f32, v_cache (v_rows, ld_v) f32 jagged, out (n_rows,
+ * ld_out).  Rows outside [0, offsets[B]) give zeros.  LDS bound: N up to ~15 K.
+ */
+GR_API size_t hstu_decode_attn_lds_bytes(int N, int dqk, int dv, int num_buckets);
+GR_API int hstu_decode_attn(const float* q_cache, const float* k_cache, int64_t ld_qk,
+                            const float* v_cache, int64_t ld_v, int64_t v_rows,
+                            const int64_t* offsets, int B, const int64_t* rows, int n_rows,
+                            int N, int H, int dqk, int dv, const int64_t* ts,
+                            const int64_t* bucket_thr, int num_buckets, const float* pos_w,
+                            const float* ts_w, float* out, int64_t ld_out, void* stream);
 
 /* hstu_rel_bias_fwd / _bwd (ABI 13) — replaces RelativeBucketedTimeAndPositionBasedBias
  * .forward (sequential_encoders/hstu.py:96-128) for callers that materialise the bias

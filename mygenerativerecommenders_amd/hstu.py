@@ -13,10 +13,15 @@ row-wave kernels with W_o in LDS up to linear_dim * num_heads = 64 and D = 128, 
 streamed-W_o form beyond).  ``autocast_dtype=torch.bfloat16`` (an extension
 of the reference constructor, whose HSTUJagged takes it) selects bf16 MFMA operands.
 
-Not supported (raise): the incremental-decoding cache path (``delta_x_offsets`` /
-``cache``, hstu.py:293-298, 415-418 — used by no config), ``normalization=
-"softmax_rel_bias"`` (hstu.py:341-389 — used by no config) and attention dropout > 0
-(the reference ignores it too).
+Cached (incremental) decoding (hstu.py:151-177, 293-298, 321-322, 415-423):
+``return_cache_states=True`` returns every layer's (v, padded q, padded k, outputs) as the
+reference does; a later call with ``delta_x_offsets`` and ``cache`` re-encodes one row per
+sequence against those caches, updating them in place (``ops.stu_decode``: the delta
+rows' attention only, not the reference's full (B, h, n, n) pass).  The cached step is
+inference-only (it raises under autograd) and computes in fp32 in either mode.
+
+Not supported (raise): ``normalization="softmax_rel_bias"`` (hstu.py:341-389 — used by no
+config) and attention dropout > 0 (the reference ignores it too).
 """
 from __future__ import annotations
 
@@ -199,18 +204,22 @@ class SequentialTransductionUnitJagged(torch.nn.Module):
         bucket_map: Optional[torch.Tensor] = None,
         dropout_step: Optional[torch.Tensor] = None,
     ):
-        """x: (rows, D) jagged; x_offsets (B+1,).  Returns (x', cache-state tuple);
-        cache states are (v, None, None, x') — padded q/k are never built.
+        """x: (rows, D) jagged; x_offsets (B+1,).  Returns (x', cache-state tuple): with
+        ``return_cache_states`` the reference's (v, padded q, padded k, x') over the
+        offsets[B] valid rows (one host sync), else (None, None, None, x').
+        ``delta_x_offsets`` + ``cache``: the cached step (hstu.py:293-298), see
+        ``ops.stu_decode``; the cache tensors are updated in place and returned.
         ``bucket_map`` (optional) is the batch's ``ops.bucket_map`` — pass it to share
         it across layers; otherwise it is built from ``all_timestamps``.
         ``dropout_step`` (optional) is an already-advanced device step counter shared by
         the layers of one encoder forward (one increment per forward instead of one per
         layer); by default the layer advances its own."""
-        if delta_x_offsets is not None or cache is not None:
-            raise NotImplementedError("incremental (cached) HSTU decoding is not supported")
         n = invalid_attn_mask.size(-1)
         geo = self._geometry(n, n if max_len is None else max_len)
         rab = self._rel_attn_bias
+        if delta_x_offsets is not None:
+            return self._decode(x, x_offsets, all_timestamps, delta_x_offsets, cache, geo,
+                                dropout_step)
         bmap = None
         if rab is not None and all_timestamps is not None:
             bmap = bucket_map if bucket_map is not None else ops.bucket_map(
@@ -227,8 +236,34 @@ class SequentialTransductionUnitJagged(torch.nn.Module):
                 self._dropout_step.add_(1)
                 step = self._dropout_step
         y = ops.stu_layer(x, x_offsets, bmap, self._uvqk, self._o.weight, self._o.bias, pos_w,
-                          ts_w, geo, self._dropout_seed, step)
+                          ts_w, geo, self._dropout_seed, step, return_uvqk=return_cache_states)
+        if return_cache_states:
+            y, uvqk = y
+            return y, ops.stu_cache_states(uvqk, y, x_offsets, int(x_offsets[-1]), geo)
         return y, (None, None, None, y)
+
+    def _decode(self, x, x_offsets, all_timestamps, delta_x_offsets, cache, geo, dropout_step):
+        """hstu.py:293-298 (assert cache is not None), 321-322, 151-177, 393-418."""
+        if cache is None:
+            raise ValueError("delta_x_offsets requires the cache states of a previous pass")
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            raise NotImplementedError(
+                "cached HSTU decoding is inference-only (no backward): run it under "
+                "torch.no_grad() or torch.inference_mode()")
+        rab = self._rel_attn_bias
+        step = None
+        if geo.dropout_p > 0:
+            if dropout_step is not None:
+                step = dropout_step
+            else:
+                self._dropout_step.add_(1)
+                step = self._dropout_step
+        out = ops.stu_decode(x, x_offsets, all_timestamps if rab is not None else None,
+                             delta_x_offsets[0], delta_x_offsets[1], cache, self._uvqk,
+                             self._o.weight, self._o.bias,
+                             rab._pos_w if rab is not None else None,
+                             rab._ts_w if rab is not None else None, geo, self._dropout_seed, step)
+        return out, (cache[0], cache[1], cache[2], out)
 
 
 class HSTUJagged(torch.nn.Module):
@@ -266,11 +301,27 @@ class HSTUJagged(torch.nn.Module):
                        delta_x_offsets=None, cache=None, return_cache_states=False,
                        max_len: Optional[int] = None, _prepared=None):
         """``_prepared`` (internal): (bucket map, advanced dropout step) already produced by
-        ops.encoder_prologue."""
-        if delta_x_offsets is not None or cache is not None:
-            raise NotImplementedError("incremental (cached) HSTU decoding is not supported")
+        ops.encoder_prologue.  ``delta_x_offsets`` + ``cache`` (one state tuple per layer):
+        the cached step, layer by layer (hstu.py:467-478)."""
         cache_states: List[HSTUCacheState] = []
         n = invalid_attn_mask.size(-1)
+        if delta_x_offsets is not None:
+            if cache is None or len(cache) != len(self._attention_layers):
+                raise ValueError("delta_x_offsets requires one cache state per layer")
+            d0 = delta_x_offsets[0].to(torch.int64)
+            d1 = delta_x_offsets[1].to(torch.int64)
+            ops.check_decode_step(x_offsets, d0, d1, n)
+            step = None
+            if self._needs_step():
+                self._dropout_step.add_(1)
+                step = self._dropout_step
+            for i, layer in enumerate(self._attention_layers):
+                x, cs = layer(x=x, x_offsets=x_offsets, all_timestamps=all_timestamps,
+                              invalid_attn_mask=invalid_attn_mask, delta_x_offsets=(d0, d1),
+                              cache=cache[i], max_len=max_len, dropout_step=step)
+                if return_cache_states:
+                    cache_states.append(cs)
+            return x, cache_states
         if _prepared is not None:
             bmap, step = _prepared
         else:

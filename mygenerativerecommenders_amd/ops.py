@@ -848,20 +848,25 @@ class STULayerFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGeometry, seed: int,
-                seed_offset, grad_on: bool = True):
+                seed_offset, grad_on: bool = True, want_uvqk: bool = False):
         y, saved, _ = _stu_forward(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo, seed,
                                    seed_offset, grad_on, w_o.requires_grad or b_o.requires_grad)
         ctx.save_for_backward(*saved)
         ctx.geo = geo
         ctx.seed = seed
         ctx.seed_offset = seed_offset
+        if want_uvqk:  # the layer's silu(LN(x) W_uvqk) rows, for the cache states
+            uvqk = saved[8]
+            ctx.mark_non_differentiable(uvqk)
+            return y, uvqk
         return y
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, *_unused):
         dx, d_w_uvqk, d_w_o, d_b_o, d_pos_w, d_ts_w, _, _ = _stu_backward(
             ctx.saved_tensors, dy, ctx.geo, ctx.seed, ctx.seed_offset, ctx.needs_input_grad[3])
-        return (dx, None, None, d_w_uvqk, d_w_o, d_b_o, d_pos_w, d_ts_w, None, None, None, None)
+        return (dx, None, None, d_w_uvqk, d_w_o, d_b_o, d_pos_w, d_ts_w, None, None, None, None,
+                None)
 
 
 _SAVED_PER_LAYER = 14  # entries of _stu_forward's saved tuple
@@ -1017,17 +1022,135 @@ def stu_stack(x, offsets, bmap, layer_params, geo: STUGeometry, seeds, seed_offs
 
 
 def stu_layer(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGeometry, seed: int = 0,
-              seed_offset: Optional[torch.Tensor] = None):
+              seed_offset: Optional[torch.Tensor] = None, return_uvqk: bool = False):
     """bmap: ``bucket_map(...)`` of the batch, or None for no relative bias.
     Dropout masks hash (seed + *seed_offset, element); seed_offset is an optional device
-    int64 counter (bumped per forward so that captured graphs draw fresh masks)."""
+    int64 counter (bumped per forward so that captured graphs draw fresh masks).
+    ``return_uvqk``: also return the layer's (rows, n_out) u | v | q | k activations (no
+    gradient; bf16 in the a16 mode), from which ``stu_cache_states`` builds the cache."""
     _lib.require_gpu(x, offsets, w_uvqk, w_o, b_o)
     if x.dtype != torch.float32:
         raise TypeError("stu_layer: float32 only (the reference runs fp32, hstu.py:592)")
     grad_on = torch.is_grad_enabled() and any(
         t is not None and t.requires_grad for t in (x, w_uvqk, w_o, b_o, pos_w, ts_w))
     return STULayerFunction.apply(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo, int(seed),
-                                  seed_offset, grad_on)
+                                  seed_offset, grad_on, bool(return_uvqk))
+
+
+# ------------------------------------------------------------------ cached decoding
+
+def stu_cache_states(uvqk: torch.Tensor, y: torch.Tensor, offsets: torch.Tensor, rows: int,
+                     geo: STUGeometry):
+    """The layer's cache states as the reference returns them with return_cache_states
+    (hstu.py:420-423): (v (rows, H dv) jagged, padded q, padded k (B, N, H dqk),
+    outputs (rows, D)), fp32, ``rows`` = offsets[B]."""
+    hv, hq = geo.H * geo.dv, geo.H * geo.dqk
+    u = uvqk[:rows]
+    v = u[:, hv:2 * hv].float().contiguous()
+    q = u[:, 2 * hv:2 * hv + hq].float().contiguous()
+    k = u[:, 2 * hv + hq:].float().contiguous()
+    with torch.no_grad():
+        pq = jagged_to_padded_dense(q, offsets, geo.N)
+        pk = jagged_to_padded_dense(k, offsets, geo.N)
+    return v, pq, pk, y[:rows]
+
+
+def check_decode_step(offsets: torch.Tensor, delta_rows: torch.Tensor, delta_pos: torch.Tensor,
+                      N: int) -> None:
+    """The reference's cached step (hstu.py:151-177, 293-298) takes one delta entry per
+    sequence (its flattened padded index is delta[1][e] + e * n) and indexes rows with
+    index_copy_, which raises on an index out of range: the same conditions, checked here
+    with one host synchronisation per step."""
+    B = offsets.numel() - 1
+    if delta_rows.numel() != B or delta_pos.numel() != B:
+        raise ValueError(f"delta_x_offsets: {delta_rows.numel()} / {delta_pos.numel()} entries "
+                         f"for {B} sequences (one per sequence, hstu.py:153-159)")
+    ok = torch.stack([(delta_rows >= 0).all(), (delta_rows < offsets[-1]).all(),
+                      (delta_pos >= 0).all(), (delta_pos < N).all()]).all()
+    if not bool(ok):
+        raise IndexError("delta_x_offsets: a row outside [0, offsets[B]) or a position "
+                         f"outside [0, {N})")
+
+
+def stu_decode(x, offsets, timestamps, delta_rows, delta_pos, cache, w_uvqk, w_o, b_o, pos_w,
+               ts_w, geo: STUGeometry, seed: int = 0, seed_offset=None) -> torch.Tensor:
+    """One cached step of a layer (hstu.py:293-298, 321-322, 151-177, 393-418), fp32:
+    x (rows, D) jagged layer input, delta_rows / delta_pos the delta_x_offsets pair
+    (validated by ``check_decode_step``), cache = (v, padded q, padded k, outputs) from a
+    pass with return_cache_states, UPDATED IN PLACE as the reference's index_copy_ does.
+    Launches: row gather, LN + UVQK on the delta rows, 3 cache scatters, the delta rows'
+    attention (hstu_decode_attn), the gate + O projection, the output scatter.  Returns
+    the updated outputs cache (the next layer's input).  Forward only."""
+    v_c, q_c, k_c, out_c = cache
+    _lib.require_gpu(x, offsets, delta_rows, delta_pos, v_c, q_c, k_c, out_c, w_uvqk, w_o, b_o)
+    dev = x.device
+    B = offsets.numel() - 1
+    E = delta_rows.numel()
+    N, D, H, dqk, dv = geo.N, geo.D, geo.H, geo.dqk, geo.dv
+    hv, hq, n_out = H * dv, H * dqk, geo.n_out
+    for name, t, shape in (("v", v_c, (None, hv)), ("q", q_c, (B, N, hq)), ("k", k_c, (B, N, hq)),
+                           ("outputs", out_c, (None, D))):
+        want = tuple(t.shape[i] if s is None else s for i, s in enumerate(shape))
+        if t.dtype != torch.float32 or tuple(t.shape) != want or not t.is_contiguous():
+            raise ValueError(f"cache {name}: expected contiguous float32 {want}, got "
+                             f"{t.dtype} {tuple(t.shape)}")
+    if x.dtype != torch.float32 or x.dim() != 2 or x.shape[1] != D:
+        raise ValueError(f"stu_decode: x must be (rows, {D}) float32")
+    st = _stream()
+    x = x.contiguous()
+    rows_i = delta_rows.to(torch.int64).contiguous()
+    pos_i = delta_pos.to(torch.int64).contiguous()
+    xd = torch.empty(E, D, dtype=torch.float32, device=dev)
+    _lib.call("gr_rows_copy", x.data_ptr(), D, rows_i.data_ptr(), 0, x.shape[0], xd.data_ptr(), D,
+              None, 0, E, E, D, st)
+    off_d = torch.arange(E + 1, dtype=torch.int64, device=dev)
+    x_stats = torch.empty(E, 2, dtype=torch.float32, device=dev)
+    uvqk = torch.empty(E, n_out, dtype=torch.float32, device=dev)
+    w_uvqk = w_uvqk.detach().float().contiguous()
+    _lib.call("hstu_ln_uvqk_fwd", xd.data_ptr(), D, off_d.data_ptr(), E, E, D, w_uvqk.data_ptr(),
+              n_out, geo.eps, geo.activation, x_stats.data_ptr(), None, uvqk.data_ptr(), n_out, st)
+    # cache updates: v at the jagged rows, q / k at (e, delta_pos[e]) of the padded caches
+    _lib.call("gr_rows_copy", uvqk[:, hv:].data_ptr(), n_out, None, 0, E, v_c.data_ptr(), hv,
+              rows_i.data_ptr(), 0, v_c.shape[0], E, hv, st)
+    _lib.call("gr_rows_copy", uvqk[:, 2 * hv:].data_ptr(), n_out, None, 0, E, q_c.data_ptr(), hq,
+              pos_i.data_ptr(), N, B * N, E, hq, st)
+    _lib.call("gr_rows_copy", uvqk[:, 2 * hv + hq:].data_ptr(), n_out, None, 0, E, k_c.data_ptr(),
+              hq, pos_i.data_ptr(), N, B * N, E, hq, st)
+    attn = torch.empty(E, hv, dtype=torch.float32, device=dev)
+    bias = timestamps is not None and pos_w is not None and ts_w is not None
+    ts = pw = tw = thr = None
+    if bias:
+        ts = timestamps.to(torch.int64).contiguous()
+        if tuple(ts.shape) != (B, N):
+            raise ValueError(f"timestamps must be ({B}, {N}), got {tuple(ts.shape)}")
+        pw = pos_w.detach().float().contiguous()
+        tw = ts_w.detach().float().contiguous()
+        thr = bucket_thresholds(dev)
+    _lib.call("hstu_decode_attn", q_c.data_ptr(), k_c.data_ptr(), hq, v_c.data_ptr(), hv,
+              v_c.shape[0], offsets.data_ptr(), B, rows_i.data_ptr(), E, N, H, dqk, dv,
+              _lib.ptr(ts), _lib.ptr(thr), NUM_BUCKETS, _lib.ptr(pw), _lib.ptr(tw),
+              attn.data_ptr(), hv, st)
+    y = torch.empty(E, D, dtype=torch.float32, device=dev)
+    attn_stats = torch.empty(E, 2, dtype=torch.float32, device=dev)
+    w_o = w_o.detach().float().contiguous()
+    b_o = b_o.detach().float().contiguous()
+    gate_args = (uvqk.data_ptr(), n_out, attn.data_ptr(), hv, off_d.data_ptr(), E, E, hv)
+    tail = (xd.data_ptr(), D, geo.eps, geo.dropout_p, seed, _lib.ptr(seed_offset),
+            attn_stats.data_ptr())
+    if not geo.concat_ua:
+        _lib.call("hstu_gate_o_fwd", *gate_args, D, w_o.data_ptr(), b_o.data_ptr(), *tail, None,
+                  y.data_ptr(), D, st)
+    elif _cat_wide(hv, D):
+        o_in = torch.empty(E, 3 * hv, dtype=torch.float32, device=dev)
+        _lib.call("hstu_gate_o_cat_wide_fwd", *gate_args, D, w_o.data_ptr(), b_o.data_ptr(), *tail,
+                  o_in.data_ptr(), y.data_ptr(), D, st)
+    else:
+        w_pad, hvp = _pad_cat_weight(w_o, hv)
+        _lib.call("hstu_gate_o_cat_fwd", *gate_args, hvp, D, w_pad.data_ptr(), b_o.data_ptr(),
+                  *tail, None, y.data_ptr(), D, st)
+    _lib.call("gr_rows_copy", y.data_ptr(), D, None, 0, E, out_c.data_ptr(), D, rows_i.data_ptr(),
+              0, out_c.shape[0], E, D, st)
+    return out_c
 
 
 # ------------------------------------------------------------------ sampled-softmax loss

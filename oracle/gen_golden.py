@@ -20,6 +20,10 @@ Fixtures written:
     ``tests/test_ops.py:7-53`` (cumsum / dense_to_jagged / jagged_to_padded_dense).
   * ``preproc.npz``            -- ``LearnablePositionalEmbeddingInputFeaturesPreprocessor``
     (``learnable_positional_embedding.py:42-58``), eval mode, with input / table grads.
+  * ``decode_*.npz``           -- the cached (incremental) ``HSTU.forward`` path: a full
+    pass with ``return_cache_states=True`` (``hstu.py:420-423``), then one step with
+    ``delta_x_offsets`` / ``cache`` (``hstu.py:293-298, 321-322, 151-177, 415-418``) that
+    re-encodes one position per sequence; outputs and every layer's cache states.
   * ``muon.npz``               -- two ``Muon.step`` (``optimizers/muon.py:46-86``) on CPU.
   * ``embeddings.npz``         -- ``LocalEmbeddingModule.get_item_embeddings``
     (``embeddings/embeddings.py:94-97``) with an installed item -> year mapping, and the
@@ -30,7 +34,7 @@ Fixtures written:
     the sampling draw, the sampled ids / offsets it produced, the loss and the
     gradients of the query rows, the supervision embeddings and the embedding table.
 
-Usage:  python oracle/gen_golden.py [--only loss|preproc|muon|embeddings]   (writes tests/golden/*.npz)
+Usage:  python oracle/gen_golden.py [--only loss|preproc|muon|embeddings|decode]   (writes tests/golden/*.npz)
 """
 from __future__ import annotations
 
@@ -165,6 +169,88 @@ def gen_hstu_case(HSTU, name, B, N0, out_len, D, H, dqk, dv, blocks, seed,
                                 else torch.zeros_like(p)).numpy()
     np.savez_compressed(os.path.join(OUT, f"hstu_{name}.npz"), **rec)
     print(f"hstu_{name}: y {tuple(y.shape)} |y|max {y.abs().max():.3f}")
+
+
+def gen_hstu_decode_case(HSTU, name, B, N0, out_len, D, H, dqk, dv, blocks, seed, lengths,
+                         positions, with_ts=True, concat_ua=False):
+    """Full pass with cache states, then one cached step: sequence b's row at position
+    positions[b] (delta_x_offsets = (offsets[b] + p, p)) gets a new embedding and a new
+    timestamp.  The reference mutates the cache tensors in place, so the first pass's
+    states are copied before the step."""
+    torch.manual_seed(seed)
+    gen = torch.Generator().manual_seed(seed)
+    N = N0 + out_len
+    enc = HSTU(
+        max_sequence_len=N0, max_output_len=out_len, embedding_dim=D,
+        item_embedding_dim=D, num_blocks=blocks, num_heads=H, linear_dim=dv,
+        attention_dim=dqk, normalization="rel_bias", linear_config="uvqk",
+        linear_activation="silu", linear_dropout_rate=0.2, attn_dropout_rate=0.0,
+        concat_ua=concat_ua,
+    )
+    with torch.no_grad():
+        for layer in enc._hstu._attention_layers:
+            layer._rel_attn_bias._ts_w.normal_(0, 0.5, generator=gen)
+            layer._rel_attn_bias._pos_w.normal_(0, 0.5, generator=gen)
+            layer._o.bias.normal_(0, 0.1, generator=gen)
+    enc.eval()
+    lengths = torch.as_tensor(lengths, dtype=torch.int64)
+    pos = torch.as_tensor(positions, dtype=torch.int64)
+    assert bool((pos < lengths).all())
+    x0 = torch.randn(B, N, D, generator=gen)
+    ts0 = synth_timestamps(gen, B, N, lengths)
+    offsets = torch.cat([torch.zeros(1, dtype=torch.int64), torch.cumsum(lengths, 0)])
+    rec = {
+        "B": B, "N0": N0, "out_len": out_len, "N": N, "D": D, "H": H, "dqk": dqk,
+        "dv": dv, "blocks": blocks, "with_ts": int(with_ts), "concat_ua": int(concat_ua),
+        "lengths": lengths.numpy(), "positions": pos.numpy(), "x0": x0.numpy(),
+        "ts0": ts0.numpy(),
+    }
+    with torch.no_grad():
+        y0, states = enc(past_lengths=lengths, user_embeddings=x0,
+                         valid_mask=torch.ones(B, N, 1),
+                         past_payloads={"timestamps": ts0} if with_ts else {},
+                         return_cache_states=True)
+        rec["y0"] = y0.numpy()
+        for l, st in enumerate(states):
+            for nm, t in zip(("v", "q", "k", "out"), st):
+                rec[f"s0:{l}:{nm}"] = t.detach().clone().numpy()
+        x1 = x0.clone()
+        ts1 = ts0.clone()
+        for b in range(B):
+            p = int(pos[b])
+            x1[b, p] = torch.randn(D, generator=gen)
+            # a new timestamp between the neighbours' (or past the last one)
+            lo = int(ts0[b, p - 1]) if p > 0 else int(ts0[b, p]) - 500000
+            ts1[b, p] = lo + int(torch.randint(1, 400000, (1,), generator=gen))
+        delta = (offsets[:-1] + pos, pos.clone())
+        y1, states1 = enc(past_lengths=lengths, user_embeddings=x1,
+                          valid_mask=torch.ones(B, N, 1),
+                          past_payloads={"timestamps": ts1} if with_ts else {},
+                          delta_x_offsets=delta, cache=states, return_cache_states=True)
+    rec["x1"] = x1.numpy()
+    rec["ts1"] = ts1.numpy()
+    rec["delta0"] = delta[0].numpy()
+    rec["delta1"] = delta[1].numpy()
+    rec["y1"] = y1.numpy()
+    for l, st in enumerate(states1):
+        for nm, t in zip(("v", "q", "k", "out"), st):
+            rec[f"s1:{l}:{nm}"] = t.detach().numpy()
+    for pname, p in enc.named_parameters():
+        rec["param:" + pname] = p.detach().numpy()
+    np.savez_compressed(os.path.join(OUT, f"decode_{name}.npz"), **rec)
+    print(f"decode_{name}: y1 {tuple(y1.shape)} |y1 - y0|max {(y1 - y0).abs().max():.3f}")
+
+
+def gen_decode():
+    HSTU = _import_reference()[0]
+    gen_hstu_decode_case(HSTU, "b3_n16_d16_h1", 3, 16, 5, 16, 1, 16, 16, 2, seed=61,
+                         lengths=[21, 9, 1], positions=[20, 4, 0])
+    gen_hstu_decode_case(HSTU, "b4_n24_d24_h2", 4, 24, 3, 24, 2, 12, 12, 2, seed=62,
+                         lengths=[27, 13, 5, 20], positions=[26, 12, 2, 0])
+    gen_hstu_decode_case(HSTU, "b2_n12_d16_nots", 2, 12, 2, 16, 1, 16, 8, 1, seed=63,
+                         lengths=[14, 6], positions=[13, 5], with_ts=False)
+    gen_hstu_decode_case(HSTU, "b2_n12_d16_cua", 2, 12, 2, 16, 1, 16, 16, 2, seed=64,
+                         lengths=[10, 14], positions=[9, 7], concat_ua=True)
 
 
 def gen_topk_case(CandidateIndex, MIPSBruteForceTopK, name, B, X, D, k, N0, seed,
@@ -400,10 +486,14 @@ def main():
     if only == "embeddings":
         gen_embeddings()
         return
+    if only == "decode":
+        gen_decode()
+        return
     gen_sampled_softmax()
     gen_preprocessor()
     gen_muon()
     gen_embeddings()
+    gen_decode()
     HSTU, CandidateIndex, MIPSBruteForceTopK, ops = _import_reference()
     gen_bucket_thresholds(HSTU)
     gen_jagged_ops(ops)

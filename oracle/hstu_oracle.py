@@ -22,6 +22,9 @@ Reference map (paths relative to ``src/generative_recommenders_pl/models``):
   * STU layer ............ ``sequential_encoders/hstu.py:266-423``
   * HSTUJagged ........... ``sequential_encoders/hstu.py:439-518``
   * HSTU.forward ......... ``sequential_encoders/hstu.py:633-672``
+  * cached decoding ...... ``sequential_encoders/hstu.py:151-177, 293-298, 321-322,
+                            393-423`` (``hstu_forward_cached``; pinned by
+                            ``tests/golden/decode_*.npz``)
 """
 from __future__ import annotations
 
@@ -256,3 +259,64 @@ def hstu_forward_reference_order(lengths, user_embeddings, ts, cfg: HSTUConfig, 
         o_in = F.dropout(o_in, p=dropout_p, training=training)
         x = F.linear(o_in, p["o_w"], p["o_b"]) + x
     return _rows_to_padded(x, offsets, N)
+
+
+# ----------------------------------------------------------------------------------
+# Cached (incremental) decoding: the delta_x_offsets / cache branch of the reference.
+# ----------------------------------------------------------------------------------
+
+def stu_layer_cached(x, offsets, ts, cfg: HSTUConfig, p, delta=None, cache=None):
+    """One layer of hstu.py:266-423 with its cache states, restated on padded tensors.
+
+    Without ``delta``: the full layer, returning (new_outputs, (v, padded_q, padded_k,
+    new_outputs)) (hstu.py:420-423).  With ``delta`` = (jagged rows, positions) and
+    ``cache`` = that tuple: only the rows x[delta[0]] are re-encoded (hstu.py:293-298);
+    v, padded q / k and the outputs are updated IN PLACE by index_copy_ (hstu.py:321-322,
+    151-177, 415-418) — position delta[1][e] of sequence e for q / k — and the attention
+    reads the updated caches."""
+    H, dv, dqk, N, D = cfg.H, cfg.dv, cfg.dqk, cfg.N, cfg.D
+    B = offsets.numel() - 1
+    xs = x[delta[0]] if delta is not None else x
+    normed = F.layer_norm(xs, [D], eps=cfg.eps)
+    h = F.silu(normed @ p["uvqk"])
+    u, v, q, k = torch.split(h, [dv * H, dv * H, dqk * H, dqk * H], dim=1)
+    if delta is not None:
+        v_c, q_c, k_c, out_c = cache
+        v = v_c.index_copy_(0, delta[0], v)
+        flat = delta[1] + torch.arange(0, B * N, N, dtype=delta[1].dtype)
+        pq = q_c.view(B * N, -1).index_copy_(0, flat, q).view(B, N, -1)
+        pk = k_c.view(B * N, -1).index_copy_(0, flat, k).view(B, N, -1)
+    else:
+        pq = _rows_to_padded(q, offsets, N)
+        pk = _rows_to_padded(k, offsets, N)
+    s = torch.einsum("bnhd,bmhd->bhnm", pq.view(B, N, H, dqk), pk.view(B, N, H, dqk))
+    if ts is not None:
+        s = s + rel_bias_padded(ts, N, p["pos_w"], p["ts_w"], None).unsqueeze(1)
+    a = F.silu(s) / N * torch.tril(torch.ones(N, N, dtype=s.dtype))
+    pv = _rows_to_padded(v, offsets, N).reshape(B, N, H, dv)
+    attn = _rows_to_jagged(torch.einsum("bhnm,bmhd->bnhd", a, pv).reshape(B, N, H * dv),
+                           offsets)
+    if delta is not None:
+        attn = attn[delta[0]]
+    an = F.layer_norm(attn, [dv * H], eps=cfg.eps)
+    o_in = torch.cat([u, an, u * an], -1) if cfg.concat_ua else u * an
+    new = o_in @ p["o_w"].t() + p["o_b"] + xs
+    if delta is not None:
+        new = cache[3].index_copy_(0, delta[0], new)
+    return new, (v.contiguous(), pq, pk, new)
+
+
+def hstu_forward_cached(lengths, user_embeddings, ts, cfg: HSTUConfig, layers,
+                        delta=None, cache=None):
+    """HSTU.forward (hstu.py:633-672 -> 482-518) with return_cache_states=True:
+    (y (B, N, D), [per-layer (v, padded_q, padded_k, outputs)]).  With ``delta`` /
+    ``cache`` the cached step; the cache tensors are updated in place."""
+    offsets = torch.cat([torch.zeros(1, dtype=torch.int64),
+                         torch.cumsum(lengths.to(torch.int64), 0)])
+    x = _rows_to_jagged(user_embeddings, offsets)
+    states = []
+    for i, p in enumerate(layers):
+        x, st = stu_layer_cached(x, offsets, ts, cfg, p, delta,
+                                 cache[i] if cache is not None else None)
+        states.append(st)
+    return _rows_to_padded(x, offsets, cfg.N), states

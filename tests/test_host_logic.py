@@ -99,21 +99,42 @@ def test_custom_bucketization_fn_checked_against_the_kernel_table():
         RelativeBucketedTimeAndPositionBasedBias(10, 128, lambda x: x.nonexistent())
 
 
-def test_incremental_decoding_raises_on_every_path():
-    """delta_x_offsets / cache (hstu.py:293-298, 415-418) are not supported: both the
-    per-layer path and the one-node stack must raise, never run a full forward."""
+def test_cached_decoding_host_checks():
+    """delta_x_offsets / cache (hstu.py:293-298, 151-177): the checks that run before any
+    device work — a cache per layer, one delta entry per sequence, entries in range, and
+    no autograd (the cached step has no backward) — then the product path refuses CPU
+    tensors (no CPU fallback)."""
+    from mygenerativerecommenders_amd._lib import GrError
     enc = _hstu(max_sequence_len=8, max_output_len=0, embedding_dim=8, item_embedding_dim=8,
                 linear_dim=8, attention_dim=8)
     x = torch.randn(16, 8)
     off = torch.tensor([0, 8, 16])
     mask = enc._attn_mask
-    delta = (torch.tensor([0, 1]), torch.tensor([7, 15]))
-    for rcs in (False, True):
-        with pytest.raises(NotImplementedError):
-            enc._hstu.jagged_forward(x, off, None, mask, delta_x_offsets=delta,
-                                     return_cache_states=rcs)
-    with pytest.raises(NotImplementedError):
-        enc._hstu.jagged_forward(x, off, None, mask, cache=[None, None])
+    delta = (torch.tensor([7, 15]), torch.tensor([7, 7]))
+    n_layers = len(enc._hstu._attention_layers)
+    with pytest.raises(ValueError, match="cache"):
+        enc._hstu.jagged_forward(x, off, None, mask, delta_x_offsets=delta)
+    with pytest.raises(ValueError, match="cache"):
+        enc._hstu.jagged_forward(x, off, None, mask, delta_x_offsets=delta,
+                                 cache=[None] * (n_layers + 1))
+    states = (torch.zeros(16, 8), torch.zeros(2, 8, 8), torch.zeros(2, 8, 8), torch.zeros(16, 8))
+    cache = [states] * n_layers
+    with pytest.raises(ValueError, match="one per sequence"):
+        enc._hstu.jagged_forward(x, off, None, mask, delta_x_offsets=(delta[0][:1], delta[1][:1]),
+                                 cache=cache)
+    with pytest.raises(IndexError):
+        enc._hstu.jagged_forward(x, off, None, mask, delta_x_offsets=(delta[0] + 1, delta[1]),
+                                 cache=cache)
+    with pytest.raises(IndexError):
+        enc._hstu.jagged_forward(x, off, None, mask, delta_x_offsets=(delta[0], delta[1] + 1),
+                                 cache=cache)
+    with pytest.raises(NotImplementedError, match="inference-only"):
+        enc._hstu.jagged_forward(x, off, None, mask, delta_x_offsets=delta, cache=cache)
+    layer = enc._hstu._attention_layers[0]
+    with pytest.raises(ValueError, match="cache"):
+        layer(x, off, None, mask, delta_x_offsets=delta, cache=None)
+    with torch.no_grad(), pytest.raises(GrError, match="CPU"):
+        layer(x, off, None, mask, delta_x_offsets=delta, cache=states)
 
 
 def test_candidate_index_contract():

@@ -15,6 +15,7 @@ from oracle import topk_oracle
 
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 HSTU_CASES = sorted(glob.glob(os.path.join(GOLDEN, "hstu_*.npz")))
+DECODE_CASES = sorted(glob.glob(os.path.join(GOLDEN, "decode_*.npz")))
 
 
 def _thr():
@@ -60,6 +61,40 @@ def test_hstu_oracle_vs_reference(path, variant):
         g = p.grad if p.grad is not None else torch.zeros_like(p)
         ref = torch.tensor(d["grad:" + k])
         assert (g - ref).abs().max().item() <= 2e-5 * (1 + ref.abs().max().item()), k
+
+
+def _decode_case(d):
+    cfg = O.HSTUConfig(N=int(d["N"]), D=int(d["D"]), H=int(d["H"]), dqk=int(d["dqk"]),
+                       dv=int(d["dv"]), concat_ua=bool(d["concat_ua"]))
+    st = {k[6:]: torch.tensor(d[k]) for k in d.files if k.startswith("param:")}
+    layers = [O.layer_params_from_state(st, i) for i in range(int(d["blocks"]))]
+    return cfg, layers
+
+
+@pytest.mark.parametrize("path", DECODE_CASES, ids=[os.path.basename(p) for p in DECODE_CASES])
+def test_decode_oracle_vs_reference(path):
+    """The cached path (hstu.py:293-298, 321-322, 151-177, 415-418): full pass with cache
+    states, then one re-encoded position per sequence, against the reference's record."""
+    d = np.load(path)
+    cfg, layers = _decode_case(d)
+    with_ts = int(d["with_ts"])
+    lengths = torch.tensor(d["lengths"])
+    y0, states = O.hstu_forward_cached(lengths, torch.tensor(d["x0"]),
+                                       torch.tensor(d["ts0"]) if with_ts else None, cfg, layers)
+    assert (y0 - torch.tensor(d["y0"])).abs().max().item() <= 1e-5
+    for l, st in enumerate(states):
+        for nm, t in zip(("v", "q", "k", "out"), st):
+            assert t.shape == d[f"s0:{l}:{nm}"].shape, (l, nm)
+            assert (t - torch.tensor(d[f"s0:{l}:{nm}"])).abs().max().item() <= 1e-5, (l, nm)
+    delta = (torch.tensor(d["delta0"]), torch.tensor(d["delta1"]))
+    y1, states1 = O.hstu_forward_cached(lengths, torch.tensor(d["x1"]),
+                                        torch.tensor(d["ts1"]) if with_ts else None, cfg,
+                                        layers, delta=delta, cache=states)
+    assert (y1 - torch.tensor(d["y1"])).abs().max().item() <= 1e-5
+    for l, st in enumerate(states1):
+        assert st[0] is states[l][0] and st[3] is states[l][3]  # updated in place
+        for nm, t in zip(("v", "q", "k", "out"), st):
+            assert (t - torch.tensor(d[f"s1:{l}:{nm}"])).abs().max().item() <= 1e-5, (l, nm)
 
 
 @pytest.mark.parametrize("name", ["T1", "T2", "T3_small"])
