@@ -47,7 +47,7 @@ GR_API int gr_version(void);
  * wgrad_reduce, mips_pack, mips_select, mips_merge, cumsum, dense_to_jagged, encoder_prologue, bf16_scale_add, adamw,
  * jagged_to_padded, l2_normalize, current_embeddings, sampled_softmax_fwd,
  * sampled_softmax_bwd, sampled_softmax_csr, sampled_softmax_table_grad, preproc, rows_copy,
- * decode_attn.  Not for use inside a captured graph.
+ * decode_attn, softmax_attn_fwd, softmax_attn_bwd.  Not for use inside a captured graph.
  */
 GR_API int gr_timing_enable(int on);
 GR_API int gr_timing_query(const char* kernel, double* total_ms, int* launches);
@@ -338,6 +338,34 @@ GR_API int hstu_decode_attn(const float* q_cache, const float* k_cache, int64_t 
                             int N, int H, int dqk, int dv, const int64_t* ts,
                             const int64_t* bucket_thr, int num_buckets, const float* pos_w,
                             const float* ts_w, float* out, int64_t ld_out, void* stream);
+
+/* ---------------------------------------------------------------- softmax attention (ABI 18)
+ * hstu_softmax_attn_fwd replaces the normalization="softmax_rel_bias" branch of
+ * SequentialTransductionUnitJagged.forward (sequential_encoders/hstu.py:341-389, no
+ * cache): for every sequence b and query row i < L_b (= offsets[b+1] - offsets[b], at most
+ * N), over ALL N keys j (k_j = 0 for j >= L_b, as the padded tensor):
+ *   s_j = (q_i . k_j + bias[b][i][j]) / sqrt_d      (q / k: the hdq = h dqk columns at once;
+ *                                                   bias (B, N, N) or NULL = no bias)
+ *   out_i = sum_{j <= i} softmax(s)_j v_j           (softmax over all N, then the causal mask)
+ *   stats[row] = (max_j s_j, sum_j exp(s_j - max))  (row = offsets[b] + i, kept for the bwd)
+ * hstu_softmax_attn_bwd: the gradients of q, k, v (times silu'(h) when the pre-activations
+ * hq / hk / hv are given, as hstu_attn_bwd) and, when dbias is not NULL, of the bias
+ * (B, N, N; rows i >= L_b zero); workspace hstu_softmax_attn_bwd_workspace_size(B, N,
+ * dbias != NULL) bytes.  LDS bounds hdq + hdv + N <= 4096.
+ */
+GR_API size_t hstu_softmax_attn_bwd_workspace_size(int B, int N, int with_dbias);
+GR_API int hstu_softmax_attn_fwd(const float* q, const float* k, int64_t ld_qk, const float* v,
+                                 int64_t ld_v, const int64_t* offsets, int B, int N, int hdq,
+                                 int hdv, float sqrt_d, const float* bias, float* out,
+                                 int64_t ld_out, float* stats, void* stream);
+GR_API int hstu_softmax_attn_bwd(const float* q, const float* k, int64_t ld_qk, const float* v,
+                                 int64_t ld_v, const int64_t* offsets, int B, int N, int hdq,
+                                 int hdv, float sqrt_d, const float* bias, const float* out,
+                                 int64_t ld_out, const float* stats, const float* dout,
+                                 int64_t ld_do, const float* hq, const float* hk,
+                                 const float* hv, int64_t ld_h, float* dq, float* dk,
+                                 float* dv, int64_t ld_d, float* dbias, void* workspace,
+                                 size_t ws_bytes, void* stream);
 
 /* hstu_rel_bias_fwd / _bwd (ABI 13) — replaces RelativeBucketedTimeAndPositionBasedBias
  * .forward (sequential_encoders/hstu.py:96-128) for callers that materialise the bias

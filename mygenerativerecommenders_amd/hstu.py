@@ -20,8 +20,12 @@ sequence against those caches, updating them in place (``ops.stu_decode``: the d
 rows' attention only, not the reference's full (B, h, n, n) pass).  The cached step is
 inference-only (it raises under autograd) and computes in fp32 in either mode.
 
-Not supported (raise): ``normalization="softmax_rel_bias"`` (hstu.py:341-389 — used by no
-config) and attention dropout > 0 (the reference ignores it too).
+``normalization="softmax_rel_bias"`` (hstu.py:341-389, used by no config) runs as an fp32
+layer (``ops.stu_softmax_layer``: the softmax attention kernels of
+``hstu_softmax_attn.hip``, the materialised (B, n, n) bias of ``hstu_rel_bias_fwd``).
+
+Not supported (raise): the cached step with ``softmax_rel_bias`` (the reference's branch
+fails at hstu.py:343) and attention dropout > 0 (the reference ignores it too).
 """
 from __future__ import annotations
 
@@ -181,15 +185,15 @@ class SequentialTransductionUnitJagged(torch.nn.Module):
             act = 0
         else:
             raise ValueError(f"Unknown linear_activation {self._linear_activation}")
-        if self._normalization not in ("rel_bias", "hstu_rel_bias"):
-            if self._normalization == "softmax_rel_bias":
-                raise NotImplementedError("normalization='softmax_rel_bias' is not supported")
+        if self._normalization not in ("rel_bias", "hstu_rel_bias", "softmax_rel_bias"):
             raise ValueError(f"Unknown normalization method {self._normalization}")
+        softmax = self._normalization == "softmax_rel_bias"
         return ops.STUGeometry(
             N=n, D=self._embedding_dim, H=self._num_heads, dqk=self._attention_dim,
             dv=self._linear_dim, eps=self._eps, activation=act,
             dropout_p=float(self._dropout_ratio) if self.training else 0.0,
-            max_len=max_len, bf16=self._bf16, concat_ua=self._concat_ua)
+            max_len=max_len, bf16=self._bf16 and not softmax, concat_ua=self._concat_ua,
+            softmax=softmax)
 
     def forward(
         self,
@@ -218,8 +222,15 @@ class SequentialTransductionUnitJagged(torch.nn.Module):
         geo = self._geometry(n, n if max_len is None else max_len)
         rab = self._rel_attn_bias
         if delta_x_offsets is not None:
+            if geo.softmax:
+                # hstu.py:342-343 evaluates x_offsets.size() - 1, which raises (TypeError)
+                raise NotImplementedError("cached decoding with normalization="
+                                          "'softmax_rel_bias' (the reference's branch fails)")
             return self._decode(x, x_offsets, all_timestamps, delta_x_offsets, cache, geo,
                                 dropout_step)
+        if geo.softmax:
+            return self._softmax_forward(x, x_offsets, all_timestamps, n, geo, return_cache_states,
+                                         dropout_step)
         bmap = None
         if rab is not None and all_timestamps is not None:
             bmap = bucket_map if bucket_map is not None else ops.bucket_map(
@@ -237,6 +248,32 @@ class SequentialTransductionUnitJagged(torch.nn.Module):
                 step = self._dropout_step
         y = ops.stu_layer(x, x_offsets, bmap, self._uvqk, self._o.weight, self._o.bias, pos_w,
                           ts_w, geo, self._dropout_seed, step, return_uvqk=return_cache_states)
+        if return_cache_states:
+            y, uvqk = y
+            return y, ops.stu_cache_states(uvqk, y, x_offsets, int(x_offsets[-1]), geo)
+        return y, (None, None, None, y)
+
+    def _softmax_forward(self, x, x_offsets, all_timestamps, n, geo, return_cache_states,
+                         dropout_step):
+        """normalization="softmax_rel_bias" (hstu.py:341-389): the (B, n, n) bias of
+        ``_rel_attn_bias`` (hstu_rel_bias_fwd; its backward gives _pos_w / _ts_w their
+        gradients), then the softmax layer (ops.stu_softmax_layer), fp32."""
+        rab = self._rel_attn_bias
+        bias = None
+        if rab is not None:
+            if all_timestamps is None:
+                raise ValueError("normalization='softmax_rel_bias' with a relative bias module "
+                                 "needs timestamps (hstu.py:379-380)")
+            bias = rab(all_timestamps)
+        step = None
+        if geo.dropout_p > 0:
+            if dropout_step is not None:
+                step = dropout_step
+            else:
+                self._dropout_step.add_(1)
+                step = self._dropout_step
+        y = ops.stu_softmax_layer(x, x_offsets, bias, self._uvqk, self._o.weight, self._o.bias,
+                                  geo, self._dropout_seed, step, return_uvqk=return_cache_states)
         if return_cache_states:
             y, uvqk = y
             return y, ops.stu_cache_states(uvqk, y, x_offsets, int(x_offsets[-1]), geo)
@@ -292,7 +329,8 @@ class HSTUJagged(torch.nn.Module):
 
     def _needs_map(self, all_timestamps) -> bool:
         return all_timestamps is not None and any(
-            layer._rel_attn_bias is not None for layer in self._attention_layers)
+            layer._rel_attn_bias is not None and layer._normalization != "softmax_rel_bias"
+            for layer in self._attention_layers)
 
     def _needs_step(self) -> bool:
         return self.training and any(layer._dropout_ratio > 0 for layer in self._attention_layers)
@@ -353,7 +391,7 @@ class HSTUJagged(torch.nn.Module):
             return None
         layers = list(self._attention_layers)
         geos = [layer._geometry(n, n if max_len is None else max_len) for layer in layers]
-        if any(g != geos[0] for g in geos) or geos[0].concat_ua:
+        if any(g != geos[0] for g in geos) or geos[0].concat_ua or geos[0].softmax:
             return None
         params = []
         for layer in layers:

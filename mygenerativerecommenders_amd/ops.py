@@ -357,6 +357,7 @@ class STUGeometry:
     max_len: int        # host bound on sequence lengths (<= N)
     bf16: bool = False  # bf16 MFMA operands (HSTU autocast_dtype=bfloat16): attention, projections, weight grads
     concat_ua: bool = False  # o_in = [u, LN(a), u * LN(a)] (hstu.py:398-400)
+    softmax: bool = False    # normalization="softmax_rel_bias" (hstu.py:341-389): fp32 layer
 
     @property
     def n_out(self):
@@ -367,7 +368,7 @@ class STUGeometry:
         """bf16 activations in HBM (ABI 16, the ``*_a16`` entries): bf16 mode at wide
         heads, dqk == dv = d with d % 32 == 0 in (128, 256] (the ml-20m width)."""
         d = self.dqk
-        return (A16 and self.bf16 and not self.concat_ua and self.dqk == self.dv
+        return (A16 and self.bf16 and not self.concat_ua and not self.softmax and self.dqk == self.dv
                 and 128 < d <= 256 and d % 32 == 0 and self.H * d <= 256)
 
 
@@ -1035,6 +1036,153 @@ def stu_layer(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo: STUGeometry,
         t is not None and t.requires_grad for t in (x, w_uvqk, w_o, b_o, pos_w, ts_w))
     return STULayerFunction.apply(x, offsets, bmap, w_uvqk, w_o, b_o, pos_w, ts_w, geo, int(seed),
                                   seed_offset, grad_on, bool(return_uvqk))
+
+
+# ------------------------------------------------------------------ softmax_rel_bias layer
+
+def _gate_forward(uvqk, attn, offsets, rows, x, geo: STUGeometry, w_o, b_o, seed, seed_offset,
+                  attn_stats, want_o_in: bool):
+    """The fp32 gate + O projection + residual (hstu.py:393-413) of ``rows`` rows; returns
+    (y, o_in or None)."""
+    dev = x.device
+    B = offsets.numel() - 1
+    hv, D, n_out = geo.H * geo.dv, geo.D, geo.n_out
+    st = _stream()
+    y = torch.empty(rows, D, dtype=torch.float32, device=dev)
+    cat_wide = geo.concat_ua and _cat_wide(hv, D)
+    ow = 3 * hv if geo.concat_ua else hv
+    o_in = (torch.empty(rows, ow, dtype=torch.float32, device=dev)
+            if want_o_in or cat_wide else None)
+    head = (uvqk.data_ptr(), n_out, attn.data_ptr(), hv, offsets.data_ptr(), B, rows, hv)
+    tail = (x.data_ptr(), x.stride(0), geo.eps, geo.dropout_p, seed, _lib.ptr(seed_offset),
+            attn_stats.data_ptr(), _lib.ptr(o_in), y.data_ptr(), D, st)
+    if not geo.concat_ua:
+        _lib.call("hstu_gate_o_fwd", *head, D, w_o.data_ptr(), b_o.data_ptr(), *tail)
+    elif cat_wide:
+        _lib.call("hstu_gate_o_cat_wide_fwd", *head, D, w_o.data_ptr(), b_o.data_ptr(), *tail)
+    else:
+        w_pad, hvp = _pad_cat_weight(w_o, hv)
+        _lib.call("hstu_gate_o_cat_fwd", *head, hvp, D, w_pad.data_ptr(), b_o.data_ptr(), *tail)
+    return y, (o_in if want_o_in else None)
+
+
+class SoftmaxSTULayerFunction(torch.autograd.Function):
+    """One SequentialTransductionUnitJagged with normalization="softmax_rel_bias"
+    (hstu.py:266-413 with the attention of :341-389), fp32: LN + UVQK + SiLU
+    (hstu_ln_uvqk_fwd), the softmax attention (hstu_softmax_attn_fwd), the gate + O
+    projection + residual (hstu_gate_o_fwd / _cat_).  ``bias`` is the (B, N, N) relative
+    bias (``rel_bias``: its gradient flows back to _pos_w / _ts_w through that node) or
+    None.  Backward: gate_o_bwd, hstu_softmax_attn_bwd (dQ / dK / dV with silu' and the bias
+    gradient), ln_uvqk_bwd, the weight gradients (gr_wgrad2)."""
+
+    @staticmethod
+    def forward(ctx, x, offsets, bias, w_uvqk, w_o, b_o, geo: STUGeometry, seed: int,
+                seed_offset, grad_on: bool, want_uvqk: bool):
+        dev = x.device
+        rows, D = x.shape
+        B = offsets.numel() - 1
+        H, dv, dqk = geo.H, geo.dv, geo.dqk
+        hv, hq, n_out = H * dv, H * dqk, geo.n_out
+        st = _stream()
+        x = x.contiguous()
+        w_uvqk = w_uvqk.contiguous()
+        w_o = w_o.contiguous()
+        b_o = b_o.contiguous()
+        x_stats, uvqk, h_pre = _ln_uvqk_outputs(rows, n_out, geo, grad_on, dev)
+        _lib.call("hstu_ln_uvqk_fwd", x.data_ptr(), x.stride(0), offsets.data_ptr(), B, rows, D,
+                  w_uvqk.data_ptr(), n_out, geo.eps, geo.activation, x_stats.data_ptr(),
+                  _lib.ptr(h_pre), uvqk.data_ptr(), n_out, st)
+        bias_c = bias.detach().contiguous() if bias is not None else None
+        if bias_c is not None and tuple(bias_c.shape) != (B, geo.N, geo.N):
+            raise ValueError(f"softmax attention bias must be ({B}, {geo.N}, {geo.N})")
+        attn = torch.empty(rows, hv, dtype=torch.float32, device=dev)
+        sm_stats = torch.empty(rows, 2, dtype=torch.float32, device=dev)
+        _lib.call("hstu_softmax_attn_fwd", uvqk[:, 2 * hv:].data_ptr(),
+                  uvqk[:, 2 * hv + hq:].data_ptr(), n_out, uvqk[:, hv:].data_ptr(), n_out,
+                  offsets.data_ptr(), B, geo.N, hq, hv, float(dqk) ** 0.5, _lib.ptr(bias_c),
+                  attn.data_ptr(), hv, sm_stats.data_ptr(), st)
+        attn_stats = torch.empty(rows, 2, dtype=torch.float32, device=dev)
+        y, o_in = _gate_forward(uvqk, attn, offsets, rows, x, geo, w_o, b_o, seed, seed_offset,
+                                attn_stats, grad_on)
+        ctx.save_for_backward(x, offsets, bias_c, w_uvqk, w_o, x_stats, uvqk, h_pre, attn,
+                              attn_stats, o_in, sm_stats)
+        ctx.geo, ctx.seed, ctx.seed_offset = geo, seed, seed_offset
+        if want_uvqk:
+            ctx.mark_non_differentiable(uvqk)
+            return y, uvqk
+        return y
+
+    @staticmethod
+    def backward(ctx, dy, *_unused):
+        (x, offsets, bias, w_uvqk, w_o, x_stats, uvqk, h_pre, attn, attn_stats, o_in,
+         sm_stats) = ctx.saved_tensors
+        geo, seed, seed_offset = ctx.geo, ctx.seed, ctx.seed_offset
+        dev = x.device
+        rows, D = x.shape
+        B = offsets.numel() - 1
+        H, dv, dqk = geo.H, geo.dv, geo.dqk
+        hv, hq, n_out = H * dv, H * dqk, geo.n_out
+        st = _stream()
+        dy = dy.contiguous()
+        d_uvqk = torch.empty(rows, n_out, dtype=torch.float32, device=dev)
+        d_attn = torch.empty(rows, hv, dtype=torch.float32, device=dev)
+        gate = (dy.data_ptr(), D, offsets.data_ptr(), B, rows, hv)
+        mid = (uvqk.data_ptr(), n_out, attn.data_ptr(), hv, attn_stats.data_ptr(),
+               _lib.ptr(h_pre), n_out, geo.dropout_p, seed, _lib.ptr(seed_offset))
+        if not geo.concat_ua:
+            _lib.call("hstu_gate_o_bwd", *gate, D, w_o.data_ptr(), *mid, d_uvqk.data_ptr(), n_out,
+                      d_attn.data_ptr(), hv, st)
+        elif _cat_wide(hv, D):
+            g_cat = torch.empty(rows, 3 * hv, dtype=torch.float32, device=dev)
+            _lib.call("hstu_gate_o_cat_wide_bwd", *gate, D, w_o.data_ptr(), *mid, g_cat.data_ptr(),
+                      d_uvqk.data_ptr(), n_out, d_attn.data_ptr(), hv, st)
+        else:
+            w_pad, hvp = _pad_cat_weight(w_o, hv)
+            _lib.call("hstu_gate_o_cat_bwd", *gate, hvp, D, w_pad.data_ptr(), *mid,
+                      d_uvqk.data_ptr(), n_out, d_attn.data_ptr(), hv, st)
+        want_bias = bias is not None and ctx.needs_input_grad[2]
+        d_bias = torch.empty_like(bias) if want_bias else None
+        L = _lib.lib()
+        ws_n = L.hstu_softmax_attn_bwd_workspace_size(B, geo.N, 1 if want_bias else 0)
+        ws = torch.empty(max(ws_n, 4), dtype=torch.uint8, device=dev)
+        hp = (lambda c: h_pre[:, c:].data_ptr()) if h_pre is not None else (lambda c: None)
+        _lib.call("hstu_softmax_attn_bwd", uvqk[:, 2 * hv:].data_ptr(),
+                  uvqk[:, 2 * hv + hq:].data_ptr(), n_out, uvqk[:, hv:].data_ptr(), n_out,
+                  offsets.data_ptr(), B, geo.N, hq, hv, float(dqk) ** 0.5, _lib.ptr(bias),
+                  attn.data_ptr(), hv, sm_stats.data_ptr(), d_attn.data_ptr(), hv,
+                  hp(2 * hv), hp(2 * hv + hq), hp(hv), n_out, d_uvqk[:, 2 * hv:].data_ptr(),
+                  d_uvqk[:, 2 * hv + hq:].data_ptr(), d_uvqk[:, hv:].data_ptr(), n_out,
+                  _lib.ptr(d_bias), ws.data_ptr(), ws_n, st)
+        dx = torch.empty(rows, D, dtype=torch.float32, device=dev)
+        _lib.call("hstu_ln_uvqk_bwd", d_uvqk.data_ptr(), n_out, offsets.data_ptr(), B, rows, D,
+                  n_out, w_uvqk.data_ptr(), x.data_ptr(), x.stride(0), x_stats.data_ptr(),
+                  dy.data_ptr(), D, dx.data_ptr(), D, st)
+        d_w_uvqk = torch.empty(D, n_out, dtype=torch.float32, device=dev)
+        ow = o_in.shape[1]
+        d_w_o = torch.empty(D, ow, dtype=torch.float32, device=dev)
+        d_b_o = torch.empty(D, dtype=torch.float32, device=dev)
+        ws2_n = L.gr_wgrad2_workspace_size(rows, D, n_out, D, ow)
+        ws2 = torch.empty(max(ws2_n, 4), dtype=torch.uint8, device=dev)
+        _lib.call("gr_wgrad2", x.data_ptr(), x.stride(0), x_stats.data_ptr(), d_uvqk.data_ptr(),
+                  n_out, D, n_out, d_w_uvqk.data_ptr(), None, dy.data_ptr(), D, None,
+                  o_in.data_ptr(), ow, D, ow, d_w_o.data_ptr(), d_b_o.data_ptr(),
+                  offsets.data_ptr(), B, rows, ws2.data_ptr(), ws2_n, st)
+        return dx, None, d_bias, d_w_uvqk, d_w_o, d_b_o, None, None, None, None, None
+
+
+def stu_softmax_layer(x, offsets, bias, w_uvqk, w_o, b_o, geo: STUGeometry, seed: int = 0,
+                      seed_offset=None, return_uvqk: bool = False):
+    """A normalization="softmax_rel_bias" layer (hstu.py:266-413, :341-389), fp32.
+    ``bias``: ``rel_bias(timestamps, N, _pos_w, _ts_w)`` (differentiable) or None."""
+    _lib.require_gpu(x, offsets, w_uvqk, w_o, b_o, bias)
+    if x.dtype != torch.float32:
+        raise TypeError("stu_softmax_layer: float32 only")
+    if not geo.softmax:
+        raise ValueError("stu_softmax_layer: geometry is not a softmax_rel_bias layer")
+    grad_on = torch.is_grad_enabled() and any(
+        t is not None and t.requires_grad for t in (x, w_uvqk, w_o, b_o, bias))
+    return SoftmaxSTULayerFunction.apply(x, offsets, bias, w_uvqk, w_o, b_o, geo, int(seed),
+                                         seed_offset, grad_on, bool(return_uvqk))
 
 
 # ------------------------------------------------------------------ cached decoding

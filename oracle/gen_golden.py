@@ -24,6 +24,8 @@ Fixtures written:
     pass with ``return_cache_states=True`` (``hstu.py:420-423``), then one step with
     ``delta_x_offsets`` / ``cache`` (``hstu.py:293-298, 321-322, 151-177, 415-418``) that
     re-encodes one position per sequence; outputs and every layer's cache states.
+  * ``softmax_*.npz``          -- ``HSTU.forward`` with ``normalization="softmax_rel_bias"``
+    (``hstu.py:341-389``): output and every gradient, as the ``hstu_*`` cases.
   * ``muon.npz``               -- two ``Muon.step`` (``optimizers/muon.py:46-86``) on CPU.
   * ``embeddings.npz``         -- ``LocalEmbeddingModule.get_item_embeddings``
     (``embeddings/embeddings.py:94-97``) with an installed item -> year mapping, and the
@@ -34,7 +36,7 @@ Fixtures written:
     the sampling draw, the sampled ids / offsets it produced, the loss and the
     gradients of the query rows, the supervision embeddings and the embedding table.
 
-Usage:  python oracle/gen_golden.py [--only loss|preproc|muon|embeddings|decode]   (writes tests/golden/*.npz)
+Usage:  python oracle/gen_golden.py [--only loss|preproc|muon|embeddings|decode|softmax]   (writes tests/golden/*.npz)
 """
 from __future__ import annotations
 
@@ -126,23 +128,25 @@ def gen_bucket_thresholds(HSTU):
 
 
 def gen_hstu_case(HSTU, name, B, N0, out_len, D, H, dqk, dv, blocks, seed,
-                  lengths=None, with_ts=True, concat_ua=False):
+                  lengths=None, with_ts=True, concat_ua=False, normalization="rel_bias",
+                  rab=True, prefix="hstu"):
     torch.manual_seed(seed)
     gen = torch.Generator().manual_seed(seed)
     N = N0 + out_len
     enc = HSTU(
         max_sequence_len=N0, max_output_len=out_len, embedding_dim=D,
         item_embedding_dim=D, num_blocks=blocks, num_heads=H, linear_dim=dv,
-        attention_dim=dqk, normalization="rel_bias", linear_config="uvqk",
+        attention_dim=dqk, normalization=normalization, linear_config="uvqk",
         linear_activation="silu", linear_dropout_rate=0.2, attn_dropout_rate=0.0,
-        concat_ua=concat_ua,
+        concat_ua=concat_ua, enable_relative_attention_bias=rab,
     )
     # the reference zero-inits nothing; pos/ts weights are N(0, 0.02).  Scale them up
     # so the bias path is exercised with O(1) magnitudes.
     with torch.no_grad():
         for layer in enc._hstu._attention_layers:
-            layer._rel_attn_bias._ts_w.normal_(0, 0.5, generator=gen)
-            layer._rel_attn_bias._pos_w.normal_(0, 0.5, generator=gen)
+            if rab:
+                layer._rel_attn_bias._ts_w.normal_(0, 0.5, generator=gen)
+                layer._rel_attn_bias._pos_w.normal_(0, 0.5, generator=gen)
             layer._o.bias.normal_(0, 0.1, generator=gen)
     enc.eval()
     if lengths is None:
@@ -160,6 +164,7 @@ def gen_hstu_case(HSTU, name, B, N0, out_len, D, H, dqk, dv, blocks, seed,
     rec = {
         "B": B, "N0": N0, "out_len": out_len, "N": N, "D": D, "H": H, "dqk": dqk,
         "dv": dv, "blocks": blocks, "with_ts": int(with_ts), "concat_ua": int(concat_ua),
+        "normalization": normalization, "rab": int(rab),
         "lengths": lengths.numpy(), "x": x.detach().numpy(), "ts": ts.numpy(),
         "y": y.detach().numpy(), "dy": dy.numpy(), "dx": x.grad.numpy(),
     }
@@ -167,8 +172,8 @@ def gen_hstu_case(HSTU, name, B, N0, out_len, D, H, dqk, dv, blocks, seed,
         rec["param:" + pname] = p.detach().numpy()
         rec["grad:" + pname] = (p.grad if p.grad is not None
                                 else torch.zeros_like(p)).numpy()
-    np.savez_compressed(os.path.join(OUT, f"hstu_{name}.npz"), **rec)
-    print(f"hstu_{name}: y {tuple(y.shape)} |y|max {y.abs().max():.3f}")
+    np.savez_compressed(os.path.join(OUT, f"{prefix}_{name}.npz"), **rec)
+    print(f"{prefix}_{name}: y {tuple(y.shape)} |y|max {y.abs().max():.3f}")
 
 
 def gen_hstu_decode_case(HSTU, name, B, N0, out_len, D, H, dqk, dv, blocks, seed, lengths,
@@ -251,6 +256,22 @@ def gen_decode():
                          lengths=[14, 6], positions=[13, 5], with_ts=False)
     gen_hstu_decode_case(HSTU, "b2_n12_d16_cua", 2, 12, 2, 16, 1, 16, 16, 2, seed=64,
                          lengths=[10, 14], positions=[9, 7], concat_ua=True)
+
+
+def gen_softmax():
+    """normalization="softmax_rel_bias" (hstu.py:341-389, non-cached branch): padded q / k
+    over all heads' columns at once, softmax over every one of the n keys (padding and
+    future keys included) of (qk + bias) / sqrt(attention_dim), then the causal mask."""
+    HSTU = _import_reference()[0]
+    gen_hstu_case(HSTU, "b4_n16_d16_h1", 4, 16, 5, 16, 1, 16, 16, 2, seed=71,
+                  normalization="softmax_rel_bias", prefix="softmax")
+    gen_hstu_case(HSTU, "b3_n24_d24_h2", 3, 24, 5, 24, 2, 8, 12, 2, seed=72,
+                  lengths=[29, 1, 13], normalization="softmax_rel_bias", prefix="softmax")
+    gen_hstu_case(HSTU, "b3_n16_d16_norab", 3, 16, 3, 16, 1, 16, 16, 1, seed=73,
+                  normalization="softmax_rel_bias", rab=False, prefix="softmax")
+    gen_hstu_case(HSTU, "b2_n12_d16_cua", 2, 12, 2, 16, 1, 16, 16, 1, seed=74,
+                  lengths=[14, 6], normalization="softmax_rel_bias", concat_ua=True,
+                  prefix="softmax")
 
 
 def gen_topk_case(CandidateIndex, MIPSBruteForceTopK, name, B, X, D, k, N0, seed,
@@ -489,11 +510,15 @@ def main():
     if only == "decode":
         gen_decode()
         return
+    if only == "softmax":
+        gen_softmax()
+        return
     gen_sampled_softmax()
     gen_preprocessor()
     gen_muon()
     gen_embeddings()
     gen_decode()
+    gen_softmax()
     HSTU, CandidateIndex, MIPSBruteForceTopK, ops = _import_reference()
     gen_bucket_thresholds(HSTU)
     gen_jagged_ops(ops)

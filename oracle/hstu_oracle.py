@@ -60,6 +60,7 @@ class HSTUConfig:
     dv: int
     concat_ua: bool = False
     eps: float = 1e-6  # hstu.py:224
+    softmax: bool = False  # normalization="softmax_rel_bias" (hstu.py:341-389)
 
 
 def layer_params_from_state(state: Dict[str, torch.Tensor], i: int,
@@ -69,8 +70,8 @@ def layer_params_from_state(state: Dict[str, torch.Tensor], i: int,
         "uvqk": state[p + "_uvqk"],
         "o_w": state[p + "_o.weight"],
         "o_b": state[p + "_o.bias"],
-        "ts_w": state[p + "_rel_attn_bias._ts_w"],
-        "pos_w": state[p + "_rel_attn_bias._pos_w"],
+        "ts_w": state.get(p + "_rel_attn_bias._ts_w"),  # None: no bias module
+        "pos_w": state.get(p + "_rel_attn_bias._pos_w"),
     }
 
 
@@ -113,15 +114,45 @@ def hstu_attention_jagged(q, k, v, offsets, ts, cfg: HSTUConfig, pos_w, ts_w,
     return torch.cat(outs, 0) if outs else q.new_zeros(0, H * dv)
 
 
+def softmax_attention_jagged(q, k, v, offsets, ts, cfg: HSTUConfig, pos_w, ts_w,
+                             thresholds) -> torch.Tensor:
+    """hstu.py:371-389 (normalization="softmax_rel_bias", no cache) restated per sequence:
+    one score over all heads' columns at once (einsum "bnd,bmd->bnm" of the padded
+    (B, n, h dqk) q / k), plus the bias when the layer has a bias module, scaled by
+    1 / sqrt(attention_dim) and normalised over ALL n keys — the padded keys (k = 0, so
+    their score is the bias alone) and the future ones included — then the causal mask,
+    then the product with the padded v.  Rows past L_b are dropped (dense_to_jagged)."""
+    N = cfg.N
+    outs = []
+    for b in range(offsets.numel() - 1):
+        s, e = int(offsets[b]), int(offsets[b + 1])
+        L = e - s
+        if L == 0:
+            continue
+        kb = torch.cat([k[s:e], k.new_zeros(N - L, k.shape[1])])  # (N, h dqk)
+        scores = q[s:e] @ kb.t()  # (L, N)
+        if pos_w is not None:
+            i = torch.arange(L).view(L, 1)
+            j = torch.arange(N).view(1, N)
+            ext = torch.cat([ts[b], ts[b, N - 1:N]])
+            delta = ext[1:L + 1].view(L, 1) - ts[b].view(1, N)
+            scores = scores + (pos_w[(N - 1) + j - i] +
+                               ts_w[bucket_via_thresholds(delta, thresholds)])
+        a = F.softmax(scores / (cfg.dqk ** 0.5), dim=-1)
+        a = a * torch.tril(torch.ones(L, N, dtype=a.dtype))
+        outs.append(a[:, :L] @ v[s:e])
+    return torch.cat(outs, 0) if outs else q.new_zeros(0, v.shape[1])
+
+
 def stu_layer_jagged(x, offsets, ts, cfg: HSTUConfig, p, thresholds):
-    """hstu.py:266-413 (eval mode, normalization='rel_bias', linear_config='uvqk',
-    linear_activation='silu')."""
+    """hstu.py:266-413 (eval mode, normalization='rel_bias' or 'softmax_rel_bias',
+    linear_config='uvqk', linear_activation='silu')."""
     H, dv, dqk = cfg.H, cfg.dv, cfg.dqk
     normed = F.layer_norm(x, [cfg.D], eps=cfg.eps)
     h = F.silu(normed @ p["uvqk"])
     u, v, q, k = torch.split(h, [dv * H, dv * H, dqk * H, dqk * H], dim=1)
-    attn = hstu_attention_jagged(q, k, v, offsets, ts, cfg, p["pos_w"], p["ts_w"],
-                                 thresholds)
+    attn_fn = softmax_attention_jagged if cfg.softmax else hstu_attention_jagged
+    attn = attn_fn(q, k, v, offsets, ts, cfg, p["pos_w"], p["ts_w"], thresholds)
     a = F.layer_norm(attn, [dv * H], eps=cfg.eps)
     o_in = torch.cat([u, a, u * a], -1) if cfg.concat_ua else u * a
     return o_in @ p["o_w"].t() + p["o_b"] + x

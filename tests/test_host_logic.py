@@ -56,9 +56,14 @@ def test_unsupported_configurations_raise():
     with pytest.raises(ValueError):
         _hstu(autocast_dtype=torch.float16)
     assert _hstu(autocast_dtype=torch.bfloat16)._hstu._attention_layers[0]._geometry(211, 211).bf16
-    enc = _hstu(normalization="softmax_rel_bias")
-    with pytest.raises(NotImplementedError):
-        enc._hstu._attention_layers[0]._geometry(211, 211)
+    enc = _hstu(normalization="softmax_rel_bias")  # supported since round 6: fp32 layer
+    geo = enc._hstu._attention_layers[0]._geometry(211, 211)
+    assert geo.softmax and not geo.a16
+    assert enc._hstu._stack_params(211, 211, None, False) is None  # per-layer nodes
+    enc = _hstu(normalization="softmax_rel_bias", autocast_dtype=torch.bfloat16)
+    assert not enc._hstu._attention_layers[0]._geometry(211, 211).bf16
+    with pytest.raises(ValueError):
+        _hstu(normalization="softmax")._hstu._attention_layers[0]._geometry(211, 211)
 
 
 def test_cpu_tensors_are_rejected_no_silent_fallback():

@@ -16,6 +16,7 @@ from oracle import topk_oracle
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 HSTU_CASES = sorted(glob.glob(os.path.join(GOLDEN, "hstu_*.npz")))
 DECODE_CASES = sorted(glob.glob(os.path.join(GOLDEN, "decode_*.npz")))
+SOFTMAX_CASES = sorted(glob.glob(os.path.join(GOLDEN, "softmax_*.npz")))
 
 
 def _thr():
@@ -54,6 +55,25 @@ def test_hstu_oracle_vs_reference(path, variant):
     ts = torch.tensor(d["ts"]) if int(d["with_ts"]) else None
     fn = O.hstu_forward if variant == "jagged" else O.hstu_forward_padded
     y = fn(torch.tensor(d["lengths"]), x, ts, cfg, layers, _thr())
+    (y * torch.tensor(d["dy"])).sum().backward()
+    assert (y - torch.tensor(d["y"])).abs().max().item() <= 1e-5
+    assert (x.grad - torch.tensor(d["dx"])).abs().max().item() <= 1e-5
+    for k, p in st.items():
+        g = p.grad if p.grad is not None else torch.zeros_like(p)
+        ref = torch.tensor(d["grad:" + k])
+        assert (g - ref).abs().max().item() <= 2e-5 * (1 + ref.abs().max().item()), k
+
+
+@pytest.mark.parametrize("path", SOFTMAX_CASES, ids=[os.path.basename(p) for p in SOFTMAX_CASES])
+def test_softmax_oracle_vs_reference(path):
+    """normalization="softmax_rel_bias" (hstu.py:341-389): output and every gradient."""
+    d = np.load(path)
+    cfg = O.HSTUConfig(N=int(d["N"]), D=int(d["D"]), H=int(d["H"]), dqk=int(d["dqk"]),
+                       dv=int(d["dv"]), concat_ua=bool(d["concat_ua"]), softmax=True)
+    st = {k[6:]: torch.tensor(d[k], requires_grad=True) for k in d.files if k.startswith("param:")}
+    layers = [O.layer_params_from_state(st, i) for i in range(int(d["blocks"]))]
+    x = torch.tensor(d["x"], requires_grad=True)
+    y = O.hstu_forward(torch.tensor(d["lengths"]), x, torch.tensor(d["ts"]), cfg, layers, _thr())
     (y * torch.tensor(d["dy"])).sum().backward()
     assert (y - torch.tensor(d["y"])).abs().max().item() <= 1e-5
     assert (x.grad - torch.tensor(d["dx"])).abs().max().item() <= 1e-5
