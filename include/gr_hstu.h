@@ -47,7 +47,7 @@ GR_API int gr_version(void);
  * wgrad_reduce, mips_pack, mips_select, mips_merge, cumsum, dense_to_jagged, encoder_prologue, bf16_scale_add, adamw,
  * jagged_to_padded, l2_normalize, current_embeddings, sampled_softmax_fwd,
  * sampled_softmax_bwd, sampled_softmax_csr, sampled_softmax_table_grad, preproc, rows_copy,
- * decode_attn, softmax_attn_fwd, softmax_attn_bwd.  Not for use inside a captured graph.
+ * decode_scatter, decode_attn, softmax_attn_fwd, softmax_attn_bwd.  Not for use inside a captured graph.
  */
 GR_API int gr_timing_enable(int on);
 GR_API int gr_timing_query(const char* kernel, double* total_ms, int* launches);
@@ -321,6 +321,16 @@ GR_API int gr_rows_copy(const float* src, int64_t ld_src, const int64_t* src_ind
                         int64_t src_step, int64_t src_rows, float* dst, int64_t ld_dst,
                         const int64_t* dst_index, int64_t dst_step, int64_t dst_rows, int n,
                         int width, void* stream);
+/* hstu_decode_scatter (replaces the cache updates of hstu.py:321-322 and :160-177, three
+ * index_copy_ in one launch): for e < n, with v | q | k the columns hv .. of row e of uvqk
+ * (u | v | q | k, widths hv, hv, hq, hq):
+ *   v_cache[rows[e]] = v_e  (v_cache (v_rows, hv)),
+ *   q_cache[pos[e] + e N] = q_e, k_cache[pos[e] + e N] = k_e  (q / k caches (qk_rows, hq)).
+ * Out-of-range rows are skipped. */
+GR_API int hstu_decode_scatter(const float* uvqk, int64_t ld_u, int hv, int hq,
+                               const int64_t* rows, const int64_t* pos, int n, int N,
+                               float* v_cache, int64_t v_rows, float* q_cache, float* k_cache,
+                               int64_t qk_rows, void* stream);
 /* hstu_decode_attn (replaces hstu.py:186-205 + 393-397 of the cached branch: the full
  * (B, h, n, n) attention over the caches of which only the delta rows are kept): for
  * e < n_rows, h < H, with r = rows[e] in sequence b (offsets[b] <= r < offsets[b + 1])
@@ -329,15 +339,18 @@ GR_API int gr_rows_copy(const float* src, int64_t ld_src, const int64_t* src_ind
  *                      * v_cache[offsets[b] + j][h dv + c]
  * (head h's columns h dqk .. of q / k; bias as hstu_rel_bias_fwd, none when ts is NULL).
  * q_cache / k_cache (B, N, ld_qk) f32, v_cache (v_rows, ld_v) f32 jagged, out (n_rows,
- * ld_out).  Rows outside [0, offsets[B]) give zeros.  LDS bound: N up to ~15 K.
+ * ld_out).  Rows outside [0, offsets[B]) give zeros.  Two launches: 64-key chunks of each
+ * row into workspace partials, then their sum in chunk order (deterministic);
+ * n_rows <= 65535.
  */
-GR_API size_t hstu_decode_attn_lds_bytes(int N, int dqk, int dv, int num_buckets);
+GR_API size_t hstu_decode_attn_workspace_size(int n_rows, int N, int H, int dv);
 GR_API int hstu_decode_attn(const float* q_cache, const float* k_cache, int64_t ld_qk,
                             const float* v_cache, int64_t ld_v, int64_t v_rows,
                             const int64_t* offsets, int B, const int64_t* rows, int n_rows,
                             int N, int H, int dqk, int dv, const int64_t* ts,
                             const int64_t* bucket_thr, int num_buckets, const float* pos_w,
-                            const float* ts_w, float* out, int64_t ld_out, void* stream);
+                            const float* ts_w, float* out, int64_t ld_out, void* workspace,
+                            size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------- softmax attention (ABI 18)
  * hstu_softmax_attn_fwd replaces the normalization="softmax_rel_bias" branch of

@@ -115,7 +115,7 @@ KERNEL_NAMES = ("bucket_map", "attn_fwd", "attn_bwd", "attn_bwd_dkv", "attn_bwd_
                 "dense_to_jagged", "jagged_to_padded", "l2_normalize", "current_embeddings",
                 "sampled_softmax_fwd", "sampled_softmax_bwd", "sampled_softmax_csr",
                 "sampled_softmax_table_grad", "preproc", "item_embedding", "mips_sort_invalid",
-                "mips_wide_score", "mips_wide_select", "rows_copy", "decode_attn",
+                "mips_wide_score", "mips_wide_select", "rows_copy", "decode_scatter", "decode_attn",
                 "softmax_attn_fwd", "softmax_attn_bwd")
 
 

@@ -5,10 +5,12 @@
 // jagged v cache and their q / k into the padded (B, n, .) caches (index_copy_), then runs
 // the WHOLE (B, h, n, n) attention over the caches and keeps the delta rows
 // (hstu.py:393-397).  Only those rows reach the output, so hstu_decode_attn computes just
-// them: one workgroup per (delta row, head) streams the cached keys 0 .. p of the row's
-// sequence (p = its position) and their values — an HBM-bound pass over K and V of
-// 4 (p + 1) (dqk + dv) bytes per (row, head), no (n, n) scores.  gr_rows_copy does the
-// row gathers / scatters (x[delta], the three cache updates, the output rows).
+// them: workgroups of 64 cached keys (chunk, head, delta row) stream the keys 0 .. p of the
+// row's sequence (p = its position) and their values — an HBM-bound pass over K and V of
+// 4 (p + 1) (dqk + dv) bytes per (row, head), no (n, n) scores — and a second launch sums
+// the chunks' partial rows in chunk order (SiLU attention has no row normaliser, so the
+// chunks' sums simply add).  hstu_decode_scatter writes the three cache updates in one
+// launch; gr_rows_copy does the other row moves (x[delta], the output rows).
 #include "common.h"
 
 #include "../../include/gr_hstu.h"
@@ -32,6 +34,30 @@ __global__ __launch_bounds__(256) void rows_copy_kernel(const float* src, int64_
   for (int c = threadIdx.x; c < width; c += 256) d[c] = s[c];
 }
 
+// v_cache[rows[e]] = v_e, q_cache[pos[e] + e N] = q_e, k_cache[pos[e] + e N] = k_e for the
+// e-th re-encoded row (u | v | q | k columns of uvqk): the three index_copy_ of
+// hstu.py:321-322 and :160-177 in one launch.
+__global__ __launch_bounds__(256) void decode_scatter_kernel(const float* uvqk, int64_t ld_u, int hv,
+                                                             int hq, const int64_t* rows,
+                                                             const int64_t* pos, int N,
+                                                             float* v_cache, int64_t v_rows,
+                                                             float* q_cache, float* k_cache,
+                                                             int64_t qk_rows) {
+  const int64_t e = blockIdx.x;
+  const float* src = uvqk + e * ld_u + hv;  // v | q | k
+  const int64_t rv = rows[e], rq = pos[e] + e * N;
+  const bool v_ok = rv >= 0 && rv < v_rows, qk_ok = pos[e] >= 0 && pos[e] < N && rq < qk_rows;
+  for (int c = threadIdx.x; c < hv + 2 * hq; c += 256) {
+    const float x = src[c];
+    if (c < hv) {
+      if (v_ok) v_cache[rv * hv + c] = x;
+    } else if (qk_ok) {
+      if (c < hv + hq) q_cache[rq * hq + (c - hv)] = x;
+      else k_cache[rq * hq + (c - hv - hq)] = x;
+    }
+  }
+}
+
 struct DecodeArgs {
   const float* q;  // padded (B, N, ld_qk) caches
   const float* k;
@@ -41,108 +67,165 @@ struct DecodeArgs {
   const int64_t* offsets;
   int B;
   const int64_t* rows;  // jagged row of each delta entry
+  int n_rows;
   int N, H, dqk, dv;
   const int64_t* ts;  // (B, N) or NULL (no relative bias)
   const int64_t* thr;
   int nb;
   const float* pos_w;
   const float* ts_w;
+  float* part;  // [chunks][n_rows][H dv] partial sums
   float* out;
   int64_t ld_out;
 };
 
-constexpr int kKeysPerPass = 4;  // keys per wave per pass of the score loop
+constexpr int kDecKeys = 64;  // keys per workgroup (one chunk of a row's keys)
 
-// Workgroup (e, h): row r = rows[e] of sequence b (offsets[b] <= r < offsets[b + 1]) at
-// position p = r - offsets[b]; query = q cache (b, p), keys j = 0 .. p (causal; p < L_b,
-// so every such key is a real item) from the k cache (b, j), values v[offsets[b] + j]:
-//   out[e, h] = sum_j silu(q . k_j + pos_w[N - 1 + j - p] + ts_w[bucket]) / N * v_j
-// (hstu.py:186-205: bias shared across heads; bucket of ts[b, p + 1] - ts[b, j] with
-// ts[b, N] = ts[b, N - 1], hstu.py:113-123).  LDS: thresholds | q | weights [N] | partial
-// sums [4][dv].
-__global__ __launch_bounds__(256) void decode_attn_kernel(DecodeArgs a) {
-  extern __shared__ int64_t smem_i64[];
-  const int e = blockIdx.x, h = blockIdx.y;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const bool bias = a.ts != nullptr;
-  int64_t* thr = smem_i64;
-  float* qs = reinterpret_cast<float*>(thr + (bias ? a.nb + 1 : 0));
-  float* wts = qs + a.dqk;
-  float* part = wts + a.N;
-  float* orow = a.out + (int64_t)e * a.ld_out + (int64_t)h * a.dv;
-  const int64_t r = a.rows[e];
-  const int64_t total = a.offsets[a.B];
-  if (r < 0 || r >= total) {  // validated by the host; zeros rather than a stray read
-    for (int c = tid; c < a.dv; c += 256) orow[c] = 0.f;
-    return;
-  }
+// (sequence, position) of jagged row r: offsets[b] <= r < offsets[b + 1]; false when r is
+// outside [0, offsets[B]) or the position is not below N.
+__device__ __forceinline__ bool decode_locate(const DecodeArgs& a, int64_t r, int& b, int& p) {
+  if (r < 0 || r >= a.offsets[a.B]) return false;
   int lo = 0, hi = a.B;  // offsets[lo] <= r < offsets[hi]
   while (hi - lo > 1) {
     const int mid = (lo + hi) >> 1;
     if (a.offsets[mid] <= r) lo = mid;
     else hi = mid;
   }
-  const int b = lo;
-  const int64_t s0 = a.offsets[b];
-  const int p = (int)(r - s0);
-  if (p >= a.N) {
-    for (int c = tid; c < a.dv; c += 256) orow[c] = 0.f;
-    return;
-  }
+  b = lo;
+  p = (int)(r - a.offsets[lo]);
+  return p < a.N;
+}
+
+// Workgroup (chunk c, head h, delta row e): keys j in [64 c, 64 c + 64) with j <= p of row
+// r = rows[e] (sequence b, position p; every such key is a real item as p < L_b):
+//   part[c][e][h dv + col] = sum_j silu(q . k_j + pos_w[N - 1 + j - p] + ts_w[bucket]) / N
+//                                  * v[offsets[b] + j][h dv + col]
+// (hstu.py:186-205: bias shared across heads; bucket of ts[b, p + 1] - ts[b, j] with
+// ts[b, N] = ts[b, N - 1], hstu.py:113-123).  Scores: 16-lane groups per key (16 keys in
+// flight per pass), lanes over the head dim, a DPP sum; values: threads over columns
+// (coalesced v rows), key subsets per thread group, an LDS reduce.  Chunks past p write
+// nothing (the reduce reads only the chunks a row has).
+template <int VEC>
+__global__ __launch_bounds__(256) void decode_attn_kernel(DecodeArgs a) {
+  extern __shared__ int64_t smem_i64[];
+  const int c = blockIdx.x, h = blockIdx.y, e = blockIdx.z;
+  const int tid = threadIdx.x;
+  int b, p;
+  if (!decode_locate(a, a.rows[e], b, p)) return;
+  const int j0 = c * kDecKeys;
+  if (j0 > p) return;
+  const int nk = p - j0 + 1 < kDecKeys ? p - j0 + 1 : kDecKeys;
+  const bool bias = a.ts != nullptr;
+  int64_t* thr = smem_i64;
+  float* qs = reinterpret_cast<float*>(thr + (bias ? (a.nb + 2) & ~1 : 0));  // 16-byte aligned
+  float* wts = qs + ((a.dqk + 3) & ~3);
+  float* red = wts + kDecKeys;  // [4][dv] group partials
   if (bias)
     for (int i = tid; i <= a.nb; i += 256) thr[i] = a.thr[i];
   const int64_t qk0 = (int64_t)b * a.N;
   const int hq = h * a.dqk;
   for (int d = tid; d < a.dqk; d += 256) qs[d] = a.q[(qk0 + p) * a.ld_qk + hq + d];
   __syncthreads();
+  const int g = tid >> 4, l16 = tid & 15;
   const int64_t tq = bias ? a.ts[qk0 + (p + 1 < a.N ? p + 1 : a.N - 1)] : 0;
   const float inv_n = 1.0f / (float)a.N;
-  // scores: wave w takes keys w*4 .. w*4+3, then +16; lanes split the head dim
-  for (int j0 = kKeysPerPass * w; j0 <= p; j0 += 4 * kKeysPerPass) {
-    float acc[kKeysPerPass];
 #pragma unroll
-    for (int u = 0; u < kKeysPerPass; ++u) {
-      acc[u] = 0.f;
-      const int j = j0 + u;
-      if (j <= p) {
-        const float* kr = a.k + (qk0 + j) * a.ld_qk + hq;
-        for (int d = lane; d < a.dqk; d += 64) acc[u] += qs[d] * kr[d];
+  for (int t = 0; t < kDecKeys / 16; ++t) {
+    const int jj = g + 16 * t;  // key within the chunk
+    float acc = 0.f;
+    if (jj < nk) {
+      const float* kr = a.k + (qk0 + j0 + jj) * a.ld_qk + hq;
+      if (VEC == 4) {
+        for (int d = 4 * l16; d < a.dqk; d += 64) {
+          const float4 kv = *reinterpret_cast<const float4*>(kr + d);
+          const float4 qv = *reinterpret_cast<const float4*>(qs + d);
+          acc += qv.x * kv.x + qv.y * kv.y + qv.z * kv.z + qv.w * kv.w;
+        }
+      } else {
+        for (int d = l16; d < a.dqk; d += 16) acc += qs[d] * kr[d];
       }
     }
-#pragma unroll
-    for (int u = 0; u < kKeysPerPass; ++u) acc[u] = wave_sum(acc[u]);
-    if (lane < kKeysPerPass) {
-      const int j = j0 + lane;
-      float x = lane == 0 ? acc[0] : lane == 1 ? acc[1] : lane == 2 ? acc[2] : acc[3];
-      if (j <= p) {
+    acc = sum16(acc);
+    if (l16 == 0 && jj < kDecKeys) {
+      float w = 0.f;
+      if (jj < nk) {
+        const int j = j0 + jj;
+        float x = acc;
         if (bias)
-          x = x + (a.pos_w[a.N - 1 + j - p] +
-                   a.ts_w[time_bucket(tq - a.ts[qk0 + j], thr, a.nb)]);
-        wts[j] = siluf_(x) * inv_n;
+          x = x + (a.pos_w[a.N - 1 + j - p] + a.ts_w[time_bucket(tq - a.ts[qk0 + j], thr, a.nb)]);
+        w = siluf_(x) * inv_n;
       }
+      wts[jj] = w;
     }
   }
   __syncthreads();
-  // out[c] = sum_j wts[j] v[s0 + j][h dv + c]: wave w sums keys j = w mod 4, lanes over c
+  // values: column groups of dvp = 64 ceil(dv / 64) threads (dv <= 256: 256 / dvp groups
+  // split the chunk's keys; wider: one group loops over the columns)
+  const int dvp = a.dv <= 64 ? 64 : a.dv <= 128 ? 128 : 256;
+  const int ng = 256 / dvp, grp = tid / dvp, lc = tid % dvp;
+  const int64_t vrow0 = a.offsets[b] + j0;
+  // keys whose value rows lie in the cache (all nk once the host has validated it)
+  const int nkv = (int)(vrow0 + nk <= a.v_rows ? nk : (a.v_rows > vrow0 ? a.v_rows - vrow0 : 0));
   const int hv = h * a.dv;
-  // keys whose value rows lie in the cache (all of 0 .. p once the host has validated it)
-  const int pe = (int)(s0 + p < a.v_rows ? p : a.v_rows - 1 - s0);
-  for (int c0 = 0; c0 < a.dv; c0 += 64) {
-    const int c = c0 + lane;
+  float* prow = a.part + ((int64_t)c * a.n_rows + e) * ((int64_t)a.H * a.dv) + hv;
+  for (int col0 = 0; col0 < a.dv; col0 += dvp) {
+    const int col = col0 + lc;
     float acc0 = 0.f, acc1 = 0.f;
-    if (c < a.dv) {
-      int j = w;
-      for (; j + 4 <= pe; j += 8) {
-        acc0 += wts[j] * a.v[(s0 + j) * a.ld_v + hv + c];
-        acc1 += wts[j + 4] * a.v[(s0 + j + 4) * a.ld_v + hv + c];
+    if (col < a.dv) {
+      // 4 independent loads in flight per step
+      const float* vp = a.v + vrow0 * a.ld_v + hv + col;
+      float acc2 = 0.f, acc3 = 0.f;
+      int jj = grp;
+      for (; jj + 3 * ng < nkv; jj += 4 * ng) {
+        const float v0 = vp[(int64_t)jj * a.ld_v], v1 = vp[(int64_t)(jj + ng) * a.ld_v];
+        const float v2 = vp[(int64_t)(jj + 2 * ng) * a.ld_v], v3 = vp[(int64_t)(jj + 3 * ng) * a.ld_v];
+        acc0 += wts[jj] * v0;
+        acc1 += wts[jj + ng] * v1;
+        acc2 += wts[jj + 2 * ng] * v2;
+        acc3 += wts[jj + 3 * ng] * v3;
       }
-      if (j <= pe) acc0 += wts[j] * a.v[(s0 + j) * a.ld_v + hv + c];
-      part[w * a.dv + c] = acc0 + acc1;
+      for (; jj < nkv; jj += ng) acc0 += wts[jj] * vp[(int64_t)jj * a.ld_v];
+      acc0 += acc2;
+      acc1 += acc3;
+    }
+    if (ng == 1) {
+      if (col < a.dv) prow[col] = acc0 + acc1;
+    } else {
+      if (col < a.dv) red[grp * a.dv + col] = acc0 + acc1;
+      __syncthreads();
+      for (int cc = tid; cc < a.dv; cc += 256) {
+        float s = 0.f;
+        for (int q2 = 0; q2 < ng; ++q2) s += red[q2 * a.dv + cc];
+        prow[cc] = s;
+      }
+      __syncthreads();
     }
   }
-  __syncthreads();
-  for (int c = tid; c < a.dv; c += 256)
-    orow[c] = (part[c] + part[a.dv + c]) + (part[2 * a.dv + c] + part[3 * a.dv + c]);
+}
+
+// out[e][col] = sum over the row's chunks of part[c][e][col], in chunk order (deterministic);
+// zeros for rows outside the batch.
+__global__ __launch_bounds__(64) void decode_reduce_kernel(DecodeArgs a) {
+  const int e = blockIdx.y;
+  const int w = a.H * a.dv;
+  const int col = blockIdx.x * 64 + threadIdx.x;
+  int b, p;
+  const bool ok = decode_locate(a, a.rows[e], b, p);
+  const int nc = ok ? p / kDecKeys + 1 : 0;
+  if (col >= w) return;
+  const int64_t cs = (int64_t)a.n_rows * w;  // chunk stride
+  const float* src = a.part + (int64_t)e * w + col;
+  // chunk order fixed (deterministic): 4 partial sums over chunks c = 0, 1, 2, 3 mod 4
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int c = 0;
+  for (; c + 3 < nc; c += 4) {
+    s0 += src[c * cs];
+    s1 += src[(c + 1) * cs];
+    s2 += src[(c + 2) * cs];
+    s3 += src[(c + 3) * cs];
+  }
+  for (; c < nc; ++c) s0 += src[c * cs];
+  a.out[(int64_t)e * a.ld_out + col] = (s0 + s1) + (s2 + s3);
 }
 
 }  // namespace gr
@@ -166,10 +249,26 @@ extern "C" int gr_rows_copy(const float* src, int64_t ld_src, const int64_t* src
   return 0;
 }
 
-extern "C" size_t hstu_decode_attn_lds_bytes(int N, int dqk, int dv, int num_buckets) {
-  if (N <= 0 || dqk <= 0 || dv <= 0) return 0;
-  return sizeof(int64_t) * (size_t)(num_buckets > 0 ? num_buckets + 1 : 0) +
-         sizeof(float) * ((size_t)dqk + (size_t)N + 4 * (size_t)dv);
+extern "C" int hstu_decode_scatter(const float* uvqk, int64_t ld_u, int hv, int hq,
+                                   const int64_t* rows, const int64_t* pos, int n, int N,
+                                   float* v_cache, int64_t v_rows, float* q_cache,
+                                   float* k_cache, int64_t qk_rows, void* stream) {
+  GR_REQUIRE(uvqk && rows && pos && v_cache && q_cache && k_cache,
+             "hstu_decode_scatter: null pointer");
+  GR_REQUIRE(n >= 0 && N > 0 && hv > 0 && hq > 0 && ld_u >= hv + 2 * (int64_t)hq + hv,
+             "hstu_decode_scatter: bad sizes (n %d, N %d, hv %d, hq %d)", n, N, hv, hq);
+  if (n == 0) return 0;
+  const hipStream_t st = (hipStream_t)stream;
+  GR_TIMED("decode_scatter", st,
+           hipLaunchKernelGGL(gr::decode_scatter_kernel, dim3(n), dim3(256), 0, st, uvqk, ld_u,
+                              hv, hq, rows, pos, N, v_cache, v_rows, q_cache, k_cache, qk_rows));
+  GR_LAUNCH_CHECK("hstu_decode_scatter");
+  return 0;
+}
+
+extern "C" size_t hstu_decode_attn_workspace_size(int n_rows, int N, int H, int dv) {
+  if (n_rows <= 0 || N <= 0 || H <= 0 || dv <= 0) return 0;
+  return sizeof(float) * (size_t)((N + gr::kDecKeys - 1) / gr::kDecKeys) * n_rows * H * dv;
 }
 
 extern "C" int hstu_decode_attn(const float* q_cache, const float* k_cache, int64_t ld_qk,
@@ -177,7 +276,8 @@ extern "C" int hstu_decode_attn(const float* q_cache, const float* k_cache, int6
                                 const int64_t* offsets, int B, const int64_t* rows, int n_rows,
                                 int N, int H, int dqk, int dv, const int64_t* ts,
                                 const int64_t* bucket_thr, int num_buckets, const float* pos_w,
-                                const float* ts_w, float* out, int64_t ld_out, void* stream) {
+                                const float* ts_w, float* out, int64_t ld_out, void* workspace,
+                                size_t ws_bytes, void* stream) {
   GR_REQUIRE(q_cache && k_cache && v_cache && offsets && rows && out,
              "hstu_decode_attn: null pointer");
   GR_REQUIRE(B > 0 && N > 0 && H > 0 && dqk > 0 && dv > 0 && n_rows >= 0 && v_rows >= 0,
@@ -186,15 +286,32 @@ extern "C" int hstu_decode_attn(const float* q_cache, const float* k_cache, int6
              "hstu_decode_attn: bad strides");
   GR_REQUIRE(!ts || (bucket_thr && pos_w && ts_w && num_buckets > 0 && num_buckets < 256),
              "hstu_decode_attn: timestamps given without bucket_thr / pos_w / ts_w");
-  const size_t lds = hstu_decode_attn_lds_bytes(N, dqk, dv, ts ? num_buckets : 0);
-  GR_REQUIRE(lds <= 64 * 1024, "hstu_decode_attn: N %d too large (%zu B of LDS)", N, lds);
+  GR_REQUIRE(n_rows <= 65535, "hstu_decode_attn: %d rows (at most 65535 per call)", n_rows);
   if (n_rows == 0) return 0;
-  gr::DecodeArgs a{q_cache, k_cache, ld_qk, v_cache, ld_v, v_rows, offsets, B, rows, N, H, dqk,
-                   dv, ts, bucket_thr, num_buckets, pos_w, ts_w, out, ld_out};
+  const size_t need = hstu_decode_attn_workspace_size(n_rows, N, H, dv);
+  GR_REQUIRE(workspace && ws_bytes >= need, "hstu_decode_attn: workspace %zu B < %zu B",
+             ws_bytes, need);
+  const int dvr = dv <= 256 ? dv : 256;  // the group-partial rows (dv > 256: one group)
+  const size_t lds = sizeof(int64_t) * (size_t)(ts ? (num_buckets + 2) & ~1 : 0) +
+                     sizeof(float) * ((size_t)((dqk + 3) & ~3) + gr::kDecKeys + 4 * (size_t)dvr);
+  GR_REQUIRE(lds <= 64 * 1024, "hstu_decode_attn: head dims too large (%zu B of LDS)", lds);
+  gr::DecodeArgs a{q_cache, k_cache, ld_qk, v_cache, ld_v, v_rows, offsets, B, rows, n_rows,
+                   N, H, dqk, dv, ts, bucket_thr, num_buckets, pos_w, ts_w, (float*)workspace,
+                   out, ld_out};
+  const bool vec = dqk % 4 == 0 && ld_qk % 4 == 0 && ((uintptr_t)q_cache & 15) == 0 &&
+                   ((uintptr_t)k_cache & 15) == 0;
   const hipStream_t st = (hipStream_t)stream;
-  GR_TIMED("decode_attn", st,
-           hipLaunchKernelGGL(gr::decode_attn_kernel, dim3(n_rows, H), dim3(256), (uint32_t)lds,
-                              st, a));
+  const dim3 grid((N + gr::kDecKeys - 1) / gr::kDecKeys, H, n_rows);
+  GR_TIMED("decode_attn", st, {
+    if (vec)
+      hipLaunchKernelGGL(gr::decode_attn_kernel<4>, grid, dim3(256), (uint32_t)lds, st, a);
+    else
+      hipLaunchKernelGGL(gr::decode_attn_kernel<1>, grid, dim3(256), (uint32_t)lds, st, a);
+  });
   GR_LAUNCH_CHECK("hstu_decode_attn");
+  GR_TIMED("decode_attn", st,
+           hipLaunchKernelGGL(gr::decode_reduce_kernel, dim3((H * dv + 63) / 64, n_rows), dim3(64),
+                              0, st, a));
+  GR_LAUNCH_CHECK("hstu_decode_attn(reduce)");
   return 0;
 }

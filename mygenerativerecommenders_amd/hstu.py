@@ -227,7 +227,7 @@ class SequentialTransductionUnitJagged(torch.nn.Module):
                 raise NotImplementedError("cached decoding with normalization="
                                           "'softmax_rel_bias' (the reference's branch fails)")
             return self._decode(x, x_offsets, all_timestamps, delta_x_offsets, cache, geo,
-                                dropout_step)
+                                dropout_step)[:2]
         if geo.softmax:
             return self._softmax_forward(x, x_offsets, all_timestamps, n, geo, return_cache_states,
                                          dropout_step)
@@ -279,8 +279,11 @@ class SequentialTransductionUnitJagged(torch.nn.Module):
             return y, ops.stu_cache_states(uvqk, y, x_offsets, int(x_offsets[-1]), geo)
         return y, (None, None, None, y)
 
-    def _decode(self, x, x_offsets, all_timestamps, delta_x_offsets, cache, geo, dropout_step):
-        """hstu.py:293-298 (assert cache is not None), 321-322, 151-177, 393-418."""
+    def _decode(self, x, x_offsets, all_timestamps, delta_x_offsets, cache, geo, dropout_step,
+                xd=None):
+        """hstu.py:293-298 (assert cache is not None), 321-322, 151-177, 393-418.  Returns
+        (outputs, cache states, the re-encoded rows); ``xd``: this layer's x[delta] rows
+        when the caller already has them."""
         if cache is None:
             raise ValueError("delta_x_offsets requires the cache states of a previous pass")
         if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
@@ -295,12 +298,13 @@ class SequentialTransductionUnitJagged(torch.nn.Module):
             else:
                 self._dropout_step.add_(1)
                 step = self._dropout_step
-        out = ops.stu_decode(x, x_offsets, all_timestamps if rab is not None else None,
-                             delta_x_offsets[0], delta_x_offsets[1], cache, self._uvqk,
-                             self._o.weight, self._o.bias,
-                             rab._pos_w if rab is not None else None,
-                             rab._ts_w if rab is not None else None, geo, self._dropout_seed, step)
-        return out, (cache[0], cache[1], cache[2], out)
+        out, y = ops.stu_decode(x, x_offsets, all_timestamps if rab is not None else None,
+                                delta_x_offsets[0], delta_x_offsets[1], cache, self._uvqk,
+                                self._o.weight, self._o.bias,
+                                rab._pos_w if rab is not None else None,
+                                rab._ts_w if rab is not None else None, geo, self._dropout_seed,
+                                step, xd=xd)
+        return out, (cache[0], cache[1], cache[2], out), y
 
 
 class HSTUJagged(torch.nn.Module):
@@ -348,15 +352,22 @@ class HSTUJagged(torch.nn.Module):
                 raise ValueError("delta_x_offsets requires one cache state per layer")
             d0 = delta_x_offsets[0].to(torch.int64)
             d1 = delta_x_offsets[1].to(torch.int64)
-            ops.check_decode_step(x_offsets, d0, d1, n)
+            distinct = ops.check_decode_step(x_offsets, d0, d1, n)
             step = None
             if self._needs_step():
                 self._dropout_step.add_(1)
                 step = self._dropout_step
+            xd = None
             for i, layer in enumerate(self._attention_layers):
-                x, cs = layer(x=x, x_offsets=x_offsets, all_timestamps=all_timestamps,
-                              invalid_attn_mask=invalid_attn_mask, delta_x_offsets=(d0, d1),
-                              cache=cache[i], max_len=max_len, dropout_step=step)
+                geo = layer._geometry(n, n if max_len is None else max_len)
+                if geo.softmax:
+                    # hstu.py:342-343 evaluates x_offsets.size() - 1, which raises (TypeError)
+                    raise NotImplementedError("cached decoding with normalization="
+                                              "'softmax_rel_bias' (the reference's branch fails)")
+                x, cs, y = layer._decode(x, x_offsets, all_timestamps, (d0, d1), cache[i], geo,
+                                         step, xd=xd)
+                # distinct delta rows: the rows just re-encoded are the next layer's x[delta]
+                xd = y if distinct else None
                 if return_cache_states:
                     cache_states.append(cs)
             return x, cache_states

@@ -1204,31 +1204,38 @@ def stu_cache_states(uvqk: torch.Tensor, y: torch.Tensor, offsets: torch.Tensor,
 
 
 def check_decode_step(offsets: torch.Tensor, delta_rows: torch.Tensor, delta_pos: torch.Tensor,
-                      N: int) -> None:
+                      N: int) -> bool:
     """The reference's cached step (hstu.py:151-177, 293-298) takes one delta entry per
     sequence (its flattened padded index is delta[1][e] + e * n) and indexes rows with
     index_copy_, which raises on an index out of range: the same conditions, checked here
-    with one host synchronisation per step."""
+    with one host synchronisation per step.  Returns whether the delta rows are distinct
+    (then a layer's re-encoded rows are the next layer's input rows as they are)."""
     B = offsets.numel() - 1
     if delta_rows.numel() != B or delta_pos.numel() != B:
         raise ValueError(f"delta_x_offsets: {delta_rows.numel()} / {delta_pos.numel()} entries "
                          f"for {B} sequences (one per sequence, hstu.py:153-159)")
-    ok = torch.stack([(delta_rows >= 0).all(), (delta_rows < offsets[-1]).all(),
-                      (delta_pos >= 0).all(), (delta_pos < N).all()]).all()
-    if not bool(ok):
+    srt = torch.sort(delta_rows)[0]
+    flags = torch.stack([(delta_rows >= 0).all(), (delta_rows < offsets[-1]).all(),
+                         (delta_pos >= 0).all(), (delta_pos < N).all(),
+                         (srt[1:] != srt[:-1]).all()]).cpu()
+    if not bool(flags[:4].all()):
         raise IndexError("delta_x_offsets: a row outside [0, offsets[B]) or a position "
                          f"outside [0, {N})")
+    return bool(flags[4])
 
 
 def stu_decode(x, offsets, timestamps, delta_rows, delta_pos, cache, w_uvqk, w_o, b_o, pos_w,
-               ts_w, geo: STUGeometry, seed: int = 0, seed_offset=None) -> torch.Tensor:
+               ts_w, geo: STUGeometry, seed: int = 0, seed_offset=None, xd=None):
     """One cached step of a layer (hstu.py:293-298, 321-322, 151-177, 393-418), fp32:
     x (rows, D) jagged layer input, delta_rows / delta_pos the delta_x_offsets pair
     (validated by ``check_decode_step``), cache = (v, padded q, padded k, outputs) from a
     pass with return_cache_states, UPDATED IN PLACE as the reference's index_copy_ does.
-    Launches: row gather, LN + UVQK on the delta rows, 3 cache scatters, the delta rows'
-    attention (hstu_decode_attn), the gate + O projection, the output scatter.  Returns
-    the updated outputs cache (the next layer's input).  Forward only."""
+    ``xd`` (optional): the rows x[delta_rows] when the caller has them (the previous
+    layer's re-encoded rows, for distinct delta rows).  Launches: the row gather (unless
+    ``xd``), LN + UVQK on the delta rows, the cache scatter (hstu_decode_scatter), the
+    delta rows' attention (hstu_decode_attn: chunks + reduce), the gate + O projection,
+    the output scatter.  Returns (the updated outputs cache = the next layer's input,
+    the re-encoded rows).  Forward only."""
     v_c, q_c, k_c, out_c = cache
     _lib.require_gpu(x, offsets, delta_rows, delta_pos, v_c, q_c, k_c, out_c, w_uvqk, w_o, b_o)
     dev = x.device
@@ -1248,9 +1255,10 @@ def stu_decode(x, offsets, timestamps, delta_rows, delta_pos, cache, w_uvqk, w_o
     x = x.contiguous()
     rows_i = delta_rows.to(torch.int64).contiguous()
     pos_i = delta_pos.to(torch.int64).contiguous()
-    xd = torch.empty(E, D, dtype=torch.float32, device=dev)
-    _lib.call("gr_rows_copy", x.data_ptr(), D, rows_i.data_ptr(), 0, x.shape[0], xd.data_ptr(), D,
-              None, 0, E, E, D, st)
+    if xd is None:
+        xd = torch.empty(E, D, dtype=torch.float32, device=dev)
+        _lib.call("gr_rows_copy", x.data_ptr(), D, rows_i.data_ptr(), 0, x.shape[0], xd.data_ptr(),
+                  D, None, 0, E, E, D, st)
     off_d = torch.arange(E + 1, dtype=torch.int64, device=dev)
     x_stats = torch.empty(E, 2, dtype=torch.float32, device=dev)
     uvqk = torch.empty(E, n_out, dtype=torch.float32, device=dev)
@@ -1258,12 +1266,9 @@ def stu_decode(x, offsets, timestamps, delta_rows, delta_pos, cache, w_uvqk, w_o
     _lib.call("hstu_ln_uvqk_fwd", xd.data_ptr(), D, off_d.data_ptr(), E, E, D, w_uvqk.data_ptr(),
               n_out, geo.eps, geo.activation, x_stats.data_ptr(), None, uvqk.data_ptr(), n_out, st)
     # cache updates: v at the jagged rows, q / k at (e, delta_pos[e]) of the padded caches
-    _lib.call("gr_rows_copy", uvqk[:, hv:].data_ptr(), n_out, None, 0, E, v_c.data_ptr(), hv,
-              rows_i.data_ptr(), 0, v_c.shape[0], E, hv, st)
-    _lib.call("gr_rows_copy", uvqk[:, 2 * hv:].data_ptr(), n_out, None, 0, E, q_c.data_ptr(), hq,
-              pos_i.data_ptr(), N, B * N, E, hq, st)
-    _lib.call("gr_rows_copy", uvqk[:, 2 * hv + hq:].data_ptr(), n_out, None, 0, E, k_c.data_ptr(),
-              hq, pos_i.data_ptr(), N, B * N, E, hq, st)
+    _lib.call("hstu_decode_scatter", uvqk.data_ptr(), n_out, hv, hq, rows_i.data_ptr(),
+              pos_i.data_ptr(), E, N, v_c.data_ptr(), v_c.shape[0], q_c.data_ptr(), k_c.data_ptr(),
+              B * N, st)
     attn = torch.empty(E, hv, dtype=torch.float32, device=dev)
     bias = timestamps is not None and pos_w is not None and ts_w is not None
     ts = pw = tw = thr = None
@@ -1274,10 +1279,12 @@ def stu_decode(x, offsets, timestamps, delta_rows, delta_pos, cache, w_uvqk, w_o
         pw = pos_w.detach().float().contiguous()
         tw = ts_w.detach().float().contiguous()
         thr = bucket_thresholds(dev)
+    ws_n = _lib.lib().hstu_decode_attn_workspace_size(E, N, H, dv)
+    ws = torch.empty(max(ws_n, 4), dtype=torch.uint8, device=dev)
     _lib.call("hstu_decode_attn", q_c.data_ptr(), k_c.data_ptr(), hq, v_c.data_ptr(), hv,
               v_c.shape[0], offsets.data_ptr(), B, rows_i.data_ptr(), E, N, H, dqk, dv,
               _lib.ptr(ts), _lib.ptr(thr), NUM_BUCKETS, _lib.ptr(pw), _lib.ptr(tw),
-              attn.data_ptr(), hv, st)
+              attn.data_ptr(), hv, ws.data_ptr(), ws_n, st)
     y = torch.empty(E, D, dtype=torch.float32, device=dev)
     attn_stats = torch.empty(E, 2, dtype=torch.float32, device=dev)
     w_o = w_o.detach().float().contiguous()
@@ -1298,7 +1305,7 @@ def stu_decode(x, offsets, timestamps, delta_rows, delta_pos, cache, w_uvqk, w_o
                   *tail, None, y.data_ptr(), D, st)
     _lib.call("gr_rows_copy", y.data_ptr(), D, None, 0, E, out_c.data_ptr(), D, rows_i.data_ptr(),
               0, out_c.shape[0], E, D, st)
-    return out_c
+    return out_c, y
 
 
 # ------------------------------------------------------------------ sampled-softmax loss

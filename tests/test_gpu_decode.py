@@ -74,12 +74,15 @@ def test_decode_matches_reference_golden(path):
             _close(t, d[f"s1:{l}:{nm}"], f"s1:{l}:{nm}")
 
 
-def _random_case(B, N, D, H, d, blocks, seed, with_ts=True, concat_ua=False):
+def _random_case(B, N, D, H, d, blocks, seed, with_ts=True, concat_ua=False, positions=None):
     g = torch.Generator().manual_seed(seed)
     lengths = torch.randint(1, N + 1, (B,), generator=g)
     lengths[0] = N  # a full-length row: query N - 1 takes the ts[N - 1] wrap
     pos = (torch.rand(B, generator=g) * lengths).long().clamp(max=lengths - 1)
     pos[1 % B] = lengths[1 % B] - 1
+    if positions is not None:
+        lengths[:] = N
+        pos = torch.tensor(positions, dtype=torch.int64)
     ts = torch.zeros(B, N, dtype=torch.int64)
     for b in range(B):
         ts[b, :] = 10**9 + torch.cumsum(torch.randint(1, 200000, (N,), generator=g), 0)
@@ -146,6 +149,28 @@ def test_decode_matches_oracle(shape):
         delta=(torch.tensor(rec["delta0"]), torch.tensor(rec["delta1"])), cache=cpu_states)
     _close(y1, y1_ref, "y1", rel=1e-4)
     for l in range(blocks):
+        for nm, t, r in zip(NAMES, states1[l], states1_ref[l]):
+            _close(t, r, f"s1:{l}:{nm}", rel=1e-4)
+
+
+@pytest.mark.parametrize("d", [50, 32], ids=["scalar_d50", "vec_d32"])
+def test_decode_chunk_boundaries(d):
+    """Positions on both sides of the 64-key chunk boundaries of hstu_decode_attn (its
+    chunk partials are summed by the reduce launch), at a head dim read by scalar loads
+    (d = 50) and by float4 loads (d = 32)."""
+    rec = _random_case(7, 200, d, 1, d, 2, seed=d, positions=[0, 63, 64, 127, 128, 198, 199])
+    enc = _build(rec)
+    cfg, layers = _oracle_layers(rec)
+    with torch.no_grad():
+        _, states = _run(enc, rec, "0")
+        cpu_states = [tuple(t.cpu().clone() for t in st) for st in states]
+        delta = (torch.tensor(rec["delta0"]).cuda(), torch.tensor(rec["delta1"]).cuda())
+        y1, states1 = _run(enc, rec, "1", states, delta)
+    y1_ref, states1_ref = O.hstu_forward_cached(
+        torch.tensor(rec["lengths"]), torch.tensor(rec["x1"]), torch.tensor(rec["ts1"]), cfg,
+        layers, delta=(torch.tensor(rec["delta0"]), torch.tensor(rec["delta1"])), cache=cpu_states)
+    _close(y1, y1_ref, "y1", rel=1e-4)
+    for l in range(2):
         for nm, t, r in zip(NAMES, states1[l], states1_ref[l]):
             _close(t, r, f"s1:{l}:{nm}", rel=1e-4)
 
@@ -218,7 +243,11 @@ def test_decode_native_entry_points():
         try:
             _lib.kernel_times()
             _run(enc, rec, "1", states, delta)
-            t = _lib.kernel_times(("decode_attn", "rows_copy", "ln_uvqk_fwd", "gate_o_fwd"))
+            t = _lib.kernel_times(("decode_attn", "decode_scatter", "rows_copy", "ln_uvqk_fwd",
+                                   "gate_o_fwd"))
         finally:
             _lib.timing_enable(False)
-    assert t["decode_attn"][1] == 1 and t["rows_copy"][1] == 5, t
+    # one layer: the row gather and the output scatter; the cache scatter; the chunk and
+    # reduce launches of the attention
+    assert t["decode_attn"][1] == 2 and t["decode_scatter"][1] == 1, t
+    assert t["rows_copy"][1] == 2, t
