@@ -352,6 +352,21 @@ GR_API int hstu_decode_attn(const float* q_cache, const float* k_cache, int64_t 
                             const float* ts_w, float* out, int64_t ld_out, void* workspace,
                             size_t ws_bytes, void* stream);
 
+/* hstu_decode_ln_uvqk / hstu_decode_gate_o: the cached step's two projections at one row
+ * per sequence (n rows, inference: no statistics, pre-activations or dropout), tiled for
+ * small n (16 rows x 16 output columns per workgroup):
+ *   uvqk[r] = act(LN(x[r]) @ w_uvqk)                       (hstu_ln_uvqk_fwd; D <= 512)
+ *   y[r]    = (u[r] * LN(attn[r])) @ w_o^T + b_o + x_res[r]  (hstu_gate_o_fwd at dropout 0;
+ *                                                           hdv <= 256; b_o, x_res may be NULL)
+ * timed as ln_uvqk_fwd / gate_o_fwd. */
+GR_API int hstu_decode_ln_uvqk(const float* x, int64_t ld_x, int n, int D, const float* w_uvqk,
+                               int n_out, float eps, int activation, float* uvqk,
+                               int64_t ld_out, void* stream);
+GR_API int hstu_decode_gate_o(const float* u, int64_t ld_u, const float* attn, int64_t ld_attn,
+                              int n, int hdv, int D, const float* w_o, const float* b_o,
+                              const float* x_res, int64_t ld_x, float eps, float* y,
+                              int64_t ld_y, void* stream);
+
 /* ---------------------------------------------------------------- softmax attention (ABI 18)
  * hstu_softmax_attn_fwd replaces the normalization="softmax_rel_bias" branch of
  * SequentialTransductionUnitJagged.forward (sequential_encoders/hstu.py:341-389, no

@@ -228,6 +228,146 @@ __global__ __launch_bounds__(64) void decode_reduce_kernel(DecodeArgs a) {
   a.out[(int64_t)e * a.ld_out + col] = (s0 + s1) + (s2 + s3);
 }
 
+// ---------------------------------------------------------------- small-M projections
+// The decode step's projections have one row per sequence (M = B: 32 at the C3 width).
+// The training GEMMs tile 64 rows per workgroup, which leaves 4 workgroups at M = 32;
+// these tile 16 rows x 16 output columns with both operands staged in LDS, so a
+// (1024-column, 32-row) projection runs as 128 workgroups, each reading its 16 weight
+// columns once (coalesced) and one output per thread.
+
+constexpr int kSmRows = 16, kSmCols = 16;
+
+// LayerNorm (no affine, biased variance, hstu.py:258-259) of rows r0 .. r0 + 15 of x into
+// LDS xn[16][D] (D <= 512); wave w normalises rows 4 w .. 4 w + 3, whose loads are all
+// issued before the first reduction.
+__device__ __forceinline__ void sm_layernorm(const float* x, int64_t ld_x, int n, int r0, int D,
+                                             float eps, float* xn) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float v[4][8];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int r = r0 + 4 * w + q;
+    const float* xr = x + (int64_t)(r < n ? r : 0) * ld_x;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const int d = lane + 64 * m;
+      v[q][m] = r < n && d < D ? xr[d] : 0.f;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int rr = 4 * w + q;
+    if (r0 + rr >= n) break;
+    float s = 0.f;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) s += v[q][m];
+    const float mean = wave_sum(s) / (float)D;
+    float var = 0.f;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const float t = lane + 64 * m < D ? v[q][m] - mean : 0.f;
+      var += t * t;
+    }
+    const float rstd = 1.0f / sqrtf(wave_sum(var) / (float)D + eps);
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const int d = lane + 64 * m;
+      if (d < D) xn[rr * D + d] = (v[q][m] - mean) * rstd;
+    }
+  }
+}
+
+// sum_k a[k] b[k * sb] over LDS rows, 4 partial sums
+__device__ __forceinline__ float sm_dot(const float* a, const float* b, int sb, int K) {
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int k = 0;
+  for (; k + 3 < K; k += 4) {
+    s0 += a[k] * b[k * sb];
+    s1 += a[k + 1] * b[(k + 1) * sb];
+    s2 += a[k + 2] * b[(k + 2) * sb];
+    s3 += a[k + 3] * b[(k + 3) * sb];
+  }
+  for (; k < K; ++k) s0 += a[k] * b[k * sb];
+  return (s0 + s1) + (s2 + s3);
+}
+
+// uvqk[r][c] = act(LN(x[r]) . w_uvqk[:, c])  (hstu.py:300-305), w_uvqk (D, n_out) row-major.
+// LDS: xn[16][D] | wl[D][16]; thread (row tid / 16, column tid % 16).
+__global__ __launch_bounds__(256) void sm_ln_uvqk_kernel(const float* x, int64_t ld_x, int n,
+                                                         int D, const float* w, int n_out,
+                                                         float eps, int activation, float* out,
+                                                         int64_t ld_out) {
+  extern __shared__ float sm_l[];
+  float* xn = sm_l;
+  float* wl = sm_l + kSmRows * D;
+  const int c0 = blockIdx.x * kSmCols, r0 = blockIdx.y * kSmRows;
+  const int rr = threadIdx.x >> 4, cc = threadIdx.x & 15;
+  {  // 16 rows of 16 columns per step (64-byte runs), all loads issued before the stores
+    float t[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      const int d = rr + kSmRows * i;
+      t[i] = d < D && c0 + cc < n_out ? w[(int64_t)d * n_out + c0 + cc] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      const int d = rr + kSmRows * i;
+      if (d < D) wl[d * kSmCols + cc] = t[i];
+    }
+  }
+  sm_layernorm(x, ld_x, n, r0, D, eps, xn);
+  __syncthreads();
+  const int r = r0 + rr, c = c0 + cc;
+  if (r >= n || c >= n_out) return;
+  const float h = sm_dot(xn + rr * D, wl + cc, kSmCols, D);
+  out[(int64_t)r * ld_out + c] = activation ? siluf_(h) : h;
+}
+
+// y[r][c] = (u[r] * LN(attn[r])) . w_o[c] + b_o[c] + x_res[r][c]  (hstu.py:393-413 without
+// dropout), w_o (D, hdv) row-major (nn.Linear.weight).  LDS: oin[16][hdv] | wt[16][hdv + 1].
+__global__ __launch_bounds__(256) void sm_gate_o_kernel(const float* u, int64_t ld_u,
+                                                        const float* attn, int64_t ld_attn, int n,
+                                                        int hdv, int D, const float* w_o,
+                                                        const float* b_o, const float* x_res,
+                                                        int64_t ld_x, float eps, float* y,
+                                                        int64_t ld_y) {
+  extern __shared__ float sm_g[];
+  float* oin = sm_g;
+  float* wt = sm_g + kSmRows * hdv;
+  const int c0 = blockIdx.x * kSmCols, r0 = blockIdx.y * kSmRows;
+  {  // one k per thread (hdv <= 256), the 16 rows' loads issued before the stores
+    const int k = threadIdx.x;
+    float t[kSmCols];
+#pragma unroll
+    for (int cc = 0; cc < kSmCols; ++cc)
+      t[cc] = k < hdv && c0 + cc < D ? w_o[(int64_t)(c0 + cc) * hdv + k] : 0.f;
+    if (k < hdv) {
+#pragma unroll
+      for (int cc = 0; cc < kSmCols; ++cc) wt[cc * (hdv + 1) + k] = t[cc];
+    }
+  }
+  sm_layernorm(attn, ld_attn, n, r0, hdv, eps, oin);
+  __syncthreads();
+  {
+    const int k = threadIdx.x;
+    float t[kSmRows];
+#pragma unroll
+    for (int rr = 0; rr < kSmRows; ++rr)
+      t[rr] = k < hdv && r0 + rr < n ? u[(int64_t)(r0 + rr) * ld_u + k] : 0.f;
+    if (k < hdv) {
+#pragma unroll
+      for (int rr = 0; rr < kSmRows; ++rr) oin[rr * hdv + k] *= t[rr];
+    }
+  }
+  __syncthreads();
+  const int rr = threadIdx.x >> 4, cc = threadIdx.x & 15;
+  const int r = r0 + rr, c = c0 + cc;
+  if (r >= n || c >= D) return;
+  const float acc = sm_dot(oin + rr * hdv, wt + cc * (hdv + 1), 1, hdv);
+  y[(int64_t)r * ld_y + c] =
+      (acc + (b_o ? b_o[c] : 0.f)) + (x_res ? x_res[(int64_t)r * ld_x + c] : 0.f);
+}
+
 }  // namespace gr
 
 extern "C" int gr_rows_copy(const float* src, int64_t ld_src, const int64_t* src_index,
@@ -313,5 +453,45 @@ extern "C" int hstu_decode_attn(const float* q_cache, const float* k_cache, int6
            hipLaunchKernelGGL(gr::decode_reduce_kernel, dim3((H * dv + 63) / 64, n_rows), dim3(64),
                               0, st, a));
   GR_LAUNCH_CHECK("hstu_decode_attn(reduce)");
+  return 0;
+}
+
+extern "C" int hstu_decode_ln_uvqk(const float* x, int64_t ld_x, int n, int D, const float* w_uvqk,
+                                   int n_out, float eps, int activation, float* uvqk,
+                                   int64_t ld_out, void* stream) {
+  GR_REQUIRE(x && w_uvqk && uvqk, "hstu_decode_ln_uvqk: null pointer");
+  GR_REQUIRE(n >= 0 && D > 0 && D <= 512 && n_out > 0 && ld_x >= D && ld_out >= n_out &&
+                 (activation == 0 || activation == 1),
+             "hstu_decode_ln_uvqk: bad sizes (n %d, D %d, n_out %d)", n, D, n_out);
+  if (n == 0) return 0;
+  const hipStream_t st = (hipStream_t)stream;
+  const dim3 grid((n_out + gr::kSmCols - 1) / gr::kSmCols, (n + gr::kSmRows - 1) / gr::kSmRows);
+  GR_REQUIRE(grid.y <= 65535, "hstu_decode_ln_uvqk: %d rows", n);
+  GR_TIMED("ln_uvqk_fwd", st,
+           hipLaunchKernelGGL(gr::sm_ln_uvqk_kernel, grid, dim3(256),
+                              (uint32_t)(sizeof(float) * (gr::kSmRows + gr::kSmCols) * D), st,
+                              x, ld_x, n, D,
+                              w_uvqk, n_out, eps, activation, uvqk, ld_out));
+  GR_LAUNCH_CHECK("hstu_decode_ln_uvqk");
+  return 0;
+}
+
+extern "C" int hstu_decode_gate_o(const float* u, int64_t ld_u, const float* attn, int64_t ld_attn,
+                                  int n, int hdv, int D, const float* w_o, const float* b_o,
+                                  const float* x_res, int64_t ld_x, float eps, float* y,
+                                  int64_t ld_y, void* stream) {
+  GR_REQUIRE(u && attn && w_o && y, "hstu_decode_gate_o: null pointer");
+  GR_REQUIRE(n >= 0 && hdv > 0 && hdv <= 256 && D > 0 && ld_u >= hdv && ld_attn >= hdv &&
+                 ld_y >= D && (!x_res || ld_x >= D),
+             "hstu_decode_gate_o: bad sizes (n %d, hdv %d, D %d)", n, hdv, D);
+  if (n == 0) return 0;
+  const hipStream_t st = (hipStream_t)stream;
+  const dim3 grid((D + gr::kSmCols - 1) / gr::kSmCols, (n + gr::kSmRows - 1) / gr::kSmRows);
+  GR_REQUIRE(grid.y <= 65535, "hstu_decode_gate_o: %d rows", n);
+  const size_t lds = sizeof(float) * ((size_t)gr::kSmRows * hdv + (size_t)gr::kSmCols * (hdv + 1));
+  GR_TIMED("gate_o_fwd", st,
+           hipLaunchKernelGGL(gr::sm_gate_o_kernel, grid, dim3(256), (uint32_t)lds, st, u, ld_u,
+                              attn, ld_attn, n, hdv, D, w_o, b_o, x_res, ld_x, eps, y, ld_y));
+  GR_LAUNCH_CHECK("hstu_decode_gate_o");
   return 0;
 }

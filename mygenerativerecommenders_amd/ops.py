@@ -1232,9 +1232,10 @@ def stu_decode(x, offsets, timestamps, delta_rows, delta_pos, cache, w_uvqk, w_o
     pass with return_cache_states, UPDATED IN PLACE as the reference's index_copy_ does.
     ``xd`` (optional): the rows x[delta_rows] when the caller has them (the previous
     layer's re-encoded rows, for distinct delta rows).  Launches: the row gather (unless
-    ``xd``), LN + UVQK on the delta rows, the cache scatter (hstu_decode_scatter), the
-    delta rows' attention (hstu_decode_attn: chunks + reduce), the gate + O projection,
-    the output scatter.  Returns (the updated outputs cache = the next layer's input,
+    ``xd``), LN + UVQK on the delta rows (hstu_decode_ln_uvqk, small-M tiles), the cache
+    scatter (hstu_decode_scatter), the delta rows' attention (hstu_decode_attn: chunks +
+    reduce), the gate + O projection (hstu_decode_gate_o without dropout / concat_ua,
+    else the training kernels), the output scatter.  Returns (the updated outputs cache = the next layer's input,
     the re-encoded rows).  Forward only."""
     v_c, q_c, k_c, out_c = cache
     _lib.require_gpu(x, offsets, delta_rows, delta_pos, v_c, q_c, k_c, out_c, w_uvqk, w_o, b_o)
@@ -1260,11 +1261,16 @@ def stu_decode(x, offsets, timestamps, delta_rows, delta_pos, cache, w_uvqk, w_o
         _lib.call("gr_rows_copy", x.data_ptr(), D, rows_i.data_ptr(), 0, x.shape[0], xd.data_ptr(),
                   D, None, 0, E, E, D, st)
     off_d = torch.arange(E + 1, dtype=torch.int64, device=dev)
-    x_stats = torch.empty(E, 2, dtype=torch.float32, device=dev)
     uvqk = torch.empty(E, n_out, dtype=torch.float32, device=dev)
     w_uvqk = w_uvqk.detach().float().contiguous()
-    _lib.call("hstu_ln_uvqk_fwd", xd.data_ptr(), D, off_d.data_ptr(), E, E, D, w_uvqk.data_ptr(),
-              n_out, geo.eps, geo.activation, x_stats.data_ptr(), None, uvqk.data_ptr(), n_out, st)
+    if D <= 512:  # the small-M projection (16 rows x 16 columns per workgroup)
+        _lib.call("hstu_decode_ln_uvqk", xd.data_ptr(), D, E, D, w_uvqk.data_ptr(), n_out, geo.eps,
+                  geo.activation, uvqk.data_ptr(), n_out, st)
+    else:
+        x_stats = torch.empty(E, 2, dtype=torch.float32, device=dev)
+        _lib.call("hstu_ln_uvqk_fwd", xd.data_ptr(), D, off_d.data_ptr(), E, E, D,
+                  w_uvqk.data_ptr(), n_out, geo.eps, geo.activation, x_stats.data_ptr(), None,
+                  uvqk.data_ptr(), n_out, st)
     # cache updates: v at the jagged rows, q / k at (e, delta_pos[e]) of the padded caches
     _lib.call("hstu_decode_scatter", uvqk.data_ptr(), n_out, hv, hq, rows_i.data_ptr(),
               pos_i.data_ptr(), E, N, v_c.data_ptr(), v_c.shape[0], q_c.data_ptr(), k_c.data_ptr(),
@@ -1292,7 +1298,11 @@ def stu_decode(x, offsets, timestamps, delta_rows, delta_pos, cache, w_uvqk, w_o
     gate_args = (uvqk.data_ptr(), n_out, attn.data_ptr(), hv, off_d.data_ptr(), E, E, hv)
     tail = (xd.data_ptr(), D, geo.eps, geo.dropout_p, seed, _lib.ptr(seed_offset),
             attn_stats.data_ptr())
-    if not geo.concat_ua:
+    # the small-M gate at wide rows; narrow rows (D <= 64: ml-1m) keep the row-wave kernel
+    if not geo.concat_ua and geo.dropout_p == 0 and hv <= 256 and D > 64:
+        _lib.call("hstu_decode_gate_o", uvqk.data_ptr(), n_out, attn.data_ptr(), hv, E, hv, D,
+                  w_o.data_ptr(), b_o.data_ptr(), xd.data_ptr(), D, geo.eps, y.data_ptr(), D, st)
+    elif not geo.concat_ua:
         _lib.call("hstu_gate_o_fwd", *gate_args, D, w_o.data_ptr(), b_o.data_ptr(), *tail, None,
                   y.data_ptr(), D, st)
     elif _cat_wide(hv, D):
