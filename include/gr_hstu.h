@@ -47,7 +47,7 @@ GR_API int gr_version(void);
  * wgrad_reduce, mips_pack, mips_select, mips_merge, cumsum, dense_to_jagged, encoder_prologue, bf16_scale_add, adamw,
  * jagged_to_padded, l2_normalize, current_embeddings, sampled_softmax_fwd,
  * sampled_softmax_bwd, sampled_softmax_csr, sampled_softmax_table_grad, preproc, rows_copy,
- * decode_scatter, decode_attn, softmax_attn_fwd, softmax_attn_bwd.  Not for use inside a captured graph.
+ * decode_scatter, decode_attn, softmax_attn_fwd, softmax_attn_bwd, rel_bias_fwd, rel_bias_bwd.  Not for use inside a captured graph.
  */
 GR_API int gr_timing_enable(int on);
 GR_API int gr_timing_query(const char* kernel, double* total_ms, int* launches);

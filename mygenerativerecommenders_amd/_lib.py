@@ -116,7 +116,7 @@ KERNEL_NAMES = ("bucket_map", "attn_fwd", "attn_bwd", "attn_bwd_dkv", "attn_bwd_
                 "sampled_softmax_fwd", "sampled_softmax_bwd", "sampled_softmax_csr",
                 "sampled_softmax_table_grad", "preproc", "item_embedding", "mips_sort_invalid",
                 "mips_wide_score", "mips_wide_select", "rows_copy", "decode_scatter", "decode_attn",
-                "softmax_attn_fwd", "softmax_attn_bwd")
+                "softmax_attn_fwd", "softmax_attn_bwd", "rel_bias_fwd", "rel_bias_bwd")
 
 
 def parse_options(path: str = HEADER_PATH) -> dict:

@@ -252,16 +252,43 @@ __global__ __launch_bounds__(256) void rel_bias_fwd_kernel(const int64_t* ts, in
   }
 }
 
+// one workgroup per diagonal r = j - i + N - 1: threads stride over its B * len entries in a
+// fixed order, then a fixed-order tree (deterministic)
 __global__ __launch_bounds__(256) void rel_bias_dpos_kernel(const float* dout, int B, int N,
                                                             float* d_pos) {
-  const int r = blockIdx.x * 256 + threadIdx.x;  // j - i + N - 1
-  if (r >= 2 * N - 1) return;
+  __shared__ float part[256];
+  const int r = blockIdx.x;
   const int dlt = r - (N - 1);
   const int i0 = dlt < 0 ? -dlt : 0, i1 = dlt < 0 ? N : N - dlt;
-  float acc = 0.f;
-  for (int b = 0; b < B; ++b)
-    for (int i = i0; i < i1; ++i) acc += dout[((int64_t)b * N + i) * N + i + dlt];
-  d_pos[r] = acc;
+  const int len = i1 - i0;
+  const int total = B * len;  // B * N < 2^31 (checked by the entry)
+  // 4 partial sums (entries t, t + 256, t + 512, t + 768 of each group of 1024): 4 loads in
+  // flight instead of a chain of dependent adds
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  int b = threadIdx.x / len, i = threadIdx.x - b * len;
+  const int bs = 256 / len, is = 256 - bs * len;  // the stride 256 as (b, i) steps
+  int q = 0;
+  for (int t = threadIdx.x; t < total; t += 256) {
+    const float v = dout[((int64_t)b * N + i0 + i) * N + i0 + i + dlt];
+    acc[0] += q == 0 ? v : 0.f;
+    acc[1] += q == 1 ? v : 0.f;
+    acc[2] += q == 2 ? v : 0.f;
+    acc[3] += q == 3 ? v : 0.f;
+    q = (q + 1) & 3;
+    b += bs;
+    i += is;
+    if (i >= len) {
+      i -= len;
+      ++b;
+    }
+  }
+  part[threadIdx.x] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) part[threadIdx.x] += part[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) d_pos[r] = part[0];
 }
 
 // one workgroup per (b, i) row: bucket sums of the row in j order -> slab[row][nb + 1]
@@ -298,9 +325,17 @@ __global__ __launch_bounds__(256) void rel_bias_dts_reduce_kernel(const float* s
                                                                   int nb, float* d_ts) {
   __shared__ float part[256];
   const int c = blockIdx.x;
-  float acc = 0.f;
-  for (int64_t r = threadIdx.x; r < rows; r += 256) acc += slabs[r * (nb + 1) + c];
-  part[threadIdx.x] = acc;
+  // 4 partial sums over rows t + 1024 k + 256 q, q = 0..3 (4 loads in flight)
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int64_t r = threadIdx.x;
+  for (; r + 768 < rows; r += 1024) {
+    a0 += slabs[r * (nb + 1) + c];
+    a1 += slabs[(r + 256) * (nb + 1) + c];
+    a2 += slabs[(r + 512) * (nb + 1) + c];
+    a3 += slabs[(r + 768) * (nb + 1) + c];
+  }
+  for (; r < rows; r += 256) a0 += slabs[r * (nb + 1) + c];
+  part[threadIdx.x] = (a0 + a1) + (a2 + a3);
   __syncthreads();
   for (int s = 128; s > 0; s >>= 1) {
     if ((int)threadIdx.x < s) part[threadIdx.x] += part[threadIdx.x + s];
@@ -319,8 +354,10 @@ extern "C" int hstu_rel_bias_fwd(const int64_t* ts, int B, int N, const int64_t*
              "hstu_rel_bias_fwd: bad sizes (num_buckets must be < 256)");
   GR_REQUIRE((int64_t)B * N < 0x7fffffff, "hstu_rel_bias_fwd: B * N too large");
   if (B == 0) return 0;
-  hipLaunchKernelGGL(gr::rel_bias_fwd_kernel, dim3(B * N), dim3(256), 0, (hipStream_t)stream, ts,
-                     B, N, bucket_thr, num_buckets, pos_w, ts_w, out);
+  GR_TIMED("rel_bias_fwd", (hipStream_t)stream,
+           hipLaunchKernelGGL(gr::rel_bias_fwd_kernel, dim3(B * N), dim3(256), 0,
+                              (hipStream_t)stream, ts, B, N, bucket_thr, num_buckets, pos_w, ts_w,
+                              out));
   GR_LAUNCH_CHECK("hstu_rel_bias_fwd");
   return 0;
 }
@@ -347,14 +384,17 @@ extern "C" int hstu_rel_bias_bwd(const int64_t* ts, int B, int N, const int64_t*
   GR_REQUIRE(workspace && ws_bytes >= need, "hstu_rel_bias_bwd: workspace %zu B < %zu B",
              ws_bytes, need);
   float* slabs = (float*)workspace;
-  hipLaunchKernelGGL(gr::rel_bias_dpos_kernel, dim3((2 * N - 1 + 255) / 256), dim3(256), 0, st,
-                     dout, B, N, d_pos_w);
+  GR_TIMED("rel_bias_bwd", st,
+           hipLaunchKernelGGL(gr::rel_bias_dpos_kernel, dim3(2 * N - 1), dim3(256), 0, st, dout,
+                              B, N, d_pos_w));
   GR_LAUNCH_CHECK("hstu_rel_bias_bwd(dpos)");
-  hipLaunchKernelGGL(gr::rel_bias_dts_rows_kernel, dim3(B * N), dim3(256), 0, st, ts, dout, B, N,
-                     bucket_thr, num_buckets, slabs);
+  GR_TIMED("rel_bias_bwd", st,
+           hipLaunchKernelGGL(gr::rel_bias_dts_rows_kernel, dim3(B * N), dim3(256), 0, st, ts,
+                              dout, B, N, bucket_thr, num_buckets, slabs));
   GR_LAUNCH_CHECK("hstu_rel_bias_bwd(dts rows)");
-  hipLaunchKernelGGL(gr::rel_bias_dts_reduce_kernel, dim3(num_buckets + 1), dim3(256), 0, st,
-                     slabs, (int64_t)B * N, num_buckets, d_ts_w);
+  GR_TIMED("rel_bias_bwd", st,
+           hipLaunchKernelGGL(gr::rel_bias_dts_reduce_kernel, dim3(num_buckets + 1), dim3(256), 0,
+                              st, slabs, (int64_t)B * N, num_buckets, d_ts_w));
   GR_LAUNCH_CHECK("hstu_rel_bias_bwd(dts reduce)");
   return 0;
 }
